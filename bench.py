@@ -1,0 +1,224 @@
+#!/usr/bin/env python3
+"""Benchmark: SND-VAE training graphs/sec + ELBO-step ms (BASELINE.json metric).
+
+Workload (BASELINE.json configs[1], "C2"): synthetic random-geometric spatial
+graphs, N=4096 nodes, d=64, bf16 MFMA operands (fp32 accumulation/params),
+node-latent SND-VAE (SURVEY.md §8 composed step).  A "step" is one full
+training iteration over the device batch: forward, hand-derived backward,
+(data parallel) one RCCL all-reduce of the flat gradient, TF1 Adam --
+captured in one HIP graph and replayed.  Inputs are resident in HBM.
+
+    python bench.py [--gpus N --steps K --warmup W --graphs-per-gpu B]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 \
+        bench.py --gpus N ...            (one rank per GPU, RCCL over xGMI)
+
+Prints ONE JSON line on rank 0.  value = graphs/sec over all ranks (weak
+scaling: B graphs per GPU).  roofline = the dominant kernel (fused zz^T + CE,
+MFMA-bound), timed with HIP events on the launch stream.  cpu_baseline = the
+reference formulation (dense A, materialised [N,N,2] logits, autograd, TF1
+Adam) in torch-CPU fp32 on the host cores (TensorFlow is unavailable).
+"""
+from __future__ import annotations
+
+import argparse
+import glob
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "training graphs/sec + ELBO-step ms, N=4096 d=64, at 1/2/4/8 MI355X"
+PEAK_TFLOPS = {"bf16": 2500.0, "f32": 157.3}      # MI355X dense MFMA (MI355X_MICROARCH.md)
+PEAK_HBM_GBS = 8000.0
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def cpu_baseline(n_nodes, latent, budget_s):
+    """Reference-formula CPU path on a bounded sample (one N-node graph per step)."""
+    import numpy as np
+    import torch
+
+    from oracle import ref_torch as T
+    from snd_vae_amd.config import tscale
+    from snd_vae_amd.data import synthetic_batch
+    from snd_vae_amd.params import init_blocks
+
+    cores = max(1, min(len(os.sched_getaffinity(0)), int(os.environ.get("OMP_NUM_THREADS", "16"))))
+    torch.set_num_threads(cores)
+    cfg = tscale(n_nodes, latent)
+    b = synthetic_batch(cfg, 1, seed=777)
+    eps = np.random.default_rng(0).standard_normal((n_nodes, latent))
+    tensors = T.to_tensors(([b.dense_adj(0)], b.features, b.feature_truth, b.spatial_truth, eps),
+                           cfg, torch.float32)
+    p = T.build_params(init_blocks(cfg, 0), torch.float32)
+    opt = T.TF1Adam(p, cfg.learning_rate)
+
+    def step():
+        cost, _ = T.loss_fn(p, *tensors, cfg)
+        cost.backward()
+        opt.step()
+
+    t0 = time.perf_counter()
+    step()                                  # warm-up (allocations)
+    first = time.perf_counter() - t0
+    n, t0 = 0, time.perf_counter()
+    while n < 5 and (n == 0 or time.perf_counter() - t0 + first < budget_s):
+        step()
+        n += 1
+    dt = time.perf_counter() - t0
+    return {"value": n / dt, "unit": "graphs/s", "cores": cores, "kind": "port",
+            "sample": f"{n} train steps x 1 graph (N={n_nodes}, d={latent}) after 1 warm-up; "
+                      "reference-formula torch-CPU fp32 (dense A@(XW), [N,N,2] logits + softmax-CE, "
+                      "autograd, TF1 Adam); TF unavailable",
+            "ms_per_graph": 1000 * dt / n}
+
+
+def load_traffic(n, d, B, dtype):
+    """HBM bytes per zz^T launch from the committed rocprofv3 PMC summary, if any."""
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc_zzt*.json"))):
+        try:
+            j = json.load(open(f))
+        except Exception:
+            continue
+        if (j.get("n_nodes"), j.get("latent"), j.get("graphs"), j.get("dtype")) == (n, d, B, dtype):
+            return j.get("hbm_bytes_per_launch")
+    return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--graphs-per-gpu", type=int, default=8)
+    ap.add_argument("--nodes", type=int, default=4096)
+    ap.add_argument("--latent", type=int, default=64)
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "f32"])
+    ap.add_argument("--no-graph", action="store_true", help="eager launches instead of HIP graph")
+    ap.add_argument("--kernel-reps", type=int, default=20)
+    ap.add_argument("--cpu-baseline-seconds", type=float, default=20.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+
+    from snd_vae_amd.config import tscale
+    from snd_vae_amd.data import synthetic_batch
+    from snd_vae_amd.model import DeviceBatch, SGCNModelVAE
+    from snd_vae_amd.optimizer import OptimizerVAE
+    from snd_vae_amd.parallel import init_from_env, max_over_ranks
+    from snd_vae_amd import _lib
+
+    info = init_from_env("nccl")
+    if info.world != args.gpus:
+        log(f"warning: --gpus {args.gpus} but WORLD_SIZE {info.world}")
+    torch.cuda.set_device(info.local_rank)
+    B, N, d = args.graphs_per_gpu, args.nodes, args.latent
+    cfg = tscale(N, d)
+    log(f"[rank {info.rank}] building {B} RGG graphs N={N}")
+    host = synthetic_batch(cfg, B, seed=1000 + info.rank * B)
+    db = DeviceBatch(host)
+    model = SGCNModelVAE(cfg, B, dtype=args.dtype)
+    opt = OptimizerVAE(model, process_group=info.group if info.world > 1 else None)
+
+    if args.no_graph:
+        run = lambda: opt.step(db)
+    else:
+        opt.capture(db, warmup=2)
+        run = opt.replay
+    for _ in range(args.warmup):
+        run()
+    torch.cuda.synchronize()
+    log(f"[rank {info.rank}] warm-up done, loss terms {opt.loss_dict()}")
+
+    def barrier():
+        if info.world > 1:
+            import torch.distributed as dist
+            dist.barrier()
+
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        run()
+    torch.cuda.synchronize()
+    barrier()
+    dt = max_over_ranks(time.perf_counter() - t0, info, device=f"cuda:{info.local_rank}")
+    losses = opt.loss_dict(global_mean=True)
+    graphs = B * info.world * args.steps
+    value = graphs / dt
+    ms = 1000.0 * dt / args.steps
+    log(f"[rank {info.rank}] {value:.1f} graphs/s, {ms:.3f} ms/step")
+
+    # ---- dominant kernel: fused zz^T + CE, HIP events on the launch stream
+    bc = db.c_struct()
+    L = _lib.lib()
+
+    def kernel_ms(name):
+        st = _lib.stream_ptr()
+        _lib.check(L.snd_plan_launch(model.plan, bc, model.workspace.data_ptr(), name.encode(), st))
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(args.kernel_reps):
+            _lib.check(L.snd_plan_launch(model.plan, bc, model.workspace.data_ptr(), name.encode(), st))
+        e1.record()
+        e1.synchronize()
+        return e0.elapsed_time(e1) / args.kernel_reps
+
+    zzt_ms = kernel_ms("zzt_dense")
+    spmm_ms = kernel_ms("spmm_dxw1")
+    flops = 4.0 * N * N * d * B                       # 2N^2 d fwd + 2N^2 d bwd per graph
+    achieved = flops / (zzt_ms * 1e-3) / 1e12
+    peak = PEAK_TFLOPS[args.dtype]
+    h1 = cfg.g_conv_hidden[1]
+    spmm_bytes = 4 * (B * N + 1) + 4 * host.nnz + 2 * 4 * B * N * h1
+    spmm_gbs = spmm_bytes / (spmm_ms * 1e-3) / 1e9
+
+    out = {
+        "metric": METRIC,
+        "value": round(value, 3),
+        "unit": "graphs/s",
+        "n_gpus": info.world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms, 4),
+        "elbo_step_ms": round(ms, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": args.dtype,
+        "data": "synthetic random-geometric graphs (U[0,1)^2 nodes, r=sqrt(16/(pi N))), random-init weights",
+        "config": {"workload": f"C2: node-latent SND-VAE train step, N={N}, d={d}, "
+                               f"{B} graphs/GPU, HIP-graph replay",
+                   "n_nodes": N, "latent": d, "graphs_per_gpu": B, "global_batch": B * info.world,
+                   "nnz_per_graph": round(host.nnz / B, 1), "parallelism": f"dp{info.world}",
+                   "hip_graph": not args.no_graph},
+        "roofline": {"kernel": "zzt_dense (fused z z^T + CE fwd+bwd)", "bound": "mfma",
+                     "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
+                     "frac": round(achieved / peak, 4),
+                     "traffic": load_traffic(N, d, B, args.dtype),
+                     "avg_launch_ms": round(zzt_ms, 5), "flops_per_launch": flops},
+        "secondary_roofline": {"kernel": "csr_spmm (A @ dP1, width 64, fp32)", "bound": "hbm",
+                               "achieved": round(spmm_gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                               "frac": round(spmm_gbs / PEAK_HBM_GBS, 4),
+                               "avg_launch_ms": round(spmm_ms, 5), "bytes_per_launch": spmm_bytes},
+        "losses": {k: round(v, 6) for k, v in losses.items()},
+    }
+    if info.rank == 0 and info.world == 1 and not args.no_cpu_baseline:
+        log("cpu baseline ...")
+        out["cpu_baseline"] = cpu_baseline(N, d, args.cpu_baseline_seconds)
+    if info.rank == 0:
+        print(json.dumps(out), flush=True)
+    if info.world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,218 @@
+/*
+ * snd_vae.h -- C ABI of the MI355X (gfx950) SND-VAE training hot path.
+ *
+ * One shared library, libsndvae.so, built by hipcc for gfx950.  Every entry
+ * point takes caller-owned DEVICE pointers plus sizes and a HIP stream (passed
+ * as an opaque pointer so FFI bindings need no HIP headers), launches
+ * stream-ordered work, never allocates or synchronises (graph-capturable), and
+ * returns 0 or a negative SND_ERR_* code; snd_last_error() gives the
+ * thread-local message.  Layouts are row-major fp32 unless stated.  A batch of
+ * B graphs with N nodes each is one block-diagonal CSR (int32 rowptr [B*N+1],
+ * sorted int32 colidx with global column ids b*N+j) plus row-major node data
+ * [B*N, width].
+ *
+ * Each function names the reference interface it replaces (file:line in
+ * xguo7/SND-VAE, TensorFlow 1.x).  The reference is a TF graph-construction
+ * API, not an FFI; INTEGRATION.md shows the ctypes binding a maintainer adds.
+ */
+#ifndef SND_VAE_H
+#define SND_VAE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef void* snd_stream_t; /* hipStream_t */
+
+enum {
+  SND_OK = 0,
+  SND_ERR_ARG = -1,         /* bad shape/pointer/enum */
+  SND_ERR_HIP = -2,         /* HIP launch/runtime error */
+  SND_ERR_UNSUPPORTED = -3  /* configuration not built for gfx950 path */
+};
+
+enum { SND_F32 = 0, SND_BF16 = 1 }; /* MFMA operand dtype; accumulation always fp32 */
+
+const char* snd_last_error(void);
+int snd_abi_version(void);
+
+/* ---- a1: adjacency ingest ------------------------------------------------
+ * Replaces the dense adj_truth feed (main.py:257, input_data.py:62-72):
+ * converts B dense [N,N] float 0/1 matrices (diagonal ignored) into the
+ * block-diagonal CSR, entries in np.where row-major order (bit-exact vs
+ * scipy.sparse.csr_matrix).  *nnz_out (device int) receives the total.
+ * Fails with SND_ERR_ARG (message set) via *nnz_out = -1 when colidx_cap is
+ * too small.  workspace: snd_dense_to_csr_workspace() bytes. */
+size_t snd_dense_to_csr_workspace(int n_graphs, int n);
+int snd_dense_to_csr(const float* adj, int n_graphs, int n, int* rowptr,
+                     int* colidx, long long colidx_cap, int* nnz_out,
+                     void* workspace, size_t workspace_bytes, snd_stream_t stream);
+
+/* ---- a2/a3/a4: CSR SpMM with GraphConvolution epilogue -------------------
+ * Replaces tf.matmul(adj, new_x) + lrelu (layers.py:122-123) and the BN /
+ * concat that follow it (model.py:107-112).
+ *   acc = A @ h                      (A symmetric: also the backward A^T @ dy)
+ *   epilogue SND_SPMM_PLAIN: out = acc
+ *   epilogue SND_SPMM_GCN:   preact = acc;
+ *       y = lrelu(acc) * gamma/sqrt(1.001) + beta        -> out[:, :width]
+ *       out[:, width:width+fx] = concat_x                 (model.py:109)
+ *       if out2: out2 = [y || concat_x] * g2/sqrt(1.001) + b2 (encoder_g BN) */
+enum { SND_SPMM_PLAIN = 0, SND_SPMM_GCN = 1 };
+int snd_csr_spmm(const int* rowptr, const int* colidx, int n_rows,
+                 const float* h, int ldh, int width, float* out, int ldo,
+                 int epilogue, const float* bn_gamma, const float* bn_beta,
+                 float* preact, int ldp, const float* concat_x, int ldx, int fx,
+                 const float* bn2_gamma, const float* bn2_beta, float* out2,
+                 int ldo2, snd_stream_t stream);
+
+/* ---- a5: linear / dense GEMM on MFMA ---------------------------------------
+ * Replaces linear() (layers.py:566-576) and the X@w of GraphConvolution
+ * (layers.py:120-121; the tile() copy is not needed):
+ *   C[m,n] = sum_k op(A)[m,k] op(B)[k,n] (+ bias[n])
+ * op(A) = A (trans_a=0, A is [m,k] lda) or A^T (A is [k,m]); same for B. */
+int snd_gemm(int trans_a, int trans_b, int m, int n, int k, const float* a,
+             int lda, const float* b, int ldb, float* c, int ldc,
+             const float* bias, int dtype, snd_stream_t stream);
+
+/* ---- a8/a9: conv1d k=5 SAME over the node axis of each graph --------------
+ * Replaces tf.layers.conv1d(k=5, stride 1, padding='SAME') + BN + lrelu
+ * (model_joint.py:115-116, 138-139).  w is TF layout [5][cin][cout].
+ *   fwd:  y_pre = conv(x) + bias;  out = lrelu(y_pre*g/sqrt(1.001) + b)
+ *         (gamma == NULL: out = y_pre, no BN/lrelu)
+ *   bwd_data:   dx = conv^T(dy)   (flipped taps, transposed channels)
+ *   bwd_weight: dw[t,c,o] = sum_rows x[r+t-2,c] dy[r,o]  (deterministic
+ *               split-K; workspace snd_conv1d_bwd_weight_workspace()).
+ * rows = B*N, n_per_graph = N: taps never cross graph boundaries. */
+int snd_conv1d_same_fwd(const float* x, int ldx, int rows, int n_per_graph,
+                        int cin, const float* w, int cout, const float* bias,
+                        const float* bn_gamma, const float* bn_beta,
+                        float* y_pre, int ldy, float* out, int ldo, int dtype,
+                        snd_stream_t stream);
+int snd_conv1d_same_bwd_data(const float* dy, int lddy, int rows,
+                             int n_per_graph, int cout, const float* w,
+                             int cin, float* dx, int lddx, int dtype,
+                             snd_stream_t stream);
+size_t snd_conv1d_bwd_weight_workspace(int rows, int cin, int cout);
+int snd_conv1d_same_bwd_weight(const float* x, int ldx, const float* dy,
+                               int lddy, int rows, int n_per_graph, int cin,
+                               int cout, float* dw, void* workspace,
+                               size_t workspace_bytes, int dtype,
+                               snd_stream_t stream);
+
+/* ---- a6/a12: reparameterisation + KL --------------------------------------
+ * Replaces get_z (model.py:153-161) and the KL term (optimizer.py:193).
+ * ms = [mu || logstd] rows of width 2L (ld).  eps: injected [rows, L] or NULL
+ * for the device Philox4x32-10 stream (seed, offset = *step_counter).
+ *   z = mu + eps*exp(s)  -> z [rows, L]; eps written to eps_out if non-NULL.
+ *   kl_part: snd_reparam_kl_blocks(rows, L) device doubles whose (fixed-order)
+ *   sum is sum(1 + 2s - mu^2 - exp(s)^2). */
+int snd_reparam_kl_blocks(int rows, int latent);
+int snd_reparam_kl(const float* ms, int ldms, int rows, int latent,
+                   const float* eps, unsigned long long seed,
+                   const int* step_counter, float* eps_out, float* z,
+                   double* kl_part, snd_stream_t stream);
+
+/* ---- a7/a10: fused inner-product decoder + 2-class CE ----------------------
+ * Replaces InnerProductDecoder (layers.py:407-409), the diagonal rule
+ * (model.py:185,205-207), argmax (model.py:208), accuracy (main.py:334) and
+ * softmax_cross_entropy (optimizer.py:142-144).  Logits never reach HBM.
+ * For each graph b (z [B*N, d], d in {16,32,64,128}):
+ *   L = z z^T; per off-diagonal pair CE = softplus(L) - A L (pos_weight,
+ *   norm generalise to the weighted BCE of SURVEY §8 decision ii);
+ *   diagonal pairs contribute softplus(-1) and no gradient.
+ * Outputs (device): stats[0] = sum CE over all B*N*N pairs (double),
+ *   stats[1] = number of pairs with argmax == A (as double),
+ *   dz [B*N, d] = d(sum CE)/dz (unscaled; divide by B*N*N for the mean).
+ * workspace: snd_zzt_ce_workspace() bytes. */
+size_t snd_zzt_ce_workspace(int n_graphs, int n, int d, int dtype);
+int snd_zzt_ce(const float* z, int n_graphs, int n, int d,
+               const int* rowptr, const int* colidx, float pos_weight,
+               float norm, double* stats, float* dz, void* workspace,
+               size_t workspace_bytes, int dtype, snd_stream_t stream);
+
+/* ---- a11: sigmoid head + MSE ----------------------------------------------
+ * Replaces tf.nn.sigmoid(linear(...)) (model_joint.py:121,144) and the
+ * squared-difference means (optimizer.py:149,153) with their gradients:
+ *   yhat = sigmoid(u @ w + b);  sse += sum (yhat - y)^2  (device double)
+ *   du = dpre @ w^T with dpre = 2 (yhat - y)/count * yhat (1 - yhat),
+ *   count = rows*cout (the mean's denominator).  dw/db accumulate (+=).
+ *   sse: snd_sigmoid_mse_blocks(rows) device doubles (per-block partials).
+ *   workspace: blocks * (cin*cout + cout) floats. */
+int snd_sigmoid_mse_blocks(int rows);
+int snd_sigmoid_mse(const float* u, int ldu, int rows, int cin,
+                    const float* w, const float* b, int cout,
+                    const float* target, int ldt, double* sse, float* yhat,
+                    float* du, int lddu, float* dw, float* db, void* workspace,
+                    size_t workspace_bytes, snd_stream_t stream);
+
+/* ---- a13: TF1 Adam over a flat buffer --------------------------------------
+ * Replaces tf.train.AdamOptimizer(lr).minimize (optimizer.py:125,197):
+ *   t = *step_counter (1-based, already advanced for this step)
+ *   g = grad*grad_scale; m = b1 m + (1-b1) g; v = b2 v + (1-b2) g^2
+ *   param -= lr*sqrt(1-b2^t)/(1-b1^t) * m / (sqrt(v) + eps) */
+int snd_adam_tf1(float* param, const float* grad, float* m, float* v,
+                 long long n, float lr, float beta1, float beta2, float eps,
+                 float grad_scale, const int* step_counter,
+                 snd_stream_t stream);
+
+/* ---- a14: the whole train step (main.py:315-334) ---------------------------
+ * A plan fixes shapes; the step runs forward + backward of the node-latent
+ * SND-VAE (SURVEY §8 "Composed step") for one batch, writes the flat
+ * gradient (same layout as params), advances *step_counter and writes
+ * losses[0..7] = {cost, spatial_cost, adj_cost, node_cost, kl, acc,
+ *                 adj_sum, correct} (device doubles; main.py:331-334
+ * overall_loss order, optimizer.py:203).  It also writes the first six as
+ * floats to grads[param_count .. +6) so one all-reduce averages them. */
+typedef struct snd_config {
+  int n_nodes;      /* N */
+  int f_in;         /* encoder input width (num_feature + spatial_dim) */
+  int num_feature;  /* node feature targets */
+  int spatial_dim;  /* coordinate targets */
+  int h0, h1;       /* g_conv_hidden */
+  int g_hidden;     /* g_hidden_size */
+  int latent;       /* L == node_h_size */
+  int s1, s2, s3;   /* s_d_channel */
+  int n1, n2;       /* n_d_channel[:2] */
+  float beta;       /* KL weight */
+  float pos_weight; /* 1 == reference */
+  float norm;       /* 1 == reference */
+  int dtype;        /* SND_F32 (parity) or SND_BF16 (throughput) */
+} snd_config_t;
+
+typedef struct snd_batch {
+  const int* rowptr;           /* [B*N+1] */
+  const int* colidx;           /* [nnz]   */
+  const float* features;       /* [B*N, f_in] */
+  const float* feature_truth;  /* [B*N, num_feature] */
+  const float* spatial_truth;  /* [B*N, spatial_dim] */
+} snd_batch_t;
+
+typedef struct snd_plan snd_plan_t;
+
+int snd_plan_create(const snd_config_t* cfg, int n_graphs, snd_plan_t** out);
+void snd_plan_destroy(snd_plan_t* plan);
+long long snd_plan_param_count(const snd_plan_t* plan);
+int snd_plan_num_blocks(const snd_plan_t* plan);
+int snd_plan_param_block(const snd_plan_t* plan, int idx, const char** name,
+                         long long* offset, long long* numel);
+size_t snd_plan_workspace_bytes(const snd_plan_t* plan);
+/* Named intermediate buffers inside the workspace (tests / inspection). */
+int snd_plan_buffer(const snd_plan_t* plan, const char* name,
+                    long long* byte_offset, long long* numel);
+int snd_train_step(const snd_plan_t* plan, const snd_batch_t* batch,
+                   const float* params, float* grads, void* workspace,
+                   const float* eps, unsigned long long seed,
+                   int* step_counter, double* losses, snd_stream_t stream);
+/* Re-launch one kernel of the step on the workspace state left by the last
+ * snd_train_step (measurement/profiling): "zzt_dense" (fused zz^T + CE) or
+ * "spmm_dxw1" (plain CSR SpMM, width h1). */
+int snd_plan_launch(const snd_plan_t* plan, const snd_batch_t* batch,
+                    void* workspace, const char* kernel, snd_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SND_VAE_H */

@@ -1,0 +1,116 @@
+"""ctypes binding of libsndvae.so (include/snd_vae.h).
+
+The HIP library is the only compute path: there is no CPU or PyTorch
+fallback.  ``lib()`` raises if the shared object is missing, and ``check``
+turns every negative return code into a ``SNDError`` carrying
+``snd_last_error()``.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libsndvae.so")
+
+c_int, c_ll, c_float, c_size, c_ull = C.c_int, C.c_longlong, C.c_float, C.c_size_t, C.c_ulonglong
+vp = C.c_void_p
+
+
+class SNDError(RuntimeError):
+    pass
+
+
+class Config(C.Structure):
+    """snd_config_t"""
+    _fields_ = [("n_nodes", c_int), ("f_in", c_int), ("num_feature", c_int),
+                ("spatial_dim", c_int), ("h0", c_int), ("h1", c_int), ("g_hidden", c_int),
+                ("latent", c_int), ("s1", c_int), ("s2", c_int), ("s3", c_int),
+                ("n1", c_int), ("n2", c_int), ("beta", c_float), ("pos_weight", c_float),
+                ("norm", c_float), ("dtype", c_int)]
+
+
+class Batch(C.Structure):
+    """snd_batch_t"""
+    _fields_ = [("rowptr", vp), ("colidx", vp), ("features", vp),
+                ("feature_truth", vp), ("spatial_truth", vp)]
+
+
+# name -> (restype, argtypes)
+_SIGS = {
+    "snd_last_error": (C.c_char_p, []),
+    "snd_abi_version": (c_int, []),
+    "snd_dense_to_csr_workspace": (c_size, [c_int, c_int]),
+    "snd_dense_to_csr": (c_int, [vp, c_int, c_int, vp, vp, c_ll, vp, vp, c_size, vp]),
+    "snd_csr_spmm": (c_int, [vp, vp, c_int, vp, c_int, c_int, vp, c_int, c_int, vp, vp, vp,
+                             c_int, vp, c_int, c_int, vp, vp, vp, c_int, vp]),
+    "snd_gemm": (c_int, [c_int, c_int, c_int, c_int, c_int, vp, c_int, vp, c_int, vp, c_int,
+                         vp, c_int, vp]),
+    "snd_conv1d_same_fwd": (c_int, [vp, c_int, c_int, c_int, c_int, vp, c_int, vp, vp, vp,
+                                    vp, c_int, vp, c_int, c_int, vp]),
+    "snd_conv1d_same_bwd_data": (c_int, [vp, c_int, c_int, c_int, c_int, vp, c_int, vp,
+                                         c_int, c_int, vp]),
+    "snd_conv1d_bwd_weight_workspace": (c_size, [c_int, c_int, c_int]),
+    "snd_conv1d_same_bwd_weight": (c_int, [vp, c_int, vp, c_int, c_int, c_int, c_int, c_int,
+                                           vp, vp, c_size, c_int, vp]),
+    "snd_reparam_kl_blocks": (c_int, [c_int, c_int]),
+    "snd_reparam_kl": (c_int, [vp, c_int, c_int, c_int, vp, c_ull, vp, vp, vp, vp, vp]),
+    "snd_zzt_ce_workspace": (c_size, [c_int, c_int, c_int, c_int]),
+    "snd_zzt_ce": (c_int, [vp, c_int, c_int, c_int, vp, vp, c_float, c_float, vp, vp, vp,
+                           c_size, c_int, vp]),
+    "snd_sigmoid_mse_blocks": (c_int, [c_int]),
+    "snd_sigmoid_mse": (c_int, [vp, c_int, c_int, c_int, vp, vp, c_int, vp, c_int, vp, vp,
+                                vp, c_int, vp, vp, vp, c_size, vp]),
+    "snd_adam_tf1": (c_int, [vp, vp, vp, vp, c_ll, c_float, c_float, c_float, c_float,
+                             c_float, vp, vp]),
+    "snd_plan_create": (c_int, [C.POINTER(Config), c_int, C.POINTER(vp)]),
+    "snd_plan_destroy": (None, [vp]),
+    "snd_plan_param_count": (c_ll, [vp]),
+    "snd_plan_num_blocks": (c_int, [vp]),
+    "snd_plan_param_block": (c_int, [vp, c_int, C.POINTER(C.c_char_p), C.POINTER(c_ll),
+                                     C.POINTER(c_ll)]),
+    "snd_plan_workspace_bytes": (c_size, [vp]),
+    "snd_plan_buffer": (c_int, [vp, C.c_char_p, C.POINTER(c_ll), C.POINTER(c_ll)]),
+    "snd_train_step": (c_int, [vp, C.POINTER(Batch), vp, vp, vp, vp, c_ull, vp, vp, vp]),
+    "snd_plan_launch": (c_int, [vp, C.POINTER(Batch), vp, C.c_char_p, vp]),
+}
+
+EXPORTS = tuple(_SIGS)
+
+_lib = None
+
+
+def lib():
+    """Load libsndvae.so once; raise loudly if it has not been built."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise SNDError(f"{LIB_PATH} not built: run `python -m snd_vae_amd.build` "
+                           "(no CPU fallback exists)")
+        L = C.CDLL(LIB_PATH)
+        for name, (res, args) in _SIGS.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def last_error() -> str:
+    return lib().snd_last_error().decode(errors="replace")
+
+
+def check(rc: int, what: str = "") -> None:
+    if rc != 0:
+        raise SNDError(f"{what or 'libsndvae'} failed ({rc}): {last_error()}")
+
+
+def ptr(t) -> int:
+    """Device pointer of a torch tensor (or 0 for None)."""
+    return 0 if t is None else t.data_ptr()
+
+
+def stream_ptr(stream=None) -> int:
+    import torch
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return s.cuda_stream

@@ -1,0 +1,74 @@
+// Shared device/host helpers for the SND-VAE gfx950 kernels.
+// Error model: every extern "C" entry returns 0 or a negative code and sets a
+// thread-local message readable through snd_last_error() (include/snd_vae.h).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+#include <cstdio>
+#include <string>
+
+#include "../../include/snd_vae.h"
+
+namespace snd {
+
+void set_error(const char* fmt, ...);
+
+#define SND_CHECK_ARG(cond, ...)                                   \
+  do {                                                             \
+    if (!(cond)) {                                                 \
+      ::snd::set_error(__VA_ARGS__);                               \
+      return SND_ERR_ARG;                                          \
+    }                                                              \
+  } while (0)
+
+#define SND_LAUNCH_CHECK(what)                                     \
+  do {                                                             \
+    hipError_t e_ = hipGetLastError();                             \
+    if (e_ != hipSuccess) {                                        \
+      ::snd::set_error("%s: %s", what, hipGetErrorString(e_));     \
+      return SND_ERR_HIP;                                          \
+    }                                                              \
+  } while (0)
+
+#define SND_TRY(expr)                                              \
+  do {                                                             \
+    int rc_ = (expr);                                              \
+    if (rc_ != 0) return rc_;                                      \
+  } while (0)
+
+// Keras BatchNormalization in inference mode: moving var 1, eps 1e-3.
+constexpr float kBnC = 0.99950037468777325f;   // 1/sqrt(1.001)
+constexpr float kLeak = 0.2f;                  // layers.py:112-113
+constexpr float kLog2e = 1.4426950408889634f;
+constexpr float kLn2 = 0.69314718055994531f;
+constexpr double kSoftplusM1 = 0.31326168751822286;  // CE of a diagonal pair: logsumexp(1,0) - 1
+
+__device__ __forceinline__ float lrelu(float x) { return x >= 0.f ? x : kLeak * x; }
+// TF Maximum gradient: routed to x where x >= 0.2x  =>  1 for x >= 0.
+__device__ __forceinline__ float lrelu_grad(float x) { return x >= 0.f ? 1.f : kLeak; }
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ double wave_sum_d(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ unsigned wave_sum_u(unsigned v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+inline int cdiv(long long a, long long b) { return (int)((a + b - 1) / b); }
+inline long long round_up(long long a, long long b) { return (a + b - 1) / b * b; }
+
+}  // namespace snd

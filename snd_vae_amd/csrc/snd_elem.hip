@@ -1,0 +1,399 @@
+// Element-wise and reduction kernels of the SND-VAE step: reparameterisation
+// + KL, sigmoid/MSE heads, BN/lrelu backward with column partial sums,
+// deterministic slab reduction, TF1 Adam, and the loss finalizer.
+// All memory-bound; each reads its inputs once (HBM roofline).
+#include "snd_elem.hpp"
+#include "snd_gemm.hpp"
+
+namespace snd {
+namespace {
+
+// ---------------------------------------------------------------- Philox
+__device__ __forceinline__ uint4 philox4x32_10(uint4 c, uint2 k) {
+  const unsigned M0 = 0xD2511F53u, M1 = 0xCD9E8D57u, W0 = 0x9E3779B9u, W1 = 0xBB67AE85u;
+#pragma unroll
+  for (int i = 0; i < 10; ++i) {
+    const unsigned hi0 = __umulhi(M0, c.x), lo0 = M0 * c.x;
+    const unsigned hi1 = __umulhi(M1, c.z), lo1 = M1 * c.z;
+    c = make_uint4(hi1 ^ c.y ^ k.x, lo1, hi0 ^ c.w ^ k.y, lo0);
+    k.x += W0;
+    k.y += W1;
+  }
+  return c;
+}
+
+__device__ __forceinline__ float philox_normal(unsigned long long seed, unsigned offset,
+                                               unsigned long long idx) {
+  const uint4 r = philox4x32_10(make_uint4((unsigned)idx, (unsigned)(idx >> 32), offset, 0u),
+                                make_uint2((unsigned)seed, (unsigned)(seed >> 32)));
+  const float u1 = ((float)r.x + 1.0f) * 2.3283064365386963e-10f;  // (0, 1]
+  const float u2 = (float)r.y * 2.3283064365386963e-10f;
+  return sqrtf(-2.0f * __logf(u1)) * __cosf(6.283185307179586f * u2);
+}
+
+template <typename T>
+__device__ __forceinline__ T block_sum(T v) {
+  __shared__ T sh[16];
+  v = (sizeof(T) == 8) ? (T)wave_sum_d((double)v) : (T)wave_sum((float)v);
+  const int w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  if ((threadIdx.x & 63) == 0) sh[w] = v;
+  __syncthreads();
+  T t = 0;
+  if (threadIdx.x == 0)
+    for (int k = 0; k < nw; ++k) t += sh[k];
+  return t;  // valid in thread 0
+}
+
+// ---------------------------------------------------------------- reparam
+constexpr int kReparamGrid = 512;
+
+__global__ void __launch_bounds__(256) reparam_fwd_kernel(ReparamFwdArgs a) {
+  const long long n = (long long)a.rows * a.L;
+  const unsigned off = a.step ? (unsigned)(*a.step) : 0u;
+  double kl = 0.0;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n;
+       i += (long long)gridDim.x * 256) {
+    const int r = (int)(i / a.L), c = (int)(i - (long long)r * a.L);
+    const float mu = a.ms[(long long)r * a.ldms + c];
+    const float ls = a.ms[(long long)r * a.ldms + a.L + c];
+    const float eps = a.eps_in ? a.eps_in[i] : philox_normal(a.seed, off, (unsigned long long)i);
+    const float es = __expf(ls);
+    a.z[i] = mu + eps * es;               // model.py:159
+    if (a.eps_out) a.eps_out[i] = eps;
+    kl += (double)(1.f + 2.f * ls - mu * mu - es * es);   // optimizer.py:193
+  }
+  const double t = block_sum(kl);
+  if (threadIdx.x == 0) a.kl_part[blockIdx.x] = t;
+}
+
+__global__ void __launch_bounds__(256) reparam_bwd_kernel(ReparamBwdArgs a) {
+  const long long n = (long long)a.rows * a.L;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n;
+       i += (long long)gridDim.x * 256) {
+    const int r = (int)(i / a.L), c = (int)(i - (long long)r * a.L);
+    const float mu = a.ms[(long long)r * a.ldms + c];
+    const float ls = a.ms[(long long)r * a.ldms + a.L + c];
+    const float es = __expf(ls);
+    float dz = a.adj_scale * (a.dJd[i] + a.ej[i]);
+    if (a.dz_dec) dz += a.dz_dec[i];
+    a.dms[(long long)r * a.lddms + c] = dz + a.kl_scale * mu;
+    a.dms[(long long)r * a.lddms + a.L + c] = dz * a.eps[i] * es + a.kl_scale * (es * es - 1.f);
+  }
+}
+
+// ---------------------------------------------------------------- heads
+constexpr int kHeadRows = 256;
+constexpr int kHeadK = 64, kHeadO = 4;
+
+struct HeadPack { HeadArgs h[2]; };
+struct DecPack { DecBwdArgs d[2]; };
+
+__global__ void __launch_bounds__(256) heads_kernel(HeadPack pk, int rows) {
+  const HeadArgs& h = pk.h[blockIdx.y];
+  __shared__ float su[kHeadRows][kHeadK + 1];
+  __shared__ float sd[kHeadRows][kHeadO];
+  const int r = blockIdx.x * kHeadRows + threadIdx.x;
+  double sse = 0.0;
+  if (r < rows) {
+    float u[kHeadK];
+    for (int k = 0; k < h.cin; ++k) {
+      u[k] = h.u[(long long)r * h.ldu + k];
+      su[threadIdx.x][k] = u[k];
+    }
+    float dp[kHeadO];
+    for (int o = 0; o < h.cout; ++o) {
+      float zo = h.b[o];
+      for (int k = 0; k < h.cin; ++k) zo += u[k] * h.w[k * h.cout + o];
+      const float y = 1.f / (1.f + __expf(-zo));
+      if (h.yhat) h.yhat[(long long)r * h.cout + o] = y;
+      const float diff = y - h.target[(long long)r * h.ldt + o];
+      sse += (double)diff * diff;
+      dp[o] = 2.f * diff / h.count * y * (1.f - y);
+      sd[threadIdx.x][o] = dp[o];
+    }
+    for (int k = 0; k < h.cin; ++k) {
+      float du = 0.f;
+      for (int o = 0; o < h.cout; ++o) du += dp[o] * h.w[k * h.cout + o];
+      h.du[(long long)r * h.lddu + k] = du;
+    }
+  } else {
+    for (int k = 0; k < h.cin; ++k) su[threadIdx.x][k] = 0.f;
+    for (int o = 0; o < h.cout; ++o) sd[threadIdx.x][o] = 0.f;
+  }
+  const double t = block_sum(sse);
+  if (threadIdx.x == 0) h.sse_part[blockIdx.x] = t;
+  __syncthreads();
+  const int nw = h.cin * h.cout;
+  for (int idx = threadIdx.x; idx < nw + h.cout; idx += 256) {
+    float acc = 0.f;
+    if (idx < nw) {
+      const int k = idx / h.cout, o = idx - k * h.cout;
+      for (int rr = 0; rr < kHeadRows; ++rr) acc += su[rr][k] * sd[rr][o];
+    } else {
+      const int o = idx - nw;
+      for (int rr = 0; rr < kHeadRows; ++rr) acc += sd[rr][o];
+    }
+    h.wpart[(long long)blockIdx.x * (nw + h.cout) + idx] = acc;
+  }
+}
+
+// ---------------------------------------------------------------- BN/lrelu bwd
+__global__ void __launch_bounds__(256) dec_bwd_kernel(DecPack pk, int rows) {
+  const DecBwdArgs& a = pk.d[blockIdx.y];
+  const int c = threadIdx.x;
+  if (c >= a.ncols) return;
+  const float gc = a.gamma[c] * kBnC, be = a.beta[c];
+  float sg = 0.f, sb = 0.f, sy = 0.f;
+  const int r0 = blockIdx.x * kColRows, r1 = min(rows, r0 + kColRows);
+  for (int r = r0; r < r1; ++r) {
+    const float y = a.y[(long long)r * a.ldy + c];
+    const float t = y * gc + be;
+    const float dt = a.du[(long long)r * a.lddu + c] * lrelu_grad(t);
+    const float dy = dt * gc;
+    a.dy[(long long)r * a.lddy + c] = dy;
+    sg += dt * y;
+    sb += dt;
+    sy += dy;
+  }
+  float* p = a.part + (long long)blockIdx.x * 3 * a.ncols;
+  p[c] = sg * kBnC;
+  p[a.ncols + c] = sb;
+  p[2 * a.ncols + c] = sy;
+}
+
+__global__ void __launch_bounds__(256) enc_bwd_kernel(EncBwdArgs a, int rows) {
+  const int c = threadIdx.x;
+  const int width = a.has_enc ? a.wenc : a.h;
+  if (c >= width) return;
+  const int r0 = blockIdx.x * kColRows, r1 = min(rows, r0 + kColRows);
+  const float gec = a.has_enc ? a.ge[c] * kBnC : 1.f;
+  const float gc = c < a.h ? a.g[c] * kBnC : 0.f;
+  float sge = 0.f, sbe = 0.f, sg = 0.f, sb = 0.f;
+  for (int r = r0; r < r1; ++r) {
+    float d = a.dg[(long long)r * a.lddg + c];
+    if (a.has_enc) {
+      sge += d * a.h2[(long long)r * a.ldh2 + c];
+      sbe += d;
+      d *= gec;
+    }
+    if (c < a.h) {
+      const float p = a.p[(long long)r * a.ldp + c];
+      sg += d * lrelu(p);
+      sb += d;
+      a.dp[(long long)r * a.lddp + c] = d * gc * lrelu_grad(p);
+    }
+  }
+  const int stride = (a.has_enc ? 2 * a.wenc : 0) + 2 * a.h;
+  float* pp = a.part + (long long)blockIdx.x * stride;
+  int o = 0;
+  if (a.has_enc) {
+    pp[c] = sge * kBnC;
+    pp[a.wenc + c] = sbe;
+    o = 2 * a.wenc;
+  }
+  if (c < a.h) {
+    pp[o + c] = sg * kBnC;
+    pp[o + a.h + c] = sb;
+  }
+}
+
+// ---------------------------------------------------------------- reduce
+struct ReducePack {
+  ReduceDesc d[kMaxReduce];
+};
+
+__global__ void __launch_bounds__(256) reduce_kernel(ReducePack pk) {
+  const ReduceDesc& d = pk.d[blockIdx.y];
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < d.len; i += gridDim.x * 256) {
+    double acc = 0.0;
+    for (int p = 0; p < d.nparts; ++p) acc += (double)d.src[(long long)p * d.stride + i];
+    float v = (float)(acc * (double)d.scale);
+    if (d.accumulate) v += d.dst[i];
+    d.dst[i] = v;
+  }
+}
+
+// ---------------------------------------------------------------- finalize
+__global__ void __launch_bounds__(256) finalize_kernel(FinalizeArgs a) {
+  double dl = 0, dc = 0, el = 0, tp = 0, kl = 0, ss = 0, sn = 0;
+  for (int k = threadIdx.x; k < a.n_zzt; k += 256) { dl += a.zzt_part[2 * k]; dc += a.zzt_part[2 * k + 1]; }
+  for (int k = threadIdx.x; k < a.n_edge; k += 256) { el += a.edge_part[2 * k]; tp += a.edge_part[2 * k + 1]; }
+  for (int k = threadIdx.x; k < a.n_kl; k += 256) kl += a.kl_part[k];
+  for (int k = threadIdx.x; k < a.n_s; k += 256) {
+    ss += a.sse_s[k];
+    sn += a.sse_n[k];
+  }
+  dl = block_sum(dl); __syncthreads();
+  dc = block_sum(dc); __syncthreads();
+  el = block_sum(el); __syncthreads();
+  tp = block_sum(tp); __syncthreads();
+  kl = block_sum(kl); __syncthreads();
+  ss = block_sum(ss); __syncthreads();
+  sn = block_sum(sn);
+  if (threadIdx.x != 0) return;
+  const double rows = (double)a.ngraphs * a.n;
+  const double pairs = rows * (double)a.n;
+  const double nnz = (double)a.rowptr[(long long)a.ngraphs * a.n];
+  const double adj_sum = (double)a.norm * (dl + el + rows * kSoftplusM1);
+  const double adj_cost = adj_sum / pairs;                      // optimizer.py:144
+  const double correct = pairs - nnz - dc + 2.0 * tp;           // main.py:334
+  const double klm = -0.5 * kl / (rows * a.L);                 // optimizer.py:193
+  const double spatial = ss / (rows * a.sdim);                  // optimizer.py:153
+  const double node = sn / (rows * a.nfeat);                    // optimizer.py:149
+  const double cost = adj_cost + node + spatial + (double)a.beta * klm;   // :157,194
+  double* L = a.losses;
+  L[0] = cost; L[1] = spatial; L[2] = adj_cost; L[3] = node; L[4] = klm;
+  L[5] = correct / pairs; L[6] = adj_sum; L[7] = correct;
+  if (a.grad_tail)
+    for (int k = 0; k < 6; ++k) a.grad_tail[k] = (float)L[k];
+  if (a.step) *a.step += 1;
+}
+
+// ---------------------------------------------------------------- Adam
+__global__ void __launch_bounds__(256) adam_kernel(float* p, const float* g, float* m, float* v,
+                                                   long long n, float lr, float b1, float b2,
+                                                   float eps, float gscale, const int* step) {
+  const int t = *step;
+  const double lr_t = (double)lr * sqrt(1.0 - pow((double)b2, t)) / (1.0 - pow((double)b1, t));
+  const float lrt = (float)lr_t;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n;
+       i += (long long)gridDim.x * 256) {
+    const float gi = g[i] * gscale;
+    const float mi = b1 * m[i] + (1.f - b1) * gi;
+    const float vi = b2 * v[i] + (1.f - b2) * gi * gi;
+    m[i] = mi;
+    v[i] = vi;
+    p[i] -= lrt * mi / (sqrtf(vi) + eps);
+  }
+}
+
+}  // namespace
+
+int reparam_blocks(int rows, int L) {
+  int b = cdiv((long long)rows * L, 256);
+  return b < kReparamGrid ? (b < 1 ? 1 : b) : kReparamGrid;
+}
+int launch_reparam_fwd(const ReparamFwdArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL(reparam_fwd_kernel, dim3(reparam_blocks(a.rows, a.L)), dim3(256), 0, s, a);
+  SND_LAUNCH_CHECK("reparam_fwd_kernel");
+  return 0;
+}
+int launch_reparam_bwd(const ReparamBwdArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL(reparam_bwd_kernel, dim3(reparam_blocks(a.rows, a.L)), dim3(256), 0, s, a);
+  SND_LAUNCH_CHECK("reparam_bwd_kernel");
+  return 0;
+}
+
+int head_blocks(int rows) { return cdiv(rows, kHeadRows); }
+
+int launch_heads(const HeadArgs* h, int nheads, int rows, hipStream_t s) {
+  if (nheads < 1 || nheads > 2) { set_error("heads: 1 or 2 heads"); return SND_ERR_ARG; }
+  HeadPack pk{};
+  for (int i = 0; i < nheads; ++i) {
+    if (h[i].cin > kHeadK || h[i].cout > kHeadO) {
+      set_error("heads: cin <= %d, cout <= %d", kHeadK, kHeadO);
+      return SND_ERR_ARG;
+    }
+    pk.h[i] = h[i];
+  }
+  if (rows <= 0) return 0;
+  hipLaunchKernelGGL(heads_kernel, dim3(head_blocks(rows), nheads), dim3(256), 0, s, pk, rows);
+  SND_LAUNCH_CHECK("heads_kernel");
+  return 0;
+}
+
+int col_blocks(int rows) { return cdiv(rows, kColRows); }
+
+int launch_dec_bwd(const DecBwdArgs* a, int n, int rows, hipStream_t s) {
+  if (n < 1 || n > 2) { set_error("dec_bwd: 1 or 2 descriptors"); return SND_ERR_ARG; }
+  DecPack pk{};
+  for (int i = 0; i < n; ++i) {
+    if (a[i].ncols > 256) { set_error("dec_bwd: ncols %d > 256", a[i].ncols); return SND_ERR_ARG; }
+    pk.d[i] = a[i];
+  }
+  if (rows <= 0) return 0;
+  hipLaunchKernelGGL(dec_bwd_kernel, dim3(col_blocks(rows), n), dim3(256), 0, s, pk, rows);
+  SND_LAUNCH_CHECK("dec_bwd_kernel");
+  return 0;
+}
+
+int launch_enc_bwd(const EncBwdArgs& a, int rows, hipStream_t s) {
+  const int width = a.has_enc ? a.wenc : a.h;
+  if (width > 256) { set_error("enc_bwd: width %d > 256", width); return SND_ERR_ARG; }
+  hipLaunchKernelGGL(enc_bwd_kernel, dim3(col_blocks(rows)), dim3(256), 0, s, a, rows);
+  SND_LAUNCH_CHECK("enc_bwd_kernel");
+  return 0;
+}
+
+int launch_reduce(const ReduceDesc* d, int n, hipStream_t s) {
+  for (int base = 0; base < n; base += kMaxReduce) {
+    ReducePack pk{};
+    const int cnt = n - base < kMaxReduce ? n - base : kMaxReduce;
+    int maxlen = 1;
+    for (int i = 0; i < cnt; ++i) {
+      pk.d[i] = d[base + i];
+      if (pk.d[i].len > maxlen) maxlen = pk.d[i].len;
+    }
+    int gx = cdiv(maxlen, 256);
+    if (gx > 64) gx = 64;
+    hipLaunchKernelGGL(reduce_kernel, dim3(gx, cnt), dim3(256), 0, s, pk);
+    SND_LAUNCH_CHECK("reduce_kernel");
+  }
+  return 0;
+}
+
+int launch_finalize(const FinalizeArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(256), 0, s, a);
+  SND_LAUNCH_CHECK("finalize_kernel");
+  return 0;
+}
+
+}  // namespace snd
+
+using namespace snd;
+
+extern "C" int snd_reparam_kl_blocks(int rows, int latent) { return reparam_blocks(rows, latent); }
+extern "C" int snd_sigmoid_mse_blocks(int rows) { return head_blocks(rows); }
+
+extern "C" int snd_sigmoid_mse(const float* u, int ldu, int rows, int cin, const float* w,
+                               const float* b, int cout, const float* target, int ldt,
+                               double* sse, float* yhat, float* du, int lddu, float* dw,
+                               float* db, void* workspace, size_t workspace_bytes,
+                               snd_stream_t stream) {
+  SND_CHECK_ARG(u && w && b && target && sse && du && dw && db, "snd_sigmoid_mse: null operand");
+  const int nb = head_blocks(rows);
+  const size_t need = (size_t)nb * (cin * cout + cout) * sizeof(float);
+  SND_CHECK_ARG(workspace && workspace_bytes >= need, "snd_sigmoid_mse: workspace %zu < %zu",
+                workspace_bytes, need);
+  hipStream_t s = (hipStream_t)stream;
+  HeadArgs h{u, ldu, cin, w, b, cout, target, ldt, (float)rows * cout, yhat, du, lddu,
+             (float*)workspace, sse};
+  SND_TRY(launch_heads(&h, 1, rows, s));
+  const int stride = cin * cout + cout;
+  ReduceDesc d[2] = {{(const float*)workspace, dw, nb, cin * cout, stride, 1.f, 1},
+                     {(const float*)workspace + cin * cout, db, nb, cout, stride, 1.f, 1}};
+  return launch_reduce(d, 2, s);
+}
+
+extern "C" int snd_reparam_kl(const float* ms, int ldms, int rows, int latent,
+                              const float* eps, unsigned long long seed,
+                              const int* step_counter, float* eps_out, float* z,
+                              double* kl_sum, snd_stream_t stream) {
+  SND_CHECK_ARG(ms && z && kl_sum && rows >= 0 && latent > 0, "snd_reparam_kl: bad args");
+  // kl_sum receives one partial per block; callers sum reparam_blocks() values.
+  ReparamFwdArgs a{ms, ldms, rows, latent, eps, seed, step_counter, eps_out, z, kl_sum};
+  return launch_reparam_fwd(a, (hipStream_t)stream);
+}
+
+extern "C" int snd_adam_tf1(float* param, const float* grad, float* m, float* v, long long n,
+                            float lr, float beta1, float beta2, float eps, float grad_scale,
+                            const int* step_counter, snd_stream_t stream) {
+  SND_CHECK_ARG(param && grad && m && v && step_counter && n >= 0, "snd_adam_tf1: bad args");
+  int blocks = cdiv(n, 256);
+  if (blocks > 2048) blocks = 2048;
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL(adam_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, param, grad,
+                     m, v, n, lr, beta1, beta2, eps, grad_scale, step_counter);
+  SND_LAUNCH_CHECK("adam_kernel");
+  return 0;
+}

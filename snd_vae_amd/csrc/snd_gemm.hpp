@@ -1,0 +1,44 @@
+// Internal launch interfaces shared by the kernel files and the step plan.
+#pragma once
+#include "snd_common.hpp"
+
+namespace snd {
+
+enum AMode { A_ROW = 0, A_COL = 1, A_CONV = 2, A_CONVT = 3 };
+enum BMode { B_ROW = 0, B_COL = 1, B_FLIP = 2 };
+enum Epi { E_STORE = 0, E_CONV = 1, E_PART = 2 };
+
+struct GemmArgs {
+  int M, N, K;
+  const float* A; int lda; int a_cin; int a_npg;
+  const float* B; int ldb; int b_cout;
+  float* C; int ldc;
+  const float* bias; const float* gamma; const float* beta;
+  float* pre; int ldp;
+  int kchunk;       // K range per blockIdx.z (multiple of 32)
+  int accumulate;   // E_STORE: C += result
+  int a_ones_m1;    // A_COL: 1 + row index m that reads as 1.0 (bias-gradient row); 0 = none
+};
+
+int launch_gemm(GemmArgs g, int amode, int bmode, int epi, int dtype, int splits,
+                hipStream_t s);
+int gemm_splits(int K, int target_blocks_per_tile);
+
+// Deterministic reduction of partial slabs: dst[i] (+)= scale * sum_p src[p*stride + i]
+struct ReduceDesc {
+  const float* src;
+  float* dst;
+  int nparts;
+  int len;
+  long long stride;
+  float scale;
+  int accumulate;
+};
+constexpr int kMaxReduce = 48;
+int launch_reduce(const ReduceDesc* d, int n, hipStream_t s);
+
+// Column partial sums written by elementwise kernels are laid out as
+// slab[block][ncols]; helpers compute the block count used.
+constexpr int kColRows = 256;  // rows per block in column-reduction kernels
+
+}  // namespace snd

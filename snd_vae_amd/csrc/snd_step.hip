@@ -1,0 +1,489 @@
+// The SND-VAE train step as one stream-ordered launch sequence (main.py:315-334).
+//
+// snd_plan fixes the shapes of one device batch (B graphs x N nodes), the flat
+// parameter layout (same order and 64-float alignment as
+// snd_vae_amd/params.py::flat_layout) and a workspace map of every
+// intermediate.  snd_train_step enqueues forward + hand-derived backward
+// (~40 kernels, no allocation, no host sync) so the caller can capture it,
+// together with the RCCL gradient all-reduce and snd_adam_tf1, into one HIP
+// graph.  Forward/backward equations: SURVEY.md §8 "Composed step";
+// oracle/ref_numpy.py restates them in float64.
+#include <cstdarg>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "snd_elem.hpp"
+#include "snd_gemm.hpp"
+#include "snd_spmm.hpp"
+#include "snd_zzt.hpp"
+
+namespace snd {
+
+static thread_local char g_err[512] = "";
+
+void set_error(const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+}
+
+namespace {
+
+struct Block { std::string name; long long off, numel; };
+struct Buf { std::string name; long long off, numel; };
+
+// wgrad GEMM split-K geometry
+struct Split { int splits, kchunk; };
+Split wgrad_split(int M, int N, int R) {
+  const int tiles = cdiv(M, 64) * cdiv(N, 64);
+  int s = cdiv(512, tiles);
+  const int smax = cdiv(R, 256);
+  if (s > smax) s = smax;
+  if (s < 1) s = 1;
+  const int kchunk = (int)round_up(cdiv(R, s), 32);
+  return {cdiv(R, kchunk), kchunk};
+}
+
+}  // namespace
+}  // namespace snd
+
+using namespace snd;
+
+struct snd_plan {
+  snd_config_t c;
+  int B, N, R;
+  int W, C1;                   // enc width, fused first decoder conv width
+  std::vector<Block> blocks;
+  long long pcount = 0;
+  std::vector<Buf> bufs;
+  long long ws = 0;
+  // split geometry of the weight-gradient GEMMs
+  Split sW0, sW1, sWh, sWms, sK1, sK2s, sK2n, sK3s;
+
+  long long blk(const char* n) const {
+    for (auto& b : blocks) if (b.name == n) return b.off;
+    return -1;
+  }
+  long long buf(const char* n) const {
+    for (auto& b : bufs) if (b.name == n) return b.off;
+    return -1;
+  }
+  void add_block(const char* n, long long numel) {
+    blocks.push_back({n, pcount, numel});
+    pcount += round_up(numel, 64);
+  }
+  void add_buf(const char* n, long long numel, int esize = 4) {
+    bufs.push_back({n, ws, numel});
+    ws += round_up(numel * esize, 256);
+  }
+};
+
+extern "C" const char* snd_last_error(void) { return g_err; }
+extern "C" int snd_abi_version(void) { return 1; }
+
+extern "C" int snd_plan_create(const snd_config_t* cfg, int n_graphs, snd_plan_t** out) {
+  SND_CHECK_ARG(cfg && out && n_graphs > 0, "snd_plan_create: bad args");
+  const snd_config_t& c = *cfg;
+  SND_CHECK_ARG(c.n_nodes > 0 && c.f_in > 0 && c.h0 > 0 && c.h1 > 0 && c.g_hidden > 0,
+                "snd_plan_create: non-positive width");
+  SND_CHECK_ARG(c.latent == 16 || c.latent == 32 || c.latent == 64 || c.latent == 128,
+                "snd_plan_create: latent %d not in {16,32,64,128}", c.latent);
+  SND_CHECK_ARG(c.h0 <= 128 && c.h1 <= 128, "snd_plan_create: g_conv_hidden <= 128");
+  SND_CHECK_ARG(c.h1 + c.f_in <= 256 && c.s1 + c.n1 <= 256, "snd_plan_create: width <= 256");
+  SND_CHECK_ARG(c.s3 <= 64 && c.n2 <= 64 && c.spatial_dim <= 4 && c.num_feature <= 4,
+                "snd_plan_create: head widths");
+  SND_CHECK_ARG(c.dtype == SND_F32 || c.dtype == SND_BF16, "snd_plan_create: bad dtype");
+  SND_CHECK_ARG((long long)n_graphs * c.n_nodes < (1ll << 30), "snd_plan_create: batch too large");
+  snd_plan* p = new (std::nothrow) snd_plan();
+  if (!p) { set_error("snd_plan_create: out of memory"); return SND_ERR_ARG; }
+  p->c = c;
+  p->B = n_graphs; p->N = c.n_nodes; p->R = n_graphs * c.n_nodes;
+  p->W = c.h1 + c.f_in;
+  p->C1 = c.s1 + c.n1;
+  const int f = c.f_in, h0 = c.h0, h1 = c.h1, gh = c.g_hidden, L = c.latent;
+  const int W = p->W, C1 = p->C1;
+  const long long R = p->R;
+  // ---- flat parameter layout (params.py::block_shapes order)
+  p->add_block("enc.W0", (long long)f * h0);
+  p->add_block("enc.bn0.gamma", h0);
+  p->add_block("enc.bn0.beta", h0);
+  p->add_block("enc.W1", (long long)(h0 + f) * h1);
+  p->add_block("enc.bn1.gamma", h1);
+  p->add_block("enc.bn1.beta", h1);
+  p->add_block("enc.bne.gamma", W);
+  p->add_block("enc.bne.beta", W);
+  p->add_block("enc.Wh", (long long)W * gh);
+  p->add_block("enc.bh", gh);
+  p->add_block("enc.Wms", (long long)gh * 2 * L);
+  p->add_block("enc.bms", 2 * L);
+  p->add_block("dec.K1", 5LL * L * C1);
+  p->add_block("dec.b1", C1);
+  p->add_block("dec.bn1.gamma", C1);
+  p->add_block("dec.bn1.beta", C1);
+  p->add_block("dec.K2s", 5LL * c.s1 * c.s2);
+  p->add_block("dec.b2s", c.s2);
+  p->add_block("dec.bn2s.gamma", c.s2);
+  p->add_block("dec.bn2s.beta", c.s2);
+  p->add_block("dec.K2n", 5LL * c.n1 * c.n2);
+  p->add_block("dec.b2n", c.n2);
+  p->add_block("dec.bn2n.gamma", c.n2);
+  p->add_block("dec.bn2n.beta", c.n2);
+  p->add_block("dec.K3s", 5LL * c.s2 * c.s3);
+  p->add_block("dec.b3s", c.s3);
+  p->add_block("dec.bn3s.gamma", c.s3);
+  p->add_block("dec.bn3s.beta", c.s3);
+  p->add_block("dec.Ws", (long long)c.s3 * c.spatial_dim);
+  p->add_block("dec.bs", c.spatial_dim);
+  p->add_block("dec.Wn", (long long)c.n2 * c.num_feature);
+  p->add_block("dec.bn", c.num_feature);
+
+  // ---- workspace
+  p->add_buf("XW0", R * h0);  p->add_buf("P0", R * h0);  p->add_buf("H1", R * (h0 + f));
+  p->add_buf("XW1", R * h1);  p->add_buf("P1", R * h1);  p->add_buf("H2", R * W);
+  p->add_buf("G", R * W);     p->add_buf("Hh", R * gh);  p->add_buf("MS", R * 2 * L);
+  p->add_buf("EPS", R * L);   p->add_buf("Z", R * L);
+  p->add_buf("ZSTAGE", (long long)zzt_staging_bytes(p->B, p->N, L, c.dtype), 1);
+  p->add_buf("DJD", R * L);   p->add_buf("EJ", R * L);
+  p->add_buf("Y1", R * C1);   p->add_buf("U1", R * C1);
+  p->add_buf("Y2S", R * c.s2); p->add_buf("U2S", R * c.s2);
+  p->add_buf("Y2N", R * c.n2); p->add_buf("U2N", R * c.n2);
+  p->add_buf("Y3S", R * c.s3); p->add_buf("U3S", R * c.s3);
+  p->add_buf("SHAT", R * c.spatial_dim); p->add_buf("XHAT", R * c.num_feature);
+  p->add_buf("DU3S", R * c.s3); p->add_buf("DY3S", R * c.s3);
+  p->add_buf("DU2S", R * c.s2); p->add_buf("DY2S", R * c.s2);
+  p->add_buf("DU2N", R * c.n2); p->add_buf("DY2N", R * c.n2);
+  p->add_buf("DU1", R * C1);  p->add_buf("DY1", R * C1);  p->add_buf("DZDEC", R * L);
+  p->add_buf("DMS", R * 2 * L); p->add_buf("DH", R * gh); p->add_buf("DG", R * W);
+  p->add_buf("DP1", R * h1);  p->add_buf("DXW1", R * h1); p->add_buf("DH1", R * h0);
+  p->add_buf("DP0", R * h0);  p->add_buf("DXW0", R * h0);
+  const int nz = zzt_dense_blocks(p->B, p->N), ne = edge_blocks(p->R, L);
+  const int nk = reparam_blocks(p->R, L), nh = head_blocks(p->R), nc = col_blocks(p->R);
+  p->add_buf("PZZT", 2LL * nz, 8); p->add_buf("PEDGE", 2LL * ne, 8); p->add_buf("PKL", nk, 8);
+  p->add_buf("PSSES", nh, 8); p->add_buf("PSSEN", nh, 8);
+  p->add_buf("PHS", (long long)nh * (c.s3 * c.spatial_dim + c.spatial_dim));
+  p->add_buf("PHN", (long long)nh * (c.n2 * c.num_feature + c.num_feature));
+  p->add_buf("PDEC3", (long long)nc * 3 * c.s3); p->add_buf("PDEC2S", (long long)nc * 3 * c.s2);
+  p->add_buf("PDEC2N", (long long)nc * 3 * c.n2); p->add_buf("PDEC1", (long long)nc * 3 * C1);
+  p->add_buf("PENC1", (long long)nc * (2 * W + 2 * h1)); p->add_buf("PENC0", (long long)nc * 2 * h0);
+  p->sW0 = wgrad_split(f, h0, p->R);
+  p->sW1 = wgrad_split(h0 + f, h1, p->R);
+  p->sWh = wgrad_split(W + 1, gh, p->R);
+  p->sWms = wgrad_split(gh + 1, 2 * L, p->R);
+  p->sK1 = wgrad_split(5 * L, C1, p->R);
+  p->sK2s = wgrad_split(5 * c.s1, c.s2, p->R);
+  p->sK2n = wgrad_split(5 * c.n1, c.n2, p->R);
+  p->sK3s = wgrad_split(5 * c.s2, c.s3, p->R);
+  p->add_buf("SW0", (long long)p->sW0.splits * f * h0);
+  p->add_buf("SW1", (long long)p->sW1.splits * (h0 + f) * h1);
+  p->add_buf("SWH", (long long)p->sWh.splits * (W + 1) * gh);
+  p->add_buf("SWMS", (long long)p->sWms.splits * (gh + 1) * 2 * L);
+  p->add_buf("SK1", (long long)p->sK1.splits * 5 * L * C1);
+  p->add_buf("SK2S", (long long)p->sK2s.splits * 5 * c.s1 * c.s2);
+  p->add_buf("SK2N", (long long)p->sK2n.splits * 5 * c.n1 * c.n2);
+  p->add_buf("SK3S", (long long)p->sK3s.splits * 5 * c.s2 * c.s3);
+  *out = p;
+  return 0;
+}
+
+extern "C" void snd_plan_destroy(snd_plan_t* p) { delete p; }
+extern "C" long long snd_plan_param_count(const snd_plan_t* p) { return p ? p->pcount : -1; }
+extern "C" int snd_plan_num_blocks(const snd_plan_t* p) { return p ? (int)p->blocks.size() : -1; }
+extern "C" int snd_plan_param_block(const snd_plan_t* p, int idx, const char** name,
+                                    long long* offset, long long* numel) {
+  SND_CHECK_ARG(p && idx >= 0 && idx < (int)p->blocks.size(), "snd_plan_param_block: bad index");
+  if (name) *name = p->blocks[idx].name.c_str();
+  if (offset) *offset = p->blocks[idx].off;
+  if (numel) *numel = p->blocks[idx].numel;
+  return 0;
+}
+extern "C" size_t snd_plan_workspace_bytes(const snd_plan_t* p) { return p ? (size_t)p->ws : 0; }
+extern "C" int snd_plan_buffer(const snd_plan_t* p, const char* name, long long* off,
+                               long long* numel) {
+  SND_CHECK_ARG(p && name, "snd_plan_buffer: bad args");
+  for (auto& b : p->bufs)
+    if (b.name == name) {
+      if (off) *off = b.off;
+      if (numel) *numel = b.numel;
+      return 0;
+    }
+  set_error("snd_plan_buffer: no buffer '%s'", name);
+  return SND_ERR_ARG;
+}
+
+namespace {
+
+struct Ctx {
+  const snd_plan* p;
+  char* ws;
+  const float* P;
+  float* Gr;
+  hipStream_t s;
+  float* f(const char* n) const { return (float*)(ws + p->buf(n)); }
+  double* d(const char* n) const { return (double*)(ws + p->buf(n)); }
+  const float* w(const char* n) const { return P + p->blk(n); }
+  float* g(const char* n) const { return Gr + p->blk(n); }
+};
+
+int gemm_fwd(const Ctx& x, int M, int N, int K, const float* A, int lda, const float* B, int ldb,
+             int bmode, float* C, int ldc, const float* bias) {
+  GemmArgs g{};
+  g.M = M; g.N = N; g.K = K; g.A = A; g.lda = lda; g.B = B; g.ldb = ldb; g.C = C; g.ldc = ldc;
+  g.bias = bias; g.kchunk = (int)round_up(K, 32);
+  return launch_gemm(g, A_ROW, bmode, E_STORE, x.p->c.dtype, 1, x.s);
+}
+
+int gemm_wgrad(const Ctx& x, const float* A, int lda, int Mreal, bool ones, const float* D,
+               int ldd, int N, float* slab, const Split& sp) {
+  GemmArgs g{};
+  g.M = Mreal + (ones ? 1 : 0); g.N = N; g.K = x.p->R;
+  g.A = A; g.lda = lda; g.a_ones_m1 = ones ? Mreal + 1 : 0;
+  g.B = D; g.ldb = ldd; g.C = slab; g.kchunk = sp.kchunk;
+  return launch_gemm(g, A_COL, B_ROW, E_PART, x.p->c.dtype, sp.splits, x.s);
+}
+
+int conv_fwd(const Ctx& x, const float* in, int ldi, int cin, const char* K, int cout,
+             const char* b, const char* gam, const char* bet, float* ypre, float* out) {
+  GemmArgs g{};
+  g.M = x.p->R; g.N = cout; g.K = 5 * cin;
+  g.A = in; g.lda = ldi; g.a_cin = cin; g.a_npg = x.p->N;
+  g.B = x.w(K); g.ldb = cout; g.C = out; g.ldc = cout; g.bias = x.w(b);
+  g.gamma = x.w(gam); g.beta = x.w(bet); g.pre = ypre; g.ldp = cout;
+  g.kchunk = (int)round_up(g.K, 32);
+  return launch_gemm(g, A_CONV, B_ROW, E_CONV, x.p->c.dtype, 1, x.s);
+}
+
+int conv_bwd_data(const Ctx& x, const float* dy, int cout, const char* K, int cin, float* dx,
+                  int lddx) {
+  GemmArgs g{};
+  g.M = x.p->R; g.N = cin; g.K = 5 * cout;
+  g.A = dy; g.lda = cout; g.a_cin = cout; g.a_npg = x.p->N;
+  g.B = x.w(K); g.b_cout = cout; g.C = dx; g.ldc = lddx;
+  g.kchunk = (int)round_up(g.K, 32);
+  return launch_gemm(g, A_CONV, B_FLIP, E_STORE, x.p->c.dtype, 1, x.s);
+}
+
+int conv_wgrad(const Ctx& x, const float* in, int ldi, int cin, const float* dy, int cout,
+               float* slab, const Split& sp) {
+  GemmArgs g{};
+  g.M = 5 * cin; g.N = cout; g.K = x.p->R;
+  g.A = in; g.lda = ldi; g.a_cin = cin; g.a_npg = x.p->N;
+  g.B = dy; g.ldb = cout; g.C = slab; g.kchunk = sp.kchunk;
+  return launch_gemm(g, A_CONVT, B_ROW, E_PART, x.p->c.dtype, sp.splits, x.s);
+}
+
+}  // namespace
+
+extern "C" int snd_plan_launch(const snd_plan_t* plan, const snd_batch_t* batch,
+                               void* workspace, const char* kernel, snd_stream_t stream) {
+  SND_CHECK_ARG(plan && batch && workspace && kernel, "snd_plan_launch: null argument");
+  SND_TRY(zzt_init_attributes());
+  const snd_plan& p = *plan;
+  char* ws = (char*)workspace;
+  hipStream_t s = (hipStream_t)stream;
+  const int L = p.c.latent;
+  if (!strcmp(kernel, "zzt_dense")) {
+    const size_t half = zzt_staging_bytes(p.B, p.N, L, p.c.dtype) / 2;
+    char* st = ws + p.buf("ZSTAGE");
+    ZztArgs za{st, st + half, p.N, zzt_npad(p.N), p.B, L, (float*)(ws + p.buf("DJD")),
+               (double*)(ws + p.buf("PZZT"))};
+    return launch_zzt_dense(za, p.c.dtype, s);
+  }
+  if (!strcmp(kernel, "spmm_dxw1")) {   // A @ dP1 (plain SpMM, width h1)
+    SpmmArgs a{batch->rowptr, batch->colidx, p.R, (const float*)(ws + p.buf("DP1")), p.c.h1,
+               p.c.h1, (float*)(ws + p.buf("DXW1")), p.c.h1, SND_SPMM_PLAIN};
+    return launch_spmm(a, s);
+  }
+  set_error("snd_plan_launch: unknown kernel '%s'", kernel);
+  return SND_ERR_ARG;
+}
+
+extern "C" int snd_train_step(const snd_plan_t* plan, const snd_batch_t* batch,
+                              const float* params, float* grads, void* workspace,
+                              const float* eps, unsigned long long seed, int* step_counter,
+                              double* losses, snd_stream_t stream) {
+  SND_CHECK_ARG(plan && batch && params && grads && workspace && losses,
+                "snd_train_step: null argument");
+  SND_CHECK_ARG(batch->rowptr && batch->colidx && batch->features && batch->feature_truth &&
+                    batch->spatial_truth, "snd_train_step: incomplete batch");
+  SND_TRY(zzt_init_attributes());
+  const snd_plan& p = *plan;
+  const snd_config_t& c = p.c;
+  Ctx x{&p, (char*)workspace, params, grads, (hipStream_t)stream};
+  const int R = p.R, N = p.N, f = c.f_in, h0 = c.h0, h1 = c.h1, gh = c.g_hidden, L = c.latent;
+  const int W = p.W, C1 = p.C1, s1 = c.s1, s2 = c.s2, s3 = c.s3, n1 = c.n1, n2 = c.n2;
+  const int sd = c.spatial_dim, nf = c.num_feature;
+  const int* rp = batch->rowptr;
+  const int* ci = batch->colidx;
+  const float* X = batch->features;
+
+  // =============================== forward ===============================
+  // encoder, model.py:104-112: H_{i+1} = [BN(lrelu(A (H_i W_i))) || X]
+  SND_TRY(gemm_fwd(x, R, h0, f, X, f, x.w("enc.W0"), h0, B_ROW, x.f("XW0"), h0, nullptr));
+  {
+    SpmmArgs a{rp, ci, R, x.f("XW0"), h0, h0, x.f("H1"), h0 + f, SND_SPMM_GCN,
+               x.w("enc.bn0.gamma"), x.w("enc.bn0.beta"), x.f("P0"), h0, X, f, f,
+               nullptr, nullptr, nullptr, 0};
+    SND_TRY(launch_spmm(a, x.s));
+  }
+  SND_TRY(gemm_fwd(x, R, h1, h0 + f, x.f("H1"), h0 + f, x.w("enc.W1"), h1, B_ROW, x.f("XW1"), h1,
+                   nullptr));
+  {
+    SpmmArgs a{rp, ci, R, x.f("XW1"), h1, h1, x.f("H2"), W, SND_SPMM_GCN,
+               x.w("enc.bn1.gamma"), x.w("enc.bn1.beta"), x.f("P1"), h1, X, f, f,
+               x.w("enc.bne.gamma"), x.w("enc.bne.beta"), x.f("G"), W};
+    SND_TRY(launch_spmm(a, x.s));
+  }
+  // node-wise heads (model.py:113-115): h = G Wh + bh; [mu || s] = h Wms + bms
+  SND_TRY(gemm_fwd(x, R, gh, W, x.f("G"), W, x.w("enc.Wh"), gh, B_ROW, x.f("Hh"), gh,
+                   x.w("enc.bh")));
+  SND_TRY(gemm_fwd(x, R, 2 * L, gh, x.f("Hh"), gh, x.w("enc.Wms"), 2 * L, B_ROW, x.f("MS"), 2 * L,
+                   x.w("enc.bms")));
+  // z = mu + eps exp(s) (model.py:159); KL partials (optimizer.py:193)
+  {
+    ReparamFwdArgs a{x.f("MS"), 2 * L, R, L, eps, seed, step_counter, x.f("EPS"), x.f("Z"),
+                     x.d("PKL")};
+    SND_TRY(launch_reparam_fwd(a, x.s));
+  }
+  // inner-product decoder + CE (fused) and per-edge terms
+  {
+    const size_t half = zzt_staging_bytes(p.B, N, L, c.dtype) / 2;
+    char* st = x.ws + p.buf("ZSTAGE");
+    SND_TRY(launch_zzt_prep(x.f("Z"), p.B, N, L, c.dtype, st, st + half, x.s));
+    ZztArgs za{st, st + half, N, zzt_npad(N), p.B, L, x.f("DJD"), x.d("PZZT")};
+    SND_TRY(launch_zzt_dense(za, c.dtype, x.s));
+    EdgeArgs ea{rp, ci, R, x.f("Z"), L, c.pos_weight, x.f("EJ"), x.d("PEDGE")};
+    SND_TRY(launch_edge(ea, x.s));
+  }
+  // decoders (model_joint.py:112-145): conv1d k5 SAME -> BN -> lrelu
+  SND_TRY(conv_fwd(x, x.f("Z"), L, L, "dec.K1", C1, "dec.b1", "dec.bn1.gamma", "dec.bn1.beta",
+                   x.f("Y1"), x.f("U1")));
+  SND_TRY(conv_fwd(x, x.f("U1"), C1, s1, "dec.K2s", s2, "dec.b2s", "dec.bn2s.gamma",
+                   "dec.bn2s.beta", x.f("Y2S"), x.f("U2S")));
+  SND_TRY(conv_fwd(x, x.f("U1") + s1, C1, n1, "dec.K2n", n2, "dec.b2n", "dec.bn2n.gamma",
+                   "dec.bn2n.beta", x.f("Y2N"), x.f("U2N")));
+  SND_TRY(conv_fwd(x, x.f("U2S"), s2, s2, "dec.K3s", s3, "dec.b3s", "dec.bn3s.gamma",
+                   "dec.bn3s.beta", x.f("Y3S"), x.f("U3S")));
+  // sigmoid heads + MSE + their backward (optimizer.py:149,153)
+  {
+    HeadArgs h[2] = {
+        {x.f("U3S"), s3, s3, x.w("dec.Ws"), x.w("dec.bs"), sd, batch->spatial_truth, sd,
+         (float)R * sd, x.f("SHAT"), x.f("DU3S"), s3, x.f("PHS"), x.d("PSSES")},
+        {x.f("U2N"), n2, n2, x.w("dec.Wn"), x.w("dec.bn"), nf, batch->feature_truth, nf,
+         (float)R * nf, x.f("XHAT"), x.f("DU2N"), n2, x.f("PHN"), x.d("PSSEN")}};
+    SND_TRY(launch_heads(h, 2, R, x.s));
+  }
+  // =============================== backward ==============================
+  {
+    DecBwdArgs d{x.f("DU3S"), s3, x.f("Y3S"), s3, x.w("dec.bn3s.gamma"), x.w("dec.bn3s.beta"), s3,
+                 x.f("DY3S"), s3, x.f("PDEC3")};
+    SND_TRY(launch_dec_bwd(&d, 1, R, x.s));
+  }
+  SND_TRY(conv_bwd_data(x, x.f("DY3S"), s3, "dec.K3s", s2, x.f("DU2S"), s2));
+  SND_TRY(conv_wgrad(x, x.f("U2S"), s2, s2, x.f("DY3S"), s3, x.f("SK3S"), p.sK3s));
+  {
+    DecBwdArgs d[2] = {
+        {x.f("DU2S"), s2, x.f("Y2S"), s2, x.w("dec.bn2s.gamma"), x.w("dec.bn2s.beta"), s2,
+         x.f("DY2S"), s2, x.f("PDEC2S")},
+        {x.f("DU2N"), n2, x.f("Y2N"), n2, x.w("dec.bn2n.gamma"), x.w("dec.bn2n.beta"), n2,
+         x.f("DY2N"), n2, x.f("PDEC2N")}};
+    SND_TRY(launch_dec_bwd(d, 2, R, x.s));
+  }
+  SND_TRY(conv_bwd_data(x, x.f("DY2S"), s2, "dec.K2s", s1, x.f("DU1"), C1));
+  SND_TRY(conv_bwd_data(x, x.f("DY2N"), n2, "dec.K2n", n1, x.f("DU1") + s1, C1));
+  SND_TRY(conv_wgrad(x, x.f("U1"), C1, s1, x.f("DY2S"), s2, x.f("SK2S"), p.sK2s));
+  SND_TRY(conv_wgrad(x, x.f("U1") + s1, C1, n1, x.f("DY2N"), n2, x.f("SK2N"), p.sK2n));
+  {
+    DecBwdArgs d{x.f("DU1"), C1, x.f("Y1"), C1, x.w("dec.bn1.gamma"), x.w("dec.bn1.beta"), C1,
+                 x.f("DY1"), C1, x.f("PDEC1")};
+    SND_TRY(launch_dec_bwd(&d, 1, R, x.s));
+  }
+  SND_TRY(conv_bwd_data(x, x.f("DY1"), C1, "dec.K1", L, x.f("DZDEC"), L));
+  SND_TRY(conv_wgrad(x, x.f("Z"), L, L, x.f("DY1"), C1, x.f("SK1"), p.sK1));
+  // reparameterisation + KL backward; dz = conv-decoder grad + zz^T CE grad
+  {
+    const double pairs = (double)p.B * N * (double)N;
+    // dL/dz_i = sum_j (G_ij + G_ji) z_j = 2 sum_j G_ij z_j (G symmetric)
+    const float adj_scale = (float)(2.0 * (double)c.norm / pairs);
+    const float kl_scale = (float)((double)c.beta / ((double)R * L));
+    ReparamBwdArgs a{x.f("MS"), 2 * L, R, L, x.f("EPS"), x.f("DZDEC"), x.f("DJD"), x.f("EJ"),
+                     adj_scale, kl_scale, x.f("DMS"), 2 * L};
+    SND_TRY(launch_reparam_bwd(a, x.s));
+  }
+  SND_TRY(gemm_wgrad(x, x.f("Hh"), gh, gh, true, x.f("DMS"), 2 * L, 2 * L, x.f("SWMS"), p.sWms));
+  SND_TRY(gemm_fwd(x, R, gh, 2 * L, x.f("DMS"), 2 * L, x.w("enc.Wms"), 2 * L, B_COL, x.f("DH"), gh,
+                   nullptr));
+  SND_TRY(gemm_wgrad(x, x.f("G"), W, W, true, x.f("DH"), gh, gh, x.f("SWH"), p.sWh));
+  SND_TRY(gemm_fwd(x, R, W, gh, x.f("DH"), gh, x.w("enc.Wh"), gh, B_COL, x.f("DG"), W, nullptr));
+  {
+    EncBwdArgs a{x.f("DG"), W, x.f("H2"), W, x.w("enc.bne.gamma"), W, x.f("P1"), h1,
+                 x.w("enc.bn1.gamma"), h1, x.f("DP1"), h1, x.f("PENC1"), 1};
+    SND_TRY(launch_enc_bwd(a, R, x.s));
+  }
+  {
+    SpmmArgs a{rp, ci, R, x.f("DP1"), h1, h1, x.f("DXW1"), h1, SND_SPMM_PLAIN};
+    SND_TRY(launch_spmm(a, x.s));
+  }
+  SND_TRY(gemm_wgrad(x, x.f("H1"), h0 + f, h0 + f, false, x.f("DXW1"), h1, h1, x.f("SW1"), p.sW1));
+  SND_TRY(gemm_fwd(x, R, h0, h1, x.f("DXW1"), h1, x.w("enc.W1"), h1, B_COL, x.f("DH1"), h0,
+                   nullptr));
+  {
+    EncBwdArgs a{x.f("DH1"), h0, nullptr, 0, nullptr, 0, x.f("P0"), h0, x.w("enc.bn0.gamma"), h0,
+                 x.f("DP0"), h0, x.f("PENC0"), 0};
+    SND_TRY(launch_enc_bwd(a, R, x.s));
+  }
+  {
+    SpmmArgs a{rp, ci, R, x.f("DP0"), h0, h0, x.f("DXW0"), h0, SND_SPMM_PLAIN};
+    SND_TRY(launch_spmm(a, x.s));
+  }
+  SND_TRY(gemm_wgrad(x, X, f, f, false, x.f("DXW0"), h0, h0, x.f("SW0"), p.sW0));
+
+  // ======================= deterministic gradient reduction =================
+  const int nc = col_blocks(R), nh = head_blocks(R);
+  std::vector<ReduceDesc> rd;
+  auto slab = [&](const char* buf, const Split& sp, int Mtot, int N_, const char* wname,
+                  int wlen, const char* bname) {
+    const float* s0 = x.f(buf);
+    rd.push_back({s0, x.g(wname), sp.splits, wlen, (long long)Mtot * N_, 1.f, 0});
+    if (bname) rd.push_back({s0 + wlen, x.g(bname), sp.splits, N_, (long long)Mtot * N_, 1.f, 0});
+  };
+  slab("SW0", p.sW0, f, h0, "enc.W0", f * h0, nullptr);
+  slab("SW1", p.sW1, h0 + f, h1, "enc.W1", (h0 + f) * h1, nullptr);
+  slab("SWH", p.sWh, W + 1, gh, "enc.Wh", W * gh, "enc.bh");
+  slab("SWMS", p.sWms, gh + 1, 2 * L, "enc.Wms", gh * 2 * L, "enc.bms");
+  slab("SK1", p.sK1, 5 * L, C1, "dec.K1", 5 * L * C1, nullptr);
+  slab("SK2S", p.sK2s, 5 * s1, s2, "dec.K2s", 5 * s1 * s2, nullptr);
+  slab("SK2N", p.sK2n, 5 * n1, n2, "dec.K2n", 5 * n1 * n2, nullptr);
+  slab("SK3S", p.sK3s, 5 * s2, s3, "dec.K3s", 5 * s2 * s3, nullptr);
+  auto cols = [&](const char* buf, int stride, int off, int len, const char* dst) {
+    rd.push_back({x.f(buf) + off, x.g(dst), nc, len, (long long)stride, 1.f, 0});
+  };
+  cols("PENC1", 2 * W + 2 * h1, 0, W, "enc.bne.gamma");
+  cols("PENC1", 2 * W + 2 * h1, W, W, "enc.bne.beta");
+  cols("PENC1", 2 * W + 2 * h1, 2 * W, h1, "enc.bn1.gamma");
+  cols("PENC1", 2 * W + 2 * h1, 2 * W + h1, h1, "enc.bn1.beta");
+  cols("PENC0", 2 * h0, 0, h0, "enc.bn0.gamma");
+  cols("PENC0", 2 * h0, h0, h0, "enc.bn0.beta");
+  auto dec = [&](const char* buf, int w, const char* g, const char* b, const char* bias) {
+    cols(buf, 3 * w, 0, w, g);
+    cols(buf, 3 * w, w, w, b);
+    cols(buf, 3 * w, 2 * w, w, bias);
+  };
+  dec("PDEC3", s3, "dec.bn3s.gamma", "dec.bn3s.beta", "dec.b3s");
+  dec("PDEC2S", s2, "dec.bn2s.gamma", "dec.bn2s.beta", "dec.b2s");
+  dec("PDEC2N", n2, "dec.bn2n.gamma", "dec.bn2n.beta", "dec.b2n");
+  dec("PDEC1", C1, "dec.bn1.gamma", "dec.bn1.beta", "dec.b1");
+  const int hs = s3 * sd + sd, hn = n2 * nf + nf;
+  rd.push_back({x.f("PHS"), x.g("dec.Ws"), nh, s3 * sd, (long long)hs, 1.f, 0});
+  rd.push_back({x.f("PHS") + s3 * sd, x.g("dec.bs"), nh, sd, (long long)hs, 1.f, 0});
+  rd.push_back({x.f("PHN"), x.g("dec.Wn"), nh, n2 * nf, (long long)hn, 1.f, 0});
+  rd.push_back({x.f("PHN") + n2 * nf, x.g("dec.bn"), nh, nf, (long long)hn, 1.f, 0});
+  SND_TRY(launch_reduce(rd.data(), (int)rd.size(), x.s));
+
+  FinalizeArgs fa{x.d("PZZT"), zzt_dense_blocks(p.B, N), x.d("PEDGE"), edge_blocks(R, L),
+                  x.d("PKL"), reparam_blocks(R, L), x.d("PSSES"), x.d("PSSEN"), nh,
+                  rp, p.B, N, L, sd, nf, c.beta, c.norm, losses, grads + p.pcount, step_counter};
+  return launch_finalize(fa, x.s);
+}

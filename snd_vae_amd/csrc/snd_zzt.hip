@@ -1,0 +1,519 @@
+// Fused inner-product structure decoder + 2-class cross-entropy, fwd + bwd.
+//
+// Replaces, per graph: L = z z^T (InnerProductDecoder, layers.py:407-409),
+// the diagonal rule (model.py:185,205-207), argmax (model.py:208), the
+// accuracy count (main.py:334) and softmax_cross_entropy_with_logits
+// (optimizer.py:142-144) plus its gradient.  The reference materialises
+// [B,N,N,2] logits; here no logit ever reaches HBM.
+//
+// Split of the CE over pairs (i != j):  CE = softplus(L) - A L.
+//   dense kernel (this file): sum_{i!=j} softplus(L_ij), #{L_ij > 0},
+//                              dJd_i = sum_{j!=i} sigmoid(L_ij) z_j
+//   edge kernel (snd_spmm.hip): the A-weighted terms over the CSR only.
+// so the adjacency never enters the O(N^2 d) kernel.
+//
+// Dense kernel structure (flash-style, no softmax normalisation needed):
+//   workgroup = 8 waves x 16 rows i (128 rows of one graph); column tiles of
+//   64 j staged in LDS twice -- z rows (K role) and z^T (V role) -- double
+//   buffered, one barrier per tile.  Per 32-column chunk each wave runs
+//   MFMA1  X[j,i] = z_j . z_i           (16x16x32 bf16, z_i held in VGPRs)
+//   VALU   sigma / softplus / count on X (exp2 + rcp; one log2 per 8 logits
+//          via the product identity sum log(1+e_k) = log prod(1+e_k))
+//   MFMA2  dJd^T[c,i] += z^T[c,j] sigma[j,i]  -- the f32 accumulator X is
+//          re-packed to bf16 in registers and used as the B operand directly
+//          (no LDS round trip; k order permuted to match).
+// z is pre-scaled by sqrt(log2 e) for the K role, so X = L log2(e) feeds
+// v_exp_f32 (2^x) with no multiply.  LDS images are XOR-swizzled so the
+// ds_read_b128 (K role) and ds_read_b64 (V role) operand reads are
+// bank-conflict-free.  Block -> (graph, row block) puts one graph's blocks on
+// one XCD when B % 8 == 0 (blockIdx % 8 == graph % 8), so a graph's z stays
+// in that XCD's L2.
+// fp32 parity mode uses the exact-f32 MFMA 16x16x4 with the same structure.
+#include "snd_zzt.hpp"
+#include "snd_spmm.hpp"
+
+namespace snd {
+namespace {
+
+constexpr int TJ = 64;      // columns per LDS tile
+constexpr int ROWS = 128;   // rows per workgroup
+constexpr int NTH = 512;
+
+// ---------------------------------------------------------------- prep
+template <typename T, int DP>
+__global__ void __launch_bounds__(256) zzt_prep_kernel(const float* z, int n, int npad,
+                                                       int d, T* jrow, T* jt) {
+  __shared__ float tile[64][DP + 1];
+  const int g = blockIdx.y, rb = blockIdx.x;
+  const float sc = 1.2011224087864498f;  // sqrt(log2 e)
+  for (int idx = threadIdx.x; idx < 64 * DP; idx += 256) {
+    const int rr = idx / DP, c = idx - rr * DP;
+    const int row = rb * 64 + rr;
+    const float v = (row < n && c < d) ? z[((long long)g * n + row) * d + c] : 0.f;
+    tile[rr][c] = v;
+    jrow[((long long)g * npad + row) * DP + c] = (T)(v * sc);
+  }
+  __syncthreads();
+  for (int idx = threadIdx.x; idx < 64 * DP; idx += 256) {
+    const int c = idx >> 6, rr = idx & 63;
+    jt[((long long)g * DP + c) * npad + rb * 64 + rr] = (T)tile[rr][c];
+  }
+}
+
+// ---------------------------------------------------------------- epilogue
+struct ChunkStats {
+  double loss2;   // sum over valid pairs of max(x,0) + log2(1 + 2^-|x|), x = L log2 e
+  unsigned cnt;   // #{x > 0}
+};
+
+// x[8]: logits (scaled) of this lane; j of element e = jbase + 16*(e>>2) + 4*q4 + (e&3)
+template <bool SPECIAL>
+__device__ __forceinline__ void chunk_epilogue(const float (&x)[8], float (&sv)[8],
+                                               ChunkStats& st, int jbase, int q4,
+                                               int i, int n) {
+  float cs = 0.f, prod = 1.f;
+  unsigned cnt = 0;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    bool valid = true;
+    if constexpr (SPECIAL) {
+      const int j = jbase + 16 * (e >> 2) + 4 * q4 + (e & 3);
+      valid = (j < n) && (i < n) && (j != i);
+    }
+    const float xv = x[e];
+    const float ex = __builtin_amdgcn_exp2f(-fabsf(xv));
+    const float qd = 1.f + ex;
+    const float rc = __builtin_amdgcn_rcpf(qd);
+    const float sg = xv > 0.f ? rc : ex * rc;
+    if (valid) {
+      prod *= qd;
+      cs += fmaxf(xv, 0.f);
+      cnt += xv > 0.f ? 1u : 0u;
+      sv[e] = sg;
+    } else {
+      sv[e] = 0.f;
+    }
+  }
+  st.loss2 += (double)(cs + __builtin_amdgcn_logf(prod));
+  st.cnt += cnt;
+}
+
+__device__ __forceinline__ void block_reduce_write(ChunkStats st, double* part) {
+  __shared__ double sl[NTH / 64];
+  __shared__ unsigned sc[NTH / 64];
+  double l = wave_sum_d(st.loss2);
+  unsigned c = wave_sum_u(st.cnt);
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) { sl[w] = l; sc[w] = c; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double tl = 0.0, tc = 0.0;
+    for (int k = 0; k < NTH / 64; ++k) { tl += sl[k]; tc += (double)sc[k]; }
+    part[2 * blockIdx.x] = tl * (double)kLn2;
+    part[2 * blockIdx.x + 1] = tc;
+  }
+}
+
+// ---------------------------------------------------------------- bf16 MFMA
+template <int DP> struct Swz;
+template <> struct Swz<32> { static __device__ __forceinline__ int j(int) { return 0; } };
+template <> struct Swz<64> { static __device__ __forceinline__ int j(int row) { return (row >> 1) & 7; } };
+template <> struct Swz<128> { static __device__ __forceinline__ int j(int row) { return row & 15; } };
+__device__ __forceinline__ int swz_t(int c) { return (c >> 1) & 7; }   // z^T image, 16 B chunks
+
+template <int DP>
+__global__ void __launch_bounds__(NTH) zzt_dense_bf16(ZztArgs a) {
+  constexpr int JS = TJ * DP;          // z rows image (elements)
+  constexpr int TS = DP * TJ;          // z^T image
+  constexpr int KS = DP / 32;
+  constexpr int CT = DP / 16;
+  constexpr int CPR = DP / 8;          // 16 B chunks per z row
+  constexpr int JCH = TJ * CPR, TCH = DP * (TJ / 8);
+  constexpr int JPT = (JCH + NTH - 1) / NTH, TPT = (TCH + NTH - 1) / NTH;
+  __shared__ __attribute__((aligned(16))) __bf16 lds[2][JS + TS];
+
+  const int g = blockIdx.x % a.ngraphs, rb = blockIdx.x / a.ngraphs;
+  const __bf16* Jg = reinterpret_cast<const __bf16*>(a.jrow) + (long long)g * a.npad * DP;
+  const __bf16* JTg = reinterpret_cast<const __bf16*>(a.jt) + (long long)g * DP * a.npad;
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, r = lane & 15, q4 = lane >> 4;
+  const int i0 = rb * ROWS + 16 * w;
+
+  bf16x8 bI[KS];
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks)
+    bI[ks] = *reinterpret_cast<const bf16x8*>(Jg + (long long)(i0 + r) * DP + 32 * ks + 8 * q4);
+  f32x4 acc[CT];
+#pragma unroll
+  for (int ct = 0; ct < CT; ++ct) acc[ct] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  uint4 rj[JPT], rt[TPT];
+  auto gload = [&](int t) {
+#pragma unroll
+    for (int p = 0; p < JPT; ++p) {
+      const int idx = tid + p * NTH;
+      if (idx < JCH) {
+        const int row = idx / CPR, ch = idx - row * CPR;
+        rj[p] = *reinterpret_cast<const uint4*>(Jg + (long long)(t * TJ + row) * DP + ch * 8);
+      }
+    }
+#pragma unroll
+    for (int p = 0; p < TPT; ++p) {
+      const int idx = tid + p * NTH;
+      if (idx < TCH) {
+        const int c = idx >> 3, ch = idx & 7;
+        rt[p] = *reinterpret_cast<const uint4*>(JTg + (long long)c * a.npad + t * TJ + ch * 8);
+      }
+    }
+  };
+  auto sstore = [&](int buf) {
+#pragma unroll
+    for (int p = 0; p < JPT; ++p) {
+      const int idx = tid + p * NTH;
+      if (idx < JCH) {
+        const int row = idx / CPR, ch = idx - row * CPR;
+        *reinterpret_cast<uint4*>(&lds[buf][row * DP + ((ch ^ Swz<DP>::j(row)) * 8)]) = rj[p];
+      }
+    }
+#pragma unroll
+    for (int p = 0; p < TPT; ++p) {
+      const int idx = tid + p * NTH;
+      if (idx < TCH) {
+        const int c = idx >> 3, ch = idx & 7;
+        *reinterpret_cast<uint4*>(&lds[buf][JS + c * TJ + ((ch ^ swz_t(c)) * 8)]) = rt[p];
+      }
+    }
+  };
+
+  const int ntiles = a.npad / TJ;
+  gload(0);
+  sstore(0);
+  __syncthreads();
+  ChunkStats st{0.0, 0u};
+  const int i_me = i0 + r;
+  for (int t = 0; t < ntiles; ++t) {
+    const int cur = t & 1;
+    if (t + 1 < ntiles) gload(t + 1);
+    const __bf16* Ls = lds[cur];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int jbase = t * TJ + 32 * q;
+      f32x4 X0 = {0.f, 0.f, 0.f, 0.f}, X1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        const int ra = 32 * q + r, rb2 = 32 * q + 16 + r;
+        const bf16x8 a0 = *reinterpret_cast<const bf16x8*>(
+            &Ls[ra * DP + (((4 * ks + q4) ^ Swz<DP>::j(ra)) * 8)]);
+        const bf16x8 a1 = *reinterpret_cast<const bf16x8*>(
+            &Ls[rb2 * DP + (((4 * ks + q4) ^ Swz<DP>::j(rb2)) * 8)]);
+        X0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, bI[ks], X0, 0, 0, 0);
+        X1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, bI[ks], X1, 0, 0, 0);
+      }
+      float xs[8] = {X0[0], X0[1], X0[2], X0[3], X1[0], X1[1], X1[2], X1[3]};
+      float sv[8];
+      const bool special = (jbase + 32 > a.n) || (i0 + 16 > a.n) ||
+                           (i0 >= jbase && i0 < jbase + 32);
+      if (special) chunk_epilogue<true>(xs, sv, st, jbase, q4, i_me, a.n);
+      else chunk_epilogue<false>(xs, sv, st, jbase, q4, i_me, a.n);
+      bf16x8 sb;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) sb[e] = (__bf16)sv[e];
+#pragma unroll
+      for (int ct = 0; ct < CT; ++ct) {
+        const int c = 16 * ct + r;
+        const int u0 = 8 * q + q4, u1 = 8 * q + 4 + q4;     // 8 B units of 4 j
+        const int sw = swz_t(c) << 1;
+        const bf16x4 lo = *reinterpret_cast<const bf16x4*>(&Ls[JS + c * TJ + ((u0 ^ sw) * 4)]);
+        const bf16x4 hi = *reinterpret_cast<const bf16x4*>(&Ls[JS + c * TJ + ((u1 ^ sw) * 4)]);
+        const bf16x8 a2 = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        acc[ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a2, sb, acc[ct], 0, 0, 0);
+      }
+    }
+    if (t + 1 < ntiles) sstore(cur ^ 1);
+    __syncthreads();
+  }
+
+  if (i_me < a.n) {
+    float* dst = a.dJd + ((long long)g * a.n + i_me) * a.d;
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct) {
+      const int c0 = 16 * ct + 4 * q4;
+      if (c0 < a.d)
+        *reinterpret_cast<float4*>(dst + c0) = make_float4(acc[ct][0], acc[ct][1], acc[ct][2], acc[ct][3]);
+    }
+  }
+  block_reduce_write(st, a.part);
+}
+
+// ---------------------------------------------------------------- f32 MFMA
+__device__ __forceinline__ int hJ(int row) { return ((row & 1) << 1) | (((row >> 1) & 7) << 2); }
+__device__ __forceinline__ int hT(int c) { return (c & 3) | (((c >> 2) & 3) << 3); }
+
+template <int DP>
+__global__ void __launch_bounds__(NTH) zzt_dense_f32(ZztArgs a) {
+  constexpr int JS = TJ * DP, TS = DP * TJ;
+  constexpr int KS = DP / 4;
+  constexpr int CT = DP / 16;
+  constexpr int JCH = TJ * DP / 4, TCH = DP * TJ / 4;
+  constexpr int JPT = (JCH + NTH - 1) / NTH, TPT = (TCH + NTH - 1) / NTH;
+  extern __shared__ __attribute__((aligned(16))) float dyn[];
+  float* lds0 = dyn;
+  float* lds1 = dyn + JS + TS;
+
+  const int g = blockIdx.x % a.ngraphs, rb = blockIdx.x / a.ngraphs;
+  const float* Jg = reinterpret_cast<const float*>(a.jrow) + (long long)g * a.npad * DP;
+  const float* JTg = reinterpret_cast<const float*>(a.jt) + (long long)g * DP * a.npad;
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, r = lane & 15, q4 = lane >> 4;
+  const int i0 = rb * ROWS + 16 * w;
+
+  float bI[KS];
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) bI[ks] = Jg[(long long)(i0 + r) * DP + 4 * ks + q4];
+  f32x4 acc[CT];
+#pragma unroll
+  for (int ct = 0; ct < CT; ++ct) acc[ct] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  float4 rj[JPT], rt[TPT];
+  auto gload = [&](int t) {
+#pragma unroll
+    for (int p = 0; p < JPT; ++p) {
+      const int idx = tid + p * NTH;
+      if (idx < JCH) {
+        const int row = idx / (DP / 4), c4 = idx - row * (DP / 4);
+        rj[p] = *reinterpret_cast<const float4*>(Jg + (long long)(t * TJ + row) * DP + 4 * c4);
+      }
+    }
+#pragma unroll
+    for (int p = 0; p < TPT; ++p) {
+      const int idx = tid + p * NTH;
+      if (idx < TCH) {
+        const int c = idx >> 4, c4 = idx & 15;
+        rt[p] = *reinterpret_cast<const float4*>(JTg + (long long)c * a.npad + t * TJ + 4 * c4);
+      }
+    }
+  };
+  auto sstore = [&](float* L) {
+#pragma unroll
+    for (int p = 0; p < JPT; ++p) {
+      const int idx = tid + p * NTH;
+      if (idx < JCH) {
+        const int row = idx / (DP / 4), c4 = idx - row * (DP / 4);
+        const int h = hJ(row);
+        const float v[4] = {rj[p].x, rj[p].y, rj[p].z, rj[p].w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) L[row * DP + ((4 * c4 + e) ^ h)] = v[e];
+      }
+    }
+#pragma unroll
+    for (int p = 0; p < TPT; ++p) {
+      const int idx = tid + p * NTH;
+      if (idx < TCH) {
+        const int c = idx >> 4, c4 = idx & 15;
+        const int h = hT(c);
+        const float v[4] = {rt[p].x, rt[p].y, rt[p].z, rt[p].w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) L[JS + c * TJ + ((4 * c4 + e) ^ h)] = v[e];
+      }
+    }
+  };
+
+  const int ntiles = a.npad / TJ;
+  gload(0);
+  sstore(lds0);
+  __syncthreads();
+  ChunkStats st{0.0, 0u};
+  const int i_me = i0 + r;
+  for (int t = 0; t < ntiles; ++t) {
+    const int cur = t & 1;
+    if (t + 1 < ntiles) gload(t + 1);
+    const float* Ls = cur ? lds1 : lds0;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int jbase = t * TJ + 32 * q;
+      f32x4 X0 = {0.f, 0.f, 0.f, 0.f}, X1 = {0.f, 0.f, 0.f, 0.f};
+      const int ra = 32 * q + r, rb2 = 32 * q + 16 + r;
+      const int ha = hJ(ra), hb = hJ(rb2);
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        const float a0 = Ls[ra * DP + ((4 * ks + q4) ^ ha)];
+        const float a1 = Ls[rb2 * DP + ((4 * ks + q4) ^ hb)];
+        X0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, bI[ks], X0, 0, 0, 0);
+        X1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, bI[ks], X1, 0, 0, 0);
+      }
+      float xs[8] = {X0[0], X0[1], X0[2], X0[3], X1[0], X1[1], X1[2], X1[3]};
+      float sv[8];
+      const bool special = (jbase + 32 > a.n) || (i0 + 16 > a.n) ||
+                           (i0 >= jbase && i0 < jbase + 32);
+      if (special) chunk_epilogue<true>(xs, sv, st, jbase, q4, i_me, a.n);
+      else chunk_epilogue<false>(xs, sv, st, jbase, q4, i_me, a.n);
+#pragma unroll
+      for (int ct = 0; ct < CT; ++ct) {
+        const int c = 16 * ct + r;
+        const int h = hT(c);
+        const float* row = Ls + JS + c * TJ;
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) {
+          acc[ct] = __builtin_amdgcn_mfma_f32_16x16x4f32(row[(32 * q + 4 * q4 + rr) ^ h], sv[rr],
+                                                         acc[ct], 0, 0, 0);
+          acc[ct] = __builtin_amdgcn_mfma_f32_16x16x4f32(row[(32 * q + 16 + 4 * q4 + rr) ^ h],
+                                                         sv[4 + rr], acc[ct], 0, 0, 0);
+        }
+      }
+    }
+    if (t + 1 < ntiles) sstore(cur ? lds0 : lds1);
+    __syncthreads();
+  }
+
+  if (i_me < a.n) {
+    float* dst = a.dJd + ((long long)g * a.n + i_me) * a.d;
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct) {
+      const int c0 = 16 * ct + 4 * q4;
+      if (c0 < a.d)
+        *reinterpret_cast<float4*>(dst + c0) = make_float4(acc[ct][0], acc[ct][1], acc[ct][2], acc[ct][3]);
+    }
+  }
+  block_reduce_write(st, a.part);
+}
+
+// dz = scale * (dz + ej)
+__global__ void zzt_combine_kernel(float* dz, const float* ej, long long n, float norm) {
+  long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  for (; i < n; i += (long long)gridDim.x * blockDim.x) dz[i] = norm * (dz[i] + ej[i]);
+}
+
+__global__ void zzt_stats_kernel(const double* pd, int nd, const double* pe, int ne,
+                                 const int* rowptr, int ngraphs, int n, float norm,
+                                 double* stats) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  double dl = 0.0, dc = 0.0, el = 0.0, tp = 0.0;
+  for (int k = 0; k < nd; ++k) { dl += pd[2 * k]; dc += pd[2 * k + 1]; }
+  for (int k = 0; k < ne; ++k) { el += pe[2 * k]; tp += pe[2 * k + 1]; }
+  const double nnz = (double)rowptr[(long long)ngraphs * n];
+  const double pairs = (double)ngraphs * n * (double)n;
+  stats[0] = (double)norm * (dl + el + (double)ngraphs * n * kSoftplusM1);
+  stats[1] = pairs - nnz - dc + 2.0 * tp;
+}
+
+}  // namespace
+
+int zzt_dp(int d) {
+  if (d <= 32) return 32;
+  if (d <= 64) return 64;
+  if (d <= 128) return 128;
+  return -1;
+}
+int zzt_npad(int n) { return (int)round_up(n, ROWS); }
+int zzt_dense_blocks(int ngraphs, int n) { return ngraphs * (zzt_npad(n) / ROWS); }
+
+size_t zzt_staging_bytes(int ngraphs, int n, int d, int dtype) {
+  const int dp = zzt_dp(d);
+  const size_t es = dtype == SND_BF16 ? 2 : 4;
+  return 2 * (size_t)ngraphs * zzt_npad(n) * dp * es;
+}
+
+int launch_zzt_prep(const float* z, int ngraphs, int n, int d, int dtype, void* jrow,
+                    void* jt, hipStream_t s) {
+  const int dp = zzt_dp(d), npad = zzt_npad(n);
+  dim3 grid(npad / 64, ngraphs);
+#define SND_PREP(T, DPV)                                                                \
+  hipLaunchKernelGGL((zzt_prep_kernel<T, DPV>), grid, dim3(256), 0, s, z, n, npad, d, \
+                     (T*)jrow, (T*)jt)
+  if (dtype == SND_BF16) {
+    if (dp == 32) SND_PREP(__bf16, 32); else if (dp == 64) SND_PREP(__bf16, 64); else SND_PREP(__bf16, 128);
+  } else {
+    if (dp == 32) SND_PREP(float, 32); else if (dp == 64) SND_PREP(float, 64); else SND_PREP(float, 128);
+  }
+#undef SND_PREP
+  SND_LAUNCH_CHECK("zzt_prep_kernel");
+  return 0;
+}
+
+int launch_zzt_dense(const ZztArgs& a, int dtype, hipStream_t s) {
+  const int dp = zzt_dp(a.d);
+  dim3 grid(zzt_dense_blocks(a.ngraphs, a.n));
+  if (dtype == SND_BF16) {
+    if (dp == 32) hipLaunchKernelGGL((zzt_dense_bf16<32>), grid, dim3(NTH), 0, s, a);
+    else if (dp == 64) hipLaunchKernelGGL((zzt_dense_bf16<64>), grid, dim3(NTH), 0, s, a);
+    else hipLaunchKernelGGL((zzt_dense_bf16<128>), grid, dim3(NTH), 0, s, a);
+  } else {
+    const size_t shm = 2 * 2 * (size_t)TJ * dp * sizeof(float);
+    if (dp == 32) hipLaunchKernelGGL((zzt_dense_f32<32>), grid, dim3(NTH), shm, s, a);
+    else if (dp == 64) hipLaunchKernelGGL((zzt_dense_f32<64>), grid, dim3(NTH), shm, s, a);
+    else hipLaunchKernelGGL((zzt_dense_f32<128>), grid, dim3(NTH), shm, s, a);
+  }
+  SND_LAUNCH_CHECK("zzt_dense");
+  return 0;
+}
+
+int zzt_init_attributes() {
+  // the f32 variants use up to 128 KiB of dynamic LDS; set once per process
+  static bool done = false;
+  if (done) return 0;
+  hipError_t e = hipFuncSetAttribute((const void*)zzt_dense_f32<128>,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, 131072);
+  if (e != hipSuccess) {
+    set_error("zzt: hipFuncSetAttribute: %s", hipGetErrorString(e));
+    return SND_ERR_HIP;
+  }
+  e = hipFuncSetAttribute((const void*)zzt_dense_f32<64>,
+                          hipFuncAttributeMaxDynamicSharedMemorySize, 65536);
+  if (e != hipSuccess) {
+    set_error("zzt: hipFuncSetAttribute: %s", hipGetErrorString(e));
+    return SND_ERR_HIP;
+  }
+  done = true;
+  return 0;
+}
+
+}  // namespace snd
+
+using namespace snd;
+
+extern "C" size_t snd_zzt_ce_workspace(int n_graphs, int n, int d, int dtype) {
+  if (zzt_dp(d) < 0 || n <= 0 || n_graphs <= 0) return 0;
+  const long long rows = (long long)n_graphs * n;
+  size_t b = round_up(zzt_staging_bytes(n_graphs, n, d, dtype), 256);
+  b += round_up(rows * d * sizeof(float), 256);                               // ej
+  b += round_up(2 * sizeof(double) * (size_t)zzt_dense_blocks(n_graphs, n), 256);
+  b += round_up(2 * sizeof(double) * (size_t)edge_blocks((int)rows, d), 256);
+  return b;
+}
+
+extern "C" int snd_zzt_ce(const float* z, int n_graphs, int n, int d, const int* rowptr,
+                          const int* colidx, float pos_weight, float norm,
+                          double* stats, float* dz, void* ws, size_t ws_bytes,
+                          int dtype, snd_stream_t stream) {
+  SND_CHECK_ARG(z && rowptr && colidx && stats && dz, "snd_zzt_ce: null operand");
+  SND_CHECK_ARG(d == 16 || d == 32 || d == 64 || d == 128, "snd_zzt_ce: d=%d not in {16,32,64,128}", d);
+  SND_CHECK_ARG(n > 0 && n_graphs > 0, "snd_zzt_ce: empty batch");
+  SND_CHECK_ARG(dtype == SND_F32 || dtype == SND_BF16, "snd_zzt_ce: bad dtype");
+  const size_t need = snd_zzt_ce_workspace(n_graphs, n, d, dtype);
+  SND_CHECK_ARG(ws && ws_bytes >= need, "snd_zzt_ce: workspace %zu < %zu", ws_bytes, need);
+  SND_TRY(zzt_init_attributes());
+  hipStream_t s = (hipStream_t)stream;
+  char* p = (char*)ws;
+  const size_t half = zzt_staging_bytes(n_graphs, n, d, dtype) / 2;
+  void* jrow = p;
+  void* jt = p + half;
+  p += round_up(2 * half, 256);
+  const long long rows = (long long)n_graphs * n;
+  float* ej = (float*)p;
+  p += round_up(rows * d * sizeof(float), 256);
+  double* pd = (double*)p;
+  p += round_up(2 * sizeof(double) * (size_t)zzt_dense_blocks(n_graphs, n), 256);
+  double* pe = (double*)p;
+
+  SND_TRY(launch_zzt_prep(z, n_graphs, n, d, dtype, jrow, jt, s));
+  ZztArgs a{jrow, jt, n, zzt_npad(n), n_graphs, d, dz, pd};
+  SND_TRY(launch_zzt_dense(a, dtype, s));
+  EdgeArgs e{rowptr, colidx, (int)rows, z, d, pos_weight, ej, pe};
+  SND_TRY(launch_edge(e, s));
+  // d(sum CE)/dz_i = sum_j (G_ij + G_ji) z_j = 2 norm (dJd_i + ej_i)
+  hipLaunchKernelGGL(zzt_combine_kernel, dim3(1024), dim3(256), 0, s, dz, ej, rows * d, 2.f * norm);
+  SND_LAUNCH_CHECK("zzt_combine_kernel");
+  hipLaunchKernelGGL(zzt_stats_kernel, dim3(1), dim3(64), 0, s, pd,
+                     zzt_dense_blocks(n_graphs, n), pe, edge_blocks((int)rows, d), rowptr,
+                     n_graphs, n, norm, stats);
+  SND_LAUNCH_CHECK("zzt_stats_kernel");
+  return 0;
+}

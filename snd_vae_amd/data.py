@@ -1,0 +1,181 @@
+"""Spatial-graph batches: synthetic random-geometric graphs and CSR ingest.
+
+Reference behaviour mirrored here:
+
+* The reference feeds a dense ``adj_truth`` [B, N, N] float32 placeholder
+  (`main.py:257`), built by ``load_data_syn`` from scipy sparse matrices with
+  the diagonal zeroed and symmetry asserted (`input_data.py:62-67`).
+* Index order is row-major, the order of ``np.where`` (`input_data.py:72`) and
+  of ``sparse_to_tuple`` (`preprocessing.py:7-13`).
+
+The MI355X path never materialises the dense N x N adjacency: a batch of B
+graphs is one block-diagonal CSR (int32 ``rowptr`` [B*N+1], ``colidx`` [nnz],
+columns sorted within each row, column ids global = b*N + j).  Node data is
+row-major [B*N, width] float32.
+
+The reference datasets are not shipped, so benchmarks and tests use seeded
+random-geometric graphs: positions U[0,1)^2, radius
+r = sqrt(kbar / (pi N)), edges from ``cKDTree.query_pairs``.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import List, Optional, Sequence
+
+import numpy as np
+
+from .config import SNDConfig
+
+
+@dataclass
+class GraphBatch:
+    """Host-side batch of B spatial graphs with N nodes each.
+
+    ``rowptr``/``colidx`` form the block-diagonal CSR.  ``features`` is the
+    encoder input X = [x_feat || S] for the tscale topology (decision iii) or
+    x_feat for tref; ``feature_truth`` and ``spatial_truth`` are the decoder
+    targets (`main.py:258-259`).
+    """
+    n_graphs: int
+    n_nodes: int
+    rowptr: np.ndarray          # int32 [B*N + 1]
+    colidx: np.ndarray          # int32 [nnz]
+    features: np.ndarray        # float32 [B*N, f_in]
+    feature_truth: np.ndarray   # float32 [B*N, num_feature]
+    spatial_truth: np.ndarray   # float32 [B*N, spatial_dim]
+
+    @property
+    def nnz(self) -> int:
+        return int(self.colidx.shape[0])
+
+    def graph_nnz(self) -> np.ndarray:
+        n = self.n_nodes
+        rp = self.rowptr.astype(np.int64)
+        return rp[n::n] - rp[:-1:n]
+
+    def dense_adj(self, b: int) -> np.ndarray:
+        """Dense [N, N] adjacency of graph b (small N only; tests)."""
+        n = self.n_nodes
+        a = np.zeros((n, n), np.float32)
+        lo = b * n
+        for i in range(n):
+            s, e = self.rowptr[lo + i], self.rowptr[lo + i + 1]
+            a[i, self.colidx[s:e] - lo] = 1.0
+        return a
+
+
+def rgg_edges(n: int, kbar: float, rng: np.random.Generator):
+    """Random geometric graph: returns (positions [n,2], i<j pair array)."""
+    from scipy.spatial import cKDTree
+    pos = rng.random((n, 2))
+    r = np.sqrt(kbar / (np.pi * n))
+    pairs = cKDTree(pos).query_pairs(r, output_type="ndarray")
+    return pos, pairs
+
+
+def csr_from_pairs(n: int, pairs: np.ndarray, offset: int = 0):
+    """Symmetric CSR (sorted columns, no diagonal) from undirected pairs.
+
+    Same entry order as ``np.where(dense)`` (`input_data.py:72`).
+    """
+    pairs = np.asarray(pairs, dtype=np.int64).reshape(-1, 2)
+    keep = pairs[:, 0] != pairs[:, 1]               # diag zeroed (input_data.py:65)
+    pairs = pairs[keep]
+    rows = np.concatenate([pairs[:, 0], pairs[:, 1]])
+    cols = np.concatenate([pairs[:, 1], pairs[:, 0]])
+    key = np.unique(rows * n + cols)                 # row-major order, dedup
+    rows, cols = key // n, key % n
+    counts = np.bincount(rows, minlength=n)
+    rowptr = np.zeros(n + 1, np.int64)
+    np.cumsum(counts, out=rowptr[1:])
+    return rowptr, (cols + offset)
+
+
+def csr_from_dense(adj: np.ndarray):
+    """CSR of one dense [N, N] 0/1 matrix in np.where order (host reference)."""
+    adj = np.asarray(adj)
+    if adj.shape[0] != adj.shape[1]:
+        raise ValueError("adjacency must be square")
+    if not np.array_equal(adj, adj.T):
+        raise ValueError("adjacency must be symmetric (input_data.py:67)")
+    a = adj.copy()
+    np.fill_diagonal(a, 0)
+    rows, cols = np.where(a)
+    counts = np.bincount(rows, minlength=a.shape[0])
+    rowptr = np.zeros(a.shape[0] + 1, np.int64)
+    np.cumsum(counts, out=rowptr[1:])
+    return rowptr, cols
+
+
+def stack_csr(parts: Sequence, n: int):
+    """Block-diagonal concatenation of per-graph (rowptr, local cols)."""
+    rowptrs, cols = [], []
+    base = 0
+    for b, (rp, c) in enumerate(parts):
+        rp = np.asarray(rp, np.int64)
+        rowptrs.append(rp[:-1] + base)
+        cols.append(np.asarray(c, np.int64) + b * n)
+        base += int(rp[-1])
+    rowptr = np.concatenate(rowptrs + [np.array([base], np.int64)])
+    colidx = np.concatenate(cols) if cols else np.zeros(0, np.int64)
+    if base >= 2 ** 31:
+        raise ValueError("nnz exceeds int32 CSR range")
+    return rowptr.astype(np.int32), colidx.astype(np.int32)
+
+
+def synthetic_batch(cfg: SNDConfig, n_graphs: int, seed: Optional[int] = None,
+                    kbar: Optional[float] = None) -> GraphBatch:
+    """B seeded RGG graphs (graph b uses default_rng(seed + b))."""
+    seed = cfg.seed if seed is None else seed
+    kbar = cfg.mean_degree if kbar is None else kbar
+    n = cfg.n_nodes
+    parts: List = []
+    feats, xs, ss = [], [], []
+    for b in range(n_graphs):
+        rng = np.random.default_rng(seed + b)
+        pos, pairs = rgg_edges(n, kbar, rng)
+        x = rng.random((n, cfg.num_feature))            # like node / 120 in [0,1)
+        parts.append(csr_from_pairs(n, pairs))
+        s = pos[:, :cfg.spatial_dim]                     # like geometry / 600
+        xs.append(x)
+        ss.append(s)
+        feats.append(np.concatenate([x, s], 1) if cfg.topology == "tscale" else x)
+    rowptr, colidx = stack_csr(parts, n)
+    return GraphBatch(n_graphs, n, rowptr, colidx,
+                      np.ascontiguousarray(np.concatenate(feats), np.float32),
+                      np.ascontiguousarray(np.concatenate(xs), np.float32),
+                      np.ascontiguousarray(np.concatenate(ss), np.float32))
+
+
+def batch_from_dense(cfg: SNDConfig, adj: np.ndarray, feature: np.ndarray,
+                     spatial: np.ndarray) -> GraphBatch:
+    """Ingest the reference feed format (`main.py:253-264`) into a GraphBatch.
+
+    adj [B,N,N] (dense adj_truth), feature [B,N,num_feature], spatial [B,N,2].
+    """
+    adj = np.asarray(adj)
+    b, n, _ = adj.shape
+    rowptr, colidx = stack_csr([csr_from_dense(adj[i]) for i in range(b)], n)
+    x = np.asarray(feature, np.float32).reshape(b * n, -1)
+    s = np.asarray(spatial, np.float32).reshape(b * n, -1)
+    f = np.concatenate([x, s], 1) if cfg.topology == "tscale" else x
+    return GraphBatch(b, n, rowptr, colidx, np.ascontiguousarray(f, np.float32),
+                      np.ascontiguousarray(x), np.ascontiguousarray(s))
+
+
+def shard(batch: GraphBatch, rank: int, world: int) -> GraphBatch:
+    """Contiguous equal shard of the global batch for DP rank ``rank``.
+
+    SURVEY.md §8e: B/world graphs per rank; every loss term is a per-graph
+    mean, so the global gradient is the mean of the rank gradients.
+    """
+    if batch.n_graphs % world:
+        raise ValueError("global batch must divide evenly over ranks")
+    per = batch.n_graphs // world
+    n = batch.n_nodes
+    lo, hi = rank * per * n, (rank + 1) * per * n
+    rp = batch.rowptr[lo:hi + 1].astype(np.int64)
+    cols = batch.colidx[rp[0]:rp[-1]].astype(np.int64) - lo
+    return GraphBatch(per, n, (rp - rp[0]).astype(np.int32), cols.astype(np.int32),
+                      batch.features[lo:hi], batch.feature_truth[lo:hi],
+                      batch.spatial_truth[lo:hi])

@@ -1,0 +1,146 @@
+"""SGCNModelVAE on MI355X: parameters, plan and device batch.
+
+Host-side mirror of the reference model classes for the hot path
+(`model.py:19-161` encoder/get_z, `model_joint.py:94-182` decoders) in the
+node-latent topology.  The reference builds a TF graph whose variables live in
+the TF store; here a ``snd_plan`` (libsndvae.so) fixes the shapes of one
+device batch and all trainable state is one flat fp32 device buffer
+(`params.py`).  Forward + backward run as one native launch sequence
+(``snd_train_step``); this class owns memory, not compute.
+
+Attributes named as in the reference (read back after a step):
+``z_mean_sg``/``z_std_sg`` (`model_joint.py:84-85`), ``z_sg``
+(`model_joint.py:89`), ``generated_spatial`` (`model_joint.py:121`),
+``generated_node_feat`` (`model_joint.py:144`).
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import Dict, Optional
+
+import numpy as np
+import torch
+
+from . import _lib
+from .config import SNDConfig
+from .data import GraphBatch
+from .params import flat_layout, init_blocks
+
+DTYPES = {"f32": 0, "fp32": 0, "bf16": 1}
+TAIL = 64  # floats after the parameters in the gradient buffer (loss terms for the all-reduce)
+
+
+def c_config(cfg: SNDConfig, dtype: str) -> _lib.Config:
+    if cfg.topology != "tscale":
+        raise NotImplementedError("the GPU path implements the node-latent topology")
+    s1, s2, s3 = cfg.s_d_channel
+    n1, n2 = cfg.n_d_channel
+    return _lib.Config(cfg.n_nodes, cfg.f_in, cfg.num_feature, cfg.spatial_dim,
+                       cfg.g_conv_hidden[0], cfg.g_conv_hidden[1], cfg.g_hidden_size,
+                       cfg.latent, s1, s2, s3, n1, n2, cfg.beta, cfg.pos_weight, cfg.norm,
+                       DTYPES[dtype])
+
+
+class DeviceBatch:
+    """A GraphBatch resident in HBM (the feed dict of `main.py:327-329`)."""
+
+    def __init__(self, batch: GraphBatch, device="cuda"):
+        t = lambda a, dt: torch.from_numpy(np.ascontiguousarray(a)).to(device=device, dtype=dt)
+        self.n_graphs = batch.n_graphs
+        self.n_nodes = batch.n_nodes
+        self.nnz = batch.nnz
+        self.rowptr = t(batch.rowptr, torch.int32)
+        self.colidx = t(batch.colidx, torch.int32) if batch.nnz else torch.zeros(1, dtype=torch.int32, device=device)
+        self.features = t(batch.features, torch.float32)
+        self.feature_truth = t(batch.feature_truth, torch.float32)
+        self.spatial_truth = t(batch.spatial_truth, torch.float32)
+        self.host = batch
+
+    def c_struct(self) -> _lib.Batch:
+        p = _lib.ptr
+        return _lib.Batch(p(self.rowptr), p(self.colidx), p(self.features),
+                          p(self.feature_truth), p(self.spatial_truth))
+
+
+class SGCNModelVAE:
+    """Plan + flat parameters of the node-latent SND-VAE on one GPU."""
+
+    def __init__(self, cfg: SNDConfig, n_graphs: int, dtype: str = "bf16",
+                 device="cuda", seed: int = 0, blocks: Optional[Dict[str, np.ndarray]] = None):
+        if not torch.cuda.is_available():
+            raise _lib.SNDError("SGCNModelVAE needs a ROCm GPU (no CPU fallback)")
+        L = _lib.lib()
+        self.cfg, self.n_graphs, self.dtype, self.device = cfg, n_graphs, dtype, device
+        self._cfg_c = c_config(cfg, dtype)
+        h = C.c_void_p()
+        _lib.check(L.snd_plan_create(C.byref(self._cfg_c), n_graphs, C.byref(h)), "snd_plan_create")
+        self.plan = h
+        self.param_count = int(L.snd_plan_param_count(h))
+        self.layout = flat_layout(cfg)
+        self._check_layout()
+        self.params = torch.zeros(self.param_count + TAIL, dtype=torch.float32, device=device)
+        ws = int(L.snd_plan_workspace_bytes(h))
+        self.workspace = torch.zeros(ws, dtype=torch.uint8, device=device)
+        self.load_blocks(blocks if blocks is not None else init_blocks(cfg, seed))
+
+    def _check_layout(self):
+        L = _lib.lib()
+        nb = L.snd_plan_num_blocks(self.plan)
+        names = list(self.layout.shapes)
+        if nb != len(names) or self.layout.total != self.param_count:
+            raise _lib.SNDError("flat layout mismatch between params.py and libsndvae")
+        for i in range(nb):
+            nm, off, n = C.c_char_p(), C.c_longlong(), C.c_longlong()
+            _lib.check(L.snd_plan_param_block(self.plan, i, C.byref(nm), C.byref(off), C.byref(n)))
+            k = names[i]
+            if (nm.value.decode() != k or off.value != self.layout.offsets[k]
+                    or n.value != self.layout.numel(k)):
+                raise _lib.SNDError(f"param block {i} mismatch: {nm.value} vs {k}")
+
+    def __del__(self):
+        try:
+            if getattr(self, "plan", None):
+                _lib.lib().snd_plan_destroy(self.plan)
+                self.plan = None
+        except Exception:
+            pass
+
+    # ---- parameters
+    def load_blocks(self, blocks: Dict[str, np.ndarray]):
+        flat = self.layout.pack(blocks, np.float32)
+        self.params[:self.param_count].copy_(torch.from_numpy(flat))
+
+    def blocks(self) -> Dict[str, np.ndarray]:
+        return self.layout.unpack(self.params[:self.param_count].double().cpu().numpy())
+
+    # ---- workspace views (intermediates of the last step)
+    def buffer(self, name: str, dtype=torch.float32, shape=None) -> torch.Tensor:
+        off, n = C.c_longlong(), C.c_longlong()
+        _lib.check(_lib.lib().snd_plan_buffer(self.plan, name.encode(), C.byref(off), C.byref(n)),
+                   "snd_plan_buffer")
+        es = torch.tensor([], dtype=dtype).element_size()
+        t = self.workspace[off.value:off.value + n.value * es].view(dtype)
+        return t.view(*shape) if shape is not None else t
+
+    def _rows(self, name, width):
+        return self.buffer(name).view(self.n_graphs * self.cfg.n_nodes, width)
+
+    @property
+    def z_mean_sg(self):
+        return self._rows("MS", 2 * self.cfg.latent)[:, :self.cfg.latent]
+
+    @property
+    def z_std_sg(self):
+        return self._rows("MS", 2 * self.cfg.latent)[:, self.cfg.latent:]
+
+    @property
+    def z_sg(self):
+        return self._rows("Z", self.cfg.latent)
+
+    @property
+    def generated_spatial(self):
+        return self._rows("SHAT", self.cfg.spatial_dim)
+
+    @property
+    def generated_node_feat(self):
+        return self._rows("XHAT", self.cfg.num_feature)

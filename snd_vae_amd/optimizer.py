@@ -1,0 +1,131 @@
+"""OptimizerVAE on MI355X: ELBO terms, gradients and the TF1-Adam step.
+
+Mirror of `optimizer.py:123-203` (``OptimizerVAE``, model_type 'base'):
+``cost``/``overall_loss`` = [cost, spatial_cost, adj_cost, node_cost, kl]
+(`optimizer.py:203`) plus the accuracy of `main.py:334`.  One ``step()`` is
+one iteration of the reference train loop (`main.py:315-334`):
+
+    snd_train_step   forward + backward, flat gradient, loss terms
+    all-reduce       (data parallel only) one RCCL call on the flat gradient
+    snd_adam_tf1     tf.train.AdamOptimizer(lr).minimize (`optimizer.py:125,197`)
+
+All three are stream-ordered device work, so a step can be captured in a
+HIP graph (``capture()``) and replayed with no host involvement; the loss
+terms stay on the device until ``overall_loss`` is read.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import Optional
+
+import numpy as np
+import torch
+
+from . import _lib
+from .model import TAIL, DeviceBatch, SGCNModelVAE
+
+LOSS_NAMES = ("cost", "spatial_cost", "adj_cost", "node_cost", "kl", "acc", "adj_sum", "correct")
+
+
+class OptimizerVAE:
+    def __init__(self, model: SGCNModelVAE, learning_rate: Optional[float] = None,
+                 beta1: Optional[float] = None, beta2: Optional[float] = None,
+                 epsilon: Optional[float] = None, process_group=None, seed: int = 1234):
+        cfg = model.cfg
+        self.model = model
+        self.lr = cfg.learning_rate if learning_rate is None else learning_rate
+        self.beta1 = cfg.adam_beta1 if beta1 is None else beta1
+        self.beta2 = cfg.adam_beta2 if beta2 is None else beta2
+        self.eps = cfg.adam_eps if epsilon is None else epsilon
+        self.seed = seed
+        dev = model.device
+        n = model.param_count + TAIL
+        self.grads = torch.zeros(n, dtype=torch.float32, device=dev)
+        self.m = torch.zeros(n, dtype=torch.float32, device=dev)
+        self.v = torch.zeros(n, dtype=torch.float32, device=dev)
+        self.step_counter = torch.zeros(1, dtype=torch.int32, device=dev)   # TF global step
+        self.losses = torch.zeros(8, dtype=torch.float64, device=dev)
+        self.group = process_group
+        self.world = 1
+        if process_group is not None:
+            import torch.distributed as dist
+            self.world = dist.get_world_size(process_group)
+        self._graph = None
+        self._batch_c = None
+
+    # ------------------------------------------------------------------ step
+    def forward_backward(self, batch: DeviceBatch, eps: Optional[torch.Tensor] = None,
+                         stream=None):
+        m = self.model
+        self._batch_c = batch.c_struct()
+        _lib.check(_lib.lib().snd_train_step(
+            m.plan, C.byref(self._batch_c), _lib.ptr(m.params), _lib.ptr(self.grads),
+            _lib.ptr(m.workspace), _lib.ptr(eps), self.seed, _lib.ptr(self.step_counter),
+            _lib.ptr(self.losses), _lib.stream_ptr(stream)), "snd_train_step")
+
+    def allreduce(self):
+        """One RCCL all-reduce (sum) of [flat grads || loss terms]."""
+        if self.world > 1:
+            import torch.distributed as dist
+            dist.all_reduce(self.grads[:self.model.param_count + 8], group=self.group)
+
+    def apply(self, stream=None):
+        m = self.model
+        _lib.check(_lib.lib().snd_adam_tf1(
+            _lib.ptr(m.params), _lib.ptr(self.grads), _lib.ptr(self.m), _lib.ptr(self.v),
+            m.param_count, self.lr, self.beta1, self.beta2, self.eps, 1.0 / self.world,
+            _lib.ptr(self.step_counter), _lib.stream_ptr(stream)), "snd_adam_tf1")
+
+    def step(self, batch: DeviceBatch, eps: Optional[torch.Tensor] = None):
+        """One optimisation step (`main.py:331`): fwd+bwd, all-reduce, Adam."""
+        self.forward_backward(batch, eps)
+        self.allreduce()
+        self.apply()
+
+    # ------------------------------------------------------------ HIP graph
+    def capture(self, batch: DeviceBatch, warmup: int = 2):
+        """Capture one full step (device Philox eps) into a HIP graph."""
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            for _ in range(warmup):
+                self.step(batch)
+        torch.cuda.current_stream().wait_stream(s)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self.step(batch)
+        self._graph = g
+        self._graph_batch = batch
+        return g
+
+    def replay(self):
+        self._graph.replay()
+
+    # ------------------------------------------------------------ readback
+    @property
+    def overall_loss(self):
+        """[cost, spatial_cost, adj_cost, node_cost, kl_sg] (`optimizer.py:203`)."""
+        v = self.losses.cpu().numpy()
+        return [float(x) for x in v[:5]]
+
+    def loss_dict(self, global_mean: bool = False):
+        """All loss terms; ``global_mean`` reads the all-reduced copy (DP)."""
+        if global_mean and self.world > 1:
+            t = self.grads[self.model.param_count:self.model.param_count + 6].double().cpu().numpy()
+            t = t / self.world
+            return dict(zip(LOSS_NAMES[:6], [float(x) for x in t]))
+        return dict(zip(LOSS_NAMES, [float(x) for x in self.losses.cpu().numpy()]))
+
+    @property
+    def global_step(self) -> int:
+        return int(self.step_counter.item())
+
+    def grad_blocks(self):
+        m = self.model
+        return m.layout.unpack(self.grads[:m.param_count].double().cpu().numpy())
+
+    def state_blocks(self):
+        m = self.model
+        pc = m.param_count
+        return (m.layout.unpack(self.m[:pc].double().cpu().numpy()),
+                m.layout.unpack(self.v[:pc].double().cpu().numpy()))

@@ -1,0 +1,18 @@
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs a ROCm MI355X GPU (run with -m gpu)")
+
+
+@pytest.fixture(scope="session")
+def lib_built():
+    from snd_vae_amd.build import build
+    return build()

@@ -1,0 +1,130 @@
+"""CPU tests of host logic: CSR ingest (bit-exact vs scipy), batching,
+sharding, the flat parameter layout, and the C ABI library's exports."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+import scipy.sparse as sp
+
+from snd_vae_amd.config import PRESETS, tscale
+from snd_vae_amd.data import (batch_from_dense, csr_from_dense, csr_from_pairs, rgg_edges,
+                              shard, synthetic_batch)
+from snd_vae_amd.params import block_shapes, flat_layout, init_blocks
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_rgg_sizes_match_survey():
+    # SURVEY.md §8d seed-0 sizes
+    for n, k, nnz in [(200, 8, 1434), (4096, 16, 64548)]:
+        rng = np.random.default_rng(0)
+        _, pairs = rgg_edges(n, k, rng)
+        rp, cols = csr_from_pairs(n, pairs)
+        assert int(rp[-1]) == nnz
+
+
+@pytest.mark.parametrize("n,k", [(50, 5), (200, 8), (1, 0), (30, 0.0)])
+def test_csr_bit_exact_vs_scipy(n, k):
+    rng = np.random.default_rng(n)
+    _, pairs = rgg_edges(n, k, rng)
+    rp, cols = csr_from_pairs(n, pairs)
+    dense = np.zeros((n, n))
+    if len(pairs):
+        dense[pairs[:, 0], pairs[:, 1]] = 1
+        dense[pairs[:, 1], pairs[:, 0]] = 1
+    ref = sp.csr_matrix(dense)
+    ref.sort_indices()
+    assert np.array_equal(rp, ref.indptr) and np.array_equal(cols, ref.indices)
+    rp2, cols2 = csr_from_dense(dense)
+    assert np.array_equal(rp2, ref.indptr) and np.array_equal(cols2, ref.indices)
+    # np.where order == sparse_to_tuple order (preprocessing.py:7-13)
+    r, c = np.where(dense)
+    assert np.array_equal(np.repeat(np.arange(n), np.diff(rp)), r) and np.array_equal(cols, c)
+
+
+def test_csr_from_dense_rejects_asymmetric():
+    a = np.zeros((3, 3))
+    a[0, 1] = 1
+    with pytest.raises(ValueError):
+        csr_from_dense(a)
+
+
+def test_diagonal_dropped():
+    a = np.eye(4) + np.diag(np.ones(3), 1) + np.diag(np.ones(3), -1)
+    rp, cols = csr_from_dense(a)
+    assert int(rp[-1]) == 6 and all(c != r for r in range(4) for c in cols[rp[r]:rp[r + 1]])
+
+
+def test_batch_block_diagonal_and_dense_roundtrip():
+    cfg = tscale(40, 16, mean_degree=5.0)
+    b = synthetic_batch(cfg, 3, seed=2)
+    adj = np.stack([b.dense_adj(i) for i in range(3)])
+    b2 = batch_from_dense(cfg, adj, b.feature_truth.reshape(3, 40, 1), b.spatial_truth.reshape(3, 40, 2))
+    assert np.array_equal(b.rowptr, b2.rowptr) and np.array_equal(b.colidx, b2.colidx)
+    assert np.array_equal(b.features, b2.features)
+    # columns of graph g stay inside [g*N, (g+1)*N)
+    for g in range(3):
+        s, e = b.rowptr[g * 40], b.rowptr[(g + 1) * 40]
+        assert (b.colidx[s:e] >= g * 40).all() and (b.colidx[s:e] < (g + 1) * 40).all()
+
+
+def test_shard_partitions_graphs():
+    cfg = tscale(30, 16, mean_degree=5.0)
+    b = synthetic_batch(cfg, 4, seed=0)
+    parts = [shard(b, r, 2) for r in range(2)]
+    for r, p in enumerate(parts):
+        ref = synthetic_batch(cfg, 2, seed=2 * r)
+        assert np.array_equal(p.rowptr, ref.rowptr) and np.array_equal(p.colidx, ref.colidx)
+        assert np.array_equal(p.features, ref.features)
+
+
+def test_flat_layout_alignment_and_counts():
+    cfg = PRESETS["C2"]
+    lay = flat_layout(cfg)
+    assert all(o % 64 == 0 for o in lay.offsets.values())
+    n = sum(int(np.prod(s)) for s in block_shapes(cfg).values())
+    assert 55_000 < n < 70_000         # ~61K params (~245 KB)
+    blocks = init_blocks(cfg, 0)
+    flat = lay.pack(blocks)
+    back = lay.unpack(flat)
+    assert all(np.allclose(back[k], blocks[k].astype(np.float32)) for k in blocks)
+
+
+def _header_functions():
+    src = open(os.path.join(ROOT, "include", "snd_vae.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?[\w\s\*]+?\b(snd_\w+)\s*\(", src, flags=re.M)))
+
+
+def test_library_exports_every_header_symbol(lib_built):
+    names = _header_functions()
+    assert len(names) >= 20
+    so = ctypes.CDLL(lib_built)
+    missing = [n for n in names if not hasattr(so, n)]
+    assert not missing, missing
+    from snd_vae_amd import _lib
+    assert set(_lib.EXPORTS) == set(names)
+
+
+def test_plan_layout_matches_python(lib_built):
+    """snd_plan_create needs no GPU: check its flat layout against params.py."""
+    from snd_vae_amd import _lib
+    from snd_vae_amd.model import c_config
+    for preset in ("C1s", "C2", "C5"):
+        cfg = PRESETS[preset]
+        L = _lib.lib()
+        h = ctypes.c_void_p()
+        cc = c_config(cfg, "bf16")
+        rc = L.snd_plan_create(ctypes.byref(cc), 8, ctypes.byref(h))
+        if rc != 0 and "hipFuncSetAttribute" in _lib.last_error():
+            pytest.skip("HIP runtime unavailable on this host")
+        _lib.check(rc)
+        lay = flat_layout(cfg)
+        assert L.snd_plan_param_count(h) == lay.total
+        for i, k in enumerate(lay.shapes):
+            nm, off, n = ctypes.c_char_p(), ctypes.c_longlong(), ctypes.c_longlong()
+            _lib.check(L.snd_plan_param_block(h, i, ctypes.byref(nm), ctypes.byref(off), ctypes.byref(n)))
+            assert (nm.value.decode(), off.value, n.value) == (k, lay.offsets[k], lay.numel(k))
+        L.snd_plan_destroy(h)

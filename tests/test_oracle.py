@@ -1,0 +1,121 @@
+"""CPU tests of the float64 oracle (oracle/ref_numpy.py) -- the parity checker.
+
+Pins: analytic known-answer constants, finite differences, an independent
+torch autograd formulation of the reference graph (oracle/ref_torch.py), the
+TF1 Adam formula, and the committed golden fixtures (regenerated here).
+Parity against TensorFlow itself is unpinned (TF not installable; the
+reference ships no tests/fixtures) -- see DESIGN.md.
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import ref_numpy as R
+from oracle import ref_torch as T
+from snd_vae_amd.config import tscale
+from snd_vae_amd.data import synthetic_batch
+from snd_vae_amd.params import init_blocks
+
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def test_kat_constants():
+    # diag pair CE: logits (1, 0), label 0 -> logsumexp(1,0) - 1 = softplus(-1)
+    assert abs(R.SOFTPLUS_M1 - 0.3132616875182228) < 1e-15
+    assert abs(R.BN_C - 0.9995003746877732) < 1e-15
+    # 2-class softmax CE with logit0 = 0 equals BCE-with-logits
+    L = np.linspace(-30, 30, 121)
+    for a in (0.0, 1.0):
+        lse = np.logaddexp(0.0, L)
+        ce = lse - (1 - a) * 0.0 - a * L
+        log_sig = lambda x: -np.logaddexp(0.0, -x)
+        bce = -(a * log_sig(L) + (1 - a) * log_sig(-L))
+        assert np.allclose(ce, bce, rtol=1e-12, atol=1e-12)
+
+
+def test_lrelu_tf_maximum_gradient():
+    # tf.maximum(x, 0.2x): grad goes to x where x >= 0.2x -> 1 at x == 0
+    assert R.lrelu_grad(np.array([0.0]))[0] == 1.0
+    assert R.lrelu_grad(np.array([-1e-30]))[0] == 0.2
+
+
+def test_conv1d_same_matches_torch():
+    rng = np.random.default_rng(0)
+    x, w, b = rng.standard_normal((13, 3)), rng.standard_normal((5, 3, 4)), rng.standard_normal(4)
+    out = R.conv1d_same(x, w, b)
+    ref = T.conv1d_same(torch.tensor(x)[None], torch.tensor(w), torch.tensor(b))[0].numpy()
+    assert np.allclose(out, ref, atol=1e-12)
+
+
+def _small(n=25, d=8, B=2, seed=3):
+    cfg = tscale(n, d, mean_degree=6.0)
+    batch = synthetic_batch(cfg, B, seed=seed)
+    rng = np.random.default_rng(seed)
+    p = {k: v + 0.3 * rng.standard_normal(v.shape) for k, v in init_blocks(cfg, 1).items()}
+    eps = rng.standard_normal((B * n, d))
+    adj = [batch.dense_adj(i) for i in range(B)]
+    return cfg, batch, p, eps, adj
+
+
+def test_oracle_grads_match_torch_autograd():
+    cfg, batch, p, eps, adj = _small()
+    losses, g, _ = R.forward_backward(p, adj, batch.features, batch.feature_truth,
+                                      batch.spatial_truth, eps, cfg)
+    tp = T.build_params(p, torch.float64)
+    cost, d = T.loss_fn(tp, *T.to_tensors((adj, batch.features, batch.feature_truth,
+                                           batch.spatial_truth, eps), cfg, torch.float64), cfg)
+    cost.backward()
+    for k in ("cost", "adj_cost", "node_cost", "spatial_cost", "kl", "acc"):
+        assert abs(losses[k] - float(d[k])) <= 1e-12 * max(1.0, abs(losses[k])), k
+    for k in p:
+        ref = tp[k].grad.numpy()
+        err = np.abs(g[k] - ref).max() / (np.abs(ref).max() + 1e-30)
+        assert err < 1e-10, (k, err)
+
+
+def test_oracle_finite_differences():
+    cfg, batch, p, eps, adj = _small(n=12, d=4, B=1, seed=7)
+    args = (adj, batch.features, batch.feature_truth, batch.spatial_truth, eps, cfg)
+    _, g, _ = R.forward_backward(p, *args)
+    rng = np.random.default_rng(0)
+    h = 1e-6
+    for k in ("enc.W0", "enc.W1", "enc.bne.gamma", "enc.Wms", "dec.K1", "dec.K3s", "dec.bn1.beta",
+              "dec.Wn"):
+        idx = tuple(rng.integers(0, s) for s in p[k].shape)
+        pp = {a: b.copy() for a, b in p.items()}
+        pm = {a: b.copy() for a, b in p.items()}
+        pp[k][idx] += h
+        pm[k][idx] -= h
+        fd = (R.forward_backward(pp, *args, want_grads=False)[0]["cost"] -
+              R.forward_backward(pm, *args, want_grads=False)[0]["cost"]) / (2 * h)
+        assert abs(fd - g[k][idx]) < 1e-6 * max(1.0, abs(fd)), (k, fd, g[k][idx])
+
+
+def test_tf1_adam_formula():
+    p = {"w": np.array([1.0, -2.0])}
+    g = {"w": np.array([0.5, 0.25])}
+    m = {"w": np.zeros(2)}
+    v = {"w": np.zeros(2)}
+    R.adam_tf1(p, g, m, v, 1, 0.001)
+    # t=1: m = 0.1 g, v = 0.001 g^2, lr_t = lr sqrt(0.001)/0.1 -> step = lr*g/(|g| + eps/sqrt(.001)...)
+    lr_t = 0.001 * np.sqrt(1 - 0.999) / (1 - 0.9)
+    exp = np.array([1.0, -2.0]) - lr_t * 0.1 * g["w"] / (np.sqrt(0.001 * g["w"] ** 2) + 1e-8)
+    assert np.allclose(p["w"], exp, rtol=0, atol=1e-15)
+
+
+@pytest.mark.parametrize("name", ["tscale_n25_d16", "tscale_n200_d16"])
+def test_golden_fixture_reproduces(name):
+    z = np.load(os.path.join(GOLDEN, name + ".npz"))
+    n, d, B = int(z["n"]), int(z["d"]), int(z["B"])
+    cfg = tscale(n, d, mean_degree=float(z["kbar"]))
+    batch = synthetic_batch(cfg, B, seed=int(z["seed"]))
+    assert np.array_equal(batch.rowptr, z["rowptr"]) and np.array_equal(batch.colidx, z["colidx"])
+    p0 = {k[3:]: z[k] for k in z.files if k.startswith("p0/")}
+    adj = [batch.dense_adj(b) for b in range(B)]
+    losses, g, _ = R.forward_backward(p0, adj, z["features"], z["feature_truth"],
+                                      z["spatial_truth"], z["eps"][0].astype(np.float64), cfg)
+    assert losses["cost"] == pytest.approx(float(z["s0/loss/cost"]), rel=1e-13)
+    for k in p0:
+        assert np.allclose(g[k], z["s0/grad/" + k], rtol=1e-10, atol=1e-14)

@@ -1,0 +1,34 @@
+#!/bin/bash
+# One GPU-box session: smoke, GPU tests, bench, rocprofv3 kernel stats.
+# Every GPU step has its own time limit; a crash/abort/timeout ends the script.
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+fatal() { case "$1" in 124|134|137|139|-6|-11) return 0;; *) return 1;; esac; }
+
+step() {  # step NAME SECONDS CMD...
+  local name=$1 secs=$2; shift 2
+  echo "== $name"
+  timeout -k 10 "$secs" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "== $name exit $rc"
+  tail -n 5 "gpurun_out/$name.log"
+  if fatal $rc; then echo "FATAL in $name ($rc), stopping"; exit $rc; fi
+  return 0
+}
+
+STAGES=${STAGES:-"smoke tests bench prof"}
+for s in $STAGES; do
+  case $s in
+    smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    tests) step pytest_gpu 900 python -m pytest tests -m gpu -q -x ;;
+    bench) step bench 600 python bench.py ;;
+    prof)  step rocprof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run \
+             --output-format csv -- python bench.py --steps 20 --warmup 5 --no-cpu-baseline ;;
+    pmc1)  step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc1 -o run \
+             --output-format csv -- python bench.py --steps 5 --warmup 2 --no-cpu-baseline ;;
+    pmc2)  step pmc_write 600 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc2 -o run \
+             --output-format csv -- python bench.py --steps 5 --warmup 2 --no-cpu-baseline ;;
+  esac
+done
+echo "== done"
