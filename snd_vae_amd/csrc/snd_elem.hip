@@ -45,32 +45,37 @@ __device__ __forceinline__ T block_sum(T v) {
 }
 
 // ---------------------------------------------------------------- reparam
-constexpr int kReparamGrid = 512;
+constexpr int kReparamGrid = 2048;
 
+// thread -> (row, column) with a fixed column per thread: no per-element
+// division; rows stride over the grid.  L <= 256.
 __global__ void __launch_bounds__(256) reparam_fwd_kernel(ReparamFwdArgs a) {
-  const long long n = (long long)a.rows * a.L;
   const unsigned off = a.step ? (unsigned)(*a.step) : 0u;
+  const int rpb = 256 / a.L;                       // rows per block pass
+  const int c = threadIdx.x % a.L, rl = threadIdx.x / a.L;
   double kl = 0.0;
-  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n;
-       i += (long long)gridDim.x * 256) {
-    const int r = (int)(i / a.L), c = (int)(i - (long long)r * a.L);
-    const float mu = a.ms[(long long)r * a.ldms + c];
-    const float ls = a.ms[(long long)r * a.ldms + a.L + c];
-    const float eps = a.eps_in ? a.eps_in[i] : philox_normal(a.seed, off, (unsigned long long)i);
-    const float es = __expf(ls);
-    a.z[i] = mu + eps * es;               // model.py:159
-    if (a.eps_out) a.eps_out[i] = eps;
-    kl += (double)(1.f + 2.f * ls - mu * mu - es * es);   // optimizer.py:193
+  if (rl < rpb) {
+    for (int r = blockIdx.x * rpb + rl; r < a.rows; r += gridDim.x * rpb) {
+      const long long i = (long long)r * a.L + c;
+      const float mu = a.ms[(long long)r * a.ldms + c];
+      const float ls = a.ms[(long long)r * a.ldms + a.L + c];
+      const float eps = a.eps_in ? a.eps_in[i] : philox_normal(a.seed, off, (unsigned long long)i);
+      const float es = __expf(ls);
+      a.z[i] = mu + eps * es;               // model.py:159
+      if (a.eps_out) a.eps_out[i] = eps;
+      kl += (double)(1.f + 2.f * ls - mu * mu - es * es);   // optimizer.py:193
+    }
   }
   const double t = block_sum(kl);
   if (threadIdx.x == 0) a.kl_part[blockIdx.x] = t;
 }
 
 __global__ void __launch_bounds__(256) reparam_bwd_kernel(ReparamBwdArgs a) {
-  const long long n = (long long)a.rows * a.L;
-  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n;
-       i += (long long)gridDim.x * 256) {
-    const int r = (int)(i / a.L), c = (int)(i - (long long)r * a.L);
+  const int rpb = 256 / a.L;
+  const int c = threadIdx.x % a.L, rl = threadIdx.x / a.L;
+  if (rl >= rpb) return;
+  for (int r = blockIdx.x * rpb + rl; r < a.rows; r += gridDim.x * rpb) {
+    const long long i = (long long)r * a.L + c;
     const float mu = a.ms[(long long)r * a.ldms + c];
     const float ls = a.ms[(long long)r * a.ldms + a.L + c];
     const float es = __expf(ls);
@@ -92,108 +97,155 @@ __global__ void __launch_bounds__(256) heads_kernel(HeadPack pk, int rows) {
   const HeadArgs& h = pk.h[blockIdx.y];
   __shared__ float su[kHeadRows][kHeadK + 1];
   __shared__ float sd[kHeadRows][kHeadO];
-  const int r = blockIdx.x * kHeadRows + threadIdx.x;
+  const int r0 = blockIdx.x * kHeadRows;
+  const int nrow = min(kHeadRows, rows - r0);
+  // coalesced staging of the block's [rows x cin] input tile
+  for (int idx = threadIdx.x; idx < kHeadRows * h.cin; idx += 256) {
+    const int rr = idx / h.cin, k = idx - rr * h.cin;
+    su[rr][k] = rr < nrow ? h.u[(long long)(r0 + rr) * h.ldu + k] : 0.f;
+  }
+  __syncthreads();
+  const int rr = threadIdx.x, r = r0 + rr;
   double sse = 0.0;
-  if (r < rows) {
-    float u[kHeadK];
-    for (int k = 0; k < h.cin; ++k) {
-      u[k] = h.u[(long long)r * h.ldu + k];
-      su[threadIdx.x][k] = u[k];
-    }
-    float dp[kHeadO];
-    for (int o = 0; o < h.cout; ++o) {
+  float dp[kHeadO];
+#pragma unroll
+  for (int o = 0; o < kHeadO; ++o) {
+    dp[o] = 0.f;
+    if (o < h.cout && rr < nrow) {
       float zo = h.b[o];
-      for (int k = 0; k < h.cin; ++k) zo += u[k] * h.w[k * h.cout + o];
+      for (int k = 0; k < h.cin; ++k) zo += su[rr][k] * h.w[k * h.cout + o];
       const float y = 1.f / (1.f + __expf(-zo));
       if (h.yhat) h.yhat[(long long)r * h.cout + o] = y;
       const float diff = y - h.target[(long long)r * h.ldt + o];
       sse += (double)diff * diff;
       dp[o] = 2.f * diff / h.count * y * (1.f - y);
-      sd[threadIdx.x][o] = dp[o];
     }
-    for (int k = 0; k < h.cin; ++k) {
-      float du = 0.f;
-      for (int o = 0; o < h.cout; ++o) du += dp[o] * h.w[k * h.cout + o];
-      h.du[(long long)r * h.lddu + k] = du;
-    }
-  } else {
-    for (int k = 0; k < h.cin; ++k) su[threadIdx.x][k] = 0.f;
-    for (int o = 0; o < h.cout; ++o) sd[threadIdx.x][o] = 0.f;
+    sd[rr][o] = dp[o];
   }
   const double t = block_sum(sse);
   if (threadIdx.x == 0) h.sse_part[blockIdx.x] = t;
   __syncthreads();
+  // du = dpre @ w^T, written coalesced from LDS
+  for (int idx = threadIdx.x; idx < nrow * h.cin; idx += 256) {
+    const int row = idx / h.cin, k = idx - row * h.cin;
+    float du = 0.f;
+#pragma unroll
+    for (int o = 0; o < kHeadO; ++o)
+      if (o < h.cout) du += sd[row][o] * h.w[k * h.cout + o];
+    h.du[(long long)(r0 + row) * h.lddu + k] = du;
+  }
+  // dW, db partials of this block
   const int nw = h.cin * h.cout;
   for (int idx = threadIdx.x; idx < nw + h.cout; idx += 256) {
     float acc = 0.f;
     if (idx < nw) {
       const int k = idx / h.cout, o = idx - k * h.cout;
-      for (int rr = 0; rr < kHeadRows; ++rr) acc += su[rr][k] * sd[rr][o];
+      for (int q = 0; q < kHeadRows; ++q) acc += su[q][k] * sd[q][o];
     } else {
       const int o = idx - nw;
-      for (int rr = 0; rr < kHeadRows; ++rr) acc += sd[rr][o];
+      for (int q = 0; q < kHeadRows; ++q) acc += sd[q][o];
     }
     h.wpart[(long long)blockIdx.x * (nw + h.cout) + idx] = acc;
   }
 }
 
 // ---------------------------------------------------------------- BN/lrelu bwd
-__global__ void __launch_bounds__(256) dec_bwd_kernel(DecPack pk, int rows) {
-  const DecBwdArgs& a = pk.d[blockIdx.y];
-  const int c = threadIdx.x;
-  if (c >= a.ncols) return;
-  const float gc = a.gamma[c] * kBnC, be = a.beta[c];
-  float sg = 0.f, sb = 0.f, sy = 0.f;
-  const int r0 = blockIdx.x * kColRows, r1 = min(rows, r0 + kColRows);
-  for (int r = r0; r < r1; ++r) {
-    const float y = a.y[(long long)r * a.ldy + c];
-    const float t = y * gc + be;
-    const float dt = a.du[(long long)r * a.lddu + c] * lrelu_grad(t);
-    const float dy = dt * gc;
-    a.dy[(long long)r * a.lddy + c] = dy;
-    sg += dt * y;
-    sb += dt;
-    sy += dy;
-  }
-  float* p = a.part + (long long)blockIdx.x * 3 * a.ncols;
-  p[c] = sg * kBnC;
-  p[a.ncols + c] = sb;
-  p[2 * a.ncols + c] = sy;
+// Column-reduction kernels: block = kColRows rows x all columns; 256 threads in
+// a (RP rows) x (CP columns) layout so every row read is coalesced; per-thread
+// column sums are combined across the RP row lanes in LDS (fixed order).
+template <int CP>
+__device__ __forceinline__ float lane_rows_sum(float v, float* red) {
+  constexpr int RP = 256 / CP;
+  red[threadIdx.x] = v;
+  __syncthreads();
+  float t = 0.f;
+  if (threadIdx.x < CP)
+    for (int k = 0; k < RP; ++k) t += red[k * CP + threadIdx.x];
+  __syncthreads();
+  return t;
 }
 
-__global__ void __launch_bounds__(256) enc_bwd_kernel(EncBwdArgs a, int rows) {
-  const int c = threadIdx.x;
-  const int width = a.has_enc ? a.wenc : a.h;
-  if (c >= width) return;
+template <int CP>
+__global__ void __launch_bounds__(256) dec_bwd_kernel(DecPack pk, int rows) {
+  constexpr int RP = 256 / CP;
+  __shared__ float red[256];
+  const DecBwdArgs& a = pk.d[blockIdx.y];
+  const int c = threadIdx.x % CP, ty = threadIdx.x / CP;
+  const bool on = c < a.ncols;
+  const float gc = on ? a.gamma[c] * kBnC : 0.f, be = on ? a.beta[c] : 0.f;
+  float sg = 0.f, sb = 0.f, sy = 0.f;
   const int r0 = blockIdx.x * kColRows, r1 = min(rows, r0 + kColRows);
-  const float gec = a.has_enc ? a.ge[c] * kBnC : 1.f;
+  if (on) {
+#pragma unroll 4
+    for (int r = r0 + ty; r < r1; r += RP) {
+      const float y = a.y[(long long)r * a.ldy + c];
+      const float t = y * gc + be;
+      const float dt = a.du[(long long)r * a.lddu + c] * lrelu_grad(t);
+      const float dy = dt * gc;
+      a.dy[(long long)r * a.lddy + c] = dy;
+      sg += dt * y;
+      sb += dt;
+      sy += dy;
+    }
+  }
+  sg = lane_rows_sum<CP>(sg, red);
+  sb = lane_rows_sum<CP>(sb, red);
+  sy = lane_rows_sum<CP>(sy, red);
+  if (threadIdx.x < a.ncols) {
+    float* p = a.part + (long long)blockIdx.x * 3 * a.ncols;
+    p[c] = sg * kBnC;
+    p[a.ncols + c] = sb;
+    p[2 * a.ncols + c] = sy;
+  }
+}
+
+template <int CP>
+__global__ void __launch_bounds__(256) enc_bwd_kernel(EncBwdArgs a, int rows) {
+  constexpr int RP = 256 / CP;
+  __shared__ float red[256];
+  const int c = threadIdx.x % CP, ty = threadIdx.x / CP;
+  const int width = a.has_enc ? a.wenc : a.h;
+  const bool on = c < width;
+  const float gec = (on && a.has_enc) ? a.ge[c] * kBnC : 1.f;
   const float gc = c < a.h ? a.g[c] * kBnC : 0.f;
   float sge = 0.f, sbe = 0.f, sg = 0.f, sb = 0.f;
-  for (int r = r0; r < r1; ++r) {
-    float d = a.dg[(long long)r * a.lddg + c];
+  const int r0 = blockIdx.x * kColRows, r1 = min(rows, r0 + kColRows);
+  if (on) {
+#pragma unroll 4
+    for (int r = r0 + ty; r < r1; r += RP) {
+      float d = a.dg[(long long)r * a.lddg + c];
+      if (a.has_enc) {
+        sge += d * a.h2[(long long)r * a.ldh2 + c];
+        sbe += d;
+        d *= gec;
+      }
+      if (c < a.h) {
+        const float p = a.p[(long long)r * a.ldp + c];
+        sg += d * lrelu(p);
+        sb += d;
+        a.dp[(long long)r * a.lddp + c] = d * gc * lrelu_grad(p);
+      }
+    }
+  }
+  if (a.has_enc) {
+    sge = lane_rows_sum<CP>(sge, red);
+    sbe = lane_rows_sum<CP>(sbe, red);
+  }
+  sg = lane_rows_sum<CP>(sg, red);
+  sb = lane_rows_sum<CP>(sb, red);
+  if (threadIdx.x < width) {
+    const int stride = (a.has_enc ? 2 * a.wenc : 0) + 2 * a.h;
+    float* pp = a.part + (long long)blockIdx.x * stride;
+    int o = 0;
     if (a.has_enc) {
-      sge += d * a.h2[(long long)r * a.ldh2 + c];
-      sbe += d;
-      d *= gec;
+      pp[c] = sge * kBnC;
+      pp[a.wenc + c] = sbe;
+      o = 2 * a.wenc;
     }
     if (c < a.h) {
-      const float p = a.p[(long long)r * a.ldp + c];
-      sg += d * lrelu(p);
-      sb += d;
-      a.dp[(long long)r * a.lddp + c] = d * gc * lrelu_grad(p);
+      pp[o + c] = sg * kBnC;
+      pp[o + a.h + c] = sb;
     }
-  }
-  const int stride = (a.has_enc ? 2 * a.wenc : 0) + 2 * a.h;
-  float* pp = a.part + (long long)blockIdx.x * stride;
-  int o = 0;
-  if (a.has_enc) {
-    pp[c] = sge * kBnC;
-    pp[a.wenc + c] = sbe;
-    o = 2 * a.wenc;
-  }
-  if (c < a.h) {
-    pp[o + c] = sg * kBnC;
-    pp[o + a.h + c] = sb;
   }
 }
 
@@ -204,9 +256,24 @@ struct ReducePack {
 
 __global__ void __launch_bounds__(256) reduce_kernel(ReducePack pk) {
   const ReduceDesc& d = pk.d[blockIdx.y];
-  for (int i = blockIdx.x * 256 + threadIdx.x; i < d.len; i += gridDim.x * 256) {
-    double acc = 0.0;
-    for (int p = 0; p < d.nparts; ++p) acc += (double)d.src[(long long)p * d.stride + i];
+  __shared__ double red[4][64];
+  const int col = threadIdx.x & 63, lane = threadIdx.x >> 6;
+  const int i = blockIdx.x * 64 + col;
+  if (blockIdx.x * 64 >= d.len) return;   // uniform per block
+  double a0 = 0.0, a1 = 0.0;
+  if (i < d.len) {
+    const float* src = d.src + i;
+    int p = lane;
+    for (; p + 4 < d.nparts; p += 8) {
+      a0 += (double)src[(long long)p * d.stride];
+      a1 += (double)src[(long long)(p + 4) * d.stride];
+    }
+    if (p < d.nparts) a0 += (double)src[(long long)p * d.stride];
+  }
+  red[lane][col] = a0 + a1;
+  __syncthreads();
+  if (lane == 0 && i < d.len) {
+    const double acc = red[0][col] + red[1][col] + red[2][col] + red[3][col];
     float v = (float)(acc * (double)d.scale);
     if (d.accumulate) v += d.dst[i];
     d.dst[i] = v;
@@ -312,7 +379,14 @@ int launch_dec_bwd(const DecBwdArgs* a, int n, int rows, hipStream_t s) {
     pk.d[i] = a[i];
   }
   if (rows <= 0) return 0;
-  hipLaunchKernelGGL(dec_bwd_kernel, dim3(col_blocks(rows), n), dim3(256), 0, s, pk, rows);
+  int w = a[0].ncols;
+  if (n > 1 && a[1].ncols > w) w = a[1].ncols;
+  dim3 grid(col_blocks(rows), n);
+  if (w <= 16) hipLaunchKernelGGL(dec_bwd_kernel<16>, grid, dim3(256), 0, s, pk, rows);
+  else if (w <= 32) hipLaunchKernelGGL(dec_bwd_kernel<32>, grid, dim3(256), 0, s, pk, rows);
+  else if (w <= 64) hipLaunchKernelGGL(dec_bwd_kernel<64>, grid, dim3(256), 0, s, pk, rows);
+  else if (w <= 128) hipLaunchKernelGGL(dec_bwd_kernel<128>, grid, dim3(256), 0, s, pk, rows);
+  else hipLaunchKernelGGL(dec_bwd_kernel<256>, grid, dim3(256), 0, s, pk, rows);
   SND_LAUNCH_CHECK("dec_bwd_kernel");
   return 0;
 }
@@ -320,7 +394,10 @@ int launch_dec_bwd(const DecBwdArgs* a, int n, int rows, hipStream_t s) {
 int launch_enc_bwd(const EncBwdArgs& a, int rows, hipStream_t s) {
   const int width = a.has_enc ? a.wenc : a.h;
   if (width > 256) { set_error("enc_bwd: width %d > 256", width); return SND_ERR_ARG; }
-  hipLaunchKernelGGL(enc_bwd_kernel, dim3(col_blocks(rows)), dim3(256), 0, s, a, rows);
+  dim3 grid(col_blocks(rows));
+  if (width <= 64) hipLaunchKernelGGL(enc_bwd_kernel<64>, grid, dim3(256), 0, s, a, rows);
+  else if (width <= 128) hipLaunchKernelGGL(enc_bwd_kernel<128>, grid, dim3(256), 0, s, a, rows);
+  else hipLaunchKernelGGL(enc_bwd_kernel<256>, grid, dim3(256), 0, s, a, rows);
   SND_LAUNCH_CHECK("enc_bwd_kernel");
   return 0;
 }
@@ -334,8 +411,7 @@ int launch_reduce(const ReduceDesc* d, int n, hipStream_t s) {
       pk.d[i] = d[base + i];
       if (pk.d[i].len > maxlen) maxlen = pk.d[i].len;
     }
-    int gx = cdiv(maxlen, 256);
-    if (gx > 64) gx = 64;
+    const int gx = cdiv(maxlen, 64);
     hipLaunchKernelGGL(reduce_kernel, dim3(gx, cnt), dim3(256), 0, s, pk);
     SND_LAUNCH_CHECK("reduce_kernel");
   }
@@ -379,7 +455,8 @@ extern "C" int snd_reparam_kl(const float* ms, int ldms, int rows, int latent,
                               const float* eps, unsigned long long seed,
                               const int* step_counter, float* eps_out, float* z,
                               double* kl_sum, snd_stream_t stream) {
-  SND_CHECK_ARG(ms && z && kl_sum && rows >= 0 && latent > 0, "snd_reparam_kl: bad args");
+  SND_CHECK_ARG(ms && z && kl_sum && rows >= 0 && latent > 0 && latent <= 256,
+                "snd_reparam_kl: bad args (latent in 1..256)");
   // kl_sum receives one partial per block; callers sum reparam_blocks() values.
   ReparamFwdArgs a{ms, ldms, rows, latent, eps, seed, step_counter, eps_out, z, kl_sum};
   return launch_reparam_fwd(a, (hipStream_t)stream);

@@ -4,65 +4,127 @@
 // backward products.  Operands are fp32 in HBM; tiles are converted to the
 // MFMA operand type (bf16 or f32) when staged into LDS; accumulation is fp32.
 //
-// Tile: 64(M) x 64(N) x 32(K), 256 threads = 4 waves in a 2x2 grid of 32x32
+// Tile: 64(M) x 64(N) x 64(K), 256 threads = 4 waves in a 2x2 grid of 32x32
 // wave tiles (2x2 MFMA 16x16 sub-tiles).  Operand "views" decouple memory
 // layout from the GEMM: plain / transposed matrices, conv im2col (taps never
 // cross a graph boundary: zero padding 2|2 per graph, TF SAME), flipped conv
-// weights for the data gradient.  Weight gradients use deterministic split-K
+// weights for the data gradient.  Two register stages of prefetch (tile t+2
+// loads issued before tile t's MFMAs).  Weight gradients use deterministic split-K
 // partial slabs reduced by snd_reduce (no float atomics: bitwise reproducible).
 #include "snd_gemm.hpp"
+
+#include <type_traits>
 
 namespace snd {
 
 namespace {
 
-constexpr int BM = 64, BN = 64, BK = 32, NT = 256;
+constexpr int BM = 64, BN = 64, BK = kGemmBK, NT = 256;
+
+__device__ __forceinline__ int cdiv_d(int a, int b) { return (a + b - 1) / b; }
 
 template <typename T> struct LdsStride;
-template <> struct LdsStride<float> { static constexpr int v = BK + 2; };   // 34: conflict-free b32 reads
-template <> struct LdsStride<__bf16> { static constexpr int v = BK + 8; };  // 40 (80 B rows): conflict-free b128
+template <> struct LdsStride<float> { static constexpr int v = BK + 2; };   // 66: conflict-free b32 reads
+template <> struct LdsStride<__bf16> { static constexpr int v = BK + 8; };  // 72 (144 B rows): conflict-free b128
 
-__device__ __forceinline__ bool conv_valid(int row, int t, int npg) {
-  int local = row % npg + t - 2;
-  return local >= 0 && local < npg;
-}
+// ---- operand tile loaders, lane-contiguous: lane l of a wave reads element l
+// of 64 consecutive elements along the operand's contiguous memory axis, and
+// the 4 waves x 16 registers cover the 64 rows of the tile (row = wave + 4 i).
+// Per-lane index math (conv tap t / channel c) is done once per tile.
+// A views a(m, k): k-contiguous A_ROW, A_CONV;  m-contiguous A_COL, A_CONVT.
+// B views b(k, n): n-contiguous B_ROW;          k-contiguous B_COL, B_FLIP.
+constexpr int RPT = BK / 4;   // rows per thread per tile (16)
 
-// a(m, k)
+// node-local index of row `base + q + 4 i` inside its graph, stepped without division
+struct LocalRow {
+  int local, npg;
+  __device__ __forceinline__ LocalRow(int row, int npg_) : local(row % npg_), npg(npg_) {}
+  __device__ __forceinline__ void step4() {
+    local += 4;
+    while (local >= npg) local -= npg;
+  }
+};
+
 template <int AM>
-__device__ __forceinline__ float load_a(const GemmArgs& g, int m, int k) {
-  if (m >= g.M || k >= g.K) return 0.f;
+__device__ __forceinline__ void load_a_tile(const GemmArgs& g, int m0, int k0, float (&v)[RPT]) {
+  const int lane = threadIdx.x & 63, q = threadIdx.x >> 6;
   if constexpr (AM == A_ROW) {
-    return g.A[(long long)m * g.lda + k];
-  } else if constexpr (AM == A_COL) {
-    if (m + 1 == g.a_ones_m1) return 1.f;
-    return g.A[(long long)k * g.lda + m];
-  } else if constexpr (AM == A_CONV) {       // m = node row, k = t*cin + c
-    int t = k / g.a_cin, c = k - t * g.a_cin;
-    if (!conv_valid(m, t, g.a_npg)) return 0.f;
-    return g.A[(long long)(m + t - 2) * g.lda + c];
-  } else {                                   // A_CONVT: m = t*cin + c, k = node row
-    int t = m / g.a_cin, c = m - t * g.a_cin;
-    if (!conv_valid(k, t, g.a_npg)) return 0.f;
-    return g.A[(long long)(k + t - 2) * g.lda + c];
+    const int k = k0 + lane;
+    const bool kv = k < g.K;
+#pragma unroll
+    for (int i = 0; i < RPT; ++i) {
+      const int m = m0 + q + 4 * i;
+      v[i] = (kv && m < g.M) ? g.A[(long long)m * g.lda + k] : 0.f;
+    }
+  } else if constexpr (AM == A_CONV) {           // m = node row, k = t*cin + c
+    const int k = k0 + lane;
+    const bool kv = k < g.K;
+    const int t = k / g.a_cin, c = k - t * g.a_cin;
+    LocalRow lr(m0 + q, g.a_npg);
+#pragma unroll
+    for (int i = 0; i < RPT; ++i) {
+      const int m = m0 + q + 4 * i;
+      const int src = lr.local + t - 2;
+      v[i] = (kv && m < g.M && src >= 0 && src < g.a_npg)
+                 ? g.A[(long long)(m + t - 2) * g.lda + c] : 0.f;
+      lr.step4();
+    }
+  } else if constexpr (AM == A_COL) {            // a(m, k) = A[k][m]
+    const int m = m0 + lane;
+    const bool mv = m < g.M, ones = (m + 1 == g.a_ones_m1);
+#pragma unroll
+    for (int i = 0; i < RPT; ++i) {
+      const int k = k0 + q + 4 * i;
+      v[i] = (mv && k < g.K) ? (ones ? 1.f : g.A[(long long)k * g.lda + m]) : 0.f;
+    }
+  } else {                                       // A_CONVT: m = t*cin + c, k = node row
+    const int m = m0 + lane;
+    const bool mv = m < g.M;
+    const int t = m / g.a_cin, c = m - t * g.a_cin;
+    LocalRow lr(k0 + q, g.a_npg);
+#pragma unroll
+    for (int i = 0; i < RPT; ++i) {
+      const int k = k0 + q + 4 * i;
+      const int src = lr.local + t - 2;
+      v[i] = (mv && k < g.K && src >= 0 && src < g.a_npg)
+                 ? g.A[(long long)(k + t - 2) * g.lda + c] : 0.f;
+      lr.step4();
+    }
   }
 }
 
-// b(k, n)
 template <int BMODE>
-__device__ __forceinline__ float load_b(const GemmArgs& g, int k, int n) {
-  if (k >= g.K || n >= g.N) return 0.f;
-  if constexpr (BMODE == B_ROW) {
-    return g.B[(long long)k * g.ldb + n];
-  } else if constexpr (BMODE == B_COL) {
-    return g.B[(long long)n * g.ldb + k];
-  } else {  // B_FLIP: k = t*cout + o, n = c (input channel of the forward conv)
-    int t = k / g.b_cout, o = k - t * g.b_cout;
-    return g.B[((long long)(4 - t) * g.N + n) * g.b_cout + o];
+__device__ __forceinline__ void load_b_tile(const GemmArgs& g, int k0, int n0, float (&v)[RPT]) {
+  const int lane = threadIdx.x & 63, q = threadIdx.x >> 6;
+  if constexpr (BMODE == B_ROW) {                // n = lane, k = rows
+    const int n = n0 + lane;
+    const bool nv = n < g.N;
+#pragma unroll
+    for (int i = 0; i < RPT; ++i) {
+      const int k = k0 + q + 4 * i;
+      v[i] = (nv && k < g.K) ? g.B[(long long)k * g.ldb + n] : 0.f;
+    }
+  } else if constexpr (BMODE == B_COL) {         // k = lane, n = rows
+    const int k = k0 + lane;
+    const bool kv = k < g.K;
+#pragma unroll
+    for (int i = 0; i < RPT; ++i) {
+      const int n = n0 + q + 4 * i;
+      v[i] = (kv && n < g.N) ? g.B[(long long)n * g.ldb + k] : 0.f;
+    }
+  } else {                                       // B_FLIP: k = t*cout + o = lane, n = rows
+    const int k = k0 + lane;
+    const bool kv = k < g.K;
+    const int t = k / g.b_cout, o = k - t * g.b_cout;
+#pragma unroll
+    for (int i = 0; i < RPT; ++i) {
+      const int n = n0 + q + 4 * i;
+      v[i] = (kv && n < g.N) ? g.B[((long long)(4 - t) * g.N + n) * g.b_cout + o] : 0.f;
+    }
   }
 }
 
-template <typename T>
-__device__ __forceinline__ T cvt(float x) { return (T)x; }
+template <int I> using IC = std::integral_constant<int, I>;
 
 template <typename T, int AM, int BMODE, int EPI>
 __global__ void __launch_bounds__(NT) gemm_kernel(GemmArgs g) {
@@ -78,32 +140,27 @@ __global__ void __launch_bounds__(NT) gemm_kernel(GemmArgs g) {
   const int n0 = blockIdx.y * BN;
   const int kbeg = blockIdx.z * g.kchunk;
   const int kend = min(g.K, kbeg + g.kchunk);
+  const int ntile = kend > kbeg ? cdiv_d(kend - kbeg, BK) : 0;
 
-  // staging coordinates
-  constexpr bool a_kcontig = (AM == A_ROW || AM == A_CONV);
-  constexpr bool b_kcontig = (BMODE == B_COL || BMODE == B_FLIP);
-  const int ar = a_kcontig ? (tid >> 2) : ((tid & 7) * 8);   // m (k-contig) or m0ff
-  const int ak = a_kcontig ? ((tid & 3) * 8) : (tid >> 3);
-  const int bn_ = b_kcontig ? (tid >> 2) : ((tid & 7) * 8);
-  const int bk = b_kcontig ? ((tid & 3) * 8) : (tid >> 3);
+  constexpr bool a_kc = (AM == A_ROW || AM == A_CONV);
+  constexpr bool b_kc = (BMODE == B_COL || BMODE == B_FLIP);
+  const int q = tid >> 6;
 
-  float ra[8], rb[8];
-  auto gload = [&](int k0) {
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      if (a_kcontig) ra[e] = load_a<AM>(g, m0 + ar, k0 + ak + e);
-      else ra[e] = load_a<AM>(g, m0 + ar + e, k0 + ak);
-      if (b_kcontig) rb[e] = load_b<BMODE>(g, k0 + bk + e, n0 + bn_);
-      else rb[e] = load_b<BMODE>(g, k0 + bk, n0 + bn_ + e);
-    }
+  float ra[2][RPT], rb[2][RPT];   // [stage][row]
+  auto gload = [&](auto stc, int k0) {
+    constexpr int st = decltype(stc)::value;
+    load_a_tile<AM>(g, m0, k0, ra[st]);
+    load_b_tile<BMODE>(g, k0, n0, rb[st]);
   };
-  auto sstore = [&]() {
+  auto sstore = [&](auto stc) {
+    constexpr int st = decltype(stc)::value;
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      if (a_kcontig) As[ar * S + ak + e] = cvt<T>(ra[e]);
-      else As[(ar + e) * S + ak] = cvt<T>(ra[e]);
-      if (b_kcontig) Bs[bn_ * S + bk + e] = cvt<T>(rb[e]);
-      else Bs[(bn_ + e) * S + bk] = cvt<T>(rb[e]);
+    for (int i = 0; i < RPT; ++i) {
+      const int rr = q + 4 * i;
+      if (a_kc) As[rr * S + lane] = (T)ra[st][i];     // row m = rr, col k = lane
+      else As[lane * S + rr] = (T)ra[st][i];          // row m = lane, col k = rr
+      if (b_kc) Bs[rr * S + lane] = (T)rb[st][i];     // row n = rr, col k = lane
+      else Bs[lane * S + rr] = (T)rb[st][i];          // row n = lane, col k = rr
     }
   };
 
@@ -114,41 +171,55 @@ __global__ void __launch_bounds__(NT) gemm_kernel(GemmArgs g) {
     for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int fr = lane & 15, fq = lane >> 4;
-  if (kbeg < kend) {
-    gload(kbeg);
-    for (int k0 = kbeg; k0 < kend; k0 += BK) {
-      __syncthreads();
-      sstore();
-      __syncthreads();
-      if (k0 + BK < kend) gload(k0 + BK);
-      if constexpr (sizeof(T) == 2) {
+  auto compute = [&]() {
+    if constexpr (sizeof(T) == 2) {
+#pragma unroll
+      for (int ss = 0; ss < BK / 32; ++ss) {
         bf16x8 af[2], bfr[2];
 #pragma unroll
         for (int i = 0; i < 2; ++i)
-          af[i] = *reinterpret_cast<const bf16x8*>(&As[(32 * wr + 16 * i + fr) * S + 8 * fq]);
+          af[i] = *reinterpret_cast<const bf16x8*>(&As[(32 * wr + 16 * i + fr) * S + 32 * ss + 8 * fq]);
 #pragma unroll
         for (int j = 0; j < 2; ++j)
-          bfr[j] = *reinterpret_cast<const bf16x8*>(&Bs[(32 * wc + 16 * j + fr) * S + 8 * fq]);
+          bfr[j] = *reinterpret_cast<const bf16x8*>(&Bs[(32 * wc + 16 * j + fr) * S + 32 * ss + 8 * fq]);
 #pragma unroll
         for (int i = 0; i < 2; ++i)
 #pragma unroll
           for (int j = 0; j < 2; ++j)
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
-      } else {
-#pragma unroll
-        for (int ks = 0; ks < BK / 4; ++ks) {
-          float af[2], bfr[2];
-#pragma unroll
-          for (int i = 0; i < 2; ++i) af[i] = As[(32 * wr + 16 * i + fr) * S + 4 * ks + fq];
-#pragma unroll
-          for (int j = 0; j < 2; ++j) bfr[j] = Bs[(32 * wc + 16 * j + fr) * S + 4 * ks + fq];
-#pragma unroll
-          for (int i = 0; i < 2; ++i)
-#pragma unroll
-            for (int j = 0; j < 2; ++j)
-              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i], bfr[j], acc[i][j], 0, 0, 0);
-        }
       }
+    } else {
+#pragma unroll
+      for (int ks = 0; ks < BK / 4; ++ks) {
+        float af[2], bfr[2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) af[i] = As[(32 * wr + 16 * i + fr) * S + 4 * ks + fq];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) bfr[j] = Bs[(32 * wc + 16 * j + fr) * S + 4 * ks + fq];
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i], bfr[j], acc[i][j], 0, 0, 0);
+      }
+    }
+  };
+
+  // two register stages: tile t+2's loads are issued before tile t's MFMAs
+  if (ntile > 0) gload(IC<0>{}, kbeg);
+  if (ntile > 1) gload(IC<1>{}, kbeg + BK);
+  for (int t = 0; t < ntile; t += 2) {
+    sstore(IC<0>{});
+    __syncthreads();
+    if (t + 2 < ntile) gload(IC<0>{}, kbeg + (t + 2) * BK);
+    compute();
+    __syncthreads();
+    if (t + 1 < ntile) {
+      sstore(IC<1>{});
+      __syncthreads();
+      if (t + 3 < ntile) gload(IC<1>{}, kbeg + (t + 3) * BK);
+      compute();
+      __syncthreads();
     }
   }
 
@@ -211,6 +282,7 @@ int launch_gemm(GemmArgs g, int amode, int bmode, int epi, int dtype, int splits
   if (g.M <= 0 || g.N <= 0) return 0;
   if (splits < 1) splits = 1;
   if (g.kchunk <= 0) g.kchunk = (int)round_up(cdiv(g.K, splits), BK);
+  g.kchunk = (int)round_up(g.kchunk, BK);
   splits = cdiv(g.K, g.kchunk);
   if (splits < 1) splits = 1;
   if (epi != E_PART && splits != 1) {
@@ -242,7 +314,7 @@ extern "C" int snd_gemm(int trans_a, int trans_b, int m, int n, int k,
   GemmArgs g{};
   g.M = m; g.N = n; g.K = k;
   g.A = a; g.lda = lda; g.B = b; g.ldb = ldb; g.C = c; g.ldc = ldc; g.bias = bias;
-  g.kchunk = (int)round_up(k > 0 ? k : 1, 32);
+  g.kchunk = (int)round_up(k > 0 ? k : 1, kGemmBK);
   return launch_gemm(g, trans_a ? A_COL : A_ROW, trans_b ? B_COL : B_ROW, E_STORE,
                      dtype, 1, (hipStream_t)stream);
 }
@@ -262,7 +334,7 @@ extern "C" int snd_conv1d_same_fwd(const float* x, int ldx, int rows, int npg,
   g.B = w; g.ldb = cout;
   g.C = out; g.ldc = ldo; g.bias = bias; g.gamma = gamma; g.beta = beta;
   g.pre = y_pre; g.ldp = ldy;
-  g.kchunk = (int)round_up(g.K, 32);
+  g.kchunk = (int)round_up(g.K, kGemmBK);
   return launch_gemm(g, A_CONV, B_ROW, E_CONV, dtype, 1, (hipStream_t)stream);
 }
 
@@ -278,7 +350,7 @@ extern "C" int snd_conv1d_same_bwd_data(const float* dy, int lddy, int rows,
   g.A = dy; g.lda = lddy; g.a_cin = cout; g.a_npg = npg;
   g.B = w; g.b_cout = cout;
   g.C = dx; g.ldc = lddx;
-  g.kchunk = (int)round_up(g.K, 32);
+  g.kchunk = (int)round_up(g.K, kGemmBK);
   return launch_gemm(g, A_CONV, B_FLIP, E_STORE, dtype, 1, (hipStream_t)stream);
 }
 
@@ -301,7 +373,7 @@ extern "C" int snd_conv1d_same_bwd_weight(const float* x, int ldx, const float* 
   g.A = x; g.lda = ldx; g.a_cin = cin; g.a_npg = npg;
   g.B = dy; g.ldb = lddy;
   g.C = (float*)ws;
-  g.kchunk = (int)round_up(cdiv(rows, splits), 32);
+  g.kchunk = (int)round_up(cdiv(rows, splits), kGemmBK);
   splits = cdiv(rows, g.kchunk);
   SND_TRY(launch_gemm(g, A_CONVT, B_ROW, E_PART, dtype, splits, (hipStream_t)stream));
   ReduceDesc d{(const float*)ws, dw, splits, 5 * cin * cout, 5 * cin * cout, 1.f, 0};

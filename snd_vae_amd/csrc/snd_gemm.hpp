@@ -4,6 +4,8 @@
 
 namespace snd {
 
+constexpr int kGemmBK = 64;  // K tile of the generic GEMM; split-K chunks are multiples
+
 enum AMode { A_ROW = 0, A_COL = 1, A_CONV = 2, A_CONVT = 3 };
 enum BMode { B_ROW = 0, B_COL = 1, B_FLIP = 2 };
 enum Epi { E_STORE = 0, E_CONV = 1, E_PART = 2 };
@@ -39,6 +41,6 @@ int launch_reduce(const ReduceDesc* d, int n, hipStream_t s);
 
 // Column partial sums written by elementwise kernels are laid out as
 // slab[block][ncols]; helpers compute the block count used.
-constexpr int kColRows = 256;  // rows per block in column-reduction kernels
+constexpr int kColRows = 64;   // rows per block in column-reduction kernels
 
 }  // namespace snd

@@ -129,17 +129,7 @@ __global__ void __launch_bounds__(256) edge_kernel(EdgeArgs a) {
     }
     const int s = a.rowptr[r], e = a.rowptr[r + 1];
     const float pw = a.pos_weight;
-    for (int k = s; k < e; ++k) {
-      const int c = a.colidx[k];
-      float4 zj[NV];
-      float dot = 0.f;
-#pragma unroll
-      for (int v = 0; v < NV; ++v) {
-        zj[v] = *reinterpret_cast<const float4*>(a.z + (long long)c * a.d + 4 * (sub + LPR * v));
-        dot += zi[v].x * zj[v].x + zi[v].y * zj[v].y + zi[v].z * zj[v].z + zi[v].w * zj[v].w;
-      }
-#pragma unroll
-      for (int o = LPR / 2; o > 0; o >>= 1) dot += __shfl_xor(dot, o, 64);
+    auto edge = [&](const float4 (&zj)[NV], float dot) {
       float coef = -pw;
       if (pw != 1.f) {
         const float sg = 1.f / (1.f + __expf(-dot));
@@ -154,6 +144,45 @@ __global__ void __launch_bounds__(256) edge_kernel(EdgeArgs a) {
         acc[v].x += coef * zj[v].x; acc[v].y += coef * zj[v].y;
         acc[v].z += coef * zj[v].z; acc[v].w += coef * zj[v].w;
       }
+    };
+    auto dot4 = [&](const float4 (&zj)[NV]) {
+      float d = 0.f;
+#pragma unroll
+      for (int v = 0; v < NV; ++v)
+        d += zi[v].x * zj[v].x + zi[v].y * zj[v].y + zi[v].z * zj[v].z + zi[v].w * zj[v].w;
+      return d;
+    };
+    int k = s;
+    for (; k + 4 <= e; k += 4) {            // 4 neighbours in flight, independent reductions
+      int cc[4];
+      float4 zj[4][NV];
+      float dd[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) cc[u] = a.colidx[k + u];
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int v = 0; v < NV; ++v)
+          zj[u][v] = *reinterpret_cast<const float4*>(a.z + (long long)cc[u] * a.d + 4 * (sub + LPR * v));
+#pragma unroll
+      for (int u = 0; u < 4; ++u) dd[u] = dot4(zj[u]);
+#pragma unroll
+      for (int o = LPR / 2; o > 0; o >>= 1)
+#pragma unroll
+        for (int u = 0; u < 4; ++u) dd[u] += __shfl_xor(dd[u], o, 64);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) edge(zj[u], dd[u]);
+    }
+    for (; k < e; ++k) {
+      const int c = a.colidx[k];
+      float4 zj[NV];
+#pragma unroll
+      for (int v = 0; v < NV; ++v)
+        zj[v] = *reinterpret_cast<const float4*>(a.z + (long long)c * a.d + 4 * (sub + LPR * v));
+      float dot = dot4(zj);
+#pragma unroll
+      for (int o = LPR / 2; o > 0; o >>= 1) dot += __shfl_xor(dot, o, 64);
+      edge(zj, dot);
     }
 #pragma unroll
     for (int v = 0; v < NV; ++v)
@@ -181,11 +210,13 @@ int launch_spmm(const SpmmArgs& a, hipStream_t s) {
     set_error("spmm: width %d outside 1..128", a.width);
     return SND_ERR_ARG;
   }
+  // float4 gathers need aligned input rows; the GCN epilogue stores `out`
+  // per element (its ld, e.g. 67 = h + f_in, is not 16-B aligned)
   const bool vec = (a.width % 64 == 0) && (a.ldh % 4 == 0) &&
-                   ((uintptr_t)a.h % 16 == 0) && (a.ldo % 4 == 0) &&
-                   ((uintptr_t)a.out % 16 == 0) &&
-                   (a.epilogue == SND_SPMM_PLAIN ||
-                    (a.ldp % 4 == 0 && (uintptr_t)a.pre % 16 == 0));
+                   ((uintptr_t)a.h % 16 == 0) &&
+                   (a.epilogue == SND_SPMM_PLAIN
+                        ? (a.ldo % 4 == 0 && (uintptr_t)a.out % 16 == 0)
+                        : (a.ldp % 4 == 0 && (uintptr_t)a.pre % 16 == 0));
   dim3 grid(cdiv(a.n_rows, kRowsPerBlock));
   if (a.epilogue == SND_SPMM_PLAIN) {
     if (vec) hipLaunchKernelGGL((spmm_kernel<SND_SPMM_PLAIN, true>), grid, dim3(256), 0, s, a);
@@ -227,7 +258,8 @@ extern "C" int snd_csr_spmm(const int* rowptr, const int* colidx, int n_rows,
                             const float* concat_x, int ldx, int fx,
                             const float* bn2_gamma, const float* bn2_beta,
                             float* out2, int ldo2, snd_stream_t stream) {
-  SND_CHECK_ARG(n_rows >= 0 && rowptr && colidx && h && out, "snd_csr_spmm: null operand");
+  // colidx may be NULL for an edgeless batch (never dereferenced when nnz == 0)
+  SND_CHECK_ARG(n_rows >= 0 && rowptr && h && out, "snd_csr_spmm: null operand");
   SND_CHECK_ARG(epilogue == SND_SPMM_PLAIN || epilogue == SND_SPMM_GCN,
                 "snd_csr_spmm: bad epilogue %d", epilogue);
   SND_CHECK_ARG(epilogue == SND_SPMM_PLAIN || (bn_gamma && bn_beta && preact),

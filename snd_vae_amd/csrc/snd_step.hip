@@ -43,7 +43,7 @@ Split wgrad_split(int M, int N, int R) {
   const int smax = cdiv(R, 256);
   if (s > smax) s = smax;
   if (s < 1) s = 1;
-  const int kchunk = (int)round_up(cdiv(R, s), 32);
+  const int kchunk = (int)round_up(cdiv(R, s), kGemmBK);
   return {cdiv(R, kchunk), kchunk};
 }
 
@@ -231,7 +231,7 @@ int gemm_fwd(const Ctx& x, int M, int N, int K, const float* A, int lda, const f
              int bmode, float* C, int ldc, const float* bias) {
   GemmArgs g{};
   g.M = M; g.N = N; g.K = K; g.A = A; g.lda = lda; g.B = B; g.ldb = ldb; g.C = C; g.ldc = ldc;
-  g.bias = bias; g.kchunk = (int)round_up(K, 32);
+  g.bias = bias; g.kchunk = (int)round_up(K, kGemmBK);
   return launch_gemm(g, A_ROW, bmode, E_STORE, x.p->c.dtype, 1, x.s);
 }
 
@@ -251,7 +251,7 @@ int conv_fwd(const Ctx& x, const float* in, int ldi, int cin, const char* K, int
   g.A = in; g.lda = ldi; g.a_cin = cin; g.a_npg = x.p->N;
   g.B = x.w(K); g.ldb = cout; g.C = out; g.ldc = cout; g.bias = x.w(b);
   g.gamma = x.w(gam); g.beta = x.w(bet); g.pre = ypre; g.ldp = cout;
-  g.kchunk = (int)round_up(g.K, 32);
+  g.kchunk = (int)round_up(g.K, kGemmBK);
   return launch_gemm(g, A_CONV, B_ROW, E_CONV, x.p->c.dtype, 1, x.s);
 }
 
@@ -261,7 +261,7 @@ int conv_bwd_data(const Ctx& x, const float* dy, int cout, const char* K, int ci
   g.M = x.p->R; g.N = cin; g.K = 5 * cout;
   g.A = dy; g.lda = cout; g.a_cin = cout; g.a_npg = x.p->N;
   g.B = x.w(K); g.b_cout = cout; g.C = dx; g.ldc = lddx;
-  g.kchunk = (int)round_up(g.K, 32);
+  g.kchunk = (int)round_up(g.K, kGemmBK);
   return launch_gemm(g, A_CONV, B_FLIP, E_STORE, x.p->c.dtype, 1, x.s);
 }
 

@@ -483,7 +483,8 @@ extern "C" int snd_zzt_ce(const float* z, int n_graphs, int n, int d, const int*
                           const int* colidx, float pos_weight, float norm,
                           double* stats, float* dz, void* ws, size_t ws_bytes,
                           int dtype, snd_stream_t stream) {
-  SND_CHECK_ARG(z && rowptr && colidx && stats && dz, "snd_zzt_ce: null operand");
+  // colidx may be NULL for an edgeless batch (never dereferenced when nnz == 0)
+  SND_CHECK_ARG(z && rowptr && stats && dz, "snd_zzt_ce: null operand");
   SND_CHECK_ARG(d == 16 || d == 32 || d == 64 || d == 128, "snd_zzt_ce: d=%d not in {16,32,64,128}", d);
   SND_CHECK_ARG(n > 0 && n_graphs > 0, "snd_zzt_ce: empty batch");
   SND_CHECK_ARG(dtype == SND_F32 || dtype == SND_BF16, "snd_zzt_ce: bad dtype");

@@ -216,8 +216,8 @@ def test_reparam_injected_and_philox():
     nb = _lib.lib().snd_reparam_kl_blocks(rows, L)
     kl = torch.zeros(nb, dtype=torch.float64, device=DEV)
     z = torch.empty(rows, L, device=DEV)
-    tms = cu(ms)
-    _lib.check(_lib.lib().snd_reparam_kl(tms.data_ptr(), 2 * L, rows, L, cu(eps).data_ptr(), 0, 0, 0,
+    tms, teps = cu(ms), cu(eps)
+    _lib.check(_lib.lib().snd_reparam_kl(tms.data_ptr(), 2 * L, rows, L, teps.data_ptr(), 0, 0, 0,
                                          z.data_ptr(), kl.data_ptr(), _lib.stream_ptr()))
     mu, s = ms[:, :L].astype(np.float64), ms[:, L:].astype(np.float64)
     assert rel(z.cpu().numpy(), mu + eps * np.exp(s)) < 1e-6
@@ -252,8 +252,9 @@ def test_sigmoid_mse_head():
     db = torch.zeros(cout, device=DEV)
     ws = torch.empty(nb * (cin * cout + cout) * 4, dtype=torch.uint8, device=DEV)
     yh = torch.empty(rows, cout, device=DEV)
-    _lib.check(_lib.lib().snd_sigmoid_mse(cu(u).data_ptr(), cin, rows, cin, cu(w).data_ptr(),
-                                          cu(b).data_ptr(), cout, cu(y).data_ptr(), cout,
+    tu, tw, tb, ty = cu(u), cu(w), cu(b), cu(y)   # keep alive across the raw-pointer call
+    _lib.check(_lib.lib().snd_sigmoid_mse(tu.data_ptr(), cin, rows, cin, tw.data_ptr(),
+                                          tb.data_ptr(), cout, ty.data_ptr(), cout,
                                           sse.data_ptr(), yh.data_ptr(), du.data_ptr(), cin,
                                           dw.data_ptr(), db.data_ptr(), ws.data_ptr(), ws.numel(),
                                           _lib.stream_ptr()))
