@@ -172,6 +172,7 @@ def main():
         return e0.elapsed_time(e1) / args.kernel_reps
 
     zzt_ms = kernel_ms("zzt_dense")
+    zzt_v1_ms = kernel_ms("zzt_dense_v1") if args.dtype == "bf16" else None
     spmm_ms = kernel_ms("spmm_dxw1")
     flops = 4.0 * N * N * d * B                       # 2N^2 d fwd + 2N^2 d bwd per graph
     achieved = flops / (zzt_ms * 1e-3) / 1e12
@@ -203,7 +204,8 @@ def main():
                      "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
                      "frac": round(achieved / peak, 4),
                      "traffic": load_traffic(N, d, B, args.dtype),
-                     "avg_launch_ms": round(zzt_ms, 5), "flops_per_launch": flops},
+                     "avg_launch_ms": round(zzt_ms, 5), "flops_per_launch": flops,
+                     "previous_variant_ms": None if zzt_v1_ms is None else round(zzt_v1_ms, 5)},
         "secondary_roofline": {"kernel": "csr_spmm (A @ dP1, width 64, fp32)", "bound": "hbm",
                                "achieved": round(spmm_gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                                "frac": round(spmm_gbs / PEAK_HBM_GBS, 4),

@@ -284,11 +284,11 @@ extern "C" int snd_plan_launch(const snd_plan_t* plan, const snd_batch_t* batch,
   char* ws = (char*)workspace;
   hipStream_t s = (hipStream_t)stream;
   const int L = p.c.latent;
-  if (!strcmp(kernel, "zzt_dense")) {
+  if (!strcmp(kernel, "zzt_dense") || !strcmp(kernel, "zzt_dense_v1")) {
     const size_t half = zzt_staging_bytes(p.B, p.N, L, p.c.dtype) / 2;
     char* st = ws + p.buf("ZSTAGE");
     ZztArgs za{st, st + half, p.N, zzt_npad(p.N), p.B, L, (float*)(ws + p.buf("DJD")),
-               (double*)(ws + p.buf("PZZT"))};
+               (double*)(ws + p.buf("PZZT")), kernel[9] == '_' ? 1 : 0};
     return launch_zzt_dense(za, p.c.dtype, s);
   }
   if (!strcmp(kernel, "spmm_dxw1")) {   // A @ dP1 (plain SpMM, width h1)

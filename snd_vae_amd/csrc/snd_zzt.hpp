@@ -9,6 +9,7 @@ struct ZztArgs {
   int n, npad, ngraphs, d;
   float* dJd;        // [B*n][d]  sum_{j != i} sigmoid(L_ij) z_j
   double* part;      // [blocks][2] = {sum softplus over valid pairs, #{L > 0}}
+  int variant;       // bf16 kernel variant: 0 = default (v2), 1 = v1 (A/B measurement)
 };
 
 int zzt_dp(int d);

@@ -76,8 +76,11 @@ def test_train_step_bf16_vs_golden(name):
     for k in ("cost", "adj_cost", "kl"):
         assert got[k] == pytest.approx(float(z[f"s0/loss/{k}"]), rel=2e-2), k
     grads = opt.grad_blocks()
-    for k in ("enc.W0", "enc.Wms", "dec.K1", "dec.Ws"):
-        assert block_err(grads[k], z[f"s0/grad/{k}"]) < 8e-2, k
+    # bf16 operands (8-bit mantissa) in sums with cancellation: compare norm-wise
+    for k, g in grads.items():
+        ref = z[f"s0/grad/{k}"]
+        err = np.linalg.norm(g - ref) / max(np.linalg.norm(ref), 1e-30)
+        assert err < 5e-2, (k, err)
 
 
 @pytest.mark.parametrize("dtype,ltol,gtol", [("f32", 1e-5, 2e-4), ("bf16", 2e-2, 1e-1)])
