@@ -284,11 +284,11 @@ extern "C" int snd_plan_launch(const snd_plan_t* plan, const snd_batch_t* batch,
   char* ws = (char*)workspace;
   hipStream_t s = (hipStream_t)stream;
   const int L = p.c.latent;
-  if (!strcmp(kernel, "zzt_dense") || !strcmp(kernel, "zzt_dense_v1")) {
-    const size_t half = zzt_staging_bytes(p.B, p.N, L, p.c.dtype) / 2;
-    char* st = ws + p.buf("ZSTAGE");
-    ZztArgs za{st, st + half, p.N, zzt_npad(p.N), p.B, L, (float*)(ws + p.buf("DJD")),
-               (double*)(ws + p.buf("PZZT")), kernel[9] == '_' ? 1 : 0};
+  if (!strncmp(kernel, "zzt_dense", 9)) {   // zzt_dense | zzt_dense_v1 | zzt_dense_v2
+    const ZztStage stg = zzt_stage(ws + p.buf("ZSTAGE"), p.B, p.N, L, p.c.dtype);
+    const int variant = kernel[9] == '_' ? kernel[11] - '0' : 0;
+    ZztArgs za{stg.jrow, stg.jt, p.N, zzt_npad(p.N), p.B, L, (float*)(ws + p.buf("DJD")),
+               (double*)(ws + p.buf("PZZT")), stg.colpart, variant};
     return launch_zzt_dense(za, p.c.dtype, s);
   }
   if (!strcmp(kernel, "spmm_dxw1")) {   // A @ dP1 (plain SpMM, width h1)
@@ -349,10 +349,9 @@ extern "C" int snd_train_step(const snd_plan_t* plan, const snd_batch_t* batch,
   }
   // inner-product decoder + CE (fused) and per-edge terms
   {
-    const size_t half = zzt_staging_bytes(p.B, N, L, c.dtype) / 2;
-    char* st = x.ws + p.buf("ZSTAGE");
-    SND_TRY(launch_zzt_prep(x.f("Z"), p.B, N, L, c.dtype, st, st + half, x.s));
-    ZztArgs za{st, st + half, N, zzt_npad(N), p.B, L, x.f("DJD"), x.d("PZZT")};
+    const ZztStage stg = zzt_stage(x.ws + p.buf("ZSTAGE"), p.B, N, L, c.dtype);
+    SND_TRY(launch_zzt_prep(x.f("Z"), p.B, N, L, c.dtype, stg, x.s));
+    ZztArgs za{stg.jrow, stg.jt, N, zzt_npad(N), p.B, L, x.f("DJD"), x.d("PZZT"), stg.colpart, 0};
     SND_TRY(launch_zzt_dense(za, c.dtype, x.s));
     EdgeArgs ea{rp, ci, R, x.f("Z"), L, c.pos_weight, x.f("EJ"), x.d("PEDGE")};
     SND_TRY(launch_edge(ea, x.s));

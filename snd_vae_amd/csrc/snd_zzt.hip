@@ -42,8 +42,9 @@ constexpr int NTH = 512;
 // ---------------------------------------------------------------- prep
 template <typename T, int DP>
 __global__ void __launch_bounds__(256) zzt_prep_kernel(const float* z, int n, int npad,
-                                                       int d, T* jrow, T* jt) {
+                                                       int d, T* jrow, T* jt, float* colpart) {
   __shared__ float tile[64][DP + 1];
+  __shared__ float stile[64][DP + 1];
   const int g = blockIdx.y, rb = blockIdx.x;
   const float sc = 1.2011224087864498f;  // sqrt(log2 e)
   for (int idx = threadIdx.x; idx < 64 * DP; idx += 256) {
@@ -51,9 +52,18 @@ __global__ void __launch_bounds__(256) zzt_prep_kernel(const float* z, int n, in
     const int row = rb * 64 + rr;
     const float v = (row < n && c < d) ? z[((long long)g * n + row) * d + c] : 0.f;
     tile[rr][c] = v;
-    jrow[((long long)g * npad + row) * DP + c] = (T)(v * sc);
+    const T b = (T)(v * sc);
+    stile[rr][c] = (float)b;
+    jrow[((long long)g * npad + row) * DP + c] = b;
   }
   __syncthreads();
+  // per-64-row column sums of the stored (rounded) K-role values: sum_j x_ij
+  // of every row i follows from them without touching the N^2 logits
+  if (threadIdx.x < DP) {
+    float cs = 0.f;
+    for (int rr = 0; rr < 64; ++rr) cs += stile[rr][threadIdx.x];
+    colpart[((long long)g * (npad / 64) + rb) * DP + threadIdx.x] = cs;
+  }
   for (int idx = threadIdx.x; idx < 64 * DP; idx += 256) {
     const int c = idx >> 6, rr = idx & 63;
     jt[((long long)g * DP + c) * npad + rb * 64 + rr] = (T)tile[rr][c];
@@ -454,6 +464,249 @@ __global__ void __launch_bounds__(NTH2) zzt_dense_bf16_v2(ZztArgs a) {
   }
 }
 
+// ---------------------------------------------------------------- bf16 MFMA, v3
+// v2's structure with a mask-free main loop.  Every (i, j) of the padded
+// npad x npad square is evaluated; afterwards
+//   * padded pairs (zero rows, x = 0 exactly: 1 log2-unit of loss each, no
+//     sign count, sigma * 0 = 0 into dJ) are subtracted analytically;
+//   * the diagonal (x_ii from the wave's own z_i registers) is subtracted
+//     from loss, count and dJ_i (sigma rounded to bf16 as the MFMA saw it).
+// max(x, 0) = (x + |x|) / 2 with sum_j x_ij = z_i . sum_j z_j computed from
+// per-64-row column sums written by the prep kernel: one |x| add per logit.
+// Per logit: exp2, rcp (transcendental), q = 1 + e, running product, |x|
+// add, sign compare (its mask feeds the sigma select and a SALU popcount),
+// sigma multiply + select, bf16 pack.
+__device__ __forceinline__ void chunk_epilogue3(const f32x4& X0, const f32x4& X1, bf16x8& sb,
+                                                float& labs, float& llog, unsigned& wcnt) {
+  float prod0 = 1.f, prod1 = 1.f, sa = 0.f;
+  unsigned wc = 0;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const float xv = e < 4 ? X0[e] : X1[e - 4];
+    const float ex = __builtin_amdgcn_exp2f(-fabsf(xv));
+    const float qd = 1.f + ex;
+    const float rc = __builtin_amdgcn_rcpf(qd);
+    const bool pos = xv > 0.f;
+    if (e & 1) prod1 *= qd; else prod0 *= qd;
+    sa += fabsf(xv);
+    sb[e] = (__bf16)(pos ? rc : ex * rc);
+    wc += (unsigned)__popcll(__ballot(pos));
+  }
+  labs += sa;
+  llog += __builtin_amdgcn_logf(prod0 * prod1);
+  wcnt += wc;
+}
+
+template <int DP>
+__global__ void __launch_bounds__(NTH2) zzt_dense_bf16_v3(ZztArgs a) {
+  constexpr int JS = TJ2 * DP;
+  constexpr int TS = DP * TJ2;
+  constexpr int KS = DP / 32;
+  constexpr int CT = DP / 16;
+  constexpr int CPR = DP / 8;
+  constexpr int TCPR = TJ2 / 8;
+  constexpr int JCH = TJ2 * CPR, TCH = DP * TCPR;
+  constexpr int JPT = (JCH + NTH2 - 1) / NTH2, TPT = (TCH + NTH2 - 1) / NTH2;
+  __shared__ __attribute__((aligned(16))) __bf16 lds[2][JS + TS];
+  __shared__ float colsum[DP];
+  __shared__ float csred[NTH2 / DP][DP];
+
+  const int g = blockIdx.x % a.ngraphs, rb = blockIdx.x / a.ngraphs;
+  const __bf16* Jg = reinterpret_cast<const __bf16*>(a.jrow) + (long long)g * a.npad * DP;
+  const __bf16* JTg = reinterpret_cast<const __bf16*>(a.jt) + (long long)g * DP * a.npad;
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, r = lane & 15, q4 = lane >> 4;
+  const int rg = w & 7, half = w >> 3;
+  const int i0 = __builtin_amdgcn_readfirstlane(rb * ROWS + 16 * rg);
+  const int i_me = i0 + r;
+
+  bf16x8 bI[KS];
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks)
+    bI[ks] = *reinterpret_cast<const bf16x8*>(Jg + (long long)i_me * DP + 32 * ks + 8 * q4);
+  // graph column sums S_k = sum_j zs_jk (fixed order over the 64-row partials)
+  {
+    const int nrb = a.npad / 64;
+    const int k = tid % DP, grp = tid / DP;
+    constexpr int NG = NTH2 / DP;
+    float s = 0.f;
+    for (int p = grp; p < nrb; p += NG) s += a.colpart[((long long)g * nrb + p) * DP + k];
+    csred[grp][k] = s;
+  }
+  __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): see v2
+  __syncthreads();
+  if (tid < DP) {
+    float s = 0.f;
+    for (int p = 0; p < NTH2 / DP; ++p) s += csred[p][tid];
+    colsum[tid] = s;
+  }
+  f32x4 acc[CT];
+#pragma unroll
+  for (int ct = 0; ct < CT; ++ct) acc[ct] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  uint4 rj[JPT], rt[TPT];
+  auto gload = [&](int t) {
+#pragma unroll
+    for (int p = 0; p < JPT; ++p) {
+      const int idx = tid + p * NTH2;
+      if (idx < JCH) {
+        const int row = idx / CPR, ch = idx - row * CPR;
+        rj[p] = *reinterpret_cast<const uint4*>(Jg + (long long)(t * TJ2 + row) * DP + ch * 8);
+      }
+    }
+#pragma unroll
+    for (int p = 0; p < TPT; ++p) {
+      const int idx = tid + p * NTH2;
+      if (idx < TCH) {
+        const int c = idx / TCPR, ch = idx - c * TCPR;
+        rt[p] = *reinterpret_cast<const uint4*>(JTg + (long long)c * a.npad + t * TJ2 + ch * 8);
+      }
+    }
+  };
+  auto sstore = [&](int buf) {
+#pragma unroll
+    for (int p = 0; p < JPT; ++p) {
+      const int idx = tid + p * NTH2;
+      if (idx < JCH) {
+        const int row = idx / CPR, ch = idx - row * CPR;
+        *reinterpret_cast<uint4*>(&lds[buf][row * DP + ((ch ^ Swz<DP>::j(row)) * 8)]) = rj[p];
+      }
+    }
+    // z^T image for the PV A-operand: inside every 32-column block the two
+    // 4-column groups a lane needs (j = 4g.., 16 + 4g..) are stored as one 16 B
+    // chunk g, so the operand is ONE ds_read_b128; chunks XOR-swizzled by
+    // (c & 15), conflict-free over the b128 lane groups.
+#pragma unroll
+    for (int p = 0; p < TPT; ++p) {
+      const int idx = tid + p * NTH2;
+      if (idx < TCH) {
+        const int c = idx / TCPR, ch = idx - c * TCPR;
+        const int blk = ch >> 2, m = ch & 3, hsel = m >> 1;
+        const int c0 = ((4 * blk + ((2 * m) & 3)) ^ (c & 15)) * 8 + 4 * hsel;
+        const int c1 = ((4 * blk + ((2 * m + 1) & 3)) ^ (c & 15)) * 8 + 4 * hsel;
+        __bf16* row = &lds[buf][JS + c * TJ2];
+        *reinterpret_cast<uint2*>(row + c0) = make_uint2(rt[p].x, rt[p].y);
+        *reinterpret_cast<uint2*>(row + c1) = make_uint2(rt[p].z, rt[p].w);
+      }
+    }
+  };
+  auto qk = [&](const __bf16* Ls, int q, f32x4& X0, f32x4& X1) {
+    X0 = f32x4{0.f, 0.f, 0.f, 0.f};
+    X1 = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int ra = 32 * q + r, rb2 = 32 * q + 16 + r;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      const bf16x8 a0 = *reinterpret_cast<const bf16x8*>(
+          &Ls[ra * DP + (((4 * ks + q4) ^ Swz<DP>::j(ra)) * 8)]);
+      const bf16x8 a1 = *reinterpret_cast<const bf16x8*>(
+          &Ls[rb2 * DP + (((4 * ks + q4) ^ Swz<DP>::j(rb2)) * 8)]);
+      X0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, bI[ks], X0, 0, 0, 0);
+      X1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, bI[ks], X1, 0, 0, 0);
+    }
+  };
+  auto pv = [&](const __bf16* Ls, int q, const bf16x8& sb) {
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct) {
+      const int c = 16 * ct + r;
+      const bf16x8 a2 = *reinterpret_cast<const bf16x8*>(
+          &Ls[JS + c * TJ2 + (((4 * q + q4) ^ (c & 15)) * 8)]);
+      acc[ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a2, sb, acc[ct], 0, 0, 0);
+    }
+  };
+
+  const int ntiles = a.npad / TJ2;
+  gload(0);
+  sstore(0);
+  __syncthreads();
+  float labs = 0.f, llog = 0.f;
+  double ltot = 0.0;
+  unsigned wcnt = 0;
+  const int qa = 2 * half, qb = 2 * half + 1;
+  for (int t = 0; t < ntiles; ++t) {
+    const int cur = t & 1;
+    if (t + 1 < ntiles) gload(t + 1);
+    const __bf16* Ls = lds[cur];
+    f32x4 Xa0, Xa1, Xb0, Xb1;
+    bf16x8 sa, sbv;
+    qk(Ls, qa, Xa0, Xa1);
+    qk(Ls, qb, Xb0, Xb1);
+    chunk_epilogue3(Xa0, Xa1, sa, labs, llog, wcnt);
+    pv(Ls, qa, sa);
+    chunk_epilogue3(Xb0, Xb1, sbv, labs, llog, wcnt);
+    pv(Ls, qb, sbv);
+    if (t + 1 < ntiles) sstore(cur ^ 1);
+    __syncthreads();
+    if ((t & 7) == 7) {             // keep the fp32 partial sums short
+      ltot += (double)(0.5f * labs + llog);
+      labs = 0.f;
+      llog = 0.f;
+    }
+  }
+  ltot += (double)(0.5f * labs + llog);
+
+  // ---- corrections (row i = i_me; the 4 q4-lanes of a row share them)
+  float xd = 0.f, xs = 0.f;           // x_ii and sum_j x_ij (this lane's k-slice)
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+    for (int jj = 0; jj < 8; ++jj) {
+      const float b = (float)bI[ks][jj];
+      xd += b * b;
+      xs += b * colsum[32 * ks + 8 * q4 + jj];
+    }
+  xd += __shfl_xor(xd, 16, 64);
+  xd += __shfl_xor(xd, 32, 64);
+  xs += __shfl_xor(xs, 16, 64);
+  xs += __shfl_xor(xs, 32, 64);
+  const bool row_valid = i_me < a.n;
+  const float exd = __builtin_amdgcn_exp2f(-fabsf(xd));
+  const float sgd = xd > 0.f ? 1.f / (1.f + exd) : exd / (1.f + exd);
+  if (half == 0 && q4 == 0 && row_valid) {
+    // + sum_j x_ij / 2 (the other half of max(x,0)); - softplus2(x_ii)
+    ltot += 0.5 * (double)xs;
+    ltot -= (double)(fmaxf(xd, 0.f) + __builtin_amdgcn_logf(1.f + exd));
+  }
+  const unsigned dpos = (unsigned)__popcll(__ballot(half == 0 && q4 == 0 && row_valid && xd > 0.f));
+
+  // ---- combine the two column halves' partial dJ, subtract the diagonal term
+  float* red = reinterpret_cast<float*>(&lds[0][0]);
+  const int slot = (rg * 64 + lane) * (4 * CT);
+  if (half == 1) {
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct)
+      *reinterpret_cast<f32x4*>(&red[slot + 4 * ct]) = acc[ct];
+  }
+  __syncthreads();
+  if (half == 0 && row_valid) {
+    const float sgb = (float)(__bf16)sgd;            // sigma as the PV-MFMA consumed it
+    float* dst = a.dJd + ((long long)g * a.n + i_me) * a.d;
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct) {
+      const f32x4 o = *reinterpret_cast<const f32x4*>(&red[slot + 4 * ct]);
+      const int c0 = 16 * ct + 4 * q4;
+      if (c0 < a.d) {
+        float v[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          v[e] = acc[ct][e] + o[e] - sgb * (float)JTg[(long long)(c0 + e) * a.npad + i_me];
+        *reinterpret_cast<float4*>(dst + c0) = make_float4(v[0], v[1], v[2], v[3]);
+      }
+    }
+  }
+  __shared__ double sl[NTH2 / 64];
+  __shared__ unsigned sc[NTH2 / 64];
+  const double l = wave_sum_d(ltot);
+  if (lane == 0) { sl[w] = l; sc[w] = wcnt - dpos; }
+  __syncthreads();
+  if (tid == 0) {
+    double tl = 0.0, tc = 0.0;
+    for (int k = 0; k < NTH2 / 64; ++k) { tl += sl[k]; tc += (double)sc[k]; }
+    if (rb == 0)   // padded pairs of this graph: x = 0 exactly, log2(1 + 1) = 1 each
+      tl -= (double)a.npad * a.npad - (double)a.n * a.n;
+    a.part[2 * blockIdx.x] = tl * (double)kLn2;
+    a.part[2 * blockIdx.x + 1] = tc;
+  }
+}
+
 // ---------------------------------------------------------------- f32 MFMA
 __device__ __forceinline__ int hJ(int row) { return ((row & 1) << 1) | (((row >> 1) & 7) << 2); }
 __device__ __forceinline__ int hT(int c) { return (c & 3) | (((c >> 2) & 3) << 3); }
@@ -618,16 +871,27 @@ int zzt_dense_blocks(int ngraphs, int n) { return ngraphs * (zzt_npad(n) / ROWS)
 size_t zzt_staging_bytes(int ngraphs, int n, int d, int dtype) {
   const int dp = zzt_dp(d);
   const size_t es = dtype == SND_BF16 ? 2 : 4;
-  return 2 * (size_t)ngraphs * zzt_npad(n) * dp * es;
+  const size_t img = round_up((size_t)ngraphs * zzt_npad(n) * dp * es, 256);
+  return 2 * img + round_up((size_t)ngraphs * (zzt_npad(n) / 64) * dp * sizeof(float), 256);
 }
 
-int launch_zzt_prep(const float* z, int ngraphs, int n, int d, int dtype, void* jrow,
-                    void* jt, hipStream_t s) {
+ZztStage zzt_stage(void* base, int ngraphs, int n, int d, int dtype) {
+  const int dp = zzt_dp(d);
+  const size_t es = dtype == SND_BF16 ? 2 : 4;
+  const size_t img = round_up((size_t)ngraphs * zzt_npad(n) * dp * es, 256);
+  char* b = (char*)base;
+  return ZztStage{b, b + img, (float*)(b + 2 * img)};
+}
+
+int launch_zzt_prep(const float* z, int ngraphs, int n, int d, int dtype, const ZztStage& st,
+                    hipStream_t s) {
+  void* jrow = st.jrow;
+  void* jt = st.jt;
   const int dp = zzt_dp(d), npad = zzt_npad(n);
   dim3 grid(npad / 64, ngraphs);
 #define SND_PREP(T, DPV)                                                                \
   hipLaunchKernelGGL((zzt_prep_kernel<T, DPV>), grid, dim3(256), 0, s, z, n, npad, d, \
-                     (T*)jrow, (T*)jt)
+                     (T*)jrow, (T*)jt, st.colpart)
   if (dtype == SND_BF16) {
     if (dp == 32) SND_PREP(__bf16, 32); else if (dp == 64) SND_PREP(__bf16, 64); else SND_PREP(__bf16, 128);
   } else {
@@ -645,10 +909,14 @@ int launch_zzt_dense(const ZztArgs& a, int dtype, hipStream_t s) {
     if (dp == 32) hipLaunchKernelGGL((zzt_dense_bf16<32>), grid, dim3(NTH), 0, s, a);
     else if (dp == 64) hipLaunchKernelGGL((zzt_dense_bf16<64>), grid, dim3(NTH), 0, s, a);
     else hipLaunchKernelGGL((zzt_dense_bf16<128>), grid, dim3(NTH), 0, s, a);
-  } else if (dtype == SND_BF16) {                     // v2 (default)
+  } else if (dtype == SND_BF16 && a.variant == 2) {   // v2: masked epilogue
     if (dp == 32) hipLaunchKernelGGL((zzt_dense_bf16_v2<32>), grid, dim3(NTH2), 0, s, a);
     else if (dp == 64) hipLaunchKernelGGL((zzt_dense_bf16_v2<64>), grid, dim3(NTH2), 0, s, a);
     else hipLaunchKernelGGL((zzt_dense_bf16_v2<128>), grid, dim3(NTH2), 0, s, a);
+  } else if (dtype == SND_BF16) {                     // v3 (default): mask-free + corrections
+    if (dp == 32) hipLaunchKernelGGL((zzt_dense_bf16_v3<32>), grid, dim3(NTH2), 0, s, a);
+    else if (dp == 64) hipLaunchKernelGGL((zzt_dense_bf16_v3<64>), grid, dim3(NTH2), 0, s, a);
+    else hipLaunchKernelGGL((zzt_dense_bf16_v3<128>), grid, dim3(NTH2), 0, s, a);
   } else {
     const size_t shm = 2 * 2 * (size_t)TJ * dp * sizeof(float);
     if (dp == 32) hipLaunchKernelGGL((zzt_dense_f32<32>), grid, dim3(NTH), shm, s, a);
@@ -707,10 +975,8 @@ extern "C" int snd_zzt_ce(const float* z, int n_graphs, int n, int d, const int*
   SND_TRY(zzt_init_attributes());
   hipStream_t s = (hipStream_t)stream;
   char* p = (char*)ws;
-  const size_t half = zzt_staging_bytes(n_graphs, n, d, dtype) / 2;
-  void* jrow = p;
-  void* jt = p + half;
-  p += round_up(2 * half, 256);
+  const ZztStage stg = zzt_stage(p, n_graphs, n, d, dtype);
+  p += round_up(zzt_staging_bytes(n_graphs, n, d, dtype), 256);
   const long long rows = (long long)n_graphs * n;
   float* ej = (float*)p;
   p += round_up(rows * d * sizeof(float), 256);
@@ -718,8 +984,8 @@ extern "C" int snd_zzt_ce(const float* z, int n_graphs, int n, int d, const int*
   p += round_up(2 * sizeof(double) * (size_t)zzt_dense_blocks(n_graphs, n), 256);
   double* pe = (double*)p;
 
-  SND_TRY(launch_zzt_prep(z, n_graphs, n, d, dtype, jrow, jt, s));
-  ZztArgs a{jrow, jt, n, zzt_npad(n), n_graphs, d, dz, pd};
+  SND_TRY(launch_zzt_prep(z, n_graphs, n, d, dtype, stg, s));
+  ZztArgs a{stg.jrow, stg.jt, n, zzt_npad(n), n_graphs, d, dz, pd, stg.colpart, 0};
   SND_TRY(launch_zzt_dense(a, dtype, s));
   EdgeArgs e{rowptr, colidx, (int)rows, z, d, pos_weight, ej, pe};
   SND_TRY(launch_edge(e, s));

@@ -4,21 +4,30 @@
 namespace snd {
 
 struct ZztArgs {
-  const void* jrow;  // [B][npad][DP] z * sqrt(log2 e)   (bf16 or f32)
-  const void* jt;    // [B][DP][npad] z^T                (bf16 or f32)
+  const void* jrow;      // [B][npad][DP] z * sqrt(log2 e)   (bf16 or f32)
+  const void* jt;        // [B][DP][npad] z^T                (bf16 or f32)
   int n, npad, ngraphs, d;
-  float* dJd;        // [B*n][d]  sum_{j != i} sigmoid(L_ij) z_j
-  double* part;      // [blocks][2] = {sum softplus over valid pairs, #{L > 0}}
-  int variant;       // bf16 kernel variant: 0 = default (v2), 1 = v1 (A/B measurement)
+  float* dJd;            // [B*n][d]  sum_{j != i} sigmoid(L_ij) z_j
+  double* part;          // [blocks][2] = {sum softplus over valid pairs, #{L > 0}}
+  const float* colpart;  // [B][npad/64][DP] column sums of jrow (bf16 values), per 64 rows
+  int variant;           // bf16 kernel: 0 = default (v3), 1 = v1, 2 = v2 (A/B measurement)
+};
+
+// Staging buffers carved from one workspace region.
+struct ZztStage {
+  void* jrow;
+  void* jt;
+  float* colpart;
 };
 
 int zzt_dp(int d);
 int zzt_npad(int n);
 int zzt_dense_blocks(int ngraphs, int n);
 size_t zzt_staging_bytes(int ngraphs, int n, int d, int dtype);
+ZztStage zzt_stage(void* base, int ngraphs, int n, int d, int dtype);
 int zzt_init_attributes();
-int launch_zzt_prep(const float* z, int ngraphs, int n, int d, int dtype, void* jrow,
-                    void* jt, hipStream_t s);
+int launch_zzt_prep(const float* z, int ngraphs, int n, int d, int dtype, const ZztStage& st,
+                    hipStream_t s);
 int launch_zzt_dense(const ZztArgs& a, int dtype, hipStream_t s);
 
 }  // namespace snd
