@@ -207,10 +207,15 @@ int snd_train_step(const snd_plan_t* plan, const snd_batch_t* batch,
                    const float* eps, unsigned long long seed,
                    int* step_counter, double* losses, snd_stream_t stream);
 /* Re-launch one kernel of the step on the workspace state left by the last
- * snd_train_step (measurement/profiling): "zzt_dense" (fused zz^T + CE) or
- * "spmm_dxw1" (plain CSR SpMM, width h1). */
+ * snd_train_step (measurement/profiling): "zzt_dense" (fused zz^T + CE),
+ * "spmm_dxw1" (plain CSR SpMM, width h1), "pack" / "dec:<k>" (bf16 decoder
+ * weight packing / k-th decoder kernel, k = 0..10). */
 int snd_plan_launch(const snd_plan_t* plan, const snd_batch_t* batch,
                     void* workspace, const char* kernel, snd_stream_t stream);
+/* Measurement only: bits that make the bf16 decoder kernels skip phases
+ * (1 weight staging, 2 row staging, 4 MFMA, 8 stores, 16 column params,
+ * 32 epilogue prefetch).  0 (default) = normal operation. */
+int snd_debug_set(int flags);
 
 #ifdef __cplusplus
 }

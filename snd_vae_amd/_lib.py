@@ -73,6 +73,7 @@ _SIGS = {
     "snd_plan_buffer": (c_int, [vp, C.c_char_p, C.POINTER(c_ll), C.POINTER(c_ll)]),
     "snd_train_step": (c_int, [vp, C.POINTER(Batch), vp, vp, vp, vp, c_ull, vp, vp, vp]),
     "snd_plan_launch": (c_int, [vp, C.POINTER(Batch), vp, C.c_char_p, vp]),
+    "snd_debug_set": (c_int, [c_int]),
 }
 
 EXPORTS = tuple(_SIGS)

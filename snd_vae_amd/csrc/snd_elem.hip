@@ -3,6 +3,8 @@
 // deterministic slab reduction, TF1 Adam, and the loss finalizer.
 // All memory-bound; each reads its inputs once (HBM roofline).
 #include "snd_elem.hpp"
+
+#include <algorithm>
 #include "snd_gemm.hpp"
 
 namespace snd {
@@ -61,7 +63,9 @@ __global__ void __launch_bounds__(256) reparam_fwd_kernel(ReparamFwdArgs a) {
       const float ls = a.ms[(long long)r * a.ldms + a.L + c];
       const float eps = a.eps_in ? a.eps_in[i] : philox_normal(a.seed, off, (unsigned long long)i);
       const float es = __expf(ls);
-      a.z[i] = mu + eps * es;               // model.py:159
+      const float zv = mu + eps * es;       // model.py:159
+      a.z[i] = zv;
+      if (a.zb) a.zb[(long long)r * a.ldzb + c] = (__bf16)zv;
       if (a.eps_out) a.eps_out[i] = eps;
       kl += (double)(1.f + 2.f * ls - mu * mu - es * es);   // optimizer.py:193
     }
@@ -256,27 +260,42 @@ struct ReducePack {
 
 __global__ void __launch_bounds__(256) reduce_kernel(ReducePack pk) {
   const ReduceDesc& d = pk.d[blockIdx.y];
-  __shared__ double red[4][64];
-  const int col = threadIdx.x & 63, lane = threadIdx.x >> 6;
-  const int i = blockIdx.x * 64 + col;
-  if (blockIdx.x * 64 >= d.len) return;   // uniform per block
-  double a0 = 0.0, a1 = 0.0;
-  if (i < d.len) {
-    const float* src = d.src + i;
-    int p = lane;
-    for (; p + 4 < d.nparts; p += 8) {
-      a0 += (double)src[(long long)p * d.stride];
-      a1 += (double)src[(long long)(p + 4) * d.stride];
+  __shared__ double red[256];
+  const int rows = d.rows > 0 ? d.rows : 1;
+  const long long items = (long long)rows * d.len;
+  const int PL = d.nparts >= 64 ? 16 : 4;        // part lanes
+  const int IPB = 256 / PL;                      // items per block
+  if ((long long)blockIdx.x * IPB >= items) return;   // uniform per block
+  const int it = threadIdx.x % IPB, pl = threadIdx.x / IPB;
+  const long long j = (long long)blockIdx.x * IPB + it;
+  int r = 0, i = 0;
+  double acc = 0.0;
+  if (j < items) {
+    r = (int)(j / d.len);
+    i = (int)(j - (long long)r * d.len);
+    const float* src = d.src + (long long)r * d.src_rs + i;
+    int p = pl;
+    for (; p + 3 * PL < d.nparts; p += 4 * PL) {
+      const float v0 = src[(long long)p * d.stride];
+      const float v1 = src[(long long)(p + PL) * d.stride];
+      const float v2 = src[(long long)(p + 2 * PL) * d.stride];
+      const float v3 = src[(long long)(p + 3 * PL) * d.stride];
+      acc += (double)v0;
+      acc += (double)v1;
+      acc += (double)v2;
+      acc += (double)v3;
     }
-    if (p < d.nparts) a0 += (double)src[(long long)p * d.stride];
+    for (; p < d.nparts; p += PL) acc += (double)src[(long long)p * d.stride];
   }
-  red[lane][col] = a0 + a1;
+  red[threadIdx.x] = acc;
   __syncthreads();
-  if (lane == 0 && i < d.len) {
-    const double acc = red[0][col] + red[1][col] + red[2][col] + red[3][col];
-    float v = (float)(acc * (double)d.scale);
-    if (d.accumulate) v += d.dst[i];
-    d.dst[i] = v;
+  if (pl == 0 && j < items) {
+    double t = 0.0;
+    for (int q = 0; q < PL; ++q) t += red[q * IPB + it];
+    float* dst = d.dst + (long long)r * d.dst_rs + i;
+    float v = (float)(t * (double)d.scale);
+    if (d.accumulate) v += *dst;
+    *dst = v;
   }
 }
 
@@ -406,13 +425,14 @@ int launch_reduce(const ReduceDesc* d, int n, hipStream_t s) {
   for (int base = 0; base < n; base += kMaxReduce) {
     ReducePack pk{};
     const int cnt = n - base < kMaxReduce ? n - base : kMaxReduce;
-    int maxlen = 1;
+    long long gx = 1;
     for (int i = 0; i < cnt; ++i) {
       pk.d[i] = d[base + i];
-      if (pk.d[i].len > maxlen) maxlen = pk.d[i].len;
+      const long long items = (long long)(pk.d[i].rows > 0 ? pk.d[i].rows : 1) * pk.d[i].len;
+      const int ipb = pk.d[i].nparts >= 64 ? 16 : 64;
+      gx = std::max(gx, (items + ipb - 1) / ipb);
     }
-    const int gx = cdiv(maxlen, 64);
-    hipLaunchKernelGGL(reduce_kernel, dim3(gx, cnt), dim3(256), 0, s, pk);
+    hipLaunchKernelGGL(reduce_kernel, dim3((unsigned)gx, cnt), dim3(256), 0, s, pk);
     SND_LAUNCH_CHECK("reduce_kernel");
   }
   return 0;

@@ -9,6 +9,7 @@ struct ReparamFwdArgs {
   const float* eps_in; unsigned long long seed; const int* step;
   float* eps_out; float* z;
   double* kl_part;            // [blocks]
+  __bf16* zb; int ldzb;       // optional bf16 copy of z (fast-path MFMA operand)
 };
 int reparam_blocks(int rows, int L);
 int launch_reparam_fwd(const ReparamFwdArgs& a, hipStream_t s);

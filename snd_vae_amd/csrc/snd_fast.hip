@@ -1,0 +1,865 @@
+// bf16 fast path: packed weight images, the row-tile conv/linear engine and the
+// weight-gradient engine (see snd_fast.hpp).
+//
+// Row engine (model_joint.py:112-145 conv1d k=5 SAME, layers.py:566-576 linear,
+// and their data gradients).  A workgroup owns 128 consecutive rows and ALL
+// output columns: the x rows it needs (128 + 4 halo rows for k=5) are staged
+// once into LDS as bf16 (no 5x im2col re-read), the packed weight image
+// [tap][n][k] is copied in once, and each wave computes 32 rows x N with
+// v_mfma_f32_16x16x32_bf16 as out^T = W^T x^T, so a lane ends up holding 4
+// consecutive output columns of one row (one 16-byte store per row and
+// column group).  Epilogues fuse the bias / frozen-BN / lrelu forward, the
+// BN + lrelu backward of the NEXT layer down (dec_bwd) or of the encoder,
+// and the per-column partial sums the parameter gradients need.
+//
+// Weight-gradient engine: dW[t][k][n] = sum_r x[r+t-2][k] dy[r][n].  x and dy
+// rows are staged row-major; both MFMA operands need k = row, so they are read
+// with ds_read_b64_tr_b16 (gfx950 hardware transpose).  Each workgroup owns a
+// 512-row chunk and a group of (tap, 16-column) pairs, and writes one
+// deterministic partial slab; snd_reduce sums the slabs in a fixed order.
+#include "snd_fast.hpp"
+
+#include <algorithm>
+
+namespace snd {
+
+namespace {
+
+constexpr int NT = 256;
+
+typedef short v4s __attribute__((ext_vector_type(4)));
+typedef short v8s __attribute__((ext_vector_type(8)));
+typedef __attribute__((address_space(3))) v4s lds_v4s;
+
+// 16-byte chunk XOR of a [row][kp] bf16 image read by ds_read_b128 with lane
+// row = l & 15, chunk = 4 ks + (l >> 4) (conflict-free; as the zz^T images).
+__device__ __forceinline__ int swz(int row, int kp) {
+  return kp == 128 ? (row & 15) : (kp == 64 ? ((row >> 1) & 7) : 0);
+}
+
+__device__ __forceinline__ uint4 pack8(float4 lo, float4 hi) {
+  bf16x8 v;
+  v[0] = (__bf16)lo.x; v[1] = (__bf16)lo.y; v[2] = (__bf16)lo.z; v[3] = (__bf16)lo.w;
+  v[4] = (__bf16)hi.x; v[5] = (__bf16)hi.y; v[6] = (__bf16)hi.z; v[7] = (__bf16)hi.w;
+  return __builtin_bit_cast(uint4, v);
+}
+
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, true));
+}
+// sum over the 16 lanes of each DPP row (all lanes receive the row sum)
+__device__ __forceinline__ float row16_sum(float v) {
+  v += dpp_f<0xB1>(v);    // quad_perm [1,0,3,2]
+  v += dpp_f<0x4E>(v);    // quad_perm [2,3,0,1]
+  v += dpp_f<0x141>(v);   // row_half_mirror
+  v += dpp_f<0x140>(v);   // row_mirror
+  return v;
+}
+
+// ---------------------------------------------------------------- pack
+struct PackPack { PackDesc d[kMaxPack]; };
+
+__global__ void __launch_bounds__(NT) pack_kernel(PackPack pk) {
+  const PackDesc& d = pk.d[blockIdx.y];
+  const int kc = d.kp >> 3;
+  const int nch = d.T * d.np * kc;
+  for (int i = blockIdx.x * NT + threadIdx.x; i < nch; i += gridDim.x * NT) {
+    const int c = i % kc, tn = i / kc;
+    const int n = tn % d.np, t = tn / d.np;
+    const int lc = c ^ swz(n, d.kp);          // logical chunk stored at physical chunk c
+    bf16x8 v;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int k = 8 * lc + j;
+      float val = 0.f;
+      for (int si = 0; si < d.nsrc; ++si) {
+        const PackSrc& s = d.s[si];
+        int aa, bb, tt;
+        if (s.mode == 0) { bb = n - s.n_off + s.b0; aa = k - s.k_off + s.a0; tt = t; }
+        else { aa = n - s.n_off + s.a0; bb = k - s.k_off + s.b0; tt = d.T - 1 - t; }
+        if (aa >= s.a0 && aa < s.a1 && bb >= s.b0 && bb < s.b1)
+          val = s.w[((long long)tt * s.A + aa) * s.B + bb];
+      }
+      v[j] = (__bf16)val;
+    }
+    *reinterpret_cast<bf16x8*>(d.dst + ((long long)(t * d.np + n) * d.kp + 8 * c)) = v;
+  }
+}
+
+// ---------------------------------------------------------------- row engine
+typedef __attribute__((address_space(1))) const void* gptr_t;
+typedef __attribute__((address_space(3))) void* lptr_t;
+
+// one 16-byte LDS-DMA per lane: LDS destination = wave-uniform base + 16 * lane
+__device__ __forceinline__ void glds16(const void* g, void* lds_base) {
+  __builtin_amdgcn_global_load_lds((gptr_t)g, (lptr_t)lds_base, 16, 0, 0);
+}
+
+__device__ __forceinline__ int rc_xchunks(int T, int lkc) {
+  return (((kRcRows + T - 1) << lkc) + 63) & ~63;   // whole 1 KB pieces
+}
+
+// 16 waves: wave w owns rows 16 (w & 7) .. +15 of the 128-row tile and the
+// column blocks [NBH (w >> 3), NBH (w >> 3) + NBH) of the output.
+constexpr int RCT = 1024;
+
+template <int EPI> struct RcNcp { static constexpr int v = 0; };
+template <> struct RcNcp<RC_LIN> { static constexpr int v = 1; };
+template <> struct RcNcp<RC_DECBWD> { static constexpr int v = 3; };
+template <> struct RcNcp<RC_ENC1> { static constexpr int v = 4; };
+template <> struct RcNcp<RC_ENC0> { static constexpr int v = 2; };
+
+template <int EPI, int NBH>
+__global__ void __launch_bounds__(RCT) rowconv_kernel(RcArgs a) {
+  extern __shared__ __attribute__((aligned(16))) __bf16 lds[];
+  __shared__ __attribute__((aligned(16))) float cps[8][RcNcp<EPI>::v > 0 ? RcNcp<EPI>::v : 1][128];
+  __shared__ float colp[8][128];   // bias, gamma*c, beta, g2*c | W0 rows, b2 per physical column
+  constexpr int NCP = RcNcp<EPI>::v;
+  const int T = a.T, H = (T - 1) >> 1, kp = a.kp, np = a.np;
+  const int lkc = kp == 128 ? 4 : (kp == 64 ? 3 : 2);   // log2(kp / 8)
+  const int XR = kRcRows + T - 1;
+  const int xch = rc_xchunks(T, lkc);
+  __bf16* xs = lds;
+  __bf16* ws = lds + (xch << 3);
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int li = lane & 15, lg = lane >> 4;
+  const int rb = w & 7, nb0 = NBH * (w >> 3);
+  const int r0 = blockIdx.x * kRcRows;
+  const int rend = min(r0 + kRcRows, a.R);
+  const int nbc = np >> 4;
+  const bool use_cp = NCP > 0 && a.colpart != nullptr;
+
+  // ---- packed weight image (LDS-DMA, 1 KB per wave instruction)
+  if (!(a.dbg & 1)) {
+    const int npc = (T * np * kp) >> 9;
+    const char* g = reinterpret_cast<const char*>(a.wpk) + lane * 16;
+    for (int j = w; j < npc; j += RCT / 64) glds16(g + (j << 10), reinterpret_cast<char*>(ws) + (j << 10));
+  }
+  // ---- per-column parameters
+  if (tid < np) {
+    const int n = tid;
+    const bool cv = n < a.N && a.cols.valid(n) && !(a.dbg & 16);
+    const bool pa = n < a.cols.a;
+    const int ia = pa ? n : a.cols.logical(n), ib = n - a.cols.offb;
+    auto par = [&](const float* A, const float* Bv) {
+      return !cv || !A ? 0.f : (pa || !Bv ? A[ia] : Bv[ib]);
+    };
+    colp[0][n] = par(a.bias, a.bias_b);
+    colp[1][n] = par(a.gamma, a.gamma_b) * kBnC;
+    colp[2][n] = par(a.beta, a.beta_b);
+    if constexpr (EPI == RC_ENC1) {
+      colp[3][n] = (cv && n < a.h) ? a.g2[n] * kBnC : 0.f;
+      colp[4][n] = (cv && n < a.h) ? a.b2[n] : 0.f;
+    }
+    if constexpr (EPI == RC_ENC0) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) colp[3 + k][n] = (cv && k < a.f) ? a.w0[k * a.N + n] : 0.f;
+    }
+  }
+
+  unsigned cvm[NBH];
+#pragma unroll
+  for (int i = 0; i < NBH; ++i) {
+    cvm[i] = 0u;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int n = 16 * (nb0 + i) + 4 * lg + e;
+      if (nb0 + i < nbc && n < a.N && a.cols.valid(n)) cvm[i] |= 1u << e;
+    }
+  }
+  // per-lane LDS offsets (elements): weight rows n = 16 nb + li share the swizzle of li
+  const int wsw = swz(li, kp);
+
+  int s0 = r0;
+  bool first = true;
+  while (s0 < rend) {
+    int glo, ghi, s1;
+    if (T == 1) {
+      glo = r0; ghi = rend; s1 = rend;
+    } else {
+      const int gs = (s0 / a.npg) * a.npg;
+      glo = gs; ghi = min(a.R, gs + a.npg); s1 = min(rend, ghi);
+    }
+    if (!first) __syncthreads();
+    // ---- x rows [r0 - H, r0 - H + XR), zero outside [glo, ghi)
+    if (!(a.dbg & 2)) {
+      const int kc = 1 << lkc;
+      for (int j = w; j < (xch >> 6); j += RCT / 64) {
+        const int q = (j << 6) + lane;
+        const int row = q >> lkc, pc = q & (kc - 1);
+        const int c = pc ^ swz(row, kp);
+        const int gr = r0 - H + row;
+        const bool v = row < XR && gr >= glo && gr < ghi && 8 * c < a.K;
+        const void* g = v ? (const void*)(reinterpret_cast<const __bf16*>(a.x) + (long long)gr * a.ldx + 8 * c)
+                          : (const void*)a.zero;
+        glds16(g, reinterpret_cast<char*>(xs) + (j << 10));
+      }
+    }
+    // ---- epilogue operands fetched while the staging DMA is in flight
+    const int r = r0 + 16 * rb + li;
+    const bool rv = r >= s0 && r < s1;
+    f32x4 ypf[NBH];
+#pragma unroll
+    for (int i = 0; i < NBH; ++i) ypf[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if constexpr (EPI == RC_DECBWD || EPI == RC_ENC1) {
+      if (rv && !(a.dbg & 32)) {
+#pragma unroll
+        for (int i = 0; i < NBH; ++i) {
+          const int n0 = 16 * (nb0 + i) + 4 * lg;
+          if constexpr (EPI == RC_DECBWD) {
+            const float* yp = a.y + (long long)r * a.ldy + n0;
+            if (cvm[i] == 15u) ypf[i] = *reinterpret_cast<const f32x4*>(yp);
+            else
+#pragma unroll
+              for (int e = 0; e < 4; ++e) if (cvm[i] >> e & 1u) ypf[i][e] = yp[e];
+          } else {   // ENC1: P1 for the B1 part, X for the feature part
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const int n = n0 + e;
+              if (cvm[i] >> e & 1u)
+                ypf[i][e] = n < a.h ? a.p[(long long)r * a.ldp + n] : a.xf[(long long)r * a.ldxf + (n - a.h)];
+            }
+          }
+        }
+      }
+    }
+    float ax[4] = {0.f, 0.f, 0.f, 0.f};
+    if constexpr (EPI == RC_ENC0) {
+      if (rv)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) if (k < a.f) ax[k] = a.p[(long long)r * a.ldp + k];
+    }
+    __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): staging DMA landed
+    __syncthreads();
+
+    f32x4 acc[NBH];
+#pragma unroll
+    for (int i = 0; i < NBH; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int kcs = (a.dbg & 4) ? 0 : kp >> 5;
+    for (int t = 0; t < T; ++t) {
+      const int xrow = 16 * rb + li + t;
+      const __bf16* xrp = xs + xrow * kp;
+      const int xsw = swz(xrow, kp);
+      const __bf16* wrp = ws + (t * np + li) * kp;
+      for (int ks = 0; ks < kcs; ++ks) {
+        const int ch = 4 * ks + lg;
+        const bf16x8 bx = *reinterpret_cast<const bf16x8*>(xrp + ((ch ^ xsw) << 3));
+#pragma unroll
+        for (int i = 0; i < NBH; ++i) {
+          if (nb0 + i < nbc) {
+            const bf16x8 aw = *reinterpret_cast<const bf16x8*>(
+                wrp + 16 * (nb0 + i) * kp + ((ch ^ wsw) << 3));
+            acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aw, bx, acc[i], 0, 0, 0);
+          }
+        }
+      }
+    }
+
+    // ---- epilogue: lane holds row r, columns 16 nb + 4 lg + e
+#pragma unroll
+    for (int i = 0; i < NBH; ++i) {
+      const int nb = nb0 + i;
+      if (nb >= nbc) continue;
+      const int n0 = 16 * nb + 4 * lg;
+      const unsigned cm = rv ? cvm[i] : 0u;
+      float o[4], qs[NCP > 0 ? NCP : 1][4];
+#pragma unroll
+      for (int q = 0; q < (NCP > 0 ? NCP : 1); ++q)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) qs[q][e] = 0.f;
+      const float4 bia = *reinterpret_cast<const float4*>(&colp[0][n0]);
+      const float4 gam = *reinterpret_cast<const float4*>(&colp[1][n0]);
+      const float4 bet = *reinterpret_cast<const float4*>(&colp[2][n0]);
+      const float bi[4] = {bia.x, bia.y, bia.z, bia.w};
+      const float ga[4] = {gam.x, gam.y, gam.z, gam.w};
+      const float be[4] = {bet.x, bet.y, bet.z, bet.w};
+      unsigned sm = cm;    // columns stored
+      if constexpr (EPI == RC_LIN) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) { o[e] = acc[i][e] + bi[e]; qs[0][e] = (cm >> e & 1u) ? o[e] : 0.f; }
+      } else if constexpr (EPI == RC_FWD) {
+        float yv[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) { yv[e] = acc[i][e] + bi[e]; o[e] = lrelu(yv[e] * ga[e] + be[e]); }
+        float* yp = a.y + (long long)r * a.ldy + n0;
+        if (a.dbg & 8) {
+        } else if (cm == 15u) *reinterpret_cast<float4*>(yp) = make_float4(yv[0], yv[1], yv[2], yv[3]);
+        else
+#pragma unroll
+          for (int e = 0; e < 4; ++e) if (cm >> e & 1u) yp[e] = yv[e];
+      } else if constexpr (EPI == RC_DECBWD) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float yv = ypf[i][e];
+          const float dt = (cm >> e & 1u) ? acc[i][e] * lrelu_grad(yv * ga[e] + be[e]) : 0.f;
+          o[e] = dt * ga[e];
+          qs[0][e] = dt * yv;
+          qs[1][e] = dt;
+          qs[2][e] = o[e];
+        }
+      } else if constexpr (EPI == RC_ENC1) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int n = n0 + e;
+          const bool ok = cm >> e & 1u;
+          const float dg = ok ? acc[i][e] : 0.f;
+          const bool bpart = n < a.h;
+          const float pv = ypf[i][e];
+          const float a1 = lrelu(pv);
+          const float x2 = bpart ? a1 * colp[3][n] + colp[4][n] : pv;
+          qs[0][e] = dg * x2;
+          qs[1][e] = dg;
+          const float dh2 = dg * ga[e];
+          o[e] = 0.f;
+          qs[2][e] = 0.f;
+          qs[3][e] = 0.f;
+          if (bpart) {
+            qs[2][e] = dh2 * a1;
+            qs[3][e] = dh2;
+            o[e] = dh2 * colp[3][n] * lrelu_grad(pv);
+          } else {
+            sm &= ~(1u << e);
+          }
+        }
+      } else {  // RC_ENC0: P0 = AX W0 recomputed (f <= 4)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float pv = 0.f;
+#pragma unroll
+          for (int k = 0; k < 4; ++k) pv += ax[k] * colp[3 + k][n0 + e];
+          const float db = (cm >> e & 1u) ? acc[i][e] : 0.f;
+          qs[0][e] = db * lrelu(pv);
+          qs[1][e] = db;
+          o[e] = db * ga[e] * lrelu_grad(pv);
+        }
+      }
+      if (a.dbg & 8) sm = 0u;
+      if (a.out_bf16) {
+        __bf16* op = reinterpret_cast<__bf16*>(a.out) + (long long)r * a.ldo + n0;
+        if (sm == 15u) {
+          bf16x4 v4;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v4[e] = (__bf16)o[e];
+          *reinterpret_cast<bf16x4*>(op) = v4;
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) if (sm >> e & 1u) op[e] = (__bf16)o[e];
+        }
+      } else {
+        float* op = reinterpret_cast<float*>(a.out) + (long long)r * a.ldo + n0;
+        if (sm == 15u) *reinterpret_cast<float4*>(op) = make_float4(o[0], o[1], o[2], o[3]);
+        else
+#pragma unroll
+          for (int e = 0; e < 4; ++e) if (sm >> e & 1u) op[e] = o[e];
+      }
+      if constexpr (NCP > 0) {
+        if (use_cp) {
+#pragma unroll
+          for (int q = 0; q < NCP; ++q) {
+            float v[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] = row16_sum(qs[q][e]);
+            if (li == 0) {
+              float4* cp = reinterpret_cast<float4*>(&cps[rb][q][n0]);
+              if (first) *cp = make_float4(v[0], v[1], v[2], v[3]);
+              else { float4 o4 = *cp; o4.x += v[0]; o4.y += v[1]; o4.z += v[2]; o4.w += v[3]; *cp = o4; }
+            }
+          }
+        }
+      }
+    }
+    s0 = s1;
+    first = false;
+  }
+  if constexpr (NCP > 0) {
+    if (use_cp) {
+      __syncthreads();
+      for (int i = tid; i < NCP * a.N; i += RCT) {
+        const int q = i / a.N, n = i - q * a.N;
+        float t = 0.f;
+#pragma unroll
+        for (int b = 0; b < 8; ++b) t += cps[b][q][n];
+        a.colpart[(long long)blockIdx.x * NCP * a.N + i] = t;
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------- wgrad
+__device__ __forceinline__ bf16x8 tr_pair(const __bf16* p0, const __bf16* p1) {
+  const v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(p0));
+  const v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(p1));
+  const v8s c = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+  return __builtin_bit_cast(bf16x8, c);
+}
+
+// 16-byte chunk XOR of the [row][kp] images read with ds_read_b64_tr_b16: the
+// 8 rows one 32-lane half reads (8g + q, g = 0, 1) land on disjoint banks.
+__device__ __forceinline__ int trsw(int row, int kp) {
+  return kp == 128 ? (((row & 3) << 1) | (row & 8))
+                   : (kp == 64 ? ((row & 2) | ((row & 8) >> 1)) : (((row >> 3) & 1) << 1));
+}
+__device__ __forceinline__ int log2kc(int kp) { return kp == 128 ? 4 : (kp == 64 ? 3 : 2); }
+
+// LDS-DMA rows [base, base + nrows) of a bf16 [R][ld] operand into a swizzled
+// [row][kp] image; rows outside [vlo, vhi) and chunks at col >= K read zeros.
+__device__ __forceinline__ void stage_tr_image(const __bf16* src, int ld, int K, int base, int nrows,
+                                               int vlo, int vhi, int kp, __bf16* dst,
+                                               const void* zero) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int lk = log2kc(kp), kc = 1 << lk;
+  const int npc = ((nrows << lk) + 63) >> 6;
+  for (int j = w; j < npc; j += 4) {
+    const int q = (j << 6) + lane;
+    const int row = q >> lk, pc = q & (kc - 1);
+    const int c = pc ^ trsw(row, kp);
+    const int gr = base + row;
+    const bool v = row < nrows && gr >= vlo && gr < vhi && 8 * c < K;
+    const void* g = v ? (const void*)(src + (long long)gr * ld + 8 * c) : zero;
+    glds16(g, reinterpret_cast<char*>(dst) + (j << 10));
+  }
+}
+
+// element offset of the 8-byte tr-read piece at (row, col = 16 cb + 4 p)
+__device__ __forceinline__ int tr_off(int row, int col, int kp) {
+  const int c = col >> 3;
+  return row * kp + (((c ^ trsw(row, kp)) << 3) | (col & 4));
+}
+
+constexpr int WGT = 1024;   // 16 waves; wave w owns the (tap, 16-col k block) pair pg0 + w
+
+struct WgUnit { int sub, s0, s1, glo, ghi; };
+
+__device__ __forceinline__ WgUnit wg_unit(const WgArgs& a, int sub, int s0, int c1) {
+  const int send = min(c1, sub + kRcRows);
+  WgUnit u;
+  u.sub = sub; u.s0 = s0;
+  if (a.T == 1) { u.glo = sub; u.ghi = send; u.s1 = send; }
+  else {
+    const int gs = (s0 / a.npg) * a.npg;
+    u.glo = gs; u.ghi = min(a.R, gs + a.npg); u.s1 = min(send, u.ghi);
+  }
+  return u;
+}
+
+template <int NBO>
+__global__ void __launch_bounds__(WGT) wgrad_kernel(WgArgs a) {
+  extern __shared__ __attribute__((aligned(16))) __bf16 lds[];
+  const int T = a.T, H = (T - 1) >> 1;
+  const int XR = kRcRows + T - 1;
+  const int kpx = a.K <= 32 ? 32 : (a.K <= 64 ? 64 : 128);
+  const int kpy = a.N <= 32 ? 32 : (a.N <= 64 ? 64 : 128);
+  const int xch = ((XR << log2kc(kpx)) + 63) & ~63;
+  const int bufe = (xch << 3) + kRcRows * kpy;          // elements per staging buffer
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int li = lane & 15, lg = lane >> 4, tq = li >> 2, tp = li & 3;
+  const int cbn = (a.K + 15) >> 4;
+  const int P = T * cbn;
+  const int p = blockIdx.y * a.pairs_per_wg + w;
+  const bool pv = w < a.pairs_per_wg && p < P;
+  const int t = pv ? p / cbn : 0, cb = pv ? p - t * cbn : 0;
+
+  f32x4 acc[NBO];
+#pragma unroll
+  for (int j = 0; j < NBO; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const __bf16* xg = reinterpret_cast<const __bf16*>(a.x);
+  const __bf16* dg = reinterpret_cast<const __bf16*>(a.dy);
+  const int c0 = blockIdx.x * a.rows_per_wg, c1 = min(a.R, c0 + a.rows_per_wg);
+  auto stage = [&](const WgUnit& u, int b) {
+    if (a.dbg & 2) return;
+    __bf16* xs = lds + b * bufe;
+    __bf16* ds = xs + (xch << 3);
+    // wave-strided LDS-DMA over the 16 waves
+    const int lkx = log2kc(kpx), lky = log2kc(kpy);
+    const int npx = xch >> 6, npy = (kRcRows << lky) >> 6;
+    for (int j = w; j < npx + npy; j += WGT / 64) {
+      const bool isx = j < npx;
+      const int jj = isx ? j : j - npx;
+      const int lk = isx ? lkx : lky, kp = isx ? kpx : kpy;
+      const int q = (jj << 6) + lane;
+      const int row = q >> lk, pc = q & ((1 << lk) - 1);
+      const int c = pc ^ trsw(row, kp);
+      const void* g = a.zero;
+      if (isx) {
+        const int gr = u.sub - H + row;
+        if (row < XR && gr >= u.glo && gr < u.ghi && 8 * c < a.K) g = xg + (long long)gr * a.ldx + 8 * c;
+      } else {
+        const int gr = u.sub + row;
+        if (gr >= u.s0 && gr < u.s1 && 8 * c < a.N) g = dg + (long long)gr * a.lddy + 8 * c;
+      }
+      glds16(g, reinterpret_cast<char*>(isx ? xs : ds) + (jj << 10));
+    }
+  };
+
+  // per-lane tr-read offsets (elements) at k-step 0
+  const int rk0 = 8 * lg + tq;
+  const int xoff = tr_off(rk0 + t, 16 * cb + 4 * tp, kpx);
+  const int xoff2 = tr_off(rk0 + t + 4, 16 * cb + 4 * tp, kpx);   // + t may carry into bit 3
+  const int doff = rk0 * kpy;
+  int dobo[NBO];
+#pragma unroll
+  for (int ob = 0; ob < NBO; ++ob) dobo[ob] = tr_off(rk0, 16 * ob + 4 * tp, kpy) - doff;
+  if (c0 < c1) {
+    WgUnit u = wg_unit(a, c0, c0, c1);
+    stage(u, 0);
+    for (int k = 0;; ++k) {
+      __builtin_amdgcn_s_waitcnt(0x0F70);
+      __syncthreads();
+      // next unit: next graph segment of this 128-row block, else the next block
+      int nsub = u.sub, ns0 = u.s1;
+      if (ns0 >= min(c1, u.sub + kRcRows)) { nsub = u.sub + kRcRows; ns0 = nsub; }
+      const bool more = nsub < c1;
+      WgUnit un{};
+      if (more) { un = wg_unit(a, nsub, ns0, c1); stage(un, (k + 1) & 1); }
+      const __bf16* xs = lds + (k & 1) * bufe;
+      const __bf16* ds = xs + (xch << 3);
+      if (!(a.dbg & 4) && pv) {
+        // the tr-read swizzle of rows rk, rk + 4, rk + 32 j (+ t) is the same: offsets
+        // advance by constants across the 4 k-steps
+#pragma unroll
+        for (int ks = 0; ks < kRcRows / 32; ++ks) {
+          const __bf16* xb = xs + 32 * ks * kpx;
+          const __bf16* db = ds + doff + 32 * ks * kpy;
+          const bf16x8 bx = tr_pair(xb + xoff, xb + xoff2);
+#pragma unroll
+          for (int ob = 0; ob < NBO; ++ob) {
+            const bf16x8 af = tr_pair(db + dobo[ob], db + dobo[ob] + 4 * kpy);
+            acc[ob] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bx, acc[ob], 0, 0, 0);
+          }
+        }
+      }
+      if (!more) break;
+      u = un;
+    }
+  }
+  // D[m = n (dy col)][n = k (x col)]: lane holds k = 16cb + li, n = 16ob + 4lg + e
+  if ((a.dbg & 8) || !pv) return;
+  const int k = 16 * cb + li;
+  if (k >= a.K) return;
+  float* row = a.slab + (long long)blockIdx.x * T * a.K * a.N + ((long long)t * a.K + k) * a.N;
+#pragma unroll
+  for (int ob = 0; ob < NBO; ++ob) {
+    const int n0 = 16 * ob + 4 * lg;
+    if ((a.N & 3) == 0 && n0 + 3 < a.N) {
+      *reinterpret_cast<float4*>(row + n0) = make_float4(acc[ob][0], acc[ob][1], acc[ob][2], acc[ob][3]);
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) if (n0 + e < a.N) row[n0 + e] = acc[ob][e];
+    }
+  }
+}
+
+// ---------------------------------------------------------------- heads
+struct HeadFastPack { HeadFastArgs h[2]; };
+
+template <int CIN, int COUT>
+__device__ __forceinline__ void head_rows(const HeadFastArgs& h, int R) {
+  constexpr int NQ = CIN * COUT + COUT + 3 * CIN;
+  __shared__ float red[16][NQ];
+  __shared__ double sred[4];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int r = blockIdx.x * kHeadFastRows + tid;
+  const bool rv = r < R;
+  float wv[CIN][COUT], bv[COUT], gk[CIN], bk[CIN];
+#pragma unroll
+  for (int k = 0; k < CIN; ++k) {
+#pragma unroll
+    for (int o = 0; o < COUT; ++o) wv[k][o] = h.w[k * COUT + o];
+    gk[k] = h.gamma[k] * kBnC;
+    bk[k] = h.beta[k];
+  }
+#pragma unroll
+  for (int o = 0; o < COUT; ++o) bv[o] = h.b[o];
+  float u[CIN], yv[CIN];
+#pragma unroll
+  for (int k = 0; k < CIN; ++k) { u[k] = 0.f; yv[k] = 0.f; }
+  if (rv) {
+    if (h.u_bf16) {
+      const __bf16* up = reinterpret_cast<const __bf16*>(h.u) + (long long)r * h.ldu;
+#pragma unroll
+      for (int c = 0; c < (CIN + 7) / 8; ++c) {
+        const bf16x8 v = *reinterpret_cast<const bf16x8*>(up + 8 * c);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) if (8 * c + j < CIN) u[8 * c + j] = (float)v[j];
+      }
+    } else {
+      const float* up = reinterpret_cast<const float*>(h.u) + (long long)r * h.ldu;
+#pragma unroll
+      for (int c = 0; c < (CIN + 3) / 4; ++c) {
+        const float4 v = *reinterpret_cast<const float4*>(up + 4 * c);
+        const float vv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) if (4 * c + j < CIN) u[4 * c + j] = vv[j];
+      }
+    }
+    const float* yp = h.y + (long long)r * h.ldy;
+#pragma unroll
+    for (int c = 0; c < (CIN + 3) / 4; ++c) {
+      const float4 v = *reinterpret_cast<const float4*>(yp + 4 * c);
+      const float vv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) if (4 * c + j < CIN) yv[4 * c + j] = vv[j];
+    }
+  }
+  // head forward + MSE + d/dz (optimizer.py:149,153; model_joint.py:121,144)
+  float tg[COUT];
+#pragma unroll
+  for (int o = 0; o < COUT; ++o) tg[o] = rv ? h.target[(long long)r * h.ldt + o] : 0.f;
+  float dp[COUT];
+  double sse = 0.0;
+#pragma unroll
+  for (int o = 0; o < COUT; ++o) {
+    float zo = bv[o];
+#pragma unroll
+    for (int k = 0; k < CIN; ++k) zo += u[k] * wv[k][o];
+    const float yh = 1.f / (1.f + __expf(-zo));
+    const float diff = yh - tg[o];
+    if (rv) {
+      if (h.yhat) h.yhat[(long long)r * COUT + o] = yh;
+      sse += (double)diff * diff;
+    }
+    dp[o] = rv ? 2.f * diff / h.count * yh * (1.f - yh) : 0.f;
+  }
+  // du -> BN/lrelu backward of U's layer -> dy (bf16)
+  float dt[CIN], dyv[CIN];
+#pragma unroll
+  for (int k = 0; k < CIN; ++k) {
+    float du = 0.f;
+#pragma unroll
+    for (int o = 0; o < COUT; ++o) du += dp[o] * wv[k][o];
+    dt[k] = du * lrelu_grad(yv[k] * gk[k] + bk[k]);
+    dyv[k] = dt[k] * gk[k];
+  }
+  if (rv) {
+    __bf16* dq = h.dy + (long long)r * h.lddy;
+#pragma unroll
+    for (int c = 0; c < CIN / 4; ++c) {
+      bf16x4 v;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[j] = (__bf16)dyv[4 * c + j];
+      *reinterpret_cast<bf16x4*>(dq + 4 * c) = v;
+    }
+#pragma unroll
+    for (int k = (CIN / 4) * 4; k < CIN; ++k) dq[k] = (__bf16)dyv[k];
+  }
+  // per-block partial sums: DPP row sums, then the 16 (wave, row) groups
+  const int grp = 4 * w + (lane >> 4);
+  auto put = [&](int q, float v) {
+    v = row16_sum(v);
+    if ((lane & 15) == 0) red[grp][q] = v;
+  };
+#pragma unroll
+  for (int k = 0; k < CIN; ++k)
+#pragma unroll
+    for (int o = 0; o < COUT; ++o) put(k * COUT + o, u[k] * dp[o]);
+#pragma unroll
+  for (int o = 0; o < COUT; ++o) put(CIN * COUT + o, dp[o]);
+  constexpr int QB = CIN * COUT + COUT;
+#pragma unroll
+  for (int k = 0; k < CIN; ++k) {
+    put(QB + k, dt[k] * yv[k]);
+    put(QB + CIN + k, dt[k]);
+    put(QB + 2 * CIN + k, dyv[k]);
+  }
+  const double wsum = wave_sum_d(sse);
+  if (lane == 0) sred[w] = wsum;
+  __syncthreads();
+  for (int q = tid; q < NQ; q += NT) {
+    float t = 0.f;
+#pragma unroll
+    for (int g = 0; g < 16; ++g) t += red[g][q];
+    h.part[(long long)blockIdx.x * NQ + q] = t;
+  }
+  if (tid == 0) h.sse[blockIdx.x] = sred[0] + sred[1] + sred[2] + sred[3];
+}
+
+__global__ void __launch_bounds__(NT) heads_fast_kernel(HeadFastPack pk, int R) {
+  const HeadFastArgs& h = pk.h[blockIdx.y];
+  if (h.cin == 10 && h.cout == 2) head_rows<10, 2>(h, R);
+  else if (h.cin == 20 && h.cout == 1) head_rows<20, 1>(h, R);
+}
+
+template <int EPI>
+int rc_launch_epi(const RcArgs& a, hipStream_t s) {
+  const size_t lds = rc_lds_bytes(a.T, a.kp, a.np);
+  const dim3 grid(rc_blocks(a.R)), block(RCT);
+  switch ((a.np / 16 + 1) / 2) {
+    case 1: hipLaunchKernelGGL((rowconv_kernel<EPI, 1>), grid, block, lds, s, a); break;
+    case 2: hipLaunchKernelGGL((rowconv_kernel<EPI, 2>), grid, block, lds, s, a); break;
+    case 3: hipLaunchKernelGGL((rowconv_kernel<EPI, 3>), grid, block, lds, s, a); break;
+    default: hipLaunchKernelGGL((rowconv_kernel<EPI, 4>), grid, block, lds, s, a); break;
+  }
+  SND_LAUNCH_CHECK("rowconv_kernel");
+  return 0;
+}
+
+int kp_img(int k) { return k <= 32 ? 32 : (k <= 64 ? 64 : 128); }
+size_t wg_lds_bytes(int T, int K, int N) {
+  const int kpx = kp_img(K), kpy = kp_img(N);
+  const size_t xch = round_up((long long)(kRcRows + T - 1) * (kpx / 8), 64);
+  return 2 * (xch * 8 + (size_t)kRcRows * kpy) * 2;   // double-buffered
+}
+
+template <int NBO>
+int wg_launch(const WgArgs& a, dim3 grid, hipStream_t s) {
+  hipLaunchKernelGGL((wgrad_kernel<NBO>), grid, dim3(WGT), wg_lds_bytes(a.T, a.K, a.N), s, a);
+  SND_LAUNCH_CHECK("wgrad_kernel");
+  return 0;
+}
+
+constexpr size_t kMaxDynLds = kRcLdsLimit;
+
+}  // namespace
+
+size_t pack_bytes(int T, int kp, int np) { return (size_t)T * kp * np * 2; }
+
+int launch_pack(const PackDesc* d, int n, hipStream_t s) {
+  if (n < 1 || n > kMaxPack) { set_error("pack: 1..%d descriptors", kMaxPack); return SND_ERR_ARG; }
+  PackPack pk{};
+  int maxch = 0;
+  for (int i = 0; i < n; ++i) {
+    const PackDesc& x = d[i];
+    if (!(x.kp == 32 || x.kp == 64 || x.kp == 128) || x.np % 16 || x.np <= 0 || x.T < 1 ||
+        x.nsrc < 1 || x.nsrc > 2) {
+      set_error("pack: bad descriptor %d (kp %d np %d T %d)", i, x.kp, x.np, x.T);
+      return SND_ERR_ARG;
+    }
+    pk.d[i] = x;
+    maxch = std::max(maxch, x.T * x.np * x.kp / 8);
+  }
+  dim3 grid(cdiv(maxch, NT), n);
+  hipLaunchKernelGGL(pack_kernel, grid, dim3(NT), 0, s, pk);
+  SND_LAUNCH_CHECK("pack_kernel");
+  return 0;
+}
+
+int rc_blocks(int R) { return cdiv(R, kRcRows); }
+
+int heads_fast_blocks(int R) { return cdiv(R, kHeadFastRows); }
+bool heads_fast_supported(int cin, int cout) { return (cin == 10 && cout == 2) || (cin == 20 && cout == 1); }
+int heads_fast_parts(int cin, int cout) { return cin * cout + cout + 3 * cin; }
+
+int launch_heads_fast(const HeadFastArgs* h, int n, int R, hipStream_t s) {
+  if (n < 1 || n > 2) { set_error("heads_fast: 1 or 2 heads"); return SND_ERR_ARG; }
+  HeadFastPack pk{};
+  for (int i = 0; i < n; ++i) {
+    const HeadFastArgs& x = h[i];
+    SND_CHECK_ARG(heads_fast_supported(x.cin, x.cout), "heads_fast: (cin, cout) = (%d, %d) not built",
+                  x.cin, x.cout);
+    SND_CHECK_ARG(x.ldu >= (int)round_up(x.cin, x.u_bf16 ? 8 : 4) && x.ldy >= (int)round_up(x.cin, 4) &&
+                      x.ldu % (x.u_bf16 ? 8 : 4) == 0 && x.ldy % 4 == 0,
+                  "heads_fast: padded leading dims required");
+    SND_CHECK_ARG(x.u && x.y && x.gamma && x.beta && x.w && x.b && x.target && x.dy && x.part && x.sse,
+                  "heads_fast: null operand");
+    pk.h[i] = x;
+  }
+  if (R <= 0) return 0;
+  hipLaunchKernelGGL(heads_fast_kernel, dim3(heads_fast_blocks(R), n), dim3(NT), 0, s, pk, R);
+  SND_LAUNCH_CHECK("heads_fast_kernel");
+  return 0;
+}
+
+size_t rc_lds_bytes(int T, int kp, int np) {
+  const size_t xch = round_up((long long)(kRcRows + T - 1) * (kp / 8), 64);
+  return (xch * 8 + (size_t)T * np * kp) * 2;
+}
+
+int launch_rowconv(const RcArgs& a, int epi, hipStream_t s) {
+  if (a.R <= 0) return 0;
+  SND_CHECK_ARG(a.T == 1 || a.T == 5, "rowconv: T must be 1 or 5");
+  SND_CHECK_ARG(a.kp == 32 || a.kp == 64 || a.kp == 128, "rowconv: kp %d", a.kp);
+  SND_CHECK_ARG(a.np % 16 == 0 && a.np >= 16 && a.np <= 128, "rowconv: np %d", a.np);
+  SND_CHECK_ARG(a.K <= a.kp && a.N <= a.np && a.N > 0, "rowconv: K %d / N %d exceed image", a.K, a.N);
+  SND_CHECK_ARG(a.ldx % 8 == 0 && a.ldo % 4 == 0, "rowconv: ldx %% 8 / ldo %% 4");
+  SND_CHECK_ARG(rc_lds_bytes(a.T, a.kp, a.np) <= kMaxDynLds, "rowconv: LDS image too large");
+  SND_CHECK_ARG(a.x && a.wpk && a.out && a.zero && a.x_bf16, "rowconv: null operand / fp32 x");
+  SND_CHECK_ARG(!a.colpart || (a.ncp >= 1 && a.ncp <= 4), "rowconv: ncp");
+  SND_CHECK_ARG(a.npg > 0, "rowconv: npg");
+  switch (epi) {
+    case RC_LIN: return rc_launch_epi<RC_LIN>(a, s);
+    case RC_FWD:
+      SND_CHECK_ARG(a.y && a.bias && a.gamma && a.beta && a.ldy % 4 == 0, "rowconv fwd: BN operands");
+      return rc_launch_epi<RC_FWD>(a, s);
+    case RC_DECBWD:
+      SND_CHECK_ARG(a.y && a.gamma && a.beta && a.ldy % 4 == 0, "rowconv decbwd: BN operands");
+      return rc_launch_epi<RC_DECBWD>(a, s);
+    case RC_ENC1:
+      SND_CHECK_ARG(a.p && a.xf && a.gamma && a.g2 && a.b2 && a.h % 4 == 0, "rowconv enc1 operands");
+      return rc_launch_epi<RC_ENC1>(a, s);
+    case RC_ENC0:
+      SND_CHECK_ARG(a.p && a.w0 && a.gamma && a.f <= 4, "rowconv enc0 operands");
+      return rc_launch_epi<RC_ENC0>(a, s);
+    default: set_error("rowconv: bad epilogue %d", epi); return SND_ERR_ARG;
+  }
+}
+
+WgGeom wgrad_geom(int R, int T, int K, int N) {
+  WgGeom g{};
+  const int P = T * cdiv(K, 16);
+  g.pairs_per_wg = std::min(P, WGT / 64);
+  g.gy = cdiv(P, g.pairs_per_wg);
+  // row chunks: about 256 workgroups in all, but at most 64 slabs of a large weight
+  int gx = std::max(1, 256 / g.gy);
+  if ((long long)T * K * N >= 65536) gx = std::min(gx, 64);   // bound the slab traffic
+  g.rows_per_wg = (int)round_up(cdiv(R, gx), kRcRows);
+  g.gx = cdiv(R, g.rows_per_wg);
+  return g;
+}
+
+int launch_wgrad(const WgArgs& a, hipStream_t s) {
+  if (a.R <= 0) return 0;
+  SND_CHECK_ARG(a.T == 1 || a.T == 5, "wgrad: T must be 1 or 5");
+  SND_CHECK_ARG(a.K > 0 && a.K <= 128 && a.N > 0 && a.N <= 128, "wgrad: K %d N %d", a.K, a.N);
+  SND_CHECK_ARG(a.ldx % 8 == 0 && a.lddy % 8 == 0 && a.x_bf16 && a.dy_bf16,
+                "wgrad: bf16 operands with leading dims %% 8");
+  SND_CHECK_ARG(a.rows_per_wg % kRcRows == 0 && a.pairs_per_wg >= 1 && a.pairs_per_wg <= WGT / 64,
+                "wgrad: geometry");
+  SND_CHECK_ARG(a.x && a.dy && a.slab && a.zero && a.npg > 0, "wgrad: null operand");
+  const int P = a.T * cdiv(a.K, 16);
+  dim3 grid(cdiv(a.R, a.rows_per_wg), cdiv(P, a.pairs_per_wg));
+  switch (cdiv(a.N, 16)) {
+    case 1: return wg_launch<1>(a, grid, s);
+    case 2: return wg_launch<2>(a, grid, s);
+    case 3: return wg_launch<3>(a, grid, s);
+    case 4: return wg_launch<4>(a, grid, s);
+    case 5: return wg_launch<5>(a, grid, s);
+    case 6: return wg_launch<6>(a, grid, s);
+    case 7: return wg_launch<7>(a, grid, s);
+    default: return wg_launch<8>(a, grid, s);
+  }
+}
+
+static int g_dbg = 0;
+int debug_flags() { return g_dbg; }
+
+int fast_init_attributes() {
+  static int done = 0;
+  if (done) return 0;
+#define SND_ATTR(K)                                                                       \
+  if (hipFuncSetAttribute(reinterpret_cast<const void*>(K),                               \
+                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMaxDynLds) != \
+      hipSuccess) {                                                                       \
+    set_error("hipFuncSetAttribute(%s) failed", #K);                                      \
+    return SND_ERR_HIP;                                                                   \
+  }
+#define SND_ATTR4(E) SND_ATTR((rowconv_kernel<E, 1>)) SND_ATTR((rowconv_kernel<E, 2>)) \
+                     SND_ATTR((rowconv_kernel<E, 3>)) SND_ATTR((rowconv_kernel<E, 4>))
+  SND_ATTR4(RC_LIN) SND_ATTR4(RC_FWD) SND_ATTR4(RC_DECBWD) SND_ATTR4(RC_ENC1) SND_ATTR4(RC_ENC0)
+#undef SND_ATTR4
+  SND_ATTR((wgrad_kernel<1>)) SND_ATTR((wgrad_kernel<2>)) SND_ATTR((wgrad_kernel<3>))
+  SND_ATTR((wgrad_kernel<4>)) SND_ATTR((wgrad_kernel<5>)) SND_ATTR((wgrad_kernel<6>))
+  SND_ATTR((wgrad_kernel<7>)) SND_ATTR((wgrad_kernel<8>))
+#undef SND_ATTR
+  done = 1;
+  return 0;
+}
+
+}  // namespace snd
+
+// measurement only: phase-skip bits for the fast-path kernels (0 = normal)
+extern "C" int snd_debug_set(int flags) {
+  snd::g_dbg = flags;
+  return 0;
+}

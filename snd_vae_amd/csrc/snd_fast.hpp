@@ -1,0 +1,127 @@
+// bf16 fast path of the train step: packed bf16 weight images, the row-tile
+// conv/linear engine (halo rows staged once in LDS, fused epilogues) and the
+// weight-gradient engine (LDS transpose reads).  The f32 parity mode keeps
+// the generic GEMM engine of snd_gemm.hip.
+#pragma once
+#include "snd_common.hpp"
+
+namespace snd {
+
+// Two-part column layout of a logical [a | b] tensor: part A at physical
+// columns [0, a), part B at [offb, offb + b) (offb = round_up(a, 8) keeps
+// part B 16-byte aligned in bf16).  b == 0: plain layout.  The decoder's
+// fused [s | n] branches use it so one launch serves both.
+struct ColMap {
+  int a, b, offb;
+  __host__ __device__ int phys() const { return b ? offb + b : a; }
+  __host__ __device__ bool valid(int c) const { return c < a || (b && c >= offb && c < offb + b); }
+  __host__ __device__ int logical(int c) const { return c < a ? c : c - offb + a; }
+};
+inline ColMap colmap_plain(int n) { return {n, 0, n}; }
+inline ColMap colmap_split(int a, int b) { return {a, b, (int)round_up(a, 8)}; }
+
+// ---- packed weight images ------------------------------------------------
+// dst[t][n][k] (bf16, np x kp per tap, 16-byte chunks of k XOR-swizzled per
+// row n -- the LDS image the row engine reads with ds_read_b128).
+// Source window W[T][A][B] (fp32, row-major) placed at (n_off, k_off):
+//   mode 0 (forward):  n = b - b0 + n_off, k = a - a0 + k_off, tap t
+//   mode 1 (data grad): n = a - a0 + n_off, k = b - b0 + k_off, tap T-1-t
+struct PackSrc {
+  const float* w;
+  int A, B;
+  int a0, a1, b0, b1;
+  int n_off, k_off;
+  int mode;
+};
+struct PackDesc {
+  __bf16* dst;
+  int T, kp, np;
+  int nsrc;
+  PackSrc s[2];
+};
+constexpr int kMaxPack = 16;
+int launch_pack(const PackDesc* d, int n, hipStream_t s);
+size_t pack_bytes(int T, int kp, int np);
+
+// ---- row engine -----------------------------------------------------------
+// out[r][n] = epi( sum_t sum_k x[r + t - H][k] * Wt[t][k][n] ), H = (T-1)/2,
+// rows r + t - H outside r's graph read as zero (TF SAME padding per graph).
+enum RcEpi {
+  RC_LIN = 0,     // (+bias) -> out; optional colpart q0 = sum out
+  RC_FWD = 1,     // y = acc + bias -> y; out = lrelu(y*gamma*c + beta)
+  RC_DECBWD = 2,  // du = acc; t = y*gamma*c + beta; dt = du*lrelu'(t); out = dy = dt*gamma*c;
+                  // colpart {sum dt*y, sum dt, sum dy}
+  RC_ENC1 = 3,    // dG = acc (cols [0, h) = B1 part, [h, h+f) = X part); see snd_fast.hip
+  RC_ENC0 = 4,    // dB0 = acc; P0 recomputed from AX, W0; see snd_fast.hip
+};
+struct RcArgs {
+  const void* x; int ldx; int K; int x_bf16;
+  int R, npg, T;
+  const __bf16* wpk; int kp, np;
+  int N;                        // physical output columns
+  ColMap cols;                  // physical -> logical (per-column parameters)
+  const float* bias; const float* gamma; const float* beta;
+  // part-B parameter vectors of a split layout (nullptr: one logical vector)
+  const float* bias_b; const float* gamma_b; const float* beta_b;
+  float* y; int ldy;            // RC_FWD out / RC_DECBWD in (fp32)
+  void* out; int ldo; int out_bf16;
+  float* colpart; int ncp;      // [gridDim.x][ncp][N] (nullptr: none)
+  // encoder epilogues
+  const float* p; int ldp;      // ENC1: P1 [R][h]; ENC0: AX [R][f]
+  const float* xf; int ldxf; int f;   // ENC1: X
+  const float* w0;              // ENC0: W0 [f][h]
+  const float* g2; const float* b2;   // ENC1: bn1 gamma/beta (gamma/beta = bne)
+  int h;                        // ENC1: h1
+  const void* zero;             // >= 16 zero bytes in device memory (LDS-DMA fill source)
+  int dbg;                      // measurement only: bits skip phases (see snd_debug_set)
+};
+constexpr int kRcRows = 128;    // rows per workgroup tile
+constexpr size_t kRcLdsLimit = 136 * 1024;   // dynamic LDS (static partials use the rest)
+int rc_blocks(int R);
+size_t rc_lds_bytes(int T, int kp, int np);
+int launch_rowconv(const RcArgs& a, int epi, hipStream_t s);
+
+// ---- weight-gradient engine ----------------------------------------------
+// slab[wg][t][k][n] = sum over the workgroup's rows r of x[r + t - H][k] * dy[r][n]
+// (same per-graph zero padding), k < K, n < N.  Deterministic partials.
+struct WgArgs {
+  const void* x; int ldx; int K; int x_bf16;
+  const void* dy; int lddy; int N; int dy_bf16;
+  int R, npg, T;
+  int rows_per_wg;              // multiple of kRcRows
+  int pairs_per_wg;             // (tap, 16-column k block) pairs per workgroup (<= 20)
+  float* slab;
+  const void* zero;             // >= 16 zero bytes in device memory
+  int dbg;
+};
+struct WgGeom { int rows_per_wg, pairs_per_wg, gx, gy; };
+WgGeom wgrad_geom(int R, int T, int K, int N);
+int launch_wgrad(const WgArgs& a, hipStream_t s);
+
+// ---- fused sigmoid head + MSE + backward + BN/lrelu backward of the head's
+// input layer (model_joint.py:115-121,138-144; optimizer.py:149,153).
+// One thread per row.  part[block] = {dW [cin][cout], db [cout],
+// sum dt*y [cin], sum dt [cin], sum dy [cin]}.
+struct HeadFastArgs {
+  const void* u; int ldu; int u_bf16;     // head input U = lrelu(BN(y))
+  const float* y; int ldy;               // U's pre-activation
+  const float* gamma; const float* beta;  // U's BN
+  int cin;
+  const float* w; const float* b; int cout;
+  const float* target; int ldt;
+  float count;                            // rows * cout (mean denominator)
+  float* yhat;                            // optional [R][cout]
+  __bf16* dy; int lddy;                   // gradient wrt y (bf16)
+  float* part;
+  double* sse;                            // [blocks]
+};
+constexpr int kHeadFastRows = 256;
+int heads_fast_blocks(int R);
+bool heads_fast_supported(int cin, int cout);   // built (cin, cout) pairs
+int heads_fast_parts(int cin, int cout);
+int launch_heads_fast(const HeadFastArgs* h, int n, int R, hipStream_t s);
+
+int fast_init_attributes();
+int debug_flags();
+
+}  // namespace snd

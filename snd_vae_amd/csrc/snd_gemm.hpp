@@ -26,7 +26,9 @@ int launch_gemm(GemmArgs g, int amode, int bmode, int epi, int dtype, int splits
                 hipStream_t s);
 int gemm_splits(int K, int target_blocks_per_tile);
 
-// Deterministic reduction of partial slabs: dst[i] (+)= scale * sum_p src[p*stride + i]
+// Deterministic reduction of partial slabs, fixed summation order:
+//   dst[r*dst_rs + i] (+)= scale * sum_p src[p*stride + r*src_rs + i],  i < len, r < rows
+// (rows == 0 means one row).
 struct ReduceDesc {
   const float* src;
   float* dst;
@@ -35,6 +37,8 @@ struct ReduceDesc {
   long long stride;
   float scale;
   int accumulate;
+  int rows;
+  long long src_rs, dst_rs;
 };
 constexpr int kMaxReduce = 48;
 int launch_reduce(const ReduceDesc* d, int n, hipStream_t s);

@@ -9,12 +9,14 @@
 // graph.  Forward/backward equations: SURVEY.md §8 "Composed step";
 // oracle/ref_numpy.py restates them in float64.
 #include <cstdarg>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <string>
 #include <vector>
 
 #include "snd_elem.hpp"
+#include "snd_fast.hpp"
 #include "snd_gemm.hpp"
 #include "snd_spmm.hpp"
 #include "snd_zzt.hpp"
@@ -47,6 +49,11 @@ Split wgrad_split(int M, int N, int R) {
   return {cdiv(R, kchunk), kchunk};
 }
 
+// padded K of a packed image (16-byte chunk swizzle supports 32 / 64 / 128)
+int kp_of(int k) { return k <= 32 ? 32 : (k <= 64 ? 64 : (k <= 128 ? 128 : -1)); }
+
+struct Img { int T, kp, np; long long off; };
+
 }  // namespace
 }  // namespace snd
 
@@ -62,6 +69,15 @@ struct snd_plan {
   long long ws = 0;
   // split geometry of the weight-gradient GEMMs
   Split sW0, sW1, sWh, sWms, sK1, sK2s, sK2n, sK3s;
+  // ---- bf16 fast decoder (snd_fast.hip)
+  bool fast = false;
+  ColMap m1{}, m2{};
+  int ld1 = 0, ld2 = 0, ld3 = 0;
+  Img pk1f{}, pk2f{}, pk3f{}, pk3b{}, pk2b{}, pk1b{};
+  WgGeom gK1{}, gK2s{}, gK2n{}, gK3s{};
+  // parameters of the last snd_train_step (snd_plan_launch re-runs kernels on them)
+  mutable const float* last_params = nullptr;
+  mutable float* last_grads = nullptr;
 
   long long blk(const char* n) const {
     for (auto& b : blocks) if (b.name == n) return b.off;
@@ -184,6 +200,53 @@ extern "C" int snd_plan_create(const snd_config_t* cfg, int n_graphs, snd_plan_t
   p->add_buf("SK2S", (long long)p->sK2s.splits * 5 * c.s1 * c.s2);
   p->add_buf("SK2N", (long long)p->sK2n.splits * 5 * c.n1 * c.n2);
   p->add_buf("SK3S", (long long)p->sK3s.splits * 5 * c.s2 * c.s3);
+
+  // ---- bf16 fast decoder: split [s | n] column layouts, packed weight images
+  if (c.dtype == SND_BF16) {
+    const ColMap m1 = colmap_split(c.s1, c.n1), m2 = colmap_split(c.s2, c.n2);
+    const int w1 = m1.phys(), w2 = m2.phys();
+    auto img = [&](int kin, int nout) {
+      Img m{5, kp_of(kin), (int)round_up(nout, 16), 0};
+      return m;
+    };
+    Img ims[6] = {img(L, w1), img(w1, w2), img(c.s2, c.s3), img(c.s3, c.s2), img(w2, w1), img(w1, L)};
+    bool ok = heads_fast_supported(c.s3, c.spatial_dim) && heads_fast_supported(c.n2, c.num_feature) &&
+              w1 <= 128;
+    for (auto& m : ims)
+      ok = ok && m.kp > 0 && m.np <= 128 && rc_lds_bytes(m.T, m.kp, m.np) <= kRcLdsLimit;
+    if (ok) {
+      p->fast = true;
+      p->m1 = m1; p->m2 = m2;
+      p->ld1 = (int)round_up(w1, 8); p->ld2 = (int)round_up(w2, 8); p->ld3 = (int)round_up(c.s3, 8);
+      const char* nm[6] = {"PK1F", "PK2F", "PK3F", "PK3B", "PK2B", "PK1B"};
+      for (int i = 0; i < 6; ++i) {
+        p->add_buf(nm[i], (long long)pack_bytes(ims[i].T, ims[i].kp, ims[i].np), 1);
+        ims[i].off = p->bufs.back().off;
+      }
+      p->pk1f = ims[0]; p->pk2f = ims[1]; p->pk3f = ims[2];
+      p->pk3b = ims[3]; p->pk2b = ims[4]; p->pk1b = ims[5];
+      p->add_buf("ZERO", 64);           // never written: LDS-DMA zero source
+      p->add_buf("ZB", R * L, 2);
+      p->add_buf("FY1", R * p->ld1);    p->add_buf("FU1", R * p->ld1, 2);
+      p->add_buf("FY2", R * p->ld2);    p->add_buf("FU2", R * p->ld2, 2);
+      p->add_buf("FY3", R * p->ld3);    p->add_buf("FU3", R * p->ld3);
+      p->add_buf("FDY3", R * p->ld3, 2); p->add_buf("FDY2", R * p->ld2, 2);
+      p->add_buf("FDY1", R * p->ld1, 2);
+      const int rcb = rc_blocks(p->R), hb = heads_fast_blocks(p->R);
+      p->add_buf("PFDEC2S", (long long)rcb * 3 * c.s2);
+      p->add_buf("PFDEC1", (long long)rcb * 3 * w1);
+      p->add_buf("PFHS", (long long)hb * heads_fast_parts(c.s3, c.spatial_dim));
+      p->add_buf("PFHN", (long long)hb * heads_fast_parts(c.n2, c.num_feature));
+      p->gK1 = wgrad_geom(p->R, 5, L, w1);
+      p->gK2s = wgrad_geom(p->R, 5, c.s1, c.s2);
+      p->gK2n = wgrad_geom(p->R, 5, c.n1, c.n2);
+      p->gK3s = wgrad_geom(p->R, 5, c.s2, c.s3);
+      p->add_buf("FSK1", (long long)p->gK1.gx * 5 * L * w1);
+      p->add_buf("FSK2S", (long long)p->gK2s.gx * 5 * c.s1 * c.s2);
+      p->add_buf("FSK2N", (long long)p->gK2n.gx * 5 * c.n1 * c.n2);
+      p->add_buf("FSK3S", (long long)p->gK3s.gx * 5 * c.s2 * c.s3);
+    }
+  }
   *out = p;
   return 0;
 }
@@ -274,6 +337,178 @@ int conv_wgrad(const Ctx& x, const float* in, int ldi, int cin, const float* dy,
   return launch_gemm(g, A_CONVT, B_ROW, E_PART, x.p->c.dtype, sp.splits, x.s);
 }
 
+
+// ---- bf16 fast decoder ------------------------------------------------------
+RcArgs rc_args(const snd_plan& p, const char* ws, const Img& im, const void* x, int ldx, int K,
+               int N, ColMap cols) {
+  RcArgs a{};
+  a.x = x; a.ldx = ldx; a.K = K; a.x_bf16 = 1;
+  a.R = p.R; a.npg = p.N; a.T = im.T;
+  a.wpk = reinterpret_cast<const __bf16*>(ws + im.off); a.kp = im.kp; a.np = im.np;
+  a.N = N; a.cols = cols;
+  a.zero = ws + p.buf("ZERO");
+  a.dbg = debug_flags();
+  return a;
+}
+
+WgArgs wg_args(const snd_plan& p, const char* ws, const WgGeom& g, const void* x, int ldx, int K, const void* dy,
+               int lddy, int N, float* slab) {
+  WgArgs a{};
+  a.x = x; a.ldx = ldx; a.K = K; a.x_bf16 = 1;
+  a.dy = dy; a.lddy = lddy; a.N = N; a.dy_bf16 = 1;
+  a.R = p.R; a.npg = p.N; a.T = 5;
+  a.rows_per_wg = g.rows_per_wg; a.pairs_per_wg = g.pairs_per_wg;
+  a.slab = slab;
+  a.zero = ws + p.buf("ZERO");
+  a.dbg = debug_flags();
+  return a;
+}
+
+int pack_decoder(const Ctx& x) {
+  const snd_plan& p = *x.p;
+  const snd_config_t& c = p.c;
+  const int L = c.latent, s1 = c.s1, n1 = c.n1, s2 = c.s2, n2 = c.n2, s3 = c.s3;
+  const int C1 = p.C1;
+  auto dst = [&](const Img& im) { return reinterpret_cast<__bf16*>(x.ws + im.off); };
+  auto src = [](const float* w, int A, int B, int a0, int a1, int b0, int b1, int noff, int koff,
+                int mode) { return PackSrc{w, A, B, a0, a1, b0, b1, noff, koff, mode}; };
+  const float *K1 = x.w("dec.K1"), *K2s = x.w("dec.K2s"), *K2n = x.w("dec.K2n"), *K3s = x.w("dec.K3s");
+  const int o1 = p.m1.offb, o2 = p.m2.offb;
+  PackDesc d[6]{};
+  // conv forward images: n = output channel (split layouts), k = input channel
+  d[0] = {dst(p.pk1f), 5, p.pk1f.kp, p.pk1f.np, 2,
+          {src(K1, L, C1, 0, L, 0, s1, 0, 0, 0), src(K1, L, C1, 0, L, s1, C1, o1, 0, 0)}};
+  d[1] = {dst(p.pk2f), 5, p.pk2f.kp, p.pk2f.np, 2,
+          {src(K2s, s1, s2, 0, s1, 0, s2, 0, 0, 0), src(K2n, n1, n2, 0, n1, 0, n2, o2, o1, 0)}};
+  d[2] = {dst(p.pk3f), 5, p.pk3f.kp, p.pk3f.np, 1, {src(K3s, s2, s3, 0, s2, 0, s3, 0, 0, 0), {}}};
+  // data-gradient images: n = input channel of the forward conv, k = its output channel
+  d[3] = {dst(p.pk3b), 5, p.pk3b.kp, p.pk3b.np, 1, {src(K3s, s2, s3, 0, s2, 0, s3, 0, 0, 1), {}}};
+  d[4] = {dst(p.pk2b), 5, p.pk2b.kp, p.pk2b.np, 2,
+          {src(K2s, s1, s2, 0, s1, 0, s2, 0, 0, 1), src(K2n, n1, n2, 0, n1, 0, n2, o1, o2, 1)}};
+  d[5] = {dst(p.pk1b), 5, p.pk1b.kp, p.pk1b.np, 2,
+          {src(K1, L, C1, 0, L, 0, s1, 0, 0, 1), src(K1, L, C1, 0, L, s1, C1, 0, o1, 1)}};
+  return launch_pack(d, 6, x.s);
+}
+
+// decoder forward + heads + backward (model_joint.py:112-145, optimizer.py:149,153)
+int decoder_fast(const Ctx& x, const snd_batch_t* batch, int only = -1) {
+  const snd_plan& p = *x.p;
+  const snd_config_t& c = p.c;
+  const int R = p.R, L = c.latent, s2 = c.s2, s3 = c.s3, n2 = c.n2;
+  const int sd = c.spatial_dim, nf = c.num_feature;
+  const int w1 = p.m1.phys(), w2 = p.m2.phys(), o1 = p.m1.offb, o2 = p.m2.offb;
+  auto bf = [&](const char* n) { return reinterpret_cast<__bf16*>(x.f(n)); };
+  // conv1 (fused [s1 | n0] branches): z -> Y1, U1
+  {
+    RcArgs a = rc_args(p, x.ws, p.pk1f, bf("ZB"), L, L, w1, p.m1);
+    a.bias = x.w("dec.b1"); a.gamma = x.w("dec.bn1.gamma"); a.beta = x.w("dec.bn1.beta");
+    a.y = x.f("FY1"); a.ldy = p.ld1; a.out = bf("FU1"); a.ldo = p.ld1; a.out_bf16 = 1;
+    if (only < 0 || only == 0) SND_TRY(launch_rowconv(a, RC_FWD, x.s));
+  }
+  // conv2 (block-diagonal s2 | n1): U1 -> Y2, U2
+  {
+    RcArgs a = rc_args(p, x.ws, p.pk2f, bf("FU1"), p.ld1, w1, w2, p.m2);
+    a.bias = x.w("dec.b2s"); a.gamma = x.w("dec.bn2s.gamma"); a.beta = x.w("dec.bn2s.beta");
+    a.bias_b = x.w("dec.b2n"); a.gamma_b = x.w("dec.bn2n.gamma"); a.beta_b = x.w("dec.bn2n.beta");
+    a.y = x.f("FY2"); a.ldy = p.ld2; a.out = bf("FU2"); a.ldo = p.ld2; a.out_bf16 = 1;
+    if (only < 0 || only == 1) SND_TRY(launch_rowconv(a, RC_FWD, x.s));
+  }
+  // conv3 (s3): U2s -> Y3, U3 (fp32: head input)
+  {
+    RcArgs a = rc_args(p, x.ws, p.pk3f, bf("FU2"), p.ld2, s2, s3, colmap_plain(s3));
+    a.bias = x.w("dec.b3s"); a.gamma = x.w("dec.bn3s.gamma"); a.beta = x.w("dec.bn3s.beta");
+    a.y = x.f("FY3"); a.ldy = p.ld3; a.out = x.f("FU3"); a.ldo = p.ld3; a.out_bf16 = 0;
+    if (only < 0 || only == 2) SND_TRY(launch_rowconv(a, RC_FWD, x.s));
+  }
+  // heads + MSE + backward, fused with the BN/lrelu backward of conv3 / conv2n
+  {
+    HeadFastArgs h[2]{};
+    h[0] = {x.f("FU3"), p.ld3, 0, x.f("FY3"), p.ld3, x.w("dec.bn3s.gamma"), x.w("dec.bn3s.beta"), s3,
+            x.w("dec.Ws"), x.w("dec.bs"), sd, batch->spatial_truth, sd, (float)R * sd, x.f("SHAT"),
+            bf("FDY3"), p.ld3, x.f("PFHS"), x.d("PSSES")};
+    h[1] = {bf("FU2") + o2, p.ld2, 1, x.f("FY2") + o2, p.ld2, x.w("dec.bn2n.gamma"),
+            x.w("dec.bn2n.beta"), n2, x.w("dec.Wn"), x.w("dec.bn"), nf, batch->feature_truth, nf,
+            (float)R * nf, x.f("XHAT"), bf("FDY2") + o2, p.ld2, x.f("PFHN"), x.d("PSSEN")};
+    if (only < 0 || only == 3) SND_TRY(launch_heads_fast(h, 2, R, x.s));
+  }
+  // conv3 data gradient -> dU2s, fused BN/lrelu backward of conv2s -> dY2[:, :s2]
+  {
+    RcArgs a = rc_args(p, x.ws, p.pk3b, bf("FDY3"), p.ld3, s3, s2, colmap_plain(s2));
+    a.gamma = x.w("dec.bn2s.gamma"); a.beta = x.w("dec.bn2s.beta");
+    a.y = x.f("FY2"); a.ldy = p.ld2; a.out = bf("FDY2"); a.ldo = p.ld2; a.out_bf16 = 1;
+    a.colpart = x.f("PFDEC2S"); a.ncp = 3;
+    if (only < 0 || only == 4) SND_TRY(launch_rowconv(a, RC_DECBWD, x.s));
+  }
+  if (only < 0 || only == 5) SND_TRY(launch_wgrad(wg_args(p, x.ws, p.gK3s, bf("FU2"), p.ld2, s2, bf("FDY3"), p.ld3, s3, x.f("FSK3S")), x.s));
+  // conv2 data gradient -> dU1, fused BN/lrelu backward of conv1 -> dY1
+  {
+    RcArgs a = rc_args(p, x.ws, p.pk2b, bf("FDY2"), p.ld2, w2, w1, p.m1);
+    a.gamma = x.w("dec.bn1.gamma"); a.beta = x.w("dec.bn1.beta");
+    a.y = x.f("FY1"); a.ldy = p.ld1; a.out = bf("FDY1"); a.ldo = p.ld1; a.out_bf16 = 1;
+    a.colpart = x.f("PFDEC1"); a.ncp = 3;
+    if (only < 0 || only == 6) SND_TRY(launch_rowconv(a, RC_DECBWD, x.s));
+  }
+  if (only < 0 || only == 7) SND_TRY(launch_wgrad(wg_args(p, x.ws, p.gK2s, bf("FU1"), p.ld1, c.s1, bf("FDY2"), p.ld2, s2, x.f("FSK2S")), x.s));
+  if (only < 0 || only == 8) SND_TRY(launch_wgrad(wg_args(p, x.ws, p.gK2n, bf("FU1") + o1, p.ld1, c.n1, bf("FDY2") + o2, p.ld2, n2,
+                               x.f("FSK2N")), x.s));
+  // conv1 data gradient -> dz (decoder part)
+  {
+    RcArgs a = rc_args(p, x.ws, p.pk1b, bf("FDY1"), p.ld1, w1, L, colmap_plain(L));
+    a.out = x.f("DZDEC"); a.ldo = L; a.out_bf16 = 0;
+    if (only < 0 || only == 9) SND_TRY(launch_rowconv(a, RC_LIN, x.s));
+  }
+  if (only < 0 || only == 10)
+    SND_TRY(launch_wgrad(wg_args(p, x.ws, p.gK1, bf("ZB"), L, L, bf("FDY1"), p.ld1, w1, x.f("FSK1")), x.s));
+  return 0;
+}
+
+// reduce descriptors of the fast decoder's partials
+void decoder_fast_reduce(const Ctx& x, std::vector<ReduceDesc>& rd) {
+  const snd_plan& p = *x.p;
+  const snd_config_t& c = p.c;
+  const int L = c.latent, s1 = c.s1, n1 = c.n1, s2 = c.s2, n2 = c.n2, s3 = c.s3, C1 = p.C1;
+  const int sd = c.spatial_dim, nf = c.num_feature;
+  const int w1 = p.m1.phys(), o1 = p.m1.offb;
+  const int rcb = rc_blocks(p.R), hb = heads_fast_blocks(p.R);
+  auto flat = [&](const char* buf, int parts, long long len, const char* dst) {
+    rd.push_back({x.f(buf), x.g(dst), parts, (int)len, len, 1.f, 0, 0, 0, 0});
+  };
+  flat("FSK3S", p.gK3s.gx, 5LL * s2 * s3, "dec.K3s");
+  flat("FSK2S", p.gK2s.gx, 5LL * s1 * s2, "dec.K2s");
+  flat("FSK2N", p.gK2n.gx, 5LL * n1 * n2, "dec.K2n");
+  {  // [5][L][w1] split columns -> dec.K1 [5][L][C1]
+    const long long st = 5LL * L * w1;
+    rd.push_back({x.f("FSK1"), x.g("dec.K1"), p.gK1.gx, s1, st, 1.f, 0, 5 * L, w1, C1});
+    rd.push_back({x.f("FSK1") + o1, x.g("dec.K1") + s1, p.gK1.gx, n1, st, 1.f, 0, 5 * L, w1, C1});
+  }
+  // per-column partials {sum dt*y (x c), sum dt, sum dy} -> gamma, beta, bias
+  auto cols3 = [&](const char* buf, int parts, int width, int src0, int len, const char* g,
+                   const char* b, const char* bias, int dst0) {
+    const long long st = 3LL * width;
+    const float* s0 = x.f(buf) + src0;
+    rd.push_back({s0, x.g(g) + dst0, parts, len, st, kBnC, 0, 0, 0, 0});
+    rd.push_back({s0 + width, x.g(b) + dst0, parts, len, st, 1.f, 0, 0, 0, 0});
+    rd.push_back({s0 + 2 * width, x.g(bias) + dst0, parts, len, st, 1.f, 0, 0, 0, 0});
+  };
+  cols3("PFDEC2S", rcb, s2, 0, s2, "dec.bn2s.gamma", "dec.bn2s.beta", "dec.b2s", 0);
+  cols3("PFDEC1", rcb, w1, 0, s1, "dec.bn1.gamma", "dec.bn1.beta", "dec.b1", 0);
+  cols3("PFDEC1", rcb, w1, o1, n1, "dec.bn1.gamma", "dec.bn1.beta", "dec.b1", s1);
+  // heads: {dW, db, sum dt*y, sum dt, sum dy}
+  auto head = [&](const char* buf, int cin, int cout, const char* W, const char* bb, const char* g,
+                  const char* be, const char* bias) {
+    const long long st = heads_fast_parts(cin, cout);
+    const float* s0 = x.f(buf);
+    rd.push_back({s0, x.g(W), hb, cin * cout, st, 1.f, 0, 0, 0, 0});
+    rd.push_back({s0 + cin * cout, x.g(bb), hb, cout, st, 1.f, 0, 0, 0, 0});
+    const int q = cin * cout + cout;
+    rd.push_back({s0 + q, x.g(g), hb, cin, st, kBnC, 0, 0, 0, 0});
+    rd.push_back({s0 + q + cin, x.g(be), hb, cin, st, 1.f, 0, 0, 0, 0});
+    rd.push_back({s0 + q + 2 * cin, x.g(bias), hb, cin, st, 1.f, 0, 0, 0, 0});
+  };
+  head("PFHS", s3, sd, "dec.Ws", "dec.bs", "dec.bn3s.gamma", "dec.bn3s.beta", "dec.b3s");
+  head("PFHN", n2, nf, "dec.Wn", "dec.bn", "dec.bn2n.gamma", "dec.bn2n.beta", "dec.b2n");
+}
+
 }  // namespace
 
 extern "C" int snd_plan_launch(const snd_plan_t* plan, const snd_batch_t* batch,
@@ -296,6 +531,13 @@ extern "C" int snd_plan_launch(const snd_plan_t* plan, const snd_batch_t* batch,
                p.c.h1, (float*)(ws + p.buf("DXW1")), p.c.h1, SND_SPMM_PLAIN};
     return launch_spmm(a, s);
   }
+  if (!strncmp(kernel, "dec:", 4) || !strcmp(kernel, "pack")) {   // fast decoder kernel k
+    SND_CHECK_ARG(p.fast && p.last_params, "snd_plan_launch: no fast-path step has run");
+    SND_TRY(fast_init_attributes());
+    Ctx x{&p, ws, p.last_params, p.last_grads, s};
+    if (kernel[0] == 'p') return pack_decoder(x);
+    return decoder_fast(x, batch, atoi(kernel + 4));
+  }
   set_error("snd_plan_launch: unknown kernel '%s'", kernel);
   return SND_ERR_ARG;
 }
@@ -312,12 +554,18 @@ extern "C" int snd_train_step(const snd_plan_t* plan, const snd_batch_t* batch,
   const snd_plan& p = *plan;
   const snd_config_t& c = p.c;
   Ctx x{&p, (char*)workspace, params, grads, (hipStream_t)stream};
+  p.last_params = params;
+  p.last_grads = grads;
   const int R = p.R, N = p.N, f = c.f_in, h0 = c.h0, h1 = c.h1, gh = c.g_hidden, L = c.latent;
   const int W = p.W, C1 = p.C1, s1 = c.s1, s2 = c.s2, s3 = c.s3, n1 = c.n1, n2 = c.n2;
   const int sd = c.spatial_dim, nf = c.num_feature;
   const int* rp = batch->rowptr;
   const int* ci = batch->colidx;
   const float* X = batch->features;
+  if (p.fast) {
+    SND_TRY(fast_init_attributes());
+    SND_TRY(pack_decoder(x));   // bf16 weight images of this step's parameters
+  }
 
   // =============================== forward ===============================
   // encoder, model.py:104-112: H_{i+1} = [BN(lrelu(A (H_i W_i))) || X]
@@ -344,7 +592,7 @@ extern "C" int snd_train_step(const snd_plan_t* plan, const snd_batch_t* batch,
   // z = mu + eps exp(s) (model.py:159); KL partials (optimizer.py:193)
   {
     ReparamFwdArgs a{x.f("MS"), 2 * L, R, L, eps, seed, step_counter, x.f("EPS"), x.f("Z"),
-                     x.d("PKL")};
+                     x.d("PKL"), p.fast ? (__bf16*)x.f("ZB") : nullptr, L};
     SND_TRY(launch_reparam_fwd(a, x.s));
   }
   // inner-product decoder + CE (fused) and per-edge terms
@@ -356,51 +604,55 @@ extern "C" int snd_train_step(const snd_plan_t* plan, const snd_batch_t* batch,
     EdgeArgs ea{rp, ci, R, x.f("Z"), L, c.pos_weight, x.f("EJ"), x.d("PEDGE")};
     SND_TRY(launch_edge(ea, x.s));
   }
-  // decoders (model_joint.py:112-145): conv1d k5 SAME -> BN -> lrelu
-  SND_TRY(conv_fwd(x, x.f("Z"), L, L, "dec.K1", C1, "dec.b1", "dec.bn1.gamma", "dec.bn1.beta",
-                   x.f("Y1"), x.f("U1")));
-  SND_TRY(conv_fwd(x, x.f("U1"), C1, s1, "dec.K2s", s2, "dec.b2s", "dec.bn2s.gamma",
-                   "dec.bn2s.beta", x.f("Y2S"), x.f("U2S")));
-  SND_TRY(conv_fwd(x, x.f("U1") + s1, C1, n1, "dec.K2n", n2, "dec.b2n", "dec.bn2n.gamma",
-                   "dec.bn2n.beta", x.f("Y2N"), x.f("U2N")));
-  SND_TRY(conv_fwd(x, x.f("U2S"), s2, s2, "dec.K3s", s3, "dec.b3s", "dec.bn3s.gamma",
-                   "dec.bn3s.beta", x.f("Y3S"), x.f("U3S")));
-  // sigmoid heads + MSE + their backward (optimizer.py:149,153)
-  {
-    HeadArgs h[2] = {
-        {x.f("U3S"), s3, s3, x.w("dec.Ws"), x.w("dec.bs"), sd, batch->spatial_truth, sd,
-         (float)R * sd, x.f("SHAT"), x.f("DU3S"), s3, x.f("PHS"), x.d("PSSES")},
-        {x.f("U2N"), n2, n2, x.w("dec.Wn"), x.w("dec.bn"), nf, batch->feature_truth, nf,
-         (float)R * nf, x.f("XHAT"), x.f("DU2N"), n2, x.f("PHN"), x.d("PSSEN")}};
-    SND_TRY(launch_heads(h, 2, R, x.s));
+  if (p.fast) {
+    SND_TRY(decoder_fast(x, batch));
+  } else {
+    // decoders (model_joint.py:112-145): conv1d k5 SAME -> BN -> lrelu
+    SND_TRY(conv_fwd(x, x.f("Z"), L, L, "dec.K1", C1, "dec.b1", "dec.bn1.gamma", "dec.bn1.beta",
+                     x.f("Y1"), x.f("U1")));
+    SND_TRY(conv_fwd(x, x.f("U1"), C1, s1, "dec.K2s", s2, "dec.b2s", "dec.bn2s.gamma",
+                     "dec.bn2s.beta", x.f("Y2S"), x.f("U2S")));
+    SND_TRY(conv_fwd(x, x.f("U1") + s1, C1, n1, "dec.K2n", n2, "dec.b2n", "dec.bn2n.gamma",
+                     "dec.bn2n.beta", x.f("Y2N"), x.f("U2N")));
+    SND_TRY(conv_fwd(x, x.f("U2S"), s2, s2, "dec.K3s", s3, "dec.b3s", "dec.bn3s.gamma",
+                     "dec.bn3s.beta", x.f("Y3S"), x.f("U3S")));
+    // sigmoid heads + MSE + their backward (optimizer.py:149,153)
+    {
+      HeadArgs h[2] = {
+          {x.f("U3S"), s3, s3, x.w("dec.Ws"), x.w("dec.bs"), sd, batch->spatial_truth, sd,
+           (float)R * sd, x.f("SHAT"), x.f("DU3S"), s3, x.f("PHS"), x.d("PSSES")},
+          {x.f("U2N"), n2, n2, x.w("dec.Wn"), x.w("dec.bn"), nf, batch->feature_truth, nf,
+           (float)R * nf, x.f("XHAT"), x.f("DU2N"), n2, x.f("PHN"), x.d("PSSEN")}};
+      SND_TRY(launch_heads(h, 2, R, x.s));
+    }
+    // =============================== backward ==============================
+    {
+      DecBwdArgs d{x.f("DU3S"), s3, x.f("Y3S"), s3, x.w("dec.bn3s.gamma"), x.w("dec.bn3s.beta"), s3,
+                   x.f("DY3S"), s3, x.f("PDEC3")};
+      SND_TRY(launch_dec_bwd(&d, 1, R, x.s));
+    }
+    SND_TRY(conv_bwd_data(x, x.f("DY3S"), s3, "dec.K3s", s2, x.f("DU2S"), s2));
+    SND_TRY(conv_wgrad(x, x.f("U2S"), s2, s2, x.f("DY3S"), s3, x.f("SK3S"), p.sK3s));
+    {
+      DecBwdArgs d[2] = {
+          {x.f("DU2S"), s2, x.f("Y2S"), s2, x.w("dec.bn2s.gamma"), x.w("dec.bn2s.beta"), s2,
+           x.f("DY2S"), s2, x.f("PDEC2S")},
+          {x.f("DU2N"), n2, x.f("Y2N"), n2, x.w("dec.bn2n.gamma"), x.w("dec.bn2n.beta"), n2,
+           x.f("DY2N"), n2, x.f("PDEC2N")}};
+      SND_TRY(launch_dec_bwd(d, 2, R, x.s));
+    }
+    SND_TRY(conv_bwd_data(x, x.f("DY2S"), s2, "dec.K2s", s1, x.f("DU1"), C1));
+    SND_TRY(conv_bwd_data(x, x.f("DY2N"), n2, "dec.K2n", n1, x.f("DU1") + s1, C1));
+    SND_TRY(conv_wgrad(x, x.f("U1"), C1, s1, x.f("DY2S"), s2, x.f("SK2S"), p.sK2s));
+    SND_TRY(conv_wgrad(x, x.f("U1") + s1, C1, n1, x.f("DY2N"), n2, x.f("SK2N"), p.sK2n));
+    {
+      DecBwdArgs d{x.f("DU1"), C1, x.f("Y1"), C1, x.w("dec.bn1.gamma"), x.w("dec.bn1.beta"), C1,
+                   x.f("DY1"), C1, x.f("PDEC1")};
+      SND_TRY(launch_dec_bwd(&d, 1, R, x.s));
+    }
+    SND_TRY(conv_bwd_data(x, x.f("DY1"), C1, "dec.K1", L, x.f("DZDEC"), L));
+    SND_TRY(conv_wgrad(x, x.f("Z"), L, L, x.f("DY1"), C1, x.f("SK1"), p.sK1));
   }
-  // =============================== backward ==============================
-  {
-    DecBwdArgs d{x.f("DU3S"), s3, x.f("Y3S"), s3, x.w("dec.bn3s.gamma"), x.w("dec.bn3s.beta"), s3,
-                 x.f("DY3S"), s3, x.f("PDEC3")};
-    SND_TRY(launch_dec_bwd(&d, 1, R, x.s));
-  }
-  SND_TRY(conv_bwd_data(x, x.f("DY3S"), s3, "dec.K3s", s2, x.f("DU2S"), s2));
-  SND_TRY(conv_wgrad(x, x.f("U2S"), s2, s2, x.f("DY3S"), s3, x.f("SK3S"), p.sK3s));
-  {
-    DecBwdArgs d[2] = {
-        {x.f("DU2S"), s2, x.f("Y2S"), s2, x.w("dec.bn2s.gamma"), x.w("dec.bn2s.beta"), s2,
-         x.f("DY2S"), s2, x.f("PDEC2S")},
-        {x.f("DU2N"), n2, x.f("Y2N"), n2, x.w("dec.bn2n.gamma"), x.w("dec.bn2n.beta"), n2,
-         x.f("DY2N"), n2, x.f("PDEC2N")}};
-    SND_TRY(launch_dec_bwd(d, 2, R, x.s));
-  }
-  SND_TRY(conv_bwd_data(x, x.f("DY2S"), s2, "dec.K2s", s1, x.f("DU1"), C1));
-  SND_TRY(conv_bwd_data(x, x.f("DY2N"), n2, "dec.K2n", n1, x.f("DU1") + s1, C1));
-  SND_TRY(conv_wgrad(x, x.f("U1"), C1, s1, x.f("DY2S"), s2, x.f("SK2S"), p.sK2s));
-  SND_TRY(conv_wgrad(x, x.f("U1") + s1, C1, n1, x.f("DY2N"), n2, x.f("SK2N"), p.sK2n));
-  {
-    DecBwdArgs d{x.f("DU1"), C1, x.f("Y1"), C1, x.w("dec.bn1.gamma"), x.w("dec.bn1.beta"), C1,
-                 x.f("DY1"), C1, x.f("PDEC1")};
-    SND_TRY(launch_dec_bwd(&d, 1, R, x.s));
-  }
-  SND_TRY(conv_bwd_data(x, x.f("DY1"), C1, "dec.K1", L, x.f("DZDEC"), L));
-  SND_TRY(conv_wgrad(x, x.f("Z"), L, L, x.f("DY1"), C1, x.f("SK1"), p.sK1));
   // reparameterisation + KL backward; dz = conv-decoder grad + zz^T CE grad
   {
     const double pairs = (double)p.B * N * (double)N;
@@ -452,10 +704,12 @@ extern "C" int snd_train_step(const snd_plan_t* plan, const snd_batch_t* batch,
   slab("SW1", p.sW1, h0 + f, h1, "enc.W1", (h0 + f) * h1, nullptr);
   slab("SWH", p.sWh, W + 1, gh, "enc.Wh", W * gh, "enc.bh");
   slab("SWMS", p.sWms, gh + 1, 2 * L, "enc.Wms", gh * 2 * L, "enc.bms");
-  slab("SK1", p.sK1, 5 * L, C1, "dec.K1", 5 * L * C1, nullptr);
-  slab("SK2S", p.sK2s, 5 * s1, s2, "dec.K2s", 5 * s1 * s2, nullptr);
-  slab("SK2N", p.sK2n, 5 * n1, n2, "dec.K2n", 5 * n1 * n2, nullptr);
-  slab("SK3S", p.sK3s, 5 * s2, s3, "dec.K3s", 5 * s2 * s3, nullptr);
+  if (!p.fast) {
+    slab("SK1", p.sK1, 5 * L, C1, "dec.K1", 5 * L * C1, nullptr);
+    slab("SK2S", p.sK2s, 5 * s1, s2, "dec.K2s", 5 * s1 * s2, nullptr);
+    slab("SK2N", p.sK2n, 5 * n1, n2, "dec.K2n", 5 * n1 * n2, nullptr);
+    slab("SK3S", p.sK3s, 5 * s2, s3, "dec.K3s", 5 * s2 * s3, nullptr);
+  }
   auto cols = [&](const char* buf, int stride, int off, int len, const char* dst) {
     rd.push_back({x.f(buf) + off, x.g(dst), nc, len, (long long)stride, 1.f, 0});
   };
@@ -470,15 +724,19 @@ extern "C" int snd_train_step(const snd_plan_t* plan, const snd_batch_t* batch,
     cols(buf, 3 * w, w, w, b);
     cols(buf, 3 * w, 2 * w, w, bias);
   };
-  dec("PDEC3", s3, "dec.bn3s.gamma", "dec.bn3s.beta", "dec.b3s");
-  dec("PDEC2S", s2, "dec.bn2s.gamma", "dec.bn2s.beta", "dec.b2s");
-  dec("PDEC2N", n2, "dec.bn2n.gamma", "dec.bn2n.beta", "dec.b2n");
-  dec("PDEC1", C1, "dec.bn1.gamma", "dec.bn1.beta", "dec.b1");
-  const int hs = s3 * sd + sd, hn = n2 * nf + nf;
-  rd.push_back({x.f("PHS"), x.g("dec.Ws"), nh, s3 * sd, (long long)hs, 1.f, 0});
-  rd.push_back({x.f("PHS") + s3 * sd, x.g("dec.bs"), nh, sd, (long long)hs, 1.f, 0});
-  rd.push_back({x.f("PHN"), x.g("dec.Wn"), nh, n2 * nf, (long long)hn, 1.f, 0});
-  rd.push_back({x.f("PHN") + n2 * nf, x.g("dec.bn"), nh, nf, (long long)hn, 1.f, 0});
+  if (p.fast) {
+    decoder_fast_reduce(x, rd);
+  } else {
+    dec("PDEC3", s3, "dec.bn3s.gamma", "dec.bn3s.beta", "dec.b3s");
+    dec("PDEC2S", s2, "dec.bn2s.gamma", "dec.bn2s.beta", "dec.b2s");
+    dec("PDEC2N", n2, "dec.bn2n.gamma", "dec.bn2n.beta", "dec.b2n");
+    dec("PDEC1", C1, "dec.bn1.gamma", "dec.bn1.beta", "dec.b1");
+    const int hs = s3 * sd + sd, hn = n2 * nf + nf;
+    rd.push_back({x.f("PHS"), x.g("dec.Ws"), nh, s3 * sd, (long long)hs, 1.f, 0});
+    rd.push_back({x.f("PHS") + s3 * sd, x.g("dec.bs"), nh, sd, (long long)hs, 1.f, 0});
+    rd.push_back({x.f("PHN"), x.g("dec.Wn"), nh, n2 * nf, (long long)hn, 1.f, 0});
+    rd.push_back({x.f("PHN") + n2 * nf, x.g("dec.bn"), nh, nf, (long long)hn, 1.f, 0});
+  }
   SND_TRY(launch_reduce(rd.data(), (int)rd.size(), x.s));
 
   FinalizeArgs fa{x.d("PZZT"), zzt_dense_blocks(p.B, N), x.d("PEDGE"), edge_blocks(R, L),

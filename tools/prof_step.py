@@ -1,0 +1,37 @@
+"""Run a few eager (non-graph) train steps for per-dispatch PMC profiling.
+
+    rocprofv3 --pmc SQ_WAVES ... -d gpurun_out/pmcX -o run --output-format csv -- \
+        python tools/prof_step.py --steps 3
+"""
+import argparse
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--graphs", type=int, default=8)
+    ap.add_argument("--nodes", type=int, default=4096)
+    ap.add_argument("--latent", type=int, default=64)
+    ap.add_argument("--dtype", default="bf16")
+    args = ap.parse_args()
+    import torch
+    from snd_vae_amd.config import tscale
+    from snd_vae_amd.data import synthetic_batch
+    from snd_vae_amd.model import DeviceBatch, SGCNModelVAE
+    from snd_vae_amd.optimizer import OptimizerVAE
+    cfg = tscale(args.nodes, args.latent)
+    db = DeviceBatch(synthetic_batch(cfg, args.graphs, seed=1000))
+    model = SGCNModelVAE(cfg, args.graphs, dtype=args.dtype)
+    opt = OptimizerVAE(model)
+    for _ in range(args.steps):
+        opt.step(db)
+    torch.cuda.synchronize()
+    print("ok", args.steps)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,27 @@
+"""Print the per-dispatch timeline of the last train step in a rocprofv3 kernel trace.
+
+    python tools/step_timeline.py gpurun_out/prof/run_kernel_trace.csv
+"""
+import csv
+import sys
+
+
+def main(path):
+    rows = list(csv.DictReader(open(path)))
+    rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+    idx = [i for i, r in enumerate(rows) if "adam_kernel" in r["Kernel_Name"]]
+    a, b = idx[-2] + 1, idx[-1] + 1
+    t0 = int(rows[a]["Start_Timestamp"])
+    busy = 0
+    for r in rows[a:b]:
+        s, e = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
+        busy += e - s
+        n = r["Kernel_Name"].replace("snd::(anonymous namespace)::", "").replace("_ZN3snd12_GLOBAL__N_1", "")
+        print(f"{(s - t0) / 1e3:8.1f} {(e - s) / 1e3:7.2f}  grid {r['Grid_Size_X']:>7}x{r['Grid_Size_Y']:>3}"
+              f" lds {r['LDS_Block_Size']:>6} vgpr {r['VGPR_Count']:>3}/{r['Accum_VGPR_Count']:>3}  {n[:70]}")
+    end = int(rows[b - 1]["End_Timestamp"])
+    print(f"step span {(end - t0) / 1e3:.1f} us, kernel busy {busy / 1e3:.1f} us, {b - a} launches")
+
+
+if __name__ == "__main__":
+    main(sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/prof/run_kernel_trace.csv")
