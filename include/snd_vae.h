@@ -214,7 +214,8 @@ int snd_plan_launch(const snd_plan_t* plan, const snd_batch_t* batch,
                     void* workspace, const char* kernel, snd_stream_t stream);
 /* Measurement only: bits that make the bf16 decoder kernels skip phases
  * (1 weight staging, 2 row staging, 4 MFMA, 8 stores, 16 column params,
- * 32 epilogue prefetch).  0 (default) = normal operation. */
+ * 32 epilogue prefetch) and, read by snd_plan_create, 256 = generic-engine
+ * plan, 512 = generic encoder.  0 (default) = normal operation. */
 int snd_debug_set(int flags);
 
 #ifdef __cplusplus

@@ -68,6 +68,25 @@ __device__ __forceinline__ unsigned wave_sum_u(unsigned v) {
   return v;
 }
 
+// DPP lane exchange within a 16-lane row (bound_ctrl: out-of-row reads give 0)
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, true));
+}
+// sum over aligned groups of 8 lanes (all 8 receive the sum)
+__device__ __forceinline__ float row8_sum(float v) {
+  v += dpp_f<0xB1>(v);    // quad_perm [1,0,3,2]
+  v += dpp_f<0x4E>(v);    // quad_perm [2,3,0,1]
+  v += dpp_f<0x141>(v);   // row_half_mirror
+  return v;
+}
+// sum over the 16 lanes of each DPP row (all lanes receive the row sum)
+__device__ __forceinline__ float row16_sum(float v) {
+  v = row8_sum(v);
+  v += dpp_f<0x140>(v);   // row_mirror
+  return v;
+}
+
 inline int cdiv(long long a, long long b) { return (int)((a + b - 1) / b); }
 inline long long round_up(long long a, long long b) { return (a + b - 1) / b * b; }
 

@@ -44,19 +44,6 @@ __device__ __forceinline__ uint4 pack8(float4 lo, float4 hi) {
   return __builtin_bit_cast(uint4, v);
 }
 
-template <int CTRL>
-__device__ __forceinline__ float dpp_f(float v) {
-  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, true));
-}
-// sum over the 16 lanes of each DPP row (all lanes receive the row sum)
-__device__ __forceinline__ float row16_sum(float v) {
-  v += dpp_f<0xB1>(v);    // quad_perm [1,0,3,2]
-  v += dpp_f<0x4E>(v);    // quad_perm [2,3,0,1]
-  v += dpp_f<0x141>(v);   // row_half_mirror
-  v += dpp_f<0x140>(v);   // row_mirror
-  return v;
-}
-
 // ---------------------------------------------------------------- pack
 struct PackPack { PackDesc d[kMaxPack]; };
 

@@ -121,6 +121,44 @@ bool heads_fast_supported(int cin, int cout);   // built (cin, cout) pairs
 int heads_fast_parts(int cin, int cout);
 int launch_heads_fast(const HeadFastArgs* h, int n, int R, hipStream_t s);
 
+// ---- encoder (snd_fast_enc.hip) ------------------------------------------
+// GraphConvolution 0 as (A X) W0: AX (fp32 [R][4], bf16 [R][8]) and
+// H1 = [BN0(lrelu(AX W0)) | X] (bf16 [R][ldh1]).
+struct Gcn0Args {
+  const int* rowptr; const int* colidx; int R;
+  const float* x; int ldx; int f;
+  const float* w0; const float* g0; const float* b0; int h0;
+  __bf16* h1; int ldh1;
+  float* ax; __bf16* axb;
+};
+int gcn0_blocks(int R);
+int launch_gcn0(const Gcn0Args& a, hipStream_t s);
+
+// bf16-input CSR SpMM: PLAIN (bf16 out) or GCN (pre-activation fp32 and
+// G = BNe([BN1(lrelu(P)) | X]) bf16).
+struct SpmmBfArgs {
+  const int* rowptr; const int* colidx; int R;
+  const __bf16* h; int ldh; int width; int epi;
+  __bf16* out; int ldo;
+  float* pre; int ldp;
+  const float* g1; const float* b1;
+  const float* x; int ldx; int f;
+  const float* ge; const float* be;
+  __bf16* g; int ldg;
+};
+int launch_spmm_bf16(const SpmmBfArgs& a, hipStream_t s);
+
+// reparameterisation backward with bf16 [dmu | dlogstd] and per-block column sums
+struct ReparamBwdFastArgs {
+  const float* ms; int ldms; int R; int L;
+  const float* eps; const float* dz_dec; const float* dJd; const float* ej;
+  float adj_scale, kl_scale;
+  __bf16* dms; int lddms;
+  float* colpart;             // [blocks][2L]
+};
+int reparam_bwd_fast_blocks(int R, int L);
+int launch_reparam_bwd_fast(const ReparamBwdFastArgs& a, hipStream_t s);
+
 int fast_init_attributes();
 int debug_flags();
 

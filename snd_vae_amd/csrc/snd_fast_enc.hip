@@ -1,0 +1,257 @@
+// bf16 fast path, encoder side (model.py:104-115, layers.py:115-125, model.py:153-161).
+//
+// GraphConvolution 0 is evaluated as (A X) W0 instead of A (X W0): the same
+// product, but the SpMM gathers the 3-wide node features (12 B per
+// neighbour) instead of 64-wide projected rows, and its backward needs no
+// SpMM at all: dW0 = X^T A dP0 = (A X)^T dP0 (A symmetric).  gcn0_kernel
+// computes AX, recomputes P0 = AX W0 in registers, applies lrelu -> frozen
+// BN and writes H1 = [B0 | X] once (bf16, the next GEMM's operand).
+//
+// spmm_bf16_kernel gathers bf16 neighbour rows (one 128-byte line per
+// neighbour for width 64), accumulates in fp32 and fuses the
+// GraphConvolution 1 epilogue (lrelu -> BN -> concat X -> encoder_g BN).
+#include "snd_fast.hpp"
+
+#include <algorithm>
+
+namespace snd {
+namespace {
+
+constexpr int NT = 256;
+constexpr int LPR = 8;             // lanes per row (aligned DPP half-rows)
+constexpr int RPB = NT / LPR;      // rows per block
+
+__device__ __forceinline__ void acc8(float (&a)[8], const uint4& u) {
+  const bf16x8 v = __builtin_bit_cast(bf16x8, u);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) a[j] += (float)v[j];
+}
+
+__device__ __forceinline__ uint4 to_bf16x8(const float (&v)[8]) {
+  bf16x8 o;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) o[j] = (__bf16)v[j];
+  return __builtin_bit_cast(uint4, o);
+}
+
+// ---------------------------------------------------------------- GCN layer 0
+__global__ void __launch_bounds__(NT) gcn0_kernel(Gcn0Args a) {
+  const int sub = threadIdx.x & (LPR - 1);
+  const int r = blockIdx.x * RPB + threadIdx.x / LPR;
+  const bool rv = r < a.R;
+  float ax[4] = {0.f, 0.f, 0.f, 0.f};
+  if (rv) {
+    const int s = a.rowptr[r], e = a.rowptr[r + 1];
+    int k = s + sub;
+    for (; k + LPR < e; k += 2 * LPR) {          // two neighbours in flight per lane
+      const int c0 = a.colidx[k], c1 = a.colidx[k + LPR];
+      float v0[4], v1[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        v0[j] = j < a.f ? a.x[(long long)c0 * a.ldx + j] : 0.f;
+        v1[j] = j < a.f ? a.x[(long long)c1 * a.ldx + j] : 0.f;
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) ax[j] += v0[j] + v1[j];
+    }
+    if (k < e) {
+      const int c0 = a.colidx[k];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) ax[j] += j < a.f ? a.x[(long long)c0 * a.ldx + j] : 0.f;
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) ax[j] = row8_sum(ax[j]);
+  if (!rv) return;
+  // P0 = AX W0 -> lrelu -> BN0 -> H1[:, :h0]   (8 columns per lane per chunk)
+  for (int c8 = sub; 8 * c8 < a.h0; c8 += LPR) {
+    float o[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int col = 8 * c8 + j;
+      float p = 0.f;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) if (q < a.f) p += ax[q] * a.w0[q * a.h0 + col];
+      o[j] = lrelu(p) * (a.g0[col] * kBnC) + a.b0[col];
+    }
+    *reinterpret_cast<uint4*>(a.h1 + (long long)r * a.ldh1 + 8 * c8) = to_bf16x8(o);
+  }
+  if (sub == 0) {
+    float xv[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) xv[j] = j < a.f ? a.x[(long long)r * a.ldx + j] : 0.f;
+    *reinterpret_cast<uint4*>(a.h1 + (long long)r * a.ldh1 + a.h0) = to_bf16x8(xv);   // concat X
+    *reinterpret_cast<float4*>(a.ax + (long long)r * 4) = make_float4(ax[0], ax[1], ax[2], ax[3]);
+    const float axp[8] = {ax[0], ax[1], ax[2], ax[3], 0.f, 0.f, 0.f, 0.f};
+    *reinterpret_cast<uint4*>(a.axb + (long long)r * 8) = to_bf16x8(axp);
+  }
+}
+
+// ---------------------------------------------------------------- bf16 SpMM
+template <int EPI>
+__global__ void __launch_bounds__(NT) spmm_bf16_kernel(SpmmBfArgs a) {
+  const int sub = threadIdx.x & (LPR - 1);
+  const int r = blockIdx.x * RPB + threadIdx.x / LPR;
+  if (r >= a.R) return;
+  const int nch = a.width >> 3;   // 8-column chunks: lane sub owns chunks sub, sub + 8
+  float acc[2][8];
+#pragma unroll
+  for (int q = 0; q < 2; ++q)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[q][j] = 0.f;
+  const int s = a.rowptr[r], e = a.rowptr[r + 1];
+  const __bf16* hb = a.h + 8 * sub;
+  bool qv[2];
+#pragma unroll
+  for (int q = 0; q < 2; ++q) qv[q] = sub + 8 * q < nch;
+  int k = s;
+  for (; k + 4 <= e; k += 4) {
+    const int c0 = a.colidx[k], c1 = a.colidx[k + 1], c2 = a.colidx[k + 2], c3 = a.colidx[k + 3];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      if (!qv[q]) continue;
+      const uint4 v0 = *reinterpret_cast<const uint4*>(hb + (long long)c0 * a.ldh + 64 * q);
+      const uint4 v1 = *reinterpret_cast<const uint4*>(hb + (long long)c1 * a.ldh + 64 * q);
+      const uint4 v2 = *reinterpret_cast<const uint4*>(hb + (long long)c2 * a.ldh + 64 * q);
+      const uint4 v3 = *reinterpret_cast<const uint4*>(hb + (long long)c3 * a.ldh + 64 * q);
+      acc8(acc[q], v0); acc8(acc[q], v1); acc8(acc[q], v2); acc8(acc[q], v3);
+    }
+  }
+  for (; k < e; ++k) {
+    const int c0 = a.colidx[k];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      if (!qv[q]) continue;
+      acc8(acc[q], *reinterpret_cast<const uint4*>(hb + (long long)c0 * a.ldh + 64 * q));
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    if (!qv[q]) continue;
+    const int col = 64 * q + 8 * sub;
+    if constexpr (EPI == SND_SPMM_PLAIN) {
+      *reinterpret_cast<uint4*>(a.out + (long long)r * a.ldo + col) = to_bf16x8(acc[q]);
+    } else {
+      float* pp = a.pre + (long long)r * a.ldp + col;
+      *reinterpret_cast<float4*>(pp) = make_float4(acc[q][0], acc[q][1], acc[q][2], acc[q][3]);
+      *reinterpret_cast<float4*>(pp + 4) = make_float4(acc[q][4], acc[q][5], acc[q][6], acc[q][7]);
+      float g[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int c = col + j;
+        const float b1 = lrelu(acc[q][j]) * (a.g1[c] * kBnC) + a.b1[c];    // H2[:, :h1]
+        g[j] = b1 * (a.ge[c] * kBnC) + a.be[c];                             // encoder_g BN
+      }
+      *reinterpret_cast<uint4*>(a.g + (long long)r * a.ldg + col) = to_bf16x8(g);
+    }
+  }
+  if constexpr (EPI == SND_SPMM_GCN) {
+    if (sub == 0) {   // concat X (model.py:109) -> encoder_g BN on those columns
+      float g[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int c = a.width + j;
+        g[j] = j < a.f ? a.x[(long long)r * a.ldx + j] * (a.ge[c] * kBnC) + a.be[c] : 0.f;
+      }
+      *reinterpret_cast<uint4*>(a.g + (long long)r * a.ldg + a.width) = to_bf16x8(g);
+    }
+  }
+}
+
+// ---------------------------------------------------------------- reparam backward
+// dz = adj_scale (dJd + ej) + dz_dec;  dmu = dz + kl mu;  dlogstd = dz eps e^s + kl (e^2s - 1)
+// (model.py:159, optimizer.py:193); bf16 output (next GEMM operand) and the
+// per-column sums that give the bias gradient of the [mu | logstd] head.
+__global__ void __launch_bounds__(NT) reparam_bwd_fast_kernel(ReparamBwdFastArgs a) {
+  const int lpr = a.L >> 2, rpb = NT / lpr;
+  const int c4 = threadIdx.x % lpr, rl = threadIdx.x / lpr;
+  float sm[4] = {0.f, 0.f, 0.f, 0.f}, ss[4] = {0.f, 0.f, 0.f, 0.f};
+  for (int r = blockIdx.x * rpb + rl; r < a.R; r += gridDim.x * rpb) {
+    const long long i = (long long)r * a.L + 4 * c4;
+    const float4 mu = *reinterpret_cast<const float4*>(a.ms + (long long)r * a.ldms + 4 * c4);
+    const float4 ls = *reinterpret_cast<const float4*>(a.ms + (long long)r * a.ldms + a.L + 4 * c4);
+    const float4 ep = *reinterpret_cast<const float4*>(a.eps + i);
+    const float4 dj = *reinterpret_cast<const float4*>(a.dJd + i);
+    const float4 ej = *reinterpret_cast<const float4*>(a.ej + i);
+    const float4 dd = *reinterpret_cast<const float4*>(a.dz_dec + i);
+    const float m[4] = {mu.x, mu.y, mu.z, mu.w}, l[4] = {ls.x, ls.y, ls.z, ls.w};
+    const float e4[4] = {ep.x, ep.y, ep.z, ep.w}, j4[4] = {dj.x, dj.y, dj.z, dj.w};
+    const float q4[4] = {ej.x, ej.y, ej.z, ej.w}, d4[4] = {dd.x, dd.y, dd.z, dd.w};
+    bf16x4 om, os;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const float es = __expf(l[t]);
+      const float dz = a.adj_scale * (j4[t] + q4[t]) + d4[t];
+      const float dm = dz + a.kl_scale * m[t];
+      const float dl = dz * e4[t] * es + a.kl_scale * (es * es - 1.f);
+      om[t] = (__bf16)dm;
+      os[t] = (__bf16)dl;
+      sm[t] += dm;
+      ss[t] += dl;
+    }
+    __bf16* o = a.dms + (long long)r * a.lddms;
+    *reinterpret_cast<bf16x4*>(o + 4 * c4) = om;
+    *reinterpret_cast<bf16x4*>(o + a.L + 4 * c4) = os;
+  }
+  __shared__ float red[NT][9];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) { red[threadIdx.x][t] = sm[t]; red[threadIdx.x][4 + t] = ss[t]; }
+  __syncthreads();
+  if (threadIdx.x < lpr) {
+    float tm[4] = {0.f, 0.f, 0.f, 0.f}, ts[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int q = 0; q < rpb; ++q)
+#pragma unroll
+      for (int t = 0; t < 4; ++t) { tm[t] += red[q * lpr + c4][t]; ts[t] += red[q * lpr + c4][4 + t]; }
+    float* cp = a.colpart + (long long)blockIdx.x * 2 * a.L;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) { cp[4 * c4 + t] = tm[t]; cp[a.L + 4 * c4 + t] = ts[t]; }
+  }
+}
+
+}  // namespace
+
+int gcn0_blocks(int R) { return cdiv(R, RPB); }
+
+int launch_gcn0(const Gcn0Args& a, hipStream_t s) {
+  if (a.R <= 0) return 0;
+  SND_CHECK_ARG(a.f >= 1 && a.f <= 4 && a.h0 % 8 == 0 && a.ldh1 % 8 == 0 && a.ldh1 >= a.h0 + 8,
+                "gcn0: f in 1..4, h0 %% 8, ldh1 >= h0 + 8");
+  SND_CHECK_ARG(a.rowptr && a.x && a.w0 && a.g0 && a.b0 && a.h1 && a.ax && a.axb, "gcn0: null operand");
+  hipLaunchKernelGGL(gcn0_kernel, dim3(gcn0_blocks(a.R)), dim3(NT), 0, s, a);
+  SND_LAUNCH_CHECK("gcn0_kernel");
+  return 0;
+}
+
+int launch_spmm_bf16(const SpmmBfArgs& a, hipStream_t s) {
+  if (a.R <= 0) return 0;
+  SND_CHECK_ARG(a.width % 8 == 0 && a.width <= 128 && a.ldh % 8 == 0, "spmm_bf16: width %% 8 <= 128, ldh %% 8");
+  dim3 grid(cdiv(a.R, RPB));
+  if (a.epi == SND_SPMM_PLAIN) {
+    SND_CHECK_ARG(a.out && a.ldo % 8 == 0, "spmm_bf16: out");
+    hipLaunchKernelGGL((spmm_bf16_kernel<SND_SPMM_PLAIN>), grid, dim3(NT), 0, s, a);
+  } else {
+    SND_CHECK_ARG(a.pre && a.g && a.g1 && a.b1 && a.ge && a.be && a.x && a.f <= 8 &&
+                      a.ldp % 4 == 0 && a.ldg % 8 == 0 && a.ldg >= a.width + 8,
+                  "spmm_bf16: GCN operands");
+    hipLaunchKernelGGL((spmm_bf16_kernel<SND_SPMM_GCN>), grid, dim3(NT), 0, s, a);
+  }
+  SND_LAUNCH_CHECK("spmm_bf16_kernel");
+  return 0;
+}
+
+int reparam_bwd_fast_blocks(int R, int L) {
+  const int rpb = NT / (L / 4);
+  return std::min(cdiv(R, rpb), 512);
+}
+
+int launch_reparam_bwd_fast(const ReparamBwdFastArgs& a, hipStream_t s) {
+  if (a.R <= 0) return 0;
+  SND_CHECK_ARG((a.L == 16 || a.L == 32 || a.L == 64 || a.L == 128) && a.ldms % 4 == 0 && a.lddms % 4 == 0,
+                "reparam_bwd_fast: L / leading dims");
+  SND_CHECK_ARG(a.dz_dec && a.dJd && a.ej && a.eps && a.dms && a.colpart, "reparam_bwd_fast: null operand");
+  hipLaunchKernelGGL(reparam_bwd_fast_kernel, dim3(reparam_bwd_fast_blocks(a.R, a.L)), dim3(NT), 0, s, a);
+  SND_LAUNCH_CHECK("reparam_bwd_fast_kernel");
+  return 0;
+}
+
+}  // namespace snd

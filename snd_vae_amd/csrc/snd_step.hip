@@ -75,6 +75,11 @@ struct snd_plan {
   int ld1 = 0, ld2 = 0, ld3 = 0;
   Img pk1f{}, pk2f{}, pk3f{}, pk3b{}, pk2b{}, pk1b{};
   WgGeom gK1{}, gK2s{}, gK2n{}, gK3s{};
+  // ---- bf16 fast encoder (snd_fast_enc.hip + row engine)
+  bool fast_enc = false;
+  int ldh1 = 0, ldg = 0;
+  Img pw1f{}, pwhf{}, pwmsf{}, pwmsb{}, pwhb{}, pw1b{};
+  WgGeom gWms{}, gWh{}, gW1{}, gW0{};
   // parameters of the last snd_train_step (snd_plan_launch re-runs kernels on them)
   mutable const float* last_params = nullptr;
   mutable float* last_grads = nullptr;
@@ -202,7 +207,7 @@ extern "C" int snd_plan_create(const snd_config_t* cfg, int n_graphs, snd_plan_t
   p->add_buf("SK3S", (long long)p->sK3s.splits * 5 * c.s2 * c.s3);
 
   // ---- bf16 fast decoder: split [s | n] column layouts, packed weight images
-  if (c.dtype == SND_BF16) {
+  if (c.dtype == SND_BF16 && !(debug_flags() & 256)) {
     const ColMap m1 = colmap_split(c.s1, c.n1), m2 = colmap_split(c.s2, c.n2);
     const int w1 = m1.phys(), w2 = m2.phys();
     auto img = [&](int kin, int nout) {
@@ -245,6 +250,46 @@ extern "C" int snd_plan_create(const snd_config_t* cfg, int n_graphs, snd_plan_t
       p->add_buf("FSK2S", (long long)p->gK2s.gx * 5 * c.s1 * c.s2);
       p->add_buf("FSK2N", (long long)p->gK2n.gx * 5 * c.n1 * c.n2);
       p->add_buf("FSK3S", (long long)p->gK3s.gx * 5 * c.s2 * c.s3);
+    }
+  }
+  // ---- bf16 fast encoder: GraphConvolution 0 as (A X) W0, bf16 operands throughout
+  if (p->fast && !(debug_flags() & 512)) {
+    auto img1 = [&](int kin, int nout) { return Img{1, kp_of(kin), (int)round_up(nout, 16), 0}; };
+    Img ims[6] = {img1(h0 + f, h1), img1(W, gh), img1(gh, 2 * L), img1(2 * L, gh), img1(gh, W), img1(h1, h0)};
+    bool ok = h0 % 8 == 0 && h1 % 8 == 0 && h1 <= 128 && f <= 4 && W <= 128 && h0 + f <= 128 &&
+              gh <= 128 && 2 * L <= 128;
+    for (auto& m : ims)
+      ok = ok && m.kp > 0 && m.np <= 128 && rc_lds_bytes(m.T, m.kp, m.np) <= kRcLdsLimit;
+    if (ok) {
+      p->fast_enc = true;
+      p->ldh1 = (int)round_up(h0 + f, 8);
+      p->ldg = (int)round_up(W, 8);
+      const char* nm[6] = {"PW1F", "PWHF", "PWMSF", "PWMSB", "PWHB", "PW1B"};
+      for (int i = 0; i < 6; ++i) {
+        p->add_buf(nm[i], (long long)pack_bytes(ims[i].T, ims[i].kp, ims[i].np), 1);
+        ims[i].off = p->bufs.back().off;
+      }
+      p->pw1f = ims[0]; p->pwhf = ims[1]; p->pwmsf = ims[2];
+      p->pwmsb = ims[3]; p->pwhb = ims[4]; p->pw1b = ims[5];
+      p->add_buf("AX", R * 4);            p->add_buf("AXB", R * 8, 2);
+      p->add_buf("FH1", R * p->ldh1, 2);  p->add_buf("FXW1", R * h1, 2);
+      p->add_buf("FP1", R * h1);          p->add_buf("FG", R * p->ldg, 2);
+      p->add_buf("FHH", R * gh, 2);       p->add_buf("FDMS", R * 2 * L, 2);
+      p->add_buf("FDH", R * gh, 2);       p->add_buf("FDP1", R * h1, 2);
+      p->add_buf("FDXW1", R * h1, 2);     p->add_buf("FDP0", R * h0, 2);
+      const int rcb = rc_blocks(p->R);
+      p->add_buf("PFBMS", (long long)reparam_bwd_fast_blocks(p->R, L) * 2 * L);
+      p->add_buf("PFBH", (long long)rcb * gh);
+      p->add_buf("PFENC1", (long long)rcb * 4 * W);
+      p->add_buf("PFENC0", (long long)rcb * 2 * h0);
+      p->gWms = wgrad_geom(p->R, 1, gh, 2 * L);
+      p->gWh = wgrad_geom(p->R, 1, W, gh);
+      p->gW1 = wgrad_geom(p->R, 1, h0 + f, h1);
+      p->gW0 = wgrad_geom(p->R, 1, f, h0);
+      p->add_buf("FSWMS", (long long)p->gWms.gx * gh * 2 * L);
+      p->add_buf("FSWH", (long long)p->gWh.gx * W * gh);
+      p->add_buf("FSW1", (long long)p->gW1.gx * (h0 + f) * h1);
+      p->add_buf("FSW0", (long long)p->gW0.gx * f * h0);
     }
   }
   *out = p;
@@ -352,11 +397,11 @@ RcArgs rc_args(const snd_plan& p, const char* ws, const Img& im, const void* x, 
 }
 
 WgArgs wg_args(const snd_plan& p, const char* ws, const WgGeom& g, const void* x, int ldx, int K, const void* dy,
-               int lddy, int N, float* slab) {
+               int lddy, int N, float* slab, int T = 5) {
   WgArgs a{};
   a.x = x; a.ldx = ldx; a.K = K; a.x_bf16 = 1;
   a.dy = dy; a.lddy = lddy; a.N = N; a.dy_bf16 = 1;
-  a.R = p.R; a.npg = p.N; a.T = 5;
+  a.R = p.R; a.npg = p.N; a.T = T;
   a.rows_per_wg = g.rows_per_wg; a.pairs_per_wg = g.pairs_per_wg;
   a.slab = slab;
   a.zero = ws + p.buf("ZERO");
@@ -387,7 +432,117 @@ int pack_decoder(const Ctx& x) {
           {src(K2s, s1, s2, 0, s1, 0, s2, 0, 0, 1), src(K2n, n1, n2, 0, n1, 0, n2, o1, o2, 1)}};
   d[5] = {dst(p.pk1b), 5, p.pk1b.kp, p.pk1b.np, 2,
           {src(K1, L, C1, 0, L, 0, s1, 0, 0, 1), src(K1, L, C1, 0, L, s1, C1, 0, o1, 1)}};
-  return launch_pack(d, 6, x.s);
+  if (!p.fast_enc) return launch_pack(d, 6, x.s);
+  PackDesc e[12]{};
+  for (int i = 0; i < 6; ++i) e[i] = d[i];
+  const int f = c.f_in, h0 = c.h0, h1 = c.h1, gh = c.g_hidden, W = p.W;
+  const float *W1 = x.w("enc.W1"), *Wh = x.w("enc.Wh"), *Wms = x.w("enc.Wms");
+  auto one = [&](const Img& im, PackSrc ps) { return PackDesc{dst(im), 1, im.kp, im.np, 1, {ps, {}}}; };
+  e[6] = one(p.pw1f, src(W1, h0 + f, h1, 0, h0 + f, 0, h1, 0, 0, 0));
+  e[7] = one(p.pwhf, src(Wh, W, gh, 0, W, 0, gh, 0, 0, 0));
+  e[8] = one(p.pwmsf, src(Wms, gh, 2 * L, 0, gh, 0, 2 * L, 0, 0, 0));
+  e[9] = one(p.pwmsb, src(Wms, gh, 2 * L, 0, gh, 0, 2 * L, 0, 0, 1));
+  e[10] = one(p.pwhb, src(Wh, W, gh, 0, W, 0, gh, 0, 0, 1));
+  e[11] = one(p.pw1b, src(W1, h0 + f, h1, 0, h0, 0, h1, 0, 0, 1));
+  return launch_pack(e, 12, x.s);
+}
+
+// encoder forward (model.py:104-115): H1 -> XW1 -> GCN1 -> heads h, [mu | logstd]
+int encoder_fast_fwd(const Ctx& x, const snd_batch_t* batch) {
+  const snd_plan& p = *x.p;
+  const snd_config_t& c = p.c;
+  const int R = p.R, L = c.latent, f = c.f_in, h0 = c.h0, h1 = c.h1, gh = c.g_hidden, W = p.W;
+  auto bf = [&](const char* n) { return reinterpret_cast<__bf16*>(x.f(n)); };
+  {
+    Gcn0Args a{batch->rowptr, batch->colidx, R, batch->features, f, f, x.w("enc.W0"),
+               x.w("enc.bn0.gamma"), x.w("enc.bn0.beta"), h0, bf("FH1"), p.ldh1, x.f("AX"), bf("AXB")};
+    SND_TRY(launch_gcn0(a, x.s));
+  }
+  {
+    RcArgs a = rc_args(p, x.ws, p.pw1f, bf("FH1"), p.ldh1, h0 + f, h1, colmap_plain(h1));
+    a.out = bf("FXW1"); a.ldo = h1; a.out_bf16 = 1;
+    SND_TRY(launch_rowconv(a, RC_LIN, x.s));
+  }
+  {
+    SpmmBfArgs a{batch->rowptr, batch->colidx, R, bf("FXW1"), h1, h1, SND_SPMM_GCN, nullptr, 0,
+                 x.f("FP1"), h1, x.w("enc.bn1.gamma"), x.w("enc.bn1.beta"), batch->features, f, f,
+                 x.w("enc.bne.gamma"), x.w("enc.bne.beta"), bf("FG"), p.ldg};
+    SND_TRY(launch_spmm_bf16(a, x.s));
+  }
+  {
+    RcArgs a = rc_args(p, x.ws, p.pwhf, bf("FG"), p.ldg, W, gh, colmap_plain(gh));
+    a.bias = x.w("enc.bh"); a.out = bf("FHH"); a.ldo = gh; a.out_bf16 = 1;
+    SND_TRY(launch_rowconv(a, RC_LIN, x.s));
+  }
+  {
+    RcArgs a = rc_args(p, x.ws, p.pwmsf, bf("FHH"), gh, gh, 2 * L, colmap_plain(2 * L));
+    a.bias = x.w("enc.bms"); a.out = x.f("MS"); a.ldo = 2 * L; a.out_bf16 = 0;
+    SND_TRY(launch_rowconv(a, RC_LIN, x.s));
+  }
+  return 0;
+}
+
+// encoder backward: reparam -> heads -> GCN1 -> GCN0 (all weight gradients as slabs)
+int encoder_fast_bwd(const Ctx& x, const snd_batch_t* batch, float adj_scale, float kl_scale) {
+  const snd_plan& p = *x.p;
+  const snd_config_t& c = p.c;
+  const int R = p.R, L = c.latent, f = c.f_in, h0 = c.h0, h1 = c.h1, gh = c.g_hidden, W = p.W;
+  auto bf = [&](const char* n) { return reinterpret_cast<__bf16*>(x.f(n)); };
+  {
+    ReparamBwdFastArgs a{x.f("MS"), 2 * L, R, L, x.f("EPS"), x.f("DZDEC"), x.f("DJD"), x.f("EJ"),
+                         adj_scale, kl_scale, bf("FDMS"), 2 * L, x.f("PFBMS")};
+    SND_TRY(launch_reparam_bwd_fast(a, x.s));
+  }
+  SND_TRY(launch_wgrad(wg_args(p, x.ws, p.gWms, bf("FHH"), gh, gh, bf("FDMS"), 2 * L, 2 * L, x.f("FSWMS"), 1), x.s));
+  {
+    RcArgs a = rc_args(p, x.ws, p.pwmsb, bf("FDMS"), 2 * L, 2 * L, gh, colmap_plain(gh));
+    a.out = bf("FDH"); a.ldo = gh; a.out_bf16 = 1; a.colpart = x.f("PFBH"); a.ncp = 1;
+    SND_TRY(launch_rowconv(a, RC_LIN, x.s));
+  }
+  SND_TRY(launch_wgrad(wg_args(p, x.ws, p.gWh, bf("FG"), p.ldg, W, bf("FDH"), gh, gh, x.f("FSWH"), 1), x.s));
+  {
+    RcArgs a = rc_args(p, x.ws, p.pwhb, bf("FDH"), gh, gh, W, colmap_plain(W));
+    a.gamma = x.w("enc.bne.gamma"); a.g2 = x.w("enc.bn1.gamma"); a.b2 = x.w("enc.bn1.beta");
+    a.p = x.f("FP1"); a.ldp = h1; a.xf = batch->features; a.ldxf = f; a.f = f; a.h = h1;
+    a.out = bf("FDP1"); a.ldo = h1; a.out_bf16 = 1; a.colpart = x.f("PFENC1"); a.ncp = 4;
+    SND_TRY(launch_rowconv(a, RC_ENC1, x.s));
+  }
+  {
+    SpmmBfArgs a{batch->rowptr, batch->colidx, R, bf("FDP1"), h1, h1, SND_SPMM_PLAIN, bf("FDXW1"), h1};
+    SND_TRY(launch_spmm_bf16(a, x.s));
+  }
+  SND_TRY(launch_wgrad(wg_args(p, x.ws, p.gW1, bf("FH1"), p.ldh1, h0 + f, bf("FDXW1"), h1, h1, x.f("FSW1"), 1), x.s));
+  {
+    RcArgs a = rc_args(p, x.ws, p.pw1b, bf("FDXW1"), h1, h1, h0, colmap_plain(h0));
+    a.gamma = x.w("enc.bn0.gamma"); a.p = x.f("AX"); a.ldp = 4; a.w0 = x.w("enc.W0"); a.f = f;
+    a.out = bf("FDP0"); a.ldo = h0; a.out_bf16 = 1; a.colpart = x.f("PFENC0"); a.ncp = 2;
+    SND_TRY(launch_rowconv(a, RC_ENC0, x.s));
+  }
+  return launch_wgrad(wg_args(p, x.ws, p.gW0, bf("AXB"), 8, f, bf("FDP0"), h0, h0, x.f("FSW0"), 1), x.s);
+}
+
+void encoder_fast_reduce(const Ctx& x, std::vector<ReduceDesc>& rd) {
+  const snd_plan& p = *x.p;
+  const snd_config_t& c = p.c;
+  const int L = c.latent, f = c.f_in, h0 = c.h0, h1 = c.h1, gh = c.g_hidden, W = p.W;
+  const int rcb = rc_blocks(p.R);
+  auto flat = [&](const char* buf, int parts, long long len, long long stride, const char* dst, float sc) {
+    rd.push_back({x.f(buf), x.g(dst), parts, (int)len, stride, sc, 0, 0, 0, 0});
+  };
+  flat("FSWMS", p.gWms.gx, (long long)gh * 2 * L, (long long)gh * 2 * L, "enc.Wms", 1.f);
+  flat("PFBMS", reparam_bwd_fast_blocks(p.R, L), 2 * L, 2 * L, "enc.bms", 1.f);
+  flat("FSWH", p.gWh.gx, (long long)W * gh, (long long)W * gh, "enc.Wh", 1.f);
+  flat("PFBH", rcb, gh, gh, "enc.bh", 1.f);
+  flat("FSW1", p.gW1.gx, (long long)(h0 + f) * h1, (long long)(h0 + f) * h1, "enc.W1", 1.f);
+  flat("FSW0", p.gW0.gx, (long long)f * h0, (long long)f * h0, "enc.W0", 1.f);
+  const float* e1 = x.f("PFENC1");
+  rd.push_back({e1, x.g("enc.bne.gamma"), rcb, W, 4LL * W, kBnC, 0, 0, 0, 0});
+  rd.push_back({e1 + W, x.g("enc.bne.beta"), rcb, W, 4LL * W, 1.f, 0, 0, 0, 0});
+  rd.push_back({e1 + 2 * W, x.g("enc.bn1.gamma"), rcb, h1, 4LL * W, kBnC, 0, 0, 0, 0});
+  rd.push_back({e1 + 3 * W, x.g("enc.bn1.beta"), rcb, h1, 4LL * W, 1.f, 0, 0, 0, 0});
+  const float* e0 = x.f("PFENC0");
+  rd.push_back({e0, x.g("enc.bn0.gamma"), rcb, h0, 2LL * h0, kBnC, 0, 0, 0, 0});
+  rd.push_back({e0 + h0, x.g("enc.bn0.beta"), rcb, h0, 2LL * h0, 1.f, 0, 0, 0, 0});
 }
 
 // decoder forward + heads + backward (model_joint.py:112-145, optimizer.py:149,153)
@@ -568,27 +723,31 @@ extern "C" int snd_train_step(const snd_plan_t* plan, const snd_batch_t* batch,
   }
 
   // =============================== forward ===============================
-  // encoder, model.py:104-112: H_{i+1} = [BN(lrelu(A (H_i W_i))) || X]
-  SND_TRY(gemm_fwd(x, R, h0, f, X, f, x.w("enc.W0"), h0, B_ROW, x.f("XW0"), h0, nullptr));
-  {
-    SpmmArgs a{rp, ci, R, x.f("XW0"), h0, h0, x.f("H1"), h0 + f, SND_SPMM_GCN,
-               x.w("enc.bn0.gamma"), x.w("enc.bn0.beta"), x.f("P0"), h0, X, f, f,
-               nullptr, nullptr, nullptr, 0};
-    SND_TRY(launch_spmm(a, x.s));
+  if (p.fast_enc) {
+    SND_TRY(encoder_fast_fwd(x, batch));
+  } else {
+    // encoder, model.py:104-112: H_{i+1} = [BN(lrelu(A (H_i W_i))) || X]
+    SND_TRY(gemm_fwd(x, R, h0, f, X, f, x.w("enc.W0"), h0, B_ROW, x.f("XW0"), h0, nullptr));
+    {
+      SpmmArgs a{rp, ci, R, x.f("XW0"), h0, h0, x.f("H1"), h0 + f, SND_SPMM_GCN,
+                 x.w("enc.bn0.gamma"), x.w("enc.bn0.beta"), x.f("P0"), h0, X, f, f,
+                 nullptr, nullptr, nullptr, 0};
+      SND_TRY(launch_spmm(a, x.s));
+    }
+    SND_TRY(gemm_fwd(x, R, h1, h0 + f, x.f("H1"), h0 + f, x.w("enc.W1"), h1, B_ROW, x.f("XW1"), h1,
+                     nullptr));
+    {
+      SpmmArgs a{rp, ci, R, x.f("XW1"), h1, h1, x.f("H2"), W, SND_SPMM_GCN,
+                 x.w("enc.bn1.gamma"), x.w("enc.bn1.beta"), x.f("P1"), h1, X, f, f,
+                 x.w("enc.bne.gamma"), x.w("enc.bne.beta"), x.f("G"), W};
+      SND_TRY(launch_spmm(a, x.s));
+    }
+    // node-wise heads (model.py:113-115): h = G Wh + bh; [mu || s] = h Wms + bms
+    SND_TRY(gemm_fwd(x, R, gh, W, x.f("G"), W, x.w("enc.Wh"), gh, B_ROW, x.f("Hh"), gh,
+                     x.w("enc.bh")));
+    SND_TRY(gemm_fwd(x, R, 2 * L, gh, x.f("Hh"), gh, x.w("enc.Wms"), 2 * L, B_ROW, x.f("MS"), 2 * L,
+                     x.w("enc.bms")));
   }
-  SND_TRY(gemm_fwd(x, R, h1, h0 + f, x.f("H1"), h0 + f, x.w("enc.W1"), h1, B_ROW, x.f("XW1"), h1,
-                   nullptr));
-  {
-    SpmmArgs a{rp, ci, R, x.f("XW1"), h1, h1, x.f("H2"), W, SND_SPMM_GCN,
-               x.w("enc.bn1.gamma"), x.w("enc.bn1.beta"), x.f("P1"), h1, X, f, f,
-               x.w("enc.bne.gamma"), x.w("enc.bne.beta"), x.f("G"), W};
-    SND_TRY(launch_spmm(a, x.s));
-  }
-  // node-wise heads (model.py:113-115): h = G Wh + bh; [mu || s] = h Wms + bms
-  SND_TRY(gemm_fwd(x, R, gh, W, x.f("G"), W, x.w("enc.Wh"), gh, B_ROW, x.f("Hh"), gh,
-                   x.w("enc.bh")));
-  SND_TRY(gemm_fwd(x, R, 2 * L, gh, x.f("Hh"), gh, x.w("enc.Wms"), 2 * L, B_ROW, x.f("MS"), 2 * L,
-                   x.w("enc.bms")));
   // z = mu + eps exp(s) (model.py:159); KL partials (optimizer.py:193)
   {
     ReparamFwdArgs a{x.f("MS"), 2 * L, R, L, eps, seed, step_counter, x.f("EPS"), x.f("Z"),
@@ -654,42 +813,46 @@ extern "C" int snd_train_step(const snd_plan_t* plan, const snd_batch_t* batch,
     SND_TRY(conv_wgrad(x, x.f("Z"), L, L, x.f("DY1"), C1, x.f("SK1"), p.sK1));
   }
   // reparameterisation + KL backward; dz = conv-decoder grad + zz^T CE grad
-  {
-    const double pairs = (double)p.B * N * (double)N;
-    // dL/dz_i = sum_j (G_ij + G_ji) z_j = 2 sum_j G_ij z_j (G symmetric)
-    const float adj_scale = (float)(2.0 * (double)c.norm / pairs);
-    const float kl_scale = (float)((double)c.beta / ((double)R * L));
-    ReparamBwdArgs a{x.f("MS"), 2 * L, R, L, x.f("EPS"), x.f("DZDEC"), x.f("DJD"), x.f("EJ"),
-                     adj_scale, kl_scale, x.f("DMS"), 2 * L};
-    SND_TRY(launch_reparam_bwd(a, x.s));
+  const double pairs = (double)p.B * N * (double)N;
+  // dL/dz_i = sum_j (G_ij + G_ji) z_j = 2 sum_j G_ij z_j (G symmetric)
+  const float adj_scale = (float)(2.0 * (double)c.norm / pairs);
+  const float kl_scale = (float)((double)c.beta / ((double)R * L));
+  if (p.fast_enc) {
+    SND_TRY(encoder_fast_bwd(x, batch, adj_scale, kl_scale));
+  } else {
+    {
+      ReparamBwdArgs a{x.f("MS"), 2 * L, R, L, x.f("EPS"), x.f("DZDEC"), x.f("DJD"), x.f("EJ"),
+                       adj_scale, kl_scale, x.f("DMS"), 2 * L};
+      SND_TRY(launch_reparam_bwd(a, x.s));
+    }
+    SND_TRY(gemm_wgrad(x, x.f("Hh"), gh, gh, true, x.f("DMS"), 2 * L, 2 * L, x.f("SWMS"), p.sWms));
+    SND_TRY(gemm_fwd(x, R, gh, 2 * L, x.f("DMS"), 2 * L, x.w("enc.Wms"), 2 * L, B_COL, x.f("DH"), gh,
+                     nullptr));
+    SND_TRY(gemm_wgrad(x, x.f("G"), W, W, true, x.f("DH"), gh, gh, x.f("SWH"), p.sWh));
+    SND_TRY(gemm_fwd(x, R, W, gh, x.f("DH"), gh, x.w("enc.Wh"), gh, B_COL, x.f("DG"), W, nullptr));
+    {
+      EncBwdArgs a{x.f("DG"), W, x.f("H2"), W, x.w("enc.bne.gamma"), W, x.f("P1"), h1,
+                   x.w("enc.bn1.gamma"), h1, x.f("DP1"), h1, x.f("PENC1"), 1};
+      SND_TRY(launch_enc_bwd(a, R, x.s));
+    }
+    {
+      SpmmArgs a{rp, ci, R, x.f("DP1"), h1, h1, x.f("DXW1"), h1, SND_SPMM_PLAIN};
+      SND_TRY(launch_spmm(a, x.s));
+    }
+    SND_TRY(gemm_wgrad(x, x.f("H1"), h0 + f, h0 + f, false, x.f("DXW1"), h1, h1, x.f("SW1"), p.sW1));
+    SND_TRY(gemm_fwd(x, R, h0, h1, x.f("DXW1"), h1, x.w("enc.W1"), h1, B_COL, x.f("DH1"), h0,
+                     nullptr));
+    {
+      EncBwdArgs a{x.f("DH1"), h0, nullptr, 0, nullptr, 0, x.f("P0"), h0, x.w("enc.bn0.gamma"), h0,
+                   x.f("DP0"), h0, x.f("PENC0"), 0};
+      SND_TRY(launch_enc_bwd(a, R, x.s));
+    }
+    {
+      SpmmArgs a{rp, ci, R, x.f("DP0"), h0, h0, x.f("DXW0"), h0, SND_SPMM_PLAIN};
+      SND_TRY(launch_spmm(a, x.s));
+    }
+    SND_TRY(gemm_wgrad(x, X, f, f, false, x.f("DXW0"), h0, h0, x.f("SW0"), p.sW0));
   }
-  SND_TRY(gemm_wgrad(x, x.f("Hh"), gh, gh, true, x.f("DMS"), 2 * L, 2 * L, x.f("SWMS"), p.sWms));
-  SND_TRY(gemm_fwd(x, R, gh, 2 * L, x.f("DMS"), 2 * L, x.w("enc.Wms"), 2 * L, B_COL, x.f("DH"), gh,
-                   nullptr));
-  SND_TRY(gemm_wgrad(x, x.f("G"), W, W, true, x.f("DH"), gh, gh, x.f("SWH"), p.sWh));
-  SND_TRY(gemm_fwd(x, R, W, gh, x.f("DH"), gh, x.w("enc.Wh"), gh, B_COL, x.f("DG"), W, nullptr));
-  {
-    EncBwdArgs a{x.f("DG"), W, x.f("H2"), W, x.w("enc.bne.gamma"), W, x.f("P1"), h1,
-                 x.w("enc.bn1.gamma"), h1, x.f("DP1"), h1, x.f("PENC1"), 1};
-    SND_TRY(launch_enc_bwd(a, R, x.s));
-  }
-  {
-    SpmmArgs a{rp, ci, R, x.f("DP1"), h1, h1, x.f("DXW1"), h1, SND_SPMM_PLAIN};
-    SND_TRY(launch_spmm(a, x.s));
-  }
-  SND_TRY(gemm_wgrad(x, x.f("H1"), h0 + f, h0 + f, false, x.f("DXW1"), h1, h1, x.f("SW1"), p.sW1));
-  SND_TRY(gemm_fwd(x, R, h0, h1, x.f("DXW1"), h1, x.w("enc.W1"), h1, B_COL, x.f("DH1"), h0,
-                   nullptr));
-  {
-    EncBwdArgs a{x.f("DH1"), h0, nullptr, 0, nullptr, 0, x.f("P0"), h0, x.w("enc.bn0.gamma"), h0,
-                 x.f("DP0"), h0, x.f("PENC0"), 0};
-    SND_TRY(launch_enc_bwd(a, R, x.s));
-  }
-  {
-    SpmmArgs a{rp, ci, R, x.f("DP0"), h0, h0, x.f("DXW0"), h0, SND_SPMM_PLAIN};
-    SND_TRY(launch_spmm(a, x.s));
-  }
-  SND_TRY(gemm_wgrad(x, X, f, f, false, x.f("DXW0"), h0, h0, x.f("SW0"), p.sW0));
 
   // ======================= deterministic gradient reduction =================
   const int nc = col_blocks(R), nh = head_blocks(R);
@@ -700,10 +863,14 @@ extern "C" int snd_train_step(const snd_plan_t* plan, const snd_batch_t* batch,
     rd.push_back({s0, x.g(wname), sp.splits, wlen, (long long)Mtot * N_, 1.f, 0});
     if (bname) rd.push_back({s0 + wlen, x.g(bname), sp.splits, N_, (long long)Mtot * N_, 1.f, 0});
   };
-  slab("SW0", p.sW0, f, h0, "enc.W0", f * h0, nullptr);
-  slab("SW1", p.sW1, h0 + f, h1, "enc.W1", (h0 + f) * h1, nullptr);
-  slab("SWH", p.sWh, W + 1, gh, "enc.Wh", W * gh, "enc.bh");
-  slab("SWMS", p.sWms, gh + 1, 2 * L, "enc.Wms", gh * 2 * L, "enc.bms");
+  if (p.fast_enc) {
+    encoder_fast_reduce(x, rd);
+  } else {
+    slab("SW0", p.sW0, f, h0, "enc.W0", f * h0, nullptr);
+    slab("SW1", p.sW1, h0 + f, h1, "enc.W1", (h0 + f) * h1, nullptr);
+    slab("SWH", p.sWh, W + 1, gh, "enc.Wh", W * gh, "enc.bh");
+    slab("SWMS", p.sWms, gh + 1, 2 * L, "enc.Wms", gh * 2 * L, "enc.bms");
+  }
   if (!p.fast) {
     slab("SK1", p.sK1, 5 * L, C1, "dec.K1", 5 * L * C1, nullptr);
     slab("SK2S", p.sK2s, 5 * s1, s2, "dec.K2s", 5 * s1 * s2, nullptr);
@@ -713,12 +880,14 @@ extern "C" int snd_train_step(const snd_plan_t* plan, const snd_batch_t* batch,
   auto cols = [&](const char* buf, int stride, int off, int len, const char* dst) {
     rd.push_back({x.f(buf) + off, x.g(dst), nc, len, (long long)stride, 1.f, 0});
   };
-  cols("PENC1", 2 * W + 2 * h1, 0, W, "enc.bne.gamma");
-  cols("PENC1", 2 * W + 2 * h1, W, W, "enc.bne.beta");
-  cols("PENC1", 2 * W + 2 * h1, 2 * W, h1, "enc.bn1.gamma");
-  cols("PENC1", 2 * W + 2 * h1, 2 * W + h1, h1, "enc.bn1.beta");
-  cols("PENC0", 2 * h0, 0, h0, "enc.bn0.gamma");
-  cols("PENC0", 2 * h0, h0, h0, "enc.bn0.beta");
+  if (!p.fast_enc) {
+    cols("PENC1", 2 * W + 2 * h1, 0, W, "enc.bne.gamma");
+    cols("PENC1", 2 * W + 2 * h1, W, W, "enc.bne.beta");
+    cols("PENC1", 2 * W + 2 * h1, 2 * W, h1, "enc.bn1.gamma");
+    cols("PENC1", 2 * W + 2 * h1, 2 * W + h1, h1, "enc.bn1.beta");
+    cols("PENC0", 2 * h0, 0, h0, "enc.bn0.gamma");
+    cols("PENC0", 2 * h0, h0, h0, "enc.bn0.beta");
+  }
   auto dec = [&](const char* buf, int w, const char* g, const char* b, const char* bias) {
     cols(buf, 3 * w, 0, w, g);
     cols(buf, 3 * w, w, w, b);

@@ -76,11 +76,13 @@ def test_train_step_bf16_vs_golden(name):
     for k in ("cost", "adj_cost", "kl"):
         assert got[k] == pytest.approx(float(z[f"s0/loss/{k}"]), rel=2e-2), k
     grads = opt.grad_blocks()
-    # bf16 operands (8-bit mantissa) in sums with cancellation: compare norm-wise
+    # bf16 operands (8-bit mantissa) in sums with cancellation: compare norm-wise.
+    # The decoder-conv gradients sit at 3-5 % on both the fast and the generic
+    # bf16 engines (tools/bf16_errors.py); encoder blocks at ~0.3 %.
     for k, g in grads.items():
         ref = z[f"s0/grad/{k}"]
         err = np.linalg.norm(g - ref) / max(np.linalg.norm(ref), 1e-30)
-        assert err < 5e-2, (k, err)
+        assert err < (1e-1 if k.startswith("dec.") else 2e-2), (k, err)
 
 
 @pytest.mark.parametrize("dtype,ltol,gtol", [("f32", 1e-5, 2e-4), ("bf16", 2e-2, 1e-1)])
