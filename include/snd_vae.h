@@ -215,7 +215,8 @@ int snd_plan_launch(const snd_plan_t* plan, const snd_batch_t* batch,
 /* Measurement only: bits that make the bf16 decoder kernels skip phases
  * (1 weight staging, 2 row staging, 4 MFMA, 8 stores, 16 column params,
  * 32 epilogue prefetch) and, read by snd_plan_create, 256 = generic-engine
- * plan, 512 = generic encoder.  0 (default) = normal operation. */
+ * plan, 512 = generic encoder; read by snd_train_step, 1024 = run the edge
+ * terms and weight gradients on a side stream.  0 (default) = normal. */
 int snd_debug_set(int flags);
 
 #ifdef __cplusplus

@@ -87,6 +87,30 @@ __device__ __forceinline__ float row16_sum(float v) {
   return v;
 }
 
+// Philox4x32-10 counter RNG + Box-Muller: eps for the reparameterisation (model.py:159),
+// keyed by (seed, step counter, element index) so a replayed graph draws fresh noise.
+__device__ __forceinline__ uint4 philox4x32_10(uint4 c, uint2 k) {
+  const unsigned M0 = 0xD2511F53u, M1 = 0xCD9E8D57u, W0 = 0x9E3779B9u, W1 = 0xBB67AE85u;
+#pragma unroll
+  for (int i = 0; i < 10; ++i) {
+    const unsigned hi0 = __umulhi(M0, c.x), lo0 = M0 * c.x;
+    const unsigned hi1 = __umulhi(M1, c.z), lo1 = M1 * c.z;
+    c = make_uint4(hi1 ^ c.y ^ k.x, lo1, hi0 ^ c.w ^ k.y, lo0);
+    k.x += W0;
+    k.y += W1;
+  }
+  return c;
+}
+
+__device__ __forceinline__ float philox_normal(unsigned long long seed, unsigned offset,
+                                               unsigned long long idx) {
+  const uint4 r = philox4x32_10(make_uint4((unsigned)idx, (unsigned)(idx >> 32), offset, 0u),
+                                make_uint2((unsigned)seed, (unsigned)(seed >> 32)));
+  const float u1 = ((float)r.x + 1.0f) * 2.3283064365386963e-10f;  // (0, 1]
+  const float u2 = (float)r.y * 2.3283064365386963e-10f;
+  return sqrtf(-2.0f * __logf(u1)) * __cosf(6.283185307179586f * u2);
+}
+
 inline int cdiv(long long a, long long b) { return (int)((a + b - 1) / b); }
 inline long long round_up(long long a, long long b) { return (a + b - 1) / b * b; }
 

@@ -10,29 +10,6 @@
 namespace snd {
 namespace {
 
-// ---------------------------------------------------------------- Philox
-__device__ __forceinline__ uint4 philox4x32_10(uint4 c, uint2 k) {
-  const unsigned M0 = 0xD2511F53u, M1 = 0xCD9E8D57u, W0 = 0x9E3779B9u, W1 = 0xBB67AE85u;
-#pragma unroll
-  for (int i = 0; i < 10; ++i) {
-    const unsigned hi0 = __umulhi(M0, c.x), lo0 = M0 * c.x;
-    const unsigned hi1 = __umulhi(M1, c.z), lo1 = M1 * c.z;
-    c = make_uint4(hi1 ^ c.y ^ k.x, lo1, hi0 ^ c.w ^ k.y, lo0);
-    k.x += W0;
-    k.y += W1;
-  }
-  return c;
-}
-
-__device__ __forceinline__ float philox_normal(unsigned long long seed, unsigned offset,
-                                               unsigned long long idx) {
-  const uint4 r = philox4x32_10(make_uint4((unsigned)idx, (unsigned)(idx >> 32), offset, 0u),
-                                make_uint2((unsigned)seed, (unsigned)(seed >> 32)));
-  const float u1 = ((float)r.x + 1.0f) * 2.3283064365386963e-10f;  // (0, 1]
-  const float u2 = (float)r.y * 2.3283064365386963e-10f;
-  return sqrtf(-2.0f * __logf(u1)) * __cosf(6.283185307179586f * u2);
-}
-
 template <typename T>
 __device__ __forceinline__ T block_sum(T v) {
   __shared__ T sh[16];
@@ -256,18 +233,21 @@ __global__ void __launch_bounds__(256) enc_bwd_kernel(EncBwdArgs a, int rows) {
 // ---------------------------------------------------------------- reduce
 struct ReducePack {
   ReduceDesc d[kMaxReduce];
+  int bstart[kMaxReduce + 1];   // first block of each descriptor (flattened 1-D grid)
 };
 
 __global__ void __launch_bounds__(256) reduce_kernel(ReducePack pk) {
-  const ReduceDesc& d = pk.d[blockIdx.y];
+  int di = 0;
+  while (di + 1 < kMaxReduce && (int)blockIdx.x >= pk.bstart[di + 1]) ++di;   // uniform
+  const ReduceDesc& d = pk.d[di];
+  const int bx = blockIdx.x - pk.bstart[di];
   __shared__ double red[256];
   const int rows = d.rows > 0 ? d.rows : 1;
   const long long items = (long long)rows * d.len;
   const int PL = d.nparts >= 64 ? 16 : 4;        // part lanes
   const int IPB = 256 / PL;                      // items per block
-  if ((long long)blockIdx.x * IPB >= items) return;   // uniform per block
   const int it = threadIdx.x % IPB, pl = threadIdx.x / IPB;
-  const long long j = (long long)blockIdx.x * IPB + it;
+  const long long j = (long long)bx * IPB + it;
   int r = 0, i = 0;
   double acc = 0.0;
   if (j < items) {
@@ -300,22 +280,30 @@ __global__ void __launch_bounds__(256) reduce_kernel(ReducePack pk) {
 }
 
 // ---------------------------------------------------------------- finalize
-__global__ void __launch_bounds__(256) finalize_kernel(FinalizeArgs a) {
+constexpr int kFinT = 1024;
+__global__ void __launch_bounds__(kFinT) finalize_kernel(FinalizeArgs a) {
+  double v[7] = {0, 0, 0, 0, 0, 0, 0};   // dl, dc, el, tp, kl, ss, sn
+#pragma unroll 4
+  for (int k = threadIdx.x; k < a.n_zzt; k += kFinT) { v[0] += a.zzt_part[2 * k]; v[1] += a.zzt_part[2 * k + 1]; }
+#pragma unroll 4
+  for (int k = threadIdx.x; k < a.n_edge; k += kFinT) { v[2] += a.edge_part[2 * k]; v[3] += a.edge_part[2 * k + 1]; }
+#pragma unroll 4
+  for (int k = threadIdx.x; k < a.n_kl; k += kFinT) v[4] += a.kl_part[k];
+#pragma unroll 4
+  for (int k = threadIdx.x; k < a.n_s; k += kFinT) { v[5] += a.sse_s[k]; v[6] += a.sse_n[k]; }
+  __shared__ double sh[kFinT / 64][7];
+#pragma unroll
+  for (int q = 0; q < 7; ++q) v[q] = wave_sum_d(v[q]);
+  if ((threadIdx.x & 63) == 0)
+#pragma unroll
+    for (int q = 0; q < 7; ++q) sh[threadIdx.x >> 6][q] = v[q];
+  __syncthreads();
   double dl = 0, dc = 0, el = 0, tp = 0, kl = 0, ss = 0, sn = 0;
-  for (int k = threadIdx.x; k < a.n_zzt; k += 256) { dl += a.zzt_part[2 * k]; dc += a.zzt_part[2 * k + 1]; }
-  for (int k = threadIdx.x; k < a.n_edge; k += 256) { el += a.edge_part[2 * k]; tp += a.edge_part[2 * k + 1]; }
-  for (int k = threadIdx.x; k < a.n_kl; k += 256) kl += a.kl_part[k];
-  for (int k = threadIdx.x; k < a.n_s; k += 256) {
-    ss += a.sse_s[k];
-    sn += a.sse_n[k];
-  }
-  dl = block_sum(dl); __syncthreads();
-  dc = block_sum(dc); __syncthreads();
-  el = block_sum(el); __syncthreads();
-  tp = block_sum(tp); __syncthreads();
-  kl = block_sum(kl); __syncthreads();
-  ss = block_sum(ss); __syncthreads();
-  sn = block_sum(sn);
+  if (threadIdx.x == 0)
+    for (int w = 0; w < kFinT / 64; ++w) {
+      dl += sh[w][0]; dc += sh[w][1]; el += sh[w][2]; tp += sh[w][3];
+      kl += sh[w][4]; ss += sh[w][5]; sn += sh[w][6];
+    }
   if (threadIdx.x != 0) return;
   const double rows = (double)a.ngraphs * a.n;
   const double pairs = rows * (double)a.n;
@@ -425,21 +413,26 @@ int launch_reduce(const ReduceDesc* d, int n, hipStream_t s) {
   for (int base = 0; base < n; base += kMaxReduce) {
     ReducePack pk{};
     const int cnt = n - base < kMaxReduce ? n - base : kMaxReduce;
-    long long gx = 1;
-    for (int i = 0; i < cnt; ++i) {
-      pk.d[i] = d[base + i];
-      const long long items = (long long)(pk.d[i].rows > 0 ? pk.d[i].rows : 1) * pk.d[i].len;
-      const int ipb = pk.d[i].nparts >= 64 ? 16 : 64;
-      gx = std::max(gx, (items + ipb - 1) / ipb);
+    long long nb = 0;
+    for (int i = 0; i < kMaxReduce; ++i) {
+      pk.bstart[i] = (int)nb;
+      if (i < cnt) {
+        pk.d[i] = d[base + i];
+        const long long items = (long long)(pk.d[i].rows > 0 ? pk.d[i].rows : 1) * pk.d[i].len;
+        const int ipb = pk.d[i].nparts >= 64 ? 16 : 64;
+        nb += (items + ipb - 1) / ipb;
+      }
     }
-    hipLaunchKernelGGL(reduce_kernel, dim3((unsigned)gx, cnt), dim3(256), 0, s, pk);
+    pk.bstart[kMaxReduce] = (int)nb;
+    if (nb == 0) continue;
+    hipLaunchKernelGGL(reduce_kernel, dim3((unsigned)nb), dim3(256), 0, s, pk);
     SND_LAUNCH_CHECK("reduce_kernel");
   }
   return 0;
 }
 
 int launch_finalize(const FinalizeArgs& a, hipStream_t s) {
-  hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(kFinT), 0, s, a);
   SND_LAUNCH_CHECK("finalize_kernel");
   return 0;
 }

@@ -525,16 +525,14 @@ __global__ void __launch_bounds__(WGT) wgrad_kernel(WgArgs a) {
   if ((a.dbg & 8) || !pv) return;
   const int k = 16 * cb + li;
   if (k >= a.K) return;
-  float* row = a.slab + (long long)blockIdx.x * T * a.K * a.N + ((long long)t * a.K + k) * a.N;
+  // slab rows padded to a multiple of 4 floats: every store is a float4
+  const int n4 = (a.N + 3) & ~3;
+  float* row = a.slab + (long long)blockIdx.x * T * a.K * n4 + ((long long)t * a.K + k) * n4;
 #pragma unroll
   for (int ob = 0; ob < NBO; ++ob) {
     const int n0 = 16 * ob + 4 * lg;
-    if ((a.N & 3) == 0 && n0 + 3 < a.N) {
+    if (n0 < a.N)
       *reinterpret_cast<float4*>(row + n0) = make_float4(acc[ob][0], acc[ob][1], acc[ob][2], acc[ob][3]);
-    } else {
-#pragma unroll
-      for (int e = 0; e < 4; ++e) if (n0 + e < a.N) row[n0 + e] = acc[ob][e];
-    }
   }
 }
 

@@ -83,7 +83,8 @@ int launch_rowconv(const RcArgs& a, int epi, hipStream_t s);
 
 // ---- weight-gradient engine ----------------------------------------------
 // slab[wg][t][k][n] = sum over the workgroup's rows r of x[r + t - H][k] * dy[r][n]
-// (same per-graph zero padding), k < K, n < N.  Deterministic partials.
+// (same per-graph zero padding), k < K, n < N; slab rows are padded to
+// n4 = round_up(N, 4) floats (wgrad_n4).  Deterministic partials.
 struct WgArgs {
   const void* x; int ldx; int K; int x_bf16;
   const void* dy; int lddy; int N; int dy_bf16;
@@ -96,6 +97,7 @@ struct WgArgs {
 };
 struct WgGeom { int rows_per_wg, pairs_per_wg, gx, gy; };
 WgGeom wgrad_geom(int R, int T, int K, int N);
+inline int wgrad_n4(int N) { return (N + 3) & ~3; }
 int launch_wgrad(const WgArgs& a, hipStream_t s);
 
 // ---- fused sigmoid head + MSE + backward + BN/lrelu backward of the head's
@@ -157,6 +159,17 @@ struct ReparamBwdFastArgs {
   float* colpart;             // [blocks][2L]
 };
 int reparam_bwd_fast_blocks(int R, int L);
+
+// reparameterisation + KL fused with the zz^T staging images (snd_zzt.hpp ZztStage)
+struct ReparamPrepArgs {
+  const float* ms; int ldms; int n, npad, ngraphs, L;
+  const float* eps_in; unsigned long long seed; const int* step;
+  float* z; float* eps_out; __bf16* zb;
+  __bf16* jrow; __bf16* jt; float* colpart;
+  double* kl_part;            // [ngraphs * npad / 64]
+};
+int reparam_prep_blocks(int ngraphs, int npad);
+int launch_reparam_prep(const ReparamPrepArgs& a, int dp, hipStream_t s);
 int launch_reparam_bwd_fast(const ReparamBwdFastArgs& a, hipStream_t s);
 
 int fast_init_attributes();

@@ -36,6 +36,14 @@ __device__ __forceinline__ uint4 to_bf16x8(const float (&v)[8]) {
 
 // ---------------------------------------------------------------- GCN layer 0
 __global__ void __launch_bounds__(NT) gcn0_kernel(Gcn0Args a) {
+  __shared__ float sp[6][128];     // W0 rows (f <= 4), gamma0 * c, beta0
+  for (int i = threadIdx.x; i < a.h0; i += NT) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) sp[q][i] = q < a.f ? a.w0[q * a.h0 + i] : 0.f;
+    sp[4][i] = a.g0[i] * kBnC;
+    sp[5][i] = a.b0[i];
+  }
+  __syncthreads();
   const int sub = threadIdx.x & (LPR - 1);
   const int r = blockIdx.x * RPB + threadIdx.x / LPR;
   const bool rv = r < a.R;
@@ -71,8 +79,8 @@ __global__ void __launch_bounds__(NT) gcn0_kernel(Gcn0Args a) {
       const int col = 8 * c8 + j;
       float p = 0.f;
 #pragma unroll
-      for (int q = 0; q < 4; ++q) if (q < a.f) p += ax[q] * a.w0[q * a.h0 + col];
-      o[j] = lrelu(p) * (a.g0[col] * kBnC) + a.b0[col];
+      for (int q = 0; q < 4; ++q) p += ax[q] * sp[q][col];
+      o[j] = lrelu(p) * sp[4][col] + sp[5][col];
     }
     *reinterpret_cast<uint4*>(a.h1 + (long long)r * a.ldh1 + 8 * c8) = to_bf16x8(o);
   }
@@ -208,14 +216,72 @@ __global__ void __launch_bounds__(NT) reparam_bwd_fast_kernel(ReparamBwdFastArgs
   }
 }
 
+
+// ---------------------------------------------------------------- reparam + zz^T staging
+// z = mu + eps e^s (model.py:159) with the KL partial (optimizer.py:193), fused
+// with the zz^T staging images: one block = 64 rows of one graph, writes z (fp32,
+// edge terms), eps, z (bf16, decoder operand), z sqrt(log2 e) (bf16, K role),
+// z^T (bf16, V role, through an LDS transpose) and the per-64-row column sums.
+template <int DP>
+__global__ void __launch_bounds__(NT) reparam_prep_kernel(ReparamPrepArgs a) {
+  __shared__ float tile[64][DP + 1];
+  __shared__ float stile[64][DP + 1];
+  __shared__ double red[NT / 64];
+  const int g = blockIdx.y, rb = blockIdx.x;
+  const int L = a.L;
+  const unsigned off = a.step ? (unsigned)(*a.step) : 0u;
+  const float sc = 1.2011224087864498f;  // sqrt(log2 e)
+  double kl = 0.0;
+  for (int idx = threadIdx.x; idx < 64 * DP; idx += NT) {
+    const int rr = idx / DP, c = idx - rr * DP;
+    const int row = rb * 64 + rr;
+    float z = 0.f;
+    if (row < a.n && c < L) {
+      const long long gr = (long long)g * a.n + row;
+      const long long i = gr * L + c;
+      const float mu = a.ms[gr * a.ldms + c];
+      const float ls = a.ms[gr * a.ldms + L + c];
+      const float eps = a.eps_in ? a.eps_in[i] : philox_normal(a.seed, off, (unsigned long long)i);
+      const float es = __expf(ls);
+      z = mu + eps * es;
+      a.z[i] = z;
+      a.eps_out[i] = eps;
+      a.zb[i] = (__bf16)z;
+      kl += (double)(1.f + 2.f * ls - mu * mu - es * es);
+    }
+    tile[rr][c] = z;
+    const __bf16 b = (__bf16)(z * sc);
+    stile[rr][c] = (float)b;
+    a.jrow[((long long)g * a.npad + row) * DP + c] = b;
+  }
+  kl = wave_sum_d(kl);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = kl;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double t = 0.0;
+    for (int k = 0; k < NT / 64; ++k) t += red[k];
+    a.kl_part[blockIdx.y * gridDim.x + blockIdx.x] = t;
+  }
+  if (threadIdx.x < DP) {
+    float cs = 0.f;
+    for (int rr = 0; rr < 64; ++rr) cs += stile[rr][threadIdx.x];
+    a.colpart[((long long)g * (a.npad / 64) + rb) * DP + threadIdx.x] = cs;
+  }
+  for (int idx = threadIdx.x; idx < 64 * DP; idx += NT) {
+    const int c = idx >> 6, rr = idx & 63;
+    a.jt[((long long)g * DP + c) * a.npad + rb * 64 + rr] = (__bf16)tile[rr][c];
+  }
+}
+
 }  // namespace
 
 int gcn0_blocks(int R) { return cdiv(R, RPB); }
 
 int launch_gcn0(const Gcn0Args& a, hipStream_t s) {
   if (a.R <= 0) return 0;
-  SND_CHECK_ARG(a.f >= 1 && a.f <= 4 && a.h0 % 8 == 0 && a.ldh1 % 8 == 0 && a.ldh1 >= a.h0 + 8,
-                "gcn0: f in 1..4, h0 %% 8, ldh1 >= h0 + 8");
+  SND_CHECK_ARG(a.f >= 1 && a.f <= 4 && a.h0 % 8 == 0 && a.h0 <= 128 && a.ldh1 % 8 == 0 &&
+                    a.ldh1 >= a.h0 + 8,
+                "gcn0: f in 1..4, h0 %% 8 (<= 128), ldh1 >= h0 + 8");
   SND_CHECK_ARG(a.rowptr && a.x && a.w0 && a.g0 && a.b0 && a.h1 && a.ax && a.axb, "gcn0: null operand");
   hipLaunchKernelGGL(gcn0_kernel, dim3(gcn0_blocks(a.R)), dim3(NT), 0, s, a);
   SND_LAUNCH_CHECK("gcn0_kernel");
@@ -236,6 +302,24 @@ int launch_spmm_bf16(const SpmmBfArgs& a, hipStream_t s) {
     hipLaunchKernelGGL((spmm_bf16_kernel<SND_SPMM_GCN>), grid, dim3(NT), 0, s, a);
   }
   SND_LAUNCH_CHECK("spmm_bf16_kernel");
+  return 0;
+}
+
+int reparam_prep_blocks(int ngraphs, int npad) { return ngraphs * (npad / 64); }
+
+int launch_reparam_prep(const ReparamPrepArgs& a, int dp, hipStream_t s) {
+  if (a.ngraphs <= 0) return 0;
+  SND_CHECK_ARG(a.npad % 64 == 0 && a.L <= dp, "reparam_prep: npad %% 64, L <= dp");
+  SND_CHECK_ARG(a.ms && a.z && a.eps_out && a.zb && a.jrow && a.jt && a.colpart && a.kl_part,
+                "reparam_prep: null operand");
+  dim3 grid(a.npad / 64, a.ngraphs);
+  switch (dp) {
+    case 32: hipLaunchKernelGGL((reparam_prep_kernel<32>), grid, dim3(NT), 0, s, a); break;
+    case 64: hipLaunchKernelGGL((reparam_prep_kernel<64>), grid, dim3(NT), 0, s, a); break;
+    case 128: hipLaunchKernelGGL((reparam_prep_kernel<128>), grid, dim3(NT), 0, s, a); break;
+    default: set_error("reparam_prep: dp %d", dp); return SND_ERR_ARG;
+  }
+  SND_LAUNCH_CHECK("reparam_prep_kernel");
   return 0;
 }
 

@@ -8,6 +8,7 @@
 // together with the RCCL gradient all-reduce and snd_adam_tf1, into one HIP
 // graph.  Forward/backward equations: SURVEY.md §8 "Composed step";
 // oracle/ref_numpy.py restates them in float64.
+#include <algorithm>
 #include <cstdarg>
 #include <cstdlib>
 #include <cstring>
@@ -83,6 +84,18 @@ struct snd_plan {
   // parameters of the last snd_train_step (snd_plan_launch re-runs kernels on them)
   mutable const float* last_params = nullptr;
   mutable float* last_grads = nullptr;
+  // side stream for the independent branches (edge terms, weight gradients); created
+  // by the first non-capturing fast-path step, joined back before the reduction
+  static constexpr int kEvents = 16;
+  mutable hipStream_t side = nullptr;
+  mutable hipEvent_t ev[kEvents] = {};
+  mutable int conc = 0;   // 0 untried, 1 available, -1 unavailable
+  ~snd_plan() {
+    if (conc == 1) {
+      for (auto& e : ev) if (e) (void)hipEventDestroy(e);
+      (void)hipStreamDestroy(side);
+    }
+  }
 
   long long blk(const char* n) const {
     for (auto& b : blocks) if (b.name == n) return b.off;
@@ -182,7 +195,7 @@ extern "C" int snd_plan_create(const snd_config_t* cfg, int n_graphs, snd_plan_t
   p->add_buf("DP0", R * h0);  p->add_buf("DXW0", R * h0);
   const int nz = zzt_dense_blocks(p->B, p->N), ne = edge_blocks(p->R, L);
   const int nk = reparam_blocks(p->R, L), nh = head_blocks(p->R), nc = col_blocks(p->R);
-  p->add_buf("PZZT", 2LL * nz, 8); p->add_buf("PEDGE", 2LL * ne, 8); p->add_buf("PKL", nk, 8);
+  p->add_buf("PZZT", 2LL * nz, 8); p->add_buf("PEDGE", 2LL * ne, 8); p->add_buf("PKL", std::max(nk, reparam_prep_blocks(p->B, zzt_npad(p->N))), 8);
   p->add_buf("PSSES", nh, 8); p->add_buf("PSSEN", nh, 8);
   p->add_buf("PHS", (long long)nh * (c.s3 * c.spatial_dim + c.spatial_dim));
   p->add_buf("PHN", (long long)nh * (c.n2 * c.num_feature + c.num_feature));
@@ -246,10 +259,10 @@ extern "C" int snd_plan_create(const snd_config_t* cfg, int n_graphs, snd_plan_t
       p->gK2s = wgrad_geom(p->R, 5, c.s1, c.s2);
       p->gK2n = wgrad_geom(p->R, 5, c.n1, c.n2);
       p->gK3s = wgrad_geom(p->R, 5, c.s2, c.s3);
-      p->add_buf("FSK1", (long long)p->gK1.gx * 5 * L * w1);
-      p->add_buf("FSK2S", (long long)p->gK2s.gx * 5 * c.s1 * c.s2);
-      p->add_buf("FSK2N", (long long)p->gK2n.gx * 5 * c.n1 * c.n2);
-      p->add_buf("FSK3S", (long long)p->gK3s.gx * 5 * c.s2 * c.s3);
+      p->add_buf("FSK1", (long long)p->gK1.gx * 5 * L * wgrad_n4(w1));
+      p->add_buf("FSK2S", (long long)p->gK2s.gx * 5 * c.s1 * wgrad_n4(c.s2));
+      p->add_buf("FSK2N", (long long)p->gK2n.gx * 5 * c.n1 * wgrad_n4(c.n2));
+      p->add_buf("FSK3S", (long long)p->gK3s.gx * 5 * c.s2 * wgrad_n4(c.s3));
     }
   }
   // ---- bf16 fast encoder: GraphConvolution 0 as (A X) W0, bf16 operands throughout
@@ -286,10 +299,10 @@ extern "C" int snd_plan_create(const snd_config_t* cfg, int n_graphs, snd_plan_t
       p->gWh = wgrad_geom(p->R, 1, W, gh);
       p->gW1 = wgrad_geom(p->R, 1, h0 + f, h1);
       p->gW0 = wgrad_geom(p->R, 1, f, h0);
-      p->add_buf("FSWMS", (long long)p->gWms.gx * gh * 2 * L);
-      p->add_buf("FSWH", (long long)p->gWh.gx * W * gh);
-      p->add_buf("FSW1", (long long)p->gW1.gx * (h0 + f) * h1);
-      p->add_buf("FSW0", (long long)p->gW0.gx * f * h0);
+      p->add_buf("FSWMS", (long long)p->gWms.gx * gh * wgrad_n4(2 * L));
+      p->add_buf("FSWH", (long long)p->gWh.gx * W * wgrad_n4(gh));
+      p->add_buf("FSW1", (long long)p->gW1.gx * (h0 + f) * wgrad_n4(h1));
+      p->add_buf("FSW0", (long long)p->gW0.gx * f * wgrad_n4(h0));
     }
   }
   *out = p;
@@ -329,11 +342,65 @@ struct Ctx {
   const float* P;
   float* Gr;
   hipStream_t s;
+  hipStream_t side = nullptr;   // null: single-stream
+  int* nev = nullptr;           // next free event of p->ev
   float* f(const char* n) const { return (float*)(ws + p->buf(n)); }
   double* d(const char* n) const { return (double*)(ws + p->buf(n)); }
   const float* w(const char* n) const { return P + p->blk(n); }
   float* g(const char* n) const { return Gr + p->blk(n); }
 };
+
+// fork: work launched on side() after this point starts after everything so far on main
+int fork(const Ctx& x) {
+  if (!x.side) return 0;
+  SND_CHECK_ARG(*x.nev < snd_plan::kEvents, "train step: out of fork events");
+  hipEvent_t e = x.p->ev[(*x.nev)++];
+  if (hipEventRecord(e, x.s) != hipSuccess || hipStreamWaitEvent(x.side, e, 0) != hipSuccess) {
+    set_error("train step: fork failed");
+    return SND_ERR_HIP;
+  }
+  return 0;
+}
+// join: main waits for everything launched on side() so far
+int join(const Ctx& x) {
+  if (!x.side) return 0;
+  SND_CHECK_ARG(*x.nev < snd_plan::kEvents, "train step: out of join events");
+  hipEvent_t e = x.p->ev[(*x.nev)++];
+  if (hipEventRecord(e, x.side) != hipSuccess || hipStreamWaitEvent(x.s, e, 0) != hipSuccess) {
+    set_error("train step: join failed");
+    return SND_ERR_HIP;
+  }
+  return 0;
+}
+hipStream_t side(const Ctx& x) { return x.side ? x.side : x.s; }
+// mark: an event after the work queued on side() so far; wait_mark: main waits for it
+int mark(const Ctx& x) {
+  if (!x.side) return -1;
+  if (*x.nev >= snd_plan::kEvents) { set_error("train step: out of events"); return -2; }
+  const int i = (*x.nev)++;
+  if (hipEventRecord(x.p->ev[i], x.side) != hipSuccess) { set_error("train step: mark failed"); return -2; }
+  return i;
+}
+int wait_mark(const Ctx& x, int i) {
+  if (i == -1) return 0;
+  if (i < 0 || hipStreamWaitEvent(x.s, x.p->ev[i], 0) != hipSuccess) {
+    set_error("train step: wait failed");
+    return SND_ERR_HIP;
+  }
+  return 0;
+}
+
+// create the side stream once, outside any stream capture
+void init_concurrency(const snd_plan& p, hipStream_t main) {
+  if (p.conc != 0) return;
+  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(main, &st) != hipSuccess || st != hipStreamCaptureStatusNone) return;
+  p.conc = -1;
+  if (hipStreamCreateWithFlags(&p.side, hipStreamNonBlocking) != hipSuccess) return;
+  for (auto& e : p.ev)
+    if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return;
+  p.conc = 1;
+}
 
 int gemm_fwd(const Ctx& x, int M, int N, int K, const float* A, int lda, const float* B, int ldb,
              int bmode, float* C, int ldc, const float* bias) {
@@ -493,13 +560,15 @@ int encoder_fast_bwd(const Ctx& x, const snd_batch_t* batch, float adj_scale, fl
                          adj_scale, kl_scale, bf("FDMS"), 2 * L, x.f("PFBMS")};
     SND_TRY(launch_reparam_bwd_fast(a, x.s));
   }
-  SND_TRY(launch_wgrad(wg_args(p, x.ws, p.gWms, bf("FHH"), gh, gh, bf("FDMS"), 2 * L, 2 * L, x.f("FSWMS"), 1), x.s));
+  SND_TRY(fork(x));
+  SND_TRY(launch_wgrad(wg_args(p, x.ws, p.gWms, bf("FHH"), gh, gh, bf("FDMS"), 2 * L, 2 * L, x.f("FSWMS"), 1), side(x)));
   {
     RcArgs a = rc_args(p, x.ws, p.pwmsb, bf("FDMS"), 2 * L, 2 * L, gh, colmap_plain(gh));
     a.out = bf("FDH"); a.ldo = gh; a.out_bf16 = 1; a.colpart = x.f("PFBH"); a.ncp = 1;
     SND_TRY(launch_rowconv(a, RC_LIN, x.s));
   }
-  SND_TRY(launch_wgrad(wg_args(p, x.ws, p.gWh, bf("FG"), p.ldg, W, bf("FDH"), gh, gh, x.f("FSWH"), 1), x.s));
+  SND_TRY(fork(x));
+  SND_TRY(launch_wgrad(wg_args(p, x.ws, p.gWh, bf("FG"), p.ldg, W, bf("FDH"), gh, gh, x.f("FSWH"), 1), side(x)));
   {
     RcArgs a = rc_args(p, x.ws, p.pwhb, bf("FDH"), gh, gh, W, colmap_plain(W));
     a.gamma = x.w("enc.bne.gamma"); a.g2 = x.w("enc.bn1.gamma"); a.b2 = x.w("enc.bn1.beta");
@@ -511,14 +580,16 @@ int encoder_fast_bwd(const Ctx& x, const snd_batch_t* batch, float adj_scale, fl
     SpmmBfArgs a{batch->rowptr, batch->colidx, R, bf("FDP1"), h1, h1, SND_SPMM_PLAIN, bf("FDXW1"), h1};
     SND_TRY(launch_spmm_bf16(a, x.s));
   }
-  SND_TRY(launch_wgrad(wg_args(p, x.ws, p.gW1, bf("FH1"), p.ldh1, h0 + f, bf("FDXW1"), h1, h1, x.f("FSW1"), 1), x.s));
+  SND_TRY(fork(x));
+  SND_TRY(launch_wgrad(wg_args(p, x.ws, p.gW1, bf("FH1"), p.ldh1, h0 + f, bf("FDXW1"), h1, h1, x.f("FSW1"), 1), side(x)));
   {
     RcArgs a = rc_args(p, x.ws, p.pw1b, bf("FDXW1"), h1, h1, h0, colmap_plain(h0));
     a.gamma = x.w("enc.bn0.gamma"); a.p = x.f("AX"); a.ldp = 4; a.w0 = x.w("enc.W0"); a.f = f;
     a.out = bf("FDP0"); a.ldo = h0; a.out_bf16 = 1; a.colpart = x.f("PFENC0"); a.ncp = 2;
     SND_TRY(launch_rowconv(a, RC_ENC0, x.s));
   }
-  return launch_wgrad(wg_args(p, x.ws, p.gW0, bf("AXB"), 8, f, bf("FDP0"), h0, h0, x.f("FSW0"), 1), x.s);
+  SND_TRY(fork(x));
+  return launch_wgrad(wg_args(p, x.ws, p.gW0, bf("AXB"), 8, f, bf("FDP0"), h0, h0, x.f("FSW0"), 1), side(x));
 }
 
 void encoder_fast_reduce(const Ctx& x, std::vector<ReduceDesc>& rd) {
@@ -529,12 +600,16 @@ void encoder_fast_reduce(const Ctx& x, std::vector<ReduceDesc>& rd) {
   auto flat = [&](const char* buf, int parts, long long len, long long stride, const char* dst, float sc) {
     rd.push_back({x.f(buf), x.g(dst), parts, (int)len, stride, sc, 0, 0, 0, 0});
   };
-  flat("FSWMS", p.gWms.gx, (long long)gh * 2 * L, (long long)gh * 2 * L, "enc.Wms", 1.f);
+  auto slab2d = [&](const char* buf, int parts, int rows, int N, const char* dst) {
+    const int n4 = wgrad_n4(N);
+    rd.push_back({x.f(buf), x.g(dst), parts, N, (long long)rows * n4, 1.f, 0, rows, n4, N});
+  };
+  slab2d("FSWMS", p.gWms.gx, gh, 2 * L, "enc.Wms");
   flat("PFBMS", reparam_bwd_fast_blocks(p.R, L), 2 * L, 2 * L, "enc.bms", 1.f);
-  flat("FSWH", p.gWh.gx, (long long)W * gh, (long long)W * gh, "enc.Wh", 1.f);
+  slab2d("FSWH", p.gWh.gx, W, gh, "enc.Wh");
   flat("PFBH", rcb, gh, gh, "enc.bh", 1.f);
-  flat("FSW1", p.gW1.gx, (long long)(h0 + f) * h1, (long long)(h0 + f) * h1, "enc.W1", 1.f);
-  flat("FSW0", p.gW0.gx, (long long)f * h0, (long long)f * h0, "enc.W0", 1.f);
+  slab2d("FSW1", p.gW1.gx, h0 + f, h1, "enc.W1");
+  slab2d("FSW0", p.gW0.gx, f, h0, "enc.W0");
   const float* e1 = x.f("PFENC1");
   rd.push_back({e1, x.g("enc.bne.gamma"), rcb, W, 4LL * W, kBnC, 0, 0, 0, 0});
   rd.push_back({e1 + W, x.g("enc.bne.beta"), rcb, W, 4LL * W, 1.f, 0, 0, 0, 0});
@@ -594,7 +669,10 @@ int decoder_fast(const Ctx& x, const snd_batch_t* batch, int only = -1) {
     a.colpart = x.f("PFDEC2S"); a.ncp = 3;
     if (only < 0 || only == 4) SND_TRY(launch_rowconv(a, RC_DECBWD, x.s));
   }
-  if (only < 0 || only == 5) SND_TRY(launch_wgrad(wg_args(p, x.ws, p.gK3s, bf("FU2"), p.ld2, s2, bf("FDY3"), p.ld3, s3, x.f("FSK3S")), x.s));
+  if (only < 0 || only == 5) {
+    SND_TRY(fork(x));
+    SND_TRY(launch_wgrad(wg_args(p, x.ws, p.gK3s, bf("FU2"), p.ld2, s2, bf("FDY3"), p.ld3, s3, x.f("FSK3S")), side(x)));
+  }
   // conv2 data gradient -> dU1, fused BN/lrelu backward of conv1 -> dY1
   {
     RcArgs a = rc_args(p, x.ws, p.pk2b, bf("FDY2"), p.ld2, w2, w1, p.m1);
@@ -603,17 +681,25 @@ int decoder_fast(const Ctx& x, const snd_batch_t* batch, int only = -1) {
     a.colpart = x.f("PFDEC1"); a.ncp = 3;
     if (only < 0 || only == 6) SND_TRY(launch_rowconv(a, RC_DECBWD, x.s));
   }
-  if (only < 0 || only == 7) SND_TRY(launch_wgrad(wg_args(p, x.ws, p.gK2s, bf("FU1"), p.ld1, c.s1, bf("FDY2"), p.ld2, s2, x.f("FSK2S")), x.s));
-  if (only < 0 || only == 8) SND_TRY(launch_wgrad(wg_args(p, x.ws, p.gK2n, bf("FU1") + o1, p.ld1, c.n1, bf("FDY2") + o2, p.ld2, n2,
-                               x.f("FSK2N")), x.s));
+  if (only < 0 || only == 7) {
+    SND_TRY(fork(x));
+    SND_TRY(launch_wgrad(wg_args(p, x.ws, p.gK2s, bf("FU1"), p.ld1, c.s1, bf("FDY2"), p.ld2, s2, x.f("FSK2S")), side(x)));
+  }
+  if (only < 0 || only == 8) {
+    SND_TRY(fork(x));
+    SND_TRY(launch_wgrad(wg_args(p, x.ws, p.gK2n, bf("FU1") + o1, p.ld1, c.n1, bf("FDY2") + o2, p.ld2, n2,
+                               x.f("FSK2N")), side(x)));
+  }
   // conv1 data gradient -> dz (decoder part)
   {
     RcArgs a = rc_args(p, x.ws, p.pk1b, bf("FDY1"), p.ld1, w1, L, colmap_plain(L));
     a.out = x.f("DZDEC"); a.ldo = L; a.out_bf16 = 0;
     if (only < 0 || only == 9) SND_TRY(launch_rowconv(a, RC_LIN, x.s));
   }
-  if (only < 0 || only == 10)
-    SND_TRY(launch_wgrad(wg_args(p, x.ws, p.gK1, bf("ZB"), L, L, bf("FDY1"), p.ld1, w1, x.f("FSK1")), x.s));
+  if (only < 0 || only == 10) {
+    SND_TRY(fork(x));
+    SND_TRY(launch_wgrad(wg_args(p, x.ws, p.gK1, bf("ZB"), L, L, bf("FDY1"), p.ld1, w1, x.f("FSK1")), side(x)));
+  }
   return 0;
 }
 
@@ -625,16 +711,19 @@ void decoder_fast_reduce(const Ctx& x, std::vector<ReduceDesc>& rd) {
   const int sd = c.spatial_dim, nf = c.num_feature;
   const int w1 = p.m1.phys(), o1 = p.m1.offb;
   const int rcb = rc_blocks(p.R), hb = heads_fast_blocks(p.R);
-  auto flat = [&](const char* buf, int parts, long long len, const char* dst) {
-    rd.push_back({x.f(buf), x.g(dst), parts, (int)len, len, 1.f, 0, 0, 0, 0});
+  // slab [parts][rows][n4] -> weight [rows][N]
+  auto slab2d = [&](const char* buf, int parts, int rows, int N, const char* dst) {
+    const int n4 = wgrad_n4(N);
+    rd.push_back({x.f(buf), x.g(dst), parts, N, (long long)rows * n4, 1.f, 0, rows, n4, N});
   };
-  flat("FSK3S", p.gK3s.gx, 5LL * s2 * s3, "dec.K3s");
-  flat("FSK2S", p.gK2s.gx, 5LL * s1 * s2, "dec.K2s");
-  flat("FSK2N", p.gK2n.gx, 5LL * n1 * n2, "dec.K2n");
+  slab2d("FSK3S", p.gK3s.gx, 5 * s2, s3, "dec.K3s");
+  slab2d("FSK2S", p.gK2s.gx, 5 * s1, s2, "dec.K2s");
+  slab2d("FSK2N", p.gK2n.gx, 5 * n1, n2, "dec.K2n");
   {  // [5][L][w1] split columns -> dec.K1 [5][L][C1]
-    const long long st = 5LL * L * w1;
-    rd.push_back({x.f("FSK1"), x.g("dec.K1"), p.gK1.gx, s1, st, 1.f, 0, 5 * L, w1, C1});
-    rd.push_back({x.f("FSK1") + o1, x.g("dec.K1") + s1, p.gK1.gx, n1, st, 1.f, 0, 5 * L, w1, C1});
+    const int n4 = wgrad_n4(w1);
+    const long long st = 5LL * L * n4;
+    rd.push_back({x.f("FSK1"), x.g("dec.K1"), p.gK1.gx, s1, st, 1.f, 0, 5 * L, n4, C1});
+    rd.push_back({x.f("FSK1") + o1, x.g("dec.K1") + s1, p.gK1.gx, n1, st, 1.f, 0, 5 * L, n4, C1});
   }
   // per-column partials {sum dt*y (x c), sum dt, sum dy} -> gamma, beta, bias
   auto cols3 = [&](const char* buf, int parts, int width, int src0, int len, const char* g,
@@ -711,6 +800,14 @@ extern "C" int snd_train_step(const snd_plan_t* plan, const snd_batch_t* batch,
   Ctx x{&p, (char*)workspace, params, grads, (hipStream_t)stream};
   p.last_params = params;
   p.last_grads = grads;
+  int nev = 0;
+  // Side-stream branches are opt-in (debug bit 1024): on ROCm 7.2 a captured
+  // graph spreads them over several hardware queues, and the cross-queue
+  // dependencies cost more (5-12 us each, measured) than the overlap saves.
+  if (p.fast && (debug_flags() & 1024)) {
+    init_concurrency(p, x.s);
+    if (p.conc == 1) { x.side = p.side; x.nev = &nev; }
+  }
   const int R = p.R, N = p.N, f = c.f_in, h0 = c.h0, h1 = c.h1, gh = c.g_hidden, L = c.latent;
   const int W = p.W, C1 = p.C1, s1 = c.s1, s2 = c.s2, s3 = c.s3, n1 = c.n1, n2 = c.n2;
   const int sd = c.spatial_dim, nf = c.num_feature;
@@ -749,19 +846,29 @@ extern "C" int snd_train_step(const snd_plan_t* plan, const snd_batch_t* batch,
                      x.w("enc.bms")));
   }
   // z = mu + eps exp(s) (model.py:159); KL partials (optimizer.py:193)
-  {
+  const ZztStage stg = zzt_stage(x.ws + p.buf("ZSTAGE"), p.B, N, L, c.dtype);
+  if (p.fast) {   // fused with the zz^T staging images
+    ReparamPrepArgs a{x.f("MS"), 2 * L, N, zzt_npad(N), p.B, L, eps, seed, step_counter, x.f("Z"),
+                      x.f("EPS"), (__bf16*)x.f("ZB"), (__bf16*)stg.jrow, (__bf16*)stg.jt, stg.colpart,
+                      x.d("PKL")};
+    SND_TRY(launch_reparam_prep(a, zzt_dp(L), x.s));
+  } else {
     ReparamFwdArgs a{x.f("MS"), 2 * L, R, L, eps, seed, step_counter, x.f("EPS"), x.f("Z"),
-                     x.d("PKL"), p.fast ? (__bf16*)x.f("ZB") : nullptr, L};
+                     x.d("PKL"), nullptr, L};
     SND_TRY(launch_reparam_fwd(a, x.s));
   }
   // inner-product decoder + CE (fused) and per-edge terms
+  int edge_mark = -1;
   {
-    const ZztStage stg = zzt_stage(x.ws + p.buf("ZSTAGE"), p.B, N, L, c.dtype);
-    SND_TRY(launch_zzt_prep(x.f("Z"), p.B, N, L, c.dtype, stg, x.s));
+    // per-edge terms on the side stream, overlapping the dense kernel / decoder
+    SND_TRY(fork(x));
+    EdgeArgs ea{rp, ci, R, x.f("Z"), L, c.pos_weight, x.f("EJ"), x.d("PEDGE")};
+    SND_TRY(launch_edge(ea, side(x)));
+    edge_mark = mark(x);
+    if (edge_mark < -1) return SND_ERR_HIP;
+    if (!p.fast) SND_TRY(launch_zzt_prep(x.f("Z"), p.B, N, L, c.dtype, stg, x.s));
     ZztArgs za{stg.jrow, stg.jt, N, zzt_npad(N), p.B, L, x.f("DJD"), x.d("PZZT"), stg.colpart, 0};
     SND_TRY(launch_zzt_dense(za, c.dtype, x.s));
-    EdgeArgs ea{rp, ci, R, x.f("Z"), L, c.pos_weight, x.f("EJ"), x.d("PEDGE")};
-    SND_TRY(launch_edge(ea, x.s));
   }
   if (p.fast) {
     SND_TRY(decoder_fast(x, batch));
@@ -817,6 +924,7 @@ extern "C" int snd_train_step(const snd_plan_t* plan, const snd_batch_t* batch,
   // dL/dz_i = sum_j (G_ij + G_ji) z_j = 2 sum_j G_ij z_j (G symmetric)
   const float adj_scale = (float)(2.0 * (double)c.norm / pairs);
   const float kl_scale = (float)((double)c.beta / ((double)R * L));
+  SND_TRY(wait_mark(x, edge_mark));   // EJ
   if (p.fast_enc) {
     SND_TRY(encoder_fast_bwd(x, batch, adj_scale, kl_scale));
   } else {
@@ -853,6 +961,8 @@ extern "C" int snd_train_step(const snd_plan_t* plan, const snd_batch_t* batch,
     }
     SND_TRY(gemm_wgrad(x, X, f, f, false, x.f("DXW0"), h0, h0, x.f("SW0"), p.sW0));
   }
+
+  SND_TRY(join(x));   // weight-gradient slabs from the side stream
 
   // ======================= deterministic gradient reduction =================
   const int nc = col_blocks(R), nh = head_blocks(R);
@@ -909,7 +1019,7 @@ extern "C" int snd_train_step(const snd_plan_t* plan, const snd_batch_t* batch,
   SND_TRY(launch_reduce(rd.data(), (int)rd.size(), x.s));
 
   FinalizeArgs fa{x.d("PZZT"), zzt_dense_blocks(p.B, N), x.d("PEDGE"), edge_blocks(R, L),
-                  x.d("PKL"), reparam_blocks(R, L), x.d("PSSES"), x.d("PSSEN"), nh,
+                  x.d("PKL"), p.fast ? reparam_prep_blocks(p.B, zzt_npad(N)) : reparam_blocks(R, L), x.d("PSSES"), x.d("PSSEN"), nh,
                   rp, p.B, N, L, sd, nf, c.beta, c.norm, losses, grads + p.pcount, step_counter};
   return launch_finalize(fa, x.s);
 }
