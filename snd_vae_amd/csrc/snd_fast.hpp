@@ -132,7 +132,9 @@ struct Gcn0Args {
   const float* w0; const float* g0; const float* b0; int h0;
   __bf16* h1; int ldh1;
   float* ax; __bf16* axb;
+  int xcd_nbg;                // xcd_nbg(): row blocks per graph for the XCD-aware order
 };
+int xcd_nbg(int npg, int ngraphs);
 int gcn0_blocks(int R);
 int launch_gcn0(const Gcn0Args& a, hipStream_t s);
 
@@ -147,6 +149,7 @@ struct SpmmBfArgs {
   const float* x; int ldx; int f;
   const float* ge; const float* be;
   __bf16* g; int ldg;
+  int xcd_nbg;
 };
 int launch_spmm_bf16(const SpmmBfArgs& a, hipStream_t s);
 
@@ -169,6 +172,18 @@ struct ReparamPrepArgs {
   double* kl_part;            // [ngraphs * npad / 64]
 };
 int reparam_prep_blocks(int ngraphs, int npad);
+
+// per-edge CE terms from the bf16 z copy (snd_spmm.hpp EdgeArgs semantics)
+struct EdgeBfArgs {
+  const int* rowptr; const int* colidx; int R;
+  const __bf16* z; int d;
+  float pos_weight;
+  float* ej;                  // [R][d]
+  double* part;               // [blocks][2] = {loss, tp}
+  int xcd_nbg;
+};
+int edge_bf16_blocks(int R);
+int launch_edge_bf16(const EdgeBfArgs& a, hipStream_t s);
 int launch_reparam_prep(const ReparamPrepArgs& a, int dp, hipStream_t s);
 int launch_reparam_bwd_fast(const ReparamBwdFastArgs& a, hipStream_t s);
 

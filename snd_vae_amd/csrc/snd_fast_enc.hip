@@ -34,6 +34,38 @@ __device__ __forceinline__ uint4 to_bf16x8(const float (&v)[8]) {
   return __builtin_bit_cast(uint4, o);
 }
 
+
+
+// XCD-aware row-block order: blocks b and b + 8 share an XCD (and its L2), so
+// row blocks of graph g go to block group g % 8 -- a graph's gathered rows
+// (<= 1 MB) then stay in one L2.  nbg = row blocks per graph (0: identity).
+__device__ __forceinline__ int xcd_rowblock(int b, int nbg) {
+  if (nbg <= 0) return b;
+  const int x = b & 7, s = b >> 3;
+  const int gi = s / nbg, lb = s - gi * nbg;
+  return (x + 8 * gi) * nbg + lb;
+}
+
+// Neighbour lists of the block's RPB consecutive rows staged in LDS (one
+// coalesced pass; falls back to global reads past kNbrCap entries).
+constexpr int kNbrCap = 2048;
+struct NbrLds {
+  int base, cnt;
+  __device__ __forceinline__ int at(const int* lds, const int* colidx, int k) const {
+    return cnt <= kNbrCap ? lds[k - base] : colidx[k];
+  }
+};
+__device__ __forceinline__ NbrLds stage_nbrs(const int* rowptr, const int* colidx, int R, int r0,
+                                            int* lds) {
+  const int rl = min(R, r0 + RPB);
+  const int b = rowptr[r0], e = rowptr[rl];
+  NbrLds n{b, e - b};
+  if (n.cnt <= kNbrCap)
+    for (int i = threadIdx.x; i < n.cnt; i += NT) lds[i] = colidx[b + i];
+  __syncthreads();
+  return n;
+}
+
 // ---------------------------------------------------------------- GCN layer 0
 __global__ void __launch_bounds__(NT) gcn0_kernel(Gcn0Args a) {
   __shared__ float sp[6][128];     // W0 rows (f <= 4), gamma0 * c, beta0
@@ -45,7 +77,7 @@ __global__ void __launch_bounds__(NT) gcn0_kernel(Gcn0Args a) {
   }
   __syncthreads();
   const int sub = threadIdx.x & (LPR - 1);
-  const int r = blockIdx.x * RPB + threadIdx.x / LPR;
+  const int r = xcd_rowblock(blockIdx.x, a.xcd_nbg) * RPB + threadIdx.x / LPR;
   const bool rv = r < a.R;
   float ax[4] = {0.f, 0.f, 0.f, 0.f};
   if (rv) {
@@ -98,8 +130,11 @@ __global__ void __launch_bounds__(NT) gcn0_kernel(Gcn0Args a) {
 // ---------------------------------------------------------------- bf16 SpMM
 template <int EPI>
 __global__ void __launch_bounds__(NT) spmm_bf16_kernel(SpmmBfArgs a) {
+  __shared__ int nb_lds[kNbrCap];
   const int sub = threadIdx.x & (LPR - 1);
-  const int r = blockIdx.x * RPB + threadIdx.x / LPR;
+  const int rb = xcd_rowblock(blockIdx.x, a.xcd_nbg);
+  const int r = rb * RPB + threadIdx.x / LPR;
+  const NbrLds nl = stage_nbrs(a.rowptr, a.colidx, a.R, rb * RPB, nb_lds);
   if (r >= a.R) return;
   const int nch = a.width >> 3;   // 8-column chunks: lane sub owns chunks sub, sub + 8
   float acc[2][8];
@@ -114,7 +149,8 @@ __global__ void __launch_bounds__(NT) spmm_bf16_kernel(SpmmBfArgs a) {
   for (int q = 0; q < 2; ++q) qv[q] = sub + 8 * q < nch;
   int k = s;
   for (; k + 4 <= e; k += 4) {
-    const int c0 = a.colidx[k], c1 = a.colidx[k + 1], c2 = a.colidx[k + 2], c3 = a.colidx[k + 3];
+    const int c0 = nl.at(nb_lds, a.colidx, k), c1 = nl.at(nb_lds, a.colidx, k + 1);
+    const int c2 = nl.at(nb_lds, a.colidx, k + 2), c3 = nl.at(nb_lds, a.colidx, k + 3);
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
       if (!qv[q]) continue;
@@ -126,7 +162,7 @@ __global__ void __launch_bounds__(NT) spmm_bf16_kernel(SpmmBfArgs a) {
     }
   }
   for (; k < e; ++k) {
-    const int c0 = a.colidx[k];
+    const int c0 = nl.at(nb_lds, a.colidx, k);
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
       if (!qv[q]) continue;
@@ -163,6 +199,98 @@ __global__ void __launch_bounds__(NT) spmm_bf16_kernel(SpmmBfArgs a) {
       }
       *reinterpret_cast<uint4*>(a.g + (long long)r * a.ldg + a.width) = to_bf16x8(g);
     }
+  }
+}
+
+// ---------------------------------------------------------------- per-edge CE terms (bf16 z)
+// For row i and each neighbour j (A_ij = 1), L = z_i . z_j:
+//   loss += (pw - 1) softplus(L) - pw L ;  tp += (L > 0) ;  ej_i += ((pw - 1) sigmoid(L) - pw) z_j
+// (optimizer.py:142-144 restricted to the A = 1 pairs; the dense kernel adds softplus(L)
+// over all pairs).  8 lanes per row, one 16-byte z chunk per lane, 4 neighbours in flight.
+__global__ void __launch_bounds__(NT) edge_bf16_kernel(EdgeBfArgs a) {
+  __shared__ int nb_lds[kNbrCap];
+  __shared__ double sl[NT / 64];
+  __shared__ unsigned st[NT / 64];
+  const int sub = threadIdx.x & (LPR - 1);
+  const int rb = xcd_rowblock(blockIdx.x, a.xcd_nbg);
+  const int r = rb * RPB + threadIdx.x / LPR;
+  const NbrLds nl = stage_nbrs(a.rowptr, a.colidx, a.R, rb * RPB, nb_lds);
+  const int nch = a.d >> 3;
+  bool qv[2];
+#pragma unroll
+  for (int q = 0; q < 2; ++q) qv[q] = sub + 8 * q < nch;
+  float lossr = 0.f;
+  unsigned tp = 0;
+  if (r < a.R) {
+    float zi[2][8], acc[2][8];
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { zi[q][j] = 0.f; acc[q][j] = 0.f; }
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+      if (qv[q]) {
+        const bf16x8 v = *reinterpret_cast<const bf16x8*>(a.z + (long long)r * a.d + 64 * q + 8 * sub);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) zi[q][j] = (float)v[j];
+      }
+    const float pw = a.pos_weight;
+    const int s = a.rowptr[r], e = a.rowptr[r + 1];
+    for (int k = s; k < e; k += 4) {
+      float zj[4][2][8], dot[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const bool uv = k + u < e;
+        const int c = uv ? nl.at(nb_lds, a.colidx, k + u) : r;
+        dot[u] = 0.f;
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          bf16x8 v{};
+          if (qv[q]) v = *reinterpret_cast<const bf16x8*>(a.z + (long long)c * a.d + 64 * q + 8 * sub);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            zj[u][q][j] = uv ? (float)v[j] : 0.f;
+            dot[u] += zi[q][j] * zj[u][q][j];
+          }
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const float L = row8_sum(dot[u]);
+        if (k + u >= e) continue;
+        float coef = -pw;
+        if (pw != 1.f) {
+          const float sg = 1.f / (1.f + __expf(-L));
+          coef += (pw - 1.f) * sg;
+          lossr += (pw - 1.f) * (fmaxf(L, 0.f) + log1pf(__expf(-fabsf(L))));
+        }
+        lossr -= pw * L;
+        tp += L > 0.f ? 1u : 0u;
+#pragma unroll
+        for (int q = 0; q < 2; ++q)
+#pragma unroll
+          for (int j = 0; j < 8; ++j) acc[q][j] += coef * zj[u][q][j];
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+      if (qv[q]) {
+        float* o = a.ej + (long long)r * a.d + 64 * q + 8 * sub;
+        *reinterpret_cast<float4*>(o) = make_float4(acc[q][0], acc[q][1], acc[q][2], acc[q][3]);
+        *reinterpret_cast<float4*>(o + 4) = make_float4(acc[q][4], acc[q][5], acc[q][6], acc[q][7]);
+      }
+    if (sub != 0) { lossr = 0.f; tp = 0; }   // the row's 8 lanes hold the same sums
+  }
+  const double l = wave_sum_d((double)lossr);
+  const unsigned t = wave_sum_u(tp);
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) { sl[w] = l; st[w] = t; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double tl = 0.0, tt = 0.0;
+    for (int k = 0; k < NT / 64; ++k) { tl += sl[k]; tt += (double)st[k]; }
+    a.part[2 * blockIdx.x] = tl;
+    a.part[2 * blockIdx.x + 1] = tt;
   }
 }
 
@@ -277,6 +405,10 @@ __global__ void __launch_bounds__(NT) reparam_prep_kernel(ReparamPrepArgs a) {
 
 int gcn0_blocks(int R) { return cdiv(R, RPB); }
 
+int xcd_nbg(int npg, int ngraphs) {
+  return (npg % RPB == 0 && ngraphs % 8 == 0) ? npg / RPB : 0;
+}
+
 int launch_gcn0(const Gcn0Args& a, hipStream_t s) {
   if (a.R <= 0) return 0;
   SND_CHECK_ARG(a.f >= 1 && a.f <= 4 && a.h0 % 8 == 0 && a.h0 <= 128 && a.ldh1 % 8 == 0 &&
@@ -302,6 +434,16 @@ int launch_spmm_bf16(const SpmmBfArgs& a, hipStream_t s) {
     hipLaunchKernelGGL((spmm_bf16_kernel<SND_SPMM_GCN>), grid, dim3(NT), 0, s, a);
   }
   SND_LAUNCH_CHECK("spmm_bf16_kernel");
+  return 0;
+}
+
+int edge_bf16_blocks(int R) { return cdiv(R, RPB); }
+
+int launch_edge_bf16(const EdgeBfArgs& a, hipStream_t s) {
+  if (a.R <= 0) return 0;
+  SND_CHECK_ARG(a.d % 8 == 0 && a.d <= 128 && a.z && a.ej && a.part && a.rowptr, "edge_bf16: operands");
+  hipLaunchKernelGGL(edge_bf16_kernel, dim3(edge_bf16_blocks(a.R)), dim3(NT), 0, s, a);
+  SND_LAUNCH_CHECK("edge_bf16_kernel");
   return 0;
 }
 

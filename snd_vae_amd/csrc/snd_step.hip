@@ -195,7 +195,7 @@ extern "C" int snd_plan_create(const snd_config_t* cfg, int n_graphs, snd_plan_t
   p->add_buf("DP0", R * h0);  p->add_buf("DXW0", R * h0);
   const int nz = zzt_dense_blocks(p->B, p->N), ne = edge_blocks(p->R, L);
   const int nk = reparam_blocks(p->R, L), nh = head_blocks(p->R), nc = col_blocks(p->R);
-  p->add_buf("PZZT", 2LL * nz, 8); p->add_buf("PEDGE", 2LL * ne, 8); p->add_buf("PKL", std::max(nk, reparam_prep_blocks(p->B, zzt_npad(p->N))), 8);
+  p->add_buf("PZZT", 2LL * nz, 8); p->add_buf("PEDGE", 2LL * std::max(ne, edge_bf16_blocks(p->R)), 8); p->add_buf("PKL", std::max(nk, reparam_prep_blocks(p->B, zzt_npad(p->N))), 8);
   p->add_buf("PSSES", nh, 8); p->add_buf("PSSEN", nh, 8);
   p->add_buf("PHS", (long long)nh * (c.s3 * c.spatial_dim + c.spatial_dim));
   p->add_buf("PHN", (long long)nh * (c.n2 * c.num_feature + c.num_feature));
@@ -522,7 +522,8 @@ int encoder_fast_fwd(const Ctx& x, const snd_batch_t* batch) {
   auto bf = [&](const char* n) { return reinterpret_cast<__bf16*>(x.f(n)); };
   {
     Gcn0Args a{batch->rowptr, batch->colidx, R, batch->features, f, f, x.w("enc.W0"),
-               x.w("enc.bn0.gamma"), x.w("enc.bn0.beta"), h0, bf("FH1"), p.ldh1, x.f("AX"), bf("AXB")};
+               x.w("enc.bn0.gamma"), x.w("enc.bn0.beta"), h0, bf("FH1"), p.ldh1, x.f("AX"), bf("AXB"),
+               xcd_nbg(p.N, p.B)};
     SND_TRY(launch_gcn0(a, x.s));
   }
   {
@@ -533,7 +534,7 @@ int encoder_fast_fwd(const Ctx& x, const snd_batch_t* batch) {
   {
     SpmmBfArgs a{batch->rowptr, batch->colidx, R, bf("FXW1"), h1, h1, SND_SPMM_GCN, nullptr, 0,
                  x.f("FP1"), h1, x.w("enc.bn1.gamma"), x.w("enc.bn1.beta"), batch->features, f, f,
-                 x.w("enc.bne.gamma"), x.w("enc.bne.beta"), bf("FG"), p.ldg};
+                 x.w("enc.bne.gamma"), x.w("enc.bne.beta"), bf("FG"), p.ldg, xcd_nbg(p.N, p.B)};
     SND_TRY(launch_spmm_bf16(a, x.s));
   }
   {
@@ -578,6 +579,7 @@ int encoder_fast_bwd(const Ctx& x, const snd_batch_t* batch, float adj_scale, fl
   }
   {
     SpmmBfArgs a{batch->rowptr, batch->colidx, R, bf("FDP1"), h1, h1, SND_SPMM_PLAIN, bf("FDXW1"), h1};
+    a.xcd_nbg = xcd_nbg(p.N, p.B);
     SND_TRY(launch_spmm_bf16(a, x.s));
   }
   SND_TRY(fork(x));
@@ -862,8 +864,14 @@ extern "C" int snd_train_step(const snd_plan_t* plan, const snd_batch_t* batch,
   {
     // per-edge terms on the side stream, overlapping the dense kernel / decoder
     SND_TRY(fork(x));
-    EdgeArgs ea{rp, ci, R, x.f("Z"), L, c.pos_weight, x.f("EJ"), x.d("PEDGE")};
-    SND_TRY(launch_edge(ea, side(x)));
+    if (p.fast) {
+      EdgeBfArgs ea{rp, ci, R, (const __bf16*)x.f("ZB"), L, c.pos_weight, x.f("EJ"), x.d("PEDGE"),
+                    xcd_nbg(N, p.B)};
+      SND_TRY(launch_edge_bf16(ea, side(x)));
+    } else {
+      EdgeArgs ea{rp, ci, R, x.f("Z"), L, c.pos_weight, x.f("EJ"), x.d("PEDGE")};
+      SND_TRY(launch_edge(ea, side(x)));
+    }
     edge_mark = mark(x);
     if (edge_mark < -1) return SND_ERR_HIP;
     if (!p.fast) SND_TRY(launch_zzt_prep(x.f("Z"), p.B, N, L, c.dtype, stg, x.s));
@@ -1018,7 +1026,8 @@ extern "C" int snd_train_step(const snd_plan_t* plan, const snd_batch_t* batch,
   }
   SND_TRY(launch_reduce(rd.data(), (int)rd.size(), x.s));
 
-  FinalizeArgs fa{x.d("PZZT"), zzt_dense_blocks(p.B, N), x.d("PEDGE"), edge_blocks(R, L),
+  FinalizeArgs fa{x.d("PZZT"), zzt_dense_blocks(p.B, N), x.d("PEDGE"),
+                  p.fast ? edge_bf16_blocks(R) : edge_blocks(R, L),
                   x.d("PKL"), p.fast ? reparam_prep_blocks(p.B, zzt_npad(N)) : reparam_blocks(R, L), x.d("PSSES"), x.d("PSSEN"), nh,
                   rp, p.B, N, L, sd, nf, c.beta, c.norm, losses, grads + p.pcount, step_counter};
   return launch_finalize(fa, x.s);
