@@ -208,8 +208,9 @@ int snd_train_step(const snd_plan_t* plan, const snd_batch_t* batch,
                    int* step_counter, double* losses, snd_stream_t stream);
 /* Re-launch one kernel of the step on the workspace state left by the last
  * snd_train_step (measurement/profiling): "zzt_dense" (fused zz^T + CE),
- * "spmm_dxw1" (plain CSR SpMM, width h1), "pack" / "dec:<k>" (bf16 decoder
- * weight packing / k-th decoder kernel, k = 0..10). */
+ * "spmm_dxw1" (plain fp32 CSR SpMM, width h1; generic-engine plans),
+ * "spmm_bf16" (the bf16 path's A @ dP1), "pack" / "dec:<k>" (bf16 weight
+ * packing / k-th bf16 decoder kernel, k = 0..10). */
 int snd_plan_launch(const snd_plan_t* plan, const snd_batch_t* batch,
                     void* workspace, const char* kernel, snd_stream_t stream);
 /* Measurement only: bits that make the bf16 decoder kernels skip phases

@@ -115,7 +115,7 @@ __global__ void __launch_bounds__(RCT) rowconv_kernel(RcArgs a) {
   const int r0 = blockIdx.x * kRcRows;
   const int rend = min(r0 + kRcRows, a.R);
   const int nbc = np >> 4;
-  const bool use_cp = NCP > 0 && a.colpart != nullptr;
+  const bool use_cp = NCP > 0 && a.colpart != nullptr && !(a.dbg & 64);
 
   // ---- packed weight image (LDS-DMA, 1 KB per wave instruction)
   if (!(a.dbg & 1)) {
@@ -247,7 +247,7 @@ __global__ void __launch_bounds__(RCT) rowconv_kernel(RcArgs a) {
 #pragma unroll
     for (int i = 0; i < NBH; ++i) {
       const int nb = nb0 + i;
-      if (nb >= nbc) continue;
+      if (nb >= nbc || (a.dbg & 128)) continue;
       const int n0 = 16 * nb + 4 * lg;
       const unsigned cm = rv ? cvm[i] : 0u;
       float o[4], qs[NCP > 0 ? NCP : 1][4];

@@ -777,6 +777,13 @@ extern "C" int snd_plan_launch(const snd_plan_t* plan, const snd_batch_t* batch,
                p.c.h1, (float*)(ws + p.buf("DXW1")), p.c.h1, SND_SPMM_PLAIN};
     return launch_spmm(a, s);
   }
+  if (!strcmp(kernel, "spmm_bf16")) {   // backward GCN1 SpMM of the fast path: A @ dP1 (bf16)
+    SND_CHECK_ARG(p.fast_enc, "snd_plan_launch: spmm_bf16 needs the bf16 fast encoder");
+    SpmmBfArgs a{batch->rowptr, batch->colidx, p.R, (const __bf16*)(ws + p.buf("FDP1")), p.c.h1,
+                 p.c.h1, SND_SPMM_PLAIN, (__bf16*)(ws + p.buf("FDXW1")), p.c.h1};
+    a.xcd_nbg = xcd_nbg(p.N, p.B);
+    return launch_spmm_bf16(a, s);
+  }
   if (!strncmp(kernel, "dec:", 4) || !strcmp(kernel, "pack")) {   // fast decoder kernel k
     SND_CHECK_ARG(p.fast && p.last_params, "snd_plan_launch: no fast-path step has run");
     SND_TRY(fast_init_attributes());
