@@ -91,6 +91,132 @@ def load_traffic(n, d, B, dtype):
     return None
 
 
+def run_workload(cfg, B, args, info, steps=None, warmup=None):
+    """Build B graphs per GPU, capture one full step in a HIP graph, time `steps` replays."""
+    import torch
+
+    from snd_vae_amd.data import synthetic_batch
+    from snd_vae_amd.model import DeviceBatch, SGCNModelVAE
+    from snd_vae_amd.optimizer import OptimizerVAE
+    from snd_vae_amd.parallel import max_over_ranks
+    steps = args.steps if steps is None else steps
+    warmup = args.warmup if warmup is None else warmup
+    log(f"[rank {info.rank}] building {B} RGG graphs N={cfg.n_nodes} ({cfg.topology}, node_h "
+        f"{cfg.node_h_size}, latent {cfg.latent})")
+    host = synthetic_batch(cfg, B, seed=1000 + info.rank * B)
+    db = DeviceBatch(host)
+    model = SGCNModelVAE(cfg, B, dtype=args.dtype)
+    opt = OptimizerVAE(model, process_group=info.group if info.world > 1 else None)
+    if args.no_graph:
+        run = lambda: opt.step(db)
+    else:
+        opt.capture(db, warmup=2)
+        run = opt.replay
+    for _ in range(warmup):
+        run()
+    torch.cuda.synchronize()
+    log(f"[rank {info.rank}] warm-up done, loss terms {opt.loss_dict()}")
+
+    def barrier():
+        if info.world > 1:
+            import torch.distributed as dist
+            dist.barrier()
+
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        run()
+    torch.cuda.synchronize()
+    barrier()
+    dt = max_over_ranks(time.perf_counter() - t0, info, device=f"cuda:{info.local_rank}")
+    _LIVE.append((model, opt, db))
+    return B * info.world * steps / dt, 1000.0 * dt / steps, model, opt, db, host
+
+
+_LIVE = []
+
+
+def del_models():
+    import torch
+    _LIVE.clear()
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+
+
+def kernel_timer(model, bc, reps):
+    """ms per launch of one plan kernel: `reps` launches captured in one HIP graph
+    (times the GPU, not the host launch path), replayed between HIP events on the
+    stream the kernels run on."""
+    import torch
+
+    from snd_vae_amd import _lib
+    L = _lib.lib()
+
+    def kernel_ms(name):
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.stream(side):
+            launch = lambda: _lib.check(L.snd_plan_launch(model.plan, bc, model.workspace.data_ptr(),
+                                                          name.encode(), _lib.stream_ptr(side)))
+            launch()
+            with torch.cuda.graph(g, stream=side):
+                for _ in range(reps):
+                    launch()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        with torch.cuda.stream(side):      # warm replay + timed replays, all on `side`
+            g.replay()
+            e0.record(side)
+            for _ in range(3):
+                g.replay()
+            e1.record(side)
+        e1.synchronize()
+        torch.cuda.current_stream().wait_stream(side)
+        return e0.elapsed_time(e1) / (3 * reps)
+
+    return kernel_ms
+
+
+def extra_workload(name, args, info):
+    """Time another BASELINE config (C4: graph latent + model_joint decoders; C5: the
+    N=16384 d=128 zz^T stress) with its dominant kernels' rooflines."""
+    from snd_vae_amd.config import PRESETS
+    cfg = PRESETS[name]
+    B = {"C4": args.graphs_per_gpu, "C5": 1}[name]
+    steps = max(5, args.steps // 5)
+    value, ms, model, opt, db, host = run_workload(cfg, B, args, info, steps=steps,
+                                                   warmup=min(args.warmup, 5))
+    kms = kernel_timer(model, db.c_struct(), max(4, args.kernel_reps // 4))
+    N, dj = cfg.n_nodes, cfg.node_h_size
+    res = {"value": round(value, 3), "unit": "graphs/s", "ms_per_step": round(ms, 4),
+           "graphs_per_gpu": B, "steps": steps, "n_nodes": N, "node_h": dj,
+           "topology": cfg.topology, "param_count": model.param_count,
+           "losses": {k: round(v, 6) for k, v in opt.loss_dict().items()}}
+    kern = {}
+    zms = kms("zzt_dense")
+    zfl = 4.0 * N * N * dj * B
+    kern["zzt_dense"] = {"bound": "mfma", "avg_launch_ms": round(zms, 5), "flops_per_launch": zfl,
+                         "achieved": round(zfl / (zms * 1e-3) / 1e12, 2), "peak": PEAK_TFLOPS[args.dtype],
+                         "unit": "TFLOP/s", "frac": round(zfl / (zms * 1e-3) / 1e12 / PEAK_TFLOPS[args.dtype], 4)}
+    if cfg.topology == "tref":
+        W = cfg.enc_width
+        K, gh, L, Cp = N * W, cfg.g_hidden_size, cfg.latent, N * dj
+        # algorithmic bytes: weight read (+ weight-gradient write) + activations in / out
+        units = {"tref_head_fwd": 4 * (K * gh + B * K),
+                 "tref_head_bwd": 4 * (2 * K * gh + 2 * B * K + B * gh),
+                 "tref_proj_fwd": 4 * (L * Cp + Cp + B * Cp + B * L),
+                 "tref_proj_bwd": 4 * (2 * L * Cp + Cp + 3 * B * Cp + B * L)}
+        for k, byts in units.items():
+            t = kms(k)
+            kern[k] = {"bound": "hbm", "avg_launch_ms": round(t, 5), "bytes_per_launch": byts,
+                       "achieved": round(byts / (t * 1e-3) / 1e9, 1), "peak": PEAK_HBM_GBS,
+                       "unit": "GB/s", "frac": round(byts / (t * 1e-3) / 1e9 / PEAK_HBM_GBS, 4)}
+    res["kernels"] = kern
+    log(f"[{name}] {value:.1f} graphs/s, {ms:.3f} ms/step, kernels {kern}")
+    return res
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -104,16 +230,14 @@ def main():
     ap.add_argument("--kernel-reps", type=int, default=20)
     ap.add_argument("--cpu-baseline-seconds", type=float, default=20.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--extra", default="C4,C5",
+                    help="other BASELINE configs timed after the headline (1 GPU only): C4,C5")
     args = ap.parse_args()
 
     import torch
 
     from snd_vae_amd.config import tscale
-    from snd_vae_amd.data import synthetic_batch
-    from snd_vae_amd.model import DeviceBatch, SGCNModelVAE
-    from snd_vae_amd.optimizer import OptimizerVAE
-    from snd_vae_amd.parallel import init_from_env, max_over_ranks
-    from snd_vae_amd import _lib
+    from snd_vae_amd.parallel import init_from_env
 
     info = init_from_env("nccl")
     if info.world != args.gpus:
@@ -121,68 +245,14 @@ def main():
     torch.cuda.set_device(info.local_rank)
     B, N, d = args.graphs_per_gpu, args.nodes, args.latent
     cfg = tscale(N, d)
-    log(f"[rank {info.rank}] building {B} RGG graphs N={N}")
-    host = synthetic_batch(cfg, B, seed=1000 + info.rank * B)
-    db = DeviceBatch(host)
-    model = SGCNModelVAE(cfg, B, dtype=args.dtype)
-    opt = OptimizerVAE(model, process_group=info.group if info.world > 1 else None)
-
-    if args.no_graph:
-        run = lambda: opt.step(db)
-    else:
-        opt.capture(db, warmup=2)
-        run = opt.replay
-    for _ in range(args.warmup):
-        run()
-    torch.cuda.synchronize()
-    log(f"[rank {info.rank}] warm-up done, loss terms {opt.loss_dict()}")
-
-    def barrier():
-        if info.world > 1:
-            import torch.distributed as dist
-            dist.barrier()
-
-    barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        run()
-    torch.cuda.synchronize()
-    barrier()
-    dt = max_over_ranks(time.perf_counter() - t0, info, device=f"cuda:{info.local_rank}")
+    value, ms, model, opt, db, host = run_workload(cfg, B, args, info)
     losses = opt.loss_dict(global_mean=True)
-    graphs = B * info.world * args.steps
-    value = graphs / dt
-    ms = 1000.0 * dt / args.steps
     log(f"[rank {info.rank}] {value:.1f} graphs/s, {ms:.3f} ms/step")
 
-    # ---- dominant kernel: fused zz^T + CE, HIP events on the launch stream
     bc = db.c_struct()
-    L = _lib.lib()
+    kernel_ms = kernel_timer(model, bc, args.kernel_reps)
 
-    def kernel_ms(name):
-        # kernel_reps launches captured in one HIP graph (times the GPU, not the host
-        # launch path), replayed on the current stream between HIP events
-        side = torch.cuda.Stream()
-        side.wait_stream(torch.cuda.current_stream())
-        g = torch.cuda.CUDAGraph()
-        with torch.cuda.stream(side):
-            launch = lambda: _lib.check(L.snd_plan_launch(model.plan, bc, model.workspace.data_ptr(),
-                                                          name.encode(), _lib.stream_ptr(side)))
-            launch()
-            with torch.cuda.graph(g, stream=side):
-                for _ in range(args.kernel_reps):
-                    launch()
-        torch.cuda.current_stream().wait_stream(side)
-        g.replay()
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        for _ in range(3):
-            g.replay()
-        e1.record()
-        e1.synchronize()
-        return e0.elapsed_time(e1) / (3 * args.kernel_reps)
-
+    # ---- dominant kernel: fused zz^T + CE, HIP events on the launch stream
     zzt_ms = kernel_ms("zzt_dense")
     zzt_v1_ms = kernel_ms("zzt_dense_v1") if args.dtype == "bf16" else None
     fast = args.dtype == "bf16"
@@ -228,6 +298,12 @@ def main():
                                "avg_launch_ms": round(spmm_ms, 5), "bytes_per_launch": spmm_bytes},
         "losses": {k: round(v, 6) for k, v in losses.items()},
     }
+    extra = [w for w in args.extra.split(",") if w] if info.world == 1 else []
+    if extra:
+        out["workloads"] = {}
+        for w in extra:
+            out["workloads"][w] = extra_workload(w, args, info)
+            del_models()
     if info.rank == 0 and info.world == 1 and not args.no_cpu_baseline:
         log("cpu baseline ...")
         out["cpu_baseline"] = cpu_baseline(N, d, args.cpu_baseline_seconds)

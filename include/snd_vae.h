@@ -159,8 +159,14 @@ int snd_adam_tf1(float* param, const float* grad, float* m, float* v,
                  snd_stream_t stream);
 
 /* ---- a14: the whole train step (main.py:315-334) ---------------------------
- * A plan fixes shapes; the step runs forward + backward of the node-latent
- * SND-VAE (SURVEY §8 "Composed step") for one batch, writes the flat
+ * A plan fixes shapes; the step runs forward + backward of the SND-VAE
+ * (SURVEY §8 "Composed step") for one batch in either decoder-input topology:
+ *   SND_TSCALE  node latent: heads per node row, mu/logstd [B*N, L], J = z;
+ *   SND_TREF    graph latent (model.py:113-115, model_joint.py:87-97):
+ *               h = flat(G) Wh + bh per graph, z [B, L],
+ *               J = reshape(z Wp + bp, [B, N, node_h]); at most 8 graphs
+ *               per plan (the weight-streaming kernels keep B in registers).
+ * It writes the flat
  * gradient (same layout as params), advances *step_counter and writes
  * losses[0..7] = {cost, spatial_cost, adj_cost, node_cost, kl, acc,
  *                 adj_sum, correct} (device doubles; main.py:331-334
@@ -173,14 +179,17 @@ typedef struct snd_config {
   int spatial_dim;  /* coordinate targets */
   int h0, h1;       /* g_conv_hidden */
   int g_hidden;     /* g_hidden_size */
-  int latent;       /* L == node_h_size */
+  int latent;       /* L (g_latent_size) */
   int s1, s2, s3;   /* s_d_channel */
   int n1, n2;       /* n_d_channel[:2] */
   float beta;       /* KL weight */
   float pos_weight; /* 1 == reference */
   float norm;       /* 1 == reference */
   int dtype;        /* SND_F32 (parity) or SND_BF16 (throughput) */
+  int topology;     /* SND_TSCALE or SND_TREF (ABI version 2) */
+  int node_h;       /* width of J (node_h_size); == latent for SND_TSCALE */
 } snd_config_t;
+enum { SND_TSCALE = 0, SND_TREF = 1 };
 
 typedef struct snd_batch {
   const int* rowptr;           /* [B*N+1] */
@@ -210,7 +219,9 @@ int snd_train_step(const snd_plan_t* plan, const snd_batch_t* batch,
  * snd_train_step (measurement/profiling): "zzt_dense" (fused zz^T + CE),
  * "spmm_dxw1" (plain fp32 CSR SpMM, width h1; generic-engine plans),
  * "spmm_bf16" (the bf16 path's A @ dP1), "pack" / "dec:<k>" (bf16 weight
- * packing / k-th bf16 decoder kernel, k = 0..10). */
+ * packing / k-th bf16 decoder kernel, k = 0..10), and on SND_TREF plans
+ * "tref_head_fwd" / "tref_head_bwd" / "tref_proj_fwd" / "tref_proj_bwd"
+ * (the weight-streaming heads and projection). */
 int snd_plan_launch(const snd_plan_t* plan, const snd_batch_t* batch,
                     void* workspace, const char* kernel, snd_stream_t stream);
 /* Measurement only: bits that make the bf16 decoder kernels skip phases

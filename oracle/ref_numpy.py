@@ -19,7 +19,9 @@ Formulas and the reference lines they restate:
       y = gamma * x / sqrt(1.001) + beta                      model.py:41,107,112
   concat [g || node_feature]                                  model.py:109
   linear: x @ Matrix + bias                                   layers.py:566-576
+  tref heads: h = flat(G) Wh + bh per graph (row-major reshape) model.py:113-115
   z = mu + eps * exp(logstd)                                  model.py:153-161
+  tref projection: J = reshape(z Wp + bp, [B, N, node_h])     model_joint.py:97
   L = J @ J^T; logits (0, L) off-diagonal, (1, 0) on the
       diagonal; argmax first-index tie break                  layers.py:407-409,
                                                               model.py:185,205-208
@@ -133,10 +135,11 @@ def adj_ce(J, adj, n, pos_weight=1.0, norm=1.0):
 # ----------------------------------------------------------------- model
 def forward_backward(p: Dict[str, np.ndarray], adj, X, Xf, S, eps, cfg,
                      want_grads=True):
-    """One training step's forward + hand-derived backward (node-latent).
+    """One training step's forward + hand-derived backward.
 
     adj: list of B dense [N,N] 0/1 arrays; X [B*N, f_in]; Xf [B*N, nf];
-    S [B*N, 2]; eps [B*N, L].  Returns (losses dict, grads dict, cache).
+    S [B*N, 2]; eps [B*N, L] (tscale) or [B, L] (tref, model_joint.py:89).
+    Returns (losses dict, grads dict, cache).
     """
     n = cfg.n_nodes
     R = X.shape[0]
@@ -161,12 +164,19 @@ def forward_backward(p: Dict[str, np.ndarray], adj, X, Xf, S, eps, cfg,
     B1 = A1 * (p["enc.bn1.gamma"] * c) + p["enc.bn1.beta"]
     H2 = np.concatenate([B1, X], 1)
     G = H2 * (p["enc.bne.gamma"] * c) + p["enc.bne.beta"]
-    h = G @ p["enc.Wh"] + p["enc.bh"]
+    tref = cfg.topology == "tref"
+    # heads (model.py:113-115): per node row (tscale) or on flat(G) per graph (tref,
+    # tf.reshape(g, [B, -1]) is row-major: flat index n*W + c)
+    Gin = G.reshape(B, -1) if tref else G
+    h = Gin @ p["enc.Wh"] + p["enc.bh"]
     ms = h @ p["enc.Wms"] + p["enc.bms"]
     mu, s = ms[:, :L], ms[:, L:]
     es = np.exp(s)
-    z = mu + eps * es
-    J = z
+    z = mu + eps * es                             # eps [B, L] (tref) / [B*N, L]
+    if tref:   # J = reshape(linear(z, N*node_h, 'd_sg_lin1'), [B, N, node_h]) model_joint.py:97
+        J = (z @ p["dec.Wp"] + p["dec.bp"]).reshape(B * n, cfg.node_h_size)
+    else:
+        J = z
 
     # ---- structure decoder + CE (layers.py:407-409, optimizer.py:144)
     ce_sum, dJ_adj_sum, correct = adj_ce(J, adj, n, cfg.pos_weight, cfg.norm)
@@ -231,16 +241,23 @@ def forward_backward(p: Dict[str, np.ndarray], adj, X, Xf, S, eps, cfg,
 
     # ---- reparameterisation + KL (model.py:159, optimizer.py:193)
     dJ = dJ_dec + dJ_adj_sum / (B * n * n)
+    if tref:   # d_sg_lin1 backward
+        dJf = dJ.reshape(B, -1)
+        g["dec.Wp"] = z.T @ dJf
+        g["dec.bp"] = dJf.sum(0)
+        dz = dJf @ p["dec.Wp"].T
+    else:
+        dz = dJ
     M = mu.size
-    dmu = dJ + cfg.beta * mu / M
-    ds = dJ * eps * es + cfg.beta * (es ** 2 - 1.0) / M
+    dmu = dz + cfg.beta * mu / M
+    ds = dz * eps * es + cfg.beta * (es ** 2 - 1.0) / M
     dms = np.concatenate([dmu, ds], 1)
     g["enc.Wms"] = h.T @ dms
     g["enc.bms"] = dms.sum(0)
     dh = dms @ p["enc.Wms"].T
-    g["enc.Wh"] = G.T @ dh
+    g["enc.Wh"] = Gin.T @ dh
     g["enc.bh"] = dh.sum(0)
-    dG = dh @ p["enc.Wh"].T
+    dG = (dh @ p["enc.Wh"].T).reshape(G.shape)
     g["enc.bne.gamma"] = (dG * H2).sum(0) * c
     g["enc.bne.beta"] = dG.sum(0)
     dH2 = dG * (p["enc.bne.gamma"] * c)

@@ -46,7 +46,7 @@ def build_params(blocks: Dict[str, np.ndarray], dtype):
 
 
 def loss_fn(p, adj, X, Xf, S, eps, cfg):
-    """adj [B,N,N]; X [B,N,f]; Xf [B,N,nf]; S [B,N,2]; eps [B,N,L]."""
+    """adj [B,N,N]; X [B,N,f]; Xf [B,N,nf]; S [B,N,2]; eps [B,N,L] (tref: [B,L])."""
     B, n, _ = adj.shape
     L = cfg.latent
     s1 = cfg.s_d_channel[0]
@@ -57,11 +57,18 @@ def loss_fn(p, adj, X, Xf, S, eps, cfg):
         g = bn(lrelu(conv), p[bg], p[bb])
         g = torch.cat([g, X], -1)
     g = bn(g, p["enc.bne.gamma"], p["enc.bne.beta"])
-    h = g @ p["enc.Wh"] + p["enc.bh"]
-    ms = h @ p["enc.Wms"] + p["enc.bms"]
-    mu, s = ms[..., :L], ms[..., L:]
-    z = mu + eps * torch.exp(s)
-    J = z
+    if cfg.topology == "tref":   # model.py:113-115, model_joint.py:87-97
+        h = torch.reshape(g, [B, -1]) @ p["enc.Wh"] + p["enc.bh"]
+        ms = h @ p["enc.Wms"] + p["enc.bms"]
+        mu, s = ms[..., :L], ms[..., L:]
+        z = mu + eps.reshape(B, L) * torch.exp(s)
+        J = torch.reshape(z @ p["dec.Wp"] + p["dec.bp"], [B, n, cfg.node_h_size])
+    else:
+        h = g @ p["enc.Wh"] + p["enc.bh"]
+        ms = h @ p["enc.Wms"] + p["enc.bms"]
+        mu, s = ms[..., :L], ms[..., L:]
+        z = mu + eps * torch.exp(s)
+        J = z
     logit = torch.matmul(J, J.transpose(1, 2))
     diag = torch.ones(n, n, dtype=X.dtype) - torch.eye(n, dtype=X.dtype)
     l0 = diag * 0.0 * logit + (1 - diag)                  # model.py:206
@@ -119,4 +126,6 @@ def to_tensors(batch_arrays, cfg, dtype):
     n = cfg.n_nodes
     B = X.shape[0] // n
     t = lambda a: torch.tensor(np.asarray(a), dtype=dtype).reshape(B, n, -1)
-    return (torch.tensor(np.stack(adj), dtype=dtype), t(X), t(Xf), t(S), t(eps))
+    e = torch.tensor(np.asarray(eps), dtype=dtype)
+    e = e.reshape(B, -1) if cfg.topology == "tref" else e.reshape(B, n, -1)
+    return (torch.tensor(np.stack(adj), dtype=dtype), t(X), t(Xf), t(S), e)

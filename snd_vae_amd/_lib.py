@@ -17,6 +17,10 @@ c_int, c_ll, c_float, c_size, c_ull = C.c_int, C.c_longlong, C.c_float, C.c_size
 vp = C.c_void_p
 
 
+ABI_VERSION = 2
+TOPOLOGY = {"tscale": 0, "tref": 1}
+
+
 class SNDError(RuntimeError):
     pass
 
@@ -27,7 +31,7 @@ class Config(C.Structure):
                 ("spatial_dim", c_int), ("h0", c_int), ("h1", c_int), ("g_hidden", c_int),
                 ("latent", c_int), ("s1", c_int), ("s2", c_int), ("s3", c_int),
                 ("n1", c_int), ("n2", c_int), ("beta", c_float), ("pos_weight", c_float),
-                ("norm", c_float), ("dtype", c_int)]
+                ("norm", c_float), ("dtype", c_int), ("topology", c_int), ("node_h", c_int)]
 
 
 class Batch(C.Structure):
@@ -93,6 +97,8 @@ def lib():
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args
+        if L.snd_abi_version() != ABI_VERSION:
+            raise SNDError(f"{LIB_PATH}: ABI {L.snd_abi_version()} != {ABI_VERSION}; rebuild it")
         _lib = L
     return _lib
 

@@ -10,8 +10,13 @@ Two decoder-input topologies exist (SURVEY.md §8 "Composed step"):
   (`model.py:113-115`) are applied per node row, so mu/logstd are [N, L] and
   the inner-product decoder input is J = z (L == node_h).
 * ``tref`` (C1/C4): graph-level latent exactly as `model.py:113-115` +
-  `model_joint.py:97` ('d_sg_lin1').  Implemented in the oracle; the GPU path
-  for it is listed as "next" in DESIGN.md.
+  `model_joint.py:97` ('d_sg_lin1'): h = flat(G) W_h + b_h per graph,
+  z [B, L], J = reshape(z W_p + b_p, [N, node_h]).
+
+``encoder_coords`` appends the coordinates to the encoder input (SURVEY §8
+decision iii): on for tscale and for C4 (whose flat(G) width 4096*67 is the
+SURVEY §8a row a5 figure), off for C1, which keeps F_in = num_feature exactly
+as `model.py:104`.
 """
 from __future__ import annotations
 
@@ -50,11 +55,12 @@ class SNDConfig:
     weighted_bce: bool = False          # design decision (ii): off == reference
     pos_weight: float = 1.0
     norm: float = 1.0
+    encoder_coords: bool = True         # X = [x_feat || S] (decision iii)
 
     @property
     def f_in(self) -> int:
-        """Encoder input width.  tscale appends coordinates (decision iii)."""
-        if self.topology == "tscale":
+        """Encoder input width (coordinates appended when encoder_coords)."""
+        if self.encoder_coords:
             return self.num_feature + self.spatial_dim
         return self.num_feature
 
@@ -78,17 +84,25 @@ def tscale(n_nodes: int, latent: int, **kw) -> SNDConfig:
                      node_h_size=latent, **kw)
 
 
+def tref(n_nodes: int, node_h: int, g_hidden: int = 100, latent: int = 100,
+         **kw) -> SNDConfig:
+    """Graph-latent topology: g_hidden = L = 100 (main.py:190-191), node_h = d."""
+    return SNDConfig(n_nodes=n_nodes, g_latent_size=latent, topology="tref",
+                     g_conv_hidden=(node_h, node_h), g_hidden_size=g_hidden,
+                     node_h_size=node_h, **kw)
+
+
 PRESETS = {
     # C1: N=200 d=16, reference CPU plumbing.  tref as in model.py:104.
-    "C1": SNDConfig(n_nodes=200, g_latent_size=100, topology="tref",
-                    g_conv_hidden=(16, 16), g_hidden_size=100,
-                    node_h_size=16, mean_degree=8.0),
+    "C1": tref(200, 16, mean_degree=8.0, encoder_coords=False),
     # C1 in the node-latent topology (used for GPU parity at small N).
     "C1s": tscale(200, 16, mean_degree=8.0),
     # C2: N=4096 d=64 bf16 on 1 GPU -- the bench workload.
     "C2": tscale(4096, 64),
     # C3: C2 graphs data-parallel over 8 GPUs.
     "C3": tscale(4096, 64),
+    # C4: model_joint structure + coordinate decoders on the graph latent, N=4096 d=64.
+    "C4": tref(4096, 64),
     # C5: N=16384 d=128 inner-product decoder stress.
     "C5": tscale(16384, 128),
 }

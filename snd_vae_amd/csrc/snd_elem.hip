@@ -6,6 +6,7 @@
 
 #include <algorithm>
 #include "snd_gemm.hpp"
+#include "snd_tref.hpp"
 
 namespace snd {
 namespace {
@@ -60,7 +61,7 @@ __global__ void __launch_bounds__(256) reparam_bwd_kernel(ReparamBwdArgs a) {
     const float mu = a.ms[(long long)r * a.ldms + c];
     const float ls = a.ms[(long long)r * a.ldms + a.L + c];
     const float es = __expf(ls);
-    float dz = a.adj_scale * (a.dJd[i] + a.ej[i]);
+    float dz = a.dJd ? a.adj_scale * (a.dJd[i] + a.ej[i]) : 0.f;
     if (a.dz_dec) dz += a.dz_dec[i];
     a.dms[(long long)r * a.lddms + c] = dz + a.kl_scale * mu;
     a.dms[(long long)r * a.lddms + a.L + c] = dz * a.eps[i] * es + a.kl_scale * (es * es - 1.f);
@@ -311,7 +312,7 @@ __global__ void __launch_bounds__(kFinT) finalize_kernel(FinalizeArgs a) {
   const double adj_sum = (double)a.norm * (dl + el + rows * kSoftplusM1);
   const double adj_cost = adj_sum / pairs;                      // optimizer.py:144
   const double correct = pairs - nnz - dc + 2.0 * tp;           // main.py:334
-  const double klm = -0.5 * kl / (rows * a.L);                 // optimizer.py:193
+  const double klm = -0.5 * kl / (a.kl_count > 0 ? a.kl_count : rows * a.L);   // optimizer.py:193
   const double spatial = ss / (rows * a.sdim);                  // optimizer.py:153
   const double node = sn / (rows * a.nfeat);                    // optimizer.py:149
   const double cost = adj_cost + node + spatial + (double)a.beta * klm;   // :157,194
@@ -479,6 +480,9 @@ extern "C" int snd_adam_tf1(float* param, const float* grad, float* m, float* v,
                             float lr, float beta1, float beta2, float eps, float grad_scale,
                             const int* step_counter, snd_stream_t stream) {
   SND_CHECK_ARG(param && grad && m && v && step_counter && n >= 0, "snd_adam_tf1: bad args");
+  if (n % 4 == 0 && ((uintptr_t)param | (uintptr_t)grad | (uintptr_t)m | (uintptr_t)v) % 16 == 0)
+    return launch_adam_vec(param, grad, m, v, n, lr, beta1, beta2, eps, grad_scale, step_counter,
+                           (hipStream_t)stream);
   int blocks = cdiv(n, 256);
   if (blocks > 2048) blocks = 2048;
   if (blocks < 1) blocks = 1;

@@ -18,7 +18,7 @@ struct ReparamBwdArgs {
   const float* ms; int ldms; int rows; int L;
   const float* eps;
   const float* dz_dec;        // [rows, L] gradient from the conv decoders (may be null)
-  const float* dJd; const float* ej;   // zz^T terms, combined as adj_scale*(dJd + ej)
+  const float* dJd; const float* ej;   // zz^T terms, combined as adj_scale*(dJd + ej); may be null
   float adj_scale;            // norm / (B N^2)
   float kl_scale;             // beta / (rows * L)
   float* dms; int lddms;      // [rows, 2L] = [dmu || dlogstd]
@@ -74,6 +74,7 @@ struct FinalizeArgs {
   const int* rowptr; int ngraphs; int n; int L; int sdim; int nfeat;
   float beta; float norm;
   double* losses; float* grad_tail; int* step;
+  double kl_count;            // elements of mu (0: ngraphs * n * L, node latent)
 };
 int launch_finalize(const FinalizeArgs& a, hipStream_t s);
 

@@ -170,6 +170,7 @@ struct ReparamPrepArgs {
   float* z; float* eps_out; __bf16* zb;
   __bf16* jrow; __bf16* jt; float* colpart;
   double* kl_part;            // [ngraphs * npad / 64]
+  int stage_only;             // 1: ms is J itself (T-ref projection output); no eps / KL
 };
 int reparam_prep_blocks(int ngraphs, int npad);
 

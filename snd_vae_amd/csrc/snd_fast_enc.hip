@@ -364,7 +364,11 @@ __global__ void __launch_bounds__(NT) reparam_prep_kernel(ReparamPrepArgs a) {
     const int rr = idx / DP, c = idx - rr * DP;
     const int row = rb * 64 + rr;
     float z = 0.f;
-    if (row < a.n && c < L) {
+    if (row < a.n && c < L && a.stage_only) {
+      const long long gr = (long long)g * a.n + row;
+      z = a.ms[gr * a.ldms + c];
+      a.zb[gr * L + c] = (__bf16)z;
+    } else if (row < a.n && c < L) {
       const long long gr = (long long)g * a.n + row;
       const long long i = gr * L + c;
       const float mu = a.ms[gr * a.ldms + c];
@@ -385,7 +389,7 @@ __global__ void __launch_bounds__(NT) reparam_prep_kernel(ReparamPrepArgs a) {
   kl = wave_sum_d(kl);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = kl;
   __syncthreads();
-  if (threadIdx.x == 0) {
+  if (threadIdx.x == 0 && a.kl_part) {
     double t = 0.0;
     for (int k = 0; k < NT / 64; ++k) t += red[k];
     a.kl_part[blockIdx.y * gridDim.x + blockIdx.x] = t;
@@ -452,7 +456,8 @@ int reparam_prep_blocks(int ngraphs, int npad) { return ngraphs * (npad / 64); }
 int launch_reparam_prep(const ReparamPrepArgs& a, int dp, hipStream_t s) {
   if (a.ngraphs <= 0) return 0;
   SND_CHECK_ARG(a.npad % 64 == 0 && a.L <= dp, "reparam_prep: npad %% 64, L <= dp");
-  SND_CHECK_ARG(a.ms && a.z && a.eps_out && a.zb && a.jrow && a.jt && a.colpart && a.kl_part,
+  SND_CHECK_ARG(a.ms && a.zb && a.jrow && a.jt && a.colpart &&
+                    (a.stage_only || (a.z && a.eps_out && a.kl_part)),
                 "reparam_prep: null operand");
   dim3 grid(a.npad / 64, a.ngraphs);
   switch (dp) {

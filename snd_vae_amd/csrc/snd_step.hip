@@ -20,6 +20,7 @@
 #include "snd_fast.hpp"
 #include "snd_gemm.hpp"
 #include "snd_spmm.hpp"
+#include "snd_tref.hpp"
 #include "snd_zzt.hpp"
 
 namespace snd {
@@ -64,6 +65,9 @@ struct snd_plan {
   snd_config_t c;
   int B, N, R;
   int W, C1;                   // enc width, fused first decoder conv width
+  bool tref = false;           // graph-latent topology (SND_TREF)
+  int dj = 0;                  // width of J (decoder / zz^T input)
+  int RH = 0;                  // rows of the head tensors h, [mu || s], z: B (tref) or R
   std::vector<Block> blocks;
   long long pcount = 0;
   std::vector<Buf> bufs;
@@ -116,15 +120,23 @@ struct snd_plan {
 };
 
 extern "C" const char* snd_last_error(void) { return g_err; }
-extern "C" int snd_abi_version(void) { return 1; }
+extern "C" int snd_abi_version(void) { return 2; }
 
 extern "C" int snd_plan_create(const snd_config_t* cfg, int n_graphs, snd_plan_t** out) {
   SND_CHECK_ARG(cfg && out && n_graphs > 0, "snd_plan_create: bad args");
   const snd_config_t& c = *cfg;
   SND_CHECK_ARG(c.n_nodes > 0 && c.f_in > 0 && c.h0 > 0 && c.h1 > 0 && c.g_hidden > 0,
                 "snd_plan_create: non-positive width");
-  SND_CHECK_ARG(c.latent == 16 || c.latent == 32 || c.latent == 64 || c.latent == 128,
-                "snd_plan_create: latent %d not in {16,32,64,128}", c.latent);
+  SND_CHECK_ARG(c.topology == SND_TSCALE || c.topology == SND_TREF, "snd_plan_create: bad topology");
+  const bool tref = c.topology == SND_TREF;
+  const int dj = c.node_h;
+  SND_CHECK_ARG(dj == 16 || dj == 32 || dj == 64 || dj == 128,
+                "snd_plan_create: node_h %d not in {16,32,64,128}", dj);
+  SND_CHECK_ARG(tref || c.latent == dj, "snd_plan_create: node latent needs latent == node_h");
+  SND_CHECK_ARG(!tref || (n_graphs <= kTrefMaxB && c.latent <= 128 && c.g_hidden % 4 == 0 &&
+                          c.g_hidden <= 128),
+                "snd_plan_create: graph latent needs <= %d graphs, latent <= 128, g_hidden %% 4 <= 128",
+                kTrefMaxB);
   SND_CHECK_ARG(c.h0 <= 128 && c.h1 <= 128, "snd_plan_create: g_conv_hidden <= 128");
   SND_CHECK_ARG(c.h1 + c.f_in <= 256 && c.s1 + c.n1 <= 256, "snd_plan_create: width <= 256");
   SND_CHECK_ARG(c.s3 <= 64 && c.n2 <= 64 && c.spatial_dim <= 4 && c.num_feature <= 4,
@@ -137,9 +149,12 @@ extern "C" int snd_plan_create(const snd_config_t* cfg, int n_graphs, snd_plan_t
   p->B = n_graphs; p->N = c.n_nodes; p->R = n_graphs * c.n_nodes;
   p->W = c.h1 + c.f_in;
   p->C1 = c.s1 + c.n1;
+  p->tref = tref;
+  p->dj = dj;
+  p->RH = tref ? n_graphs : p->R;
   const int f = c.f_in, h0 = c.h0, h1 = c.h1, gh = c.g_hidden, L = c.latent;
   const int W = p->W, C1 = p->C1;
-  const long long R = p->R;
+  const long long R = p->R, RH = p->RH;
   // ---- flat parameter layout (params.py::block_shapes order)
   p->add_block("enc.W0", (long long)f * h0);
   p->add_block("enc.bn0.gamma", h0);
@@ -149,11 +164,15 @@ extern "C" int snd_plan_create(const snd_config_t* cfg, int n_graphs, snd_plan_t
   p->add_block("enc.bn1.beta", h1);
   p->add_block("enc.bne.gamma", W);
   p->add_block("enc.bne.beta", W);
-  p->add_block("enc.Wh", (long long)W * gh);
+  p->add_block("enc.Wh", (tref ? (long long)p->N * W : W) * gh);
   p->add_block("enc.bh", gh);
   p->add_block("enc.Wms", (long long)gh * 2 * L);
   p->add_block("enc.bms", 2 * L);
-  p->add_block("dec.K1", 5LL * L * C1);
+  if (tref) {
+    p->add_block("dec.Wp", (long long)L * p->N * dj);
+    p->add_block("dec.bp", (long long)p->N * dj);
+  }
+  p->add_block("dec.K1", 5LL * dj * C1);
   p->add_block("dec.b1", C1);
   p->add_block("dec.bn1.gamma", C1);
   p->add_block("dec.bn1.beta", C1);
@@ -177,10 +196,10 @@ extern "C" int snd_plan_create(const snd_config_t* cfg, int n_graphs, snd_plan_t
   // ---- workspace
   p->add_buf("XW0", R * h0);  p->add_buf("P0", R * h0);  p->add_buf("H1", R * (h0 + f));
   p->add_buf("XW1", R * h1);  p->add_buf("P1", R * h1);  p->add_buf("H2", R * W);
-  p->add_buf("G", R * W);     p->add_buf("Hh", R * gh);  p->add_buf("MS", R * 2 * L);
-  p->add_buf("EPS", R * L);   p->add_buf("Z", R * L);
-  p->add_buf("ZSTAGE", (long long)zzt_staging_bytes(p->B, p->N, L, c.dtype), 1);
-  p->add_buf("DJD", R * L);   p->add_buf("EJ", R * L);
+  p->add_buf("G", R * W);     p->add_buf("Hh", RH * gh); p->add_buf("MS", RH * 2 * L);
+  p->add_buf("EPS", RH * L);  p->add_buf("Z", R * dj);
+  p->add_buf("ZSTAGE", (long long)zzt_staging_bytes(p->B, p->N, dj, c.dtype), 1);
+  p->add_buf("DJD", R * dj);  p->add_buf("EJ", R * dj);
   p->add_buf("Y1", R * C1);   p->add_buf("U1", R * C1);
   p->add_buf("Y2S", R * c.s2); p->add_buf("U2S", R * c.s2);
   p->add_buf("Y2N", R * c.n2); p->add_buf("U2N", R * c.n2);
@@ -189,12 +208,12 @@ extern "C" int snd_plan_create(const snd_config_t* cfg, int n_graphs, snd_plan_t
   p->add_buf("DU3S", R * c.s3); p->add_buf("DY3S", R * c.s3);
   p->add_buf("DU2S", R * c.s2); p->add_buf("DY2S", R * c.s2);
   p->add_buf("DU2N", R * c.n2); p->add_buf("DY2N", R * c.n2);
-  p->add_buf("DU1", R * C1);  p->add_buf("DY1", R * C1);  p->add_buf("DZDEC", R * L);
-  p->add_buf("DMS", R * 2 * L); p->add_buf("DH", R * gh); p->add_buf("DG", R * W);
+  p->add_buf("DU1", R * C1);  p->add_buf("DY1", R * C1);  p->add_buf("DZDEC", R * dj);
+  p->add_buf("DMS", RH * 2 * L); p->add_buf("DH", RH * gh); p->add_buf("DG", R * W);
   p->add_buf("DP1", R * h1);  p->add_buf("DXW1", R * h1); p->add_buf("DH1", R * h0);
   p->add_buf("DP0", R * h0);  p->add_buf("DXW0", R * h0);
-  const int nz = zzt_dense_blocks(p->B, p->N), ne = edge_blocks(p->R, L);
-  const int nk = reparam_blocks(p->R, L), nh = head_blocks(p->R), nc = col_blocks(p->R);
+  const int nz = zzt_dense_blocks(p->B, p->N), ne = edge_blocks(p->R, dj);
+  const int nk = reparam_blocks(p->RH, L), nh = head_blocks(p->R), nc = col_blocks(p->R);
   p->add_buf("PZZT", 2LL * nz, 8); p->add_buf("PEDGE", 2LL * std::max(ne, edge_bf16_blocks(p->R)), 8); p->add_buf("PKL", std::max(nk, reparam_prep_blocks(p->B, zzt_npad(p->N))), 8);
   p->add_buf("PSSES", nh, 8); p->add_buf("PSSEN", nh, 8);
   p->add_buf("PHS", (long long)nh * (c.s3 * c.spatial_dim + c.spatial_dim));
@@ -205,8 +224,8 @@ extern "C" int snd_plan_create(const snd_config_t* cfg, int n_graphs, snd_plan_t
   p->sW0 = wgrad_split(f, h0, p->R);
   p->sW1 = wgrad_split(h0 + f, h1, p->R);
   p->sWh = wgrad_split(W + 1, gh, p->R);
-  p->sWms = wgrad_split(gh + 1, 2 * L, p->R);
-  p->sK1 = wgrad_split(5 * L, C1, p->R);
+  p->sWms = wgrad_split(gh + 1, 2 * L, p->RH);
+  p->sK1 = wgrad_split(5 * dj, C1, p->R);
   p->sK2s = wgrad_split(5 * c.s1, c.s2, p->R);
   p->sK2n = wgrad_split(5 * c.n1, c.n2, p->R);
   p->sK3s = wgrad_split(5 * c.s2, c.s3, p->R);
@@ -214,7 +233,12 @@ extern "C" int snd_plan_create(const snd_config_t* cfg, int n_graphs, snd_plan_t
   p->add_buf("SW1", (long long)p->sW1.splits * (h0 + f) * h1);
   p->add_buf("SWH", (long long)p->sWh.splits * (W + 1) * gh);
   p->add_buf("SWMS", (long long)p->sWms.splits * (gh + 1) * 2 * L);
-  p->add_buf("SK1", (long long)p->sK1.splits * 5 * L * C1);
+  p->add_buf("SK1", (long long)p->sK1.splits * 5 * dj * C1);
+  if (tref) {   // graph-latent heads / projection (snd_tref.hip)
+    p->add_buf("ZL", RH * L);   p->add_buf("DZL", RH * L);
+    p->add_buf("PHF", (long long)tref_head_fwd_blocks((long long)p->N * W, gh) * RH * gh);
+    p->add_buf("PDZ", (long long)tref_proj_bwd_blocks((long long)p->N * dj) * RH * L);
+  }
   p->add_buf("SK2S", (long long)p->sK2s.splits * 5 * c.s1 * c.s2);
   p->add_buf("SK2N", (long long)p->sK2n.splits * 5 * c.n1 * c.n2);
   p->add_buf("SK3S", (long long)p->sK3s.splits * 5 * c.s2 * c.s3);
@@ -227,7 +251,7 @@ extern "C" int snd_plan_create(const snd_config_t* cfg, int n_graphs, snd_plan_t
       Img m{5, kp_of(kin), (int)round_up(nout, 16), 0};
       return m;
     };
-    Img ims[6] = {img(L, w1), img(w1, w2), img(c.s2, c.s3), img(c.s3, c.s2), img(w2, w1), img(w1, L)};
+    Img ims[6] = {img(dj, w1), img(w1, w2), img(c.s2, c.s3), img(c.s3, c.s2), img(w2, w1), img(w1, dj)};
     bool ok = heads_fast_supported(c.s3, c.spatial_dim) && heads_fast_supported(c.n2, c.num_feature) &&
               w1 <= 128;
     for (auto& m : ims)
@@ -244,7 +268,7 @@ extern "C" int snd_plan_create(const snd_config_t* cfg, int n_graphs, snd_plan_t
       p->pk1f = ims[0]; p->pk2f = ims[1]; p->pk3f = ims[2];
       p->pk3b = ims[3]; p->pk2b = ims[4]; p->pk1b = ims[5];
       p->add_buf("ZERO", 64);           // never written: LDS-DMA zero source
-      p->add_buf("ZB", R * L, 2);
+      p->add_buf("ZB", R * dj, 2);
       p->add_buf("FY1", R * p->ld1);    p->add_buf("FU1", R * p->ld1, 2);
       p->add_buf("FY2", R * p->ld2);    p->add_buf("FU2", R * p->ld2, 2);
       p->add_buf("FY3", R * p->ld3);    p->add_buf("FU3", R * p->ld3);
@@ -255,18 +279,18 @@ extern "C" int snd_plan_create(const snd_config_t* cfg, int n_graphs, snd_plan_t
       p->add_buf("PFDEC1", (long long)rcb * 3 * w1);
       p->add_buf("PFHS", (long long)hb * heads_fast_parts(c.s3, c.spatial_dim));
       p->add_buf("PFHN", (long long)hb * heads_fast_parts(c.n2, c.num_feature));
-      p->gK1 = wgrad_geom(p->R, 5, L, w1);
+      p->gK1 = wgrad_geom(p->R, 5, dj, w1);
       p->gK2s = wgrad_geom(p->R, 5, c.s1, c.s2);
       p->gK2n = wgrad_geom(p->R, 5, c.n1, c.n2);
       p->gK3s = wgrad_geom(p->R, 5, c.s2, c.s3);
-      p->add_buf("FSK1", (long long)p->gK1.gx * 5 * L * wgrad_n4(w1));
+      p->add_buf("FSK1", (long long)p->gK1.gx * 5 * dj * wgrad_n4(w1));
       p->add_buf("FSK2S", (long long)p->gK2s.gx * 5 * c.s1 * wgrad_n4(c.s2));
       p->add_buf("FSK2N", (long long)p->gK2n.gx * 5 * c.n1 * wgrad_n4(c.n2));
       p->add_buf("FSK3S", (long long)p->gK3s.gx * 5 * c.s2 * wgrad_n4(c.s3));
     }
   }
   // ---- bf16 fast encoder: GraphConvolution 0 as (A X) W0, bf16 operands throughout
-  if (p->fast && !(debug_flags() & 512)) {
+  if (p->fast && !tref && !(debug_flags() & 512)) {
     auto img1 = [&](int kin, int nout) { return Img{1, kp_of(kin), (int)round_up(nout, 16), 0}; };
     Img ims[6] = {img1(h0 + f, h1), img1(W, gh), img1(gh, 2 * L), img1(2 * L, gh), img1(gh, W), img1(h1, h0)};
     bool ok = h0 % 8 == 0 && h1 % 8 == 0 && h1 <= 128 && f <= 4 && W <= 128 && h0 + f <= 128 &&
@@ -411,9 +435,9 @@ int gemm_fwd(const Ctx& x, int M, int N, int K, const float* A, int lda, const f
 }
 
 int gemm_wgrad(const Ctx& x, const float* A, int lda, int Mreal, bool ones, const float* D,
-               int ldd, int N, float* slab, const Split& sp) {
+               int ldd, int N, float* slab, const Split& sp, int K = -1) {
   GemmArgs g{};
-  g.M = Mreal + (ones ? 1 : 0); g.N = N; g.K = x.p->R;
+  g.M = Mreal + (ones ? 1 : 0); g.N = N; g.K = K < 0 ? x.p->R : K;
   g.A = A; g.lda = lda; g.a_ones_m1 = ones ? Mreal + 1 : 0;
   g.B = D; g.ldb = ldd; g.C = slab; g.kchunk = sp.kchunk;
   return launch_gemm(g, A_COL, B_ROW, E_PART, x.p->c.dtype, sp.splits, x.s);
@@ -479,7 +503,7 @@ WgArgs wg_args(const snd_plan& p, const char* ws, const WgGeom& g, const void* x
 int pack_decoder(const Ctx& x) {
   const snd_plan& p = *x.p;
   const snd_config_t& c = p.c;
-  const int L = c.latent, s1 = c.s1, n1 = c.n1, s2 = c.s2, n2 = c.n2, s3 = c.s3;
+  const int L = c.latent, dj = p.dj, s1 = c.s1, n1 = c.n1, s2 = c.s2, n2 = c.n2, s3 = c.s3;
   const int C1 = p.C1;
   auto dst = [&](const Img& im) { return reinterpret_cast<__bf16*>(x.ws + im.off); };
   auto src = [](const float* w, int A, int B, int a0, int a1, int b0, int b1, int noff, int koff,
@@ -489,7 +513,7 @@ int pack_decoder(const Ctx& x) {
   PackDesc d[6]{};
   // conv forward images: n = output channel (split layouts), k = input channel
   d[0] = {dst(p.pk1f), 5, p.pk1f.kp, p.pk1f.np, 2,
-          {src(K1, L, C1, 0, L, 0, s1, 0, 0, 0), src(K1, L, C1, 0, L, s1, C1, o1, 0, 0)}};
+          {src(K1, dj, C1, 0, dj, 0, s1, 0, 0, 0), src(K1, dj, C1, 0, dj, s1, C1, o1, 0, 0)}};
   d[1] = {dst(p.pk2f), 5, p.pk2f.kp, p.pk2f.np, 2,
           {src(K2s, s1, s2, 0, s1, 0, s2, 0, 0, 0), src(K2n, n1, n2, 0, n1, 0, n2, o2, o1, 0)}};
   d[2] = {dst(p.pk3f), 5, p.pk3f.kp, p.pk3f.np, 1, {src(K3s, s2, s3, 0, s2, 0, s3, 0, 0, 0), {}}};
@@ -498,7 +522,7 @@ int pack_decoder(const Ctx& x) {
   d[4] = {dst(p.pk2b), 5, p.pk2b.kp, p.pk2b.np, 2,
           {src(K2s, s1, s2, 0, s1, 0, s2, 0, 0, 1), src(K2n, n1, n2, 0, n1, 0, n2, o1, o2, 1)}};
   d[5] = {dst(p.pk1b), 5, p.pk1b.kp, p.pk1b.np, 2,
-          {src(K1, L, C1, 0, L, 0, s1, 0, 0, 1), src(K1, L, C1, 0, L, s1, C1, 0, o1, 1)}};
+          {src(K1, dj, C1, 0, dj, 0, s1, 0, 0, 1), src(K1, dj, C1, 0, dj, s1, C1, 0, o1, 1)}};
   if (!p.fast_enc) return launch_pack(d, 6, x.s);
   PackDesc e[12]{};
   for (int i = 0; i < 6; ++i) e[i] = d[i];
@@ -626,7 +650,7 @@ void encoder_fast_reduce(const Ctx& x, std::vector<ReduceDesc>& rd) {
 int decoder_fast(const Ctx& x, const snd_batch_t* batch, int only = -1) {
   const snd_plan& p = *x.p;
   const snd_config_t& c = p.c;
-  const int R = p.R, L = c.latent, s2 = c.s2, s3 = c.s3, n2 = c.n2;
+  const int R = p.R, L = p.dj, s2 = c.s2, s3 = c.s3, n2 = c.n2;   // L: width of J here
   const int sd = c.spatial_dim, nf = c.num_feature;
   const int w1 = p.m1.phys(), w2 = p.m2.phys(), o1 = p.m1.offb, o2 = p.m2.offb;
   auto bf = [&](const char* n) { return reinterpret_cast<__bf16*>(x.f(n)); };
@@ -709,7 +733,7 @@ int decoder_fast(const Ctx& x, const snd_batch_t* batch, int only = -1) {
 void decoder_fast_reduce(const Ctx& x, std::vector<ReduceDesc>& rd) {
   const snd_plan& p = *x.p;
   const snd_config_t& c = p.c;
-  const int L = c.latent, s1 = c.s1, n1 = c.n1, s2 = c.s2, n2 = c.n2, s3 = c.s3, C1 = p.C1;
+  const int L = p.dj, s1 = c.s1, n1 = c.n1, s2 = c.s2, n2 = c.n2, s3 = c.s3, C1 = p.C1;
   const int sd = c.spatial_dim, nf = c.num_feature;
   const int w1 = p.m1.phys(), o1 = p.m1.offb;
   const int rcb = rc_blocks(p.R), hb = heads_fast_blocks(p.R);
@@ -764,7 +788,7 @@ extern "C" int snd_plan_launch(const snd_plan_t* plan, const snd_batch_t* batch,
   const snd_plan& p = *plan;
   char* ws = (char*)workspace;
   hipStream_t s = (hipStream_t)stream;
-  const int L = p.c.latent;
+  const int L = p.dj;
   if (!strncmp(kernel, "zzt_dense", 9)) {   // zzt_dense | zzt_dense_v1 | zzt_dense_v2
     const ZztStage stg = zzt_stage(ws + p.buf("ZSTAGE"), p.B, p.N, L, p.c.dtype);
     const int variant = kernel[9] == '_' ? kernel[11] - '0' : 0;
@@ -783,6 +807,30 @@ extern "C" int snd_plan_launch(const snd_plan_t* plan, const snd_batch_t* batch,
                  p.c.h1, SND_SPMM_PLAIN, (__bf16*)(ws + p.buf("FDXW1")), p.c.h1};
     a.xcd_nbg = xcd_nbg(p.N, p.B);
     return launch_spmm_bf16(a, s);
+  }
+  if (!strncmp(kernel, "tref_", 5)) {   // graph-latent weight-streaming kernels
+    SND_CHECK_ARG(p.tref && p.last_params, "snd_plan_launch: no graph-latent step has run");
+    Ctx x{&p, ws, p.last_params, p.last_grads, s};
+    const snd_config_t& c = p.c;
+    const long long KH = (long long)p.N * p.W, CP = (long long)p.N * p.dj;
+    const float adj_scale = (float)(2.0 * (double)c.norm / ((double)p.B * p.N * (double)p.N));
+    if (!strcmp(kernel, "tref_head_fwd")) {
+      TrefHeadFwdArgs a{x.f("G"), KH, p.B, x.w("enc.Wh"), c.g_hidden, x.w("enc.bh"), x.f("PHF")};
+      return launch_tref_head_fwd(a, s);
+    }
+    if (!strcmp(kernel, "tref_head_bwd")) {
+      TrefHeadBwdArgs a{x.f("G"), KH, p.B, x.w("enc.Wh"), c.g_hidden, x.f("DH"), x.g("enc.Wh"), x.f("DG")};
+      return launch_tref_head_bwd(a, s);
+    }
+    if (!strcmp(kernel, "tref_proj_fwd")) {
+      TrefProjFwdArgs a{x.f("ZL"), p.B, c.latent, x.w("dec.Wp"), x.w("dec.bp"), CP, x.f("Z")};
+      return launch_tref_proj_fwd(a, s);
+    }
+    if (!strcmp(kernel, "tref_proj_bwd")) {
+      TrefProjBwdArgs a{x.f("ZL"), p.B, c.latent, x.w("dec.Wp"), CP, x.f("DZDEC"), x.f("DJD"), x.f("EJ"),
+                        adj_scale, x.g("dec.Wp"), x.g("dec.bp"), x.f("PDZ")};
+      return launch_tref_proj_bwd(a, s);
+    }
   }
   if (!strncmp(kernel, "dec:", 4) || !strcmp(kernel, "pack")) {   // fast decoder kernel k
     SND_CHECK_ARG(p.fast && p.last_params, "snd_plan_launch: no fast-path step has run");
@@ -820,6 +868,8 @@ extern "C" int snd_train_step(const snd_plan_t* plan, const snd_batch_t* batch,
   const int R = p.R, N = p.N, f = c.f_in, h0 = c.h0, h1 = c.h1, gh = c.g_hidden, L = c.latent;
   const int W = p.W, C1 = p.C1, s1 = c.s1, s2 = c.s2, s3 = c.s3, n1 = c.n1, n2 = c.n2;
   const int sd = c.spatial_dim, nf = c.num_feature;
+  const int dj = p.dj, RH = p.RH;
+  const long long KH = (long long)N * W, CP = (long long)N * dj;   // tref: flat(G) / flat(J) widths
   const int* rp = batch->rowptr;
   const int* ci = batch->colidx;
   const float* X = batch->features;
@@ -848,15 +898,41 @@ extern "C" int snd_train_step(const snd_plan_t* plan, const snd_batch_t* batch,
                  x.w("enc.bne.gamma"), x.w("enc.bne.beta"), x.f("G"), W};
       SND_TRY(launch_spmm(a, x.s));
     }
-    // node-wise heads (model.py:113-115): h = G Wh + bh; [mu || s] = h Wms + bms
-    SND_TRY(gemm_fwd(x, R, gh, W, x.f("G"), W, x.w("enc.Wh"), gh, B_ROW, x.f("Hh"), gh,
-                     x.w("enc.bh")));
-    SND_TRY(gemm_fwd(x, R, 2 * L, gh, x.f("Hh"), gh, x.w("enc.Wms"), 2 * L, B_ROW, x.f("MS"), 2 * L,
+    if (p.tref) {
+      // graph heads (model.py:113): h = flat(G) Wh + bh, split-K over the N*W rows of Wh
+      TrefHeadFwdArgs a{x.f("G"), KH, p.B, x.w("enc.Wh"), gh, x.w("enc.bh"), x.f("PHF")};
+      SND_TRY(launch_tref_head_fwd(a, x.s));
+      const ReduceDesc rd{x.f("PHF"), x.f("Hh"), tref_head_fwd_blocks(KH, gh), RH * gh,
+                          (long long)RH * gh, 1.f, 0, 0, 0, 0};
+      SND_TRY(launch_reduce(&rd, 1, x.s));
+    } else {
+      // node-wise heads (model.py:113-115): h = G Wh + bh
+      SND_TRY(gemm_fwd(x, R, gh, W, x.f("G"), W, x.w("enc.Wh"), gh, B_ROW, x.f("Hh"), gh,
+                       x.w("enc.bh")));
+    }
+    // [mu || s] = h Wms + bms (model.py:114-115)
+    SND_TRY(gemm_fwd(x, RH, 2 * L, gh, x.f("Hh"), gh, x.w("enc.Wms"), 2 * L, B_ROW, x.f("MS"), 2 * L,
                      x.w("enc.bms")));
   }
   // z = mu + eps exp(s) (model.py:159); KL partials (optimizer.py:193)
-  const ZztStage stg = zzt_stage(x.ws + p.buf("ZSTAGE"), p.B, N, L, c.dtype);
-  if (p.fast) {   // fused with the zz^T staging images
+  const ZztStage stg = zzt_stage(x.ws + p.buf("ZSTAGE"), p.B, N, dj, c.dtype);
+  if (p.tref) {
+    {   // z [B, L] (model_joint.py:89)
+      ReparamFwdArgs a{x.f("MS"), 2 * L, RH, L, eps, seed, step_counter, x.f("EPS"), x.f("ZL"),
+                       x.d("PKL"), nullptr, L};
+      SND_TRY(launch_reparam_fwd(a, x.s));
+    }
+    {   // J = reshape(z Wp + bp, [B, N, node_h]) (model_joint.py:97)
+      TrefProjFwdArgs a{x.f("ZL"), p.B, L, x.w("dec.Wp"), x.w("dec.bp"), CP, x.f("Z")};
+      SND_TRY(launch_tref_proj_fwd(a, x.s));
+    }
+    if (p.fast) {   // bf16 J for the decoder + zz^T staging images
+      ReparamPrepArgs a{x.f("Z"), dj, N, zzt_npad(N), p.B, dj, nullptr, 0, nullptr, nullptr,
+                        nullptr, (__bf16*)x.f("ZB"), (__bf16*)stg.jrow, (__bf16*)stg.jt, stg.colpart,
+                        nullptr, 1};
+      SND_TRY(launch_reparam_prep(a, zzt_dp(dj), x.s));
+    }
+  } else if (p.fast) {   // fused with the zz^T staging images
     ReparamPrepArgs a{x.f("MS"), 2 * L, N, zzt_npad(N), p.B, L, eps, seed, step_counter, x.f("Z"),
                       x.f("EPS"), (__bf16*)x.f("ZB"), (__bf16*)stg.jrow, (__bf16*)stg.jt, stg.colpart,
                       x.d("PKL")};
@@ -872,24 +948,24 @@ extern "C" int snd_train_step(const snd_plan_t* plan, const snd_batch_t* batch,
     // per-edge terms on the side stream, overlapping the dense kernel / decoder
     SND_TRY(fork(x));
     if (p.fast) {
-      EdgeBfArgs ea{rp, ci, R, (const __bf16*)x.f("ZB"), L, c.pos_weight, x.f("EJ"), x.d("PEDGE"),
+      EdgeBfArgs ea{rp, ci, R, (const __bf16*)x.f("ZB"), dj, c.pos_weight, x.f("EJ"), x.d("PEDGE"),
                     xcd_nbg(N, p.B)};
       SND_TRY(launch_edge_bf16(ea, side(x)));
     } else {
-      EdgeArgs ea{rp, ci, R, x.f("Z"), L, c.pos_weight, x.f("EJ"), x.d("PEDGE")};
+      EdgeArgs ea{rp, ci, R, x.f("Z"), dj, c.pos_weight, x.f("EJ"), x.d("PEDGE")};
       SND_TRY(launch_edge(ea, side(x)));
     }
     edge_mark = mark(x);
     if (edge_mark < -1) return SND_ERR_HIP;
-    if (!p.fast) SND_TRY(launch_zzt_prep(x.f("Z"), p.B, N, L, c.dtype, stg, x.s));
-    ZztArgs za{stg.jrow, stg.jt, N, zzt_npad(N), p.B, L, x.f("DJD"), x.d("PZZT"), stg.colpart, 0};
+    if (!p.fast) SND_TRY(launch_zzt_prep(x.f("Z"), p.B, N, dj, c.dtype, stg, x.s));
+    ZztArgs za{stg.jrow, stg.jt, N, zzt_npad(N), p.B, dj, x.f("DJD"), x.d("PZZT"), stg.colpart, 0};
     SND_TRY(launch_zzt_dense(za, c.dtype, x.s));
   }
   if (p.fast) {
     SND_TRY(decoder_fast(x, batch));
   } else {
     // decoders (model_joint.py:112-145): conv1d k5 SAME -> BN -> lrelu
-    SND_TRY(conv_fwd(x, x.f("Z"), L, L, "dec.K1", C1, "dec.b1", "dec.bn1.gamma", "dec.bn1.beta",
+    SND_TRY(conv_fwd(x, x.f("Z"), dj, dj, "dec.K1", C1, "dec.b1", "dec.bn1.gamma", "dec.bn1.beta",
                      x.f("Y1"), x.f("U1")));
     SND_TRY(conv_fwd(x, x.f("U1"), C1, s1, "dec.K2s", s2, "dec.b2s", "dec.bn2s.gamma",
                      "dec.bn2s.beta", x.f("Y2S"), x.f("U2S")));
@@ -931,28 +1007,45 @@ extern "C" int snd_train_step(const snd_plan_t* plan, const snd_batch_t* batch,
                    x.f("DY1"), C1, x.f("PDEC1")};
       SND_TRY(launch_dec_bwd(&d, 1, R, x.s));
     }
-    SND_TRY(conv_bwd_data(x, x.f("DY1"), C1, "dec.K1", L, x.f("DZDEC"), L));
-    SND_TRY(conv_wgrad(x, x.f("Z"), L, L, x.f("DY1"), C1, x.f("SK1"), p.sK1));
+    SND_TRY(conv_bwd_data(x, x.f("DY1"), C1, "dec.K1", dj, x.f("DZDEC"), dj));
+    SND_TRY(conv_wgrad(x, x.f("Z"), dj, dj, x.f("DY1"), C1, x.f("SK1"), p.sK1));
   }
-  // reparameterisation + KL backward; dz = conv-decoder grad + zz^T CE grad
+  // reparameterisation + KL backward; dJ = conv-decoder grad + zz^T CE grad
   const double pairs = (double)p.B * N * (double)N;
-  // dL/dz_i = sum_j (G_ij + G_ji) z_j = 2 sum_j G_ij z_j (G symmetric)
+  // dL/dJ_i = sum_j (G_ij + G_ji) J_j = 2 sum_j G_ij J_j (G symmetric)
   const float adj_scale = (float)(2.0 * (double)c.norm / pairs);
-  const float kl_scale = (float)((double)c.beta / ((double)R * L));
+  const float kl_scale = (float)((double)c.beta / ((double)RH * L));
   SND_TRY(wait_mark(x, edge_mark));   // EJ
   if (p.fast_enc) {
     SND_TRY(encoder_fast_bwd(x, batch, adj_scale, kl_scale));
   } else {
-    {
+    if (p.tref) {
+      {   // d_sg_lin1 backward: dWp, dbp written; dz partials per block
+        TrefProjBwdArgs a{x.f("ZL"), p.B, L, x.w("dec.Wp"), CP, x.f("DZDEC"), x.f("DJD"), x.f("EJ"),
+                          adj_scale, x.g("dec.Wp"), x.g("dec.bp"), x.f("PDZ")};
+        SND_TRY(launch_tref_proj_bwd(a, x.s));
+        const ReduceDesc rd{x.f("PDZ"), x.f("DZL"), tref_proj_bwd_blocks(CP), RH * L,
+                            (long long)RH * L, 1.f, 0, 0, 0, 0};
+        SND_TRY(launch_reduce(&rd, 1, x.s));
+      }
+      ReparamBwdArgs a{x.f("MS"), 2 * L, RH, L, x.f("EPS"), x.f("DZL"), nullptr, nullptr, 0.f,
+                       kl_scale, x.f("DMS"), 2 * L};
+      SND_TRY(launch_reparam_bwd(a, x.s));
+    } else {
       ReparamBwdArgs a{x.f("MS"), 2 * L, R, L, x.f("EPS"), x.f("DZDEC"), x.f("DJD"), x.f("EJ"),
                        adj_scale, kl_scale, x.f("DMS"), 2 * L};
       SND_TRY(launch_reparam_bwd(a, x.s));
     }
-    SND_TRY(gemm_wgrad(x, x.f("Hh"), gh, gh, true, x.f("DMS"), 2 * L, 2 * L, x.f("SWMS"), p.sWms));
-    SND_TRY(gemm_fwd(x, R, gh, 2 * L, x.f("DMS"), 2 * L, x.w("enc.Wms"), 2 * L, B_COL, x.f("DH"), gh,
+    SND_TRY(gemm_wgrad(x, x.f("Hh"), gh, gh, true, x.f("DMS"), 2 * L, 2 * L, x.f("SWMS"), p.sWms, RH));
+    SND_TRY(gemm_fwd(x, RH, gh, 2 * L, x.f("DMS"), 2 * L, x.w("enc.Wms"), 2 * L, B_COL, x.f("DH"), gh,
                      nullptr));
-    SND_TRY(gemm_wgrad(x, x.f("G"), W, W, true, x.f("DH"), gh, gh, x.f("SWH"), p.sWh));
-    SND_TRY(gemm_fwd(x, R, W, gh, x.f("DH"), gh, x.w("enc.Wh"), gh, B_COL, x.f("DG"), W, nullptr));
+    if (p.tref) {   // dWh written complete; dG = dh Wh^T per graph
+      TrefHeadBwdArgs a{x.f("G"), KH, p.B, x.w("enc.Wh"), gh, x.f("DH"), x.g("enc.Wh"), x.f("DG")};
+      SND_TRY(launch_tref_head_bwd(a, x.s));
+    } else {
+      SND_TRY(gemm_wgrad(x, x.f("G"), W, W, true, x.f("DH"), gh, gh, x.f("SWH"), p.sWh));
+      SND_TRY(gemm_fwd(x, R, W, gh, x.f("DH"), gh, x.w("enc.Wh"), gh, B_COL, x.f("DG"), W, nullptr));
+    }
     {
       EncBwdArgs a{x.f("DG"), W, x.f("H2"), W, x.w("enc.bne.gamma"), W, x.f("P1"), h1,
                    x.w("enc.bn1.gamma"), h1, x.f("DP1"), h1, x.f("PENC1"), 1};
@@ -993,11 +1086,14 @@ extern "C" int snd_train_step(const snd_plan_t* plan, const snd_batch_t* batch,
   } else {
     slab("SW0", p.sW0, f, h0, "enc.W0", f * h0, nullptr);
     slab("SW1", p.sW1, h0 + f, h1, "enc.W1", (h0 + f) * h1, nullptr);
-    slab("SWH", p.sWh, W + 1, gh, "enc.Wh", W * gh, "enc.bh");
+    if (p.tref)   // dbh = sum over graphs of dh
+      rd.push_back({x.f("DH"), x.g("enc.bh"), RH, gh, (long long)gh, 1.f, 0});
+    else
+      slab("SWH", p.sWh, W + 1, gh, "enc.Wh", W * gh, "enc.bh");
     slab("SWMS", p.sWms, gh + 1, 2 * L, "enc.Wms", gh * 2 * L, "enc.bms");
   }
   if (!p.fast) {
-    slab("SK1", p.sK1, 5 * L, C1, "dec.K1", 5 * L * C1, nullptr);
+    slab("SK1", p.sK1, 5 * dj, C1, "dec.K1", 5 * dj * C1, nullptr);
     slab("SK2S", p.sK2s, 5 * s1, s2, "dec.K2s", 5 * s1 * s2, nullptr);
     slab("SK2N", p.sK2n, 5 * n1, n2, "dec.K2n", 5 * n1 * n2, nullptr);
     slab("SK3S", p.sK3s, 5 * s2, s3, "dec.K3s", 5 * s2 * s3, nullptr);
@@ -1033,9 +1129,11 @@ extern "C" int snd_train_step(const snd_plan_t* plan, const snd_batch_t* batch,
   }
   SND_TRY(launch_reduce(rd.data(), (int)rd.size(), x.s));
 
+  const int n_kl = (p.fast && !p.tref) ? reparam_prep_blocks(p.B, zzt_npad(N)) : reparam_blocks(RH, L);
   FinalizeArgs fa{x.d("PZZT"), zzt_dense_blocks(p.B, N), x.d("PEDGE"),
-                  p.fast ? edge_bf16_blocks(R) : edge_blocks(R, L),
-                  x.d("PKL"), p.fast ? reparam_prep_blocks(p.B, zzt_npad(N)) : reparam_blocks(R, L), x.d("PSSES"), x.d("PSSEN"), nh,
-                  rp, p.B, N, L, sd, nf, c.beta, c.norm, losses, grads + p.pcount, step_counter};
+                  p.fast ? edge_bf16_blocks(R) : edge_blocks(R, dj),
+                  x.d("PKL"), n_kl, x.d("PSSES"), x.d("PSSEN"), nh,
+                  rp, p.B, N, L, sd, nf, c.beta, c.norm, losses, grads + p.pcount, step_counter,
+                  (double)RH * L};
   return launch_finalize(fa, x.s);
 }

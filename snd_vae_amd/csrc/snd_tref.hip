@@ -1,0 +1,374 @@
+// Graph-latent (T-ref) heads and decoder projection on MI355X (gfx950).
+//
+// model.py:113-115 applies linear() to tf.reshape(g, [B, -1]): a [B, N*W] x
+// [N*W, g_hidden] product whose weight (27.4 M floats at N=4096, W=67) dwarfs
+// every activation, and model_joint.py:97 ('d_sg_lin1') projects z [B, L] to
+// [B, N*node_h] through a [L, N*node_h] weight (26.2 M floats).  With B <= 8
+// graphs per GPU these are weight streams: ~8 FMA per weight element, so each
+// kernel is bound by reading (and, backward, writing) its weight once from HBM.
+// The layouts keep every weight access a coalesced float4 stream:
+//
+//   head fwd   thread = (row slot, column quad); rows stride by the slots,
+//              G[b, k] broadcast from LDS; split-K partial slab per block.
+//   head bwd   two Wh rows per wave instruction (32 lanes x column quads):
+//              dWh[k, :] = sum_b G[b, k] dh[b, :] written from registers,
+//              dG[b, k] = dh[b, :] . Wh[k, :] reduced over the 32 lanes (DPP).
+//   proj fwd   thread = column quad, z broadcast from LDS, 20 loads in flight.
+//   proj bwd   thread = column quad holding dJ[:, quad]; wave w owns latent
+//              rows l = w (mod 4): dWp written, dz wave-reduced per l (DPP).
+//
+// Reductions are fixed-order (no float atomics): results are bitwise
+// reproducible like the rest of the step.
+#include "snd_tref.hpp"
+
+#include <algorithm>
+
+namespace snd {
+namespace {
+
+constexpr int B8 = kTrefMaxB;
+
+__device__ __forceinline__ float4 f4(float a) { return make_float4(a, a, a, a); }
+__device__ __forceinline__ void fma4(float4& acc, float s, const float4& w) {
+  acc.x = fmaf(s, w.x, acc.x);
+  acc.y = fmaf(s, w.y, acc.y);
+  acc.z = fmaf(s, w.z, acc.z);
+  acc.w = fmaf(s, w.w, acc.w);
+}
+__device__ __forceinline__ float dot4(const float4& a, const float4& b) {
+  return fmaf(a.x, b.x, fmaf(a.y, b.y, fmaf(a.z, b.z, a.w * b.w)));
+}
+
+// ------------------------------------------------------------------ head fwd
+constexpr int HF_T = 256;
+
+__global__ void __launch_bounds__(HF_T) tref_head_fwd_kernel(TrefHeadFwdArgs a, int rpb) {
+  extern __shared__ float sm[];
+  const int TPR = a.gh >> 2, RPI = HF_T / TPR;
+  const int t = threadIdx.x, q = t % TPR, r = t / TPR;
+  const long long k0 = (long long)blockIdx.x * rpb;
+  const int nk = (int)std::min<long long>(rpb, a.K - k0);
+  // G[b, k0 .. k0+nk) -> gs[kk][8] (coalesced per graph)
+  for (int b = 0; b < B8; ++b)
+    for (int kk = t; kk < nk; kk += HF_T)
+      sm[kk * B8 + b] = b < a.B ? a.g[(long long)b * a.K + k0 + kk] : 0.f;
+  __syncthreads();
+  float4 acc[B8];
+#pragma unroll
+  for (int b = 0; b < B8; ++b) acc[b] = f4(0.f);
+  if (r < RPI) {
+    const float* wrow = a.wh + (k0 + r) * a.gh + 4 * q;
+    const long long wstep = (long long)RPI * a.gh;
+    int kk = r;
+    for (; kk + 7 * RPI < nk; kk += 8 * RPI) {
+      float4 w[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) w[u] = *reinterpret_cast<const float4*>(wrow + u * wstep);
+      wrow += 8 * wstep;
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const float4 g0 = *reinterpret_cast<const float4*>(sm + (kk + u * RPI) * B8);
+        const float4 g1 = *reinterpret_cast<const float4*>(sm + (kk + u * RPI) * B8 + 4);
+        fma4(acc[0], g0.x, w[u]); fma4(acc[1], g0.y, w[u]);
+        fma4(acc[2], g0.z, w[u]); fma4(acc[3], g0.w, w[u]);
+        fma4(acc[4], g1.x, w[u]); fma4(acc[5], g1.y, w[u]);
+        fma4(acc[6], g1.z, w[u]); fma4(acc[7], g1.w, w[u]);
+      }
+    }
+    for (; kk < nk; kk += RPI) {
+      const float4 w = *reinterpret_cast<const float4*>(wrow);
+      wrow += wstep;
+      const float4 g0 = *reinterpret_cast<const float4*>(sm + kk * B8);
+      const float4 g1 = *reinterpret_cast<const float4*>(sm + kk * B8 + 4);
+      fma4(acc[0], g0.x, w); fma4(acc[1], g0.y, w); fma4(acc[2], g0.z, w); fma4(acc[3], g0.w, w);
+      fma4(acc[4], g1.x, w); fma4(acc[5], g1.y, w); fma4(acc[6], g1.z, w); fma4(acc[7], g1.w, w);
+    }
+  }
+  __syncthreads();
+  // reduce the row slots: red[r][b][gh]
+  if (r < RPI)
+#pragma unroll
+    for (int b = 0; b < B8; ++b)
+      *reinterpret_cast<float4*>(sm + (r * B8 + b) * a.gh + 4 * q) = acc[b];
+  __syncthreads();
+  const int outs = a.B * a.gh;
+  for (int o = t; o < outs; o += HF_T) {
+    float s = 0.f;
+    for (int rr = 0; rr < RPI; ++rr) s += sm[rr * B8 * a.gh + o];
+    if (blockIdx.x == 0) s += a.bh[o % a.gh];
+    a.slab[(long long)blockIdx.x * outs + o] = s;
+  }
+}
+
+int head_fwd_rpb(long long K, int gh) {
+  const int RPI = HF_T / (gh / 4);
+  long long rpb = round_up(cdiv(K, 1024), RPI);
+  rpb = std::max<long long>(rpb, 4LL * RPI);
+  return (int)std::min<long long>(rpb, 1024);
+}
+
+// ------------------------------------------------------------------ head bwd
+// Two rows of Wh per wave instruction: lanes 32h + q (h = row of the pair, q =
+// column quad, q < gh/4 active).  dWh is written straight from registers; the
+// per-row dot products dG[b, k] = dh[b, :] . Wh[k, :] are reduced over the 32
+// lanes of the half with DPP (row16) + one xor-16 swizzle, and parked in LDS so
+// dG leaves the block as coalesced rows.
+constexpr int HB_T = 256, HB_RPB = 256;
+
+__global__ void __launch_bounds__(HB_T) tref_head_bwd_kernel(TrefHeadBwdArgs a) {
+  __shared__ float gs[HB_RPB * B8];      // G[b, k0 + kk] as [kk][8]
+  __shared__ float dgs[B8 * HB_RPB];     // dG[b, k0 + kk] as [b][kk]
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const int h = lane >> 5, q = lane & 31;
+  const int TPR = a.gh >> 2;
+  const bool qa = q < TPR;
+  const long long k0 = (long long)blockIdx.x * HB_RPB;
+  const int nk = (int)std::min<long long>(HB_RPB, a.K - k0);
+  for (int b = 0; b < B8; ++b)
+    for (int kk = t; kk < nk; kk += HB_T)
+      gs[kk * B8 + b] = b < a.B ? a.g[(long long)b * a.K + k0 + kk] : 0.f;
+  float4 dh[B8];
+#pragma unroll
+  for (int b = 0; b < B8; ++b)
+    dh[b] = (qa && b < a.B) ? *reinterpret_cast<const float4*>(a.dh + b * a.gh + 4 * q) : f4(0.f);
+  __syncthreads();
+  constexpr int U = 4;                   // row pairs in flight per wave
+  const int r0 = 2 * wv + h;             // row slot of this lane; 8 rows per block pass
+  for (int base = 0; base < nk; base += 8 * U) {
+    float4 w[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int kk = base + 8 * u + r0;
+      w[u] = (qa && kk < nk) ? *reinterpret_cast<const float4*>(a.wh + (k0 + kk) * a.gh + 4 * q)
+                             : f4(0.f);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int kk = base + 8 * u + r0;
+      const bool rv = kk < nk;
+      const int kc = rv ? kk : 0;
+      const float4 g0 = *reinterpret_cast<const float4*>(gs + kc * B8);
+      const float4 g1 = *reinterpret_cast<const float4*>(gs + kc * B8 + 4);
+      const float gb[B8] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
+      float4 dw = f4(0.f);
+#pragma unroll
+      for (int b = 0; b < B8; ++b) fma4(dw, gb[b], dh[b]);
+      if (qa && rv) *reinterpret_cast<float4*>(a.dwh + (k0 + kk) * a.gh + 4 * q) = dw;
+      float p[B8];
+#pragma unroll
+      for (int b = 0; b < B8; ++b) {
+        p[b] = row16_sum(dot4(dh[b], w[u]));          // all lanes active: inactive quads hold 0
+        p[b] += __shfl_xor(p[b], 16, 64);
+      }
+      if (q == 0 && rv)
+#pragma unroll
+        for (int b = 0; b < B8; ++b) dgs[b * HB_RPB + kk] = p[b];
+    }
+  }
+  __syncthreads();
+  for (int b = 0; b < a.B; ++b)
+    for (int kk = t; kk < nk; kk += HB_T) a.dg[(long long)b * a.K + k0 + kk] = dgs[b * HB_RPB + kk];
+}
+
+// ------------------------------------------------------------------ proj fwd
+__global__ void __launch_bounds__(64) tref_proj_fwd_kernel(TrefProjFwdArgs a) {
+  __shared__ float zs[128 * B8];          // [l][8]
+  for (int i = threadIdx.x; i < a.L * B8; i += 64) {
+    const int l = i >> 3, b = i & 7;
+    zs[i] = b < a.B ? a.z[b * a.L + l] : 0.f;
+  }
+  __syncthreads();
+  const long long c4 = 4LL * ((long long)blockIdx.x * 64 + threadIdx.x);
+  if (c4 >= a.Cp) return;
+  float4 acc[B8];
+  const float4 bias = *reinterpret_cast<const float4*>(a.bp + c4);
+#pragma unroll
+  for (int b = 0; b < B8; ++b) acc[b] = bias;
+  const float* wcol = a.wp + c4;
+  int l = 0;
+  constexpr int U = 20;                  // one wave per SIMD: keep 20 KB of loads in flight
+  for (; l + U - 1 < a.L; l += U) {
+    float4 w[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) w[u] = *reinterpret_cast<const float4*>(wcol + (long long)(l + u) * a.Cp);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const float4 z0 = *reinterpret_cast<const float4*>(zs + (l + u) * B8);
+      const float4 z1 = *reinterpret_cast<const float4*>(zs + (l + u) * B8 + 4);
+      fma4(acc[0], z0.x, w[u]); fma4(acc[1], z0.y, w[u]); fma4(acc[2], z0.z, w[u]);
+      fma4(acc[3], z0.w, w[u]); fma4(acc[4], z1.x, w[u]); fma4(acc[5], z1.y, w[u]);
+      fma4(acc[6], z1.z, w[u]); fma4(acc[7], z1.w, w[u]);
+    }
+  }
+  for (; l < a.L; ++l) {
+    const float4 w = *reinterpret_cast<const float4*>(wcol + (long long)l * a.Cp);
+    const float4 z0 = *reinterpret_cast<const float4*>(zs + l * B8);
+    const float4 z1 = *reinterpret_cast<const float4*>(zs + l * B8 + 4);
+    fma4(acc[0], z0.x, w); fma4(acc[1], z0.y, w); fma4(acc[2], z0.z, w); fma4(acc[3], z0.w, w);
+    fma4(acc[4], z1.x, w); fma4(acc[5], z1.y, w); fma4(acc[6], z1.z, w); fma4(acc[7], z1.w, w);
+  }
+#pragma unroll
+  for (int b = 0; b < B8; ++b)
+    if (b < a.B) *reinterpret_cast<float4*>(a.j + (long long)b * a.Cp + c4) = acc[b];
+}
+
+// ------------------------------------------------------------------ proj bwd
+// Block = 64 column quads (256 columns) x 4 waves; wave w owns latent rows
+// l = w (mod 4).  Every lane keeps dJ[b, its quad] in registers (combined from the
+// three producers on load), streams Wp[l, quad] in and dWp[l, quad] out, and the
+// 8 dot products per l are wave-reduced with DPP; lane 0 parks them in LDS, and
+// the block writes one [B][L] dz partial.
+constexpr int PB_T = 256, PB_W = PB_T / 64;
+
+__global__ void __launch_bounds__(PB_T) tref_proj_bwd_kernel(TrefProjBwdArgs a) {
+  __shared__ float zs[128 * B8];         // z as [l][8]
+  __shared__ float red[128 * B8];        // dz partial as [l][8]
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  for (int i = t; i < a.L * B8; i += PB_T) {
+    const int l = i >> 3, b = i & 7;
+    zs[i] = b < a.B ? a.z[b * a.L + l] : 0.f;
+  }
+  const long long c4 = 4LL * ((long long)blockIdx.x * 64 + lane);
+  const bool cv = c4 < a.Cp;
+  float4 d[B8];
+#pragma unroll
+  for (int b = 0; b < B8; ++b) {
+    d[b] = f4(0.f);
+    if (cv && b < a.B) {
+      const long long i = (long long)b * a.Cp + c4;
+      const float4 x = *reinterpret_cast<const float4*>(a.dz_dec + i);
+      const float4 y = *reinterpret_cast<const float4*>(a.dJd + i);
+      const float4 z = *reinterpret_cast<const float4*>(a.ej + i);
+      d[b] = make_float4(fmaf(a.adj_scale, y.x + z.x, x.x), fmaf(a.adj_scale, y.y + z.y, x.y),
+                         fmaf(a.adj_scale, y.z + z.z, x.z), fmaf(a.adj_scale, y.w + z.w, x.w));
+    }
+  }
+  if (wv == 0 && cv) {
+    float4 s = d[0];
+#pragma unroll
+    for (int b = 1; b < B8; ++b) { s.x += d[b].x; s.y += d[b].y; s.z += d[b].z; s.w += d[b].w; }
+    *reinterpret_cast<float4*>(a.dbp + c4) = s;
+  }
+  __syncthreads();
+  constexpr int U = 5;
+  for (int l0 = wv; l0 < a.L; l0 += PB_W * U) {
+    float4 w[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int l = l0 + PB_W * u;
+      w[u] = (cv && l < a.L) ? *reinterpret_cast<const float4*>(a.wp + (long long)l * a.Cp + c4) : f4(0.f);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int l = l0 + PB_W * u;
+      if (l >= a.L) break;                       // wave-uniform
+      const float4 z0 = *reinterpret_cast<const float4*>(zs + l * B8);
+      const float4 z1 = *reinterpret_cast<const float4*>(zs + l * B8 + 4);
+      float4 dw = f4(0.f);
+      fma4(dw, z0.x, d[0]); fma4(dw, z0.y, d[1]); fma4(dw, z0.z, d[2]); fma4(dw, z0.w, d[3]);
+      fma4(dw, z1.x, d[4]); fma4(dw, z1.y, d[5]); fma4(dw, z1.z, d[6]); fma4(dw, z1.w, d[7]);
+      if (cv) *reinterpret_cast<float4*>(a.dwp + (long long)l * a.Cp + c4) = dw;
+#pragma unroll
+      for (int b = 0; b < B8; ++b) {
+        float p = row16_sum(dot4(d[b], w[u]));
+        p += __shfl_xor(p, 16, 64);
+        p += __shfl_xor(p, 32, 64);
+        if (lane == 0) red[l * B8 + b] = p;
+      }
+    }
+  }
+  __syncthreads();
+  for (int i = t; i < a.L * a.B; i += PB_T) {
+    const int b = i / a.L, l = i - b * a.L;
+    a.slab[(long long)blockIdx.x * a.B * a.L + i] = red[l * B8 + b];
+  }
+}
+
+// ------------------------------------------------------------------ Adam (float4)
+__global__ void __launch_bounds__(256) adam_vec_kernel(float4* p, const float4* g, float4* m,
+                                                       float4* v, long long n4, float lr, float b1,
+                                                       float b2, float eps, float gscale,
+                                                       const int* step) {
+  const int t = *step;
+  const double lr_t = (double)lr * sqrt(1.0 - pow((double)b2, t)) / (1.0 - pow((double)b1, t));
+  const float lrt = (float)lr_t;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n4; i += (long long)gridDim.x * 256) {
+    const float4 gi = g[i];
+    float4 mi = m[i], vi = v[i], pi = p[i];
+#define SND_ADAM_LANE(c)                                   \
+    {                                                      \
+      const float gc = gi.c * gscale;                      \
+      mi.c = b1 * mi.c + (1.f - b1) * gc;                  \
+      vi.c = b2 * vi.c + (1.f - b2) * gc * gc;             \
+      pi.c -= lrt * mi.c / (sqrtf(vi.c) + eps);            \
+    }
+    SND_ADAM_LANE(x) SND_ADAM_LANE(y) SND_ADAM_LANE(z) SND_ADAM_LANE(w)
+#undef SND_ADAM_LANE
+    m[i] = mi;
+    v[i] = vi;
+    p[i] = pi;
+  }
+}
+
+}  // namespace
+
+int tref_head_fwd_blocks(long long K, int gh) { return cdiv(K, head_fwd_rpb(K, gh)); }
+
+int launch_tref_head_fwd(const TrefHeadFwdArgs& a, hipStream_t s) {
+  SND_CHECK_ARG(a.B >= 1 && a.B <= B8 && a.gh % 4 == 0 && a.gh >= 4 && a.gh <= 128 && a.K > 0,
+                "tref_head_fwd: B in 1..8, g_hidden %% 4 in 4..128");
+  SND_CHECK_ARG(a.g && a.wh && a.bh && a.slab, "tref_head_fwd: null operand");
+  const int rpb = head_fwd_rpb(a.K, a.gh);
+  const int RPI = HF_T / (a.gh / 4);
+  const size_t lds = sizeof(float) * std::max<size_t>((size_t)rpb * B8, (size_t)RPI * B8 * a.gh);
+  hipLaunchKernelGGL(tref_head_fwd_kernel, dim3(tref_head_fwd_blocks(a.K, a.gh)), dim3(HF_T), lds, s, a,
+                     rpb);
+  SND_LAUNCH_CHECK("tref_head_fwd_kernel");
+  return 0;
+}
+
+int launch_tref_head_bwd(const TrefHeadBwdArgs& a, hipStream_t s) {
+  SND_CHECK_ARG(a.B >= 1 && a.B <= B8 && a.gh % 4 == 0 && a.gh >= 4 && a.gh <= 128 && a.K > 0,
+                "tref_head_bwd: B in 1..8, g_hidden %% 4 in 4..128");
+  SND_CHECK_ARG(a.g && a.wh && a.dh && a.dwh && a.dg, "tref_head_bwd: null operand");
+  hipLaunchKernelGGL(tref_head_bwd_kernel, dim3(cdiv(a.K, HB_RPB)), dim3(HB_T), 0, s, a);
+  SND_LAUNCH_CHECK("tref_head_bwd_kernel");
+  return 0;
+}
+
+int launch_tref_proj_fwd(const TrefProjFwdArgs& a, hipStream_t s) {
+  SND_CHECK_ARG(a.B >= 1 && a.B <= B8 && a.L >= 1 && a.L <= 128 && a.Cp % 4 == 0 && a.Cp > 0,
+                "tref_proj_fwd: B in 1..8, L <= 128, Cp %% 4");
+  SND_CHECK_ARG(a.z && a.wp && a.bp && a.j, "tref_proj_fwd: null operand");
+  hipLaunchKernelGGL(tref_proj_fwd_kernel, dim3(cdiv(a.Cp / 4, 64)), dim3(64), 0, s, a);
+  SND_LAUNCH_CHECK("tref_proj_fwd_kernel");
+  return 0;
+}
+
+int tref_proj_bwd_blocks(long long Cp) { return cdiv(Cp, 256); }
+
+int launch_tref_proj_bwd(const TrefProjBwdArgs& a, hipStream_t s) {
+  SND_CHECK_ARG(a.B >= 1 && a.B <= B8 && a.L >= 1 && a.L <= 128 && a.Cp % 4 == 0 && a.Cp > 0,
+                "tref_proj_bwd: B in 1..8, L <= 128, Cp %% 4");
+  SND_CHECK_ARG(a.z && a.wp && a.dz_dec && a.dJd && a.ej && a.dwp && a.dbp && a.slab,
+                "tref_proj_bwd: null operand");
+  hipLaunchKernelGGL(tref_proj_bwd_kernel, dim3(tref_proj_bwd_blocks(a.Cp)), dim3(PB_T), 0, s, a);
+  SND_LAUNCH_CHECK("tref_proj_bwd_kernel");
+  return 0;
+}
+
+int launch_adam_vec(float* p, const float* g, float* m, float* v, long long n, float lr, float b1,
+                    float b2, float eps, float gscale, const int* step, hipStream_t s) {
+  SND_CHECK_ARG(n % 4 == 0 && ((uintptr_t)p | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v) % 16 == 0,
+                "adam_vec: n %% 4 and 16-byte aligned buffers");
+  if (n == 0) return 0;
+  const long long n4 = n / 4;
+  const int blocks = (int)std::min<long long>(cdiv(n4, 256), 8192);
+  hipLaunchKernelGGL(adam_vec_kernel, dim3(blocks), dim3(256), 0, s, reinterpret_cast<float4*>(p),
+                     reinterpret_cast<const float4*>(g), reinterpret_cast<float4*>(m),
+                     reinterpret_cast<float4*>(v), n4, lr, b1, b2, eps, gscale, step);
+  SND_LAUNCH_CHECK("adam_vec_kernel");
+  return 0;
+}
+
+}  // namespace snd

@@ -32,8 +32,8 @@ class GraphBatch:
     """Host-side batch of B spatial graphs with N nodes each.
 
     ``rowptr``/``colidx`` form the block-diagonal CSR.  ``features`` is the
-    encoder input X = [x_feat || S] for the tscale topology (decision iii) or
-    x_feat for tref; ``feature_truth`` and ``spatial_truth`` are the decoder
+    encoder input X = [x_feat || S] when ``cfg.encoder_coords`` (decision iii)
+    or x_feat alone; ``feature_truth`` and ``spatial_truth`` are the decoder
     targets (`main.py:258-259`).
     """
     n_graphs: int
@@ -139,7 +139,7 @@ def synthetic_batch(cfg: SNDConfig, n_graphs: int, seed: Optional[int] = None,
         s = pos[:, :cfg.spatial_dim]                     # like geometry / 600
         xs.append(x)
         ss.append(s)
-        feats.append(np.concatenate([x, s], 1) if cfg.topology == "tscale" else x)
+        feats.append(np.concatenate([x, s], 1) if cfg.encoder_coords else x)
     rowptr, colidx = stack_csr(parts, n)
     return GraphBatch(n_graphs, n, rowptr, colidx,
                       np.ascontiguousarray(np.concatenate(feats), np.float32),
@@ -158,7 +158,7 @@ def batch_from_dense(cfg: SNDConfig, adj: np.ndarray, feature: np.ndarray,
     rowptr, colidx = stack_csr([csr_from_dense(adj[i]) for i in range(b)], n)
     x = np.asarray(feature, np.float32).reshape(b * n, -1)
     s = np.asarray(spatial, np.float32).reshape(b * n, -1)
-    f = np.concatenate([x, s], 1) if cfg.topology == "tscale" else x
+    f = np.concatenate([x, s], 1) if cfg.encoder_coords else x
     return GraphBatch(b, n, rowptr, colidx, np.ascontiguousarray(f, np.float32),
                       np.ascontiguousarray(x), np.ascontiguousarray(s))
 

@@ -1,8 +1,9 @@
 """SGCNModelVAE on MI355X: parameters, plan and device batch.
 
 Host-side mirror of the reference model classes for the hot path
-(`model.py:19-161` encoder/get_z, `model_joint.py:94-182` decoders) in the
-node-latent topology.  The reference builds a TF graph whose variables live in
+(`model.py:19-161` encoder/get_z, `model_joint.py:94-182` decoders) in both
+decoder-input topologies (node latent ``tscale``; graph latent ``tref`` with
+the 'd_sg_lin1' projection of `model_joint.py:97`).  The reference builds a TF graph whose variables live in
 the TF store; here a ``snd_plan`` (libsndvae.so) fixes the shapes of one
 device batch and all trainable state is one flat fp32 device buffer
 (`params.py`).  Forward + backward run as one native launch sequence
@@ -31,14 +32,12 @@ TAIL = 64  # floats after the parameters in the gradient buffer (loss terms for 
 
 
 def c_config(cfg: SNDConfig, dtype: str) -> _lib.Config:
-    if cfg.topology != "tscale":
-        raise NotImplementedError("the GPU path implements the node-latent topology")
     s1, s2, s3 = cfg.s_d_channel
     n1, n2 = cfg.n_d_channel
     return _lib.Config(cfg.n_nodes, cfg.f_in, cfg.num_feature, cfg.spatial_dim,
                        cfg.g_conv_hidden[0], cfg.g_conv_hidden[1], cfg.g_hidden_size,
                        cfg.latent, s1, s2, s3, n1, n2, cfg.beta, cfg.pos_weight, cfg.norm,
-                       DTYPES[dtype])
+                       DTYPES[dtype], _lib.TOPOLOGY[cfg.topology], cfg.node_h_size)
 
 
 class DeviceBatch:
@@ -63,7 +62,7 @@ class DeviceBatch:
 
 
 class SGCNModelVAE:
-    """Plan + flat parameters of the node-latent SND-VAE on one GPU."""
+    """Plan + flat parameters of the SND-VAE on one GPU (either topology)."""
 
     def __init__(self, cfg: SNDConfig, n_graphs: int, dtype: str = "bf16",
                  device="cuda", seed: int = 0, blocks: Optional[Dict[str, np.ndarray]] = None):
@@ -122,20 +121,34 @@ class SGCNModelVAE:
         t = self.workspace[off.value:off.value + n.value * es].view(dtype)
         return t.view(*shape) if shape is not None else t
 
-    def _rows(self, name, width):
-        return self.buffer(name).view(self.n_graphs * self.cfg.n_nodes, width)
+    def _rows(self, name, width, per_graph=False):
+        rows = self.n_graphs if per_graph else self.n_graphs * self.cfg.n_nodes
+        return self.buffer(name)[:rows * width].view(rows, width)
+
+    @property
+    def _graph_latent(self):
+        return self.cfg.topology == "tref"
 
     @property
     def z_mean_sg(self):
-        return self._rows("MS", 2 * self.cfg.latent)[:, :self.cfg.latent]
+        """[B, L] (graph latent) or [B*N, L] (node latent), model_joint.py:84."""
+        return self._rows("MS", 2 * self.cfg.latent, self._graph_latent)[:, :self.cfg.latent]
 
     @property
     def z_std_sg(self):
-        return self._rows("MS", 2 * self.cfg.latent)[:, self.cfg.latent:]
+        return self._rows("MS", 2 * self.cfg.latent, self._graph_latent)[:, self.cfg.latent:]
 
     @property
     def z_sg(self):
+        """z (model_joint.py:89)."""
+        if self._graph_latent:
+            return self._rows("ZL", self.cfg.latent, True)
         return self._rows("Z", self.cfg.latent)
+
+    @property
+    def joint_h(self):
+        """Decoder input J [B*N, node_h] (model_joint.py:97; == z for the node latent)."""
+        return self._rows("Z", self.cfg.node_h_size)
 
     @property
     def generated_spatial(self):

@@ -1,4 +1,4 @@
-"""Parameter layout of the SND-VAE hot path (node-latent topology).
+"""Parameter layout of the SND-VAE hot path (both decoder-input topologies).
 
 The reference keeps one TF variable per layer in the variable store, keyed by
 variable_scope (`layers.py:115-125`, `layers.py:566-576`, Keras BN and
@@ -14,6 +14,11 @@ Physical blocks fuse layers that read the same input:
   decoders' first conv1d both read J (`model_joint.py:112-115,129-138`).
 
 ``LOGICAL`` maps each reference variable name to (block, column slice).
+
+Graph-latent (tref) layouts differ in two places: ``enc.Wh`` is the
+[N*W, g_hidden] matrix of `model.py:113` (row index n*W + c, the row-major
+tf.reshape of G), and the decoder projection ``dec.Wp`` [L, N*node_h] /
+``dec.bp`` (`model_joint.py:97`, 'd_sg_lin1') follows the heads.
 """
 from __future__ import annotations
 
@@ -29,12 +34,14 @@ ALIGN = 64
 
 
 def block_shapes(cfg: SNDConfig) -> "OrderedDict[str, Tuple[int, ...]]":
-    if cfg.topology != "tscale":
-        raise NotImplementedError("GPU layout covers the node-latent topology")
+    if cfg.topology not in ("tscale", "tref"):
+        raise ValueError(f"unknown topology {cfg.topology!r}")
+    tref = cfg.topology == "tref"
     f, (h0, h1), gh, L, nh = (cfg.f_in, cfg.g_conv_hidden, cfg.g_hidden_size,
                               cfg.latent, cfg.node_h_size)
-    if nh != L:
+    if not tref and nh != L:
         raise ValueError("tscale requires node_h_size == latent (J = z)")
+    n = cfg.n_nodes
     s1, s2, s3 = cfg.s_d_channel
     n1, n2 = cfg.n_d_channel
     k = CONV_K
@@ -47,10 +54,13 @@ def block_shapes(cfg: SNDConfig) -> "OrderedDict[str, Tuple[int, ...]]":
     shapes["enc.bn1.beta"] = (h1,)
     shapes["enc.bne.gamma"] = (h1 + f,)
     shapes["enc.bne.beta"] = (h1 + f,)
-    shapes["enc.Wh"] = (h1 + f, gh)
+    shapes["enc.Wh"] = ((n * (h1 + f)) if tref else (h1 + f), gh)
     shapes["enc.bh"] = (gh,)
     shapes["enc.Wms"] = (gh, 2 * L)
     shapes["enc.bms"] = (2 * L,)
+    if tref:
+        shapes["dec.Wp"] = (L, n * nh)
+        shapes["dec.bp"] = (n * nh,)
     shapes["dec.K1"] = (k, nh, s1 + n1)
     shapes["dec.b1"] = (s1 + n1,)
     shapes["dec.bn1.gamma"] = (s1 + n1,)
@@ -95,6 +105,8 @@ def logical_names(cfg: SNDConfig) -> Dict[str, Tuple[str, slice]]:
         "encoder/g_g2_lin/bias": ("enc.bms", slice(0, L)),
         "encoder/g_g3_lin/Matrix": ("enc.Wms", slice(L, 2 * L)),
         "encoder/g_g3_lin/bias": ("enc.bms", slice(L, 2 * L)),
+        "decoder/d_sg_lin1/Matrix": ("dec.Wp", full),
+        "decoder/d_sg_lin1/bias": ("dec.bp", full),
         "decoder/s1_deconv/kernel": ("dec.K1", slice(0, s1)),
         "decoder/s1_deconv/bias": ("dec.b1", slice(0, s1)),
         "decoder/d_bn_s0/gamma": ("dec.bn1.gamma", slice(0, s1)),
@@ -120,6 +132,8 @@ def logical_names(cfg: SNDConfig) -> Dict[str, Tuple[str, slice]]:
         "decoder/d_n_lin2/Matrix": ("dec.Wn", full),
         "decoder/d_n_lin2/bias": ("dec.bn", full),
     }
+    if cfg.topology != "tref":
+        del m["decoder/d_sg_lin1/Matrix"], m["decoder/d_sg_lin1/bias"]
     return m
 
 
@@ -182,7 +196,7 @@ def init_blocks(cfg: SNDConfig, seed: int = 0) -> Dict[str, np.ndarray]:
     for k, s in shapes.items():
         if k in ("enc.W0", "enc.W1"):
             v = _truncated_normal(rng, s, 0.02)           # GraphConvolution w
-        elif k in ("enc.Wh", "dec.Ws", "dec.Wn"):
+        elif k in ("enc.Wh", "dec.Ws", "dec.Wn", "dec.Wp"):
             v = rng.normal(0.0, 0.02, s)                  # linear Matrix
         elif k == "enc.Wms":
             v = np.concatenate([rng.normal(0.0, 0.02, (s[0], L)),

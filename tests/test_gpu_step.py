@@ -10,9 +10,10 @@ import numpy as np
 import pytest
 import torch
 
+import golden_io
 from oracle import ref_numpy as R
-from snd_vae_amd.config import tscale
-from snd_vae_amd.data import GraphBatch, synthetic_batch
+from snd_vae_amd.config import tref, tscale
+from snd_vae_amd.data import synthetic_batch
 
 pytestmark = pytest.mark.gpu
 GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
@@ -25,14 +26,7 @@ def _gpu(lib_built):
         pytest.fail("GPU tests need a ROCm device")
 
 
-def load_fixture(name):
-    z = np.load(os.path.join(GOLDEN, name + ".npz"))
-    n, d, B = int(z["n"]), int(z["d"]), int(z["B"])
-    cfg = tscale(n, d, mean_degree=float(z["kbar"]))
-    batch = GraphBatch(B, n, z["rowptr"], z["colidx"], z["features"], z["feature_truth"],
-                       z["spatial_truth"])
-    p0 = {k[3:]: z[k] for k in z.files if k.startswith("p0/")}
-    return z, cfg, batch, p0
+load_fixture = golden_io.load
 
 
 def make(cfg, batch, p0, dtype):
@@ -46,7 +40,7 @@ def block_err(g, ref):
     return np.abs(g - ref).max() / max(np.abs(ref).max(), 1e-30)
 
 
-@pytest.mark.parametrize("name", ["tscale_n25_d16", "tscale_n200_d16"])
+@pytest.mark.parametrize("name", golden_io.NAMES)
 def test_train_steps_f32_vs_golden(name):
     z, cfg, batch, p0 = load_fixture(name)
     model, opt, db = make(cfg, batch, p0, "f32")
@@ -59,15 +53,16 @@ def test_train_steps_f32_vs_golden(name):
             assert got[k] == pytest.approx(ref, rel=1e-5, abs=1e-7), (t, k, got[k], ref)
         grads = opt.grad_blocks()
         for k, g in grads.items():
-            assert block_err(g, z[f"s{t}/grad/{k}"]) < 2e-4, (t, k, block_err(g, z[f"s{t}/grad/{k}"]))
+            err, nerr = golden_io.block_error(z, f"s{t}/grad", k, g)
+            assert err < 2e-4 and (nerr is None or nerr < 1e-4), (t, k, err, nerr)
     final = model.blocks()
     for k, v in final.items():
         # Adam normalises each update to ~lr: compare against the step size
-        assert np.abs(v - z["p_final/" + k]).max() < 0.05 * 3 * cfg.learning_rate, k
+        assert golden_io.max_abs_diff(z, "p_final", k, v) < 0.05 * 3 * cfg.learning_rate, k
     assert opt.global_step == 3
 
 
-@pytest.mark.parametrize("name", ["tscale_n200_d16"])
+@pytest.mark.parametrize("name", ["tscale_n200_d16", "tref_c1_n200_d16"])
 def test_train_step_bf16_vs_golden(name):
     z, cfg, batch, p0 = load_fixture(name)
     model, opt, db = make(cfg, batch, p0, "bf16")
@@ -80,6 +75,10 @@ def test_train_step_bf16_vs_golden(name):
     # The decoder-conv gradients sit at 3-5 % on both the fast and the generic
     # bf16 engines (tools/bf16_errors.py); encoder blocks at ~0.3 %.
     for k, g in grads.items():
+        if f"s0/grad/{k}" not in z.files:     # sampled big block: sampled max-abs check
+            err, nerr = golden_io.block_error(z, "s0/grad", k, g)
+            assert err < 5e-2 and nerr < 2e-2, (k, err, nerr)
+            continue
         ref = z[f"s0/grad/{k}"]
         err = np.linalg.norm(g - ref) / max(np.linalg.norm(ref), 1e-30)
         assert err < (1e-1 if k.startswith("dec.") else 2e-2), (k, err)
@@ -105,6 +104,34 @@ def test_train_step_c2_size_vs_oracle(dtype, ltol, gtol):
     g = opt.grad_blocks()
     bad = {k: block_err(g[k], rg[k]) for k in rg if block_err(g[k], rg[k]) > gtol}
     assert not bad, bad
+
+
+@pytest.mark.parametrize("dtype,ltol,gtol", [("f32", 1e-5, 2e-4), ("bf16", 2e-2, 1e-1)])
+def test_train_step_c4_size_vs_oracle(dtype, ltol, gtol):
+    """C4: graph latent + model_joint decoders at N=4096 d=64 (B=2), one step vs the oracle.
+
+    Exercises the 27 M-row-element head stream (flat(G) [2, 274432]) and the
+    26 M-element d_sg_lin1 projection at the BASELINE size."""
+    cfg = tref(4096, 64)
+    batch = synthetic_batch(cfg, 2, seed=0)
+    from snd_vae_amd.params import init_blocks
+    p0 = {k: v.astype(np.float32).astype(np.float64) for k, v in init_blocks(cfg, 0).items()}
+    eps = np.random.default_rng(9).standard_normal((2, cfg.latent)).astype(np.float32)
+    model, opt, db = make(cfg, batch, p0, dtype)
+    opt.step(db, torch.from_numpy(eps).cuda())
+    got = opt.loss_dict()
+    adj = [batch.dense_adj(b) for b in range(2)]
+    ref, rg, _ = R.forward_backward(p0, adj, batch.features, batch.feature_truth,
+                                    batch.spatial_truth, eps.astype(np.float64), cfg)
+    for k in ("cost", "spatial_cost", "adj_cost", "node_cost", "kl"):
+        assert got[k] == pytest.approx(ref[k], rel=ltol), (k, got[k], ref[k])
+    assert abs(got["acc"] - ref["acc"]) < (1e-6 if dtype == "f32" else 1e-3)
+    g = opt.grad_blocks()
+    bad = {k: block_err(g[k], rg[k]) for k in rg if block_err(g[k], rg[k]) > gtol}
+    assert not bad, bad
+    # decoder input J and the graph latent read back under the reference names
+    assert model.joint_h.shape == (2 * 4096, 64) and model.z_sg.shape == (2, cfg.latent)
+    assert model.z_mean_sg.shape == (2, cfg.latent)
 
 
 def test_graph_replay_is_deterministic():

@@ -12,9 +12,10 @@ import numpy as np
 import pytest
 import torch
 
+import golden_io
 from oracle import ref_numpy as R
 from oracle import ref_torch as T
-from snd_vae_amd.config import tscale
+from snd_vae_amd.config import tref, tscale
 from snd_vae_amd.data import synthetic_batch
 from snd_vae_amd.params import init_blocks
 
@@ -49,18 +50,22 @@ def test_conv1d_same_matches_torch():
     assert np.allclose(out, ref, atol=1e-12)
 
 
-def _small(n=25, d=8, B=2, seed=3):
-    cfg = tscale(n, d, mean_degree=6.0)
+def _small(n=25, d=8, B=2, seed=3, topology="tscale"):
+    if topology == "tref":
+        cfg = tref(n, d, g_hidden=12, latent=10, mean_degree=6.0)
+    else:
+        cfg = tscale(n, d, mean_degree=6.0)
     batch = synthetic_batch(cfg, B, seed=seed)
     rng = np.random.default_rng(seed)
     p = {k: v + 0.3 * rng.standard_normal(v.shape) for k, v in init_blocks(cfg, 1).items()}
-    eps = rng.standard_normal((B * n, d))
+    eps = rng.standard_normal((B, cfg.latent) if topology == "tref" else (B * n, d))
     adj = [batch.dense_adj(i) for i in range(B)]
     return cfg, batch, p, eps, adj
 
 
-def test_oracle_grads_match_torch_autograd():
-    cfg, batch, p, eps, adj = _small()
+@pytest.mark.parametrize("topology", ["tscale", "tref"])
+def test_oracle_grads_match_torch_autograd(topology):
+    cfg, batch, p, eps, adj = _small(topology=topology)
     losses, g, _ = R.forward_backward(p, adj, batch.features, batch.feature_truth,
                                       batch.spatial_truth, eps, cfg)
     tp = T.build_params(p, torch.float64)
@@ -75,14 +80,19 @@ def test_oracle_grads_match_torch_autograd():
         assert err < 1e-10, (k, err)
 
 
-def test_oracle_finite_differences():
-    cfg, batch, p, eps, adj = _small(n=12, d=4, B=1, seed=7)
+@pytest.mark.parametrize("topology", ["tscale", "tref"])
+def test_oracle_finite_differences(topology):
+    cfg, batch, p, eps, adj = _small(n=12, d=4, B=2 if topology == "tref" else 1, seed=7,
+                                     topology=topology)
     args = (adj, batch.features, batch.feature_truth, batch.spatial_truth, eps, cfg)
     _, g, _ = R.forward_backward(p, *args)
     rng = np.random.default_rng(0)
     h = 1e-6
-    for k in ("enc.W0", "enc.W1", "enc.bne.gamma", "enc.Wms", "dec.K1", "dec.K3s", "dec.bn1.beta",
-              "dec.Wn"):
+    keys = ["enc.W0", "enc.W1", "enc.bne.gamma", "enc.Wms", "dec.K1", "dec.K3s", "dec.bn1.beta",
+            "dec.Wn"]
+    if topology == "tref":
+        keys += ["enc.Wh", "enc.bh", "dec.Wp", "dec.bp"]
+    for k in keys:
         idx = tuple(rng.integers(0, s) for s in p[k].shape)
         pp = {a: b.copy() for a, b in p.items()}
         pm = {a: b.copy() for a, b in p.items()}
@@ -105,17 +115,24 @@ def test_tf1_adam_formula():
     assert np.allclose(p["w"], exp, rtol=0, atol=1e-15)
 
 
-@pytest.mark.parametrize("name", ["tscale_n25_d16", "tscale_n200_d16"])
+@pytest.mark.parametrize("name", golden_io.NAMES)
 def test_golden_fixture_reproduces(name):
-    z = np.load(os.path.join(GOLDEN, name + ".npz"))
-    n, d, B = int(z["n"]), int(z["d"]), int(z["B"])
-    cfg = tscale(n, d, mean_degree=float(z["kbar"]))
+    z, cfg, fixture_batch, p0 = golden_io.load(name)
+    B = fixture_batch.n_graphs
     batch = synthetic_batch(cfg, B, seed=int(z["seed"]))
     assert np.array_equal(batch.rowptr, z["rowptr"]) and np.array_equal(batch.colidx, z["colidx"])
-    p0 = {k[3:]: z[k] for k in z.files if k.startswith("p0/")}
+    assert np.array_equal(batch.features, z["features"])
     adj = [batch.dense_adj(b) for b in range(B)]
     losses, g, _ = R.forward_backward(p0, adj, z["features"], z["feature_truth"],
                                       z["spatial_truth"], z["eps"][0].astype(np.float64), cfg)
     assert losses["cost"] == pytest.approx(float(z["s0/loss/cost"]), rel=1e-13)
     for k in p0:
-        assert np.allclose(g[k], z["s0/grad/" + k], rtol=1e-10, atol=1e-14)
+        err, nerr = golden_io.block_error(z, "s0/grad", k, g[k])
+        assert err < 1e-10 and (nerr is None or nerr < 1e-12), (k, err, nerr)
+
+
+def test_c1_fixture_is_the_reference_topology():
+    """BASELINE configs[0]: graph latent, F_in = num_feature (model.py:104), L = 100."""
+    z, cfg, batch, p0 = golden_io.load("tref_c1_n200_d16")
+    assert cfg.topology == "tref" and cfg.f_in == 1 and cfg.latent == 100
+    assert p0["enc.Wh"].shape == (200 * 17, 100) and p0["dec.Wp"].shape == (100, 200 * 16)
