@@ -68,6 +68,15 @@ int snd_csr_spmm(const int* rowptr, const int* colidx, int n_rows,
                  const float* bn2_gamma, const float* bn2_beta, float* out2,
                  int ldo2, snd_stream_t stream);
 
+/* a2 in the bf16 throughput mode (the SpMM of the fast path, layers.py:122 and
+ * its backward): out = A @ h over bf16 rows with fp32 accumulation, rounded to
+ * bf16.  width % 8 == 0 and <= 128; ldh, ldo % 8 == 0 (16-byte rows).  When
+ * n_per_graph % 32 == 0 and n_graphs % 8 == 0 the row blocks are ordered so one
+ * graph's rows stay on one XCD (its gathered rows then hit that XCD's L2);
+ * otherwise natural order.  h and out are bf16 device buffers. */
+int snd_csr_spmm_bf16(const int* rowptr, const int* colidx, int n_rows,
+                      const void* h, int ldh, int width, void* out, int ldo,
+                      int n_per_graph, int n_graphs, snd_stream_t stream);
 /* ---- a5: linear / dense GEMM on MFMA ---------------------------------------
  * Replaces linear() (layers.py:566-576) and the X@w of GraphConvolution
  * (layers.py:120-121; the tile() copy is not needed):

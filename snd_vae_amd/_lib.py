@@ -48,6 +48,7 @@ _SIGS = {
     "snd_dense_to_csr": (c_int, [vp, c_int, c_int, vp, vp, c_ll, vp, vp, c_size, vp]),
     "snd_csr_spmm": (c_int, [vp, vp, c_int, vp, c_int, c_int, vp, c_int, c_int, vp, vp, vp,
                              c_int, vp, c_int, c_int, vp, vp, vp, c_int, vp]),
+    "snd_csr_spmm_bf16": (c_int, [vp, vp, c_int, vp, c_int, c_int, vp, c_int, c_int, c_int, vp]),
     "snd_gemm": (c_int, [c_int, c_int, c_int, c_int, c_int, vp, c_int, vp, c_int, vp, c_int,
                          vp, c_int, vp]),
     "snd_conv1d_same_fwd": (c_int, [vp, c_int, c_int, c_int, c_int, vp, c_int, vp, vp, vp,

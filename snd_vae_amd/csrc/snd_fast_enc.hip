@@ -486,3 +486,17 @@ int launch_reparam_bwd_fast(const ReparamBwdFastArgs& a, hipStream_t s) {
 }
 
 }  // namespace snd
+
+using namespace snd;
+
+extern "C" int snd_csr_spmm_bf16(const int* rowptr, const int* colidx, int n_rows, const void* h,
+                                 int ldh, int width, void* out, int ldo, int n_per_graph,
+                                 int n_graphs, snd_stream_t stream) {
+  SND_CHECK_ARG(rowptr && (colidx || n_rows == 0) && h && out && n_rows >= 0,
+                "snd_csr_spmm_bf16: null operand");
+  SpmmBfArgs a{rowptr, colidx, n_rows, reinterpret_cast<const __bf16*>(h), ldh, width,
+               SND_SPMM_PLAIN, reinterpret_cast<__bf16*>(out), ldo};
+  a.xcd_nbg = (n_per_graph > 0 && n_graphs > 0 && (long long)n_per_graph * n_graphs == n_rows)
+                  ? xcd_nbg(n_per_graph, n_graphs) : 0;
+  return launch_spmm_bf16(a, (hipStream_t)stream);
+}

@@ -200,6 +200,7 @@ extern "C" int snd_plan_create(const snd_config_t* cfg, int n_graphs, snd_plan_t
   p->add_buf("EPS", RH * L);  p->add_buf("Z", R * dj);
   p->add_buf("ZSTAGE", (long long)zzt_staging_bytes(p->B, p->N, dj, c.dtype), 1);
   p->add_buf("DJD", R * dj);  p->add_buf("EJ", R * dj);
+  p->add_buf("DJDX", std::max(1LL, (zzt_tsplit(p->B, p->N, c.dtype) - 1) * R * dj));
   p->add_buf("Y1", R * C1);   p->add_buf("U1", R * C1);
   p->add_buf("Y2S", R * c.s2); p->add_buf("U2S", R * c.s2);
   p->add_buf("Y2N", R * c.n2); p->add_buf("U2N", R * c.n2);
@@ -212,7 +213,7 @@ extern "C" int snd_plan_create(const snd_config_t* cfg, int n_graphs, snd_plan_t
   p->add_buf("DMS", RH * 2 * L); p->add_buf("DH", RH * gh); p->add_buf("DG", R * W);
   p->add_buf("DP1", R * h1);  p->add_buf("DXW1", R * h1); p->add_buf("DH1", R * h0);
   p->add_buf("DP0", R * h0);  p->add_buf("DXW0", R * h0);
-  const int nz = zzt_dense_blocks(p->B, p->N), ne = edge_blocks(p->R, dj);
+  const int nz = zzt_dense_blocks(p->B, p->N, c.dtype), ne = edge_blocks(p->R, dj);
   const int nk = reparam_blocks(p->RH, L), nh = head_blocks(p->R), nc = col_blocks(p->R);
   p->add_buf("PZZT", 2LL * nz, 8); p->add_buf("PEDGE", 2LL * std::max(ne, edge_bf16_blocks(p->R)), 8); p->add_buf("PKL", std::max(nk, reparam_prep_blocks(p->B, zzt_npad(p->N))), 8);
   p->add_buf("PSSES", nh, 8); p->add_buf("PSSEN", nh, 8);
@@ -793,7 +794,7 @@ extern "C" int snd_plan_launch(const snd_plan_t* plan, const snd_batch_t* batch,
     const ZztStage stg = zzt_stage(ws + p.buf("ZSTAGE"), p.B, p.N, L, p.c.dtype);
     const int variant = kernel[9] == '_' ? kernel[11] - '0' : 0;
     ZztArgs za{stg.jrow, stg.jt, p.N, zzt_npad(p.N), p.B, L, (float*)(ws + p.buf("DJD")),
-               (double*)(ws + p.buf("PZZT")), stg.colpart, variant};
+               (double*)(ws + p.buf("PZZT")), stg.colpart, variant, (float*)(ws + p.buf("DJDX"))};
     return launch_zzt_dense(za, p.c.dtype, s);
   }
   if (!strcmp(kernel, "spmm_dxw1")) {   // A @ dP1 (plain SpMM, width h1)
@@ -958,7 +959,8 @@ extern "C" int snd_train_step(const snd_plan_t* plan, const snd_batch_t* batch,
     edge_mark = mark(x);
     if (edge_mark < -1) return SND_ERR_HIP;
     if (!p.fast) SND_TRY(launch_zzt_prep(x.f("Z"), p.B, N, dj, c.dtype, stg, x.s));
-    ZztArgs za{stg.jrow, stg.jt, N, zzt_npad(N), p.B, dj, x.f("DJD"), x.d("PZZT"), stg.colpart, 0};
+    ZztArgs za{stg.jrow, stg.jt, N, zzt_npad(N), p.B, dj, x.f("DJD"), x.d("PZZT"), stg.colpart, 0,
+               x.f("DJDX")};
     SND_TRY(launch_zzt_dense(za, c.dtype, x.s));
   }
   if (p.fast) {
@@ -1130,7 +1132,7 @@ extern "C" int snd_train_step(const snd_plan_t* plan, const snd_batch_t* batch,
   SND_TRY(launch_reduce(rd.data(), (int)rd.size(), x.s));
 
   const int n_kl = (p.fast && !p.tref) ? reparam_prep_blocks(p.B, zzt_npad(N)) : reparam_blocks(RH, L);
-  FinalizeArgs fa{x.d("PZZT"), zzt_dense_blocks(p.B, N), x.d("PEDGE"),
+  FinalizeArgs fa{x.d("PZZT"), zzt_dense_blocks(p.B, N, c.dtype), x.d("PEDGE"),
                   p.fast ? edge_bf16_blocks(R) : edge_blocks(R, dj),
                   x.d("PKL"), n_kl, x.d("PSSES"), x.d("PSSEN"), nh,
                   rp, p.B, N, L, sd, nf, c.beta, c.norm, losses, grads + p.pcount, step_counter,

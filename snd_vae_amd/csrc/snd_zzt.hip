@@ -32,6 +32,8 @@
 #include "snd_zzt.hpp"
 #include "snd_spmm.hpp"
 
+#include <algorithm>
+
 namespace snd {
 namespace {
 
@@ -511,7 +513,11 @@ __global__ void __launch_bounds__(NTH2) zzt_dense_bf16_v3(ZztArgs a) {
   __shared__ float colsum[DP];
   __shared__ float csred[NTH2 / DP][DP];
 
-  const int g = blockIdx.x % a.ngraphs, rb = blockIdx.x / a.ngraphs;
+  // block -> (column split sp, graph g, row block rb)
+  const int wgs = a.ngraphs * (a.npad / ROWS);
+  const int sp = blockIdx.x / wgs, bx = blockIdx.x - sp * wgs;
+  const int nsplit = gridDim.x / wgs;
+  const int g = bx % a.ngraphs, rb = bx / a.ngraphs;
   const __bf16* Jg = reinterpret_cast<const __bf16*>(a.jrow) + (long long)g * a.npad * DP;
   const __bf16* JTg = reinterpret_cast<const __bf16*>(a.jt) + (long long)g * DP * a.npad;
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, r = lane & 15, q4 = lane >> 4;
@@ -613,16 +619,17 @@ __global__ void __launch_bounds__(NTH2) zzt_dense_bf16_v3(ZztArgs a) {
     }
   };
 
-  const int ntiles = a.npad / TJ2;
-  gload(0);
+  const int ntot = a.npad / TJ2;
+  const int t0 = sp * ntot / nsplit, ntiles = (sp + 1) * ntot / nsplit;
+  gload(t0);
   sstore(0);
   __syncthreads();
   float labs = 0.f, llog = 0.f;
   double ltot = 0.0;
   unsigned wcnt = 0;
   const int qa = 2 * half, qb = 2 * half + 1;
-  for (int t = 0; t < ntiles; ++t) {
-    const int cur = t & 1;
+  for (int t = t0; t < ntiles; ++t) {
+    const int cur = (t - t0) & 1;
     if (t + 1 < ntiles) gload(t + 1);
     const __bf16* Ls = lds[cur];
     f32x4 Xa0, Xa1, Xb0, Xb1;
@@ -635,7 +642,7 @@ __global__ void __launch_bounds__(NTH2) zzt_dense_bf16_v3(ZztArgs a) {
     pv(Ls, qb, sbv);
     if (t + 1 < ntiles) sstore(cur ^ 1);
     __syncthreads();
-    if ((t & 7) == 7) {             // keep the fp32 partial sums short
+    if (((t - t0) & 7) == 7) {      // keep the fp32 partial sums short
       ltot += (double)(0.5f * labs + llog);
       labs = 0.f;
       llog = 0.f;
@@ -658,14 +665,15 @@ __global__ void __launch_bounds__(NTH2) zzt_dense_bf16_v3(ZztArgs a) {
   xs += __shfl_xor(xs, 16, 64);
   xs += __shfl_xor(xs, 32, 64);
   const bool row_valid = i_me < a.n;
+  const bool corr = sp == 0;           // analytic corrections: once per row, in split 0
   const float exd = __builtin_amdgcn_exp2f(-fabsf(xd));
   const float sgd = xd > 0.f ? 1.f / (1.f + exd) : exd / (1.f + exd);
-  if (half == 0 && q4 == 0 && row_valid) {
+  if (half == 0 && q4 == 0 && row_valid && corr) {
     // + sum_j x_ij / 2 (the other half of max(x,0)); - softplus2(x_ii)
     ltot += 0.5 * (double)xs;
     ltot -= (double)(fmaxf(xd, 0.f) + __builtin_amdgcn_logf(1.f + exd));
   }
-  const unsigned dpos = (unsigned)__popcll(__ballot(half == 0 && q4 == 0 && row_valid && xd > 0.f));
+  const unsigned dpos = (unsigned)__popcll(__ballot(half == 0 && q4 == 0 && row_valid && corr && xd > 0.f));
 
   // ---- combine the two column halves' partial dJ, subtract the diagonal term
   float* red = reinterpret_cast<float*>(&lds[0][0]);
@@ -677,8 +685,9 @@ __global__ void __launch_bounds__(NTH2) zzt_dense_bf16_v3(ZztArgs a) {
   }
   __syncthreads();
   if (half == 0 && row_valid) {
-    const float sgb = (float)(__bf16)sgd;            // sigma as the PV-MFMA consumed it
-    float* dst = a.dJd + ((long long)g * a.n + i_me) * a.d;
+    const float sgb = corr ? (float)(__bf16)sgd : 0.f;   // sigma as the PV-MFMA consumed it
+    float* dst = (sp == 0 ? a.dJd : a.dJd_extra + (long long)(sp - 1) * a.ngraphs * a.n * a.d) +
+                 ((long long)g * a.n + i_me) * a.d;
 #pragma unroll
     for (int ct = 0; ct < CT; ++ct) {
       const f32x4 o = *reinterpret_cast<const f32x4*>(&red[slot + 4 * ct]);
@@ -700,7 +709,7 @@ __global__ void __launch_bounds__(NTH2) zzt_dense_bf16_v3(ZztArgs a) {
   if (tid == 0) {
     double tl = 0.0, tc = 0.0;
     for (int k = 0; k < NTH2 / 64; ++k) { tl += sl[k]; tc += (double)sc[k]; }
-    if (rb == 0)   // padded pairs of this graph: x = 0 exactly, log2(1 + 1) = 1 each
+    if (rb == 0 && corr)   // padded pairs of this graph: x = 0 exactly, log2(1 + 1) = 1 each
       tl -= (double)a.npad * a.npad - (double)a.n * a.n;
     a.part[2 * blockIdx.x] = tl * (double)kLn2;
     a.part[2 * blockIdx.x + 1] = tc;
@@ -838,6 +847,16 @@ __global__ void __launch_bounds__(NTH) zzt_dense_f32(ZztArgs a) {
   block_reduce_write(st, a.part);
 }
 
+// dJd += sum of the column-split partials (fixed order)
+__global__ void zzt_split_sum_kernel(float* dJd, const float* extra, long long n, int nextra) {
+  long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  for (; i < n; i += (long long)gridDim.x * blockDim.x) {
+    float v = dJd[i];
+    for (int s = 0; s < nextra; ++s) v += extra[(long long)s * n + i];
+    dJd[i] = v;
+  }
+}
+
 // dz = scale * (dz + ej)
 __global__ void zzt_combine_kernel(float* dz, const float* ej, long long n, float norm) {
   long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -866,7 +885,14 @@ int zzt_dp(int d) {
   return -1;
 }
 int zzt_npad(int n) { return (int)round_up(n, ROWS); }
-int zzt_dense_blocks(int ngraphs, int n) { return ngraphs * (zzt_npad(n) / ROWS); }
+int zzt_tsplit(int ngraphs, int n, int dtype) {
+  const int wgs = ngraphs * (zzt_npad(n) / ROWS), ntiles = zzt_npad(n) / TJ2;
+  if (dtype != SND_BF16 || wgs >= 256) return 1;
+  return std::max(1, std::min({cdiv(256, wgs), 4, ntiles}));
+}
+int zzt_dense_blocks(int ngraphs, int n, int dtype) {
+  return ngraphs * (zzt_npad(n) / ROWS) * zzt_tsplit(ngraphs, n, dtype);
+}
 
 size_t zzt_staging_bytes(int ngraphs, int n, int d, int dtype) {
   const int dp = zzt_dp(d);
@@ -904,7 +930,9 @@ int launch_zzt_prep(const float* z, int ngraphs, int n, int d, int dtype, const 
 
 int launch_zzt_dense(const ZztArgs& a, int dtype, hipStream_t s) {
   const int dp = zzt_dp(a.d);
-  dim3 grid(zzt_dense_blocks(a.ngraphs, a.n));
+  const int ts = (dtype == SND_BF16 && a.variant == 0) ? zzt_tsplit(a.ngraphs, a.n, dtype) : 1;
+  SND_CHECK_ARG(ts == 1 || a.dJd_extra, "zzt_dense: column splits need dJd_extra");
+  dim3 grid(a.ngraphs * (a.npad / ROWS) * ts);
   if (dtype == SND_BF16 && a.variant == 1) {          // v1: 8 waves x 16 rows, TJ 64
     if (dp == 32) hipLaunchKernelGGL((zzt_dense_bf16<32>), grid, dim3(NTH), 0, s, a);
     else if (dp == 64) hipLaunchKernelGGL((zzt_dense_bf16<64>), grid, dim3(NTH), 0, s, a);
@@ -924,6 +952,12 @@ int launch_zzt_dense(const ZztArgs& a, int dtype, hipStream_t s) {
     else hipLaunchKernelGGL((zzt_dense_f32<128>), grid, dim3(NTH), shm, s, a);
   }
   SND_LAUNCH_CHECK("zzt_dense");
+  if (ts > 1) {
+    const long long cnt = (long long)a.ngraphs * a.n * a.d;
+    hipLaunchKernelGGL(zzt_split_sum_kernel, dim3((unsigned)std::min<long long>(cdiv(cnt, 256), 4096)),
+                       dim3(256), 0, s, a.dJd, a.dJd_extra, cnt, ts - 1);
+    SND_LAUNCH_CHECK("zzt_split_sum_kernel");
+  }
   return 0;
 }
 
@@ -956,8 +990,9 @@ extern "C" size_t snd_zzt_ce_workspace(int n_graphs, int n, int d, int dtype) {
   const long long rows = (long long)n_graphs * n;
   size_t b = round_up(zzt_staging_bytes(n_graphs, n, d, dtype), 256);
   b += round_up(rows * d * sizeof(float), 256);                               // ej
-  b += round_up(2 * sizeof(double) * (size_t)zzt_dense_blocks(n_graphs, n), 256);
+  b += round_up(2 * sizeof(double) * (size_t)zzt_dense_blocks(n_graphs, n, dtype), 256);
   b += round_up(2 * sizeof(double) * (size_t)edge_blocks((int)rows, d), 256);
+  b += round_up((size_t)(zzt_tsplit(n_graphs, n, dtype) - 1) * rows * d * sizeof(float), 256);
   return b;
 }
 
@@ -981,11 +1016,13 @@ extern "C" int snd_zzt_ce(const float* z, int n_graphs, int n, int d, const int*
   float* ej = (float*)p;
   p += round_up(rows * d * sizeof(float), 256);
   double* pd = (double*)p;
-  p += round_up(2 * sizeof(double) * (size_t)zzt_dense_blocks(n_graphs, n), 256);
+  p += round_up(2 * sizeof(double) * (size_t)zzt_dense_blocks(n_graphs, n, dtype), 256);
   double* pe = (double*)p;
+  p += round_up(2 * sizeof(double) * (size_t)edge_blocks((int)rows, d), 256);
+  float* extra = (float*)p;
 
   SND_TRY(launch_zzt_prep(z, n_graphs, n, d, dtype, stg, s));
-  ZztArgs a{stg.jrow, stg.jt, n, zzt_npad(n), n_graphs, d, dz, pd, stg.colpart, 0};
+  ZztArgs a{stg.jrow, stg.jt, n, zzt_npad(n), n_graphs, d, dz, pd, stg.colpart, 0, extra};
   SND_TRY(launch_zzt_dense(a, dtype, s));
   EdgeArgs e{rowptr, colidx, (int)rows, z, d, pos_weight, ej, pe};
   SND_TRY(launch_edge(e, s));
@@ -993,7 +1030,7 @@ extern "C" int snd_zzt_ce(const float* z, int n_graphs, int n, int d, const int*
   hipLaunchKernelGGL(zzt_combine_kernel, dim3(1024), dim3(256), 0, s, dz, ej, rows * d, 2.f * norm);
   SND_LAUNCH_CHECK("zzt_combine_kernel");
   hipLaunchKernelGGL(zzt_stats_kernel, dim3(1), dim3(64), 0, s, pd,
-                     zzt_dense_blocks(n_graphs, n), pe, edge_blocks((int)rows, d), rowptr,
+                     zzt_dense_blocks(n_graphs, n, dtype), pe, edge_blocks((int)rows, d), rowptr,
                      n_graphs, n, norm, stats);
   SND_LAUNCH_CHECK("zzt_stats_kernel");
   return 0;

@@ -11,6 +11,7 @@ struct ZztArgs {
   double* part;          // [blocks][2] = {sum softplus over valid pairs, #{L > 0}}
   const float* colpart;  // [B][npad/64][DP] column sums of jrow (bf16 values), per 64 rows
   int variant;           // bf16 kernel: 0 = default (v3), 1 = v1, 2 = v2 (A/B measurement)
+  float* dJd_extra;      // v3 column splits 1.. (zzt_tsplit > 1): [(tsplit-1)][B*n][d] scratch
 };
 
 // Staging buffers carved from one workspace region.
@@ -22,7 +23,11 @@ struct ZztStage {
 
 int zzt_dp(int d);
 int zzt_npad(int n);
-int zzt_dense_blocks(int ngraphs, int n);
+// Small batches (fewer row blocks than CUs) split the column range of every row
+// block over zzt_tsplit() workgroups (bf16 only); their partial dJ rows are summed
+// in fixed order by launch_zzt_dense.  Loss partials: zzt_dense_blocks() entries.
+int zzt_tsplit(int ngraphs, int n, int dtype);
+int zzt_dense_blocks(int ngraphs, int n, int dtype);
 size_t zzt_staging_bytes(int ngraphs, int n, int d, int dtype);
 ZztStage zzt_stage(void* base, int ngraphs, int n, int d, int dtype);
 int zzt_init_attributes();

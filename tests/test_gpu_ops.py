@@ -61,6 +61,23 @@ def test_spmm_plain(width):
     assert rel(out, ref) < 1e-6
 
 
+@pytest.mark.parametrize("n,B,kbar,width", [(256, 8, 12.0, 64), (300, 3, 10.0, 128),
+                                             (96, 2, 2.0, 48), (64, 8, 0.0, 64)])
+def test_spmm_bf16(n, B, kbar, width):
+    """bf16 rows, fp32 accumulation, bf16 out; XCD row-block order when n % 32 == 0 and
+    B % 8 == 0.  Isolated nodes (kbar 2, 0) give all-zero rows."""
+    from snd_vae_amd import layers
+    rp, ci, dense = rand_batch(n, B, kbar, 5)
+    h = torch.from_numpy(np.random.default_rng(1).standard_normal((n * B, width)).astype(np.float32))
+    hb = h.to(torch.bfloat16)
+    out = layers.spmm_bf16(cu(rp, torch.int32), cu(ci if len(ci) else np.zeros(1, np.int32), torch.int32),
+                           hb.cuda(), n, B).float().cpu().numpy()
+    ref = R.spmm(dense, hb.float().numpy().astype(np.float64), n)
+    assert np.abs(out - ref).max() <= 2 ** -7 * max(np.abs(ref).max(), 1.0)
+    iso = np.diff(rp) == 0
+    assert np.all(out[iso] == 0.0)
+
+
 def test_graph_convolution_epilogue():
     from snd_vae_amd import layers
     n, B, f, w = 150, 2, 3, 64
