@@ -191,19 +191,23 @@ def spmm_batched(host, width, copies, reps):
     import torch
 
     from snd_vae_amd import _lib
+    from snd_vae_amd.data import locality_order
     rp0, ci0 = host.rowptr.astype(np.int64), host.colidx.astype(np.int64)
     nnz0, R0 = int(rp0[-1]), host.n_graphs * host.n_nodes
     rp = np.concatenate([rp0[:-1] + c * nnz0 for c in range(copies)] + [np.array([copies * nnz0])])
     ci = np.concatenate([ci0 + c * R0 for c in range(copies)])
+    o0 = locality_order(host).astype(np.int64)
+    order = np.concatenate([o0 + c * R0 for c in range(copies)])
     R = R0 * copies
     d_rp = torch.from_numpy(rp.astype(np.int32)).cuda()
     d_ci = torch.from_numpy(ci.astype(np.int32)).cuda()
+    d_order = torch.from_numpy(order.astype(np.int32)).cuda()
     h = torch.randn(R, width, device="cuda").to(torch.bfloat16)
     out = torch.empty_like(h)
     L = _lib.lib()
     ms = time_launches(lambda sp: _lib.check(L.snd_csr_spmm_bf16(
         d_rp.data_ptr(), d_ci.data_ptr(), R, h.data_ptr(), width, width, out.data_ptr(), width,
-        host.n_nodes, host.n_graphs * copies, sp)), reps)
+        host.n_nodes, host.n_graphs * copies, d_order.data_ptr(), sp)), reps)
     byts = 4 * (R + 1) + 4 * len(ci) + 2 * 2 * R * width
     gbs = byts / (ms * 1e-3) / 1e9
     return {"kernel": f"csr_spmm_bf16 (A @ H, width {width}, {host.n_graphs * copies} graphs "

@@ -73,10 +73,15 @@ int snd_csr_spmm(const int* rowptr, const int* colidx, int n_rows,
  * bf16.  width % 8 == 0 and <= 128; ldh, ldo % 8 == 0 (16-byte rows).  When
  * n_per_graph % 32 == 0 and n_graphs % 8 == 0 the row blocks are ordered so one
  * graph's rows stay on one XCD (its gathered rows then hit that XCD's L2);
- * otherwise natural order.  h and out are bf16 device buffers. */
+ * otherwise natural order.  row_order (optional, NULL = 0..n_rows-1) is the
+ * order rows are processed in, a permutation of 0..n_rows-1 that keeps each
+ * graph's rows inside its own slot range (snd_vae_amd/data.py locality_order:
+ * per-graph reverse Cuthill-McKee, so a workgroup's neighbour rows overlap in
+ * L1); the result does not depend on it.  h and out are bf16 device buffers. */
 int snd_csr_spmm_bf16(const int* rowptr, const int* colidx, int n_rows,
                       const void* h, int ldh, int width, void* out, int ldo,
-                      int n_per_graph, int n_graphs, snd_stream_t stream);
+                      int n_per_graph, int n_graphs, const int* row_order,
+                      snd_stream_t stream);
 /* ---- a5: linear / dense GEMM on MFMA ---------------------------------------
  * Replaces linear() (layers.py:566-576) and the X@w of GraphConvolution
  * (layers.py:120-121; the tile() copy is not needed):
@@ -206,6 +211,8 @@ typedef struct snd_batch {
   const float* features;       /* [B*N, f_in] */
   const float* feature_truth;  /* [B*N, num_feature] */
   const float* spatial_truth;  /* [B*N, spatial_dim] */
+  const int* row_order;        /* optional [B*N] locality schedule of the gather
+                                  kernels (see snd_csr_spmm_bf16); NULL = natural */
 } snd_batch_t;
 
 typedef struct snd_plan snd_plan_t;

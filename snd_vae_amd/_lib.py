@@ -17,7 +17,7 @@ c_int, c_ll, c_float, c_size, c_ull = C.c_int, C.c_longlong, C.c_float, C.c_size
 vp = C.c_void_p
 
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 TOPOLOGY = {"tscale": 0, "tref": 1}
 
 
@@ -37,7 +37,7 @@ class Config(C.Structure):
 class Batch(C.Structure):
     """snd_batch_t"""
     _fields_ = [("rowptr", vp), ("colidx", vp), ("features", vp),
-                ("feature_truth", vp), ("spatial_truth", vp)]
+                ("feature_truth", vp), ("spatial_truth", vp), ("row_order", vp)]
 
 
 # name -> (restype, argtypes)
@@ -48,7 +48,7 @@ _SIGS = {
     "snd_dense_to_csr": (c_int, [vp, c_int, c_int, vp, vp, c_ll, vp, vp, c_size, vp]),
     "snd_csr_spmm": (c_int, [vp, vp, c_int, vp, c_int, c_int, vp, c_int, c_int, vp, vp, vp,
                              c_int, vp, c_int, c_int, vp, vp, vp, c_int, vp]),
-    "snd_csr_spmm_bf16": (c_int, [vp, vp, c_int, vp, c_int, c_int, vp, c_int, c_int, c_int, vp]),
+    "snd_csr_spmm_bf16": (c_int, [vp, vp, c_int, vp, c_int, c_int, vp, c_int, c_int, c_int, vp, vp]),
     "snd_gemm": (c_int, [c_int, c_int, c_int, c_int, c_int, vp, c_int, vp, c_int, vp, c_int,
                          vp, c_int, vp]),
     "snd_conv1d_same_fwd": (c_int, [vp, c_int, c_int, c_int, c_int, vp, c_int, vp, vp, vp,

@@ -133,6 +133,7 @@ struct Gcn0Args {
   __bf16* h1; int ldh1;
   float* ax; __bf16* axb;
   int xcd_nbg;                // xcd_nbg(): row blocks per graph for the XCD-aware order
+  const int* row_order;       // optional processing order of the rows (locality schedule)
 };
 int xcd_nbg(int npg, int ngraphs);
 int gcn0_blocks(int R);
@@ -150,6 +151,7 @@ struct SpmmBfArgs {
   const float* ge; const float* be;
   __bf16* g; int ldg;
   int xcd_nbg;
+  const int* row_order;       // optional processing order of the rows (locality schedule)
 };
 int launch_spmm_bf16(const SpmmBfArgs& a, hipStream_t s);
 
@@ -182,6 +184,7 @@ struct EdgeBfArgs {
   float* ej;                  // [R][d]
   double* part;               // [blocks][2] = {loss, tp}
   int xcd_nbg;
+  const int* row_order;       // optional processing order of the rows (locality schedule)
 };
 int edge_bf16_blocks(int R);
 int launch_edge_bf16(const EdgeBfArgs& a, hipStream_t s);

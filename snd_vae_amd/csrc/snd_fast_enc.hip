@@ -36,6 +36,15 @@ __device__ __forceinline__ uint4 to_bf16x8(const float (&v)[8]) {
 
 
 
+// Row processed by this lane's 8-lane group: slot rb*RPB + threadIdx/LPR of the
+// optional locality order (a per-graph reverse Cuthill-McKee permutation made at
+// ingest: consecutive slots are graph neighbours, so a block's gathers share
+// rows in L1), else the slot itself.  Results do not depend on the order.
+__device__ __forceinline__ int row_of(const int* order, int rb, int R) {
+  const int slot = rb * RPB + threadIdx.x / LPR;
+  return (order && slot < R) ? order[slot] : slot;
+}
+
 // XCD-aware row-block order: blocks b and b + 8 share an XCD (and its L2), so
 // row blocks of graph g go to block group g % 8 -- a graph's gathered rows
 // (<= 1 MB) then stay in one L2.  nbg = row blocks per graph (0: identity).
@@ -46,24 +55,61 @@ __device__ __forceinline__ int xcd_rowblock(int b, int nbg) {
   return (x + 8 * gi) * nbg + lb;
 }
 
-// Neighbour lists of the block's RPB consecutive rows staged in LDS (one
-// coalesced pass; falls back to global reads past kNbrCap entries).
-constexpr int kNbrCap = 2048;
-struct NbrLds {
-  int base, cnt;
-  __device__ __forceinline__ int at(const int* lds, const int* colidx, int k) const {
-    return cnt <= kNbrCap ? lds[k - base] : colidx[k];
+// Lane u of each aligned 8-lane group to all 8 lanes (ds_swizzle bit mode:
+// and-mask 0x18 keeps the group, or-mask u selects the lane; no LDS access).
+template <int U>
+__device__ __forceinline__ int bcast8(int v) {
+  return __builtin_amdgcn_ds_swizzle(v, 0x18 | (U << 5));
+}
+
+// Gather engine of the bf16 row kernels (8 lanes per row, lane `sub` owns the
+// 16-byte chunks sub, sub + 8 of a neighbour row).  Per round the row's next 16
+// neighbour ids are loaded one or two per lane and broadcast inside the 8-lane
+// group, and all 16 neighbour chunks are requested before any is consumed: a row
+// of degree <= 16 costs one rowptr -> colidx -> gather latency chain.  The
+// gathers are buffer loads with a 32-bit offset (one mad per neighbour, no 64-bit
+// address arithmetic); a missing neighbour (past the row end, id -1) wraps its
+// offset past the descriptor's range, so the hardware returns zeros with no
+// select.  fn(u, v, valid) consumes neighbour u of the round in order; cross-lane
+// work inside fn stays uniform over the row's 8 lanes.
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rows_rsrc(const void* base, long long bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, (int)bytes, 0x00020000);
+}
+
+template <int NQ, typename Fn>
+__device__ __forceinline__ void gather_rows16(const int* colidx, int s, int e, __amdgpu_buffer_rsrc_t rs,
+                                              unsigned row_bytes, int sub, Fn&& fn) {
+  for (int k0 = s; k0 < e; k0 += 16) {
+    const int id0 = k0 + sub < e ? colidx[k0 + sub] : -1;
+    const int id1 = k0 + 8 + sub < e ? colidx[k0 + 8 + sub] : -1;
+    int c[16];
+    c[0] = bcast8<0>(id0); c[1] = bcast8<1>(id0); c[2] = bcast8<2>(id0); c[3] = bcast8<3>(id0);
+    c[4] = bcast8<4>(id0); c[5] = bcast8<5>(id0); c[6] = bcast8<6>(id0); c[7] = bcast8<7>(id0);
+    c[8] = bcast8<0>(id1); c[9] = bcast8<1>(id1); c[10] = bcast8<2>(id1); c[11] = bcast8<3>(id1);
+    c[12] = bcast8<4>(id1); c[13] = bcast8<5>(id1); c[14] = bcast8<6>(id1); c[15] = bcast8<7>(id1);
+    u32x4 v[16][NQ];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const unsigned off = (unsigned)c[u] * row_bytes + 16u * sub;   // id -1: out of range -> 0
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) v[u][q] = __builtin_amdgcn_raw_buffer_load_b128(rs, off + 128u * q, 0, 0);
+    }
+    __builtin_amdgcn_sched_barrier(0);   // all 16 requests issue before the first is consumed
+#pragma unroll
+    for (int u = 0; u < 16; ++u) fn(u, v[u], c[u] >= 0);
   }
-};
-__device__ __forceinline__ NbrLds stage_nbrs(const int* rowptr, const int* colidx, int R, int r0,
-                                            int* lds) {
-  const int rl = min(R, r0 + RPB);
-  const int b = rowptr[r0], e = rowptr[rl];
-  NbrLds n{b, e - b};
-  if (n.cnt <= kNbrCap)
-    for (int i = threadIdx.x; i < n.cnt; i += NT) lds[i] = colidx[b + i];
-  __syncthreads();
-  return n;
+}
+
+// acc[0..7] += the 8 bf16 of a packed 16-byte chunk (exact widening + fp32 add)
+__device__ __forceinline__ void acc8v(float (&a)[8], const u32x4& v) {
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    const unsigned w = v[p];
+    a[2 * p] += __uint_as_float(w << 16);
+    a[2 * p + 1] += __uint_as_float(w & 0xFFFF0000u);
+  }
 }
 
 // ---------------------------------------------------------------- GCN layer 0
@@ -77,7 +123,7 @@ __global__ void __launch_bounds__(NT) gcn0_kernel(Gcn0Args a) {
   }
   __syncthreads();
   const int sub = threadIdx.x & (LPR - 1);
-  const int r = xcd_rowblock(blockIdx.x, a.xcd_nbg) * RPB + threadIdx.x / LPR;
+  const int r = row_of(a.row_order, xcd_rowblock(blockIdx.x, a.xcd_nbg), a.R);
   const bool rv = r < a.R;
   float ax[4] = {0.f, 0.f, 0.f, 0.f};
   if (rv) {
@@ -128,49 +174,29 @@ __global__ void __launch_bounds__(NT) gcn0_kernel(Gcn0Args a) {
 }
 
 // ---------------------------------------------------------------- bf16 SpMM
-template <int EPI>
+template <int EPI, int NQ>
 __global__ void __launch_bounds__(NT) spmm_bf16_kernel(SpmmBfArgs a) {
-  __shared__ int nb_lds[kNbrCap];
   const int sub = threadIdx.x & (LPR - 1);
-  const int rb = xcd_rowblock(blockIdx.x, a.xcd_nbg);
-  const int r = rb * RPB + threadIdx.x / LPR;
-  const NbrLds nl = stage_nbrs(a.rowptr, a.colidx, a.R, rb * RPB, nb_lds);
-  if (r >= a.R) return;
-  const int nch = a.width >> 3;   // 8-column chunks: lane sub owns chunks sub, sub + 8
+  const int r = row_of(a.row_order, xcd_rowblock(blockIdx.x, a.xcd_nbg), a.R);
+  if (r >= a.R) return;            // whole 8-lane row groups leave together
+  const int nch = a.width >> 3;    // 8-column chunks: lane sub owns chunks sub, sub + 8
   float acc[2][8];
 #pragma unroll
   for (int q = 0; q < 2; ++q)
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc[q][j] = 0.f;
-  const int s = a.rowptr[r], e = a.rowptr[r + 1];
-  const __bf16* hb = a.h + 8 * sub;
-  bool qv[2];
+  bool qv[NQ];
 #pragma unroll
-  for (int q = 0; q < 2; ++q) qv[q] = sub + 8 * q < nch;
-  int k = s;
-  for (; k + 4 <= e; k += 4) {
-    const int c0 = nl.at(nb_lds, a.colidx, k), c1 = nl.at(nb_lds, a.colidx, k + 1);
-    const int c2 = nl.at(nb_lds, a.colidx, k + 2), c3 = nl.at(nb_lds, a.colidx, k + 3);
+  for (int q = 0; q < NQ; ++q) qv[q] = sub + 8 * q < nch;
+  // chunks past the width read the next row's bytes (or zeros past the end): never stored
+  const __amdgpu_buffer_rsrc_t rs = rows_rsrc(a.h, (long long)a.R * a.ldh * 2);
+  gather_rows16<NQ>(a.colidx, a.rowptr[r], a.rowptr[r + 1], rs, 2u * a.ldh, sub,
+                    [&](int, const u32x4 (&v)[NQ], bool) {
 #pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      if (!qv[q]) continue;
-      const uint4 v0 = *reinterpret_cast<const uint4*>(hb + (long long)c0 * a.ldh + 64 * q);
-      const uint4 v1 = *reinterpret_cast<const uint4*>(hb + (long long)c1 * a.ldh + 64 * q);
-      const uint4 v2 = *reinterpret_cast<const uint4*>(hb + (long long)c2 * a.ldh + 64 * q);
-      const uint4 v3 = *reinterpret_cast<const uint4*>(hb + (long long)c3 * a.ldh + 64 * q);
-      acc8(acc[q], v0); acc8(acc[q], v1); acc8(acc[q], v2); acc8(acc[q], v3);
-    }
-  }
-  for (; k < e; ++k) {
-    const int c0 = nl.at(nb_lds, a.colidx, k);
+                      for (int q = 0; q < NQ; ++q) acc8v(acc[q], v[q]);
+                    });
 #pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      if (!qv[q]) continue;
-      acc8(acc[q], *reinterpret_cast<const uint4*>(hb + (long long)c0 * a.ldh + 64 * q));
-    }
-  }
-#pragma unroll
-  for (int q = 0; q < 2; ++q) {
+  for (int q = 0; q < NQ; ++q) {
     if (!qv[q]) continue;
     const int col = 64 * q + 8 * sub;
     if constexpr (EPI == SND_SPMM_PLAIN) {
@@ -207,80 +233,74 @@ __global__ void __launch_bounds__(NT) spmm_bf16_kernel(SpmmBfArgs a) {
 //   loss += (pw - 1) softplus(L) - pw L ;  tp += (L > 0) ;  ej_i += ((pw - 1) sigmoid(L) - pw) z_j
 // (optimizer.py:142-144 restricted to the A = 1 pairs; the dense kernel adds softplus(L)
 // over all pairs).  8 lanes per row, one 16-byte z chunk per lane, 4 neighbours in flight.
+template <int NQ>
 __global__ void __launch_bounds__(NT) edge_bf16_kernel(EdgeBfArgs a) {
-  __shared__ int nb_lds[kNbrCap];
   __shared__ double sl[NT / 64];
   __shared__ unsigned st[NT / 64];
   const int sub = threadIdx.x & (LPR - 1);
-  const int rb = xcd_rowblock(blockIdx.x, a.xcd_nbg);
-  const int r = rb * RPB + threadIdx.x / LPR;
-  const NbrLds nl = stage_nbrs(a.rowptr, a.colidx, a.R, rb * RPB, nb_lds);
+  const int r = row_of(a.row_order, xcd_rowblock(blockIdx.x, a.xcd_nbg), a.R);
+  const bool rv = r < a.R;
   const int nch = a.d >> 3;
-  bool qv[2];
+  bool qv[NQ];
 #pragma unroll
-  for (int q = 0; q < 2; ++q) qv[q] = sub + 8 * q < nch;
+  for (int q = 0; q < NQ; ++q) qv[q] = sub + 8 * q < nch;
   float lossr = 0.f;
   unsigned tp = 0;
-  if (r < a.R) {
-    float zi[2][8], acc[2][8];
+  float zi[NQ][8], acc[NQ][8];
 #pragma unroll
-    for (int q = 0; q < 2; ++q)
+  for (int q = 0; q < NQ; ++q)
 #pragma unroll
-      for (int j = 0; j < 8; ++j) { zi[q][j] = 0.f; acc[q][j] = 0.f; }
+    for (int j = 0; j < 8; ++j) { zi[q][j] = 0.f; acc[q][j] = 0.f; }
+  if (rv)
 #pragma unroll
-    for (int q = 0; q < 2; ++q)
+    for (int q = 0; q < NQ; ++q)
       if (qv[q]) {
         const bf16x8 v = *reinterpret_cast<const bf16x8*>(a.z + (long long)r * a.d + 64 * q + 8 * sub);
 #pragma unroll
         for (int j = 0; j < 8; ++j) zi[q][j] = (float)v[j];
       }
-    const float pw = a.pos_weight;
-    const int s = a.rowptr[r], e = a.rowptr[r + 1];
-    for (int k = s; k < e; k += 4) {
-      float zj[4][2][8], dot[4];
+  const float pw = a.pos_weight;
+  const __amdgpu_buffer_rsrc_t rs = rows_rsrc(a.z, (long long)a.R * a.d * 2);
+  gather_rows16<NQ>(a.colidx, rv ? a.rowptr[r] : 0, rv ? a.rowptr[r + 1] : 0, rs, 2u * a.d, sub,
+                    [&](int, const u32x4 (&v)[NQ], bool valid) {
+    float zj[NQ][8], dot = 0.f;
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const bool uv = k + u < e;
-        const int c = uv ? nl.at(nb_lds, a.colidx, k + u) : r;
-        dot[u] = 0.f;
+    for (int q = 0; q < NQ; ++q)
 #pragma unroll
-        for (int q = 0; q < 2; ++q) {
-          bf16x8 v{};
-          if (qv[q]) v = *reinterpret_cast<const bf16x8*>(a.z + (long long)c * a.d + 64 * q + 8 * sub);
-#pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            zj[u][q][j] = uv ? (float)v[j] : 0.f;
-            dot[u] += zi[q][j] * zj[u][q][j];
-          }
-        }
+      for (int p = 0; p < 4; ++p) {
+        const unsigned w = v[q][p];
+        zj[q][2 * p] = qv[q] ? __uint_as_float(w << 16) : 0.f;
+        zj[q][2 * p + 1] = qv[q] ? __uint_as_float(w & 0xFFFF0000u) : 0.f;
       }
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const float L = row8_sum(dot[u]);
-        if (k + u >= e) continue;
-        float coef = -pw;
-        if (pw != 1.f) {
-          const float sg = 1.f / (1.f + __expf(-L));
-          coef += (pw - 1.f) * sg;
-          lossr += (pw - 1.f) * (fmaxf(L, 0.f) + log1pf(__expf(-fabsf(L))));
-        }
-        lossr -= pw * L;
-        tp += L > 0.f ? 1u : 0u;
+    for (int q = 0; q < NQ; ++q)
 #pragma unroll
-        for (int q = 0; q < 2; ++q)
-#pragma unroll
-          for (int j = 0; j < 8; ++j) acc[q][j] += coef * zj[u][q][j];
-      }
+      for (int j = 0; j < 8; ++j) dot += zi[q][j] * zj[q][j];
+    const float L = row8_sum(dot);
+    if (!valid) return;
+    float coef = -pw;
+    if (pw != 1.f) {
+      const float sg = 1.f / (1.f + __expf(-L));
+      coef += (pw - 1.f) * sg;
+      lossr += (pw - 1.f) * (fmaxf(L, 0.f) + log1pf(__expf(-fabsf(L))));
     }
+    lossr -= pw * L;
+    tp += L > 0.f ? 1u : 0u;
 #pragma unroll
-    for (int q = 0; q < 2; ++q)
+    for (int q = 0; q < NQ; ++q)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[q][j] += coef * zj[q][j];
+  });
+  if (rv) {
+#pragma unroll
+    for (int q = 0; q < NQ; ++q)
       if (qv[q]) {
         float* o = a.ej + (long long)r * a.d + 64 * q + 8 * sub;
         *reinterpret_cast<float4*>(o) = make_float4(acc[q][0], acc[q][1], acc[q][2], acc[q][3]);
         *reinterpret_cast<float4*>(o + 4) = make_float4(acc[q][4], acc[q][5], acc[q][6], acc[q][7]);
       }
-    if (sub != 0) { lossr = 0.f; tp = 0; }   // the row's 8 lanes hold the same sums
   }
+  if (sub != 0 || !rv) { lossr = 0.f; tp = 0; }   // the row's 8 lanes hold the same sums
   const double l = wave_sum_d((double)lossr);
   const unsigned t = wave_sum_u(tp);
   const int w = threadIdx.x >> 6;
@@ -427,15 +447,19 @@ int launch_gcn0(const Gcn0Args& a, hipStream_t s) {
 int launch_spmm_bf16(const SpmmBfArgs& a, hipStream_t s) {
   if (a.R <= 0) return 0;
   SND_CHECK_ARG(a.width % 8 == 0 && a.width <= 128 && a.ldh % 8 == 0, "spmm_bf16: width %% 8 <= 128, ldh %% 8");
+  SND_CHECK_ARG((long long)a.R * a.ldh * 2 < (1ll << 31), "spmm_bf16: rows x ldh beyond the 2 GB buffer range");
   dim3 grid(cdiv(a.R, RPB));
+  const bool two = a.width > 64;
   if (a.epi == SND_SPMM_PLAIN) {
     SND_CHECK_ARG(a.out && a.ldo % 8 == 0, "spmm_bf16: out");
-    hipLaunchKernelGGL((spmm_bf16_kernel<SND_SPMM_PLAIN>), grid, dim3(NT), 0, s, a);
+    if (two) hipLaunchKernelGGL((spmm_bf16_kernel<SND_SPMM_PLAIN, 2>), grid, dim3(NT), 0, s, a);
+    else hipLaunchKernelGGL((spmm_bf16_kernel<SND_SPMM_PLAIN, 1>), grid, dim3(NT), 0, s, a);
   } else {
     SND_CHECK_ARG(a.pre && a.g && a.g1 && a.b1 && a.ge && a.be && a.x && a.f <= 8 &&
                       a.ldp % 4 == 0 && a.ldg % 8 == 0 && a.ldg >= a.width + 8,
                   "spmm_bf16: GCN operands");
-    hipLaunchKernelGGL((spmm_bf16_kernel<SND_SPMM_GCN>), grid, dim3(NT), 0, s, a);
+    if (two) hipLaunchKernelGGL((spmm_bf16_kernel<SND_SPMM_GCN, 2>), grid, dim3(NT), 0, s, a);
+    else hipLaunchKernelGGL((spmm_bf16_kernel<SND_SPMM_GCN, 1>), grid, dim3(NT), 0, s, a);
   }
   SND_LAUNCH_CHECK("spmm_bf16_kernel");
   return 0;
@@ -446,7 +470,9 @@ int edge_bf16_blocks(int R) { return cdiv(R, RPB); }
 int launch_edge_bf16(const EdgeBfArgs& a, hipStream_t s) {
   if (a.R <= 0) return 0;
   SND_CHECK_ARG(a.d % 8 == 0 && a.d <= 128 && a.z && a.ej && a.part && a.rowptr, "edge_bf16: operands");
-  hipLaunchKernelGGL(edge_bf16_kernel, dim3(edge_bf16_blocks(a.R)), dim3(NT), 0, s, a);
+  SND_CHECK_ARG((long long)a.R * a.d * 2 < (1ll << 31), "edge_bf16: rows x d beyond the 2 GB buffer range");
+  if (a.d > 64) hipLaunchKernelGGL(edge_bf16_kernel<2>, dim3(edge_bf16_blocks(a.R)), dim3(NT), 0, s, a);
+  else hipLaunchKernelGGL(edge_bf16_kernel<1>, dim3(edge_bf16_blocks(a.R)), dim3(NT), 0, s, a);
   SND_LAUNCH_CHECK("edge_bf16_kernel");
   return 0;
 }
@@ -491,12 +517,13 @@ using namespace snd;
 
 extern "C" int snd_csr_spmm_bf16(const int* rowptr, const int* colidx, int n_rows, const void* h,
                                  int ldh, int width, void* out, int ldo, int n_per_graph,
-                                 int n_graphs, snd_stream_t stream) {
+                                 int n_graphs, const int* row_order, snd_stream_t stream) {
   SND_CHECK_ARG(rowptr && (colidx || n_rows == 0) && h && out && n_rows >= 0,
                 "snd_csr_spmm_bf16: null operand");
   SpmmBfArgs a{rowptr, colidx, n_rows, reinterpret_cast<const __bf16*>(h), ldh, width,
                SND_SPMM_PLAIN, reinterpret_cast<__bf16*>(out), ldo};
   a.xcd_nbg = (n_per_graph > 0 && n_graphs > 0 && (long long)n_per_graph * n_graphs == n_rows)
                   ? xcd_nbg(n_per_graph, n_graphs) : 0;
+  a.row_order = row_order;
   return launch_spmm_bf16(a, (hipStream_t)stream);
 }

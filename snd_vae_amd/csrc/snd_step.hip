@@ -120,7 +120,7 @@ struct snd_plan {
 };
 
 extern "C" const char* snd_last_error(void) { return g_err; }
-extern "C" int snd_abi_version(void) { return 2; }
+extern "C" int snd_abi_version(void) { return 3; }
 
 extern "C" int snd_plan_create(const snd_config_t* cfg, int n_graphs, snd_plan_t** out) {
   SND_CHECK_ARG(cfg && out && n_graphs > 0, "snd_plan_create: bad args");
@@ -549,6 +549,7 @@ int encoder_fast_fwd(const Ctx& x, const snd_batch_t* batch) {
     Gcn0Args a{batch->rowptr, batch->colidx, R, batch->features, f, f, x.w("enc.W0"),
                x.w("enc.bn0.gamma"), x.w("enc.bn0.beta"), h0, bf("FH1"), p.ldh1, x.f("AX"), bf("AXB"),
                xcd_nbg(p.N, p.B)};
+    a.row_order = batch->row_order;
     SND_TRY(launch_gcn0(a, x.s));
   }
   {
@@ -560,6 +561,7 @@ int encoder_fast_fwd(const Ctx& x, const snd_batch_t* batch) {
     SpmmBfArgs a{batch->rowptr, batch->colidx, R, bf("FXW1"), h1, h1, SND_SPMM_GCN, nullptr, 0,
                  x.f("FP1"), h1, x.w("enc.bn1.gamma"), x.w("enc.bn1.beta"), batch->features, f, f,
                  x.w("enc.bne.gamma"), x.w("enc.bne.beta"), bf("FG"), p.ldg, xcd_nbg(p.N, p.B)};
+    a.row_order = batch->row_order;
     SND_TRY(launch_spmm_bf16(a, x.s));
   }
   {
@@ -605,6 +607,7 @@ int encoder_fast_bwd(const Ctx& x, const snd_batch_t* batch, float adj_scale, fl
   {
     SpmmBfArgs a{batch->rowptr, batch->colidx, R, bf("FDP1"), h1, h1, SND_SPMM_PLAIN, bf("FDXW1"), h1};
     a.xcd_nbg = xcd_nbg(p.N, p.B);
+    a.row_order = batch->row_order;
     SND_TRY(launch_spmm_bf16(a, x.s));
   }
   SND_TRY(fork(x));
@@ -807,6 +810,7 @@ extern "C" int snd_plan_launch(const snd_plan_t* plan, const snd_batch_t* batch,
     SpmmBfArgs a{batch->rowptr, batch->colidx, p.R, (const __bf16*)(ws + p.buf("FDP1")), p.c.h1,
                  p.c.h1, SND_SPMM_PLAIN, (__bf16*)(ws + p.buf("FDXW1")), p.c.h1};
     a.xcd_nbg = xcd_nbg(p.N, p.B);
+    a.row_order = batch->row_order;
     return launch_spmm_bf16(a, s);
   }
   if (!strncmp(kernel, "tref_", 5)) {   // graph-latent weight-streaming kernels
@@ -951,6 +955,7 @@ extern "C" int snd_train_step(const snd_plan_t* plan, const snd_batch_t* batch,
     if (p.fast) {
       EdgeBfArgs ea{rp, ci, R, (const __bf16*)x.f("ZB"), dj, c.pos_weight, x.f("EJ"), x.d("PEDGE"),
                     xcd_nbg(N, p.B)};
+      ea.row_order = batch->row_order;
       SND_TRY(launch_edge_bf16(ea, side(x)));
     } else {
       EdgeArgs ea{rp, ci, R, x.f("Z"), dj, c.pos_weight, x.f("EJ"), x.d("PEDGE")};

@@ -163,6 +163,30 @@ def batch_from_dense(cfg: SNDConfig, adj: np.ndarray, feature: np.ndarray,
                       np.ascontiguousarray(x), np.ascontiguousarray(s))
 
 
+def locality_order(batch: GraphBatch) -> np.ndarray:
+    """Processing order of the rows for the gather kernels (int32 [B*N]).
+
+    Per graph, the reverse Cuthill-McKee permutation of its adjacency: rows that
+    are consecutive in this order are graph neighbours, so the neighbour rows a
+    workgroup gathers overlap and hit in L1 (32 consecutive rows of a seed-0
+    N=4096 RGG share each gathered row ~4x, against ~1.06x in generator order).
+    It is a schedule, not a relabelling: outputs stay at their original rows and
+    the node order the conv1d decoders see (decision iv) is untouched.
+    """
+    import scipy.sparse as sp
+    from scipy.sparse.csgraph import reverse_cuthill_mckee
+    n, B = batch.n_nodes, batch.n_graphs
+    out = np.empty(B * n, np.int32)
+    rp = batch.rowptr.astype(np.int64)
+    for b in range(B):
+        lo = b * n
+        s, e = rp[lo], rp[lo + n]
+        a = sp.csr_matrix((np.ones(e - s, np.int8), batch.colidx[s:e] - lo, rp[lo:lo + n + 1] - s),
+                          shape=(n, n))
+        out[lo:lo + n] = reverse_cuthill_mckee(a, symmetric_mode=True).astype(np.int32) + lo
+    return out
+
+
 def shard(batch: GraphBatch, rank: int, world: int) -> GraphBatch:
     """Contiguous equal shard of the global batch for DP rank ``rank``.
 

@@ -66,17 +66,18 @@ def spmm(rowptr, colidx, h):
     return out
 
 
-def spmm_bf16(rowptr, colidx, h, n_per_graph=0, n_graphs=0):
+def spmm_bf16(rowptr, colidx, h, n_per_graph=0, n_graphs=0, row_order=None):
     """A @ h over bf16 rows, fp32 accumulation (the bf16 path's SpMM, layers.py:122).
 
-    n_per_graph / n_graphs let the kernel keep each graph's row blocks on one XCD."""
+    n_per_graph / n_graphs let the kernel keep each graph's row blocks on one XCD;
+    row_order (int32 device tensor, data.locality_order) is the processing schedule."""
     if not (h.is_cuda and h.is_contiguous() and h.dtype == torch.bfloat16):
         raise ValueError("spmm_bf16: expected a contiguous bfloat16 device tensor")
     rows, width = h.shape
     out = torch.empty_like(h)
     _lib.check(_lib.lib().snd_csr_spmm_bf16(
         _P(rowptr), _P(colidx), rows, _P(h), width, width, _P(out), width, n_per_graph,
-        n_graphs, _lib.stream_ptr()), "snd_csr_spmm_bf16")
+        n_graphs, _P(row_order), _lib.stream_ptr()), "snd_csr_spmm_bf16")
     return out
 
 

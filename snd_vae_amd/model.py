@@ -24,7 +24,7 @@ import torch
 
 from . import _lib
 from .config import SNDConfig
-from .data import GraphBatch
+from .data import GraphBatch, locality_order
 from .params import flat_layout, init_blocks
 
 DTYPES = {"f32": 0, "fp32": 0, "bf16": 1}
@@ -43,7 +43,9 @@ def c_config(cfg: SNDConfig, dtype: str) -> _lib.Config:
 class DeviceBatch:
     """A GraphBatch resident in HBM (the feed dict of `main.py:327-329`)."""
 
-    def __init__(self, batch: GraphBatch, device="cuda"):
+    def __init__(self, batch: GraphBatch, device="cuda", locality: bool = True):
+        """locality: upload the per-graph RCM row schedule of the gather kernels
+        (data.locality_order); results do not depend on it."""
         t = lambda a, dt: torch.from_numpy(np.ascontiguousarray(a)).to(device=device, dtype=dt)
         self.n_graphs = batch.n_graphs
         self.n_nodes = batch.n_nodes
@@ -53,12 +55,13 @@ class DeviceBatch:
         self.features = t(batch.features, torch.float32)
         self.feature_truth = t(batch.feature_truth, torch.float32)
         self.spatial_truth = t(batch.spatial_truth, torch.float32)
+        self.row_order = t(locality_order(batch), torch.int32) if locality and batch.nnz else None
         self.host = batch
 
     def c_struct(self) -> _lib.Batch:
         p = _lib.ptr
         return _lib.Batch(p(self.rowptr), p(self.colidx), p(self.features),
-                          p(self.feature_truth), p(self.spatial_truth))
+                          p(self.feature_truth), p(self.spatial_truth), p(self.row_order))
 
 
 class SGCNModelVAE:

@@ -76,6 +76,16 @@ def test_spmm_bf16(n, B, kbar, width):
     assert np.abs(out - ref).max() <= 2 ** -7 * max(np.abs(ref).max(), 1.0)
     iso = np.diff(rp) == 0
     assert np.all(out[iso] == 0.0)
+    # the locality schedule changes the processing order only: bitwise-equal rows
+    from snd_vae_amd.data import GraphBatch, locality_order
+    gb = GraphBatch(B, n, rp, ci, np.zeros((n * B, 1), np.float32), np.zeros((n * B, 1), np.float32),
+                    np.zeros((n * B, 2), np.float32))
+    order = locality_order(gb)
+    assert np.array_equal(np.sort(order), np.arange(n * B))
+    assert all(set(order[b * n:(b + 1) * n]) == set(range(b * n, (b + 1) * n)) for b in range(B))
+    out2 = layers.spmm_bf16(cu(rp, torch.int32), cu(ci if len(ci) else np.zeros(1, np.int32), torch.int32),
+                            hb.cuda(), n, B, cu(order, torch.int32)).float().cpu().numpy()
+    assert np.array_equal(out, out2)
 
 
 def test_graph_convolution_epilogue():
