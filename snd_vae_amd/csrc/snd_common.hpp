@@ -102,13 +102,30 @@ __device__ __forceinline__ uint4 philox4x32_10(uint4 c, uint2 k) {
   return c;
 }
 
+// Four standard normals for elements 4q .. 4q+3: one Philox block, two Box-Muller pairs.
+__device__ __forceinline__ float4 philox_normal4(unsigned long long seed, unsigned offset,
+                                                unsigned long long q) {
+  const uint4 r = philox4x32_10(make_uint4((unsigned)q, (unsigned)(q >> 32), offset, 0u),
+                                make_uint2((unsigned)seed, (unsigned)(seed >> 32)));
+  const float k = 2.3283064365386963e-10f;
+  const float m1 = sqrtf(-2.0f * __logf(((float)r.x + 1.0f) * k));   // u in (0, 1]
+  const float m2 = sqrtf(-2.0f * __logf(((float)r.z + 1.0f) * k));
+  float s1, c1, s2, c2;
+  __sincosf(6.283185307179586f * ((float)r.y * k), &s1, &c1);
+  __sincosf(6.283185307179586f * ((float)r.w * k), &s2, &c2);
+  return make_float4(m1 * c1, m1 * s1, m2 * c2, m2 * s2);
+}
+
+// Element idx of the same stream (every engine draws identical eps for a (seed, step)).
 __device__ __forceinline__ float philox_normal(unsigned long long seed, unsigned offset,
                                                unsigned long long idx) {
-  const uint4 r = philox4x32_10(make_uint4((unsigned)idx, (unsigned)(idx >> 32), offset, 0u),
-                                make_uint2((unsigned)seed, (unsigned)(seed >> 32)));
-  const float u1 = ((float)r.x + 1.0f) * 2.3283064365386963e-10f;  // (0, 1]
-  const float u2 = (float)r.y * 2.3283064365386963e-10f;
-  return sqrtf(-2.0f * __logf(u1)) * __cosf(6.283185307179586f * u2);
+  const float4 v = philox_normal4(seed, offset, idx >> 2);
+  switch (idx & 3) {
+    case 0: return v.x;
+    case 1: return v.y;
+    case 2: return v.z;
+    default: return v.w;
+  }
 }
 
 inline int cdiv(long long a, long long b) { return (int)((a + b - 1) / b); }

@@ -237,11 +237,19 @@ struct ReducePack {
   int bstart[kMaxReduce + 1];   // first block of each descriptor (flattened 1-D grid)
 };
 
-__global__ void __launch_bounds__(256) reduce_kernel(ReducePack pk) {
+template <int NTF> __device__ void finalize_block(const FinalizeArgs& a);
+
+// fin: block 0 computes the loss terms (finalize) instead of a reduction block
+template <bool FIN>
+__global__ void __launch_bounds__(256) reduce_kernel(ReducePack pk, FinalizeArgs fin) {
+  if constexpr (FIN) {
+    if (blockIdx.x == 0) { finalize_block<256>(fin); return; }
+  }
+  const int bid = (int)blockIdx.x - (FIN ? 1 : 0);
   int di = 0;
-  while (di + 1 < kMaxReduce && (int)blockIdx.x >= pk.bstart[di + 1]) ++di;   // uniform
+  while (di + 1 < kMaxReduce && bid >= pk.bstart[di + 1]) ++di;   // uniform
   const ReduceDesc& d = pk.d[di];
-  const int bx = blockIdx.x - pk.bstart[di];
+  const int bx = bid - pk.bstart[di];
   __shared__ double red[256];
   const int rows = d.rows > 0 ? d.rows : 1;
   const long long items = (long long)rows * d.len;
@@ -281,18 +289,19 @@ __global__ void __launch_bounds__(256) reduce_kernel(ReducePack pk) {
 }
 
 // ---------------------------------------------------------------- finalize
-constexpr int kFinT = 1024;
-__global__ void __launch_bounds__(kFinT) finalize_kernel(FinalizeArgs a) {
+// Loss terms from the per-block partials, in fixed order (one workgroup of NTF threads).
+template <int NTF>
+__device__ __forceinline__ void finalize_block(const FinalizeArgs& a) {
   double v[7] = {0, 0, 0, 0, 0, 0, 0};   // dl, dc, el, tp, kl, ss, sn
 #pragma unroll 4
-  for (int k = threadIdx.x; k < a.n_zzt; k += kFinT) { v[0] += a.zzt_part[2 * k]; v[1] += a.zzt_part[2 * k + 1]; }
+  for (int k = threadIdx.x; k < a.n_zzt; k += NTF) { v[0] += a.zzt_part[2 * k]; v[1] += a.zzt_part[2 * k + 1]; }
 #pragma unroll 4
-  for (int k = threadIdx.x; k < a.n_edge; k += kFinT) { v[2] += a.edge_part[2 * k]; v[3] += a.edge_part[2 * k + 1]; }
+  for (int k = threadIdx.x; k < a.n_edge; k += NTF) { v[2] += a.edge_part[2 * k]; v[3] += a.edge_part[2 * k + 1]; }
 #pragma unroll 4
-  for (int k = threadIdx.x; k < a.n_kl; k += kFinT) v[4] += a.kl_part[k];
+  for (int k = threadIdx.x; k < a.n_kl; k += NTF) v[4] += a.kl_part[k];
 #pragma unroll 4
-  for (int k = threadIdx.x; k < a.n_s; k += kFinT) { v[5] += a.sse_s[k]; v[6] += a.sse_n[k]; }
-  __shared__ double sh[kFinT / 64][7];
+  for (int k = threadIdx.x; k < a.n_s; k += NTF) { v[5] += a.sse_s[k]; v[6] += a.sse_n[k]; }
+  __shared__ double sh[NTF / 64][7];
 #pragma unroll
   for (int q = 0; q < 7; ++q) v[q] = wave_sum_d(v[q]);
   if ((threadIdx.x & 63) == 0)
@@ -301,7 +310,7 @@ __global__ void __launch_bounds__(kFinT) finalize_kernel(FinalizeArgs a) {
   __syncthreads();
   double dl = 0, dc = 0, el = 0, tp = 0, kl = 0, ss = 0, sn = 0;
   if (threadIdx.x == 0)
-    for (int w = 0; w < kFinT / 64; ++w) {
+    for (int w = 0; w < NTF / 64; ++w) {
       dl += sh[w][0]; dc += sh[w][1]; el += sh[w][2]; tp += sh[w][3];
       kl += sh[w][4]; ss += sh[w][5]; sn += sh[w][6];
     }
@@ -323,6 +332,9 @@ __global__ void __launch_bounds__(kFinT) finalize_kernel(FinalizeArgs a) {
     for (int k = 0; k < 6; ++k) a.grad_tail[k] = (float)L[k];
   if (a.step) *a.step += 1;
 }
+
+constexpr int kFinT = 1024;
+__global__ void __launch_bounds__(kFinT) finalize_kernel(FinalizeArgs a) { finalize_block<kFinT>(a); }
 
 // ---------------------------------------------------------------- Adam
 __global__ void __launch_bounds__(256) adam_kernel(float* p, const float* g, float* m, float* v,
@@ -410,8 +422,9 @@ int launch_enc_bwd(const EncBwdArgs& a, int rows, hipStream_t s) {
   return 0;
 }
 
-int launch_reduce(const ReduceDesc* d, int n, hipStream_t s) {
-  for (int base = 0; base < n; base += kMaxReduce) {
+int launch_reduce(const ReduceDesc* d, int n, hipStream_t s, const FinalizeArgs* fin) {
+  for (int base = 0; base < n || (base == 0 && fin); base += kMaxReduce) {
+    const bool last = base + kMaxReduce >= n;
     ReducePack pk{};
     const int cnt = n - base < kMaxReduce ? n - base : kMaxReduce;
     long long nb = 0;
@@ -425,8 +438,12 @@ int launch_reduce(const ReduceDesc* d, int n, hipStream_t s) {
       }
     }
     pk.bstart[kMaxReduce] = (int)nb;
-    if (nb == 0) continue;
-    hipLaunchKernelGGL(reduce_kernel, dim3((unsigned)nb), dim3(256), 0, s, pk);
+    if (fin && last) {   // the loss terms ride in the last reduction launch
+      hipLaunchKernelGGL(reduce_kernel<true>, dim3((unsigned)nb + 1), dim3(256), 0, s, pk, *fin);
+    } else {
+      if (nb == 0) continue;
+      hipLaunchKernelGGL(reduce_kernel<false>, dim3((unsigned)nb), dim3(256), 0, s, pk, FinalizeArgs{});
+    }
     SND_LAUNCH_CHECK("reduce_kernel");
   }
   return 0;

@@ -376,35 +376,49 @@ __global__ void __launch_bounds__(NT) reparam_prep_kernel(ReparamPrepArgs a) {
   __shared__ float stile[64][DP + 1];
   __shared__ double red[NT / 64];
   const int g = blockIdx.y, rb = blockIdx.x;
-  const int L = a.L;
+  const int L = a.L;                      // multiple of 4 (16 / 32 / 64 / 128)
   const unsigned off = a.step ? (unsigned)(*a.step) : 0u;
   const float sc = 1.2011224087864498f;  // sqrt(log2 e)
+  constexpr int Q = DP / 4;               // 4-column quads per row: one Philox block each
   double kl = 0.0;
-  for (int idx = threadIdx.x; idx < 64 * DP; idx += NT) {
-    const int rr = idx / DP, c = idx - rr * DP;
+  for (int idx = threadIdx.x; idx < 64 * Q; idx += NT) {
+    const int rr = idx / Q, c = 4 * (idx - rr * Q);
     const int row = rb * 64 + rr;
-    float z = 0.f;
-    if (row < a.n && c < L && a.stage_only) {
-      const long long gr = (long long)g * a.n + row;
-      z = a.ms[gr * a.ldms + c];
-      a.zb[gr * L + c] = (__bf16)z;
-    } else if (row < a.n && c < L) {
+    float z[4] = {0.f, 0.f, 0.f, 0.f};
+    if (row < a.n && c < L) {
       const long long gr = (long long)g * a.n + row;
       const long long i = gr * L + c;
-      const float mu = a.ms[gr * a.ldms + c];
-      const float ls = a.ms[gr * a.ldms + L + c];
-      const float eps = a.eps_in ? a.eps_in[i] : philox_normal(a.seed, off, (unsigned long long)i);
-      const float es = __expf(ls);
-      z = mu + eps * es;
-      a.z[i] = z;
-      a.eps_out[i] = eps;
-      a.zb[i] = (__bf16)z;
-      kl += (double)(1.f + 2.f * ls - mu * mu - es * es);
+      const float4 m = *reinterpret_cast<const float4*>(a.ms + gr * a.ldms + c);
+      if (a.stage_only) {
+        z[0] = m.x; z[1] = m.y; z[2] = m.z; z[3] = m.w;
+      } else {
+        const float4 ls = *reinterpret_cast<const float4*>(a.ms + gr * a.ldms + L + c);
+        const float4 ep = a.eps_in ? *reinterpret_cast<const float4*>(a.eps_in + i)
+                                   : philox_normal4(a.seed, off, (unsigned long long)i >> 2);
+        const float mu[4] = {m.x, m.y, m.z, m.w}, s[4] = {ls.x, ls.y, ls.z, ls.w};
+        const float e[4] = {ep.x, ep.y, ep.z, ep.w};
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const float es = __expf(s[t]);
+          z[t] = mu[t] + e[t] * es;                                      // model.py:159
+          kl += (double)(1.f + 2.f * s[t] - mu[t] * mu[t] - es * es);    // optimizer.py:193
+        }
+        *reinterpret_cast<float4*>(a.z + i) = make_float4(z[0], z[1], z[2], z[3]);
+        *reinterpret_cast<float4*>(a.eps_out + i) = ep;
+      }
+      bf16x4 zb;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) zb[t] = (__bf16)z[t];
+      *reinterpret_cast<bf16x4*>(a.zb + gr * L + c) = zb;
     }
-    tile[rr][c] = z;
-    const __bf16 b = (__bf16)(z * sc);
-    stile[rr][c] = (float)b;
-    a.jrow[((long long)g * a.npad + row) * DP + c] = b;
+    bf16x4 jb;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      tile[rr][c + t] = z[t];
+      jb[t] = (__bf16)(z[t] * sc);
+      stile[rr][c + t] = (float)jb[t];
+    }
+    *reinterpret_cast<bf16x4*>(a.jrow + ((long long)g * a.npad + row) * DP + c) = jb;
   }
   kl = wave_sum_d(kl);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = kl;
@@ -419,9 +433,13 @@ __global__ void __launch_bounds__(NT) reparam_prep_kernel(ReparamPrepArgs a) {
     for (int rr = 0; rr < 64; ++rr) cs += stile[rr][threadIdx.x];
     a.colpart[((long long)g * (a.npad / 64) + rb) * DP + threadIdx.x] = cs;
   }
-  for (int idx = threadIdx.x; idx < 64 * DP; idx += NT) {
-    const int c = idx >> 6, rr = idx & 63;
-    a.jt[((long long)g * DP + c) * a.npad + rb * 64 + rr] = (__bf16)tile[rr][c];
+  // z^T image: 4 consecutive rows per lane (8-byte stores)
+  for (int idx = threadIdx.x; idx < 16 * DP; idx += NT) {
+    const int c = idx >> 4, r4 = 4 * (idx & 15);
+    bf16x4 t;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) t[u] = (__bf16)tile[r4 + u][c];
+    *reinterpret_cast<bf16x4*>(a.jt + ((long long)g * DP + c) * a.npad + rb * 64 + r4) = t;
   }
 }
 
@@ -481,7 +499,8 @@ int reparam_prep_blocks(int ngraphs, int npad) { return ngraphs * (npad / 64); }
 
 int launch_reparam_prep(const ReparamPrepArgs& a, int dp, hipStream_t s) {
   if (a.ngraphs <= 0) return 0;
-  SND_CHECK_ARG(a.npad % 64 == 0 && a.L <= dp, "reparam_prep: npad %% 64, L <= dp");
+  SND_CHECK_ARG(a.npad % 64 == 0 && a.L <= dp && a.L % 4 == 0 && a.ldms % 4 == 0,
+                "reparam_prep: npad %% 64, L <= dp, L and ldms %% 4");
   SND_CHECK_ARG(a.ms && a.zb && a.jrow && a.jt && a.colpart &&
                     (a.stage_only || (a.z && a.eps_out && a.kl_part)),
                 "reparam_prep: null operand");

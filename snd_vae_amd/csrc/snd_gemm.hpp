@@ -41,7 +41,10 @@ struct ReduceDesc {
   long long src_rs, dst_rs;
 };
 constexpr int kMaxReduce = 48;
-int launch_reduce(const ReduceDesc* d, int n, hipStream_t s);
+struct FinalizeArgs;
+// Deterministic slab reductions; with fin, the same launch also computes the loss
+// terms (snd_elem.hpp FinalizeArgs) in an extra workgroup.
+int launch_reduce(const ReduceDesc* d, int n, hipStream_t s, const FinalizeArgs* fin = nullptr);
 
 // Column partial sums written by elementwise kernels are laid out as
 // slab[block][ncols]; helpers compute the block count used.

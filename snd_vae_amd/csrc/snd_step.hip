@@ -1134,13 +1134,11 @@ extern "C" int snd_train_step(const snd_plan_t* plan, const snd_batch_t* batch,
     rd.push_back({x.f("PHN"), x.g("dec.Wn"), nh, n2 * nf, (long long)hn, 1.f, 0});
     rd.push_back({x.f("PHN") + n2 * nf, x.g("dec.bn"), nh, nf, (long long)hn, 1.f, 0});
   }
-  SND_TRY(launch_reduce(rd.data(), (int)rd.size(), x.s));
-
   const int n_kl = (p.fast && !p.tref) ? reparam_prep_blocks(p.B, zzt_npad(N)) : reparam_blocks(RH, L);
   FinalizeArgs fa{x.d("PZZT"), zzt_dense_blocks(p.B, N, c.dtype), x.d("PEDGE"),
                   p.fast ? edge_bf16_blocks(R) : edge_blocks(R, dj),
                   x.d("PKL"), n_kl, x.d("PSSES"), x.d("PSSEN"), nh,
                   rp, p.B, N, L, sd, nf, c.beta, c.norm, losses, grads + p.pcount, step_counter,
                   (double)RH * L};
-  return launch_finalize(fa, x.s);
+  return launch_reduce(rd.data(), (int)rd.size(), x.s, &fa);   // + loss terms in one launch
 }

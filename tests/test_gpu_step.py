@@ -134,6 +134,23 @@ def test_train_step_c4_size_vs_oracle(dtype, ltol, gtol):
     assert model.z_mean_sg.shape == (2, cfg.latent)
 
 
+def test_device_rng_same_draw_on_both_engines():
+    """Philox eps (seed, step) is the same stream on the bf16 fast path and the fp32
+    generic engine: standard-normal moments, bitwise-equal draws."""
+    from snd_vae_amd.params import init_blocks
+    cfg = tscale(512, 64)
+    batch = synthetic_batch(cfg, 2, seed=6)
+    eps = []
+    for dtype in ("bf16", "f32"):
+        m, o, b = make(cfg, batch, init_blocks(cfg, 0), dtype)
+        o.forward_backward(b)
+        torch.cuda.synchronize()
+        eps.append(m.buffer("EPS")[:2 * 512 * 64].clone())
+    assert torch.equal(eps[0], eps[1])
+    e = eps[0].double()
+    assert abs(float(e.mean())) < 0.02 and abs(float(e.std()) - 1.0) < 0.02
+
+
 def test_graph_replay_is_deterministic():
     """A captured step replays bit-identically to eager steps (no atomics)."""
     cfg = tscale(512, 64)

@@ -17,13 +17,14 @@ def main():
     ap.add_argument("--nodes", type=int, default=4096)
     ap.add_argument("--latent", type=int, default=64)
     ap.add_argument("--dtype", default="bf16")
+    ap.add_argument("--config", default="", help="preset (C4, C5, ...) instead of --nodes/--latent")
     args = ap.parse_args()
     import torch
-    from snd_vae_amd.config import tscale
+    from snd_vae_amd.config import PRESETS, tscale
     from snd_vae_amd.data import synthetic_batch
     from snd_vae_amd.model import DeviceBatch, SGCNModelVAE
     from snd_vae_amd.optimizer import OptimizerVAE
-    cfg = tscale(args.nodes, args.latent)
+    cfg = PRESETS[args.config] if args.config else tscale(args.nodes, args.latent)
     db = DeviceBatch(synthetic_batch(cfg, args.graphs, seed=1000))
     model = SGCNModelVAE(cfg, args.graphs, dtype=args.dtype)
     opt = OptimizerVAE(model)

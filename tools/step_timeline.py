@@ -9,7 +9,7 @@ import sys
 def main(path):
     rows = list(csv.DictReader(open(path)))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-    idx = [i for i, r in enumerate(rows) if "adam_kernel" in r["Kernel_Name"]]
+    idx = [i for i, r in enumerate(rows) if "adam" in r["Kernel_Name"]]
     a, b = idx[-2] + 1, idx[-1] + 1
     t0 = int(rows[a]["Start_Timestamp"])
     busy = 0
