@@ -1,0 +1,34 @@
+"""A/B the C2 step and its zz^T kernel under snd_debug_set flags (plan-time choices).
+
+    python tools/ab_flags.py --flags 0,4096
+"""
+import argparse
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    import bench
+    from snd_vae_amd import _lib
+    from snd_vae_amd.config import tscale
+    from snd_vae_amd.parallel import init_from_env
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--flags", default="0")
+    ap.add_argument("--kernels", default="zzt_dense")
+    ns = ap.parse_args()
+    args = argparse.Namespace(steps=50, warmup=10, no_graph=False, dtype="bf16")
+    info = init_from_env("nccl")
+    for f in [int(x) for x in ns.flags.split(",")]:
+        _lib.check(_lib.lib().snd_debug_set(f))
+        v, ms, model, opt, db, host = bench.run_workload(tscale(4096, 64), 8, args, info)
+        kms = bench.kernel_timer(model, db.c_struct(), 20)
+        ks = {k: round(kms(k), 5) for k in ns.kernels.split(",")}
+        _lib.check(_lib.lib().snd_debug_set(0))
+        print(f"flags {f}: step {ms:.4f} ms, {ks}, losses {opt.loss_dict()['cost']:.6f}", flush=True)
+        bench.del_models()
+
+
+if __name__ == "__main__":
+    main()
