@@ -62,6 +62,10 @@ __global__ void __launch_bounds__(NT) pack_kernel(PackPack pk) {
       float val = 0.f;
       for (int si = 0; si < d.nsrc; ++si) {
         const PackSrc& s = d.s[si];
+        if (s.mode == 2) {                  // identity over [a0, a1)
+          if (k == n && k >= s.a0 && k < s.a1) val = 1.f;
+          continue;
+        }
         int aa, bb, tt;
         if (s.mode == 0) { bb = n - s.n_off + s.b0; aa = k - s.k_off + s.a0; tt = t; }
         else { aa = n - s.n_off + s.a0; bb = k - s.k_off + s.b0; tt = d.T - 1 - t; }

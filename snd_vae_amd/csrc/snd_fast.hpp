@@ -31,7 +31,7 @@ struct PackSrc {
   int A, B;
   int a0, a1, b0, b1;
   int n_off, k_off;
-  int mode;
+  int mode;                   // 0: w[t][k][n] -> (n, k); 1: transposed, taps flipped; 2: identity
 };
 struct PackDesc {
   __bf16* dst;

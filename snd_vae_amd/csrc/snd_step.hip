@@ -84,6 +84,7 @@ struct snd_plan {
   bool fast_enc = false;
   int ldh1 = 0, ldg = 0;
   Img pw1f{}, pwhf{}, pwmsf{}, pwmsb{}, pwhb{}, pw1b{};
+  Img pidg{};                  // graph latent: identity [W -> W] (dG enters RC_ENC1 directly)
   WgGeom gWms{}, gWh{}, gW1{}, gW0{};
   // parameters of the last snd_train_step (snd_plan_launch re-runs kernels on them)
   mutable const float* last_params = nullptr;
@@ -288,6 +289,38 @@ extern "C" int snd_plan_create(const snd_config_t* cfg, int n_graphs, snd_plan_t
       p->add_buf("FSK2S", (long long)p->gK2s.gx * 5 * c.s1 * wgrad_n4(c.s2));
       p->add_buf("FSK2N", (long long)p->gK2n.gx * 5 * c.n1 * wgrad_n4(c.n2));
       p->add_buf("FSK3S", (long long)p->gK3s.gx * 5 * c.s2 * wgrad_n4(c.s3));
+    }
+  }
+  // ---- bf16 fast encoder, graph latent: GCN layers + BN backward on the fast engine;
+  // the heads stream flat(G) in bf16 (snd_tref.hip)
+  if (p->fast && tref && !(debug_flags() & 512)) {
+    auto img1 = [&](int kin, int nout) { return Img{1, kp_of(kin), (int)round_up(nout, 16), 0}; };
+    Img ims[3] = {img1(h0 + f, h1), img1(h1, h0), img1(W, W)};
+    bool ok = h0 % 8 == 0 && h1 % 8 == 0 && h1 <= 128 && f <= 4 && W <= 128 && h0 + f <= 128;
+    for (auto& m : ims)
+      ok = ok && m.kp > 0 && m.np <= 128 && rc_lds_bytes(m.T, m.kp, m.np) <= kRcLdsLimit;
+    if (ok) {
+      p->fast_enc = true;
+      p->ldh1 = (int)round_up(h0 + f, 8);
+      p->ldg = (int)round_up(W, 8);
+      const char* nm[3] = {"PW1F", "PW1B", "PIDG"};
+      for (int i = 0; i < 3; ++i) {
+        p->add_buf(nm[i], (long long)pack_bytes(ims[i].T, ims[i].kp, ims[i].np), 1);
+        ims[i].off = p->bufs.back().off;
+      }
+      p->pw1f = ims[0]; p->pw1b = ims[1]; p->pidg = ims[2];
+      p->add_buf("AX", R * 4);            p->add_buf("AXB", R * 8, 2);
+      p->add_buf("FH1", R * p->ldh1, 2);  p->add_buf("FXW1", R * h1, 2);
+      p->add_buf("FP1", R * h1);          p->add_buf("FG", R * p->ldg, 2);
+      p->add_buf("FDG", R * p->ldg, 2);   p->add_buf("FDP1", R * h1, 2);
+      p->add_buf("FDXW1", R * h1, 2);     p->add_buf("FDP0", R * h0, 2);
+      const int rcb = rc_blocks(p->R);
+      p->add_buf("PFENC1", (long long)rcb * 4 * W);
+      p->add_buf("PFENC0", (long long)rcb * 2 * h0);
+      p->gW1 = wgrad_geom(p->R, 1, h0 + f, h1);
+      p->gW0 = wgrad_geom(p->R, 1, f, h0);
+      p->add_buf("FSW1", (long long)p->gW1.gx * (h0 + f) * wgrad_n4(h1));
+      p->add_buf("FSW0", (long long)p->gW0.gx * f * wgrad_n4(h0));
     }
   }
   // ---- bf16 fast encoder: GraphConvolution 0 as (A X) W0, bf16 operands throughout
@@ -528,8 +561,15 @@ int pack_decoder(const Ctx& x) {
   PackDesc e[12]{};
   for (int i = 0; i < 6; ++i) e[i] = d[i];
   const int f = c.f_in, h0 = c.h0, h1 = c.h1, gh = c.g_hidden, W = p.W;
-  const float *W1 = x.w("enc.W1"), *Wh = x.w("enc.Wh"), *Wms = x.w("enc.Wms");
   auto one = [&](const Img& im, PackSrc ps) { return PackDesc{dst(im), 1, im.kp, im.np, 1, {ps, {}}}; };
+  if (p.tref) {
+    const float* W1 = x.w("enc.W1");
+    e[6] = one(p.pw1f, src(W1, h0 + f, h1, 0, h0 + f, 0, h1, 0, 0, 0));
+    e[7] = one(p.pw1b, src(W1, h0 + f, h1, 0, h0, 0, h1, 0, 0, 1));
+    e[8] = one(p.pidg, src(nullptr, W, W, 0, W, 0, W, 0, 0, 2));
+    return launch_pack(e, 9, x.s);
+  }
+  const float *W1 = x.w("enc.W1"), *Wh = x.w("enc.Wh"), *Wms = x.w("enc.Wms");
   e[6] = one(p.pw1f, src(W1, h0 + f, h1, 0, h0 + f, 0, h1, 0, 0, 0));
   e[7] = one(p.pwhf, src(Wh, W, gh, 0, W, 0, gh, 0, 0, 0));
   e[8] = one(p.pwmsf, src(Wms, gh, 2 * L, 0, gh, 0, 2 * L, 0, 0, 0));
@@ -564,6 +604,7 @@ int encoder_fast_fwd(const Ctx& x, const snd_batch_t* batch) {
     a.row_order = batch->row_order;
     SND_TRY(launch_spmm_bf16(a, x.s));
   }
+  if (p.tref) return 0;   // graph heads: snd_tref.hip on bf16 flat(G)
   {
     RcArgs a = rc_args(p, x.ws, p.pwhf, bf("FG"), p.ldg, W, gh, colmap_plain(gh));
     a.bias = x.w("enc.bh"); a.out = bf("FHH"); a.ldo = gh; a.out_bf16 = 1;
@@ -576,6 +617,8 @@ int encoder_fast_fwd(const Ctx& x, const snd_batch_t* batch) {
   }
   return 0;
 }
+
+int encoder_fast_bwd_tail(const Ctx& x, const snd_batch_t* batch);
 
 // encoder backward: reparam -> heads -> GCN1 -> GCN0 (all weight gradients as slabs)
 int encoder_fast_bwd(const Ctx& x, const snd_batch_t* batch, float adj_scale, float kl_scale) {
@@ -597,8 +640,20 @@ int encoder_fast_bwd(const Ctx& x, const snd_batch_t* batch, float adj_scale, fl
   }
   SND_TRY(fork(x));
   SND_TRY(launch_wgrad(wg_args(p, x.ws, p.gWh, bf("FG"), p.ldg, W, bf("FDH"), gh, gh, x.f("FSWH"), 1), side(x)));
+  return encoder_fast_bwd_tail(x, batch);
+}
+
+// encoder backward from dG: BN/lrelu backward (RC_ENC1 epilogue) -> GCN1 -> GCN0.
+// Node latent: dG = dH Wh^T is the RC_ENC1 GEMM itself; graph latent: dG (bf16,
+// from tref_head_bwd) passes through an identity image.
+int encoder_fast_bwd_tail(const Ctx& x, const snd_batch_t* batch) {
+  const snd_plan& p = *x.p;
+  const snd_config_t& c = p.c;
+  const int R = p.R, f = c.f_in, h0 = c.h0, h1 = c.h1, gh = c.g_hidden, W = p.W;
+  auto bf = [&](const char* n) { return reinterpret_cast<__bf16*>(x.f(n)); };
   {
-    RcArgs a = rc_args(p, x.ws, p.pwhb, bf("FDH"), gh, gh, W, colmap_plain(W));
+    RcArgs a = p.tref ? rc_args(p, x.ws, p.pidg, bf("FDG"), p.ldg, W, W, colmap_plain(W))
+                      : rc_args(p, x.ws, p.pwhb, bf("FDH"), gh, gh, W, colmap_plain(W));
     a.gamma = x.w("enc.bne.gamma"); a.g2 = x.w("enc.bn1.gamma"); a.b2 = x.w("enc.bn1.beta");
     a.p = x.f("FP1"); a.ldp = h1; a.xf = batch->features; a.ldxf = f; a.f = f; a.h = h1;
     a.out = bf("FDP1"); a.ldo = h1; a.out_bf16 = 1; a.colpart = x.f("PFENC1"); a.ncp = 4;
@@ -634,10 +689,12 @@ void encoder_fast_reduce(const Ctx& x, std::vector<ReduceDesc>& rd) {
     const int n4 = wgrad_n4(N);
     rd.push_back({x.f(buf), x.g(dst), parts, N, (long long)rows * n4, 1.f, 0, rows, n4, N});
   };
-  slab2d("FSWMS", p.gWms.gx, gh, 2 * L, "enc.Wms");
-  flat("PFBMS", reparam_bwd_fast_blocks(p.R, L), 2 * L, 2 * L, "enc.bms", 1.f);
-  slab2d("FSWH", p.gWh.gx, W, gh, "enc.Wh");
-  flat("PFBH", rcb, gh, gh, "enc.bh", 1.f);
+  if (!p.tref) {   // graph-latent heads are reduced by the generic path / written directly
+    slab2d("FSWMS", p.gWms.gx, gh, 2 * L, "enc.Wms");
+    flat("PFBMS", reparam_bwd_fast_blocks(p.R, L), 2 * L, 2 * L, "enc.bms", 1.f);
+    slab2d("FSWH", p.gWh.gx, W, gh, "enc.Wh");
+    flat("PFBH", rcb, gh, gh, "enc.bh", 1.f);
+  }
   slab2d("FSW1", p.gW1.gx, h0 + f, h1, "enc.W1");
   slab2d("FSW0", p.gW0.gx, f, h0, "enc.W0");
   const float* e1 = x.f("PFENC1");
@@ -819,12 +876,16 @@ extern "C" int snd_plan_launch(const snd_plan_t* plan, const snd_batch_t* batch,
     const snd_config_t& c = p.c;
     const long long KH = (long long)p.N * p.W, CP = (long long)p.N * p.dj;
     const float adj_scale = (float)(2.0 * (double)c.norm / ((double)p.B * p.N * (double)p.N));
+    const __bf16* gb = p.fast_enc ? reinterpret_cast<const __bf16*>(x.f("FG")) : nullptr;
     if (!strcmp(kernel, "tref_head_fwd")) {
-      TrefHeadFwdArgs a{x.f("G"), KH, p.B, x.w("enc.Wh"), c.g_hidden, x.w("enc.bh"), x.f("PHF")};
+      TrefHeadFwdArgs a{gb ? nullptr : x.f("G"), KH, p.B, x.w("enc.Wh"), c.g_hidden, x.w("enc.bh"),
+                        x.f("PHF"), gb, p.ldg, p.W, p.N};
       return launch_tref_head_fwd(a, s);
     }
     if (!strcmp(kernel, "tref_head_bwd")) {
-      TrefHeadBwdArgs a{x.f("G"), KH, p.B, x.w("enc.Wh"), c.g_hidden, x.f("DH"), x.g("enc.Wh"), x.f("DG")};
+      TrefHeadBwdArgs a{gb ? nullptr : x.f("G"), KH, p.B, x.w("enc.Wh"), c.g_hidden, x.f("DH"),
+                        x.g("enc.Wh"), gb ? nullptr : x.f("DG"), gb, p.ldg, p.W, p.N,
+                        gb ? reinterpret_cast<__bf16*>(x.f("FDG")) : nullptr};
       return launch_tref_head_bwd(a, s);
     }
     if (!strcmp(kernel, "tref_proj_fwd")) {
@@ -916,6 +977,16 @@ extern "C" int snd_train_step(const snd_plan_t* plan, const snd_batch_t* batch,
                        x.w("enc.bh")));
     }
     // [mu || s] = h Wms + bms (model.py:114-115)
+    SND_TRY(gemm_fwd(x, RH, 2 * L, gh, x.f("Hh"), gh, x.w("enc.Wms"), 2 * L, B_ROW, x.f("MS"), 2 * L,
+                     x.w("enc.bms")));
+  }
+  if (p.fast_enc && p.tref) {   // graph heads on the fast encoder's bf16 G
+    TrefHeadFwdArgs a{nullptr, KH, p.B, x.w("enc.Wh"), gh, x.w("enc.bh"), x.f("PHF"),
+                      reinterpret_cast<const __bf16*>(x.f("FG")), p.ldg, W, N};
+    SND_TRY(launch_tref_head_fwd(a, x.s));
+    const ReduceDesc rd{x.f("PHF"), x.f("Hh"), tref_head_fwd_blocks(KH, gh), RH * gh,
+                        (long long)RH * gh, 1.f, 0, 0, 0, 0};
+    SND_TRY(launch_reduce(&rd, 1, x.s));
     SND_TRY(gemm_fwd(x, RH, 2 * L, gh, x.f("Hh"), gh, x.w("enc.Wms"), 2 * L, B_ROW, x.f("MS"), 2 * L,
                      x.w("enc.bms")));
   }
@@ -1023,7 +1094,7 @@ extern "C" int snd_train_step(const snd_plan_t* plan, const snd_batch_t* batch,
   const float adj_scale = (float)(2.0 * (double)c.norm / pairs);
   const float kl_scale = (float)((double)c.beta / ((double)RH * L));
   SND_TRY(wait_mark(x, edge_mark));   // EJ
-  if (p.fast_enc) {
+  if (p.fast_enc && !p.tref) {
     SND_TRY(encoder_fast_bwd(x, batch, adj_scale, kl_scale));
   } else {
     if (p.tref) {
@@ -1048,11 +1119,20 @@ extern "C" int snd_train_step(const snd_plan_t* plan, const snd_batch_t* batch,
                      nullptr));
     if (p.tref) {   // dWh written complete; dG = dh Wh^T per graph
       TrefHeadBwdArgs a{x.f("G"), KH, p.B, x.w("enc.Wh"), gh, x.f("DH"), x.g("enc.Wh"), x.f("DG")};
+      if (p.fast_enc) {   // bf16 G in, bf16 dG rows out (the fast encoder's operands)
+        a.g = nullptr; a.dg = nullptr;
+        a.gb = reinterpret_cast<const __bf16*>(x.f("FG")); a.ldg = p.ldg; a.W = W; a.npg = N;
+        a.dgb = reinterpret_cast<__bf16*>(x.f("FDG"));
+      }
       SND_TRY(launch_tref_head_bwd(a, x.s));
     } else {
       SND_TRY(gemm_wgrad(x, x.f("G"), W, W, true, x.f("DH"), gh, gh, x.f("SWH"), p.sWh));
       SND_TRY(gemm_fwd(x, R, W, gh, x.f("DH"), gh, x.w("enc.Wh"), gh, B_COL, x.f("DG"), W, nullptr));
     }
+  }
+  if (p.fast_enc && p.tref) {
+    SND_TRY(encoder_fast_bwd_tail(x, batch));
+  } else if (!p.fast_enc) {
     {
       EncBwdArgs a{x.f("DG"), W, x.f("H2"), W, x.w("enc.bne.gamma"), W, x.f("P1"), h1,
                    x.w("enc.bn1.gamma"), h1, x.f("DP1"), h1, x.f("PENC1"), 1};
@@ -1093,12 +1173,11 @@ extern "C" int snd_train_step(const snd_plan_t* plan, const snd_batch_t* batch,
   } else {
     slab("SW0", p.sW0, f, h0, "enc.W0", f * h0, nullptr);
     slab("SW1", p.sW1, h0 + f, h1, "enc.W1", (h0 + f) * h1, nullptr);
-    if (p.tref)   // dbh = sum over graphs of dh
-      rd.push_back({x.f("DH"), x.g("enc.bh"), RH, gh, (long long)gh, 1.f, 0});
-    else
-      slab("SWH", p.sWh, W + 1, gh, "enc.Wh", W * gh, "enc.bh");
-    slab("SWMS", p.sWms, gh + 1, 2 * L, "enc.Wms", gh * 2 * L, "enc.bms");
+    if (!p.tref) slab("SWH", p.sWh, W + 1, gh, "enc.Wh", W * gh, "enc.bh");
   }
+  if (p.tref)   // dbh = sum over graphs of dh
+    rd.push_back({x.f("DH"), x.g("enc.bh"), RH, gh, (long long)gh, 1.f, 0});
+  if (!p.fast_enc || p.tref) slab("SWMS", p.sWms, gh + 1, 2 * L, "enc.Wms", gh * 2 * L, "enc.bms");
   if (!p.fast) {
     slab("SK1", p.sK1, 5 * dj, C1, "dec.K1", 5 * dj * C1, nullptr);
     slab("SK2S", p.sK2s, 5 * s1, s2, "dec.K2s", 5 * s1 * s2, nullptr);

@@ -39,6 +39,16 @@ __device__ __forceinline__ float dot4(const float4& a, const float4& b) {
   return fmaf(a.x, b.x, fmaf(a.y, b.y, fmaf(a.z, b.z, a.w * b.w)));
 }
 
+// element (b, k) of flat(G): fp32 [B, K] or the fast encoder's bf16 node rows
+template <typename A>
+__device__ __forceinline__ float g_at(const A& a, int b, long long k) {
+  if (a.gb) {
+    const long long n = k / a.W;
+    return (float)a.gb[((long long)b * a.npg + n) * a.ldg + (k - n * a.W)];
+  }
+  return a.g[(long long)b * a.K + k];
+}
+
 // ------------------------------------------------------------------ head fwd
 constexpr int HF_T = 256;
 
@@ -51,7 +61,7 @@ __global__ void __launch_bounds__(HF_T) tref_head_fwd_kernel(TrefHeadFwdArgs a, 
   // G[b, k0 .. k0+nk) -> gs[kk][8] (coalesced per graph)
   for (int b = 0; b < B8; ++b)
     for (int kk = t; kk < nk; kk += HF_T)
-      sm[kk * B8 + b] = b < a.B ? a.g[(long long)b * a.K + k0 + kk] : 0.f;
+      sm[kk * B8 + b] = b < a.B ? g_at(a, b, k0 + kk) : 0.f;
   __syncthreads();
   float4 acc[B8];
 #pragma unroll
@@ -126,7 +136,7 @@ __global__ void __launch_bounds__(HB_T) tref_head_bwd_kernel(TrefHeadBwdArgs a) 
   const int nk = (int)std::min<long long>(HB_RPB, a.K - k0);
   for (int b = 0; b < B8; ++b)
     for (int kk = t; kk < nk; kk += HB_T)
-      gs[kk * B8 + b] = b < a.B ? a.g[(long long)b * a.K + k0 + kk] : 0.f;
+      gs[kk * B8 + b] = b < a.B ? g_at(a, b, k0 + kk) : 0.f;
   float4 dh[B8];
 #pragma unroll
   for (int b = 0; b < B8; ++b)
@@ -167,7 +177,15 @@ __global__ void __launch_bounds__(HB_T) tref_head_bwd_kernel(TrefHeadBwdArgs a) 
   }
   __syncthreads();
   for (int b = 0; b < a.B; ++b)
-    for (int kk = t; kk < nk; kk += HB_T) a.dg[(long long)b * a.K + k0 + kk] = dgs[b * HB_RPB + kk];
+    for (int kk = t; kk < nk; kk += HB_T) {
+      const long long k = k0 + kk;
+      if (a.dgb) {
+        const long long n = k / a.W;
+        a.dgb[((long long)b * a.npg + n) * a.ldg + (k - n * a.W)] = (__bf16)dgs[b * HB_RPB + kk];
+      } else {
+        a.dg[(long long)b * a.K + k] = dgs[b * HB_RPB + kk];
+      }
+    }
 }
 
 // ------------------------------------------------------------------ proj fwd
@@ -317,7 +335,8 @@ int tref_head_fwd_blocks(long long K, int gh) { return cdiv(K, head_fwd_rpb(K, g
 int launch_tref_head_fwd(const TrefHeadFwdArgs& a, hipStream_t s) {
   SND_CHECK_ARG(a.B >= 1 && a.B <= B8 && a.gh % 4 == 0 && a.gh >= 4 && a.gh <= 128 && a.K > 0,
                 "tref_head_fwd: B in 1..8, g_hidden %% 4 in 4..128");
-  SND_CHECK_ARG(a.g && a.wh && a.bh && a.slab, "tref_head_fwd: null operand");
+  SND_CHECK_ARG((a.g || (a.gb && a.W > 0 && a.npg > 0 && a.ldg >= a.W && (long long)a.W * a.npg == a.K)) &&
+                    a.wh && a.bh && a.slab, "tref_head_fwd: null operand / bf16 G geometry");
   const int rpb = head_fwd_rpb(a.K, a.gh);
   const int RPI = HF_T / (a.gh / 4);
   const size_t lds = sizeof(float) * std::max<size_t>((size_t)rpb * B8, (size_t)RPI * B8 * a.gh);
@@ -330,7 +349,9 @@ int launch_tref_head_fwd(const TrefHeadFwdArgs& a, hipStream_t s) {
 int launch_tref_head_bwd(const TrefHeadBwdArgs& a, hipStream_t s) {
   SND_CHECK_ARG(a.B >= 1 && a.B <= B8 && a.gh % 4 == 0 && a.gh >= 4 && a.gh <= 128 && a.K > 0,
                 "tref_head_bwd: B in 1..8, g_hidden %% 4 in 4..128");
-  SND_CHECK_ARG(a.g && a.wh && a.dh && a.dwh && a.dg, "tref_head_bwd: null operand");
+  SND_CHECK_ARG((a.g || (a.gb && a.W > 0 && a.npg > 0 && a.ldg >= a.W && (long long)a.W * a.npg == a.K)) &&
+                    a.wh && a.dh && a.dwh && (a.dg || (a.dgb && a.gb)),
+                "tref_head_bwd: null operand / bf16 G geometry");
   hipLaunchKernelGGL(tref_head_bwd_kernel, dim3(cdiv(a.K, HB_RPB)), dim3(HB_T), 0, s, a);
   SND_LAUNCH_CHECK("tref_head_bwd_kernel");
   return 0;

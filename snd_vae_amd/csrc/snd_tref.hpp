@@ -15,6 +15,9 @@ struct TrefHeadFwdArgs {
   const float* g; long long K; int B;
   const float* wh; int gh; const float* bh;
   float* slab;
+  // bf16 G of the fast encoder instead of g: node rows of width W at leading dim ldg
+  // (flat index k = n * W + c -> gb[(b * npg + n) * ldg + c])
+  const __bf16* gb; int ldg; int W; int npg;
 };
 int tref_head_fwd_blocks(long long K, int gh);
 int launch_tref_head_fwd(const TrefHeadFwdArgs& a, hipStream_t s);
@@ -26,7 +29,8 @@ struct TrefHeadBwdArgs {
   const float* wh; int gh;
   const float* dh;            // [B, gh]
   float* dwh;                 // [K, gh]
-  float* dg;                  // [B, K]
+  float* dg;                  // [B, K]   (or, with gb, bf16 rows dgb[(b * npg + n) * ldg + c])
+  const __bf16* gb; int ldg; int W; int npg; __bf16* dgb;
 };
 int launch_tref_head_bwd(const TrefHeadBwdArgs& a, hipStream_t s);
 
