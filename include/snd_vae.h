@@ -224,6 +224,16 @@ int snd_plan_num_blocks(const snd_plan_t* plan);
 int snd_plan_param_block(const snd_plan_t* plan, int idx, const char** name,
                          long long* offset, long long* numel);
 size_t snd_plan_workspace_bytes(const snd_plan_t* plan);
+/* Fused TF1 Adam (1 GPU: no all-reduce between gradient and update).  With m and
+ * v set (flat buffers in the parameter layout), snd_train_step applies the Adam
+ * update of optimizer.py:125,197 to the blocks snd_plan_block_fused() reports (the
+ * graph-latent head and d_sg_lin1 weights, whose gradients are produced complete
+ * by one kernel) in place, through the params pointer, and does not write their
+ * gradient; the caller's snd_adam_tf1 then covers the other blocks.  m = v = NULL
+ * turns it off (default).  lr/betas/eps as snd_adam_tf1; grad_scale is 1. */
+int snd_plan_fuse_adam(snd_plan_t* plan, float* m, float* v, float lr, float beta1,
+                       float beta2, float eps);
+int snd_plan_block_fused(const snd_plan_t* plan, int idx);
 /* Named intermediate buffers inside the workspace (tests / inspection). */
 int snd_plan_buffer(const snd_plan_t* plan, const char* name,
                     long long* byte_offset, long long* numel);

@@ -75,6 +75,8 @@ _SIGS = {
     "snd_plan_param_block": (c_int, [vp, c_int, C.POINTER(C.c_char_p), C.POINTER(c_ll),
                                      C.POINTER(c_ll)]),
     "snd_plan_workspace_bytes": (c_size, [vp]),
+    "snd_plan_fuse_adam": (c_int, [vp, vp, vp, c_float, c_float, c_float, c_float]),
+    "snd_plan_block_fused": (c_int, [vp, c_int]),
     "snd_plan_buffer": (c_int, [vp, C.c_char_p, C.POINTER(c_ll), C.POINTER(c_ll)]),
     "snd_train_step": (c_int, [vp, C.POINTER(Batch), vp, vp, vp, vp, c_ull, vp, vp, vp]),
     "snd_plan_launch": (c_int, [vp, C.POINTER(Batch), vp, C.c_char_p, vp]),

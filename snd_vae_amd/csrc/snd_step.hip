@@ -86,6 +86,12 @@ struct snd_plan {
   Img pw1f{}, pwhf{}, pwmsf{}, pwmsb{}, pwhb{}, pw1b{};
   Img pidg{};                  // graph latent: identity [W -> W] (dG enters RC_ENC1 directly)
   WgGeom gWms{}, gWh{}, gW1{}, gW0{};
+  // fused TF1 Adam (snd_plan_fuse_adam): Adam state of the blocks updated inside the step
+  float* fuse_m = nullptr; float* fuse_v = nullptr;
+  float fuse_lr = 0.f, fuse_b1 = 0.f, fuse_b2 = 0.f, fuse_eps = 0.f;
+  bool block_fused(const std::string& n) const {
+    return fuse_m && tref && (n == "enc.Wh" || n == "dec.Wp");
+  }
   // parameters of the last snd_train_step (snd_plan_launch re-runs kernels on them)
   mutable const float* last_params = nullptr;
   mutable float* last_grads = nullptr;
@@ -379,6 +385,19 @@ extern "C" int snd_plan_param_block(const snd_plan_t* p, int idx, const char** n
   return 0;
 }
 extern "C" size_t snd_plan_workspace_bytes(const snd_plan_t* p) { return p ? (size_t)p->ws : 0; }
+
+extern "C" int snd_plan_fuse_adam(snd_plan_t* p, float* m, float* v, float lr, float beta1,
+                                  float beta2, float eps) {
+  SND_CHECK_ARG(p && ((m && v) || (!m && !v)), "snd_plan_fuse_adam: bad args");
+  p->fuse_m = m; p->fuse_v = v;
+  p->fuse_lr = lr; p->fuse_b1 = beta1; p->fuse_b2 = beta2; p->fuse_eps = eps;
+  return 0;
+}
+
+extern "C" int snd_plan_block_fused(const snd_plan_t* p, int idx) {
+  SND_CHECK_ARG(p && idx >= 0 && idx < (int)p->blocks.size(), "snd_plan_block_fused: bad index");
+  return p->block_fused(p->blocks[idx].name) ? 1 : 0;
+}
 extern "C" int snd_plan_buffer(const snd_plan_t* p, const char* name, long long* off,
                                long long* numel) {
   SND_CHECK_ARG(p && name, "snd_plan_buffer: bad args");
@@ -407,6 +426,15 @@ struct Ctx {
   const float* w(const char* n) const { return P + p->blk(n); }
   float* g(const char* n) const { return Gr + p->blk(n); }
 };
+
+// Adam state of a block updated inside the step (snd_plan_fuse_adam); params are
+// written in place through the (caller-owned, writable) parameter buffer
+AdamFuse fused_adam(const Ctx& x, const char* blk, const int* step) {
+  const snd_plan& p = *x.p;
+  const long long o = p.blk(blk);
+  return AdamFuse{const_cast<float*>(x.P) + o, p.fuse_m + o, p.fuse_v + o,
+                  p.fuse_lr, p.fuse_b1, p.fuse_b2, p.fuse_eps, step};
+}
 
 // fork: work launched on side() after this point starts after everything so far on main
 int fork(const Ctx& x) {
@@ -1101,6 +1129,7 @@ extern "C" int snd_train_step(const snd_plan_t* plan, const snd_batch_t* batch,
       {   // d_sg_lin1 backward: dWp, dbp written; dz partials per block
         TrefProjBwdArgs a{x.f("ZL"), p.B, L, x.w("dec.Wp"), CP, x.f("DZDEC"), x.f("DJD"), x.f("EJ"),
                           adj_scale, x.g("dec.Wp"), x.g("dec.bp"), x.f("PDZ")};
+        if (p.block_fused("dec.Wp")) a.adam = fused_adam(x, "dec.Wp", step_counter);
         SND_TRY(launch_tref_proj_bwd(a, x.s));
         const ReduceDesc rd{x.f("PDZ"), x.f("DZL"), tref_proj_bwd_blocks(CP), RH * L,
                             (long long)RH * L, 1.f, 0, 0, 0, 0};
@@ -1124,6 +1153,7 @@ extern "C" int snd_train_step(const snd_plan_t* plan, const snd_batch_t* batch,
         a.gb = reinterpret_cast<const __bf16*>(x.f("FG")); a.ldg = p.ldg; a.W = W; a.npg = N;
         a.dgb = reinterpret_cast<__bf16*>(x.f("FDG"));
       }
+      if (p.block_fused("enc.Wh")) a.adam = fused_adam(x, "enc.Wh", step_counter);
       SND_TRY(launch_tref_head_bwd(a, x.s));
     } else {
       SND_TRY(gemm_wgrad(x, x.f("G"), W, W, true, x.f("DH"), gh, gh, x.f("SWH"), p.sWh));

@@ -49,6 +49,25 @@ __device__ __forceinline__ float g_at(const A& a, int b, long long k) {
   return a.g[(long long)b * a.K + k];
 }
 
+// fused TF1 Adam on 4 consecutive elements; g is the (complete) gradient
+__device__ __forceinline__ float adam_lrt(const AdamFuse& f) {
+  const int t = *f.step + 1;
+  return (float)((double)f.lr * sqrt(1.0 - pow((double)f.b2, t)) / (1.0 - pow((double)f.b1, t)));
+}
+__device__ __forceinline__ void adam4(const AdamFuse& f, float lrt, long long i, const float4& g,
+                                      float4 p) {   // p: the parameters as already loaded
+  float4 m = *reinterpret_cast<const float4*>(f.m + i), v = *reinterpret_cast<const float4*>(f.v + i);
+#define SND_ADAM_C(c)                                        \
+  m.c = f.b1 * m.c + (1.f - f.b1) * g.c;                     \
+  v.c = f.b2 * v.c + (1.f - f.b2) * g.c * g.c;               \
+  p.c -= lrt * m.c / (sqrtf(v.c) + f.eps);
+  SND_ADAM_C(x) SND_ADAM_C(y) SND_ADAM_C(z) SND_ADAM_C(w)
+#undef SND_ADAM_C
+  *reinterpret_cast<float4*>(f.m + i) = m;
+  *reinterpret_cast<float4*>(f.v + i) = v;
+  *reinterpret_cast<float4*>(f.p + i) = p;
+}
+
 // ------------------------------------------------------------------ head fwd
 constexpr int HF_T = 256;
 
@@ -142,6 +161,8 @@ __global__ void __launch_bounds__(HB_T) tref_head_bwd_kernel(TrefHeadBwdArgs a) 
   for (int b = 0; b < B8; ++b)
     dh[b] = (qa && b < a.B) ? *reinterpret_cast<const float4*>(a.dh + b * a.gh + 4 * q) : f4(0.f);
   __syncthreads();
+  const bool fused = a.adam.p != nullptr;
+  const float lrt = fused ? adam_lrt(a.adam) : 0.f;
   constexpr int U = 4;                   // row pairs in flight per wave
   const int r0 = 2 * wv + h;             // row slot of this lane; 8 rows per block pass
   for (int base = 0; base < nk; base += 8 * U) {
@@ -163,7 +184,10 @@ __global__ void __launch_bounds__(HB_T) tref_head_bwd_kernel(TrefHeadBwdArgs a) 
       float4 dw = f4(0.f);
 #pragma unroll
       for (int b = 0; b < B8; ++b) fma4(dw, gb[b], dh[b]);
-      if (qa && rv) *reinterpret_cast<float4*>(a.dwh + (k0 + kk) * a.gh + 4 * q) = dw;
+      if (qa && rv) {
+        if (fused) adam4(a.adam, lrt, (k0 + kk) * a.gh + 4 * q, dw, w[u]);
+        else *reinterpret_cast<float4*>(a.dwh + (k0 + kk) * a.gh + 4 * q) = dw;
+      }
       float p[B8];
 #pragma unroll
       for (int b = 0; b < B8; ++b) {
@@ -268,6 +292,8 @@ __global__ void __launch_bounds__(PB_T) tref_proj_bwd_kernel(TrefProjBwdArgs a) 
     *reinterpret_cast<float4*>(a.dbp + c4) = s;
   }
   __syncthreads();
+  const bool fused = a.adam.p != nullptr;
+  const float lrt = fused ? adam_lrt(a.adam) : 0.f;
   constexpr int U = 5;
   for (int l0 = wv; l0 < a.L; l0 += PB_W * U) {
     float4 w[U];
@@ -285,7 +311,10 @@ __global__ void __launch_bounds__(PB_T) tref_proj_bwd_kernel(TrefProjBwdArgs a) 
       float4 dw = f4(0.f);
       fma4(dw, z0.x, d[0]); fma4(dw, z0.y, d[1]); fma4(dw, z0.z, d[2]); fma4(dw, z0.w, d[3]);
       fma4(dw, z1.x, d[4]); fma4(dw, z1.y, d[5]); fma4(dw, z1.z, d[6]); fma4(dw, z1.w, d[7]);
-      if (cv) *reinterpret_cast<float4*>(a.dwp + (long long)l * a.Cp + c4) = dw;
+      if (cv) {
+        if (fused) adam4(a.adam, lrt, (long long)l * a.Cp + c4, dw, w[u]);
+        else *reinterpret_cast<float4*>(a.dwp + (long long)l * a.Cp + c4) = dw;
+      }
 #pragma unroll
       for (int b = 0; b < B8; ++b) {
         float p = row16_sum(dot4(d[b], w[u]));
@@ -350,8 +379,10 @@ int launch_tref_head_bwd(const TrefHeadBwdArgs& a, hipStream_t s) {
   SND_CHECK_ARG(a.B >= 1 && a.B <= B8 && a.gh % 4 == 0 && a.gh >= 4 && a.gh <= 128 && a.K > 0,
                 "tref_head_bwd: B in 1..8, g_hidden %% 4 in 4..128");
   SND_CHECK_ARG((a.g || (a.gb && a.W > 0 && a.npg > 0 && a.ldg >= a.W && (long long)a.W * a.npg == a.K)) &&
-                    a.wh && a.dh && a.dwh && (a.dg || (a.dgb && a.gb)),
+                    a.wh && a.dh && (a.dwh || a.adam.p) && (a.dg || (a.dgb && a.gb)),
                 "tref_head_bwd: null operand / bf16 G geometry");
+  SND_CHECK_ARG(!a.adam.p || (a.adam.m && a.adam.v && a.adam.step && a.adam.p == a.wh),
+                "tref_head_bwd: fused Adam needs m, v, step and p == wh");
   hipLaunchKernelGGL(tref_head_bwd_kernel, dim3(cdiv(a.K, HB_RPB)), dim3(HB_T), 0, s, a);
   SND_LAUNCH_CHECK("tref_head_bwd_kernel");
   return 0;
@@ -371,8 +402,10 @@ int tref_proj_bwd_blocks(long long Cp) { return cdiv(Cp, 256); }
 int launch_tref_proj_bwd(const TrefProjBwdArgs& a, hipStream_t s) {
   SND_CHECK_ARG(a.B >= 1 && a.B <= B8 && a.L >= 1 && a.L <= 128 && a.Cp % 4 == 0 && a.Cp > 0,
                 "tref_proj_bwd: B in 1..8, L <= 128, Cp %% 4");
-  SND_CHECK_ARG(a.z && a.wp && a.dz_dec && a.dJd && a.ej && a.dwp && a.dbp && a.slab,
+  SND_CHECK_ARG(a.z && a.wp && a.dz_dec && a.dJd && a.ej && (a.dwp || a.adam.p) && a.dbp && a.slab,
                 "tref_proj_bwd: null operand");
+  SND_CHECK_ARG(!a.adam.p || (a.adam.m && a.adam.v && a.adam.step && a.adam.p == a.wp),
+                "tref_proj_bwd: fused Adam needs m, v, step and p == wp");
   hipLaunchKernelGGL(tref_proj_bwd_kernel, dim3(tref_proj_bwd_blocks(a.Cp)), dim3(PB_T), 0, s, a);
   SND_LAUNCH_CHECK("tref_proj_bwd_kernel");
   return 0;

@@ -8,6 +8,15 @@ namespace snd {
 // per launch; every kernel reads its weight matrix exactly once (HBM-bound).
 constexpr int kTrefMaxB = 8;
 
+// TF1 Adam applied where a weight gradient is produced complete (1 GPU: no
+// all-reduce between gradient and update).  The step counter is read before the
+// step's finalize advances it, so the update uses t = *step + 1 (optimizer.py:125).
+struct AdamFuse {
+  float* p; float* m; float* v;   // block base of params / Adam state (same layout)
+  float lr, b1, b2, eps;
+  const int* step;
+};
+
 // h[b, j] = sum_k G[b, k] Wh[k, j] (+ bh[j] in block 0): split-K partial slab
 // [blocks][B][gh]; reduce over blocks gives h.  G [B, K] contiguous per graph
 // (the row-major tf.reshape of [N, W] node rows, model.py:113).
@@ -31,6 +40,7 @@ struct TrefHeadBwdArgs {
   float* dwh;                 // [K, gh]
   float* dg;                  // [B, K]   (or, with gb, bf16 rows dgb[(b * npg + n) * ldg + c])
   const __bf16* gb; int ldg; int W; int npg; __bf16* dgb;
+  AdamFuse adam;              // adam.p != null: update Wh in place instead of writing dwh
 };
 int launch_tref_head_bwd(const TrefHeadBwdArgs& a, hipStream_t s);
 
@@ -51,6 +61,7 @@ struct TrefProjBwdArgs {
   const float* dz_dec; const float* dJd; const float* ej; float adj_scale;
   float* dwp; float* dbp;
   float* slab;
+  AdamFuse adam;              // adam.p != null: update Wp in place instead of writing dwp
 };
 int tref_proj_bwd_blocks(long long Cp);
 int launch_tref_proj_bwd(const TrefProjBwdArgs& a, hipStream_t s);

@@ -30,7 +30,11 @@ LOSS_NAMES = ("cost", "spatial_cost", "adj_cost", "node_cost", "kl", "acc", "adj
 class OptimizerVAE:
     def __init__(self, model: SGCNModelVAE, learning_rate: Optional[float] = None,
                  beta1: Optional[float] = None, beta2: Optional[float] = None,
-                 epsilon: Optional[float] = None, process_group=None, seed: int = 1234):
+                 epsilon: Optional[float] = None, process_group=None, seed: int = 1234,
+                 fuse_adam: Optional[bool] = None):
+        """fuse_adam (default: on for one process): blocks whose gradient one kernel
+        produces complete (graph-latent heads / d_sg_lin1) take their Adam update
+        inside the step (snd_plan_fuse_adam); their gradient is then not written."""
         cfg = model.cfg
         self.model = model
         self.lr = cfg.learning_rate if learning_rate is None else learning_rate
@@ -52,6 +56,29 @@ class OptimizerVAE:
             self.world = dist.get_world_size(process_group)
         self._graph = None
         self._batch_c = None
+        L = _lib.lib()
+        if fuse_adam is None:
+            fuse_adam = self.world == 1
+        if fuse_adam and self.world != 1:
+            raise ValueError("fused Adam needs the full gradient on one process (world 1)")
+        self.fused = bool(fuse_adam)
+        _lib.check(L.snd_plan_fuse_adam(
+            model.plan, _lib.ptr(self.m) if self.fused else None,
+            _lib.ptr(self.v) if self.fused else None, self.lr, self.beta1, self.beta2, self.eps),
+            "snd_plan_fuse_adam")
+        # contiguous [offset, count) ranges of the blocks snd_adam_tf1 still updates
+        self._adam_ranges = []
+        lay = model.layout
+        names = list(lay.shapes)
+        for i, k in enumerate(names):
+            if L.snd_plan_block_fused(model.plan, i):
+                continue
+            off = lay.offsets[k]
+            end = lay.offsets[names[i + 1]] if i + 1 < len(names) else model.param_count
+            if self._adam_ranges and self._adam_ranges[-1][0] + self._adam_ranges[-1][1] == off:
+                self._adam_ranges[-1][1] += end - off
+            else:
+                self._adam_ranges.append([off, end - off])
 
     # ------------------------------------------------------------------ step
     def forward_backward(self, batch: DeviceBatch, eps: Optional[torch.Tensor] = None,
@@ -71,10 +98,13 @@ class OptimizerVAE:
 
     def apply(self, stream=None):
         m = self.model
-        _lib.check(_lib.lib().snd_adam_tf1(
-            _lib.ptr(m.params), _lib.ptr(self.grads), _lib.ptr(self.m), _lib.ptr(self.v),
-            m.param_count, self.lr, self.beta1, self.beta2, self.eps, 1.0 / self.world,
-            _lib.ptr(self.step_counter), _lib.stream_ptr(stream)), "snd_adam_tf1")
+        for off, n in self._adam_ranges:
+            b = 4 * off
+            _lib.check(_lib.lib().snd_adam_tf1(
+                _lib.ptr(m.params) + b, _lib.ptr(self.grads) + b, _lib.ptr(self.m) + b,
+                _lib.ptr(self.v) + b, n, self.lr, self.beta1, self.beta2, self.eps,
+                1.0 / self.world, _lib.ptr(self.step_counter), _lib.stream_ptr(stream)),
+                "snd_adam_tf1")
 
     def step(self, batch: DeviceBatch, eps: Optional[torch.Tensor] = None):
         """One optimisation step (`main.py:331`): fwd+bwd, all-reduce, Adam."""
@@ -121,6 +151,7 @@ class OptimizerVAE:
         return int(self.step_counter.item())
 
     def grad_blocks(self):
+        """Flat gradient by block (fused-Adam blocks are updated in the step, not stored)."""
         m = self.model
         return m.layout.unpack(self.grads[:m.param_count].double().cpu().numpy())
 

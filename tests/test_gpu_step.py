@@ -29,11 +29,12 @@ def _gpu(lib_built):
 load_fixture = golden_io.load
 
 
-def make(cfg, batch, p0, dtype):
+def make(cfg, batch, p0, dtype, fuse_adam=False):
+    """fuse_adam off by default: the parity tests read every block's gradient back."""
     from snd_vae_amd.model import DeviceBatch, SGCNModelVAE
     from snd_vae_amd.optimizer import OptimizerVAE
     model = SGCNModelVAE(cfg, batch.n_graphs, dtype=dtype, blocks=p0)
-    return model, OptimizerVAE(model), DeviceBatch(batch)
+    return model, OptimizerVAE(model, fuse_adam=fuse_adam), DeviceBatch(batch)
 
 
 def block_err(g, ref):
@@ -132,6 +133,35 @@ def test_train_step_c4_size_vs_oracle(dtype, ltol, gtol):
     # decoder input J and the graph latent read back under the reference names
     assert model.joint_h.shape == (2 * 4096, 64) and model.z_sg.shape == (2, cfg.latent)
     assert model.z_mean_sg.shape == (2, cfg.latent)
+
+
+@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+def test_fused_adam_matches_separate_update(dtype):
+    """Graph-latent heads / d_sg_lin1 updated inside the step (snd_plan_fuse_adam)
+    give the parameters and Adam moments of the separate snd_adam_tf1 pass."""
+    from snd_vae_amd.params import init_blocks
+    cfg = tref(1024, 64)
+    batch = synthetic_batch(cfg, 2, seed=4)
+    p0 = init_blocks(cfg, 0)
+    runs = []
+    for fuse in (False, True):
+        m, o, b = make(cfg, batch, p0, dtype, fuse_adam=fuse)
+        for _ in range(3):
+            o.step(b)
+        torch.cuda.synchronize()
+        runs.append((m, o))
+    (m0, o0), (m1, o1) = runs
+    assert o1.fused and not o0.fused and o1.global_step == 3
+    for k in ("enc.Wh", "dec.Wp"):
+        assert k in m1.layout.shapes
+    p_a, p_b = m0.blocks(), m1.blocks()
+    for k in p_a:
+        # same gradients, same update formula: only rounding order may differ
+        d = np.abs(p_a[k] - p_b[k]).max()
+        assert d <= 1e-6 + 1e-5 * np.abs(p_a[k]).max(), (k, d)
+    for a, b in ((o0.m, o1.m), (o0.v, o1.v)):   # fma contraction may differ per kernel
+        assert float((a - b).abs().max()) <= 1e-5 * float(a.abs().max())
+    assert o0.loss_dict()["cost"] == pytest.approx(o1.loss_dict()["cost"], rel=1e-5)
 
 
 def test_device_rng_same_draw_on_both_engines():

@@ -30,7 +30,7 @@ def main():
             _lib.check(_lib.lib().snd_debug_set(flag))
             model = SGCNModelVAE(cfg, B, dtype="bf16", blocks=p0)
             _lib.check(_lib.lib().snd_debug_set(0))
-            opt = OptimizerVAE(model)
+            opt = OptimizerVAE(model, fuse_adam=False)
             opt.forward_backward(DeviceBatch(batch), torch.from_numpy(eps).cuda())
             torch.cuda.synchronize()
             g = opt.grad_blocks()
