@@ -241,6 +241,25 @@ int snd_train_step(const snd_plan_t* plan, const snd_batch_t* batch,
                    const float* params, float* grads, void* workspace,
                    const float* eps, unsigned long long seed,
                    int* step_counter, double* losses, snd_stream_t stream);
+/* Forward-only evaluation / sampling on the plan's shapes and dtype, generic
+ * kernels (main.py:358-469 generate_new / generate_new_train; model.py:163-169
+ * get_random_z).  mode:
+ *   SND_GEN_SAMPLE  encode `batch`, z = mu + eps exp(s) (eps_or_z = eps [RH, L]
+ *                   or NULL: device Philox at (seed, *step_counter)), as in training
+ *   SND_GEN_MEAN    encode `batch`, z = mu (z_mean_*, main.py:361,367)
+ *   SND_GEN_PRIOR   z ~ N(0, 1) (eps_or_z = eps or NULL: Philox); batch unused
+ *   SND_GEN_GIVEN   z = eps_or_z [RH, L]; batch unused
+ * RH = n_graphs (SND_TREF) or n_graphs * n_nodes (SND_TSCALE).  Results stay in
+ * the workspace (snd_plan_buffer): "MS" [mu || s], "Z" (node latent z / decoder
+ * input J), "ZL" (graph latent z), "SHAT" generated_spatial, "XHAT"
+ * generated_node_feat.  gen_adj (optional, uint8 [B, N, N]) receives
+ * generated_adj: 1 iff i != j and (J J^T)_ij > 0 (argmax of the 2-class logits,
+ * first index on ties, model.py:205-208).  Stream-ordered, no allocation;
+ * *step_counter is read, not advanced. */
+enum { SND_GEN_SAMPLE = 0, SND_GEN_MEAN = 1, SND_GEN_PRIOR = 2, SND_GEN_GIVEN = 3 };
+int snd_generate(const snd_plan_t* plan, const snd_batch_t* batch, const float* params,
+                 void* workspace, int mode, const float* eps_or_z, unsigned long long seed,
+                 const int* step_counter, unsigned char* gen_adj, snd_stream_t stream);
 /* Re-launch one kernel of the step on the workspace state left by the last
  * snd_train_step (measurement/profiling): "zzt_dense" (fused zz^T + CE),
  * "spmm_dxw1" (plain fp32 CSR SpMM, width h1; generic-engine plans),

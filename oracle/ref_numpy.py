@@ -279,6 +279,44 @@ def forward_backward(p: Dict[str, np.ndarray], adj, X, Xf, S, eps, cfg,
 
 
 # ----------------------------------------------------------------- TF1 Adam
+
+def generated_adj(J, n):
+    """model.py:205-208: argmax of softmax over (0, L_ij) off-diagonal, (1, 0) on it.
+
+    Returns (uint8 [B, N, N] predictions, float64 [B, N, N] logits L)."""
+    B = len(J) // n
+    Lg = np.stack([J[b * n:(b + 1) * n] @ J[b * n:(b + 1) * n].T for b in range(B)])
+    pred = (Lg > 0).astype(np.uint8)               # ties (L == 0) -> index 0
+    for b in range(B):
+        np.fill_diagonal(pred[b], 0)               # diag logits (1, 0) -> index 0
+    return pred, Lg
+
+
+def decode(p: Dict[str, np.ndarray], z, cfg):
+    """Decoder forward from a latent z (model.py:163-169 get_random_z + decoder;
+    model_joint.py:97,112-145): returns J, generated_spatial, generated_node_feat."""
+    n = cfg.n_nodes
+    c = BN_C
+    s1 = cfg.s_d_channel[0]
+    z = np.asarray(z, np.float64)
+    if cfg.topology == "tref":
+        B = z.shape[0]
+        J = (z @ p["dec.Wp"] + p["dec.bp"]).reshape(B * n, cfg.node_h_size)
+    else:
+        J = z
+    U1 = lrelu(per_graph_conv(J, p["dec.K1"], p["dec.b1"], n) * (p["dec.bn1.gamma"] * c)
+               + p["dec.bn1.beta"])
+    U2s = lrelu(per_graph_conv(U1[:, :s1], p["dec.K2s"], p["dec.b2s"], n)
+                * (p["dec.bn2s.gamma"] * c) + p["dec.bn2s.beta"])
+    U3s = lrelu(per_graph_conv(U2s, p["dec.K3s"], p["dec.b3s"], n)
+                * (p["dec.bn3s.gamma"] * c) + p["dec.bn3s.beta"])
+    Shat = sigmoid(U3s @ p["dec.Ws"] + p["dec.bs"])
+    U2n = lrelu(per_graph_conv(U1[:, s1:], p["dec.K2n"], p["dec.b2n"], n)
+                * (p["dec.bn2n.gamma"] * c) + p["dec.bn2n.beta"])
+    Xhat = sigmoid(U2n @ p["dec.Wn"] + p["dec.bn"])
+    return J, Shat, Xhat
+
+
 def adam_tf1(p, g, m, v, t, lr, b1=0.9, b2=0.999, eps=1e-8):
     """tf.train.AdamOptimizer.apply_gradients step t (1-based), in place."""
     lr_t = lr * np.sqrt(1.0 - b2 ** t) / (1.0 - b1 ** t)

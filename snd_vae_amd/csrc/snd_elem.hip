@@ -98,7 +98,7 @@ __global__ void __launch_bounds__(256) heads_kernel(HeadPack pk, int rows) {
       for (int k = 0; k < h.cin; ++k) zo += su[rr][k] * h.w[k * h.cout + o];
       const float y = 1.f / (1.f + __expf(-zo));
       if (h.yhat) h.yhat[(long long)r * h.cout + o] = y;
-      const float diff = y - h.target[(long long)r * h.ldt + o];
+      const float diff = y - (h.target ? h.target[(long long)r * h.ldt + o] : 0.f);
       sse += (double)diff * diff;
       dp[o] = 2.f * diff / h.count * y * (1.f - y);
     }

@@ -16,6 +16,7 @@
 #include <string>
 #include <vector>
 
+#include "snd_decode.hpp"
 #include "snd_elem.hpp"
 #include "snd_fast.hpp"
 #include "snd_gemm.hpp"
@@ -127,7 +128,7 @@ struct snd_plan {
 };
 
 extern "C" const char* snd_last_error(void) { return g_err; }
-extern "C" int snd_abi_version(void) { return 3; }
+extern "C" int snd_abi_version(void) { return 4; }
 
 extern "C" int snd_plan_create(const snd_config_t* cfg, int n_graphs, snd_plan_t** out) {
   SND_CHECK_ARG(cfg && out && n_graphs > 0, "snd_plan_create: bad args");
@@ -536,6 +537,51 @@ int conv_wgrad(const Ctx& x, const float* in, int ldi, int cin, const float* dy,
 }
 
 
+// generic-engine encoder forward (model.py:104-115): H_{i+1} = [BN(lrelu(A (H_i W_i))) || X],
+// G = BN_enc(H2), heads h and [mu || s] into MS (fp32 buffers, any plan)
+int encoder_generic_fwd(const Ctx& x, const snd_batch_t* batch) {
+  const snd_plan& p = *x.p;
+  const snd_config_t& c = p.c;
+  const int R = p.R, N = p.N, f = c.f_in, h0 = c.h0, h1 = c.h1, gh = c.g_hidden, L = c.latent;
+  const int W = p.W, RH = p.RH;
+  const long long KH = (long long)N * W;
+  const int* rp = batch->rowptr;
+  const int* ci = batch->colidx;
+  const float* X = batch->features;
+  // encoder, model.py:104-112: H_{i+1} = [BN(lrelu(A (H_i W_i))) || X]
+  SND_TRY(gemm_fwd(x, R, h0, f, X, f, x.w("enc.W0"), h0, B_ROW, x.f("XW0"), h0, nullptr));
+  {
+    SpmmArgs a{rp, ci, R, x.f("XW0"), h0, h0, x.f("H1"), h0 + f, SND_SPMM_GCN,
+               x.w("enc.bn0.gamma"), x.w("enc.bn0.beta"), x.f("P0"), h0, X, f, f,
+               nullptr, nullptr, nullptr, 0};
+    SND_TRY(launch_spmm(a, x.s));
+  }
+  SND_TRY(gemm_fwd(x, R, h1, h0 + f, x.f("H1"), h0 + f, x.w("enc.W1"), h1, B_ROW, x.f("XW1"), h1,
+                   nullptr));
+  {
+    SpmmArgs a{rp, ci, R, x.f("XW1"), h1, h1, x.f("H2"), W, SND_SPMM_GCN,
+               x.w("enc.bn1.gamma"), x.w("enc.bn1.beta"), x.f("P1"), h1, X, f, f,
+               x.w("enc.bne.gamma"), x.w("enc.bne.beta"), x.f("G"), W};
+    SND_TRY(launch_spmm(a, x.s));
+  }
+  if (p.tref) {
+    // graph heads (model.py:113): h = flat(G) Wh + bh, split-K over the N*W rows of Wh
+    TrefHeadFwdArgs a{x.f("G"), KH, p.B, x.w("enc.Wh"), gh, x.w("enc.bh"), x.f("PHF")};
+    SND_TRY(launch_tref_head_fwd(a, x.s));
+    const ReduceDesc rd{x.f("PHF"), x.f("Hh"), tref_head_fwd_blocks(KH, gh), RH * gh,
+                        (long long)RH * gh, 1.f, 0, 0, 0, 0};
+    SND_TRY(launch_reduce(&rd, 1, x.s));
+  } else {
+    // node-wise heads (model.py:113-115): h = G Wh + bh
+    SND_TRY(gemm_fwd(x, R, gh, W, x.f("G"), W, x.w("enc.Wh"), gh, B_ROW, x.f("Hh"), gh,
+                     x.w("enc.bh")));
+  }
+  // [mu || s] = h Wms + bms (model.py:114-115)
+  SND_TRY(gemm_fwd(x, RH, 2 * L, gh, x.f("Hh"), gh, x.w("enc.Wms"), 2 * L, B_ROW, x.f("MS"), 2 * L,
+                   x.w("enc.bms")));
+  return 0;
+}
+
 // ---- bf16 fast decoder ------------------------------------------------------
 RcArgs rc_args(const snd_plan& p, const char* ws, const Img& im, const void* x, int ldx, int K,
                int N, ColMap cols) {
@@ -870,6 +916,78 @@ void decoder_fast_reduce(const Ctx& x, std::vector<ReduceDesc>& rd) {
 
 }  // namespace
 
+// Forward-only pass for evaluation and sampling (main.py:358-469 generate_new*,
+// model.py:163-169 get_random_z) on the generic kernels of the plan's dtype:
+// encoder (modes SAMPLE / MEAN) -> z -> [d_sg_lin1] -> J -> conv decoders + sigmoid
+// heads (SHAT, XHAT) -> optional predicted adjacency (model.py:205-208).
+extern "C" int snd_generate(const snd_plan_t* plan, const snd_batch_t* batch, const float* params,
+                            void* workspace, int mode, const float* eps_or_z,
+                            unsigned long long seed, const int* step_counter,
+                            unsigned char* gen_adj, snd_stream_t stream) {
+  SND_CHECK_ARG(plan && params && workspace, "snd_generate: null argument");
+  SND_CHECK_ARG(mode >= SND_GEN_SAMPLE && mode <= SND_GEN_GIVEN, "snd_generate: bad mode %d", mode);
+  const bool enc = mode == SND_GEN_SAMPLE || mode == SND_GEN_MEAN;
+  SND_CHECK_ARG(!enc || (batch && batch->rowptr && batch->colidx && batch->features),
+                "snd_generate: modes SAMPLE/MEAN encode a batch (rowptr, colidx, features)");
+  SND_CHECK_ARG(mode != SND_GEN_GIVEN || eps_or_z, "snd_generate: mode GIVEN needs z");
+  const snd_plan& p = *plan;
+  const snd_config_t& c = p.c;
+  Ctx x{&p, (char*)workspace, params, nullptr, (hipStream_t)stream};
+  const int R = p.R, N = p.N, L = c.latent, RH = p.RH, dj = p.dj, C1 = p.C1;
+  const int sd = c.spatial_dim, nf = c.num_feature;
+  const long long CP = (long long)N * dj;
+  float* zl = p.tref ? x.f("ZL") : x.f("Z");
+  if (enc) SND_TRY(encoder_generic_fwd(x, batch));
+  if (mode == SND_GEN_MEAN) {             // z = mu
+    if (hipMemcpy2DAsync(zl, (size_t)L * 4, x.f("MS"), (size_t)2 * L * 4, (size_t)L * 4, RH,
+                         hipMemcpyDeviceToDevice, x.s) != hipSuccess) {
+      set_error("snd_generate: copy of mu failed");
+      return SND_ERR_HIP;
+    }
+  } else if (mode == SND_GEN_GIVEN) {
+    if (hipMemcpyAsync(zl, eps_or_z, (size_t)RH * L * 4, hipMemcpyDeviceToDevice, x.s) !=
+        hipSuccess) {
+      set_error("snd_generate: copy of z failed");
+      return SND_ERR_HIP;
+    }
+  } else {                                // z = mu + eps exp(s); PRIOR: mu = s = 0
+    if (mode == SND_GEN_PRIOR &&
+        hipMemsetAsync(x.f("MS"), 0, (size_t)RH * 2 * L * 4, x.s) != hipSuccess) {
+      set_error("snd_generate: memset failed");
+      return SND_ERR_HIP;
+    }
+    ReparamFwdArgs a{x.f("MS"), 2 * L, RH, L, eps_or_z, seed, step_counter, x.f("EPS"), zl,
+                     x.d("PKL"), nullptr, L};
+    SND_TRY(launch_reparam_fwd(a, x.s));
+  }
+  if (p.tref) {   // J = reshape(z Wp + bp, [B, N, node_h]) (model_joint.py:97)
+    TrefProjFwdArgs a{x.f("ZL"), p.B, L, x.w("dec.Wp"), x.w("dec.bp"), CP, x.f("Z")};
+    SND_TRY(launch_tref_proj_fwd(a, x.s));
+  }
+  // decoders (model_joint.py:112-145): conv1d k5 SAME -> BN -> lrelu, sigmoid heads
+  SND_TRY(conv_fwd(x, x.f("Z"), dj, dj, "dec.K1", C1, "dec.b1", "dec.bn1.gamma", "dec.bn1.beta",
+                   x.f("Y1"), x.f("U1")));
+  SND_TRY(conv_fwd(x, x.f("U1"), C1, c.s1, "dec.K2s", c.s2, "dec.b2s", "dec.bn2s.gamma",
+                   "dec.bn2s.beta", x.f("Y2S"), x.f("U2S")));
+  SND_TRY(conv_fwd(x, x.f("U1") + c.s1, C1, c.n1, "dec.K2n", c.n2, "dec.b2n", "dec.bn2n.gamma",
+                   "dec.bn2n.beta", x.f("Y2N"), x.f("U2N")));
+  SND_TRY(conv_fwd(x, x.f("U2S"), c.s2, c.s2, "dec.K3s", c.s3, "dec.b3s", "dec.bn3s.gamma",
+                   "dec.bn3s.beta", x.f("Y3S"), x.f("U3S")));
+  {
+    HeadArgs h[2] = {
+        {x.f("U3S"), c.s3, c.s3, x.w("dec.Ws"), x.w("dec.bs"), sd, nullptr, sd, (float)R * sd,
+         x.f("SHAT"), x.f("DU3S"), c.s3, x.f("PHS"), x.d("PSSES")},
+        {x.f("U2N"), c.n2, c.n2, x.w("dec.Wn"), x.w("dec.bn"), nf, nullptr, nf, (float)R * nf,
+         x.f("XHAT"), x.f("DU2N"), c.n2, x.f("PHN"), x.d("PSSEN")}};
+    SND_TRY(launch_heads(h, 2, R, x.s));
+  }
+  if (gen_adj) {
+    GenAdjArgs a{x.f("Z"), dj, dj, N, p.B, gen_adj};
+    SND_TRY(launch_gen_adj(a, x.s));
+  }
+  return 0;
+}
+
 extern "C" int snd_plan_launch(const snd_plan_t* plan, const snd_batch_t* batch,
                                void* workspace, const char* kernel, snd_stream_t stream) {
   SND_CHECK_ARG(plan && batch && workspace && kernel, "snd_plan_launch: null argument");
@@ -976,37 +1094,7 @@ extern "C" int snd_train_step(const snd_plan_t* plan, const snd_batch_t* batch,
   if (p.fast_enc) {
     SND_TRY(encoder_fast_fwd(x, batch));
   } else {
-    // encoder, model.py:104-112: H_{i+1} = [BN(lrelu(A (H_i W_i))) || X]
-    SND_TRY(gemm_fwd(x, R, h0, f, X, f, x.w("enc.W0"), h0, B_ROW, x.f("XW0"), h0, nullptr));
-    {
-      SpmmArgs a{rp, ci, R, x.f("XW0"), h0, h0, x.f("H1"), h0 + f, SND_SPMM_GCN,
-                 x.w("enc.bn0.gamma"), x.w("enc.bn0.beta"), x.f("P0"), h0, X, f, f,
-                 nullptr, nullptr, nullptr, 0};
-      SND_TRY(launch_spmm(a, x.s));
-    }
-    SND_TRY(gemm_fwd(x, R, h1, h0 + f, x.f("H1"), h0 + f, x.w("enc.W1"), h1, B_ROW, x.f("XW1"), h1,
-                     nullptr));
-    {
-      SpmmArgs a{rp, ci, R, x.f("XW1"), h1, h1, x.f("H2"), W, SND_SPMM_GCN,
-                 x.w("enc.bn1.gamma"), x.w("enc.bn1.beta"), x.f("P1"), h1, X, f, f,
-                 x.w("enc.bne.gamma"), x.w("enc.bne.beta"), x.f("G"), W};
-      SND_TRY(launch_spmm(a, x.s));
-    }
-    if (p.tref) {
-      // graph heads (model.py:113): h = flat(G) Wh + bh, split-K over the N*W rows of Wh
-      TrefHeadFwdArgs a{x.f("G"), KH, p.B, x.w("enc.Wh"), gh, x.w("enc.bh"), x.f("PHF")};
-      SND_TRY(launch_tref_head_fwd(a, x.s));
-      const ReduceDesc rd{x.f("PHF"), x.f("Hh"), tref_head_fwd_blocks(KH, gh), RH * gh,
-                          (long long)RH * gh, 1.f, 0, 0, 0, 0};
-      SND_TRY(launch_reduce(&rd, 1, x.s));
-    } else {
-      // node-wise heads (model.py:113-115): h = G Wh + bh
-      SND_TRY(gemm_fwd(x, R, gh, W, x.f("G"), W, x.w("enc.Wh"), gh, B_ROW, x.f("Hh"), gh,
-                       x.w("enc.bh")));
-    }
-    // [mu || s] = h Wms + bms (model.py:114-115)
-    SND_TRY(gemm_fwd(x, RH, 2 * L, gh, x.f("Hh"), gh, x.w("enc.Wms"), 2 * L, B_ROW, x.f("MS"), 2 * L,
-                     x.w("enc.bms")));
+    SND_TRY(encoder_generic_fwd(x, batch));
   }
   if (p.fast_enc && p.tref) {   // graph heads on the fast encoder's bf16 G
     TrefHeadFwdArgs a{nullptr, KH, p.B, x.w("enc.Wh"), gh, x.w("enc.bh"), x.f("PHF"),

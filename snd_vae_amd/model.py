@@ -160,3 +160,60 @@ class SGCNModelVAE:
     @property
     def generated_node_feat(self):
         return self._rows("XHAT", self.cfg.num_feature)
+
+    # ---- evaluation / sampling (snd_generate)
+    def generate(self, batch: Optional[DeviceBatch] = None, mode: str = "mean",
+                 z: Optional[torch.Tensor] = None, eps: Optional[torch.Tensor] = None,
+                 seed: int = 0, step: int = 0, want_adj: bool = True, stream=None) -> dict:
+        """Forward-only decode (`main.py:358-469`, `model.py:163-169`).
+
+        mode: "mean" (z = z_mean, reconstruction), "sample" (z = mu + eps e^s as
+        in training), "prior" (z ~ N(0, 1), get_random_z) or "given" (``z``).
+        ``eps``: injected normals [RH, L]; None draws them on the device from
+        Philox at (seed, step).  Returns generated_adj (uint8 [B, N, N]),
+        generated_spatial [B*N, 2], generated_node_feat [B*N, F], z, and
+        z_mean / z_std for the encoding modes (all fresh tensors).
+        """
+        L = _lib.lib()
+        m = _lib.GEN_MODES[mode]
+        if mode in ("mean", "sample") and batch is None:
+            raise ValueError(f"mode {mode!r} encodes a batch")
+        src = z if mode == "given" else eps
+        if mode == "given" and z is None:
+            raise ValueError("mode 'given' needs z")
+        if src is not None:
+            rh = self.n_graphs if self._graph_latent else self.n_graphs * self.cfg.n_nodes
+            src = src.to(device=self.device, dtype=torch.float32).contiguous()
+            if tuple(src.shape) != (rh, self.cfg.latent):
+                raise ValueError(f"z/eps must be [{rh}, {self.cfg.latent}], got {tuple(src.shape)}")
+        n = self.cfg.n_nodes
+        adj = (torch.empty(self.n_graphs, n, n, dtype=torch.uint8, device=self.device)
+               if want_adj else None)
+        step_t = torch.full((1,), step, dtype=torch.int32, device=self.device)
+        bc = batch.c_struct() if batch is not None else None
+        _lib.check(L.snd_generate(self.plan, C.byref(bc) if bc is not None else None,
+                                  _lib.ptr(self.params), _lib.ptr(self.workspace), m,
+                                  _lib.ptr(src), seed, _lib.ptr(step_t), _lib.ptr(adj),
+                                  _lib.stream_ptr(stream)), "snd_generate")
+        out = {"generated_adj": adj,
+               "generated_spatial": self.generated_spatial.clone(),
+               "generated_node_feat": self.generated_node_feat.clone(),
+               "z": self.z_sg.clone()}
+        if mode in ("mean", "sample"):
+            out["z_mean"] = self.z_mean_sg.clone()
+            out["z_std"] = self.z_std_sg.clone()
+        return out
+
+
+def adj_accuracy(gen_adj: torch.Tensor, batch: DeviceBatch) -> float:
+    """`main.py:334`: mean over B*N*N of (generated_adj == adj_truth), from the CSR."""
+    B, n = batch.n_graphs, batch.n_nodes
+    total = B * n * n
+    ones = int(gen_adj.sum(dtype=torch.int64).item())
+    if batch.nnz == 0:
+        return (total - ones) / total
+    rows = torch.repeat_interleave(torch.arange(B * n, device=gen_adj.device),
+                                   torch.diff(batch.rowptr.long()))
+    flat = rows * n + batch.colidx[:batch.nnz].long() % n
+    hits = int(gen_adj.view(-1)[flat].sum(dtype=torch.int64).item())
+    return (total - batch.nnz - ones + 2 * hits) / total

@@ -21,7 +21,7 @@ STAGES=${STAGES:-"smoke tests bench prof"}
 for s in $STAGES; do
   case $s in
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
-    tests) step pytest_gpu 900 python -m pytest tests -m gpu -q -x ;;
+    tests) step pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread ;;
     bench) step bench 600 python bench.py ;;
     prof)  step rocprof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run \
              --output-format csv -- python bench.py --steps 20 --warmup 5 --no-cpu-baseline --extra "" ;;
