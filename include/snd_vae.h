@@ -172,6 +172,45 @@ int snd_adam_tf1(float* param, const float* grad, float* m, float* v,
                  float grad_scale, const int* step_counter,
                  snd_stream_t stream);
 
+/* ---- SpatialGraphConvolution (layers.py:143-198) and the model_joint
+ * spatial-graph encoder layer s' = lrelu(BN(SGConv(adj, s, rel)))
+ * (model_joint.py:77-80), factorised to O(nnz (h0 + deg)) + row GEMMs (see
+ * snd_sg.hip).  adj must be symmetric (spanning trees and adj_truth are;
+ * input_data.py:31-37,67) with rel_dim 1 (Matrix1 has 3F+3 rows).
+ * Per-layer parameter buffer (fp32, snd_sg_param_count floats), row-major:
+ *   Matrix1 [3F+3][h0] (rows: x_i | x_j | x_k | rel_ij | rel_jk | dis_ik), bias1 [h0],
+ *   Matrix2 [2F+1+h0][h1] (x_i | x_j | rel_ij | m3_sum), bias2 [h1],
+ *   Matrix3 [F+h1][h2] (x | m2_sum), bias3 [h2], BN gamma [h2], BN beta [h2].
+ * Gradients use the same layout (written, not accumulated). */
+typedef struct snd_sg_graph {
+  const int* rowptr;   /* [R+1] symmetric CSR, block-diagonal, sorted global ids */
+  const int* colidx;   /* [nnz] */
+  int n_rows;          /* R = B * n_per_graph */
+  int n_per_graph;
+  float* edge_lr;      /* [nnz] lrelu(rel_ij)                      (snd_sg_prep) */
+  float* edge_q;       /* [nnz] sum_{k in N(j)} lrelu(rel_ik)      (snd_sg_prep) */
+  int* edge_rev;       /* [nnz] index of the reverse edge (j, i)   (snd_sg_prep) */
+  float* node_deg;     /* [R] degree                               (snd_sg_prep) */
+  float* node_e;       /* [R] sum_{j in N(i)} lrelu(rel_ij)        (snd_sg_prep) */
+} snd_sg_graph_t;
+/* Edge / node scalars of a batch from rel [B, N, N] (the 'rel' feed, main.py:262,
+ * /600 at load); *n_unmatched (device int) = edges without a reverse edge (must be 0). */
+int snd_sg_prep(const snd_sg_graph_t* g, const float* rel, int* n_unmatched,
+                snd_stream_t stream);
+long long snd_sg_param_count(int f, int h0, int h1, int h2);
+size_t snd_sg_workspace(int n_rows, int f, int h0, int h1, int h2);
+/* y [R, h2] = SGConv(adj, x, rel); bn_act: out = lrelu(BN(y)) (frozen Keras BN).
+ * The workspace keeps what snd_sg_layer_bwd needs: pass the same one. */
+int snd_sg_layer_fwd(const snd_sg_graph_t* g, const float* x, int ldx, int f, int h0, int h1,
+                     int h2, const float* params, int bn_act, float* y, float* out,
+                     void* workspace, snd_stream_t stream);
+/* dout = dL/d(out) (bn_act) or dL/dy; writes grads (param layout) and, if dx is
+ * not NULL, dL/dx [R, f]. */
+int snd_sg_layer_bwd(const snd_sg_graph_t* g, const float* x, int ldx, int f, int h0, int h1,
+                     int h2, const float* params, int bn_act, const float* y,
+                     const float* dout, float* dx, int lddx, float* grads, void* workspace,
+                     snd_stream_t stream);
+
 /* ---- a14: the whole train step (main.py:315-334) ---------------------------
  * A plan fixes shapes; the step runs forward + backward of the SND-VAE
  * (SURVEY §8 "Composed step") for one batch in either decoder-input topology:

@@ -35,6 +35,13 @@ class Config(C.Structure):
                 ("norm", c_float), ("dtype", c_int), ("topology", c_int), ("node_h", c_int)]
 
 
+class SGGraph(C.Structure):
+    """snd_sg_graph_t"""
+    _fields_ = [("rowptr", vp), ("colidx", vp), ("n_rows", c_int), ("n_per_graph", c_int),
+                ("edge_lr", vp), ("edge_q", vp), ("edge_rev", vp), ("node_deg", vp),
+                ("node_e", vp)]
+
+
 class Batch(C.Structure):
     """snd_batch_t"""
     _fields_ = [("rowptr", vp), ("colidx", vp), ("features", vp),
@@ -69,6 +76,13 @@ _SIGS = {
                                 vp, c_int, vp, vp, vp, c_size, vp]),
     "snd_adam_tf1": (c_int, [vp, vp, vp, vp, c_ll, c_float, c_float, c_float, c_float,
                              c_float, vp, vp]),
+    "snd_sg_prep": (c_int, [C.POINTER(SGGraph), vp, vp, vp]),
+    "snd_sg_param_count": (c_ll, [c_int, c_int, c_int, c_int]),
+    "snd_sg_workspace": (c_size, [c_int, c_int, c_int, c_int, c_int]),
+    "snd_sg_layer_fwd": (c_int, [C.POINTER(SGGraph), vp, c_int, c_int, c_int, c_int, c_int, vp,
+                                 c_int, vp, vp, vp, vp]),
+    "snd_sg_layer_bwd": (c_int, [C.POINTER(SGGraph), vp, c_int, c_int, c_int, c_int, c_int, vp,
+                                 c_int, vp, vp, vp, c_int, vp, vp, vp]),
     "snd_plan_create": (c_int, [C.POINTER(Config), c_int, C.POINTER(vp)]),
     "snd_plan_destroy": (None, [vp]),
     "snd_plan_param_count": (c_ll, [vp]),
