@@ -156,9 +156,13 @@ def test_fused_adam_matches_separate_update(dtype):
         assert k in m1.layout.shapes
     p_a, p_b = m0.blocks(), m1.blocks()
     for k in p_a:
-        # same gradients, same update formula: only rounding order may differ
+        # same gradients, same update formula: only rounding order may differ.  Adam
+        # normalises the step (lr m/sqrt(v)), so a rounding difference in a small
+        # gradient moves the update by up to ~1e-2 lr in bf16 mode (dJ is bf16-rounded
+        # at different points of the fused and separate weight-gradient kernels).
+        rel = 1e-5 if dtype == "f32" else 1e-4
         d = np.abs(p_a[k] - p_b[k]).max()
-        assert d <= 1e-6 + 1e-5 * np.abs(p_a[k]).max(), (k, d)
+        assert d <= 1e-6 + rel * np.abs(p_a[k]).max(), (k, d)
     for a, b in ((o0.m, o1.m), (o0.v, o1.v)):   # fma contraction may differ per kernel
         assert float((a - b).abs().max()) <= 1e-5 * float(a.abs().max())
     assert o0.loss_dict()["cost"] == pytest.approx(o1.loss_dict()["cost"], rel=1e-5)
