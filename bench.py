@@ -95,7 +95,7 @@ def run_workload(cfg, B, args, info, steps=None, warmup=None):
     """Build B graphs per GPU, capture one full step in a HIP graph, time `steps` replays."""
     import torch
 
-    from snd_vae_amd.data import synthetic_batch
+    from snd_vae_amd.data import default_tile_rows, synthetic_batch
     from snd_vae_amd.model import DeviceBatch, SGCNModelVAE
     from snd_vae_amd.optimizer import OptimizerVAE
     from snd_vae_amd.parallel import max_over_ranks
@@ -104,7 +104,7 @@ def run_workload(cfg, B, args, info, steps=None, warmup=None):
     log(f"[rank {info.rank}] building {B} RGG graphs N={cfg.n_nodes} ({cfg.topology}, node_h "
         f"{cfg.node_h_size}, latent {cfg.latent})")
     host = synthetic_batch(cfg, B, seed=1000 + info.rank * B)
-    db = DeviceBatch(host)
+    db = DeviceBatch(host, tile_rows=0 if args.no_tiles else default_tile_rows(cfg.g_conv_hidden[1]))
     model = SGCNModelVAE(cfg, B, dtype=args.dtype)
     opt = OptimizerVAE(model, process_group=info.group if info.world > 1 else None)
     if args.no_graph:
@@ -184,14 +184,18 @@ def kernel_timer(model, bc, reps):
 
 
 def spmm_batched(host, width, copies, reps):
-    """The bf16 SpMM (snd_csr_spmm_bf16) on `copies` x the bench batch stacked
-    block-diagonally (8 x copies graphs): a working set above the 256 MB Infinity
-    Cache, so the HBM fraction is not a cache artefact."""
+    """The bf16 SpMM on `copies` x the bench batch stacked block-diagonally (8 x copies
+    graphs): a working set above the 256 MB Infinity Cache, so the HBM fraction is not
+    a cache artefact.  Headline: the row-tiled kernel
+    (snd_csr_spmm_bf16_tiled, neighbour rows staged in LDS); previous_variant: the
+    register-gather kernel (snd_csr_spmm_bf16) on the same input."""
+    import ctypes
+
     import numpy as np
     import torch
 
     from snd_vae_amd import _lib
-    from snd_vae_amd.data import locality_order
+    from snd_vae_amd.data import GraphBatch, default_tile_rows, locality_order, row_tiles
     rp0, ci0 = host.rowptr.astype(np.int64), host.colidx.astype(np.int64)
     nnz0, R0 = int(rp0[-1]), host.n_graphs * host.n_nodes
     rp = np.concatenate([rp0[:-1] + c * nnz0 for c in range(copies)] + [np.array([copies * nnz0])])
@@ -199,22 +203,35 @@ def spmm_batched(host, width, copies, reps):
     o0 = locality_order(host).astype(np.int64)
     order = np.concatenate([o0 + c * R0 for c in range(copies)])
     R = R0 * copies
+    z = np.zeros((1, 1), np.float32)
+    big = GraphBatch(host.n_graphs * copies, host.n_nodes, rp.astype(np.int32), ci.astype(np.int32), z, z, z)
+    tr = default_tile_rows(width)
+    from snd_vae_amd.model import DeviceTiles
+    rt = row_tiles(big, order.astype(np.int32), tr)
+    dt = DeviceTiles(rt)
     d_rp = torch.from_numpy(rp.astype(np.int32)).cuda()
     d_ci = torch.from_numpy(ci.astype(np.int32)).cuda()
     d_order = torch.from_numpy(order.astype(np.int32)).cuda()
+    tiles = dt.c_struct()
     h = torch.randn(R, width, device="cuda").to(torch.bfloat16)
     out = torch.empty_like(h)
     L = _lib.lib()
-    ms = time_launches(lambda sp: _lib.check(L.snd_csr_spmm_bf16(
+    ng = host.n_graphs * copies
+    ms = time_launches(lambda sp: _lib.check(L.snd_csr_spmm_bf16_tiled(
+        d_rp.data_ptr(), d_ci.data_ptr(), R, ctypes.byref(tiles), h.data_ptr(), width, width,
+        out.data_ptr(), width, host.n_nodes, ng, d_order.data_ptr(), sp)), reps)
+    ms_prev = time_launches(lambda sp: _lib.check(L.snd_csr_spmm_bf16(
         d_rp.data_ptr(), d_ci.data_ptr(), R, h.data_ptr(), width, width, out.data_ptr(), width,
-        host.n_nodes, host.n_graphs * copies, d_order.data_ptr(), sp)), reps)
+        host.n_nodes, ng, d_order.data_ptr(), sp)), reps)
     byts = 4 * (R + 1) + 4 * len(ci) + 2 * 2 * R * width
     gbs = byts / (ms * 1e-3) / 1e9
-    return {"kernel": f"csr_spmm_bf16 (A @ H, width {width}, {host.n_graphs * copies} graphs "
-                      f"block-diagonal, {len(ci)} nnz)",
+    return {"kernel": f"csr_spmm_bf16_tiled (A @ H, width {width}, {ng} graphs "
+                      f"block-diagonal, {len(ci)} nnz, {tr}-row tiles, sets <= {rt.ustride} rows)",
             "bound": "hbm", "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
             "frac": round(gbs / PEAK_HBM_GBS, 4), "avg_launch_ms": round(ms, 5),
-            "bytes_per_launch": byts}
+            "bytes_per_launch": byts,
+            "previous_variant": {"kernel": "csr_spmm_bf16 (register gathers)", "avg_launch_ms": round(ms_prev, 5),
+                                 "frac": round(byts / (ms_prev * 1e-3) / 1e9 / PEAK_HBM_GBS, 4)}}
 
 
 def extra_workload(name, args, info):
@@ -266,6 +283,7 @@ def main():
     ap.add_argument("--latent", type=int, default=64)
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "f32"])
     ap.add_argument("--no-graph", action="store_true", help="eager launches instead of HIP graph")
+    ap.add_argument("--no-tiles", action="store_true", help="register-gather SpMM instead of LDS row tiles")
     ap.add_argument("--kernel-reps", type=int, default=20)
     ap.add_argument("--cpu-baseline-seconds", type=float, default=20.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")

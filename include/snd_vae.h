@@ -82,6 +82,45 @@ int snd_csr_spmm_bf16(const int* rowptr, const int* colidx, int n_rows,
                       const void* h, int ldh, int width, void* out, int ldo,
                       int n_per_graph, int n_graphs, const int* row_order,
                       snd_stream_t stream);
+
+/* Row tiles of a CSR (ABI 5): a per-batch companion format of the bf16 SpMM
+ * that stages neighbour rows in LDS.  The schedule (row_order, or natural
+ * order) is cut into tiles of tile_rows consecutive slots.  Per tile:
+ *   rows[slot]   the tile's rows, by degree (descending, ties by schedule
+ *                order), so a wavefront's rows have similar lengths;
+ *   trp[slot]    row pointers in slot order into lcol ([n_rows+1]);
+ *   lcol[k]      1 + each neighbour's index in its tile's set, every
+ *                row's entries in colidx order (u16; 0 is never used);
+ *   ucol[t*ustride + u]  the tile's set: ascending distinct neighbour rows,
+ *                padded with -1 to ustride = the largest set.
+ * The adjacency is static across training steps, so the tiles are built
+ * once per batch, on the HOST (plain C++ over host arrays): call
+ * snd_spmm_tile_plan with rows/trp/lcol/ucol NULL to size (*ustride), then
+ * with them to fill; it returns the ucol length n_tiles*ustride (>= 0) or a
+ * negative error.  A tile set of 65535 rows or more is an error.  The
+ * SpMM relies on the degree order: a wavefront's first row is its longest. */
+typedef struct snd_row_tiles {
+  const int* rows;              /* [n_rows] device */
+  const int* trp;               /* [n_rows+1] device */
+  const uint16_t* lcol;         /* [nnz] device */
+  const int* ucol;              /* [n_tiles*ustride] device */
+  int tile_rows;                /* rows per tile (<= 128); 0 = no tiles */
+  int ustride;                  /* largest tile set */
+} snd_row_tiles_t;
+long long snd_spmm_tile_plan(const int* rowptr, const int* colidx, int n_rows,
+                             const int* row_order, int tile_rows, int* rows,
+                             int* trp, uint16_t* lcol, int* ucol, int* ustride);
+/* snd_csr_spmm_bf16 over row tiles: a persistent, software-pipelined kernel.
+ * Each workgroup walks its tiles; while it sums tile i from LDS, the rows of
+ * tile i+1 are in flight into registers and the set of tile i+2 is read.
+ * A tile's rows are widened to fp32 in LDS once; every row accumulates its
+ * neighbours from LDS in colidx order (the same fp32 sums as
+ * snd_csr_spmm_bf16, bit for bit).  If ustride exceeds the LDS image
+ * (319 rows) the launch runs snd_csr_spmm_bf16's kernel instead. */
+int snd_csr_spmm_bf16_tiled(const int* rowptr, const int* colidx, int n_rows,
+                            const snd_row_tiles_t* tiles, const void* h, int ldh,
+                            int width, void* out, int ldo, int n_per_graph,
+                            int n_graphs, const int* row_order, snd_stream_t stream);
 /* ---- a5: linear / dense GEMM on MFMA ---------------------------------------
  * Replaces linear() (layers.py:566-576) and the X@w of GraphConvolution
  * (layers.py:120-121; the tile() copy is not needed):
@@ -252,6 +291,9 @@ typedef struct snd_batch {
   const float* spatial_truth;  /* [B*N, spatial_dim] */
   const int* row_order;        /* optional [B*N] locality schedule of the gather
                                   kernels (see snd_csr_spmm_bf16); NULL = natural */
+  snd_row_tiles_t tiles;       /* optional row tiles over row_order (ABI 5; all
+                                  zero = none): the bf16 encoder SpMMs stage
+                                  neighbour rows in LDS */
 } snd_batch_t;
 
 typedef struct snd_plan snd_plan_t;

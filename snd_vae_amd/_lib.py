@@ -17,7 +17,7 @@ c_int, c_ll, c_float, c_size, c_ull = C.c_int, C.c_longlong, C.c_float, C.c_size
 vp = C.c_void_p
 
 
-ABI_VERSION = 4
+ABI_VERSION = 5
 GEN_MODES = {"sample": 0, "mean": 1, "prior": 2, "given": 3}
 TOPOLOGY = {"tscale": 0, "tref": 1}
 
@@ -42,10 +42,17 @@ class SGGraph(C.Structure):
                 ("node_e", vp)]
 
 
+class RowTiles(C.Structure):
+    """snd_row_tiles_t"""
+    _fields_ = [("rows", vp), ("trp", vp), ("lcol", vp), ("ucol", vp), ("tile_rows", c_int),
+                ("ustride", c_int)]
+
+
 class Batch(C.Structure):
     """snd_batch_t"""
     _fields_ = [("rowptr", vp), ("colidx", vp), ("features", vp),
-                ("feature_truth", vp), ("spatial_truth", vp), ("row_order", vp)]
+                ("feature_truth", vp), ("spatial_truth", vp), ("row_order", vp),
+                ("tiles", RowTiles)]
 
 
 # name -> (restype, argtypes)
@@ -57,6 +64,9 @@ _SIGS = {
     "snd_csr_spmm": (c_int, [vp, vp, c_int, vp, c_int, c_int, vp, c_int, c_int, vp, vp, vp,
                              c_int, vp, c_int, c_int, vp, vp, vp, c_int, vp]),
     "snd_csr_spmm_bf16": (c_int, [vp, vp, c_int, vp, c_int, c_int, vp, c_int, c_int, c_int, vp, vp]),
+    "snd_spmm_tile_plan": (c_ll, [vp, vp, c_int, vp, c_int, vp, vp, vp, vp, C.POINTER(c_int)]),
+    "snd_csr_spmm_bf16_tiled": (c_int, [vp, vp, c_int, C.POINTER(RowTiles), vp, c_int, c_int, vp,
+                                        c_int, c_int, c_int, vp, vp]),
     "snd_gemm": (c_int, [c_int, c_int, c_int, c_int, c_int, vp, c_int, vp, c_int, vp, c_int,
                          vp, c_int, vp]),
     "snd_conv1d_same_fwd": (c_int, [vp, c_int, c_int, c_int, c_int, vp, c_int, vp, vp, vp,

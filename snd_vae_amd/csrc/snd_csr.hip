@@ -9,6 +9,9 @@
 // HBM-bound: each dense row is read twice (count and fill).
 #include "snd_common.hpp"
 
+#include <algorithm>
+#include <vector>
+
 namespace snd {
 namespace {
 
@@ -113,4 +116,61 @@ extern "C" int snd_dense_to_csr(const float* adj, int n_graphs, int n, int* rowp
     SND_LAUNCH_CHECK("csr_fill_kernel");
   }
   return 0;
+}
+
+// Row tiles of the bf16 SpMM (snd_row_tiles_t; host code, once per batch).
+// Tile t = schedule slots [t*tile_rows, (t+1)*tile_rows) of row_order (or the
+// natural order), its rows sorted by degree (descending, stable); its set is the
+// ascending distinct colidx values of those rows, and lcol maps every entry, in
+// slot order, to 1 + its position in that set (0 is the kernel's zero row).
+extern "C" long long snd_spmm_tile_plan(const int* rowptr, const int* colidx, int n_rows,
+                                        const int* row_order, int tile_rows, int* rows, int* trp,
+                                        uint16_t* lcol, int* ucol, int* ustride) {
+  SND_CHECK_ARG(rowptr && n_rows >= 0 && tile_rows > 0 && ustride, "snd_spmm_tile_plan: bad args");
+  const bool fill = rows || trp || lcol || ucol;
+  SND_CHECK_ARG(!fill || (rows && trp && lcol && ucol), "snd_spmm_tile_plan: rows, trp, lcol, ucol go together");
+  const long long nnz = rowptr[n_rows];
+  SND_CHECK_ARG(colidx || nnz == 0, "snd_spmm_tile_plan: null colidx");
+  const int ntiles = (n_rows + tile_rows - 1) / tile_rows;
+  std::vector<int> cols, trow;
+  int mx = 0;
+  if (fill) SND_CHECK_ARG(*ustride >= 0, "snd_spmm_tile_plan: ustride from the sizing call");
+  const int stride = fill ? *ustride : 0;
+  long long k_out = 0;
+  if (fill) trp[0] = 0;
+  for (int t = 0; t < ntiles; ++t) {
+    cols.clear();
+    trow.clear();
+    const int s_lo = t * tile_rows, s_hi = std::min(n_rows, (t + 1) * tile_rows);
+    for (int slot = s_lo; slot < s_hi; ++slot) {
+      const int r = row_order ? row_order[slot] : slot;
+      SND_CHECK_ARG(r >= 0 && r < n_rows, "snd_spmm_tile_plan: row_order entry %d out of range", r);
+      trow.push_back(r);
+      for (int k = rowptr[r]; k < rowptr[r + 1]; ++k) cols.push_back(colidx[k]);
+    }
+    std::sort(cols.begin(), cols.end());
+    cols.erase(std::unique(cols.begin(), cols.end()), cols.end());
+    const int nu = (int)cols.size();
+    SND_CHECK_ARG(nu < 65535, "snd_spmm_tile_plan: tile %d has %d distinct rows (>= 65535)", t, nu);
+    mx = std::max(mx, nu);
+    if (!fill) continue;
+    SND_CHECK_ARG(nu <= stride, "snd_spmm_tile_plan: tile %d set %d > ustride %d", t, nu, stride);
+    std::stable_sort(trow.begin(), trow.end(), [&](int x, int y) {
+      return rowptr[x + 1] - rowptr[x] > rowptr[y + 1] - rowptr[y];
+    });
+    int* uc = ucol + (long long)t * stride;
+    std::copy(cols.begin(), cols.end(), uc);
+    std::fill(uc + nu, uc + stride, -1);
+    for (int i = 0; i < (int)trow.size(); ++i) {
+      const int r = trow[i];
+      rows[s_lo + i] = r;
+      for (int k = rowptr[r]; k < rowptr[r + 1]; ++k)
+        lcol[k_out++] = (uint16_t)(1 + (std::lower_bound(cols.begin(), cols.end(), colidx[k]) - cols.begin()));
+      trp[s_lo + i + 1] = (int)k_out;
+    }
+  }
+  if (!fill) *ustride = mx;
+  const long long len = (long long)ntiles * (fill ? stride : mx);
+  SND_CHECK_ARG(len < (1ll << 31), "snd_spmm_tile_plan: tile sets beyond 2^31 entries");
+  return len;
 }

@@ -152,6 +152,10 @@ struct SpmmBfArgs {
   __bf16* g; int ldg;
   int xcd_nbg;
   const int* row_order;       // optional processing order of the rows (locality schedule)
+  // optional row tiles (snd_row_tiles_t over row_order): tile_rows > 0 selects the LDS-staged kernel
+  const int* t_rowid = nullptr; const int* t_trp = nullptr; const uint16_t* t_lcol = nullptr;
+  const int* t_ucol = nullptr; int t_rows = 0; int t_ustride = 0;
+  int npg = 0; int ngraphs = 0;  // graph shape for the XCD-aware tile order (0: natural)
 };
 int launch_spmm_bf16(const SpmmBfArgs& a, hipStream_t s);
 

@@ -174,30 +174,15 @@ __global__ void __launch_bounds__(NT) gcn0_kernel(Gcn0Args a) {
 }
 
 // ---------------------------------------------------------------- bf16 SpMM
+// Epilogue of a finished row (acc = A[r,:] @ h in fp32): plain bf16 store, or the
+// GraphConvolution 1 epilogue (preact fp32, lrelu -> BN1 -> concat X -> encoder_g BN).
 template <int EPI, int NQ>
-__global__ void __launch_bounds__(NT) spmm_bf16_kernel(SpmmBfArgs a) {
-  const int sub = threadIdx.x & (LPR - 1);
-  const int r = row_of(a.row_order, xcd_rowblock(blockIdx.x, a.xcd_nbg), a.R);
-  if (r >= a.R) return;            // whole 8-lane row groups leave together
+__device__ __forceinline__ void spmm_row_epilogue(const SpmmBfArgs& a, int r, int sub,
+                                                  const float (&acc)[NQ][8]) {
   const int nch = a.width >> 3;    // 8-column chunks: lane sub owns chunks sub, sub + 8
-  float acc[2][8];
-#pragma unroll
-  for (int q = 0; q < 2; ++q)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) acc[q][j] = 0.f;
-  bool qv[NQ];
-#pragma unroll
-  for (int q = 0; q < NQ; ++q) qv[q] = sub + 8 * q < nch;
-  // chunks past the width read the next row's bytes (or zeros past the end): never stored
-  const __amdgpu_buffer_rsrc_t rs = rows_rsrc(a.h, (long long)a.R * a.ldh * 2);
-  gather_rows16<NQ>(a.colidx, a.rowptr[r], a.rowptr[r + 1], rs, 2u * a.ldh, sub,
-                    [&](int, const u32x4 (&v)[NQ], bool) {
-#pragma unroll
-                      for (int q = 0; q < NQ; ++q) acc8v(acc[q], v[q]);
-                    });
 #pragma unroll
   for (int q = 0; q < NQ; ++q) {
-    if (!qv[q]) continue;
+    if (sub + 8 * q >= nch) continue;
     const int col = 64 * q + 8 * sub;
     if constexpr (EPI == SND_SPMM_PLAIN) {
       *reinterpret_cast<uint4*>(a.out + (long long)r * a.ldo + col) = to_bf16x8(acc[q]);
@@ -226,6 +211,310 @@ __global__ void __launch_bounds__(NT) spmm_bf16_kernel(SpmmBfArgs a) {
       *reinterpret_cast<uint4*>(a.g + (long long)r * a.ldg + a.width) = to_bf16x8(g);
     }
   }
+}
+
+template <int NQ>
+__device__ __forceinline__ void zero_acc(float (&acc)[NQ][8]) {
+#pragma unroll
+  for (int q = 0; q < NQ; ++q)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[q][j] = 0.f;
+}
+
+template <int EPI, int NQ>
+__global__ void __launch_bounds__(NT) spmm_bf16_kernel(SpmmBfArgs a) {
+  const int sub = threadIdx.x & (LPR - 1);
+  const int r = row_of(a.row_order, xcd_rowblock(blockIdx.x, a.xcd_nbg), a.R);
+  if (r >= a.R) return;            // whole 8-lane row groups leave together
+  float acc[NQ][8];
+  zero_acc(acc);
+  // chunks past the width read the next row's bytes (or zeros past the end): never stored
+  const __amdgpu_buffer_rsrc_t rs = rows_rsrc(a.h, (long long)a.R * a.ldh * 2);
+  gather_rows16<NQ>(a.colidx, a.rowptr[r], a.rowptr[r + 1], rs, 2u * a.ldh, sub,
+                    [&](int, const u32x4 (&v)[NQ], bool) {
+#pragma unroll
+                      for (int q = 0; q < NQ; ++q) acc8v(acc[q], v[q]);
+                    });
+  spmm_row_epilogue<EPI, NQ>(a, r, sub, acc);
+}
+
+// ---------------------------------------------------------------- bf16 SpMM over row tiles
+// Persistent, software-pipelined SpMM over the row tiles of snd_row_tiles_t.
+//  * A tile's distinct neighbour rows (its set; ascending ids, so mostly consecutive
+//    128-byte lines) are read once from HBM/L2 and widened to fp32 in LDS, plus one
+//    zero row at index ustride.
+//  * Every row's 8-lane group walks its neighbours in colidx order, 16 per round
+//    (local ids broadcast inside the group), LDS reads in flight, packed fp32 adds;
+//    a round's trip count is the wavefront's longest row (rows sorted by degree in
+//    the tile keep that close to each row's own), shorter rows read the zero row
+//    (exact +0 adds).  Same fp32 sums in the same order as spmm_bf16_kernel:
+//    bitwise-equal output.
+//  * Each workgroup walks a run of tiles (one graph's tiles stay on one XCD).  While
+//    it sums tile i from LDS, tile i+1's rows and first local ids are in flight into
+//    registers and tile i+2's row metadata and set ids are read: every dependent
+//    load chain (set ids -> rows, row pointers -> local ids) spans one tile of work.
+// Bank-conflict-free reads: ds_read_b128 serves a wave in 16-lane groups holding
+// four 4-lane pieces of four different rows ({0-3,12-15,20-23,24-27} ...); the
+// piece of 8-lane group g, half h reads row quarter (2g + h + 2 r) mod 4 in read r,
+// so the four pieces of every 16-lane group hit four distinct bank quarters for any
+// four rows (fp32 rows are 256 B = 64 banks: the quarter is fixed by the column).
+constexpr int TNT = 512;                   // 64 row groups of 8 lanes
+constexpr int TG = TNT / LPR;
+constexpr int TILE_CAP = 319;              // largest set: 320 fp32 image rows with the zero row
+constexpr int TRPG = 2;                    // rows per 8-lane group (tile_rows <= 128)
+constexpr int TPRE = 4;                    // local ids prefetched per lane and row (32 per row)
+// LDS image bytes: 80 KB for 64-wide rows (two workgroups per CU), 160 KB for 128-wide
+template <int NQ> constexpr int tile_lds_bytes() { return (TILE_CAP + 1) * 256 * NQ; }
+// 16-byte bf16 chunks staged per thread and tile: (TILE_CAP + 1) * 8 NQ / TNT
+template <int NQ> constexpr int tile_chunks() { return (TILE_CAP + 1) * 8 * NQ / TNT; }
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+
+// float4 chunk of a 64-column block read by this lane in read r (0, 1)
+__device__ __forceinline__ int tile_chunk(int sub, int r) {
+  const int g = (threadIdx.x >> 3) & 3;
+  return 4 * ((2 * g + (sub >> 2) + 2 * r) & 3) + (sub & 3);
+}
+
+template <int NQ>
+__device__ __forceinline__ void lds_round16(int id0, int id1, int n, const f32x4* img, const int (&chb)[2 * NQ],
+                                            f32x2 (&acc)[2 * NQ][2]) {
+  // n (wave-uniform) = the wave's longest row in this round; shorter rows read the
+  // zero row there (exact +0 adds: bit-identical sums).  Ids become byte offsets
+  // before the broadcast (one multiply per lane, not per neighbour).
+  const int b0 = id0 * (256 * NQ), b1 = id1 * (256 * NQ);
+  int c[16];
+  c[0] = bcast8<0>(b0); c[1] = bcast8<1>(b0); c[2] = bcast8<2>(b0); c[3] = bcast8<3>(b0);
+  c[4] = bcast8<4>(b0); c[5] = bcast8<5>(b0); c[6] = bcast8<6>(b0); c[7] = bcast8<7>(b0);
+  c[8] = bcast8<0>(b1); c[9] = bcast8<1>(b1); c[10] = bcast8<2>(b1); c[11] = bcast8<3>(b1);
+  c[12] = bcast8<4>(b1); c[13] = bcast8<5>(b1); c[14] = bcast8<6>(b1); c[15] = bcast8<7>(b1);
+  const char* base = reinterpret_cast<const char*>(img);
+  constexpr int IF = 8 / NQ;        // neighbours in flight: 64 VGPRs of LDS reads
+#pragma unroll
+  for (int u0 = 0; u0 < 16; u0 += IF) {
+    if (u0 >= n) break;
+    f32x4 v[IF][2 * NQ];
+#pragma unroll
+    for (int u = 0; u < IF; ++u)
+#pragma unroll
+      for (int i = 0; i < 2 * NQ; ++i) v[u][i] = *reinterpret_cast<const f32x4*>(base + c[u0 + u] + chb[i]);
+#pragma unroll
+    for (int u = 0; u < IF; ++u) {
+      if (u0 + u >= n) break;
+#pragma unroll
+      for (int i = 0; i < 2 * NQ; ++i) {
+        acc[i][0] += v[u][i].xy;
+        acc[i][1] += v[u][i].zw;
+      }
+    }
+  }
+}
+
+// Epilogue of a row finished in the tiled kernel: this lane holds the 4-column
+// groups 4 ch[i] .. 4 ch[i] + 3 (tile_chunk order), acc[i] = {cols 0-1, cols 2-3}.
+template <int EPI, int NQ>
+__device__ __forceinline__ void spmm_tile_epilogue(const SpmmBfArgs& a, int r, const int (&ch)[2 * NQ],
+                                                   const f32x2 (&acc)[2 * NQ][2]) {
+#pragma unroll
+  for (int i = 0; i < 2 * NQ; ++i) {
+    const int col = 4 * ch[i];
+    if (col >= a.width) continue;
+    const float v[4] = {acc[i][0].x, acc[i][0].y, acc[i][1].x, acc[i][1].y};
+    if constexpr (EPI == SND_SPMM_PLAIN) {
+      bf16x4 o;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) o[k] = (__bf16)v[k];
+      *reinterpret_cast<bf16x4*>(a.out + (long long)r * a.ldo + col) = o;
+    } else {
+      *reinterpret_cast<float4*>(a.pre + (long long)r * a.ldp + col) = make_float4(v[0], v[1], v[2], v[3]);
+      bf16x4 o;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int c = col + k;
+        const float b1 = lrelu(v[k]) * (a.g1[c] * kBnC) + a.b1[c];    // H2[:, :h1]
+        o[k] = (__bf16)(b1 * (a.ge[c] * kBnC) + a.be[c]);             // encoder_g BN
+      }
+      *reinterpret_cast<bf16x4*>(a.g + (long long)r * a.ldg + col) = o;
+    }
+  }
+  if constexpr (EPI == SND_SPMM_GCN) {
+    if ((threadIdx.x & (LPR - 1)) == 0) {   // concat X (model.py:109) -> encoder_g BN on those columns
+      float g[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int c = a.width + j;
+        g[j] = j < a.f ? a.x[(long long)r * a.ldx + j] * (a.ge[c] * kBnC) + a.be[c] : 0.f;
+      }
+      *reinterpret_cast<uint4*>(a.g + (long long)r * a.ldg + a.width) = to_bf16x8(g);
+    }
+  }
+}
+
+// Tile run of workgroup b: tiles [lo, hi) of the XCD-major tile list.  With tpg
+// tiles per graph and ngraphs % 8 == 0 (and the grid a multiple of 8), XCD x
+// = b % 8 owns the graphs g = x (mod 8) and its workgroups split that list into
+// contiguous runs; otherwise the tiles are split contiguously.
+struct TileRun {
+  int lo, hi, tpg, x;
+  __device__ int tile(int i) const {
+    if (tpg <= 0) return i;
+    const int gi = i / tpg;
+    return (x + 8 * gi) * tpg + (i - gi * tpg);
+  }
+};
+
+__device__ __forceinline__ TileRun tile_run(int ntiles, int tpg, int ngraphs) {
+  const int G = gridDim.x, b = blockIdx.x;
+  if (tpg > 0 && ngraphs % 8 == 0 && G % 8 == 0 && ntiles == tpg * ngraphs) {
+    const int x = b & 7, l = b >> 3, gx = G >> 3, tx = ntiles >> 3;
+    return TileRun{(int)((long long)l * tx / gx), (int)((long long)(l + 1) * tx / gx), tpg, x};
+  }
+  return TileRun{(int)((long long)b * ntiles / G), (int)((long long)(b + 1) * ntiles / G), 0, 0};
+}
+
+template <int NQ, int RPG>
+struct TileMeta {                 // stage 1: row slots and set ids of a tile
+  int r[RPG], s[RPG], e[RPG];
+  int uc[tile_chunks<NQ>()];
+};
+template <int NQ, int RPG>
+struct TileRows {                 // stage 2: the tile's rows (bf16 chunks) and first local ids
+  u32x4 raw[tile_chunks<NQ>()];
+  int pre[RPG][TPRE];
+};
+
+// RPG rows per 8-lane group: 1 for tiles of <= 64 rows, 2 for <= 128.
+// Image row 0 is the zero row, row 1 + u holds set entry u (lcol = 1 + u).
+template <int EPI, int NQ, int RPG>
+__global__ void __launch_bounds__(TNT) __attribute__((amdgpu_waves_per_eu(NQ == 1 ? 4 : 2)))
+spmm_bf16_tiled_kernel(SpmmBfArgs a, int ntiles, int tpg) {
+  extern __shared__ f32x4 img[];   // [ustride + 1][16 NQ float4]
+  constexpr int CPR = 8 * NQ;      // 16-byte bf16 chunks per row in HBM
+  constexpr int TSC = tile_chunks<NQ>();
+  const int sub = threadIdx.x & (LPR - 1), grp = threadIdx.x / LPR;
+  const int ust = a.t_ustride;
+  const int nchunk = (ust + 1) * CPR;           // image chunks incl. the zero row
+  const __amdgpu_buffer_rsrc_t rs = rows_rsrc(a.h, (long long)a.R * a.ldh * 2);
+  const TileRun run = tile_run(ntiles, tpg, a.ngraphs);
+  const int count = run.hi - run.lo;
+
+  auto stage1 = [&](int t, TileMeta<NQ, RPG>& m) {
+#pragma unroll
+    for (int j = 0; j < RPG; ++j) {
+      const int ls = grp + j * TG, slot = t * a.t_rows + ls;
+      const bool v = ls < a.t_rows && slot < a.R;
+      m.r[j] = v ? a.t_rowid[slot] : -1;
+      m.s[j] = v ? a.t_trp[slot] : 0;
+      m.e[j] = v ? a.t_trp[slot + 1] : 0;
+    }
+#pragma unroll
+    for (int c = 0; c < TSC; ++c) {
+      const int u = (threadIdx.x + c * TNT) / CPR - 1;              // set entry (-1: zero row)
+      m.uc[c] = (u >= 0 && u < ust) ? a.t_ucol[(long long)t * ust + u] : -1;   // -1: zeros
+    }
+  };
+  auto stage2 = [&](const TileMeta<NQ, RPG>& m, TileRows<NQ, RPG>& w) {
+#pragma unroll
+    for (int c = 0; c < TSC; ++c) {
+      const int ch = (threadIdx.x + c * TNT) % CPR;
+      w.raw[c] = __builtin_amdgcn_raw_buffer_load_b128(rs, (unsigned)m.uc[c] * (2u * a.ldh) + 16u * ch, 0, 0);
+    }
+#pragma unroll
+    for (int j = 0; j < RPG; ++j)
+#pragma unroll
+      for (int q = 0; q < TPRE; ++q) {
+        const int k = m.s[j] + 8 * q + sub;
+        w.pre[j][q] = k < m.e[j] ? (int)a.t_lcol[k] : 0;
+      }
+  };
+  // exact bf16 -> fp32 widening of the staged rows into the image (the zero row
+  // and the set's rows; set padding is skipped)
+  auto write_image = [&](const TileMeta<NQ, RPG>& m, const TileRows<NQ, RPG>& w) {
+#pragma unroll
+    for (int c = 0; c < TSC; ++c) {
+      const int cidx = threadIdx.x + c * TNT;
+      if (cidx < nchunk && (cidx < CPR || m.uc[c] >= 0)) {
+        const u32x4 v = w.raw[c];
+        f32x4 lo, hi;
+        lo.x = __uint_as_float(v[0] << 16); lo.y = __uint_as_float(v[0] & 0xFFFF0000u);
+        lo.z = __uint_as_float(v[1] << 16); lo.w = __uint_as_float(v[1] & 0xFFFF0000u);
+        hi.x = __uint_as_float(v[2] << 16); hi.y = __uint_as_float(v[2] & 0xFFFF0000u);
+        hi.z = __uint_as_float(v[3] << 16); hi.w = __uint_as_float(v[3] & 0xFFFF0000u);
+        img[2 * cidx] = lo;
+        img[2 * cidx + 1] = hi;
+      }
+    }
+  };
+
+  int ch[2 * NQ], chb[2 * NQ];     // this lane's float4 chunks of a row, and their byte offsets
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) {
+    ch[2 * q] = 16 * q + tile_chunk(sub, 0);
+    ch[2 * q + 1] = 16 * q + tile_chunk(sub, 1);
+  }
+#pragma unroll
+  for (int i = 0; i < 2 * NQ; ++i) chb[i] = 16 * ch[i];
+  TileMeta<NQ, RPG> m0, m1;        // m0: the tile in the image, m1: the next one
+  TileRows<NQ, RPG> w;
+  if (count > 0) {
+    stage1(run.tile(run.lo), m0);
+    stage2(m0, w);
+    if (count > 1) stage1(run.tile(run.lo + 1), m1);
+    write_image(m0, w);
+  }
+  __syncthreads();
+  // the previous tile's sums: stored after the next loads are issued, so no wait for
+  // a store stands between two tiles' loads
+  int prr[RPG];
+  f32x2 acc[RPG][2 * NQ][2];
+#pragma unroll
+  for (int j = 0; j < RPG; ++j) prr[j] = -1;
+  // one tile: cur = its metadata (then reused for tile i+2's), nxt = tile i+1's.  The
+  // loop runs two tiles per trip with the roles swapped, so no register copy of an
+  // in-flight load forces a wait.
+  auto body = [&](int i, TileMeta<NQ, RPG>& cur, TileMeta<NQ, RPG>& nxt) {
+    int rr[RPG], s0[RPG], e0[RPG], pre[RPG][TPRE];
+#pragma unroll
+    for (int j = 0; j < RPG; ++j) {
+      rr[j] = cur.r[j]; s0[j] = cur.s[j]; e0[j] = cur.e[j];
+#pragma unroll
+      for (int q = 0; q < TPRE; ++q) pre[j][q] = w.pre[j][q];
+    }
+    if (i + 1 < count) stage2(nxt, w);             // tile i+1: rows + first local ids
+#pragma unroll
+    for (int j = 0; j < RPG; ++j)
+      if (prr[j] >= 0) spmm_tile_epilogue<EPI, NQ>(a, prr[j], ch, acc[j]);
+    if (i + 2 < count) stage1(run.tile(run.lo + i + 2), cur);   // tile i+2: slots + set ids
+#pragma unroll
+    for (int j = 0; j < RPG; ++j) {
+      prr[j] = rr[j];
+#pragma unroll
+      for (int q = 0; q < 2 * NQ; ++q) acc[j][q][0] = acc[j][q][1] = (f32x2){0.f, 0.f};
+      if (j * TG >= a.t_rows) break;               // uniform: no slot of this pass in any tile
+      const int s = s0[j], e = e0[j];
+      // trip counts: a tile's rows are sorted by degree, so the wave's first row (lane 0)
+      // is its longest; shorter and empty rows read the zero row
+      const int dm = __builtin_amdgcn_readfirstlane(e - s);
+      if (dm > 0) lds_round16<NQ>(pre[j][0], pre[j][1], min(16, dm), img, chb, acc[j]);
+      if (dm > 16) lds_round16<NQ>(pre[j][2], pre[j][3], min(16, dm - 16), img, chb, acc[j]);
+      for (int o = 8 * TPRE; o < dm; o += 16) {
+        const int id0 = s + o + sub < e ? (int)a.t_lcol[s + o + sub] : 0;
+        const int id1 = s + o + 8 + sub < e ? (int)a.t_lcol[s + o + 8 + sub] : 0;
+        lds_round16<NQ>(id0, id1, min(16, dm - o), img, chb, acc[j]);
+      }
+    }
+    __syncthreads();                               // every wave is done with this image
+    if (i + 1 < count) write_image(nxt, w);        // the next tile (its loads ran during the sums)
+    __syncthreads();
+  };
+  for (int i = 0; i < count; i += 2) {
+    body(i, m0, m1);
+    if (i + 1 < count) body(i + 1, m1, m0);
+  }
+#pragma unroll
+  for (int j = 0; j < RPG; ++j)
+    if (prr[j] >= 0) spmm_tile_epilogue<EPI, NQ>(a, prr[j], ch, acc[j]);
 }
 
 // ---------------------------------------------------------------- per-edge CE terms (bf16 z)
@@ -462,22 +751,59 @@ int launch_gcn0(const Gcn0Args& a, hipStream_t s) {
   return 0;
 }
 
+template <typename K>
+static int tile_lds_attr(K kern, int bytes) {
+  return hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                             bytes) == hipSuccess ? 0 : SND_ERR_HIP;
+}
+
+template <int EPI>
+static int launch_spmm_bf16_epi(const SpmmBfArgs& a, bool two, hipStream_t s) {
+  if (a.t_rows > 0 && a.t_ustride <= TILE_CAP) {
+    static const int attr = tile_lds_attr(spmm_bf16_tiled_kernel<EPI, 1, 1>, tile_lds_bytes<1>()) |
+                            tile_lds_attr(spmm_bf16_tiled_kernel<EPI, 1, 2>, tile_lds_bytes<1>()) |
+                            tile_lds_attr(spmm_bf16_tiled_kernel<EPI, 2, 1>, tile_lds_bytes<2>()) |
+                            tile_lds_attr(spmm_bf16_tiled_kernel<EPI, 2, 2>, tile_lds_bytes<2>());
+    if (attr) { set_error("spmm_bf16_tiled: hipFuncSetAttribute failed"); return SND_ERR_HIP; }
+    const int ntiles = cdiv(a.R, a.t_rows);
+    const size_t lds = (size_t)(a.t_ustride + 1) * 256 * (two ? 2 : 1);
+    const int tpg = (a.npg > 0 && a.npg % a.t_rows == 0 && a.ngraphs % 8 == 0 &&
+                     (long long)a.npg * a.ngraphs == a.R) ? a.npg / a.t_rows : 0;
+    const int per_cu = std::max(1, std::min(2, (160 * 1024) / (int)std::max<size_t>(lds, 1)));
+    const int grid = std::min(ntiles, 256 * per_cu);
+    const bool one = a.t_rows <= TG;
+#define SND_TILED(NQ, RPG) \
+  hipLaunchKernelGGL((spmm_bf16_tiled_kernel<EPI, NQ, RPG>), dim3(grid), dim3(TNT), lds, s, a, ntiles, tpg)
+    if (two) { if (one) SND_TILED(2, 1); else SND_TILED(2, 2); }
+    else { if (one) SND_TILED(1, 1); else SND_TILED(1, 2); }
+#undef SND_TILED
+    return 0;
+  }
+  // no tiles, or a tile set beyond the LDS image: the register-gather kernel
+  SND_CHECK_ARG(a.colidx || a.R == 0, "spmm_bf16: colidx");
+  dim3 grid(cdiv(a.R, RPB));
+  if (two) hipLaunchKernelGGL((spmm_bf16_kernel<EPI, 2>), grid, dim3(NT), 0, s, a);
+  else hipLaunchKernelGGL((spmm_bf16_kernel<EPI, 1>), grid, dim3(NT), 0, s, a);
+  return 0;
+}
+
 int launch_spmm_bf16(const SpmmBfArgs& a, hipStream_t s) {
   if (a.R <= 0) return 0;
   SND_CHECK_ARG(a.width % 8 == 0 && a.width <= 128 && a.ldh % 8 == 0, "spmm_bf16: width %% 8 <= 128, ldh %% 8");
   SND_CHECK_ARG((long long)a.R * a.ldh * 2 < (1ll << 31), "spmm_bf16: rows x ldh beyond the 2 GB buffer range");
-  dim3 grid(cdiv(a.R, RPB));
+  SND_CHECK_ARG(a.t_rows >= 0 && a.t_rows <= TRPG * TG, "spmm_bf16: tile_rows <= 128");
+  SND_CHECK_ARG(a.t_rows == 0 || (a.t_rowid && a.t_trp && a.t_lcol && a.t_ucol && a.t_ustride >= 0 &&
+                                  a.t_ustride <= 65535),
+                "spmm_bf16: row tiles need rows, trp, lcol, ucol and 0 <= ustride <= 65535");
   const bool two = a.width > 64;
   if (a.epi == SND_SPMM_PLAIN) {
     SND_CHECK_ARG(a.out && a.ldo % 8 == 0, "spmm_bf16: out");
-    if (two) hipLaunchKernelGGL((spmm_bf16_kernel<SND_SPMM_PLAIN, 2>), grid, dim3(NT), 0, s, a);
-    else hipLaunchKernelGGL((spmm_bf16_kernel<SND_SPMM_PLAIN, 1>), grid, dim3(NT), 0, s, a);
+    SND_TRY(launch_spmm_bf16_epi<SND_SPMM_PLAIN>(a, two, s));
   } else {
     SND_CHECK_ARG(a.pre && a.g && a.g1 && a.b1 && a.ge && a.be && a.x && a.f <= 8 &&
                       a.ldp % 4 == 0 && a.ldg % 8 == 0 && a.ldg >= a.width + 8,
                   "spmm_bf16: GCN operands");
-    if (two) hipLaunchKernelGGL((spmm_bf16_kernel<SND_SPMM_GCN, 2>), grid, dim3(NT), 0, s, a);
-    else hipLaunchKernelGGL((spmm_bf16_kernel<SND_SPMM_GCN, 1>), grid, dim3(NT), 0, s, a);
+    SND_TRY(launch_spmm_bf16_epi<SND_SPMM_GCN>(a, two, s));
   }
   SND_LAUNCH_CHECK("spmm_bf16_kernel");
   return 0;
@@ -544,5 +870,21 @@ extern "C" int snd_csr_spmm_bf16(const int* rowptr, const int* colidx, int n_row
   a.xcd_nbg = (n_per_graph > 0 && n_graphs > 0 && (long long)n_per_graph * n_graphs == n_rows)
                   ? xcd_nbg(n_per_graph, n_graphs) : 0;
   a.row_order = row_order;
+  return launch_spmm_bf16(a, (hipStream_t)stream);
+}
+
+extern "C" int snd_csr_spmm_bf16_tiled(const int* rowptr, const int* colidx, int n_rows,
+                                       const snd_row_tiles_t* tiles, const void* h, int ldh, int width,
+                                       void* out, int ldo, int n_per_graph, int n_graphs,
+                                       const int* row_order, snd_stream_t stream) {
+  SND_CHECK_ARG(rowptr && (colidx || n_rows == 0) && h && out && n_rows >= 0 && tiles && tiles->tile_rows > 0,
+                "snd_csr_spmm_bf16_tiled: null operand or no tiles");
+  SpmmBfArgs a{rowptr, colidx, n_rows, reinterpret_cast<const __bf16*>(h), ldh, width,
+               SND_SPMM_PLAIN, reinterpret_cast<__bf16*>(out), ldo};
+  a.xcd_nbg = 0;
+  a.row_order = row_order;
+  a.t_rowid = tiles->rows; a.t_trp = tiles->trp; a.t_lcol = tiles->lcol; a.t_ucol = tiles->ucol;
+  a.t_rows = tiles->tile_rows; a.t_ustride = tiles->ustride;
+  a.npg = n_per_graph; a.ngraphs = n_graphs;
   return launch_spmm_bf16(a, (hipStream_t)stream);
 }

@@ -128,7 +128,7 @@ struct snd_plan {
 };
 
 extern "C" const char* snd_last_error(void) { return g_err; }
-extern "C" int snd_abi_version(void) { return 4; }
+extern "C" int snd_abi_version(void) { return 5; }
 
 extern "C" int snd_plan_create(const snd_config_t* cfg, int n_graphs, snd_plan_t** out) {
   SND_CHECK_ARG(cfg && out && n_graphs > 0, "snd_plan_create: bad args");
@@ -653,6 +653,15 @@ int pack_decoder(const Ctx& x) {
   return launch_pack(e, 12, x.s);
 }
 
+// optional row tiles of the batch (snd_row_tiles_t): the SpMM stages neighbour rows in LDS
+static void use_tiles(SpmmBfArgs& a, const snd_batch_t* batch, int npg, int ngraphs) {
+  a.row_order = batch->row_order;
+  if (batch->tiles.tile_rows <= 0) return;
+  a.t_rowid = batch->tiles.rows; a.t_trp = batch->tiles.trp; a.t_lcol = batch->tiles.lcol;
+  a.t_ucol = batch->tiles.ucol; a.t_rows = batch->tiles.tile_rows; a.t_ustride = batch->tiles.ustride;
+  a.npg = npg; a.ngraphs = ngraphs;
+}
+
 // encoder forward (model.py:104-115): H1 -> XW1 -> GCN1 -> heads h, [mu | logstd]
 int encoder_fast_fwd(const Ctx& x, const snd_batch_t* batch) {
   const snd_plan& p = *x.p;
@@ -675,7 +684,7 @@ int encoder_fast_fwd(const Ctx& x, const snd_batch_t* batch) {
     SpmmBfArgs a{batch->rowptr, batch->colidx, R, bf("FXW1"), h1, h1, SND_SPMM_GCN, nullptr, 0,
                  x.f("FP1"), h1, x.w("enc.bn1.gamma"), x.w("enc.bn1.beta"), batch->features, f, f,
                  x.w("enc.bne.gamma"), x.w("enc.bne.beta"), bf("FG"), p.ldg, xcd_nbg(p.N, p.B)};
-    a.row_order = batch->row_order;
+    use_tiles(a, batch, p.N, p.B);
     SND_TRY(launch_spmm_bf16(a, x.s));
   }
   if (p.tref) return 0;   // graph heads: snd_tref.hip on bf16 flat(G)
@@ -736,7 +745,7 @@ int encoder_fast_bwd_tail(const Ctx& x, const snd_batch_t* batch) {
   {
     SpmmBfArgs a{batch->rowptr, batch->colidx, R, bf("FDP1"), h1, h1, SND_SPMM_PLAIN, bf("FDXW1"), h1};
     a.xcd_nbg = xcd_nbg(p.N, p.B);
-    a.row_order = batch->row_order;
+    use_tiles(a, batch, p.N, p.B);
     SND_TRY(launch_spmm_bf16(a, x.s));
   }
   SND_TRY(fork(x));
@@ -1013,7 +1022,7 @@ extern "C" int snd_plan_launch(const snd_plan_t* plan, const snd_batch_t* batch,
     SpmmBfArgs a{batch->rowptr, batch->colidx, p.R, (const __bf16*)(ws + p.buf("FDP1")), p.c.h1,
                  p.c.h1, SND_SPMM_PLAIN, (__bf16*)(ws + p.buf("FDXW1")), p.c.h1};
     a.xcd_nbg = xcd_nbg(p.N, p.B);
-    a.row_order = batch->row_order;
+    use_tiles(a, batch, p.N, p.B);
     return launch_spmm_bf16(a, s);
   }
   if (!strncmp(kernel, "tref_", 5)) {   // graph-latent weight-streaming kernels

@@ -187,6 +187,53 @@ def locality_order(batch: GraphBatch) -> np.ndarray:
     return out
 
 
+def default_tile_rows(width: int) -> int:
+    """Rows per SpMM tile: 64.  The tile's neighbour set of an RCM-ordered RGG
+    (<= ~310 rows at N = 4096 and 16384) then fits the 319-row fp32 LDS image
+    (80 KB at width 64, two workgroups per CU; 160 KB at width 128)."""
+    return 64
+
+
+@dataclass
+class RowTiles:
+    """Host image of snd_row_tiles_t (see include/snd_vae.h)."""
+    rows: np.ndarray     # int32 [R]      tile slot -> row (by degree inside a tile)
+    trp: np.ndarray      # int32 [R+1]    slot-order row pointers into lcol
+    lcol: np.ndarray     # uint16 [nnz]   local neighbour ids, slot order
+    ucol: np.ndarray     # int32 [T*ustride] tile sets, padded with -1
+    tile_rows: int
+    ustride: int
+
+
+def row_tiles(batch: GraphBatch, order: Optional[np.ndarray], tile_rows: int) -> RowTiles:
+    """Row tiles of the bf16 SpMM over the schedule ``order`` (None = natural).
+
+    Built on the host by the library's snd_spmm_tile_plan (plain C++, no GPU)
+    once per batch."""
+    import ctypes
+
+    from . import _lib
+    L = _lib.lib()
+    R = batch.n_graphs * batch.n_nodes
+    rp = np.ascontiguousarray(batch.rowptr, np.int32)
+    ci = np.ascontiguousarray(batch.colidx, np.int32)
+    od = None if order is None else np.ascontiguousarray(order, np.int32)
+    P = lambda a: None if a is None else a.ctypes.data
+    ust = ctypes.c_int(0)
+    n = L.snd_spmm_tile_plan(P(rp), P(ci), R, P(od), tile_rows, None, None, None, None, ctypes.byref(ust))
+    if n < 0:
+        raise _lib.SNDError(f"snd_spmm_tile_plan failed ({n}): {_lib.last_error()}")
+    rows = np.zeros(max(R, 1), np.int32)
+    trp = np.zeros(R + 1, np.int32)
+    lcol = np.zeros(max(len(ci), 1), np.uint16)
+    ucol = np.zeros(max(n, 1), np.int32)
+    n2 = L.snd_spmm_tile_plan(P(rp), P(ci), R, P(od), tile_rows, P(rows), P(trp), P(lcol), P(ucol),
+                              ctypes.byref(ust))
+    if n2 != n:
+        raise _lib.SNDError(f"snd_spmm_tile_plan failed ({n2}): {_lib.last_error()}")
+    return RowTiles(rows, trp, lcol, ucol, tile_rows, int(ust.value))
+
+
 def shard(batch: GraphBatch, rank: int, world: int) -> GraphBatch:
     """Contiguous equal shard of the global batch for DP rank ``rank``.
 

@@ -81,6 +81,22 @@ def spmm_bf16(rowptr, colidx, h, n_per_graph=0, n_graphs=0, row_order=None):
     return out
 
 
+def spmm_bf16_tiled(rowptr, colidx, tiles, h, n_per_graph=0, n_graphs=0, row_order=None):
+    """spmm_bf16 over row tiles (snd_csr_spmm_bf16_tiled): neighbour rows staged in LDS.
+
+    tiles: model.DeviceTiles over the schedule row_order (data.row_tiles);
+    bit-identical to spmm_bf16."""
+    if not (h.is_cuda and h.is_contiguous() and h.dtype == torch.bfloat16):
+        raise ValueError("spmm_bf16_tiled: expected a contiguous bfloat16 device tensor")
+    rows, width = h.shape
+    out = torch.empty_like(h)
+    t = tiles.c_struct()
+    _lib.check(_lib.lib().snd_csr_spmm_bf16_tiled(
+        _P(rowptr), _P(colidx), rows, C.byref(t), _P(h), width, width, _P(out), width,
+        n_per_graph, n_graphs, _P(row_order), _lib.stream_ptr()), "snd_csr_spmm_bf16_tiled")
+    return out
+
+
 def linear(x, w, b=None, dtype="f32", trans_w=False):
     """x @ w + b (layers.py:566-576) on MFMA (fp32 or bf16 operands, fp32 acc)."""
     _need(x, "linear x")

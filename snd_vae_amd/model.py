@@ -24,7 +24,7 @@ import torch
 
 from . import _lib
 from .config import SNDConfig
-from .data import GraphBatch, locality_order
+from .data import GraphBatch, locality_order, row_tiles
 from .params import flat_layout, init_blocks
 
 DTYPES = {"f32": 0, "fp32": 0, "bf16": 1}
@@ -40,12 +40,29 @@ def c_config(cfg: SNDConfig, dtype: str) -> _lib.Config:
                        DTYPES[dtype], _lib.TOPOLOGY[cfg.topology], cfg.node_h_size)
 
 
+class DeviceTiles:
+    """data.RowTiles resident in HBM (snd_row_tiles_t)."""
+
+    def __init__(self, rt, device="cuda"):
+        t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(device)
+        self.rows, self.trp, self.ucol = t(rt.rows), t(rt.trp), t(rt.ucol)
+        self.lcol = t(rt.lcol.view(np.int16))
+        self.tile_rows, self.ustride = rt.tile_rows, rt.ustride
+
+    def c_struct(self) -> _lib.RowTiles:
+        p = _lib.ptr
+        return _lib.RowTiles(p(self.rows), p(self.trp), p(self.lcol), p(self.ucol), self.tile_rows,
+                             self.ustride)
+
+
 class DeviceBatch:
     """A GraphBatch resident in HBM (the feed dict of `main.py:327-329`)."""
 
-    def __init__(self, batch: GraphBatch, device="cuda", locality: bool = True):
+    def __init__(self, batch: GraphBatch, device="cuda", locality: bool = True, tile_rows: int = 64):
         """locality: upload the per-graph RCM row schedule of the gather kernels
-        (data.locality_order); results do not depend on it."""
+        (data.locality_order); results do not depend on it.  tile_rows > 0 (with
+        locality) also uploads the SpMM row tiles over that schedule
+        (data.row_tiles, data.default_tile_rows); bit-identical results."""
         t = lambda a, dt: torch.from_numpy(np.ascontiguousarray(a)).to(device=device, dtype=dt)
         self.n_graphs = batch.n_graphs
         self.n_nodes = batch.n_nodes
@@ -55,13 +72,18 @@ class DeviceBatch:
         self.features = t(batch.features, torch.float32)
         self.feature_truth = t(batch.feature_truth, torch.float32)
         self.spatial_truth = t(batch.spatial_truth, torch.float32)
-        self.row_order = t(locality_order(batch), torch.int32) if locality and batch.nnz else None
+        order = locality_order(batch) if locality and batch.nnz else None
+        self.row_order = t(order, torch.int32) if order is not None else None
+        self.tiles = None
+        if order is not None and tile_rows > 0:
+            self.tiles = DeviceTiles(row_tiles(batch, order, tile_rows), device)
         self.host = batch
 
     def c_struct(self) -> _lib.Batch:
         p = _lib.ptr
+        tl = self.tiles.c_struct() if self.tiles else _lib.RowTiles()
         return _lib.Batch(p(self.rowptr), p(self.colidx), p(self.features),
-                          p(self.feature_truth), p(self.spatial_truth), p(self.row_order))
+                          p(self.feature_truth), p(self.spatial_truth), p(self.row_order), tl)
 
 
 class SGCNModelVAE:

@@ -27,6 +27,7 @@ import torch
 
 from . import checkpoint as ckpt
 from .config import SNDConfig
+from .data import default_tile_rows
 from .input_data import SynDataset
 from .model import DeviceBatch, SGCNModelVAE
 from .optimizer import LOSS_NAMES, OptimizerVAE
@@ -55,7 +56,8 @@ class Trainer:
         for i in range(self.batch_num):
             lo = i * batch_size + rank * per
             self.batches.append(DeviceBatch(dataset.batch(cfg, range(lo, lo + per)), device=device,
-                                            locality=locality))
+                                            locality=locality,
+                                            tile_rows=default_tile_rows(cfg.g_conv_hidden[1])))
         self.model = SGCNModelVAE(cfg, per, dtype=dtype, device=device, blocks=blocks)
         self.opt = OptimizerVAE(self.model, process_group=process_group, seed=seed)
         self.use_graphs = use_graphs

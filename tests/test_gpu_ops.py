@@ -34,6 +34,15 @@ def rel(a, b):
     return np.abs(a - b).max() / max(np.abs(b).max(), 1e-30)
 
 
+def rand_batch_csr(n, B, kbar, seed):
+    parts = []
+    for b in range(B):
+        _, pairs = rgg_edges(n, kbar, np.random.default_rng(seed + b))
+        parts.append(csr_from_pairs(n, pairs))
+    rp, ci = stack_csr(parts, n)
+    return rp, ci, None
+
+
 def rand_batch(n, B, kbar, seed):
     parts = []
     for b in range(B):
@@ -86,6 +95,42 @@ def test_spmm_bf16(n, B, kbar, width):
     out2 = layers.spmm_bf16(cu(rp, torch.int32), cu(ci if len(ci) else np.zeros(1, np.int32), torch.int32),
                             hb.cuda(), n, B, cu(order, torch.int32)).float().cpu().numpy()
     assert np.array_equal(out, out2)
+
+
+@pytest.mark.parametrize("n,B,kbar,width,tile_rows,locality",
+                         [(4096, 8, 16.0, 64, 64, True), (4096, 64, 16.0, 64, 64, True),
+                          (4096, 8, 16.0, 64, 128, True), (4096, 2, 16.0, 64, 64, False),
+                          (2048, 1, 16.0, 128, 64, True), (300, 3, 10.0, 48, 64, True),
+                          (96, 2, 0.0, 64, 32, True), (200, 1, 8.0, 64, 7, True),
+                          (256, 4, 40.0, 64, 64, True), (1000, 3, 16.0, 128, 100, True)])
+def test_spmm_bf16_tiled_bitwise(n, B, kbar, width, tile_rows, locality):
+    """The LDS-staged, pipelined SpMM over row tiles sums every row's neighbours in
+    colidx order: bitwise equal to spmm_bf16.  64 graphs give every workgroup a run
+    of several tiles (the pipeline); natural order at N = 4096 makes the sets exceed
+    the 319-row LDS image, so the launch takes the register-gather kernel; degree
+    ~40 rows take the lcol-reading rounds past the 32 prefetched ids; 100-row tiles
+    put two rows on an 8-lane group."""
+    from snd_vae_amd import layers
+    from snd_vae_amd.data import GraphBatch, locality_order, row_tiles
+    from snd_vae_amd.model import DeviceTiles
+    rp, ci, dense = rand_batch(n, B, kbar, 9) if B <= 8 else rand_batch_csr(n, B, kbar, 9)
+    gb = GraphBatch(B, n, rp, ci, np.zeros((n * B, 1), np.float32), np.zeros((n * B, 1), np.float32),
+                    np.zeros((n * B, 2), np.float32))
+    order = locality_order(gb) if locality else None
+    rt = row_tiles(gb, order, tile_rows)
+    if not locality and n >= 2048:
+        assert rt.ustride > 319                          # the register-gather fallback
+    tiles = DeviceTiles(rt)
+    hb = torch.from_numpy(np.random.default_rng(2).standard_normal((n * B, width)).astype(np.float32)).to(torch.bfloat16)
+    d_rp, d_ci = cu(rp, torch.int32), cu(ci if len(ci) else np.zeros(1, np.int32), torch.int32)
+    d_o = cu(order, torch.int32) if order is not None else None
+    ref = layers.spmm_bf16(d_rp, d_ci, hb.cuda(), n, B, d_o)
+    out = layers.spmm_bf16_tiled(d_rp, d_ci, tiles, hb.cuda(), n, B, d_o)
+    torch.cuda.synchronize()
+    assert torch.equal(out.view(torch.int16), ref.view(torch.int16))
+    if dense is not None:
+        r64 = R.spmm(dense, hb.float().numpy().astype(np.float64), n)
+        assert np.abs(out.float().cpu().numpy() - r64).max() <= 2 ** -7 * max(np.abs(r64).max(), 1.0)
 
 
 def test_graph_convolution_epilogue():

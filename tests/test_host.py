@@ -128,3 +128,46 @@ def test_plan_layout_matches_python(lib_built):
             _lib.check(L.snd_plan_param_block(h, i, ctypes.byref(nm), ctypes.byref(off), ctypes.byref(n)))
             assert (nm.value.decode(), off.value, n.value) == (k, lay.offsets[k], lay.numel(k))
         L.snd_plan_destroy(h)
+
+
+@pytest.mark.parametrize("n,B,kbar,tile_rows,locality", [(4096, 2, 16.0, 64, True), (300, 3, 10.0, 64, False),
+                                                          (96, 2, 0.0, 32, True), (200, 1, 8.0, 7, True),
+                                                          (256, 2, 12.0, 128, True)])
+def test_spmm_tile_plan(lib_built, n, B, kbar, tile_rows, locality):
+    """snd_spmm_tile_plan (host C++) against a numpy restatement: each tile holds
+    its schedule slots' rows sorted by degree (descending, stable), its set is the
+    ascending distinct neighbour rows padded with -1 to ustride, and the slot-order
+    lcol maps every entry back to its column id in colidx order."""
+    from snd_vae_amd.data import GraphBatch, locality_order, row_tiles, csr_from_pairs, rgg_edges, stack_csr
+    parts = []
+    for b in range(B):
+        _, pairs = rgg_edges(n, kbar, np.random.default_rng(11 + b))
+        parts.append(csr_from_pairs(n, pairs))
+    rp, ci = stack_csr(parts, n)
+    gb = GraphBatch(B, n, rp, ci, np.zeros((n * B, 1), np.float32), np.zeros((n * B, 1), np.float32),
+                    np.zeros((n * B, 2), np.float32))
+    order = locality_order(gb) if locality else None
+    rt = row_tiles(gb, order, tile_rows)
+    R = n * B
+    sched = np.arange(R) if order is None else order.astype(np.int64)
+    T = (R + tile_rows - 1) // tile_rows
+    deg = np.diff(rp.astype(np.int64))
+    assert rt.trp[0] == 0 and rt.trp[-1] == len(ci) and len(rt.ucol) >= T * rt.ustride
+    sizes = []
+    for t in range(T):
+        sl = sched[t * tile_rows:(t + 1) * tile_rows]
+        want_rows = sl[np.argsort(-deg[sl], kind="stable")]
+        got_rows = rt.rows[t * tile_rows:t * tile_rows + len(sl)]
+        assert np.array_equal(got_rows, want_rows)
+        cols = np.concatenate([ci[rp[r]:rp[r + 1]] for r in sl] + [np.zeros(0, ci.dtype)])
+        u = np.unique(cols)
+        us = rt.ucol[t * rt.ustride:(t + 1) * rt.ustride]
+        assert np.array_equal(us[:len(u)], u) and np.all(us[len(u):] == -1)
+        sizes.append(len(u))
+        for i, r in enumerate(got_rows):
+            slot = t * tile_rows + i
+            s, e = rt.trp[slot], rt.trp[slot + 1]
+            assert e - s == deg[r]
+            assert np.all(rt.lcol[s:e] >= 1)
+            assert np.array_equal(us[rt.lcol[s:e].astype(np.int64) - 1], ci[rp[r]:rp[r + 1]])
+    assert rt.ustride == max(sizes)

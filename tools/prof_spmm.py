@@ -17,6 +17,7 @@ def main():
     ap.add_argument("--width", type=int, default=64)
     ap.add_argument("--natural-order", action="store_true", help="no XCD-aware row-block order")
     ap.add_argument("--no-locality", action="store_true", help="no RCM row schedule")
+    ap.add_argument("--tile-rows", type=int, default=0, help="> 0: the row-tiled LDS kernel")
     args = ap.parse_args()
     import numpy as np
     import torch
@@ -41,7 +42,24 @@ def main():
     out = torch.empty_like(h)
     L = _lib.lib()
     npg, ng = (0, 0) if args.natural_order else (host.n_nodes, host.n_graphs * c)
-    for _ in range(args.reps):
+    if args.tile_rows > 0:
+        import ctypes
+        from snd_vae_amd.data import GraphBatch, row_tiles
+        z = np.zeros((1, 1), np.float32)
+        big = GraphBatch(host.n_graphs * c, host.n_nodes, rp.astype(np.int32), ci.astype(np.int32), z, z, z)
+        order = None if d_order is None else d_order.cpu().numpy()
+        from snd_vae_amd.model import DeviceTiles
+        rt = row_tiles(big, order, args.tile_rows)
+        dt = DeviceTiles(rt)
+        tiles = dt.c_struct()
+        print("tile rows", args.tile_rows, "ustride", rt.ustride)
+        for _ in range(args.reps):
+            _lib.check(L.snd_csr_spmm_bf16_tiled(d_rp.data_ptr(), d_ci.data_ptr(), R, ctypes.byref(tiles),
+                                                 h.data_ptr(), args.width, args.width, out.data_ptr(),
+                                                 args.width, npg, ng,
+                                                 0 if d_order is None else d_order.data_ptr(),
+                                                 _lib.stream_ptr()))
+    for _ in range(args.reps if args.tile_rows <= 0 else 0):
         _lib.check(L.snd_csr_spmm_bf16(d_rp.data_ptr(), d_ci.data_ptr(), R, h.data_ptr(), args.width,
                                        args.width, out.data_ptr(), args.width, npg, ng,
                                        0 if d_order is None else d_order.data_ptr(),

@@ -21,11 +21,11 @@ def main():
     args = ap.parse_args()
     import torch
     from snd_vae_amd.config import PRESETS, tscale
-    from snd_vae_amd.data import synthetic_batch
+    from snd_vae_amd.data import default_tile_rows, synthetic_batch
     from snd_vae_amd.model import DeviceBatch, SGCNModelVAE
     from snd_vae_amd.optimizer import OptimizerVAE
     cfg = PRESETS[args.config] if args.config else tscale(args.nodes, args.latent)
-    db = DeviceBatch(synthetic_batch(cfg, args.graphs, seed=1000))
+    db = DeviceBatch(synthetic_batch(cfg, args.graphs, seed=1000), tile_rows=default_tile_rows(cfg.g_conv_hidden[1]))
     model = SGCNModelVAE(cfg, args.graphs, dtype=args.dtype)
     opt = OptimizerVAE(model)
     for _ in range(args.steps):
