@@ -106,7 +106,7 @@ def run_workload(cfg, B, args, info, steps=None, warmup=None):
     host = synthetic_batch(cfg, B, seed=1000 + info.rank * B)
     db = DeviceBatch(host, tile_rows=0 if args.no_tiles else default_tile_rows(cfg.g_conv_hidden[1]))
     model = SGCNModelVAE(cfg, B, dtype=args.dtype)
-    opt = OptimizerVAE(model, process_group=info.group if info.world > 1 else None)
+    opt = OptimizerVAE(model, process_group=info.group)
     opt.step(db)          # first step (counts as warm-up): the ELBO of the initial weights
     torch.cuda.synchronize()
     opt.first_losses = {k: round(v, 6) for k, v in opt.loss_dict().items()}
@@ -296,6 +296,9 @@ def main():
     ap.add_argument("--kernel-reps", type=int, default=20)
     ap.add_argument("--cpu-baseline-seconds", type=float, default=20.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--force-dist", action="store_true",
+                    help="under torchrun with one rank: init RCCL and run the gradient all-reduce "
+                         "(the N>1 step, captured in the HIP graph) anyway")
     ap.add_argument("--spmm-copies", type=int, default=32,
                     help="secondary roofline: SpMM over this many copies of the batch (8 x 32 graphs)")
     ap.add_argument("--extra", default="C4,C5",
@@ -307,7 +310,7 @@ def main():
     from snd_vae_amd.config import tscale
     from snd_vae_amd.parallel import init_from_env
 
-    info = init_from_env("nccl")
+    info = init_from_env("nccl", force=args.force_dist)
     if info.world != args.gpus:
         log(f"warning: --gpus {args.gpus} but WORLD_SIZE {info.world}")
     torch.cuda.set_device(info.local_rank)
@@ -378,7 +381,7 @@ def main():
         out["cpu_baseline"] = cpu_baseline(N, d, args.cpu_baseline_seconds)
     if info.rank == 0:
         print(json.dumps(out), flush=True)
-    if info.world > 1:
+    if info.group is not None:
         import torch.distributed as dist
         dist.destroy_process_group()
 

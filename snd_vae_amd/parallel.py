@@ -25,10 +25,12 @@ class DistInfo:
     group: object = None
 
 
-def init_from_env(backend: str = "nccl") -> DistInfo:
-    """torchrun-style init; single process when WORLD_SIZE is unset or 1."""
+def init_from_env(backend: str = "nccl", force: bool = False) -> DistInfo:
+    """torchrun-style init; single process when WORLD_SIZE is unset or 1, unless
+    ``force`` (a torchrun world of 1: the N>1 code path, collectives included,
+    rehearsed on one GPU)."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
-    if world <= 1:
+    if world <= 1 and not (force and "RANK" in os.environ):
         return DistInfo()
     import torch.distributed as dist
     rank = int(os.environ["RANK"])
