@@ -11,7 +11,7 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libsndvae.so")
+LIB_PATH = os.environ.get("SND_LIB_PATH") or os.path.join(_HERE, "libsndvae.so")   # override: A/B builds
 
 c_int, c_ll, c_float, c_size, c_ull = C.c_int, C.c_longlong, C.c_float, C.c_size_t, C.c_ulonglong
 vp = C.c_void_p
