@@ -485,7 +485,11 @@ __device__ __forceinline__ void chunk_epilogue3(const f32x4& X0, const f32x4& X1
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
     const float xv = e < 4 ? X0[e] : X1[e - 4];
-    const float ex = __builtin_amdgcn_exp2f(-fabsf(xv));
+    // 2^-|x| with the -|x| input modifier written out, so the |x| below folds into
+    // the add's own source modifier instead of a shared v_and: one VALU op per
+    // logit fewer (163 vs 179 per loop trip), 2-3 % on the kernel
+    float ex;
+    asm volatile("v_exp_f32_e64 %0, -|%1|" : "=v"(ex) : "v"(xv));
     const float qd = 1.f + ex;
     const float rc = __builtin_amdgcn_rcpf(qd);
     const bool pos = xv > 0.f;
