@@ -30,6 +30,8 @@
 // in that XCD's L2.
 // fp32 parity mode uses the exact-f32 MFMA 16x16x4 with the same structure.
 #include "snd_zzt.hpp"
+
+#include <type_traits>
 #include "snd_spmm.hpp"
 
 #include <algorithm>
@@ -485,11 +487,10 @@ __device__ __forceinline__ void chunk_epilogue3(const f32x4& X0, const f32x4& X1
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
     const float xv = e < 4 ? X0[e] : X1[e - 4];
-    // 2^-|x| with the -|x| input modifier written out, so the |x| below folds into
-    // the add's own source modifier instead of a shared v_and: one VALU op per
-    // logit fewer (163 vs 179 per loop trip), 2-3 % on the kernel
-    float ex;
-    asm volatile("v_exp_f32_e64 %0, -|%1|" : "=v"(ex) : "v"(xv));
+    // (an inline-asm v_exp_f32 with the -|x| modifier would drop the v_and hipcc
+    // keeps for |x|, but the hazard recognizer does not see a transcendental inside
+    // asm: a dependent VALU may read the result without the required wait states)
+    const float ex = __builtin_amdgcn_exp2f(-fabsf(xv));
     const float qd = 1.f + ex;
     const float rc = __builtin_amdgcn_rcpf(qd);
     const bool pos = xv > 0.f;
@@ -632,8 +633,10 @@ __global__ void __launch_bounds__(NTH2) zzt_dense_bf16_v3(ZztArgs a) {
   double ltot = 0.0;
   unsigned wcnt = 0;
   const int qa = 2 * half, qb = 2 * half + 1;
-  for (int t = t0; t < ntiles; ++t) {
-    const int cur = (t - t0) & 1;
+  // one tile out of LDS buffer CUR (a compile-time constant: the loop runs two
+  // tiles per trip, so every LDS address is a per-lane base + an immediate)
+  auto tile = [&](int t, auto curc) {
+    constexpr int cur = decltype(curc)::value;
     if (t + 1 < ntiles) gload(t + 1);
     const __bf16* Ls = lds[cur];
     f32x4 Xa0, Xa1, Xb0, Xb1;
@@ -646,7 +649,11 @@ __global__ void __launch_bounds__(NTH2) zzt_dense_bf16_v3(ZztArgs a) {
     pv(Ls, qb, sbv);
     if (t + 1 < ntiles) sstore(cur ^ 1);
     __syncthreads();
-    if (((t - t0) & 7) == 7) {      // keep the fp32 partial sums short
+  };
+  for (int t = t0; t < ntiles; t += 2) {
+    tile(t, std::integral_constant<int, 0>{});
+    if (t + 1 < ntiles) tile(t + 1, std::integral_constant<int, 1>{});
+    if (((t - t0) & 7) == 6) {      // keep the fp32 partial sums short
       ltot += (double)(0.5f * labs + llog);
       labs = 0.f;
       llog = 0.f;
