@@ -495,7 +495,7 @@ __device__ __forceinline__ void chunk_epilogue3(const f32x4& X0, const f32x4& X1
     const float rc = __builtin_amdgcn_rcpf(qd);
     const bool pos = xv > 0.f;
     if (e & 1) prod1 *= qd; else prod0 *= qd;
-    sa += fabsf(xv);
+    sa = __builtin_fmaf(fabsf(xv), 0.5f, sa);   // v_fma_f32 takes |x| as a source modifier (an add gets a v_and)
     sb[e] = (__bf16)(pos ? rc : ex * rc);
     wc += (unsigned)__popcll(__ballot(pos));
   }
@@ -637,7 +637,9 @@ __global__ void __launch_bounds__(NTH2) zzt_dense_bf16_v3(ZztArgs a) {
   // tiles per trip, so every LDS address is a per-lane base + an immediate)
   auto tile = [&](int t, auto curc) {
     constexpr int cur = decltype(curc)::value;
-    if (t + 1 < ntiles) gload(t + 1);
+    // branch-free body (the last tile reloads itself into the idle buffer): one
+    // basic block, so |x| folds into the accumulate as a source modifier
+    gload(min(t + 1, ntiles - 1));
     const __bf16* Ls = lds[cur];
     f32x4 Xa0, Xa1, Xb0, Xb1;
     bf16x8 sa, sbv;
@@ -647,19 +649,19 @@ __global__ void __launch_bounds__(NTH2) zzt_dense_bf16_v3(ZztArgs a) {
     pv(Ls, qa, sa);
     chunk_epilogue3(Xb0, Xb1, sbv, labs, llog, wcnt);
     pv(Ls, qb, sbv);
-    if (t + 1 < ntiles) sstore(cur ^ 1);
+    sstore(cur ^ 1);
     __syncthreads();
   };
   for (int t = t0; t < ntiles; t += 2) {
     tile(t, std::integral_constant<int, 0>{});
     if (t + 1 < ntiles) tile(t + 1, std::integral_constant<int, 1>{});
     if (((t - t0) & 7) == 6) {      // keep the fp32 partial sums short
-      ltot += (double)(0.5f * labs + llog);
+      ltot += (double)(labs + llog);
       labs = 0.f;
       llog = 0.f;
     }
   }
-  ltot += (double)(0.5f * labs + llog);
+  ltot += (double)(labs + llog);
 
   // ---- corrections (row i = i_me; the 4 q4-lanes of a row share them)
   float xd = 0.f, xs = 0.f;           // x_ii and sum_j x_ij (this lane's k-slice)
