@@ -759,7 +759,14 @@ static int tile_lds_attr(K kern, int bytes) {
 
 template <int EPI>
 static int launch_spmm_bf16_epi(const SpmmBfArgs& a, bool two, hipStream_t s) {
-  if (a.t_rows > 0 && a.t_ustride <= TILE_CAP) {
+  // The tiled kernel pays off through its pipeline (runs of tiles per workgroup)
+  // and, for the plain epilogue, its LDS sums; a GraphConvolution epilogue over
+  // at most ~1 tile per workgroup (the step's 8-graph batch) is faster on the
+  // register kernel, whose epilogue stores whole rows per 8-lane group
+  // (16.6 vs 10.8 us at B = 8).  debug bit 2048 keeps the tiles (A/B).
+  const bool gcn_small = EPI == SND_SPMM_GCN && a.t_rows > 0 && cdiv(a.R, a.t_rows) <= 4 * 512 &&
+                         !(debug_flags() & 2048);
+  if (a.t_rows > 0 && a.t_ustride <= TILE_CAP && !gcn_small) {
     static const int attr = tile_lds_attr(spmm_bf16_tiled_kernel<EPI, 1, 1>, tile_lds_bytes<1>()) |
                             tile_lds_attr(spmm_bf16_tiled_kernel<EPI, 1, 2>, tile_lds_bytes<1>()) |
                             tile_lds_attr(spmm_bf16_tiled_kernel<EPI, 2, 1>, tile_lds_bytes<2>()) |

@@ -18,7 +18,7 @@ def main():
     ap.add_argument("--flags", default="0")
     ap.add_argument("--kernels", default="zzt_dense")
     ns = ap.parse_args()
-    args = argparse.Namespace(steps=50, warmup=10, no_graph=False, dtype="bf16")
+    args = argparse.Namespace(steps=50, warmup=10, no_graph=False, dtype="bf16", no_tiles=False)
     info = init_from_env("nccl")
     for f in [int(x) for x in ns.flags.split(",")]:
         _lib.check(_lib.lib().snd_debug_set(f))
