@@ -1017,6 +1017,13 @@ extern "C" int snd_plan_launch(const snd_plan_t* plan, const snd_batch_t* batch,
                p.c.h1, (float*)(ws + p.buf("DXW1")), p.c.h1, SND_SPMM_PLAIN};
     return launch_spmm(a, s);
   }
+  if (!strcmp(kernel, "edge_bf16")) {   // per-edge CE terms of the fast path (A = 1 pairs)
+    SND_CHECK_ARG(p.fast, "snd_plan_launch: edge_bf16 needs the bf16 fast path");
+    EdgeBfArgs ea{batch->rowptr, batch->colidx, p.R, (const __bf16*)(ws + p.buf("ZB")), p.dj, p.c.pos_weight,
+                  (float*)(ws + p.buf("EJ")), (double*)(ws + p.buf("PEDGE")), xcd_nbg(p.N, p.B)};
+    ea.row_order = batch->row_order;
+    return launch_edge_bf16(ea, s);
+  }
   if (!strcmp(kernel, "spmm_bf16")) {   // backward GCN1 SpMM of the fast path: A @ dP1 (bf16)
     SND_CHECK_ARG(p.fast_enc, "snd_plan_launch: spmm_bf16 needs the bf16 fast encoder");
     SpmmBfArgs a{batch->rowptr, batch->colidx, p.R, (const __bf16*)(ws + p.buf("FDP1")), p.c.h1,
