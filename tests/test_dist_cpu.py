@@ -82,3 +82,49 @@ def test_dp_allreduce_equals_full_batch_gradient():
     assert np.allclose(flat[:-1], ref, rtol=1e-12, atol=1e-15)
     assert flat[-1] == pytest.approx(losses["cost"], rel=1e-12)   # mean of shard means
     assert mx == 2.0
+
+
+def _force_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    from snd_vae_amd.parallel import init_from_env, max_over_ranks
+    info = init_from_env("gloo", force=True)
+    t = max_over_ranks(1.5 + rank, info)
+    flat = torch.full((4,), float(rank + 1))
+    dist.all_reduce(flat, group=info.group)
+    q.put((info.world, info.group is not None, t, flat.tolist()))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [1, 2])
+def test_force_dist_init(world):
+    """bench.py --force-dist: under a torchrun environment even a world of 1
+    initialises the process group, so the collective code path (all-reduce,
+    max-over-ranks timing) runs on one device; without force a world of 1 stays
+    single-process."""
+    from snd_vae_amd.parallel import init_from_env
+    old = {k: os.environ.get(k) for k in ("RANK", "WORLD_SIZE")}
+    os.environ.pop("RANK", None)
+    os.environ["WORLD_SIZE"] = "1"
+    try:
+        assert init_from_env("gloo", force=True).group is None        # no torchrun env: no group
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_force_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for w, has_group, t, flat in res:
+        assert w == world and has_group
+        assert t == 1.5 + (world - 1)
+        assert flat == [world * (world + 1) / 2] * 4
