@@ -121,7 +121,7 @@ def run_workload(cfg, B, args, info, steps=None, warmup=None):
     log(f"[rank {info.rank}] warm-up done, loss terms {opt.loss_dict()}")
 
     def barrier():
-        if info.world > 1:
+        if info.group is not None:
             import torch.distributed as dist
             dist.barrier()
 

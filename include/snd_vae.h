@@ -315,6 +315,11 @@ size_t snd_plan_workspace_bytes(const snd_plan_t* plan);
 int snd_plan_fuse_adam(snd_plan_t* plan, float* m, float* v, float lr, float beta1,
                        float beta2, float eps);
 int snd_plan_block_fused(const snd_plan_t* plan, int idx);
+/* Data parallel (ABI 6): the device Philox normals of this plan's head rows start at
+ * global head row `head_row_offset` (rank * n_graphs for SND_TREF, rank * n_graphs *
+ * n_nodes for SND_TSCALE), so every rank of a sharded global batch draws exactly the
+ * eps a single device would draw for those rows (model.py:155-159).  Default 0. */
+int snd_plan_set_rng_offset(snd_plan_t* plan, long long head_row_offset);
 /* Named intermediate buffers inside the workspace (tests / inspection). */
 int snd_plan_buffer(const snd_plan_t* plan, const char* name,
                     long long* byte_offset, long long* numel);

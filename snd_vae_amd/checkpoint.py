@@ -72,3 +72,129 @@ def restore(path: str, model, optimizer=None, strict_config: bool = True) -> Opt
             step = int(f.get_tensor("global_step")[0])
             optimizer.step_counter.fill_(step)
     return step
+
+
+# ---------------------------------------------------------------------------
+# Reference (tf.train.Saver) variable names <-> the flat layout.
+#
+# The reference checkpoint is TF's binary bundle, which needs TensorFlow to
+# read.  The bridge here works on a plain {variable name: array} mapping -- what
+# ``{n: tf.train.load_variable(ckpt, n) for n, _ in tf.train.list_variables(ckpt)}``
+# returns in a TF environment, saved with ``np.savez`` -- and on the same
+# mapping in the other direction.  Names are the TF variable names of the hot
+# path (params.logical_names: e.g. "encoder/g_g1_lin/Matrix", Keras BN
+# "decoder/d_bn_s0/gamma", tf.layers.conv1d "decoder/s1_deconv/kernel"); any
+# outer scope prefix and a ":0" suffix are accepted.  TF1 Adam keeps its slots
+# as "<var>/Adam" (m) and "<var>/Adam_1" (v) and the bias-correction powers
+# "beta1_power" / "beta2_power" (optimizer.py:125,197), from which the global
+# step is recovered.  Keras BN moving statistics must be the frozen
+# inference-mode values (mean 0, variance 1).
+
+def _strip(name: str) -> str:
+    return name[:-2] if name.endswith(":0") else name
+
+
+def _lookup(variables: dict, name: str):
+    hits = [k for k in variables if _strip(k) == name or _strip(k).endswith("/" + name)]
+    if len(hits) > 1:
+        raise ValueError(f"ambiguous reference variable {name!r}: {hits}")
+    return variables[hits[0]] if hits else None
+
+
+def reference_to_blocks(cfg: SNDConfig, variables: dict, beta1: float = 0.9):
+    """{TF variable name: array} -> (blocks, adam_m, adam_v, global_step).
+
+    blocks / adam_m / adam_v are dicts in the params.py layout (adam_m / adam_v /
+    global_step are None when the mapping holds no Adam slots).  Raises on a
+    missing variable, a shape mismatch, or BN moving statistics that are not the
+    frozen (0, 1) the hot path assumes."""
+    import numpy as np
+
+    from .params import block_shapes, logical_names
+    shapes = block_shapes(cfg)
+    blocks = {k: np.zeros(s) for k, s in shapes.items()}
+    has_adam = any(_strip(k).endswith("/Adam") for k in variables)
+    m = {k: np.zeros(s) for k, s in shapes.items()} if has_adam else None
+    v = {k: np.zeros(s) for k, s in shapes.items()} if has_adam else None
+    for name, (blk, sl) in logical_names(cfg).items():
+        val = _lookup(variables, name)
+        if val is None:
+            raise KeyError(f"reference variable {name!r} not found")
+        val = np.asarray(val, dtype=np.float64)
+        dst = blocks[blk][..., sl]
+        if val.shape != dst.shape:
+            raise ValueError(f"{name}: shape {val.shape} != {dst.shape} of {blk}")
+        blocks[blk][..., sl] = val
+        if has_adam:
+            for slot, tgt in (("Adam", m), ("Adam_1", v)):
+                s = _lookup(variables, f"{name}/{slot}")
+                if s is None:
+                    raise KeyError(f"Adam slot {name}/{slot} not found")
+                tgt[blk][..., sl] = np.asarray(s, dtype=np.float64)
+        if name.endswith("/gamma"):       # Keras BN: frozen moving statistics only
+            scope = name[:-len("gamma")]
+            for stat, want in (("moving_mean", 0.0), ("moving_variance", 1.0)):
+                s = _lookup(variables, scope + stat)
+                if s is not None and not np.allclose(s, want):
+                    raise ValueError(f"{scope}{stat} is not the frozen value {want}: "
+                                     "the hot path runs Keras BN in inference mode (SURVEY §0.3)")
+    step = None
+    b1p = _lookup(variables, "beta1_power")
+    if b1p is not None:
+        step = int(round(np.log(float(np.asarray(b1p))) / np.log(beta1)))
+    return blocks, m, v, step
+
+
+def blocks_to_reference(cfg: SNDConfig, blocks: dict, adam_m: Optional[dict] = None,
+                        adam_v: Optional[dict] = None, global_step: Optional[int] = None,
+                        beta1: float = 0.9, beta2: float = 0.999) -> dict:
+    """The inverse of reference_to_blocks: {TF variable name: float32 array},
+    with the Adam slots, bias-correction powers and frozen BN statistics."""
+    import numpy as np
+
+    from .params import logical_names
+    out = {}
+    for name, (blk, sl) in logical_names(cfg).items():
+        out[name] = np.ascontiguousarray(blocks[blk][..., sl], dtype=np.float32)
+        if adam_m is not None:
+            out[name + "/Adam"] = np.ascontiguousarray(adam_m[blk][..., sl], dtype=np.float32)
+            out[name + "/Adam_1"] = np.ascontiguousarray(adam_v[blk][..., sl], dtype=np.float32)
+        if name.endswith("/gamma"):
+            scope = name[:-len("gamma")]
+            out[scope + "moving_mean"] = np.zeros_like(out[name])
+            out[scope + "moving_variance"] = np.ones_like(out[name])
+    if global_step is not None:
+        out["beta1_power"] = np.float32(beta1 ** global_step)
+        out["beta2_power"] = np.float32(beta2 ** global_step)
+    return out
+
+
+def load_reference(path: str, model, optimizer=None) -> Optional[int]:
+    """Load an .npz of reference variables (np.load, allow_pickle=False) into the
+    device model (and optimizer); returns the recovered global step."""
+    import numpy as np
+    with np.load(path, allow_pickle=False) as z:
+        variables = {k: z[k] for k in z.files}
+    b1 = optimizer.beta1 if optimizer is not None else model.cfg.adam_beta1
+    blocks, m, v, step = reference_to_blocks(model.cfg, variables, beta1=b1)
+    model.load_blocks(blocks)
+    if optimizer is not None and m is not None:
+        lay = model.layout
+        pc = model.param_count
+        optimizer.m[:pc].copy_(torch.from_numpy(lay.pack(m, np.float32)))
+        optimizer.v[:pc].copy_(torch.from_numpy(lay.pack(v, np.float32)))
+        if step is not None:
+            optimizer.step_counter.fill_(step)
+    return step
+
+
+def save_reference(path: str, model, optimizer=None) -> None:
+    """Write the device state under the reference variable names (.npz)."""
+    import numpy as np
+    m = v = step = None
+    if optimizer is not None:
+        m, v = optimizer.state_blocks()
+        step = optimizer.global_step
+    out = blocks_to_reference(model.cfg, model.blocks(), m, v, step,
+                              *((optimizer.beta1, optimizer.beta2) if optimizer is not None else ()))
+    np.savez(path, **out)

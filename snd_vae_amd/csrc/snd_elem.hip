@@ -39,7 +39,7 @@ __global__ void __launch_bounds__(256) reparam_fwd_kernel(ReparamFwdArgs a) {
       const long long i = (long long)r * a.L + c;
       const float mu = a.ms[(long long)r * a.ldms + c];
       const float ls = a.ms[(long long)r * a.ldms + a.L + c];
-      const float eps = a.eps_in ? a.eps_in[i] : philox_normal(a.seed, off, (unsigned long long)i);
+      const float eps = a.eps_in ? a.eps_in[i] : philox_normal(a.seed, off, a.eps_base + (unsigned long long)i);
       const float es = __expf(ls);
       const float zv = mu + eps * es;       // model.py:159
       a.z[i] = zv;

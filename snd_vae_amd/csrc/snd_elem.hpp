@@ -10,6 +10,7 @@ struct ReparamFwdArgs {
   float* eps_out; float* z;
   double* kl_part;            // [blocks]
   __bf16* zb; int ldzb;       // optional bf16 copy of z (fast-path MFMA operand)
+  unsigned long long eps_base = 0;   // Philox element index of row 0 (data parallel: rank * rows * L)
 };
 int reparam_blocks(int rows, int L);
 int launch_reparam_fwd(const ReparamFwdArgs& a, hipStream_t s);

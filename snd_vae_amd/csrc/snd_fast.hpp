@@ -177,6 +177,7 @@ struct ReparamPrepArgs {
   __bf16* jrow; __bf16* jt; float* colpart;
   double* kl_part;            // [ngraphs * npad / 64]
   int stage_only;             // 1: ms is J itself (T-ref projection output); no eps / KL
+  unsigned long long eps_base = 0;   // Philox element index of row 0 (data parallel: rank * rows * L)
 };
 int reparam_prep_blocks(int ngraphs, int npad);
 

@@ -683,7 +683,7 @@ __global__ void __launch_bounds__(NT) reparam_prep_kernel(ReparamPrepArgs a) {
       } else {
         const float4 ls = *reinterpret_cast<const float4*>(a.ms + gr * a.ldms + L + c);
         const float4 ep = a.eps_in ? *reinterpret_cast<const float4*>(a.eps_in + i)
-                                   : philox_normal4(a.seed, off, (unsigned long long)i >> 2);
+                                   : philox_normal4(a.seed, off, (a.eps_base + (unsigned long long)i) >> 2);
         const float mu[4] = {m.x, m.y, m.z, m.w}, s[4] = {ls.x, ls.y, ls.z, ls.w};
         const float e[4] = {ep.x, ep.y, ep.z, ep.w};
 #pragma unroll

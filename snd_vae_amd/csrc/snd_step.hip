@@ -90,6 +90,10 @@ struct snd_plan {
   // fused TF1 Adam (snd_plan_fuse_adam): Adam state of the blocks updated inside the step
   float* fuse_m = nullptr; float* fuse_v = nullptr;
   float fuse_lr = 0.f, fuse_b1 = 0.f, fuse_b2 = 0.f, fuse_eps = 0.f;
+  // Philox row offset of this plan's head rows (snd_plan_set_rng_offset): a data-parallel
+  // rank draws the normals a single device would draw for its rows of the global batch
+  unsigned long long rng_row0 = 0;
+  unsigned long long eps_base() const { return rng_row0 * (unsigned long long)c.latent; }
   bool block_fused(const std::string& n) const {
     return fuse_m && tref && (n == "enc.Wh" || n == "dec.Wp");
   }
@@ -128,7 +132,7 @@ struct snd_plan {
 };
 
 extern "C" const char* snd_last_error(void) { return g_err; }
-extern "C" int snd_abi_version(void) { return 5; }
+extern "C" int snd_abi_version(void) { return 6; }
 
 extern "C" int snd_plan_create(const snd_config_t* cfg, int n_graphs, snd_plan_t** out) {
   SND_CHECK_ARG(cfg && out && n_graphs > 0, "snd_plan_create: bad args");
@@ -392,6 +396,12 @@ extern "C" int snd_plan_fuse_adam(snd_plan_t* p, float* m, float* v, float lr, f
   SND_CHECK_ARG(p && ((m && v) || (!m && !v)), "snd_plan_fuse_adam: bad args");
   p->fuse_m = m; p->fuse_v = v;
   p->fuse_lr = lr; p->fuse_b1 = beta1; p->fuse_b2 = beta2; p->fuse_eps = eps;
+  return 0;
+}
+
+extern "C" int snd_plan_set_rng_offset(snd_plan_t* p, long long head_row_offset) {
+  SND_CHECK_ARG(p && head_row_offset >= 0, "snd_plan_set_rng_offset: bad args");
+  p->rng_row0 = (unsigned long long)head_row_offset;
   return 0;
 }
 
@@ -967,6 +977,7 @@ extern "C" int snd_generate(const snd_plan_t* plan, const snd_batch_t* batch, co
     }
     ReparamFwdArgs a{x.f("MS"), 2 * L, RH, L, eps_or_z, seed, step_counter, x.f("EPS"), zl,
                      x.d("PKL"), nullptr, L};
+    a.eps_base = p.eps_base();
     SND_TRY(launch_reparam_fwd(a, x.s));
   }
   if (p.tref) {   // J = reshape(z Wp + bp, [B, N, node_h]) (model_joint.py:97)
@@ -1128,6 +1139,7 @@ extern "C" int snd_train_step(const snd_plan_t* plan, const snd_batch_t* batch,
     {   // z [B, L] (model_joint.py:89)
       ReparamFwdArgs a{x.f("MS"), 2 * L, RH, L, eps, seed, step_counter, x.f("EPS"), x.f("ZL"),
                        x.d("PKL"), nullptr, L};
+      a.eps_base = p.eps_base();
       SND_TRY(launch_reparam_fwd(a, x.s));
     }
     {   // J = reshape(z Wp + bp, [B, N, node_h]) (model_joint.py:97)
@@ -1144,10 +1156,12 @@ extern "C" int snd_train_step(const snd_plan_t* plan, const snd_batch_t* batch,
     ReparamPrepArgs a{x.f("MS"), 2 * L, N, zzt_npad(N), p.B, L, eps, seed, step_counter, x.f("Z"),
                       x.f("EPS"), (__bf16*)x.f("ZB"), (__bf16*)stg.jrow, (__bf16*)stg.jt, stg.colpart,
                       x.d("PKL")};
+    a.eps_base = p.eps_base();
     SND_TRY(launch_reparam_prep(a, zzt_dp(L), x.s));
   } else {
     ReparamFwdArgs a{x.f("MS"), 2 * L, R, L, eps, seed, step_counter, x.f("EPS"), x.f("Z"),
                      x.d("PKL"), nullptr, L};
+    a.eps_base = p.eps_base();
     SND_TRY(launch_reparam_fwd(a, x.s));
   }
   // inner-product decoder + CE (fused) and per-edge terms

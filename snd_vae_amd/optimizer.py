@@ -32,9 +32,16 @@ class OptimizerVAE:
                  beta1: Optional[float] = None, beta2: Optional[float] = None,
                  epsilon: Optional[float] = None, process_group=None, seed: int = 1234,
                  fuse_adam: Optional[bool] = None):
-        """fuse_adam (default: on for one process): blocks whose gradient one kernel
-        produces complete (graph-latent heads / d_sg_lin1) take their Adam update
-        inside the step (snd_plan_fuse_adam); their gradient is then not written."""
+        """fuse_adam (default: on without a process group): blocks whose gradient one
+        kernel produces complete (graph-latent heads / d_sg_lin1) take their Adam
+        update inside the step (snd_plan_fuse_adam); their gradient is then not written.
+
+        process_group: data parallel.  Its presence (not its size) selects the
+        distributed step: the all-reduce always runs and Adam is never fused, so a
+        forced world of 1 executes exactly the N > 1 code path.  The device Philox
+        stream is offset to this rank's rows of the global batch
+        (snd_plan_set_rng_offset), so the ranks draw the normals one device would
+        draw for the whole batch."""
         cfg = model.cfg
         self.model = model
         self.lr = cfg.learning_rate if learning_rate is None else learning_rate
@@ -50,17 +57,22 @@ class OptimizerVAE:
         self.step_counter = torch.zeros(1, dtype=torch.int32, device=dev)   # TF global step
         self.losses = torch.zeros(8, dtype=torch.float64, device=dev)
         self.group = process_group
-        self.world = 1
-        if process_group is not None:
+        self.distributed = process_group is not None
+        self.world, self.rank = 1, 0
+        L = _lib.lib()
+        if self.distributed:
             import torch.distributed as dist
             self.world = dist.get_world_size(process_group)
+            self.rank = dist.get_rank(process_group)
+            head_rows = model.n_graphs * (1 if cfg.topology == "tref" else cfg.n_nodes)
+            _lib.check(L.snd_plan_set_rng_offset(model.plan, self.rank * head_rows),
+                       "snd_plan_set_rng_offset")
         self._graph = None
         self._batch_c = None
-        L = _lib.lib()
         if fuse_adam is None:
-            fuse_adam = self.world == 1
-        if fuse_adam and self.world != 1:
-            raise ValueError("fused Adam needs the full gradient on one process (world 1)")
+            fuse_adam = not self.distributed
+        if fuse_adam and self.distributed:
+            raise ValueError("fused Adam updates before the all-reduce: not with a process group")
         self.fused = bool(fuse_adam)
         _lib.check(L.snd_plan_fuse_adam(
             model.plan, _lib.ptr(self.m) if self.fused else None,
@@ -92,7 +104,7 @@ class OptimizerVAE:
 
     def allreduce(self):
         """One RCCL all-reduce (sum) of [flat grads || loss terms]."""
-        if self.world > 1:
+        if self.distributed:
             import torch.distributed as dist
             dist.all_reduce(self.grads[:self.model.param_count + 8], group=self.group)
 
@@ -113,8 +125,23 @@ class OptimizerVAE:
         self.apply()
 
     # ------------------------------------------------------------ HIP graph
+    def _state(self):
+        return [t.clone() for t in (self.model.params, self.m, self.v, self.step_counter,
+                                    self.grads, self.losses)]
+
+    def _set_state(self, saved):
+        for dst, src in zip((self.model.params, self.m, self.v, self.step_counter,
+                             self.grads, self.losses), saved):
+            dst.copy_(src)
+
     def capture(self, batch: DeviceBatch, warmup: int = 2):
-        """Capture one full step (device Philox eps) into a HIP graph."""
+        """Capture one full step (device Philox eps) into a HIP graph.
+
+        The ``warmup`` eager steps (kernel attributes, RCCL communicator) and the
+        captured step run on the live state; parameters, Adam moments, the step
+        counter, gradients and loss terms are restored afterwards, so capturing
+        leaves the training state exactly as it was."""
+        saved = self._state()
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
@@ -124,6 +151,8 @@ class OptimizerVAE:
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
             self.step(batch)
+        torch.cuda.synchronize()
+        self._set_state(saved)
         self._graph = g
         self._graph_batch = batch
         return g
@@ -140,7 +169,7 @@ class OptimizerVAE:
 
     def loss_dict(self, global_mean: bool = False):
         """All loss terms; ``global_mean`` reads the all-reduced copy (DP)."""
-        if global_mean and self.world > 1:
+        if global_mean and self.distributed:
             t = self.grads[self.model.param_count:self.model.param_count + 6].double().cpu().numpy()
             t = t / self.world
             return dict(zip(LOSS_NAMES[:6], [float(x) for x in t]))

@@ -108,7 +108,7 @@ class Trainer:
         t0 = time.time()
         for i in range(self.batch_num):
             self.step(i)
-            if self.world > 1:        # global means ride in the all-reduced gradient tail
+            if self.opt.distributed:   # global means ride in the all-reduced gradient tail
                 pc = self.model.param_count
                 hist[i, :6].copy_(self.opt.grads[pc:pc + 6].double() / self.world)
             else:

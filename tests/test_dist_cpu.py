@@ -6,6 +6,11 @@ flat gradient buffer gives the full-batch gradient.  Here every rank computes
 its shard's gradient with the oracle (float64), packs it into the product's
 flat layout, and the product's all-reduce helper combines them; the result
 must equal the single-process gradient of the whole batch.
+
+Noise is drawn the way the product draws it: each rank takes the device Philox
+stream from its first global head row on (oracle/ref_rng.py, the restatement of
+snd_common.hpp's generator; snd_plan_set_rng_offset), never a slice of a
+global array, so the test fails if shards share or misplace their normals.
 """
 import os
 import socket
@@ -17,6 +22,7 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 from oracle import ref_numpy as R
+from oracle import ref_rng
 from snd_vae_amd.config import tscale
 from snd_vae_amd.data import shard, synthetic_batch
 from snd_vae_amd.params import flat_layout, init_blocks
@@ -30,12 +36,14 @@ def _free_port():
     return p
 
 
+SEED, STEP = 1234, 3
+
+
 def _case():
     cfg = tscale(30, 8, mean_degree=5.0)
     batch = synthetic_batch(cfg, 4, seed=2)
     p = init_blocks(cfg, 3)
-    eps = np.random.default_rng(4).standard_normal((batch.features.shape[0], cfg.latent))
-    return cfg, batch, p, eps
+    return cfg, batch, p
 
 
 def _grads(cfg, b, p, eps):
@@ -49,16 +57,21 @@ def _worker(rank, world, port, out):
                       WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
     from snd_vae_amd.parallel import allreduce_mean_, init_from_env, max_over_ranks
     info = init_from_env("gloo")
-    cfg, batch, p, eps = _case()
+    cfg, batch, p = _case()
     part = shard(batch, rank, world)
     rows = part.features.shape[0]
-    losses, g = _grads(cfg, part, p, eps[rank * rows:(rank + 1) * rows])
+    eps = ref_rng.eps(SEED, STEP, rows, cfg.latent, row0=rank * rows)   # this rank's own draw
+    losses, g = _grads(cfg, part, p, eps)
     lay = flat_layout(cfg)
     flat = torch.from_numpy(np.concatenate([lay.pack(g, np.float64), [losses["cost"]]]))
     allreduce_mean_(flat, info)
     mx = max_over_ranks(float(rank + 1), info)
     if rank == 0:
         out.put((flat.numpy(), mx))
+    eps_all = [torch.zeros(rows, cfg.latent, dtype=torch.float64) for _ in range(world)]
+    dist.all_gather(eps_all, torch.from_numpy(eps))
+    if rank == 0:
+        out.put(torch.cat(eps_all).numpy())
     dist.barrier()
     dist.destroy_process_group()
 
@@ -72,10 +85,13 @@ def test_dp_allreduce_equals_full_batch_gradient():
     for pr in procs:
         pr.start()
     flat, mx = q.get(timeout=180)
+    eps_shards = q.get(timeout=60)
     for pr in procs:
         pr.join(timeout=60)
         assert pr.exitcode == 0
-    cfg, batch, p, eps = _case()
+    cfg, batch, p = _case()
+    eps = ref_rng.eps(SEED, STEP, batch.features.shape[0], cfg.latent)    # one device, whole batch
+    assert np.array_equal(eps_shards, eps)       # shards draw disjoint, correctly placed normals
     losses, g = _grads(cfg, batch, p, eps)
     lay = flat_layout(cfg)
     ref = lay.pack(g, np.float64)

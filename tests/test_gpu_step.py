@@ -195,8 +195,11 @@ def test_graph_replay_is_deterministic():
     for _ in range(5):
         o1.step(b1)
     m2, o2, b2 = make(cfg, batch, p0, "bf16")
-    o2.capture(b2, warmup=2)       # runs 2 eager steps, captures (not executed) the 3rd
-    for _ in range(3):
+    p_init, m_init = m2.params.clone(), o2.m.clone()
+    o2.capture(b2, warmup=2)       # 2 eager warm-up steps + the capture; state restored
+    assert o2.global_step == 0
+    assert torch.equal(m2.params, p_init) and torch.equal(o2.m, m_init)
+    for _ in range(5):
         o2.replay()
     torch.cuda.synchronize()
     assert o1.global_step == o2.global_step == 5
@@ -215,3 +218,75 @@ def test_training_reduces_cost():
         o.step(b)
     last = o.loss_dict()["cost"]
     assert np.isfinite(last) and last < first
+
+
+def test_device_rng_matches_restatement_and_rank_offset():
+    """Device normals equal the oracle's Philox4x32-10 + Box-Muller restatement
+    (oracle/ref_rng.py; fast f32 log/sincos on the device, float64 here), and a
+    data-parallel shard (snd_plan_set_rng_offset at its first global row) draws
+    bit-for-bit the rows one device draws for the whole batch."""
+    from oracle import ref_rng
+    from snd_vae_amd import _lib
+    from snd_vae_amd.data import shard
+    from snd_vae_amd.params import init_blocks
+    cfg = tscale(512, 64)
+    batch = synthetic_batch(cfg, 2, seed=6)
+    p0 = init_blocks(cfg, 0)
+    m, o, b = make(cfg, batch, p0, "bf16")
+    o.forward_backward(b)
+    torch.cuda.synchronize()
+    full = m.buffer("EPS")[:2 * 512 * 64].view(1024, 64).clone()
+    ref = ref_rng.eps(o.seed, 0, 1024, 64)
+    d = np.abs(full.double().cpu().numpy() - ref)
+    assert np.median(d) < 1e-6 and d.max() < 5e-3, (np.median(d), d.max())
+    for dtype in ("bf16", "f32"):
+        m1, o1, b1 = make(cfg, shard(batch, 1, 2), p0, dtype)
+        _lib.check(_lib.lib().snd_plan_set_rng_offset(m1.plan, 512))
+        o1.forward_backward(b1)
+        torch.cuda.synchronize()
+        assert torch.equal(m1.buffer("EPS")[:512 * 64].view(512, 64), full[512:])
+
+
+def test_forced_world1_process_group_runs_the_distributed_step():
+    """with a process group present -- even a world of 1 -- the step
+    always runs the RCCL all-reduce and never fuses Adam.  Its result must equal
+    an eager single-process run with fuse_adam off, bit for bit (all-reduce of one
+    rank and grad_scale 1/world = 1 are identities), on the graph-latent plan
+    where fusion matters."""
+    import socket
+
+    import torch.distributed as dist
+
+    from snd_vae_amd.model import DeviceBatch, SGCNModelVAE
+    from snd_vae_amd.optimizer import OptimizerVAE
+    from snd_vae_amd.params import init_blocks
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
+                            device_id=torch.device("cuda", 0))
+    try:
+        cfg = tref(64, 16, mean_degree=6.0)
+        batch = synthetic_batch(cfg, 2, seed=4)
+        p0 = init_blocks(cfg, 0)
+        ma = SGCNModelVAE(cfg, 2, dtype="bf16", blocks=p0)
+        oa = OptimizerVAE(ma, process_group=dist.group.WORLD)
+        assert oa.distributed and not oa.fused
+        mb, ob, bb = make(cfg, batch, p0, "bf16", fuse_adam=False)
+        ba = DeviceBatch(batch)
+        calls = []
+        real = dist.all_reduce
+        dist.all_reduce = lambda t, **kw: (calls.append(t.numel()), real(t, **kw))[1]
+        try:
+            for _ in range(3):
+                oa.step(ba)
+                ob.step(bb)
+        finally:
+            dist.all_reduce = real
+        torch.cuda.synchronize()
+        assert calls == [ma.param_count + 8] * 3
+        assert torch.equal(ma.params, mb.params)
+        assert torch.equal(oa.losses, ob.losses)
+    finally:
+        dist.destroy_process_group()

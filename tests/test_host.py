@@ -171,3 +171,41 @@ def test_spmm_tile_plan(lib_built, n, B, kbar, tile_rows, locality):
             assert np.all(rt.lcol[s:e] >= 1)
             assert np.array_equal(us[rt.lcol[s:e].astype(np.int64) - 1], ci[rp[r]:rp[r + 1]])
     assert rt.ustride == max(sizes)
+
+
+@pytest.mark.parametrize("topology", ["tscale", "tref"])
+def test_reference_checkpoint_names_roundtrip(topology):
+    """checkpoint.reference_to_blocks / blocks_to_reference: the tf.train.Saver
+    variable names of the hot path (params.logical_names) map onto the flat layout
+    and back, with TF1 Adam slots (<var>/Adam, <var>/Adam_1) and the global step
+    recovered from beta1_power (optimizer.py:125,197)."""
+    import numpy as np
+
+    from snd_vae_amd import checkpoint
+    from snd_vae_amd.config import tref, tscale
+    from snd_vae_amd.params import init_blocks, logical_names
+    cfg = tscale(40, 8) if topology == "tscale" else tref(40, 8, g_hidden=12, latent=6)
+    b = init_blocks(cfg, 5)
+    rng = np.random.default_rng(0)
+    m = {k: rng.standard_normal(v.shape) for k, v in b.items()}
+    v = {k: rng.random(v.shape) for k, v in b.items()}
+    ref = checkpoint.blocks_to_reference(cfg, b, m, v, global_step=17)
+    assert set(logical_names(cfg)) <= set(ref)
+    # a TF session dump carries an outer scope and ":0" suffixes
+    dumped = {f"SGCNModelVAE/{k}:0": a for k, a in ref.items()}
+    b2, m2, v2, step = checkpoint.reference_to_blocks(cfg, dumped)
+    assert step == 17
+    for k in b:
+        np.testing.assert_array_equal(b2[k], b[k].astype(np.float32))
+        np.testing.assert_array_equal(m2[k], m[k].astype(np.float32))
+        np.testing.assert_array_equal(v2[k], v[k].astype(np.float32))
+    # the mu / log-std heads are separate reference variables fused in enc.Wms
+    L = cfg.latent
+    np.testing.assert_array_equal(ref["encoder/g_g3_lin/Matrix"], b["enc.Wms"][:, L:].astype(np.float32))
+    bad = dict(ref)
+    bad["decoder/d_bn_s0/moving_variance"] = bad["decoder/d_bn_s0/moving_variance"] * 2
+    with pytest.raises(ValueError, match="frozen"):
+        checkpoint.reference_to_blocks(cfg, bad)
+    del bad["encoder/g_g0_conv/w"]
+    with pytest.raises(KeyError):
+        checkpoint.reference_to_blocks(cfg, bad)

@@ -17,17 +17,20 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--flags", default="0")
     ap.add_argument("--kernels", default="zzt_dense")
+    ap.add_argument("--graphs", default="8", help="graphs per GPU, comma list")
     ns = ap.parse_args()
     args = argparse.Namespace(steps=50, warmup=10, no_graph=False, dtype="bf16", no_tiles=False)
     info = init_from_env("nccl")
-    for f in [int(x) for x in ns.flags.split(",")]:
-        _lib.check(_lib.lib().snd_debug_set(f))
-        v, ms, model, opt, db, host = bench.run_workload(tscale(4096, 64), 8, args, info)
-        kms = bench.kernel_timer(model, db.c_struct(), 20)
-        ks = {k: round(kms(k), 5) for k in ns.kernels.split(",")}
-        _lib.check(_lib.lib().snd_debug_set(0))
-        print(f"flags {f}: step {ms:.4f} ms, {ks}, losses {opt.loss_dict()['cost']:.6f}", flush=True)
-        bench.del_models()
+    for B in [int(x) for x in ns.graphs.split(",")]:
+        for f in [int(x) for x in ns.flags.split(",")]:
+            _lib.check(_lib.lib().snd_debug_set(f))
+            v, ms, model, opt, db, host = bench.run_workload(tscale(4096, 64), B, args, info)
+            kms = bench.kernel_timer(model, db.c_struct(), 20)
+            ks = {k: round(kms(k), 5) for k in ns.kernels.split(",") if k}
+            _lib.check(_lib.lib().snd_debug_set(0))
+            print(f"B {B} flags {f}: step {ms:.4f} ms, {v:.1f} graphs/s, {ks}, "
+                  f"cost {opt.loss_dict()['cost']:.6f}", flush=True)
+            bench.del_models()
 
 
 if __name__ == "__main__":
