@@ -419,6 +419,7 @@ __device__ __forceinline__ int tr_off(int row, int col, int kp) {
 }
 
 constexpr int WGT = 1024;   // 16 waves; wave w owns the (tap, 16-col k block) pair pg0 + w
+__device__ __forceinline__ int cdiv_d(int a, int b) { return (a + b - 1) / b; }
 
 struct WgUnit { int sub, s0, s1, glo, ghi; };
 
@@ -435,8 +436,7 @@ __device__ __forceinline__ WgUnit wg_unit(const WgArgs& a, int sub, int s0, int 
 }
 
 template <int NBO>
-__global__ void __launch_bounds__(WGT) wgrad_kernel(WgArgs a) {
-  extern __shared__ __attribute__((aligned(16))) __bf16 lds[];
+__device__ __forceinline__ void wgrad_body(const WgArgs& a, const int bx, const int by, __bf16* lds) {
   const int T = a.T, H = (T - 1) >> 1;
   const int XR = kRcRows + T - 1;
   const int kpx = a.K <= 32 ? 32 : (a.K <= 64 ? 64 : 128);
@@ -447,7 +447,7 @@ __global__ void __launch_bounds__(WGT) wgrad_kernel(WgArgs a) {
   const int li = lane & 15, lg = lane >> 4, tq = li >> 2, tp = li & 3;
   const int cbn = (a.K + 15) >> 4;
   const int P = T * cbn;
-  const int p = blockIdx.y * a.pairs_per_wg + w;
+  const int p = by * a.pairs_per_wg + w;
   const bool pv = w < a.pairs_per_wg && p < P;
   const int t = pv ? p / cbn : 0, cb = pv ? p - t * cbn : 0;
 
@@ -457,7 +457,7 @@ __global__ void __launch_bounds__(WGT) wgrad_kernel(WgArgs a) {
 
   const __bf16* xg = reinterpret_cast<const __bf16*>(a.x);
   const __bf16* dg = reinterpret_cast<const __bf16*>(a.dy);
-  const int c0 = blockIdx.x * a.rows_per_wg, c1 = min(a.R, c0 + a.rows_per_wg);
+  const int c0 = bx * a.rows_per_wg, c1 = min(a.R, c0 + a.rows_per_wg);
   auto stage = [&](const WgUnit& u, int b) {
     if (a.dbg & 2) return;
     __bf16* xs = lds + b * bufe;
@@ -531,12 +531,50 @@ __global__ void __launch_bounds__(WGT) wgrad_kernel(WgArgs a) {
   if (k >= a.K) return;
   // slab rows padded to a multiple of 4 floats: every store is a float4
   const int n4 = (a.N + 3) & ~3;
-  float* row = a.slab + (long long)blockIdx.x * T * a.K * n4 + ((long long)t * a.K + k) * n4;
+  float* row = a.slab + (long long)bx * T * a.K * n4 + ((long long)t * a.K + k) * n4;
 #pragma unroll
   for (int ob = 0; ob < NBO; ++ob) {
     const int n0 = 16 * ob + 4 * lg;
     if (n0 < a.N)
       *reinterpret_cast<float4*>(row + n0) = make_float4(acc[ob][0], acc[ob][1], acc[ob][2], acc[ob][3]);
+  }
+}
+
+template <int NBO>
+__global__ void __launch_bounds__(WGT) wgrad_kernel(WgArgs a) {
+  extern __shared__ __attribute__((aligned(16))) __bf16 lds[];
+  wgrad_body<NBO>(a, blockIdx.x, blockIdx.y, lds);
+}
+
+// Several weight gradients in ONE launch (the step's deferred wgrad queue): the
+// flattened grid is cut into segments, segment s = descriptor s with its own
+// (row chunk, pair group) geometry.  Segments are independent (they read
+// finished dy's and write their own slabs), so one launch replaces one dependent
+// launch per weight.
+struct WgMultiPack {
+  WgArgs a[kMaxWgMulti];
+  int start[kMaxWgMulti + 1];
+  int nseg;
+};
+
+__global__ void __launch_bounds__(WGT) wgrad_multi_kernel(WgMultiPack m) {
+  extern __shared__ __attribute__((aligned(16))) __bf16 lds[];
+  int s = 0;
+  while (s + 1 < m.nseg && (int)blockIdx.x >= m.start[s + 1]) ++s;
+  s = __builtin_amdgcn_readfirstlane(s);
+  const WgArgs& a = m.a[s];
+  const int local = blockIdx.x - m.start[s];
+  const int gx = cdiv_d(a.R, a.rows_per_wg);
+  const int bx = local % gx, by = local / gx;
+  switch ((a.N + 15) >> 4) {
+    case 1: wgrad_body<1>(a, bx, by, lds); break;
+    case 2: wgrad_body<2>(a, bx, by, lds); break;
+    case 3: wgrad_body<3>(a, bx, by, lds); break;
+    case 4: wgrad_body<4>(a, bx, by, lds); break;
+    case 5: wgrad_body<5>(a, bx, by, lds); break;
+    case 6: wgrad_body<6>(a, bx, by, lds); break;
+    case 7: wgrad_body<7>(a, bx, by, lds); break;
+    default: wgrad_body<8>(a, bx, by, lds); break;
   }
 }
 
@@ -784,6 +822,37 @@ int launch_rowconv(const RcArgs& a, int epi, hipStream_t s) {
   }
 }
 
+int launch_wgrad_multi(const WgArgs* a, int n, hipStream_t s) {
+  if (n <= 0) return 0;
+  SND_CHECK_ARG(n <= kMaxWgMulti, "wgrad_multi: at most %d segments", kMaxWgMulti);
+  WgMultiPack pk{};
+  size_t lds = 0;
+  int total = 0;
+  pk.nseg = 0;
+  for (int i = 0; i < n; ++i) {
+    const WgArgs& x = a[i];
+    if (x.R <= 0) continue;
+    SND_CHECK_ARG(x.T == 1 || x.T == 5, "wgrad_multi: T must be 1 or 5");
+    SND_CHECK_ARG(x.K > 0 && x.K <= 128 && x.N > 0 && x.N <= 128, "wgrad_multi: K %d N %d", x.K, x.N);
+    SND_CHECK_ARG(x.ldx % 8 == 0 && x.lddy % 8 == 0 && x.x_bf16 && x.dy_bf16,
+                  "wgrad_multi: bf16 operands with leading dims %% 8");
+    SND_CHECK_ARG(x.rows_per_wg % kRcRows == 0 && x.pairs_per_wg >= 1 && x.pairs_per_wg <= WGT / 64,
+                  "wgrad_multi: geometry");
+    SND_CHECK_ARG(x.x && x.dy && x.slab && x.zero && x.npg > 0, "wgrad_multi: null operand");
+    const int P = x.T * cdiv(x.K, 16);
+    pk.a[pk.nseg] = x;
+    pk.start[pk.nseg] = total;
+    total += cdiv(x.R, x.rows_per_wg) * cdiv(P, x.pairs_per_wg);
+    lds = std::max(lds, wg_lds_bytes(x.T, x.K, x.N));
+    ++pk.nseg;
+  }
+  if (pk.nseg == 0) return 0;
+  pk.start[pk.nseg] = total;
+  hipLaunchKernelGGL(wgrad_multi_kernel, dim3(total), dim3(WGT), lds, s, pk);
+  SND_LAUNCH_CHECK("wgrad_multi_kernel");
+  return 0;
+}
+
 WgGeom wgrad_geom(int R, int T, int K, int N) {
   WgGeom g{};
   const int P = T * cdiv(K, 16);
@@ -839,7 +908,7 @@ int fast_init_attributes() {
 #undef SND_ATTR4
   SND_ATTR((wgrad_kernel<1>)) SND_ATTR((wgrad_kernel<2>)) SND_ATTR((wgrad_kernel<3>))
   SND_ATTR((wgrad_kernel<4>)) SND_ATTR((wgrad_kernel<5>)) SND_ATTR((wgrad_kernel<6>))
-  SND_ATTR((wgrad_kernel<7>)) SND_ATTR((wgrad_kernel<8>))
+  SND_ATTR((wgrad_kernel<7>)) SND_ATTR((wgrad_kernel<8>)) SND_ATTR(wgrad_multi_kernel)
 #undef SND_ATTR
   done = 1;
   return 0;

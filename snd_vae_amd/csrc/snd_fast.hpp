@@ -99,6 +99,9 @@ struct WgGeom { int rows_per_wg, pairs_per_wg, gx, gy; };
 WgGeom wgrad_geom(int R, int T, int K, int N);
 inline int wgrad_n4(int N) { return (N + 3) & ~3; }
 int launch_wgrad(const WgArgs& a, hipStream_t s);
+// n independent weight gradients (each its own geometry and slab) in one launch
+constexpr int kMaxWgMulti = 12;
+int launch_wgrad_multi(const WgArgs* a, int n, hipStream_t s);
 
 // ---- fused sigmoid head + MSE + backward + BN/lrelu backward of the head's
 // input layer (model_joint.py:115-121,138-144; optimizer.py:149,153).

@@ -761,9 +761,12 @@ template <int EPI>
 static int launch_spmm_bf16_epi(const SpmmBfArgs& a, bool two, hipStream_t s) {
   // The tiled kernel pays off through its pipeline (runs of tiles per workgroup)
   // and, for the plain epilogue, its LDS sums; a GraphConvolution epilogue over
-  // at most ~1 tile per workgroup (the step's 8-graph batch) is faster on the
+  // ~1 tile per workgroup (the step's 8-graph batch, 512 tiles) is faster on the
   // register kernel, whose epilogue stores whole rows per 8-lane group
-  // (16.6 vs 10.8 us at B = 8).  debug bit 2048 keeps the tiles (A/B).
+  // (16.6 vs 10.8 us at B = 8).  Up to 4 tiles per workgroup (B <= 32) the choice
+  // is a wash: whole-step A/B with debug bit 2048 (tiles kept) at B = 8 / 16 / 32
+  // measured 0.3407 / 0.5673 / 0.9867 ms (register) vs 0.3396 / 0.5670 / 0.9894 ms
+  // (tiled), round 2; beyond that the tiled pipeline is used.
   const bool gcn_small = EPI == SND_SPMM_GCN && a.t_rows > 0 && cdiv(a.R, a.t_rows) <= 4 * 512 &&
                          !(debug_flags() & 2048);
   if (a.t_rows > 0 && a.t_ustride <= TILE_CAP && !gcn_small) {

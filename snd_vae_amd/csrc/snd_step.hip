@@ -432,6 +432,7 @@ struct Ctx {
   hipStream_t s;
   hipStream_t side = nullptr;   // null: single-stream
   int* nev = nullptr;           // next free event of p->ev
+  std::vector<WgArgs>* wq = nullptr;   // deferred weight gradients (one launch at the end)
   float* f(const char* n) const { return (float*)(ws + p->buf(n)); }
   double* d(const char* n) const { return (double*)(ws + p->buf(n)); }
   const float* w(const char* n) const { return P + p->blk(n); }
@@ -470,6 +471,11 @@ int join(const Ctx& x) {
   return 0;
 }
 hipStream_t side(const Ctx& x) { return x.side ? x.side : x.s; }
+// a weight gradient: queued for the step's single multi-segment launch, or launched now
+int wgrad(const Ctx& x, const WgArgs& a, hipStream_t s) {
+  if (x.wq) { x.wq->push_back(a); return 0; }
+  return launch_wgrad(a, s);
+}
 // mark: an event after the work queued on side() so far; wait_mark: main waits for it
 int mark(const Ctx& x) {
   if (!x.side) return -1;
@@ -725,14 +731,14 @@ int encoder_fast_bwd(const Ctx& x, const snd_batch_t* batch, float adj_scale, fl
     SND_TRY(launch_reparam_bwd_fast(a, x.s));
   }
   SND_TRY(fork(x));
-  SND_TRY(launch_wgrad(wg_args(p, x.ws, p.gWms, bf("FHH"), gh, gh, bf("FDMS"), 2 * L, 2 * L, x.f("FSWMS"), 1), side(x)));
+  SND_TRY(wgrad(x, wg_args(p, x.ws, p.gWms, bf("FHH"), gh, gh, bf("FDMS"), 2 * L, 2 * L, x.f("FSWMS"), 1), side(x)));
   {
     RcArgs a = rc_args(p, x.ws, p.pwmsb, bf("FDMS"), 2 * L, 2 * L, gh, colmap_plain(gh));
     a.out = bf("FDH"); a.ldo = gh; a.out_bf16 = 1; a.colpart = x.f("PFBH"); a.ncp = 1;
     SND_TRY(launch_rowconv(a, RC_LIN, x.s));
   }
   SND_TRY(fork(x));
-  SND_TRY(launch_wgrad(wg_args(p, x.ws, p.gWh, bf("FG"), p.ldg, W, bf("FDH"), gh, gh, x.f("FSWH"), 1), side(x)));
+  SND_TRY(wgrad(x, wg_args(p, x.ws, p.gWh, bf("FG"), p.ldg, W, bf("FDH"), gh, gh, x.f("FSWH"), 1), side(x)));
   return encoder_fast_bwd_tail(x, batch);
 }
 
@@ -759,7 +765,7 @@ int encoder_fast_bwd_tail(const Ctx& x, const snd_batch_t* batch) {
     SND_TRY(launch_spmm_bf16(a, x.s));
   }
   SND_TRY(fork(x));
-  SND_TRY(launch_wgrad(wg_args(p, x.ws, p.gW1, bf("FH1"), p.ldh1, h0 + f, bf("FDXW1"), h1, h1, x.f("FSW1"), 1), side(x)));
+  SND_TRY(wgrad(x, wg_args(p, x.ws, p.gW1, bf("FH1"), p.ldh1, h0 + f, bf("FDXW1"), h1, h1, x.f("FSW1"), 1), side(x)));
   {
     RcArgs a = rc_args(p, x.ws, p.pw1b, bf("FDXW1"), h1, h1, h0, colmap_plain(h0));
     a.gamma = x.w("enc.bn0.gamma"); a.p = x.f("AX"); a.ldp = 4; a.w0 = x.w("enc.W0"); a.f = f;
@@ -767,7 +773,7 @@ int encoder_fast_bwd_tail(const Ctx& x, const snd_batch_t* batch) {
     SND_TRY(launch_rowconv(a, RC_ENC0, x.s));
   }
   SND_TRY(fork(x));
-  return launch_wgrad(wg_args(p, x.ws, p.gW0, bf("AXB"), 8, f, bf("FDP0"), h0, h0, x.f("FSW0"), 1), side(x));
+  return wgrad(x, wg_args(p, x.ws, p.gW0, bf("AXB"), 8, f, bf("FDP0"), h0, h0, x.f("FSW0"), 1), side(x));
 }
 
 void encoder_fast_reduce(const Ctx& x, std::vector<ReduceDesc>& rd) {
@@ -851,7 +857,7 @@ int decoder_fast(const Ctx& x, const snd_batch_t* batch, int only = -1) {
   }
   if (only < 0 || only == 5) {
     SND_TRY(fork(x));
-    SND_TRY(launch_wgrad(wg_args(p, x.ws, p.gK3s, bf("FU2"), p.ld2, s2, bf("FDY3"), p.ld3, s3, x.f("FSK3S")), side(x)));
+    SND_TRY(wgrad(x, wg_args(p, x.ws, p.gK3s, bf("FU2"), p.ld2, s2, bf("FDY3"), p.ld3, s3, x.f("FSK3S")), side(x)));
   }
   // conv2 data gradient -> dU1, fused BN/lrelu backward of conv1 -> dY1
   {
@@ -863,11 +869,11 @@ int decoder_fast(const Ctx& x, const snd_batch_t* batch, int only = -1) {
   }
   if (only < 0 || only == 7) {
     SND_TRY(fork(x));
-    SND_TRY(launch_wgrad(wg_args(p, x.ws, p.gK2s, bf("FU1"), p.ld1, c.s1, bf("FDY2"), p.ld2, s2, x.f("FSK2S")), side(x)));
+    SND_TRY(wgrad(x, wg_args(p, x.ws, p.gK2s, bf("FU1"), p.ld1, c.s1, bf("FDY2"), p.ld2, s2, x.f("FSK2S")), side(x)));
   }
   if (only < 0 || only == 8) {
     SND_TRY(fork(x));
-    SND_TRY(launch_wgrad(wg_args(p, x.ws, p.gK2n, bf("FU1") + o1, p.ld1, c.n1, bf("FDY2") + o2, p.ld2, n2,
+    SND_TRY(wgrad(x, wg_args(p, x.ws, p.gK2n, bf("FU1") + o1, p.ld1, c.n1, bf("FDY2") + o2, p.ld2, n2,
                                x.f("FSK2N")), side(x)));
   }
   // conv1 data gradient -> dz (decoder part)
@@ -878,7 +884,7 @@ int decoder_fast(const Ctx& x, const snd_batch_t* batch, int only = -1) {
   }
   if (only < 0 || only == 10) {
     SND_TRY(fork(x));
-    SND_TRY(launch_wgrad(wg_args(p, x.ws, p.gK1, bf("ZB"), L, L, bf("FDY1"), p.ld1, w1, x.f("FSK1")), side(x)));
+    SND_TRY(wgrad(x, wg_args(p, x.ws, p.gK1, bf("ZB"), L, L, bf("FDY1"), p.ld1, w1, x.f("FSK1")), side(x)));
   }
   return 0;
 }
@@ -1104,6 +1110,13 @@ extern "C" int snd_train_step(const snd_plan_t* plan, const snd_batch_t* batch,
     init_concurrency(p, x.s);
     if (p.conc == 1) { x.side = p.side; x.nev = &nev; }
   }
+  // single stream: every fast-path weight gradient waits for one launch before the
+  // reduction (debug bit 4096: one launch per weight, as before)
+  std::vector<WgArgs> wq;
+  if (p.fast && !x.side && !(debug_flags() & 4096)) {
+    wq.reserve(kMaxWgMulti);
+    x.wq = &wq;
+  }
   const int R = p.R, N = p.N, f = c.f_in, h0 = c.h0, h1 = c.h1, gh = c.g_hidden, L = c.latent;
   const int W = p.W, C1 = p.C1, s1 = c.s1, s2 = c.s2, s3 = c.s3, n1 = c.n1, n2 = c.n2;
   const int sd = c.spatial_dim, nf = c.num_feature;
@@ -1306,6 +1319,13 @@ extern "C" int snd_train_step(const snd_plan_t* plan, const snd_batch_t* batch,
   }
 
   SND_TRY(join(x));   // weight-gradient slabs from the side stream
+  if (x.wq && !x.wq->empty()) {
+    // largest weight first: its workgroups start in the first wave of the launch
+    std::stable_sort(x.wq->begin(), x.wq->end(), [](const WgArgs& u, const WgArgs& v) {
+      return (long long)u.T * u.K * u.N > (long long)v.T * v.K * v.N;
+    });
+    SND_TRY(launch_wgrad_multi(x.wq->data(), (int)x.wq->size(), x.s));
+  }
 
   // ======================= deterministic gradient reduction =================
   const int nc = col_blocks(R), nh = head_blocks(R);
