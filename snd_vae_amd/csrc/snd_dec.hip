@@ -1,0 +1,724 @@
+// Fused bf16 decoder of the train step: two launches instead of seven.
+//
+//   dec_fwd_kernel  conv1 -> conv2 -> conv3 (k=5 SAME + bias + frozen BN + lrelu,
+//                   model_joint.py:112-118,129-140), then the sigmoid heads, their
+//                   MSE and the head backward (model_joint.py:121,144;
+//                   optimizer.py:149,153)
+//   dec_bwd_kernel  conv3^T -> BN/lrelu backward -> conv2^T -> BN/lrelu backward
+//                   -> conv1^T = d cost / dJ of the decoders
+//
+// One workgroup owns a tile of 128 rows of one graph.  A k=5 conv needs two
+// halo rows on each side, so a chain of c convs recomputes 2c halo rows per
+// side instead of round-tripping every intermediate through HBM: the forward
+// stages J rows [r0 - 6, r0 + 134), computes conv1 on [r0 - 4, r0 + 132),
+// conv2 on [r0 - 2, r0 + 130) and conv3 on the own rows, each layer's bf16
+// output staying in LDS as the next layer's MFMA operand (the [row][k] image
+// the row engine of snd_fast.hip reads, 16-byte chunks XOR-swizzled).  Rows
+// outside the tile's graph are written as zeros: TF SAME padding per graph.
+// Only what the backward pass and the weight gradients need leaves the chip:
+// Y1/Y2 (fp32 BN inputs), U1/U2 (bf16 wgrad operands), dY3 / dY2n (bf16).
+// The backward chain recomputes its halos the same way (dY3 rows +-6).
+//
+// The arithmetic is the row engine's (same MFMA order over taps and k chunks,
+// same epilogues): every activation and data gradient equals the unfused
+// path's bit for bit; only the column partial sums are added in another order.
+#include "snd_dec.hpp"
+
+#include <algorithm>
+
+namespace snd {
+namespace {
+
+constexpr int DT = 1024;                  // 16 waves
+constexpr int NW = DT / 64;
+constexpr int TR = kDecRows;
+
+typedef __attribute__((address_space(1))) const void* gptr_t;
+typedef __attribute__((address_space(3))) void* lptr_t;
+
+__device__ __forceinline__ void dglds16(const void* g, void* lds_base) {
+  __builtin_amdgcn_global_load_lds((gptr_t)g, (lptr_t)lds_base, 16, 0, 0);
+}
+// chunk swizzle of a [row][kp] bf16 image (snd_fast.hip swz)
+__host__ __device__ __forceinline__ int dswz(int row, int kp) {
+  return kp == 128 ? (row & 15) : (kp == 64 ? ((row >> 1) & 7) : 0);
+}
+__host__ __device__ __forceinline__ int lkc_of(int kp) { return kp == 128 ? 4 : (kp == 64 ? 3 : 2); }
+__host__ __device__ __forceinline__ int img_bytes(int rows, int kp) {
+  return ((rows * kp * 2) + 1023) & ~1023;
+}
+__host__ __device__ __forceinline__ int rup(int a, int b) { return (a + b - 1) / b * b; }
+__host__ __device__ constexpr int head_nq(int cin, int cout) { return cin * cout + cout + 3 * cin; }
+
+// rows of the input image of a k=5 phase whose output window has n_out rows
+__host__ __device__ __forceinline__ int in_rows(int n_out) { return rup(n_out, 16) + 4; }
+
+// ---- LDS layouts (bytes), shared by host (launch size) and device
+struct FwdLay {
+  int w, a, b, c, total;        // offsets: weights | A: J -> U2 | B: U1 -> U3,Y3 | C: Y2n
+  int ldY2n;
+  __host__ __device__ FwdLay(const DecChainFwdArgs& p) {
+    const int wb = max(max(p.k1.np * p.k1.kp, p.k2.np * p.k2.kp), p.k3.np * p.k3.kp) * 5 * 2;
+    const int kp_u2 = p.m2.phys() <= 32 ? 32 : (p.m2.phys() <= 64 ? 64 : 128);
+    const int ja = img_bytes(in_rows(TR + 8), p.k1.kp);
+    const int ua = img_bytes(in_rows(TR), kp_u2);
+    const int u1 = img_bytes(in_rows(TR + 4), p.k2.kp);
+    const int u3 = 2 * TR * 16 * 4;
+    ldY2n = rup(max(p.m2.b, 1), 4);
+    w = 0; a = wb; b = a + max(ja, ua); c = b + max(u1, u3);
+    total = c + TR * ldY2n * 4;
+  }
+};
+struct BwdLay {
+  int w, d3, d2, d1, cps, total;
+  __host__ __device__ BwdLay(const DecChainBwdArgs& p) {
+    const int wb = max(max(p.k3t.np * p.k3t.kp, p.k2t.np * p.k2t.kp), p.k1t.np * p.k1t.kp) * 5 * 2;
+    w = 0;
+    d3 = wb;
+    d2 = d3 + img_bytes(in_rows(TR + 8), p.k3t.kp);
+    d1 = d2 + img_bytes(in_rows(TR + 4), p.k2t.kp);
+    cps = d1 + img_bytes(in_rows(TR), p.k1t.kp);
+    // per-wave column partial slots: (16 / ncg) slots x 3 x np, max over the two BN phases
+    const int c1 = (16 / ((p.k2t.np / 16 + 1) / 2)) * 3 * p.k2t.np;
+    const int c2 = (16 / (p.k3t.np / 16)) * 3 * p.k3t.np;
+    total = cps + max(c1, c2) * 4;
+  }
+};
+
+// tile -> own rows [r0, rend) of graph [glo, ghi)
+struct Tile { int r0, rend, glo, ghi; };
+__device__ __forceinline__ Tile tile_of(int t, int npg) {
+  const int tpg = (npg + TR - 1) / TR;
+  const int g = t / tpg, lt = t - g * tpg;
+  Tile x;
+  x.glo = g * npg; x.ghi = x.glo + npg;
+  x.r0 = x.glo + lt * TR; x.rend = min(x.r0 + TR, x.ghi);
+  return x;
+}
+
+// LDS-DMA a bf16 [R][ld] window of rows [wr0, wr0 + nrows) into a [row][kp] image;
+// rows outside [glo, ghi) or at/after nvalid, and chunks at col >= K, read zeros.
+__device__ __forceinline__ void stage_window(const __bf16* src, int ld, int K, int wr0, int nrows,
+                                             int nvalid, int glo, int ghi, int kp, char* img,
+                                             const void* zero) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int lk = lkc_of(kp), kc = 1 << lk;
+  const int npc = ((nrows << lk) + 63) >> 6;
+  for (int j = w; j < npc; j += NW) {
+    const int q = (j << 6) + lane;
+    const int row = q >> lk, pc = q & (kc - 1);
+    const int c = pc ^ dswz(row, kp);
+    const int gr = wr0 + row;
+    const bool v = row < nvalid && gr >= glo && gr < ghi && 8 * c < K;
+    const void* g = v ? (const void*)(src + (long long)gr * ld + 8 * c) : zero;
+    dglds16(g, img + (j << 10));
+  }
+}
+__device__ __forceinline__ void stage_weights(const DecImg& im, char* dst) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int npc = (5 * im.np * im.kp * 2) >> 10;
+  const char* g = reinterpret_cast<const char*>(im.w) + lane * 16;
+  for (int j = w; j < npc; j += NW) dglds16(g + (j << 10), dst + (j << 10));
+}
+__device__ __forceinline__ void wait_dma() {
+  __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0)
+  __syncthreads();
+}
+
+// 4 bf16 of row `row`, columns n0 .. n0 + 3 (n0 % 4 == 0) of a [row][kp] image
+__device__ __forceinline__ __bf16* img_at(__bf16* img, int row, int kp, int n0) {
+  return img + row * kp + ((((n0 >> 3) ^ dswz(row, kp)) << 3) | (n0 & 4));
+}
+
+// One k=5 phase: out^T = W^T x^T on v_mfma_f32_16x16x32_bf16 (the row engine's
+// operand roles and order).  Output window rows o in [0, n_out) read image rows
+// o .. o + 4.  Waves are assigned column group cg = w % ncg and row blocks
+// k, k + wpc, ... (k = w / ncg); PRE(orow, nb0, yp) loads epilogue operands before
+// the MFMAs, EPI(orow, nb0, acc, yp) consumes a finished 16-row x NBH-block item.
+template <int NBH, class Pre, class Epi>
+__device__ __forceinline__ void conv_phase(const __bf16* xs, int kpx, const __bf16* ws, int kpw, int np,
+                                           int n_out, Pre&& pre, Epi&& epi) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, li = lane & 15, lg = lane >> 4;
+  const int nrb = (n_out + 15) >> 4, nbc = np >> 4;
+  const int ncg = (nbc + NBH - 1) / NBH, wpc = NW / ncg;
+  const int cg = w % ncg, k0 = w / ncg;
+  if (k0 >= wpc) return;
+  const int nb0 = cg * NBH;
+  const int kcs = kpw >> 5;
+  const int wsw = dswz(li, kpw);
+  for (int rb = k0; rb < nrb; rb += wpc) {
+    f32x4 yp[NBH];
+    pre(16 * rb + li, nb0, yp);
+    f32x4 acc[NBH];
+#pragma unroll
+    for (int i = 0; i < NBH; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int t = 0; t < 5; ++t) {
+      const int xrow = 16 * rb + li + t;
+      const __bf16* xrp = xs + xrow * kpx;
+      const int xsw = dswz(xrow, kpx);
+      const __bf16* wrp = ws + (t * np + li) * kpw;
+      for (int ks = 0; ks < kcs; ++ks) {
+        const int ch = 4 * ks + lg;
+        const bf16x8 bx = *reinterpret_cast<const bf16x8*>(xrp + ((ch ^ xsw) << 3));
+#pragma unroll
+        for (int i = 0; i < NBH; ++i) {
+          if (nb0 + i < nbc) {
+            const bf16x8 aw = *reinterpret_cast<const bf16x8*>(wrp + 16 * (nb0 + i) * kpw + ((ch ^ wsw) << 3));
+            acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aw, bx, acc[i], 0, 0, 0);
+          }
+        }
+      }
+    }
+    epi(16 * rb + li, nb0, acc, yp);
+  }
+}
+
+// per-column parameters of a (possibly split) layout, physical column n
+__device__ __forceinline__ float colpar(const ColMap& m, int n, const float* A, const float* Bv) {
+  if (!m.valid(n) || !A) return 0.f;
+  if (n < m.a || !Bv) return A[n < m.a ? n : m.logical(n)];
+  return Bv[n - m.offb];
+}
+
+// ------------------------------------------------------------------ heads
+// One thread per own row (model_joint.py:121,144; optimizer.py:149,153): as
+// heads_fast_kernel's head_rows, with the inputs read from LDS.  Partial sums
+// {dW, db, sum dt*y, sum dt, sum dy} reduced over the tile in fixed order.
+template <int CIN, int COUT>
+__device__ __forceinline__ void head_tile(int hi, int orow, bool rv, long long gr, const float (&u)[CIN],
+                                          const float (&yv)[CIN], const float* w, const float* b,
+                                          const float* gamma, const float* beta, const float* target,
+                                          float count, float* yhat, __bf16* dyp, float* part,
+                                          double* sse_out, float* red, double* sred) {
+  constexpr int NQ = head_nq(CIN, COUT);
+  const int lane = threadIdx.x & 63, wl = (threadIdx.x >> 6) & 1;   // 2 waves per head
+  float wv[CIN][COUT], bv[COUT], gk[CIN], bk[CIN];
+#pragma unroll
+  for (int k = 0; k < CIN; ++k) {
+#pragma unroll
+    for (int o = 0; o < COUT; ++o) wv[k][o] = w[k * COUT + o];
+    gk[k] = gamma[k] * kBnC;
+    bk[k] = beta[k];
+  }
+#pragma unroll
+  for (int o = 0; o < COUT; ++o) bv[o] = b[o];
+  float tg[COUT];
+#pragma unroll
+  for (int o = 0; o < COUT; ++o) tg[o] = rv ? target[gr * COUT + o] : 0.f;
+  float dp[COUT];
+  double sse = 0.0;
+#pragma unroll
+  for (int o = 0; o < COUT; ++o) {
+    float zo = bv[o];
+#pragma unroll
+    for (int k = 0; k < CIN; ++k) zo += u[k] * wv[k][o];
+    const float yh = 1.f / (1.f + __expf(-zo));
+    const float diff = yh - tg[o];
+    if (rv) {
+      if (yhat) yhat[gr * COUT + o] = yh;
+      sse += (double)diff * diff;
+    }
+    dp[o] = rv ? 2.f * diff / count * yh * (1.f - yh) : 0.f;
+  }
+  float dt[CIN], dyv[CIN];
+#pragma unroll
+  for (int k = 0; k < CIN; ++k) {
+    float du = 0.f;
+#pragma unroll
+    for (int o = 0; o < COUT; ++o) du += dp[o] * wv[k][o];
+    dt[k] = du * lrelu_grad(yv[k] * gk[k] + bk[k]);
+    dyv[k] = dt[k] * gk[k];
+  }
+  if (rv) {
+#pragma unroll
+    for (int c = 0; c < CIN / 4; ++c) {
+      bf16x4 v;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[j] = (__bf16)dyv[4 * c + j];
+      *reinterpret_cast<bf16x4*>(dyp + 4 * c) = v;
+    }
+#pragma unroll
+    for (int k = (CIN / 4) * 4; k < CIN; ++k) dyp[k] = (__bf16)dyv[k];
+  }
+  // partials: wave sums, then the head's 2 waves in fixed order
+  float* rw = red + wl * NQ;
+  auto put = [&](int q, float v) {
+    v = wave_sum(v);
+    if (lane == 0) rw[q] = v;
+  };
+#pragma unroll
+  for (int k = 0; k < CIN; ++k)
+#pragma unroll
+    for (int o = 0; o < COUT; ++o) put(k * COUT + o, u[k] * dp[o]);
+#pragma unroll
+  for (int o = 0; o < COUT; ++o) put(CIN * COUT + o, dp[o]);
+  constexpr int QB = CIN * COUT + COUT;
+#pragma unroll
+  for (int k = 0; k < CIN; ++k) {
+    put(QB + k, dt[k] * yv[k]);
+    put(QB + CIN + k, dt[k]);
+    put(QB + 2 * CIN + k, dyv[k]);
+  }
+  const double ws_ = wave_sum_d(sse);
+  if (lane == 0) sred[wl] = ws_;
+  __syncthreads();   // all 1024 threads reach this (see the caller)
+  const int tl = threadIdx.x & 127;
+  for (int q = tl; q < NQ; q += 128) part[q] = red[q] + red[NQ + q];
+  if (tl == 0) *sse_out = sred[0] + sred[1];
+  (void)hi; (void)orow;
+}
+
+// ------------------------------------------------------------------ forward
+__global__ void __launch_bounds__(DT) dec_fwd_kernel(DecChainFwdArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  __shared__ float cp1[3][128], cp2[3][128], cp3[3][16];
+  __shared__ float hred[2][2 * 96];
+  __shared__ double hsred[2][2];
+  const FwdLay L(a);
+  const Tile tl = tile_of(blockIdx.x, a.npg);
+  const int tid = threadIdx.x, lane = tid & 63, lg = lane >> 4;
+  __bf16* wimg = reinterpret_cast<__bf16*>(smem + L.w);
+  __bf16* jimg = reinterpret_cast<__bf16*>(smem + L.a);
+  __bf16* u2img = jimg;                                   // A: J, then U2
+  __bf16* u1img = reinterpret_cast<__bf16*>(smem + L.b);
+  float* u3 = reinterpret_cast<float*>(smem + L.b);       // B: U1, then U3 | Y3
+  float* y3 = u3 + TR * 16;
+  float* y2n = reinterpret_cast<float*>(smem + L.c);
+  const int kpu2 = a.m2.phys() <= 32 ? 32 : (a.m2.phys() <= 64 ? 64 : 128);
+  const int own = tl.rend - tl.r0;
+
+  // zero the activation images (pad columns and rows past a window are MFMA operands)
+  for (int i = tid * 16; i < L.total - L.a; i += DT * 16)
+    *reinterpret_cast<uint4*>(smem + L.a + i) = make_uint4(0u, 0u, 0u, 0u);
+  __syncthreads();
+  // J window [r0 - 6, r0 + own + 6) and the conv1 weights
+  stage_window(a.zb, a.ldz, a.dj, tl.r0 - 6, in_rows(TR + 8), own + 12, tl.glo, tl.ghi, a.k1.kp,
+               reinterpret_cast<char*>(jimg), a.zero);
+  stage_weights(a.k1, reinterpret_cast<char*>(wimg));
+  if (tid < 128) {
+    const int n = tid;
+    cp1[0][n] = colpar(a.m1, n, a.b1, nullptr);
+    cp1[1][n] = colpar(a.m1, n, a.g1, nullptr) * kBnC;
+    cp1[2][n] = colpar(a.m1, n, a.be1, nullptr);
+    cp2[0][n] = colpar(a.m2, n, a.b2s, a.b2n);
+    cp2[1][n] = colpar(a.m2, n, a.g2s, a.g2n) * kBnC;
+    cp2[2][n] = colpar(a.m2, n, a.be2s, a.be2n);
+    if (n < 16) {
+      const ColMap m3{a.s3, 0, a.s3};
+      cp3[0][n] = colpar(m3, n, a.b3, nullptr);
+      cp3[1][n] = colpar(m3, n, a.g3, nullptr) * kBnC;
+      cp3[2][n] = colpar(m3, n, a.be3, nullptr);
+    }
+  }
+  wait_dma();
+
+  auto nopre = [](int, int, auto&) {};
+  // ---- conv1: window [r0 - 4, r0 + own + 4) -> U1 image (bf16), Y1 / U1 own rows to HBM
+  {
+    const int wr0 = tl.r0 - 4, n_out = own + 8, N = a.m1.phys(), kpo = a.k2.kp;
+    conv_phase<2>(jimg, a.k1.kp, wimg, a.k1.kp, a.k1.np, n_out, nopre,
+                  [&](int orow, int nb0, f32x4 (&acc)[2], f32x4 (&)[2]) {
+      if (orow >= n_out) return;
+      const int gr = wr0 + orow;
+      const bool ing = gr >= tl.glo && gr < tl.ghi, mine = gr >= tl.r0 && gr < tl.rend;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int n0 = 16 * (nb0 + i) + 4 * lg;
+        if (n0 >= a.k1.np) continue;
+        float yv[4], o[4];
+        unsigned cm = 0u;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int n = n0 + e;
+          if (n < N && a.m1.valid(n)) cm |= 1u << e;
+          yv[e] = acc[i][e] + cp1[0][n];
+          o[e] = lrelu(yv[e] * cp1[1][n] + cp1[2][n]);
+        }
+        bf16x4 ub;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) ub[e] = (__bf16)((ing && (cm >> e & 1u)) ? o[e] : 0.f);
+        *reinterpret_cast<bf16x4*>(img_at(u1img, orow, kpo, n0)) = ub;
+        if (mine && cm) {
+          float* yp = a.y1 + (long long)gr * a.ldy1 + n0;
+          __bf16* up = a.u1 + (long long)gr * a.ldy1 + n0;
+          if (cm == 15u) {
+            *reinterpret_cast<float4*>(yp) = make_float4(yv[0], yv[1], yv[2], yv[3]);
+            *reinterpret_cast<bf16x4*>(up) = ub;
+          } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) if (cm >> e & 1u) { yp[e] = yv[e]; up[e] = ub[e]; }
+          }
+        }
+      }
+    });
+  }
+  __syncthreads();
+  stage_weights(a.k2, reinterpret_cast<char*>(wimg));
+  wait_dma();
+  // ---- conv2: window [r0 - 2, r0 + own + 2) -> U2 image; Y2 / U2 own rows; Y2n own rows in LDS
+  {
+    const int wr0 = tl.r0 - 2, n_out = own + 4, N = a.m2.phys();
+    conv_phase<2>(u1img, a.k2.kp, wimg, a.k2.kp, a.k2.np, n_out, nopre,
+                  [&](int orow, int nb0, f32x4 (&acc)[2], f32x4 (&)[2]) {
+      if (orow >= n_out) return;
+      const int gr = wr0 + orow;
+      const bool ing = gr >= tl.glo && gr < tl.ghi, mine = gr >= tl.r0 && gr < tl.rend;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int n0 = 16 * (nb0 + i) + 4 * lg;
+        if (n0 >= a.k2.np) continue;
+        float yv[4], o[4];
+        unsigned cm = 0u;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int n = n0 + e;
+          if (n < N && a.m2.valid(n)) cm |= 1u << e;
+          yv[e] = acc[i][e] + cp2[0][n];
+          o[e] = lrelu(yv[e] * cp2[1][n] + cp2[2][n]);
+        }
+        bf16x4 ub;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) ub[e] = (__bf16)((ing && (cm >> e & 1u)) ? o[e] : 0.f);
+        *reinterpret_cast<bf16x4*>(img_at(u2img, orow, kpu2, n0)) = ub;
+        if (mine && cm) {
+          float* yp = a.y2 + (long long)gr * a.ldy2 + n0;
+          __bf16* up = a.u2 + (long long)gr * a.ldy2 + n0;
+          if (cm == 15u) {
+            *reinterpret_cast<float4*>(yp) = make_float4(yv[0], yv[1], yv[2], yv[3]);
+            *reinterpret_cast<bf16x4*>(up) = ub;
+          } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) if (cm >> e & 1u) { yp[e] = yv[e]; up[e] = ub[e]; }
+          }
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int n = n0 + e;
+            if ((cm >> e & 1u) && n >= a.m2.offb && a.m2.b)
+              y2n[(gr - tl.r0) * L.ldY2n + (n - a.m2.offb)] = yv[e];
+          }
+        }
+      }
+    });
+  }
+  __syncthreads();
+  stage_weights(a.k3, reinterpret_cast<char*>(wimg));
+  wait_dma();
+  // ---- conv3 (s branch): own rows -> U3, Y3 (fp32, LDS; the spatial head's input)
+  {
+    const int n_out = own;
+    conv_phase<1>(u2img, kpu2, wimg, a.k3.kp, a.k3.np, n_out, nopre,
+                  [&](int orow, int nb0, f32x4 (&acc)[1], f32x4 (&)[1]) {
+      if (orow >= n_out) return;
+      const int n0 = 16 * nb0 + 4 * lg;
+      float yv[4], o[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int n = n0 + e;
+        const bool cv = n < a.s3;
+        yv[e] = cv ? acc[0][e] + cp3[0][n] : 0.f;
+        o[e] = cv ? lrelu(yv[e] * cp3[1][n] + cp3[2][n]) : 0.f;
+      }
+      *reinterpret_cast<float4*>(u3 + orow * 16 + n0) = make_float4(o[0], o[1], o[2], o[3]);
+      *reinterpret_cast<float4*>(y3 + orow * 16 + n0) = make_float4(yv[0], yv[1], yv[2], yv[3]);
+    });
+  }
+  __syncthreads();
+  // ---- heads: spatial (s3 -> sd) on threads 0..127, node (n2 -> nf) on 128..255
+  const int t = blockIdx.x;
+  if (tid < 256) {
+    const int hi = tid >> 7, orow = tid & 127;
+    const bool rv = orow < own;
+    const long long gr = tl.r0 + orow;
+    if (hi == 0) {
+      float u[10], yv[10];
+#pragma unroll
+      for (int k = 0; k < 10; ++k) { u[k] = rv ? u3[orow * 16 + k] : 0.f; yv[k] = rv ? y3[orow * 16 + k] : 0.f; }
+      head_tile<10, 2>(0, orow, rv, gr, u, yv, a.ws, a.bs, a.g3, a.be3, a.s_truth, a.cnt_s, a.shat,
+                       a.dy3 + gr * a.lddy3, a.phs + (long long)t * head_nq(10, 2), a.sse_s + t,
+                       hred[0], hsred[0]);
+    } else {
+      float u[20], yv[20];
+#pragma unroll
+      for (int k = 0; k < 20; ++k) {   // U2n: window row orow + 2 of the U2 image (bf16)
+        const int n = a.m2.offb + k;
+        u[k] = rv ? (float)img_at(u2img, orow + 2, kpu2, n & ~3)[n & 3] : 0.f;
+        yv[k] = rv ? y2n[orow * L.ldY2n + k] : 0.f;
+      }
+      head_tile<20, 1>(1, orow, rv, gr, u, yv, a.wn, a.bn, a.g2n, a.be2n, a.x_truth, a.cnt_n, a.xhat,
+                       a.dy2 + gr * a.lddy2 + a.m2.offb, a.phn + (long long)t * head_nq(20, 1),
+                       a.sse_n + t, hred[1], hsred[1]);
+    }
+  } else {
+    __syncthreads();   // matches the barrier inside head_tile
+  }
+}
+
+// ------------------------------------------------------------------ backward
+template <int NBH>
+__device__ __forceinline__ void colpart_flush(float (&q)[3][NBH][4], float* slots, int np, int nb0, int nbc,
+                                              int slot) {
+  const int lane = threadIdx.x & 63, li = lane & 15, lg = lane >> 4;
+#pragma unroll
+  for (int k = 0; k < 3; ++k)
+#pragma unroll
+    for (int i = 0; i < NBH; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float v = row16_sum(q[k][i][e]);
+        const int n = 16 * (nb0 + i) + 4 * lg + e;
+        if (li == 0 && nb0 + i < nbc) slots[(slot * 3 + k) * np + n] = v;
+      }
+}
+
+__global__ void __launch_bounds__(DT) dec_bwd_kernel(DecChainBwdArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  __shared__ float cpa[2][128], cpb[2][128];   // conv2-s BN (gamma c, beta), conv1 BN
+  const BwdLay L(a);
+  const Tile tl = tile_of(blockIdx.x, a.npg);
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, lg = lane >> 4;
+  __bf16* wimg = reinterpret_cast<__bf16*>(smem + L.w);
+  __bf16* d3 = reinterpret_cast<__bf16*>(smem + L.d3);
+  __bf16* d2 = reinterpret_cast<__bf16*>(smem + L.d2);
+  __bf16* d1 = reinterpret_cast<__bf16*>(smem + L.d1);
+  float* slots = reinterpret_cast<float*>(smem + L.cps);
+  const int own = tl.rend - tl.r0;
+  const int t = blockIdx.x;
+
+  for (int i = tid * 16; i < L.cps - L.d3; i += DT * 16)
+    *reinterpret_cast<uint4*>(smem + L.d3 + i) = make_uint4(0u, 0u, 0u, 0u);
+  __syncthreads();
+  // dY3 window [r0 - 6, r0 + own + 6), conv3^T weights
+  stage_window(a.dy3, a.lddy3, a.s3, tl.r0 - 6, in_rows(TR + 8), own + 12, tl.glo, tl.ghi, a.k3t.kp,
+               reinterpret_cast<char*>(d3), a.zero);
+  stage_weights(a.k3t, reinterpret_cast<char*>(wimg));
+  if (tid < 128) {
+    const int n = tid;
+    const ColMap ms{a.m2.a, 0, a.m2.a};
+    cpa[0][n] = colpar(ms, n, a.g2s, nullptr) * kBnC;
+    cpa[1][n] = colpar(ms, n, a.be2s, nullptr);
+    cpb[0][n] = colpar(a.m1, n, a.g1, nullptr) * kBnC;
+    cpb[1][n] = colpar(a.m1, n, a.be1, nullptr);
+  }
+  // dY2 n part of the window [r0 - 4, r0 + own + 4) (the heads' output) into the dY2 image
+  {
+    const int wr0 = tl.r0 - 4, nv = own + 8, kp2 = a.k2t.kp;
+    const int nq = (a.m2.b + 3) / 4;             // 4-column groups of the n part
+    for (int i = tid; i < nv * nq; i += DT) {
+      const int row = i / nq, q = i - row * nq;
+      const int gr = wr0 + row;
+      if (gr < tl.glo || gr >= tl.ghi) continue;
+      const int n0 = a.m2.offb + 4 * q;
+      const bf16x4 v = *reinterpret_cast<const bf16x4*>(a.dy2 + (long long)gr * a.lddy2 + n0);
+      *reinterpret_cast<bf16x4*>(img_at(d2, row, kp2, n0)) = v;
+    }
+  }
+  wait_dma();
+  // ---- conv3^T: window [r0 - 4, r0 + own + 4): dU2s -> BN/lrelu backward -> dY2s
+  {
+    const int wr0 = tl.r0 - 4, n_out = own + 8, N = a.m2.a, kpo = a.k2t.kp;
+    const int nbc = a.k3t.np >> 4, ncg = nbc, wpc = NW / ncg;
+    const int nb0 = w % ncg;
+    float q[3][1][4] = {};
+    conv_phase<1>(d3, a.k3t.kp, wimg, a.k3t.kp, a.k3t.np, n_out,
+                  [&](int orow, int nb, f32x4 (&yp)[1]) {
+                    yp[0] = f32x4{0.f, 0.f, 0.f, 0.f};
+                    const int gr = wr0 + orow;
+                    if (orow < n_out && gr >= tl.glo && gr < tl.ghi) {
+                      const int n0 = 16 * nb + 4 * lg;
+                      const float* p = a.y2 + (long long)gr * a.ldy2 + n0;
+#pragma unroll
+                      for (int e = 0; e < 4; ++e) if (n0 + e < N) yp[0][e] = p[e];
+                    }
+                  },
+                  [&](int orow, int nb, f32x4 (&acc)[1], f32x4 (&yp)[1]) {
+      if (orow >= n_out) return;
+      const int gr = wr0 + orow;
+      const bool ing = gr >= tl.glo && gr < tl.ghi, mine = gr >= tl.r0 && gr < tl.rend;
+      const int n0 = 16 * nb + 4 * lg;
+      float o[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int n = n0 + e;
+        const bool cv = n < N && ing;
+        const float ga = cpa[0][n], be = cpa[1][n];
+        const float dt = cv ? acc[0][e] * lrelu_grad(yp[0][e] * ga + be) : 0.f;
+        o[e] = dt * ga;
+        if (mine) { q[0][0][e] += dt * yp[0][e]; q[1][0][e] += dt; q[2][0][e] += o[e]; }
+      }
+      bf16x4 ob;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) ob[e] = (__bf16)o[e];
+      if (n0 < a.m2.offb || !a.m2.b)    // s part only (the n part came from the heads)
+        *reinterpret_cast<bf16x4*>(img_at(d2, orow, kpo, n0)) = ob;
+      if (mine) {
+        __bf16* dp = a.dy2 + (long long)gr * a.lddy2 + n0;
+        if (n0 + 3 < N) *reinterpret_cast<bf16x4*>(dp) = ob;
+        else
+#pragma unroll
+          for (int e = 0; e < 4; ++e) if (n0 + e < N) dp[e] = ob[e];
+      }
+    });
+    if (w / ncg < wpc) colpart_flush<1>(q, slots, a.k3t.np, nb0, nbc, w / ncg);
+    __syncthreads();
+    for (int i = tid; i < 3 * N; i += DT) {
+      const int k = i / N, n = i - k * N;
+      float s = 0.f;
+      for (int sl = 0; sl < wpc; ++sl) s += slots[(sl * 3 + k) * a.k3t.np + n];
+      a.pc2s[(long long)t * 3 * N + i] = s;
+    }
+  }
+  __syncthreads();
+  stage_weights(a.k2t, reinterpret_cast<char*>(wimg));
+  wait_dma();
+  // ---- conv2^T: window [r0 - 2, r0 + own + 2): dU1 -> BN/lrelu backward -> dY1
+  {
+    const int wr0 = tl.r0 - 2, n_out = own + 4, W1 = a.m1.phys(), kpo = a.k1t.kp;
+    const int nbc = a.k2t.np >> 4, ncg = (nbc + 1) / 2, wpc = NW / ncg;
+    const int nb0 = 2 * (w % ncg);
+    float q[3][2][4] = {};
+    conv_phase<2>(d2, a.k2t.kp, wimg, a.k2t.kp, a.k2t.np, n_out,
+                  [&](int orow, int nb, f32x4 (&yp)[2]) {
+                    const int gr = wr0 + orow;
+                    const bool ok = orow < n_out && gr >= tl.glo && gr < tl.ghi;
+#pragma unroll
+                    for (int i = 0; i < 2; ++i) {
+                      yp[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+                      const int n0 = 16 * (nb + i) + 4 * lg;
+                      if (ok && n0 < W1) {
+                        const float* p = a.y1 + (long long)gr * a.ldy1 + n0;
+                        if (n0 + 3 < W1) yp[i] = *reinterpret_cast<const f32x4*>(p);
+                        else
+#pragma unroll
+                          for (int e = 0; e < 4; ++e) if (n0 + e < W1) yp[i][e] = p[e];
+                      }
+                    }
+                  },
+                  [&](int orow, int nb, f32x4 (&acc)[2], f32x4 (&yp)[2]) {
+      if (orow >= n_out) return;
+      const int gr = wr0 + orow;
+      const bool ing = gr >= tl.glo && gr < tl.ghi, mine = gr >= tl.r0 && gr < tl.rend;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int n0 = 16 * (nb + i) + 4 * lg;
+        if (n0 >= a.k2t.np) continue;
+        float o[4];
+        unsigned cm = 0u;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int n = n0 + e;
+          const bool cv = n < W1 && a.m1.valid(n);
+          if (cv) cm |= 1u << e;
+          const float ga = cpb[0][n], be = cpb[1][n];
+          const float dt = (cv && ing) ? acc[i][e] * lrelu_grad(yp[i][e] * ga + be) : 0.f;
+          o[e] = dt * ga;
+          if (mine) { q[0][i][e] += dt * yp[i][e]; q[1][i][e] += dt; q[2][i][e] += o[e]; }
+        }
+        bf16x4 ob;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) ob[e] = (__bf16)o[e];
+        *reinterpret_cast<bf16x4*>(img_at(d1, orow, kpo, n0)) = ob;
+        if (mine && cm) {
+          __bf16* dp = a.dy1 + (long long)gr * a.lddy1 + n0;
+          if (cm == 15u) *reinterpret_cast<bf16x4*>(dp) = ob;
+          else
+#pragma unroll
+            for (int e = 0; e < 4; ++e) if (cm >> e & 1u) dp[e] = ob[e];
+        }
+      }
+    });
+    __syncthreads();   // slots: the conv3^T partials were consumed above
+    if (w / ncg < wpc) colpart_flush<2>(q, slots, a.k2t.np, nb0, nbc, w / ncg);
+    __syncthreads();
+    for (int i = tid; i < 3 * W1; i += DT) {
+      const int k = i / W1, n = i - k * W1;
+      float s = 0.f;
+      for (int sl = 0; sl < wpc; ++sl) s += slots[(sl * 3 + k) * a.k2t.np + n];
+      a.pc1[(long long)t * 3 * W1 + i] = s;
+    }
+  }
+  __syncthreads();
+  stage_weights(a.k1t, reinterpret_cast<char*>(wimg));
+  wait_dma();
+  // ---- conv1^T: own rows -> dJ (fp32)
+  {
+    const int n_out = own, N = a.dj;
+    conv_phase<2>(d1, a.k1t.kp, wimg, a.k1t.kp, a.k1t.np, n_out, [](int, int, auto&) {},
+                  [&](int orow, int nb, f32x4 (&acc)[2], f32x4 (&)[2]) {
+      if (orow >= n_out) return;
+      const long long gr = tl.r0 + orow;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int n0 = 16 * (nb + i) + 4 * lg;
+        if (n0 >= N) continue;
+        *reinterpret_cast<float4*>(a.dz + gr * a.lddz + n0) =
+            make_float4(acc[i][0], acc[i][1], acc[i][2], acc[i][3]);
+      }
+    });
+  }
+}
+
+}  // namespace
+
+int dec_tiles(int ngraphs, int npg) { return ngraphs * ((npg + kDecRows - 1) / kDecRows); }
+int dec_head_parts(int cin, int cout) { return head_nq(cin, cout); }
+
+bool dec_fused_supported(int dj, const ColMap& m1, const ColMap& m2, int s3, int sd, int nf,
+                         const DecImg& k1, const DecImg& k2, const DecImg& k3, const DecImg& k3t,
+                         const DecImg& k2t, const DecImg& k1t) {
+  if (!(s3 == 10 && sd == 2 && m2.b == 20 && nf == 1)) return false;   // built heads (10,2), (20,1)
+  if (dj % 16 || dj > 128 || m1.phys() > 128 || m2.phys() > 64) return false;
+  DecChainFwdArgs f{};
+  f.k1 = k1; f.k2 = k2; f.k3 = k3; f.m1 = m1; f.m2 = m2; f.s3 = s3;
+  DecChainBwdArgs b{};
+  b.k3t = k3t; b.k2t = k2t; b.k1t = k1t; b.m1 = m1; b.m2 = m2; b.s3 = s3; b.dj = dj;
+  const int lim = 160 * 1024 - 8 * 1024;   // static LDS of the kernels
+  if (FwdLay(f).total > lim || BwdLay(b).total > lim) return false;
+  // image kp: conv inputs must match the packed images
+  if (k3.kp > 64 || k3t.np != 32 || k2t.np > 128 || k1t.np != ((dj + 15) / 16) * 16) return false;
+  return 16 % ((k2t.np / 16 + 1) / 2) == 0 && 16 % (k3t.np / 16) == 0;
+}
+
+int dec_init_attributes() {
+  static int done = 0;
+  if (done) return 0;
+  const int lim = 160 * 1024 - 8 * 1024;
+  if (hipFuncSetAttribute(reinterpret_cast<const void*>(dec_fwd_kernel),
+                          hipFuncAttributeMaxDynamicSharedMemorySize, lim) != hipSuccess ||
+      hipFuncSetAttribute(reinterpret_cast<const void*>(dec_bwd_kernel),
+                          hipFuncAttributeMaxDynamicSharedMemorySize, lim) != hipSuccess) {
+    set_error("dec: hipFuncSetAttribute failed");
+    return SND_ERR_HIP;
+  }
+  done = 1;
+  return 0;
+}
+
+int launch_dec_chain_fwd(const DecChainFwdArgs& a, hipStream_t s) {
+  SND_CHECK_ARG(a.R == a.npg * a.ngraphs && a.R > 0, "dec_fwd: R != npg * ngraphs");
+  SND_CHECK_ARG(a.zb && a.y1 && a.u1 && a.y2 && a.u2 && a.dy3 && a.dy2 && a.phs && a.phn && a.sse_s &&
+                    a.sse_n && a.s_truth && a.x_truth && a.zero && a.k1.w && a.k2.w && a.k3.w,
+                "dec_fwd: null operand");
+  SND_CHECK_ARG(a.ldz % 8 == 0 && a.ldy1 % 4 == 0 && a.ldy2 % 4 == 0 && a.lddy3 % 4 == 0 && a.lddy2 % 4 == 0,
+                "dec_fwd: leading dims");
+  SND_TRY(dec_init_attributes());
+  const size_t lds = FwdLay(a).total;
+  hipLaunchKernelGGL(dec_fwd_kernel, dim3(dec_tiles(a.ngraphs, a.npg)), dim3(DT), lds, s, a);
+  SND_LAUNCH_CHECK("dec_fwd_kernel");
+  return 0;
+}
+
+int launch_dec_chain_bwd(const DecChainBwdArgs& a, hipStream_t s) {
+  SND_CHECK_ARG(a.R == a.npg * a.ngraphs && a.R > 0, "dec_bwd: R != npg * ngraphs");
+  SND_CHECK_ARG(a.y1 && a.y2 && a.dy3 && a.dy2 && a.dy1 && a.dz && a.pc2s && a.pc1 && a.zero &&
+                    a.k3t.w && a.k2t.w && a.k1t.w, "dec_bwd: null operand");
+  SND_CHECK_ARG(a.lddy3 % 8 == 0 && a.lddy2 % 4 == 0 && a.lddy1 % 4 == 0 && a.lddz % 4 == 0,
+                "dec_bwd: leading dims");
+  SND_TRY(dec_init_attributes());
+  const size_t lds = BwdLay(a).total;
+  hipLaunchKernelGGL(dec_bwd_kernel, dim3(dec_tiles(a.ngraphs, a.npg)), dim3(DT), lds, s, a);
+  SND_LAUNCH_CHECK("dec_bwd_kernel");
+  return 0;
+}
+
+}  // namespace snd

@@ -853,11 +853,16 @@ int launch_wgrad_multi(const WgArgs* a, int n, hipStream_t s) {
   return 0;
 }
 
-WgGeom wgrad_geom(int R, int T, int K, int N) {
+WgGeom wgrad_geom(int R, int T, int K, int N, int chunks) {
   WgGeom g{};
   const int P = T * cdiv(K, 16);
   g.pairs_per_wg = std::min(P, WGT / 64);
   g.gy = cdiv(P, g.pairs_per_wg);
+  if (chunks > 0) {   // multi-segment launch: long row chunks pipeline their staging
+    g.rows_per_wg = (int)round_up(cdiv(R, chunks), kRcRows);
+    g.gx = cdiv(R, g.rows_per_wg);
+    return g;
+  }
   // row chunks: about 256 workgroups in all, but at most 64 slabs of a large weight
   int gx = std::max(1, 256 / g.gy);
   if ((long long)T * K * N >= 65536) gx = std::min(gx, 64);   // bound the slab traffic

@@ -96,7 +96,9 @@ struct WgArgs {
   int dbg;
 };
 struct WgGeom { int rows_per_wg, pairs_per_wg, gx, gy; };
-WgGeom wgrad_geom(int R, int T, int K, int N);
+// chunks > 0: that many row chunks per weight (the step's multi-segment launch);
+// 0: about 256 workgroups per weight (one launch each)
+WgGeom wgrad_geom(int R, int T, int K, int N, int chunks = 0);
 inline int wgrad_n4(int N) { return (N + 3) & ~3; }
 int launch_wgrad(const WgArgs& a, hipStream_t s);
 // n independent weight gradients (each its own geometry and slab) in one launch

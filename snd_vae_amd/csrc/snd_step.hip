@@ -16,6 +16,7 @@
 #include <string>
 #include <vector>
 
+#include "snd_dec.hpp"
 #include "snd_decode.hpp"
 #include "snd_elem.hpp"
 #include "snd_fast.hpp"
@@ -77,6 +78,8 @@ struct snd_plan {
   Split sW0, sW1, sWh, sWms, sK1, sK2s, sK2n, sK3s;
   // ---- bf16 fast decoder (snd_fast.hip)
   bool fast = false;
+  bool dec_fused = false;      // fused decoder (snd_dec.hip): 2 launches instead of 7
+  int dtiles = 0;
   ColMap m1{}, m2{};
   int ld1 = 0, ld2 = 0, ld3 = 0;
   Img pk1f{}, pk2f{}, pk3f{}, pk3b{}, pk2b{}, pk1b{};
@@ -256,6 +259,10 @@ extern "C" int snd_plan_create(const snd_config_t* cfg, int n_graphs, snd_plan_t
   p->add_buf("SK2N", (long long)p->sK2n.splits * 5 * c.n1 * c.n2);
   p->add_buf("SK3S", (long long)p->sK3s.splits * 5 * c.s2 * c.s3);
 
+  // row chunks per weight gradient: the step launches them all at once (debug bit
+  // 4096: one launch each, 8192: one launch each's ~256-workgroup geometry)
+  const int dbg = debug_flags();
+  const int wgc = (dbg & (4096 | 8192)) ? 0 : ((dbg & 16384) ? 64 : 32);
   // ---- bf16 fast decoder: split [s | n] column layouts, packed weight images
   if (c.dtype == SND_BF16 && !(debug_flags() & 256)) {
     const ColMap m1 = colmap_split(c.s1, c.n1), m2 = colmap_split(c.s2, c.n2);
@@ -292,14 +299,26 @@ extern "C" int snd_plan_create(const snd_config_t* cfg, int n_graphs, snd_plan_t
       p->add_buf("PFDEC1", (long long)rcb * 3 * w1);
       p->add_buf("PFHS", (long long)hb * heads_fast_parts(c.s3, c.spatial_dim));
       p->add_buf("PFHN", (long long)hb * heads_fast_parts(c.n2, c.num_feature));
-      p->gK1 = wgrad_geom(p->R, 5, dj, w1);
-      p->gK2s = wgrad_geom(p->R, 5, c.s1, c.s2);
-      p->gK2n = wgrad_geom(p->R, 5, c.n1, c.n2);
-      p->gK3s = wgrad_geom(p->R, 5, c.s2, c.s3);
+      p->gK1 = wgrad_geom(p->R, 5, dj, w1, wgc);
+      p->gK2s = wgrad_geom(p->R, 5, c.s1, c.s2, wgc);
+      p->gK2n = wgrad_geom(p->R, 5, c.n1, c.n2, wgc);
+      p->gK3s = wgrad_geom(p->R, 5, c.s2, c.s3, wgc);
       p->add_buf("FSK1", (long long)p->gK1.gx * 5 * dj * wgrad_n4(w1));
       p->add_buf("FSK2S", (long long)p->gK2s.gx * 5 * c.s1 * wgrad_n4(c.s2));
       p->add_buf("FSK2N", (long long)p->gK2n.gx * 5 * c.n1 * wgrad_n4(c.n2));
       p->add_buf("FSK3S", (long long)p->gK3s.gx * 5 * c.s2 * wgrad_n4(c.s3));
+      auto dimg = [&](const Img& im) { return DecImg{nullptr, im.kp, im.np}; };
+      if (!(dbg & 32768) &&
+          dec_fused_supported(dj, m1, m2, c.s3, c.spatial_dim, c.num_feature, dimg(p->pk1f), dimg(p->pk2f),
+                              dimg(p->pk3f), dimg(p->pk3b), dimg(p->pk2b), dimg(p->pk1b))) {
+        p->dec_fused = true;
+        p->dtiles = dec_tiles(p->B, p->N);
+        const long long t = p->dtiles;
+        p->add_buf("PDHS", t * dec_head_parts(c.s3, c.spatial_dim));
+        p->add_buf("PDHN", t * dec_head_parts(c.n2, c.num_feature));
+        p->add_buf("PDSSES", t, 8); p->add_buf("PDSSEN", t, 8);
+        p->add_buf("PDC2S", t * 3 * c.s2); p->add_buf("PDC1", t * 3 * w1);
+      }
     }
   }
   // ---- bf16 fast encoder, graph latent: GCN layers + BN backward on the fast engine;
@@ -328,8 +347,8 @@ extern "C" int snd_plan_create(const snd_config_t* cfg, int n_graphs, snd_plan_t
       const int rcb = rc_blocks(p->R);
       p->add_buf("PFENC1", (long long)rcb * 4 * W);
       p->add_buf("PFENC0", (long long)rcb * 2 * h0);
-      p->gW1 = wgrad_geom(p->R, 1, h0 + f, h1);
-      p->gW0 = wgrad_geom(p->R, 1, f, h0);
+      p->gW1 = wgrad_geom(p->R, 1, h0 + f, h1, wgc);
+      p->gW0 = wgrad_geom(p->R, 1, f, h0, wgc);
       p->add_buf("FSW1", (long long)p->gW1.gx * (h0 + f) * wgrad_n4(h1));
       p->add_buf("FSW0", (long long)p->gW0.gx * f * wgrad_n4(h0));
     }
@@ -364,10 +383,10 @@ extern "C" int snd_plan_create(const snd_config_t* cfg, int n_graphs, snd_plan_t
       p->add_buf("PFBH", (long long)rcb * gh);
       p->add_buf("PFENC1", (long long)rcb * 4 * W);
       p->add_buf("PFENC0", (long long)rcb * 2 * h0);
-      p->gWms = wgrad_geom(p->R, 1, gh, 2 * L);
-      p->gWh = wgrad_geom(p->R, 1, W, gh);
-      p->gW1 = wgrad_geom(p->R, 1, h0 + f, h1);
-      p->gW0 = wgrad_geom(p->R, 1, f, h0);
+      p->gWms = wgrad_geom(p->R, 1, gh, 2 * L, wgc);
+      p->gWh = wgrad_geom(p->R, 1, W, gh, wgc);
+      p->gW1 = wgrad_geom(p->R, 1, h0 + f, h1, wgc);
+      p->gW0 = wgrad_geom(p->R, 1, f, h0, wgc);
       p->add_buf("FSWMS", (long long)p->gWms.gx * gh * wgrad_n4(2 * L));
       p->add_buf("FSWH", (long long)p->gWh.gx * W * wgrad_n4(gh));
       p->add_buf("FSW1", (long long)p->gW1.gx * (h0 + f) * wgrad_n4(h1));
@@ -814,6 +833,48 @@ int decoder_fast(const Ctx& x, const snd_batch_t* batch, int only = -1) {
   const int sd = c.spatial_dim, nf = c.num_feature;
   const int w1 = p.m1.phys(), w2 = p.m2.phys(), o1 = p.m1.offb, o2 = p.m2.offb;
   auto bf = [&](const char* n) { return reinterpret_cast<__bf16*>(x.f(n)); };
+  if (p.dec_fused && only < 0) {
+    auto img = [&](const Img& im) {
+      return DecImg{reinterpret_cast<const __bf16*>(x.ws + im.off), im.kp, im.np};
+    };
+    DecChainFwdArgs f{};
+    f.zb = bf("ZB"); f.ldz = L; f.dj = L;
+    f.R = R; f.npg = p.N; f.ngraphs = p.B;
+    f.k1 = img(p.pk1f); f.k2 = img(p.pk2f); f.k3 = img(p.pk3f);
+    f.m1 = p.m1; f.m2 = p.m2; f.s3 = s3;
+    f.b1 = x.w("dec.b1"); f.g1 = x.w("dec.bn1.gamma"); f.be1 = x.w("dec.bn1.beta");
+    f.b2s = x.w("dec.b2s"); f.g2s = x.w("dec.bn2s.gamma"); f.be2s = x.w("dec.bn2s.beta");
+    f.b2n = x.w("dec.b2n"); f.g2n = x.w("dec.bn2n.gamma"); f.be2n = x.w("dec.bn2n.beta");
+    f.b3 = x.w("dec.b3s"); f.g3 = x.w("dec.bn3s.gamma"); f.be3 = x.w("dec.bn3s.beta");
+    f.y1 = x.f("FY1"); f.ldy1 = p.ld1; f.u1 = bf("FU1");
+    f.y2 = x.f("FY2"); f.ldy2 = p.ld2; f.u2 = bf("FU2");
+    f.ws = x.w("dec.Ws"); f.bs = x.w("dec.bs"); f.sd = sd; f.s_truth = batch->spatial_truth;
+    f.cnt_s = (float)R * sd; f.shat = x.f("SHAT");
+    f.wn = x.w("dec.Wn"); f.bn = x.w("dec.bn"); f.nf = nf; f.x_truth = batch->feature_truth;
+    f.cnt_n = (float)R * nf; f.xhat = x.f("XHAT");
+    f.dy3 = bf("FDY3"); f.lddy3 = p.ld3; f.dy2 = bf("FDY2"); f.lddy2 = p.ld2;
+    f.phs = x.f("PDHS"); f.phn = x.f("PDHN"); f.sse_s = x.d("PDSSES"); f.sse_n = x.d("PDSSEN");
+    f.zero = x.ws + p.buf("ZERO");
+    SND_TRY(launch_dec_chain_fwd(f, x.s));
+    DecChainBwdArgs b{};
+    b.R = R; b.npg = p.N; b.ngraphs = p.B; b.dj = L;
+    b.k3t = img(p.pk3b); b.k2t = img(p.pk2b); b.k1t = img(p.pk1b);
+    b.m1 = p.m1; b.m2 = p.m2; b.s3 = s3;
+    b.g1 = x.w("dec.bn1.gamma"); b.be1 = x.w("dec.bn1.beta");
+    b.g2s = x.w("dec.bn2s.gamma"); b.be2s = x.w("dec.bn2s.beta");
+    b.y1 = x.f("FY1"); b.ldy1 = p.ld1; b.y2 = x.f("FY2"); b.ldy2 = p.ld2;
+    b.dy3 = bf("FDY3"); b.lddy3 = p.ld3; b.dy2 = bf("FDY2"); b.lddy2 = p.ld2;
+    b.dy1 = bf("FDY1"); b.lddy1 = p.ld1; b.dz = x.f("DZDEC"); b.lddz = L;
+    b.pc2s = x.f("PDC2S"); b.pc1 = x.f("PDC1");
+    b.zero = x.ws + p.buf("ZERO");
+    SND_TRY(launch_dec_chain_bwd(b, x.s));
+    SND_TRY(wgrad(x, wg_args(p, x.ws, p.gK3s, bf("FU2"), p.ld2, s2, bf("FDY3"), p.ld3, s3, x.f("FSK3S")), x.s));
+    SND_TRY(wgrad(x, wg_args(p, x.ws, p.gK2s, bf("FU1"), p.ld1, c.s1, bf("FDY2"), p.ld2, s2, x.f("FSK2S")), x.s));
+    SND_TRY(wgrad(x, wg_args(p, x.ws, p.gK2n, bf("FU1") + o1, p.ld1, c.n1, bf("FDY2") + o2, p.ld2, n2,
+                             x.f("FSK2N")), x.s));
+    SND_TRY(wgrad(x, wg_args(p, x.ws, p.gK1, bf("ZB"), L, L, bf("FDY1"), p.ld1, w1, x.f("FSK1")), x.s));
+    return 0;
+  }
   // conv1 (fused [s1 | n0] branches): z -> Y1, U1
   {
     RcArgs a = rc_args(p, x.ws, p.pk1f, bf("ZB"), L, L, w1, p.m1);
@@ -896,7 +957,8 @@ void decoder_fast_reduce(const Ctx& x, std::vector<ReduceDesc>& rd) {
   const int L = p.dj, s1 = c.s1, n1 = c.n1, s2 = c.s2, n2 = c.n2, s3 = c.s3, C1 = p.C1;
   const int sd = c.spatial_dim, nf = c.num_feature;
   const int w1 = p.m1.phys(), o1 = p.m1.offb;
-  const int rcb = rc_blocks(p.R), hb = heads_fast_blocks(p.R);
+  const int rcb = p.dec_fused ? p.dtiles : rc_blocks(p.R);
+  const int hb = p.dec_fused ? p.dtiles : heads_fast_blocks(p.R);
   // slab [parts][rows][n4] -> weight [rows][N]
   auto slab2d = [&](const char* buf, int parts, int rows, int N, const char* dst) {
     const int n4 = wgrad_n4(N);
@@ -920,9 +982,11 @@ void decoder_fast_reduce(const Ctx& x, std::vector<ReduceDesc>& rd) {
     rd.push_back({s0 + width, x.g(b) + dst0, parts, len, st, 1.f, 0, 0, 0, 0});
     rd.push_back({s0 + 2 * width, x.g(bias) + dst0, parts, len, st, 1.f, 0, 0, 0, 0});
   };
-  cols3("PFDEC2S", rcb, s2, 0, s2, "dec.bn2s.gamma", "dec.bn2s.beta", "dec.b2s", 0);
-  cols3("PFDEC1", rcb, w1, 0, s1, "dec.bn1.gamma", "dec.bn1.beta", "dec.b1", 0);
-  cols3("PFDEC1", rcb, w1, o1, n1, "dec.bn1.gamma", "dec.bn1.beta", "dec.b1", s1);
+  const char* pc2 = p.dec_fused ? "PDC2S" : "PFDEC2S";
+  const char* pc1 = p.dec_fused ? "PDC1" : "PFDEC1";
+  cols3(pc2, rcb, s2, 0, s2, "dec.bn2s.gamma", "dec.bn2s.beta", "dec.b2s", 0);
+  cols3(pc1, rcb, w1, 0, s1, "dec.bn1.gamma", "dec.bn1.beta", "dec.b1", 0);
+  cols3(pc1, rcb, w1, o1, n1, "dec.bn1.gamma", "dec.bn1.beta", "dec.b1", s1);
   // heads: {dW, db, sum dt*y, sum dt, sum dy}
   auto head = [&](const char* buf, int cin, int cout, const char* W, const char* bb, const char* g,
                   const char* be, const char* bias) {
@@ -935,8 +999,8 @@ void decoder_fast_reduce(const Ctx& x, std::vector<ReduceDesc>& rd) {
     rd.push_back({s0 + q + cin, x.g(be), hb, cin, st, 1.f, 0, 0, 0, 0});
     rd.push_back({s0 + q + 2 * cin, x.g(bias), hb, cin, st, 1.f, 0, 0, 0, 0});
   };
-  head("PFHS", s3, sd, "dec.Ws", "dec.bs", "dec.bn3s.gamma", "dec.bn3s.beta", "dec.b3s");
-  head("PFHN", n2, nf, "dec.Wn", "dec.bn", "dec.bn2n.gamma", "dec.bn2n.beta", "dec.b2n");
+  head(p.dec_fused ? "PDHS" : "PFHS", s3, sd, "dec.Ws", "dec.bs", "dec.bn3s.gamma", "dec.bn3s.beta", "dec.b3s");
+  head(p.dec_fused ? "PDHN" : "PFHN", n2, nf, "dec.Wn", "dec.bn", "dec.bn2n.gamma", "dec.bn2n.beta", "dec.b2n");
 }
 
 }  // namespace
@@ -1113,7 +1177,7 @@ extern "C" int snd_train_step(const snd_plan_t* plan, const snd_batch_t* batch,
   // single stream: every fast-path weight gradient waits for one launch before the
   // reduction (debug bit 4096: one launch per weight, as before)
   std::vector<WgArgs> wq;
-  if (p.fast && !x.side && !(debug_flags() & 4096)) {
+  if (p.fast && !x.side && !(debug_flags() & (4096 | 8192))) {
     wq.reserve(kMaxWgMulti);
     x.wq = &wq;
   }
@@ -1384,7 +1448,8 @@ extern "C" int snd_train_step(const snd_plan_t* plan, const snd_batch_t* batch,
   const int n_kl = (p.fast && !p.tref) ? reparam_prep_blocks(p.B, zzt_npad(N)) : reparam_blocks(RH, L);
   FinalizeArgs fa{x.d("PZZT"), zzt_dense_blocks(p.B, N, c.dtype), x.d("PEDGE"),
                   p.fast ? edge_bf16_blocks(R) : edge_blocks(R, dj),
-                  x.d("PKL"), n_kl, x.d("PSSES"), x.d("PSSEN"), nh,
+                  x.d("PKL"), n_kl, x.d(p.dec_fused ? "PDSSES" : "PSSES"),
+                  x.d(p.dec_fused ? "PDSSEN" : "PSSEN"), p.dec_fused ? p.dtiles : nh,
                   rp, p.B, N, L, sd, nf, c.beta, c.norm, losses, grads + p.pcount, step_counter,
                   (double)RH * L};
   return launch_reduce(rd.data(), (int)rd.size(), x.s, &fa);   // + loss terms in one launch

@@ -290,3 +290,53 @@ def test_forced_world1_process_group_runs_the_distributed_step():
         assert torch.equal(oa.losses, ob.losses)
     finally:
         dist.destroy_process_group()
+
+
+DEC_BUFS = (("FY1", torch.float32), ("FU1", torch.bfloat16), ("FY2", torch.float32),
+            ("FU2", torch.bfloat16), ("FDY3", torch.bfloat16), ("FDY2", torch.bfloat16),
+            ("FDY1", torch.bfloat16), ("DZDEC", torch.float32), ("SHAT", torch.float32),
+            ("XHAT", torch.float32))
+
+
+@pytest.mark.parametrize("topology,n,d,B", [("tscale", 512, 64, 2), ("tscale", 200, 16, 3),
+                                            ("tref", 300, 32, 2)])
+def test_fused_decoder_matches_row_engine(topology, n, d, B):
+    """The fused decoder (snd_dec.hip: conv chain + heads in one launch, the
+    backward data chain in another, halos recomputed in LDS) against the row
+    engine's seven launches (debug bit 32768): every activation, data gradient
+    and head output is bitwise equal; the parameter gradients built from
+    column partials (biases, BN, heads) agree to fp32 reassociation, and the
+    conv weight gradients (same operands) are bitwise equal.  Covers partial
+    tiles (N = 200, 300: 128-row tiles never span graphs) and the graph latent."""
+    from snd_vae_amd import _lib
+    from snd_vae_amd.params import init_blocks
+    cfg = tscale(n, d) if topology == "tscale" else tref(n, d, g_hidden=16, latent=8)
+    batch = synthetic_batch(cfg, B, seed=11)
+    p0 = init_blocks(cfg, 2)
+    runs = []
+    for flags in (32768, 0):
+        _lib.check(_lib.lib().snd_debug_set(flags))
+        try:
+            m, o, b = make(cfg, batch, p0, "bf16")
+        finally:
+            _lib.check(_lib.lib().snd_debug_set(0))
+        o.forward_backward(b)
+        torch.cuda.synchronize()
+        runs.append((m, o))
+    (m0, o0), (m1, o1) = runs
+    R = B * n
+    for name, dt in DEC_BUFS:
+        a, c = m0.buffer(name, dt), m1.buffer(name, dt)
+        assert torch.equal(a, c), name
+    g0, g1 = o0.grad_blocks(), o1.grad_blocks()
+    for k in g0:
+        if not k.startswith("dec."):
+            continue
+        if k.startswith("dec.K"):
+            assert np.array_equal(g0[k], g1[k]), k
+        else:
+            np.testing.assert_allclose(g1[k], g0[k], rtol=1e-4, atol=1e-7 * max(1.0, np.abs(g0[k]).max()),
+                                       err_msg=k)
+    l0, l1 = o0.loss_dict(), o1.loss_dict()
+    for k in ("spatial_cost", "node_cost", "cost"):
+        assert l1[k] == pytest.approx(l0[k], rel=1e-6), k
