@@ -32,6 +32,9 @@ namespace {
 constexpr int DT = 1024;                  // 16 waves
 constexpr int NW = DT / 64;
 constexpr int TR = kDecRows;
+// dynamic LDS of both kernels (their static LDS -- column parameters, head partials -- stays
+// below 160 KB - kDynLds)
+constexpr int kDynLds = 148 * 1024;
 
 typedef __attribute__((address_space(1))) const void* gptr_t;
 typedef __attribute__((address_space(3))) void* lptr_t;
@@ -49,6 +52,12 @@ __host__ __device__ __forceinline__ int img_bytes(int rows, int kp) {
 }
 __host__ __device__ __forceinline__ int rup(int a, int b) { return (a + b - 1) / b * b; }
 __host__ __device__ constexpr int head_nq(int cin, int cout) { return cin * cout + cout + 3 * cin; }
+// head reduction scratch (aliases the weight image once the convs are done): per head
+// [NQ][kScr] floats (row stride 129 words) + 128 doubles of squared errors
+constexpr int kScr = 129;
+__host__ __device__ constexpr int head_scr_bytes() {
+  return (head_nq(10, 2) + head_nq(20, 1)) * kScr * 4 + 2 * 128 * 8;
+}
 
 // rows of the input image of a k=5 phase whose output window has n_out rows
 __host__ __device__ __forceinline__ int in_rows(int n_out) { return rup(n_out, 16) + 4; }
@@ -58,7 +67,8 @@ struct FwdLay {
   int w, a, b, c, total;        // offsets: weights | A: J -> U2 | B: U1 -> U3,Y3 | C: Y2n
   int ldY2n;
   __host__ __device__ FwdLay(const DecChainFwdArgs& p) {
-    const int wb = max(max(p.k1.np * p.k1.kp, p.k2.np * p.k2.kp), p.k3.np * p.k3.kp) * 5 * 2;
+    const int wb = max(max(max(p.k1.np * p.k1.kp, p.k2.np * p.k2.kp), p.k3.np * p.k3.kp) * 5 * 2,
+                       (head_scr_bytes() + 1023) & ~1023);
     const int kp_u2 = p.m2.phys() <= 32 ? 32 : (p.m2.phys() <= 64 ? 64 : 128);
     const int ja = img_bytes(in_rows(TR + 8), p.k1.kp);
     const int ua = img_bytes(in_rows(TR), kp_u2);
@@ -114,7 +124,8 @@ __device__ __forceinline__ void stage_window(const __bf16* src, int ld, int K, i
     dglds16(g, img + (j << 10));
   }
 }
-__device__ __forceinline__ void stage_weights(const DecImg& im, char* dst) {
+__device__ __forceinline__ void stage_weights(const DecImg& im, char* dst, int dbg) {
+  if (dbg & 1) return;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int npc = (5 * im.np * im.kp * 2) >> 10;
   const char* g = reinterpret_cast<const char*>(im.w) + lane * 16;
@@ -137,14 +148,14 @@ __device__ __forceinline__ __bf16* img_at(__bf16* img, int row, int kp, int n0) 
 // the MFMAs, EPI(orow, nb0, acc, yp) consumes a finished 16-row x NBH-block item.
 template <int NBH, class Pre, class Epi>
 __device__ __forceinline__ void conv_phase(const __bf16* xs, int kpx, const __bf16* ws, int kpw, int np,
-                                           int n_out, Pre&& pre, Epi&& epi) {
+                                           int n_out, Pre&& pre, Epi&& epi, int dbg = 0) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, li = lane & 15, lg = lane >> 4;
   const int nrb = (n_out + 15) >> 4, nbc = np >> 4;
   const int ncg = (nbc + NBH - 1) / NBH, wpc = NW / ncg;
   const int cg = w % ncg, k0 = w / ncg;
   if (k0 >= wpc) return;
   const int nb0 = cg * NBH;
-  const int kcs = kpw >> 5;
+  const int kcs = (dbg & 4) ? 0 : kpw >> 5;
   const int wsw = dswz(li, kpw);
   for (int rb = k0; rb < nrb; rb += wpc) {
     f32x4 yp[NBH];
@@ -187,25 +198,20 @@ __device__ __forceinline__ float colpar(const ColMap& m, int n, const float* A, 
 // {dW, db, sum dt*y, sum dt, sum dy} reduced over the tile in fixed order.
 template <int CIN, int COUT>
 __device__ __forceinline__ void head_tile(int hi, int orow, bool rv, long long gr, const float (&u)[CIN],
-                                          const float (&yv)[CIN], const float* w, const float* b,
-                                          const float* gamma, const float* beta, const float* target,
-                                          float count, float* yhat, __bf16* dyp, float* part,
-                                          double* sse_out, float* red, double* sred) {
-  constexpr int NQ = head_nq(CIN, COUT);
-  const int lane = threadIdx.x & 63, wl = (threadIdx.x >> 6) & 1;   // 2 waves per head
+                                          const float (&yv)[CIN], const float* hp, const float (&tg)[COUT],
+                                          float count, float* yhat, __bf16* dyp, float* scr,
+                                          double* sscr) {
+  // hp (LDS, loaded at kernel start): W [CIN][COUT] | b [COUT] at 20 | gamma at 24 | beta at 24 + CIN
   float wv[CIN][COUT], bv[COUT], gk[CIN], bk[CIN];
 #pragma unroll
   for (int k = 0; k < CIN; ++k) {
 #pragma unroll
-    for (int o = 0; o < COUT; ++o) wv[k][o] = w[k * COUT + o];
-    gk[k] = gamma[k] * kBnC;
-    bk[k] = beta[k];
+    for (int o = 0; o < COUT; ++o) wv[k][o] = hp[k * COUT + o];
+    gk[k] = hp[24 + k] * kBnC;
+    bk[k] = hp[24 + CIN + k];
   }
 #pragma unroll
-  for (int o = 0; o < COUT; ++o) bv[o] = b[o];
-  float tg[COUT];
-#pragma unroll
-  for (int o = 0; o < COUT; ++o) tg[o] = rv ? target[gr * COUT + o] : 0.f;
+  for (int o = 0; o < COUT; ++o) bv[o] = hp[20 + o];
   float dp[COUT];
   double sse = 0.0;
 #pragma unroll
@@ -241,40 +247,31 @@ __device__ __forceinline__ void head_tile(int hi, int orow, bool rv, long long g
 #pragma unroll
     for (int k = (CIN / 4) * 4; k < CIN; ++k) dyp[k] = (__bf16)dyv[k];
   }
-  // partials: wave sums, then the head's 2 waves in fixed order
-  float* rw = red + wl * NQ;
-  auto put = [&](int q, float v) {
-    v = wave_sum(v);
-    if (lane == 0) rw[q] = v;
-  };
+  // per-row quantities {dW, db, sum dt*y, sum dt, sum dy} and the squared error into
+  // q-major scratch (row stride kScr: conflict-free both ways); the caller sums rows
+  float* sc = scr + orow;
 #pragma unroll
   for (int k = 0; k < CIN; ++k)
 #pragma unroll
-    for (int o = 0; o < COUT; ++o) put(k * COUT + o, u[k] * dp[o]);
+    for (int o = 0; o < COUT; ++o) sc[(k * COUT + o) * kScr] = u[k] * dp[o];
 #pragma unroll
-  for (int o = 0; o < COUT; ++o) put(CIN * COUT + o, dp[o]);
+  for (int o = 0; o < COUT; ++o) sc[(CIN * COUT + o) * kScr] = dp[o];
   constexpr int QB = CIN * COUT + COUT;
 #pragma unroll
   for (int k = 0; k < CIN; ++k) {
-    put(QB + k, dt[k] * yv[k]);
-    put(QB + CIN + k, dt[k]);
-    put(QB + 2 * CIN + k, dyv[k]);
+    sc[(QB + k) * kScr] = dt[k] * yv[k];
+    sc[(QB + CIN + k) * kScr] = dt[k];
+    sc[(QB + 2 * CIN + k) * kScr] = dyv[k];
   }
-  const double ws_ = wave_sum_d(sse);
-  if (lane == 0) sred[wl] = ws_;
-  __syncthreads();   // all 1024 threads reach this (see the caller)
-  const int tl = threadIdx.x & 127;
-  for (int q = tl; q < NQ; q += 128) part[q] = red[q] + red[NQ + q];
-  if (tl == 0) *sse_out = sred[0] + sred[1];
-  (void)hi; (void)orow;
+  sscr[orow] = sse;
+  (void)hi; (void)gr;
 }
 
 // ------------------------------------------------------------------ forward
 __global__ void __launch_bounds__(DT) dec_fwd_kernel(DecChainFwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   __shared__ float cp1[3][128], cp2[3][128], cp3[3][16];
-  __shared__ float hred[2][2 * 96];
-  __shared__ double hsred[2][2];
+  __shared__ float hp[2][64];   // head parameters (head_tile layout)
   const FwdLay L(a);
   const Tile tl = tile_of(blockIdx.x, a.npg);
   const int tid = threadIdx.x, lane = tid & 63, lg = lane >> 4;
@@ -289,13 +286,38 @@ __global__ void __launch_bounds__(DT) dec_fwd_kernel(DecChainFwdArgs a) {
   const int own = tl.rend - tl.r0;
 
   // zero the activation images (pad columns and rows past a window are MFMA operands)
-  for (int i = tid * 16; i < L.total - L.a; i += DT * 16)
-    *reinterpret_cast<uint4*>(smem + L.a + i) = make_uint4(0u, 0u, 0u, 0u);
+  if (!(a.dbg & 32))
+    for (int i = tid * 16; i < L.total - L.a; i += DT * 16)
+      *reinterpret_cast<uint4*>(smem + L.a + i) = make_uint4(0u, 0u, 0u, 0u);
   __syncthreads();
   // J window [r0 - 6, r0 + own + 6) and the conv1 weights
-  stage_window(a.zb, a.ldz, a.dj, tl.r0 - 6, in_rows(TR + 8), own + 12, tl.glo, tl.ghi, a.k1.kp,
+  if (!(a.dbg & 16)) stage_window(a.zb, a.ldz, a.dj, tl.r0 - 6, in_rows(TR + 8), own + 12, tl.glo, tl.ghi, a.k1.kp,
                reinterpret_cast<char*>(jimg), a.zero);
-  stage_weights(a.k1, reinterpret_cast<char*>(wimg));
+  stage_weights(a.k1, reinterpret_cast<char*>(wimg), a.dbg);
+  // head parameters and the tile's targets, fetched now so their latency hides under the convs
+  if (tid >= 512 && tid < 512 + 128) {
+    const int i = tid - 512, hh = i >> 6, j = i & 63;
+    const int cin = hh ? 20 : 10, cout = hh ? 1 : 2;
+    const float* w = hh ? a.wn : a.ws;
+    const float* b = hh ? a.bn : a.bs;
+    const float* g = hh ? a.g2n : a.g3;
+    const float* be = hh ? a.be2n : a.be3;
+    float v = 0.f;
+    if (j < cin * cout) v = w[j];
+    else if (j >= 20 && j < 20 + cout) v = b[j - 20];
+    else if (j >= 24 && j < 24 + cin) v = g[j - 24];
+    else if (j >= 24 + cin && j < 24 + 2 * cin) v = be[j - 24 - cin];
+    hp[hh][j] = v;
+  }
+  float tg[2] = {0.f, 0.f};
+  if (tid < 256) {
+    const int orow = tid & 127;
+    const long long gr = tl.r0 + orow;
+    if (orow < own) {
+      if (tid < 128) { tg[0] = a.s_truth[gr * 2]; tg[1] = a.s_truth[gr * 2 + 1]; }
+      else tg[0] = a.x_truth[gr];
+    }
+  }
   if (tid < 128) {
     const int n = tid;
     cp1[0][n] = colpar(a.m1, n, a.b1, nullptr);
@@ -339,7 +361,7 @@ __global__ void __launch_bounds__(DT) dec_fwd_kernel(DecChainFwdArgs a) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) ub[e] = (__bf16)((ing && (cm >> e & 1u)) ? o[e] : 0.f);
         *reinterpret_cast<bf16x4*>(img_at(u1img, orow, kpo, n0)) = ub;
-        if (mine && cm) {
+        if (mine && cm && !(a.dbg & 8)) {
           float* yp = a.y1 + (long long)gr * a.ldy1 + n0;
           __bf16* up = a.u1 + (long long)gr * a.ldy1 + n0;
           if (cm == 15u) {
@@ -351,10 +373,10 @@ __global__ void __launch_bounds__(DT) dec_fwd_kernel(DecChainFwdArgs a) {
           }
         }
       }
-    });
+    }, a.dbg);
   }
   __syncthreads();
-  stage_weights(a.k2, reinterpret_cast<char*>(wimg));
+  stage_weights(a.k2, reinterpret_cast<char*>(wimg), a.dbg);
   wait_dma();
   // ---- conv2: window [r0 - 2, r0 + own + 2) -> U2 image; Y2 / U2 own rows; Y2n own rows in LDS
   {
@@ -381,7 +403,7 @@ __global__ void __launch_bounds__(DT) dec_fwd_kernel(DecChainFwdArgs a) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) ub[e] = (__bf16)((ing && (cm >> e & 1u)) ? o[e] : 0.f);
         *reinterpret_cast<bf16x4*>(img_at(u2img, orow, kpu2, n0)) = ub;
-        if (mine && cm) {
+        if (mine && cm && !(a.dbg & 8)) {
           float* yp = a.y2 + (long long)gr * a.ldy2 + n0;
           __bf16* up = a.u2 + (long long)gr * a.ldy2 + n0;
           if (cm == 15u) {
@@ -399,10 +421,10 @@ __global__ void __launch_bounds__(DT) dec_fwd_kernel(DecChainFwdArgs a) {
           }
         }
       }
-    });
+    }, a.dbg);
   }
   __syncthreads();
-  stage_weights(a.k3, reinterpret_cast<char*>(wimg));
+  stage_weights(a.k3, reinterpret_cast<char*>(wimg), a.dbg);
   wait_dma();
   // ---- conv3 (s branch): own rows -> U3, Y3 (fp32, LDS; the spatial head's input)
   {
@@ -421,36 +443,55 @@ __global__ void __launch_bounds__(DT) dec_fwd_kernel(DecChainFwdArgs a) {
       }
       *reinterpret_cast<float4*>(u3 + orow * 16 + n0) = make_float4(o[0], o[1], o[2], o[3]);
       *reinterpret_cast<float4*>(y3 + orow * 16 + n0) = make_float4(yv[0], yv[1], yv[2], yv[3]);
-    });
+    }, a.dbg);
   }
   __syncthreads();
-  // ---- heads: spatial (s3 -> sd) on threads 0..127, node (n2 -> nf) on 128..255
+  // ---- heads: spatial (s3 -> sd) on threads 0..127, node (n2 -> nf) on 128..255; the
+  // per-row partial quantities go to scratch over the (now idle) weight image
   const int t = blockIdx.x;
-  if (tid < 256) {
-    const int hi = tid >> 7, orow = tid & 127;
-    const bool rv = orow < own;
-    const long long gr = tl.r0 + orow;
-    if (hi == 0) {
-      float u[10], yv[10];
+  constexpr int NQS = head_nq(10, 2), NQN = head_nq(20, 1);
+  float* scr = reinterpret_cast<float*>(smem + L.w);
+  double* sscr = reinterpret_cast<double*>(smem + L.w + (NQS + NQN) * kScr * 4);
+  if (!(a.dbg & 2)) {
+    if (tid < 256) {
+      const int hi = tid >> 7, orow = tid & 127;
+      const bool rv = orow < own;
+      const long long gr = tl.r0 + orow;
+      if (hi == 0) {
+        float u[10], yv[10];
 #pragma unroll
-      for (int k = 0; k < 10; ++k) { u[k] = rv ? u3[orow * 16 + k] : 0.f; yv[k] = rv ? y3[orow * 16 + k] : 0.f; }
-      head_tile<10, 2>(0, orow, rv, gr, u, yv, a.ws, a.bs, a.g3, a.be3, a.s_truth, a.cnt_s, a.shat,
-                       a.dy3 + gr * a.lddy3, a.phs + (long long)t * head_nq(10, 2), a.sse_s + t,
-                       hred[0], hsred[0]);
-    } else {
-      float u[20], yv[20];
+        for (int k = 0; k < 10; ++k) { u[k] = rv ? u3[orow * 16 + k] : 0.f; yv[k] = rv ? y3[orow * 16 + k] : 0.f; }
+        const float t2[2] = {tg[0], tg[1]};
+        head_tile<10, 2>(0, orow, rv, gr, u, yv, hp[0], t2, a.cnt_s, a.shat, a.dy3 + gr * a.lddy3, scr, sscr);
+      } else {
+        float u[20], yv[20];
 #pragma unroll
-      for (int k = 0; k < 20; ++k) {   // U2n: window row orow + 2 of the U2 image (bf16)
-        const int n = a.m2.offb + k;
-        u[k] = rv ? (float)img_at(u2img, orow + 2, kpu2, n & ~3)[n & 3] : 0.f;
-        yv[k] = rv ? y2n[orow * L.ldY2n + k] : 0.f;
+        for (int k = 0; k < 20; ++k) {   // U2n: window row orow + 2 of the U2 image (bf16)
+          const int n = a.m2.offb + k;
+          u[k] = rv ? (float)img_at(u2img, orow + 2, kpu2, n & ~3)[n & 3] : 0.f;
+          yv[k] = rv ? y2n[orow * L.ldY2n + k] : 0.f;
+        }
+        const float t1[1] = {tg[0]};
+        head_tile<20, 1>(1, orow, rv, gr, u, yv, hp[1], t1, a.cnt_n, a.xhat, a.dy2 + gr * a.lddy2 + a.m2.offb,
+                         scr + NQS * kScr, sscr + 128);
       }
-      head_tile<20, 1>(1, orow, rv, gr, u, yv, a.wn, a.bn, a.g2n, a.be2n, a.x_truth, a.cnt_n, a.xhat,
-                       a.dy2 + gr * a.lddy2 + a.m2.offb, a.phn + (long long)t * head_nq(20, 1),
-                       a.sse_n + t, hred[1], hsred[1]);
     }
-  } else {
-    __syncthreads();   // matches the barrier inside head_tile
+    __syncthreads();
+    // tile partials: each quantity summed over the 128 rows in order
+    if (tid < NQS + NQN) {
+      const float* src = scr + tid * kScr;
+      float v = 0.f;
+#pragma unroll 32
+      for (int r = 0; r < 128; ++r) v += src[r];
+      if (tid < NQS) a.phs[(long long)t * NQS + tid] = v;
+      else a.phn[(long long)t * NQN + tid - NQS] = v;
+    } else if (tid >= 256 && tid < 258) {
+      const double* src = sscr + 128 * (tid - 256);
+      double v = 0.0;
+#pragma unroll 32
+      for (int r = 0; r < 128; ++r) v += src[r];
+      (tid == 256 ? a.sse_s : a.sse_n)[t] = v;
+    }
   }
 }
 
@@ -485,13 +526,14 @@ __global__ void __launch_bounds__(DT) dec_bwd_kernel(DecChainBwdArgs a) {
   const int own = tl.rend - tl.r0;
   const int t = blockIdx.x;
 
-  for (int i = tid * 16; i < L.cps - L.d3; i += DT * 16)
-    *reinterpret_cast<uint4*>(smem + L.d3 + i) = make_uint4(0u, 0u, 0u, 0u);
+  if (!(a.dbg & 32))
+    for (int i = tid * 16; i < L.cps - L.d3; i += DT * 16)
+      *reinterpret_cast<uint4*>(smem + L.d3 + i) = make_uint4(0u, 0u, 0u, 0u);
   __syncthreads();
   // dY3 window [r0 - 6, r0 + own + 6), conv3^T weights
-  stage_window(a.dy3, a.lddy3, a.s3, tl.r0 - 6, in_rows(TR + 8), own + 12, tl.glo, tl.ghi, a.k3t.kp,
+  if (!(a.dbg & 16)) stage_window(a.dy3, a.lddy3, a.s3, tl.r0 - 6, in_rows(TR + 8), own + 12, tl.glo, tl.ghi, a.k3t.kp,
                reinterpret_cast<char*>(d3), a.zero);
-  stage_weights(a.k3t, reinterpret_cast<char*>(wimg));
+  stage_weights(a.k3t, reinterpret_cast<char*>(wimg), a.dbg);
   if (tid < 128) {
     const int n = tid;
     const ColMap ms{a.m2.a, 0, a.m2.a};
@@ -504,7 +546,7 @@ __global__ void __launch_bounds__(DT) dec_bwd_kernel(DecChainBwdArgs a) {
   {
     const int wr0 = tl.r0 - 4, nv = own + 8, kp2 = a.k2t.kp;
     const int nq = (a.m2.b + 3) / 4;             // 4-column groups of the n part
-    for (int i = tid; i < nv * nq; i += DT) {
+    for (int i = tid; i < ((a.dbg & 16) ? 0 : nv * nq); i += DT) {
       const int row = i / nq, q = i - row * nq;
       const int gr = wr0 + row;
       if (gr < tl.glo || gr >= tl.ghi) continue;
@@ -551,14 +593,14 @@ __global__ void __launch_bounds__(DT) dec_bwd_kernel(DecChainBwdArgs a) {
       for (int e = 0; e < 4; ++e) ob[e] = (__bf16)o[e];
       if (n0 < a.m2.offb || !a.m2.b)    // s part only (the n part came from the heads)
         *reinterpret_cast<bf16x4*>(img_at(d2, orow, kpo, n0)) = ob;
-      if (mine) {
+      if (mine && !(a.dbg & 8)) {
         __bf16* dp = a.dy2 + (long long)gr * a.lddy2 + n0;
         if (n0 + 3 < N) *reinterpret_cast<bf16x4*>(dp) = ob;
         else
 #pragma unroll
           for (int e = 0; e < 4; ++e) if (n0 + e < N) dp[e] = ob[e];
       }
-    });
+    }, a.dbg);
     if (w / ncg < wpc) colpart_flush<1>(q, slots, a.k3t.np, nb0, nbc, w / ncg);
     __syncthreads();
     for (int i = tid; i < 3 * N; i += DT) {
@@ -569,7 +611,7 @@ __global__ void __launch_bounds__(DT) dec_bwd_kernel(DecChainBwdArgs a) {
     }
   }
   __syncthreads();
-  stage_weights(a.k2t, reinterpret_cast<char*>(wimg));
+  stage_weights(a.k2t, reinterpret_cast<char*>(wimg), a.dbg);
   wait_dma();
   // ---- conv2^T: window [r0 - 2, r0 + own + 2): dU1 -> BN/lrelu backward -> dY1
   {
@@ -618,7 +660,7 @@ __global__ void __launch_bounds__(DT) dec_bwd_kernel(DecChainBwdArgs a) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) ob[e] = (__bf16)o[e];
         *reinterpret_cast<bf16x4*>(img_at(d1, orow, kpo, n0)) = ob;
-        if (mine && cm) {
+        if (mine && cm && !(a.dbg & 8)) {
           __bf16* dp = a.dy1 + (long long)gr * a.lddy1 + n0;
           if (cm == 15u) *reinterpret_cast<bf16x4*>(dp) = ob;
           else
@@ -626,7 +668,7 @@ __global__ void __launch_bounds__(DT) dec_bwd_kernel(DecChainBwdArgs a) {
             for (int e = 0; e < 4; ++e) if (cm >> e & 1u) dp[e] = ob[e];
         }
       }
-    });
+    }, a.dbg);
     __syncthreads();   // slots: the conv3^T partials were consumed above
     if (w / ncg < wpc) colpart_flush<2>(q, slots, a.k2t.np, nb0, nbc, w / ncg);
     __syncthreads();
@@ -638,7 +680,7 @@ __global__ void __launch_bounds__(DT) dec_bwd_kernel(DecChainBwdArgs a) {
     }
   }
   __syncthreads();
-  stage_weights(a.k1t, reinterpret_cast<char*>(wimg));
+  stage_weights(a.k1t, reinterpret_cast<char*>(wimg), a.dbg);
   wait_dma();
   // ---- conv1^T: own rows -> dJ (fp32)
   {
@@ -650,11 +692,11 @@ __global__ void __launch_bounds__(DT) dec_bwd_kernel(DecChainBwdArgs a) {
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
         const int n0 = 16 * (nb + i) + 4 * lg;
-        if (n0 >= N) continue;
+        if (n0 >= N || (a.dbg & 8)) continue;
         *reinterpret_cast<float4*>(a.dz + gr * a.lddz + n0) =
             make_float4(acc[i][0], acc[i][1], acc[i][2], acc[i][3]);
       }
-    });
+    }, a.dbg);
   }
 }
 
@@ -672,7 +714,7 @@ bool dec_fused_supported(int dj, const ColMap& m1, const ColMap& m2, int s3, int
   f.k1 = k1; f.k2 = k2; f.k3 = k3; f.m1 = m1; f.m2 = m2; f.s3 = s3;
   DecChainBwdArgs b{};
   b.k3t = k3t; b.k2t = k2t; b.k1t = k1t; b.m1 = m1; b.m2 = m2; b.s3 = s3; b.dj = dj;
-  const int lim = 160 * 1024 - 8 * 1024;   // static LDS of the kernels
+  const int lim = kDynLds;
   if (FwdLay(f).total > lim || BwdLay(b).total > lim) return false;
   // image kp: conv inputs must match the packed images
   if (k3.kp > 64 || k3t.np != 32 || k2t.np > 128 || k1t.np != ((dj + 15) / 16) * 16) return false;
@@ -682,11 +724,10 @@ bool dec_fused_supported(int dj, const ColMap& m1, const ColMap& m2, int s3, int
 int dec_init_attributes() {
   static int done = 0;
   if (done) return 0;
-  const int lim = 160 * 1024 - 8 * 1024;
   if (hipFuncSetAttribute(reinterpret_cast<const void*>(dec_fwd_kernel),
-                          hipFuncAttributeMaxDynamicSharedMemorySize, lim) != hipSuccess ||
+                          hipFuncAttributeMaxDynamicSharedMemorySize, kDynLds) != hipSuccess ||
       hipFuncSetAttribute(reinterpret_cast<const void*>(dec_bwd_kernel),
-                          hipFuncAttributeMaxDynamicSharedMemorySize, lim) != hipSuccess) {
+                          hipFuncAttributeMaxDynamicSharedMemorySize, kDynLds) != hipSuccess) {
     set_error("dec: hipFuncSetAttribute failed");
     return SND_ERR_HIP;
   }

@@ -28,6 +28,7 @@ struct DecChainFwdArgs {
   float* phs; float* phn;                     // [tiles][dec_head_parts]
   double* sse_s; double* sse_n;               // [tiles]
   const void* zero;
+  int dbg;                                    // measurement only (snd_debug_set): phase-skip bits
 };
 
 struct DecChainBwdArgs {
@@ -45,6 +46,7 @@ struct DecChainBwdArgs {
   float* pc2s;                                // [tiles][3 s2]  {sum dt y, sum dt, sum dy}
   float* pc1;                                 // [tiles][3 w1]
   const void* zero;
+  int dbg;
 };
 
 int dec_tiles(int ngraphs, int npg);

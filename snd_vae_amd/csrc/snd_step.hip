@@ -260,9 +260,9 @@ extern "C" int snd_plan_create(const snd_config_t* cfg, int n_graphs, snd_plan_t
   p->add_buf("SK3S", (long long)p->sK3s.splits * 5 * c.s2 * c.s3);
 
   // row chunks per weight gradient: the step launches them all at once (debug bit
-  // 4096: one launch each, 8192: one launch each's ~256-workgroup geometry)
+  // 4096 or 8192: one launch each with the ~256-workgroup geometry; 16384: 32 chunks)
   const int dbg = debug_flags();
-  const int wgc = (dbg & (4096 | 8192)) ? 0 : ((dbg & 16384) ? 64 : 32);
+  const int wgc = (dbg & (4096 | 8192)) ? 0 : ((dbg & 16384) ? 32 : 64);
   // ---- bf16 fast decoder: split [s | n] column layouts, packed weight images
   if (c.dtype == SND_BF16 && !(debug_flags() & 256)) {
     const ColMap m1 = colmap_split(c.s1, c.n1), m2 = colmap_split(c.s2, c.n2);
@@ -833,7 +833,7 @@ int decoder_fast(const Ctx& x, const snd_batch_t* batch, int only = -1) {
   const int sd = c.spatial_dim, nf = c.num_feature;
   const int w1 = p.m1.phys(), w2 = p.m2.phys(), o1 = p.m1.offb, o2 = p.m2.offb;
   auto bf = [&](const char* n) { return reinterpret_cast<__bf16*>(x.f(n)); };
-  if (p.dec_fused && only < 0) {
+  if (p.dec_fused && (only < 0 || only >= 100)) {   // 100: forward kernel only, 101: backward only
     auto img = [&](const Img& im) {
       return DecImg{reinterpret_cast<const __bf16*>(x.ws + im.off), im.kp, im.np};
     };
@@ -855,7 +855,9 @@ int decoder_fast(const Ctx& x, const snd_batch_t* batch, int only = -1) {
     f.dy3 = bf("FDY3"); f.lddy3 = p.ld3; f.dy2 = bf("FDY2"); f.lddy2 = p.ld2;
     f.phs = x.f("PDHS"); f.phn = x.f("PDHN"); f.sse_s = x.d("PDSSES"); f.sse_n = x.d("PDSSEN");
     f.zero = x.ws + p.buf("ZERO");
-    SND_TRY(launch_dec_chain_fwd(f, x.s));
+    f.dbg = debug_flags();
+    if (only != 101) SND_TRY(launch_dec_chain_fwd(f, x.s));
+    if (only == 100) return 0;
     DecChainBwdArgs b{};
     b.R = R; b.npg = p.N; b.ngraphs = p.B; b.dj = L;
     b.k3t = img(p.pk3b); b.k2t = img(p.pk2b); b.k1t = img(p.pk1b);
@@ -867,7 +869,9 @@ int decoder_fast(const Ctx& x, const snd_batch_t* batch, int only = -1) {
     b.dy1 = bf("FDY1"); b.lddy1 = p.ld1; b.dz = x.f("DZDEC"); b.lddz = L;
     b.pc2s = x.f("PDC2S"); b.pc1 = x.f("PDC1");
     b.zero = x.ws + p.buf("ZERO");
+    b.dbg = debug_flags();
     SND_TRY(launch_dec_chain_bwd(b, x.s));
+    if (only == 101) return 0;
     SND_TRY(wgrad(x, wg_args(p, x.ws, p.gK3s, bf("FU2"), p.ld2, s2, bf("FDY3"), p.ld3, s3, x.f("FSK3S")), x.s));
     SND_TRY(wgrad(x, wg_args(p, x.ws, p.gK2s, bf("FU1"), p.ld1, c.s1, bf("FDY2"), p.ld2, s2, x.f("FSK2S")), x.s));
     SND_TRY(wgrad(x, wg_args(p, x.ws, p.gK2n, bf("FU1") + o1, p.ld1, c.n1, bf("FDY2") + o2, p.ld2, n2,
@@ -1146,6 +1150,10 @@ extern "C" int snd_plan_launch(const snd_plan_t* plan, const snd_batch_t* batch,
     SND_TRY(fast_init_attributes());
     Ctx x{&p, ws, p.last_params, p.last_grads, s};
     if (kernel[0] == 'p') return pack_decoder(x);
+    if (!strcmp(kernel, "dec:fwd") || !strcmp(kernel, "dec:bwd")) {
+      SND_CHECK_ARG(p.dec_fused, "snd_plan_launch: %s needs the fused decoder", kernel);
+      return decoder_fast(x, batch, kernel[4] == 'f' ? 100 : 101);
+    }
     return decoder_fast(x, batch, atoi(kernel + 4));
   }
   set_error("snd_plan_launch: unknown kernel '%s'", kernel);
