@@ -1,0 +1,83 @@
+// Row-gather engine shared by the bf16 gather kernels (snd_fast_enc.hip) and the
+// fused encoder heads (snd_head.hip): 8 lanes per CSR row, lane `sub` owns the
+// 16-byte chunks sub, sub + 8 of a neighbour row.
+#pragma once
+#include "snd_common.hpp"
+
+namespace snd {
+
+constexpr int kLpr = 8;   // lanes per row (aligned DPP half-rows)
+
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
+// Lane u of each aligned 8-lane group to all 8 lanes (ds_swizzle bit mode:
+// and-mask 0x18 keeps the group, or-mask u selects the lane; no LDS access).
+template <int U>
+__device__ __forceinline__ int bcast8(int v) {
+  return __builtin_amdgcn_ds_swizzle(v, 0x18 | (U << 5));
+}
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rows_rsrc(const void* base, long long bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, (int)bytes, 0x00020000);
+}
+
+// Per round the row's next 16 neighbour ids are loaded one or two per lane and
+// broadcast inside the 8-lane group, and all 16 neighbour chunks are requested
+// before any is consumed: a row of degree <= 16 costs one rowptr -> colidx ->
+// gather latency chain.  The gathers are buffer loads with a 32-bit offset (one
+// mad per neighbour, no 64-bit address arithmetic); a missing neighbour (past the
+// row end, id -1) wraps its offset past the descriptor's range, so the hardware
+// returns zeros with no select.  fn(u, v, valid) consumes neighbour u of the round
+// in order; cross-lane work inside fn stays uniform over the row's 8 lanes.
+template <int NQ, typename Fn>
+__device__ __forceinline__ void gather_rows16(const int* colidx, int s, int e, __amdgpu_buffer_rsrc_t rs,
+                                              unsigned row_bytes, int sub, Fn&& fn) {
+  for (int k0 = s; k0 < e; k0 += 16) {
+    const int id0 = k0 + sub < e ? colidx[k0 + sub] : -1;
+    const int id1 = k0 + 8 + sub < e ? colidx[k0 + 8 + sub] : -1;
+    int c[16];
+    c[0] = bcast8<0>(id0); c[1] = bcast8<1>(id0); c[2] = bcast8<2>(id0); c[3] = bcast8<3>(id0);
+    c[4] = bcast8<4>(id0); c[5] = bcast8<5>(id0); c[6] = bcast8<6>(id0); c[7] = bcast8<7>(id0);
+    c[8] = bcast8<0>(id1); c[9] = bcast8<1>(id1); c[10] = bcast8<2>(id1); c[11] = bcast8<3>(id1);
+    c[12] = bcast8<4>(id1); c[13] = bcast8<5>(id1); c[14] = bcast8<6>(id1); c[15] = bcast8<7>(id1);
+    u32x4 v[16][NQ];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const unsigned off = (unsigned)c[u] * row_bytes + 16u * sub;   // id -1: out of range -> 0
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) v[u][q] = __builtin_amdgcn_raw_buffer_load_b128(rs, off + 128u * q, 0, 0);
+    }
+    __builtin_amdgcn_sched_barrier(0);   // all 16 requests issue before the first is consumed
+#pragma unroll
+    for (int u = 0; u < 16; ++u) fn(u, v[u], c[u] >= 0);
+  }
+}
+
+// acc[0..7] += the 8 bf16 of a packed 16-byte chunk (exact widening + fp32 add)
+__device__ __forceinline__ void acc8v(float (&a)[8], const u32x4& v) {
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    const unsigned w = v[p];
+    a[2 * p] += __uint_as_float(w << 16);
+    a[2 * p + 1] += __uint_as_float(w & 0xFFFF0000u);
+  }
+}
+
+// the 8 bf16 of a packed chunk, widened
+__device__ __forceinline__ void widen8(float (&a)[8], const u32x4& v) {
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    const unsigned w = v[p];
+    a[2 * p] = __uint_as_float(w << 16);
+    a[2 * p + 1] = __uint_as_float(w & 0xFFFF0000u);
+  }
+}
+
+__device__ __forceinline__ uint4 to_bf16x8(const float (&v)[8]) {
+  bf16x8 o;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) o[j] = (__bf16)v[j];
+  return __builtin_bit_cast(uint4, o);
+}
+
+}  // namespace snd

@@ -1,0 +1,355 @@
+// Fused encoder heads of the node-latent bf16 fast path.
+//
+// head_fwd_kernel replaces four launches of the step's forward (the GraphConvolution 1
+// SpMM with its epilogue, the two head linears on the row engine, reparam_prep) with
+// one: a workgroup owns 128 rows of one graph and
+//   1. gathers A XW1 for its rows (the spmm_bf16_kernel engine: 8 lanes per row,
+//      16 neighbours in flight, fp32 sums in colidx order) and applies the
+//      GraphConvolution 1 epilogue (layers.py:122-123, model.py:107-112): P1 (fp32)
+//      and G = BNe([BN1(lrelu(P1)) | X]) leave for the backward pass, G also lands in
+//      LDS as the [row][k] image the row engine would have staged from HBM;
+//   2. h = G Wh + bh (model.py:113) on v_mfma_f32_16x16x32_bf16 from that image and
+//      the packed weight image (LDS-DMA'd during the gather), bf16 h to HBM (the Wms
+//      weight gradient reads it) and to LDS;
+//   3. [mu | s] = h Wms + bms (model.py:114-115), fp32 to HBM; the s half crosses to
+//      the mu waves through LDS;
+//   4. z = mu + eps e^s (model.py:159), the KL partials (optimizer.py:193), bf16 z and
+//      the zz^T staging images (z sqrt(log2 e), its transpose, per-64-row column sums).
+// Every product and epilogue is the unfused kernels' own arithmetic in the same order:
+// P1, G, h, [mu | s], z, eps, the staging images and the column sums equal theirs bit
+// for bit (tests/test_gpu_step.py); only the KL partials group their rows differently.
+#include "snd_head.hpp"
+#include "snd_gather.hpp"
+
+#include <algorithm>
+
+namespace snd {
+namespace {
+
+// HR rows of one graph per workgroup, 8 lanes per row in the gather: HR * 8 threads.
+// 64-row tiles (8 waves, ~73 KB LDS at C2) put two workgroups on a CU, so one's
+// gather latency overlaps the other's GEMMs and stores; 128 (debug bit 131072) is one.
+constexpr int kHeadRows = 64;
+constexpr int HWMAX = 16;
+constexpr float kSqrtLog2e = 1.2011224087864498f;
+
+typedef __attribute__((address_space(1))) const void* gptr_t;
+typedef __attribute__((address_space(3))) void* lptr_t;
+
+__device__ __forceinline__ void hglds16(const void* g, void* lds) {
+  __builtin_amdgcn_global_load_lds((gptr_t)g, (lptr_t)lds, 16, 0, 0);
+}
+// 16-byte chunk XOR of a [row][kp] bf16 image (snd_fast.hip swz: conflict-free b128 reads)
+__host__ __device__ __forceinline__ int hswz(int row, int kp) {
+  return kp == 128 ? (row & 15) : (kp == 64 ? ((row >> 1) & 7) : 0);
+}
+
+// LDS layout (bytes) of head_fwd_kernel, shared by host and device.  The s exchange
+// buffer (fp32 [128][L + 4]) reuses the Wh image and the G image, dead after step 2.
+struct FwdLay {
+  int w2, w1, g, h, zt, total, sx_end;
+  __host__ __device__ FwdLay(int HR, int kp1, int np1, int kp2, int np2, int L) {
+    w2 = 0;
+    w1 = np2 * kp2 * 2;
+    g = w1 + np1 * kp1 * 2;
+    h = g + HR * kp1 * 2;
+    zt = h + HR * kp2 * 2;
+    total = zt + HR * (L + 1) * 4;
+    sx_end = w1 + HR * (L + 4) * 4;
+  }
+};
+constexpr int kHeadStaticLds = 2 * 128 * 4 + HWMAX * 8;
+constexpr int kHeadDynLds = 160 * 1024 - kHeadStaticLds - 512;
+
+// LDS-DMA a packed [np][kp] bf16 weight image (whole 1 KB pieces)
+__device__ __forceinline__ void stage_img(const __bf16* src, int bytes, char* dst, int nw) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const char* g = reinterpret_cast<const char*>(src) + lane * 16;
+  for (int j = w; j < (bytes >> 10); j += nw) hglds16(g + (j << 10), dst + (j << 10));
+}
+
+// out^T = W^T x^T over one tap (the row engine's MFMA loop, snd_fast.hip rowconv_kernel):
+// lane (li, lg) of wave (rb, nb0) ends with row 16 rb + li, columns 16 (nb0 + i) + 4 lg ..+3
+template <int NBH>
+__device__ __forceinline__ void img_gemm(const __bf16* xs, const __bf16* ws, int kp, int np, int rb,
+                                         int nb0, int li, int lg, f32x4 (&acc)[NBH]) {
+  const int nbc = np >> 4;
+#pragma unroll
+  for (int i = 0; i < NBH; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int xrow = 16 * rb + li;
+  const __bf16* xrp = xs + xrow * kp;
+  const int xsw = hswz(xrow, kp), wsw = hswz(li, kp);
+  const __bf16* wrp = ws + li * kp;
+  const int kcs = kp >> 5;
+  for (int ks = 0; ks < kcs; ++ks) {
+    const int ch = 4 * ks + lg;
+    const bf16x8 bx = *reinterpret_cast<const bf16x8*>(xrp + ((ch ^ xsw) << 3));
+#pragma unroll
+    for (int i = 0; i < NBH; ++i) {
+      if (nb0 + i < nbc) {
+        const bf16x8 aw = *reinterpret_cast<const bf16x8*>(wrp + 16 * (nb0 + i) * kp + ((ch ^ wsw) << 3));
+        acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aw, bx, acc[i], 0, 0, 0);
+      }
+    }
+  }
+}
+
+// bf16x4 at (row, column n0) of a [row][kp] image (n0 % 4 == 0)
+__device__ __forceinline__ bf16x4* img_at4(__bf16* img, int row, int n0, int kp) {
+  return reinterpret_cast<bf16x4*>(img + row * kp + (((n0 >> 3) ^ hswz(row, kp)) << 3) + (n0 & 4));
+}
+
+template <int HR, int NB1, int NB2>
+__global__ void __launch_bounds__(HR * 8) head_fwd_kernel(HeadFwdArgs a) {
+  constexpr int HT = HR * 8, HW = HT / 64, NRB = HR / 16;   // threads, waves, 16-row blocks
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  __shared__ float cb1[128], cb2[128];   // bh, bms per physical column
+  __shared__ double klw[HWMAX];
+  const FwdLay lay(HR, a.kp1, a.np1, a.kp2, a.np2, a.L);
+  __bf16* w2s = reinterpret_cast<__bf16*>(smem + lay.w2);
+  __bf16* w1s = reinterpret_cast<__bf16*>(smem + lay.w1);
+  __bf16* gs = reinterpret_cast<__bf16*>(smem + lay.g);
+  __bf16* hs = reinterpret_cast<__bf16*>(smem + lay.h);
+  float* sx = reinterpret_cast<float*>(smem + lay.w1);
+  float* zt = reinterpret_cast<float*>(smem + lay.zt);
+  const int L = a.L, sxs = L + 4, zts = L + 1;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int tpg = a.npad / HR;
+  const int gi = blockIdx.x / tpg, lt = blockIdx.x - gi * tpg;
+  const int lr0 = lt * HR;                          // first row of the tile in its graph
+  const long long gr0 = (long long)gi * a.npg;      // the graph's first global row
+
+  // ---- weight images in flight during the gather; biases; zero h image (pad columns)
+  stage_img(a.wh_img, a.np1 * a.kp1 * 2, reinterpret_cast<char*>(w1s), HW);
+  stage_img(a.wms_img, a.np2 * a.kp2 * 2, reinterpret_cast<char*>(w2s), HW);
+  for (int i = tid; i < 128; i += HT) {
+    cb1[i] = i < a.gh ? a.bh[i] : 0.f;
+    cb2[i] = i < 2 * L ? a.bms[i] : 0.f;
+  }
+  for (int i = tid; i < HR * a.kp2 / 8; i += HT) reinterpret_cast<uint4*>(hs)[i] = make_uint4(0u, 0u, 0u, 0u);
+
+  // ---- 1. P1 = A XW1 for row rs (8 lanes), GraphConvolution 1 epilogue
+  const int rs = tid >> 3, sub = tid & 7;
+  const int lr = lr0 + rs;
+  const bool rv = lr < a.npg;
+  const long long r = gr0 + lr;
+  float acc[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) acc[j] = 0.f;
+  if (rv && !(a.dbg & 1)) {
+    const __amdgpu_buffer_rsrc_t rsd = rows_rsrc(a.xw1, (long long)a.R * a.h1 * 2);
+    gather_rows16<1>(a.colidx, a.rowptr[r], a.rowptr[r + 1], rsd, 2u * a.h1, sub,
+                     [&](int, const u32x4 (&v)[1], bool) { acc8v(acc, v[0]); });
+  }
+  const int nch = a.h1 >> 3, kc1 = a.kp1 >> 3;
+  uint4 gdat = make_uint4(0u, 0u, 0u, 0u), gxv = make_uint4(0u, 0u, 0u, 0u);
+  if (sub < nch) {
+    float gv[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int c = 8 * sub + j;
+      const float b1 = lrelu(acc[j]) * (a.g1[c] * kBnC) + a.b1[c];     // H2[:, :h1]
+      gv[j] = b1 * (a.ge[c] * kBnC) + a.be[c];                          // encoder_g BN
+    }
+    gdat = to_bf16x8(gv);
+  }
+  // the concat-X chunk (model.py:109) is chunk nch: lane nch's first or lane nch-8's second
+  const int xo = (sub == nch) ? 0 : (sub + 8 == nch ? 1 : -1);
+  if (xo >= 0 && rv) {
+    float gv[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int c = a.h1 + j;
+      gv[j] = j < a.f ? a.x[r * a.ldx + j] * (a.ge[c] * kBnC) + a.be[c] : 0.f;
+    }
+    gxv = to_bf16x8(gv);
+  }
+  {
+    // chunk sub: data, the X chunk or zeros; chunk sub + 8: the X chunk or zeros
+    // (component selects: a select of whole vectors goes through scratch)
+    const bool d0 = sub < nch, x0 = xo == 0, x1 = xo == 1;
+    const uint4 v0 = make_uint4(d0 ? gdat.x : (x0 ? gxv.x : 0u), d0 ? gdat.y : (x0 ? gxv.y : 0u),
+                                d0 ? gdat.z : (x0 ? gxv.z : 0u), d0 ? gdat.w : (x0 ? gxv.w : 0u));
+    const uint4 v1 = make_uint4(x1 ? gxv.x : 0u, x1 ? gxv.y : 0u, x1 ? gxv.z : 0u, x1 ? gxv.w : 0u);
+    if (sub < kc1) *reinterpret_cast<uint4*>(gs + rs * a.kp1 + ((sub ^ hswz(rs, a.kp1)) << 3)) = v0;
+    if (sub + 8 < kc1) *reinterpret_cast<uint4*>(gs + rs * a.kp1 + (((sub + 8) ^ hswz(rs, a.kp1)) << 3)) = v1;
+  }
+  __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): weight images landed (gathers consumed)
+  __syncthreads();
+  // P1 and G leave for the backward pass while the heads run
+  if (rv && !(a.dbg & 8)) {
+    if (sub < nch) {
+      float* pp = a.p1 + r * a.h1 + 8 * sub;
+      *reinterpret_cast<float4*>(pp) = make_float4(acc[0], acc[1], acc[2], acc[3]);
+      *reinterpret_cast<float4*>(pp + 4) = make_float4(acc[4], acc[5], acc[6], acc[7]);
+      *reinterpret_cast<uint4*>(a.g + r * a.ldg + 8 * sub) = gdat;
+    }
+    if (xo >= 0) *reinterpret_cast<uint4*>(a.g + r * a.ldg + a.h1) = gxv;
+  }
+
+  // ---- 2. h = G Wh + bh
+  const int li = lane & 15, lg = lane >> 4, rb = w % NRB, half = w / NRB;
+  const int row = 16 * rb + li, lrw = lr0 + row;
+  const bool vrow = lrw < a.npg;
+  const long long rr = gr0 + lrw;
+  {
+    f32x4 acc1[NB1];
+    img_gemm<NB1>(gs, w1s, a.kp1, a.np1, rb, NB1 * half, li, lg, acc1);
+#pragma unroll
+    for (int i = 0; i < NB1; ++i) {
+      const int n0 = 16 * (NB1 * half + i) + 4 * lg;
+      if (n0 >= a.gh) continue;
+      bf16x4 v4;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v4[e] = (__bf16)(acc1[i][e] + cb1[n0 + e]);
+      *img_at4(hs, row, n0, a.kp2) = v4;
+      if (vrow && !(a.dbg & 8)) *reinterpret_cast<bf16x4*>(a.hh + rr * a.gh + n0) = v4;
+    }
+  }
+  __syncthreads();
+
+  // ---- 3. [mu | s] = h Wms + bms: the s half (waves NRB..) crosses to the mu waves
+  float mu[NB2][4];
+  {
+    f32x4 acc2[NB2];
+    img_gemm<NB2>(hs, w2s, a.kp2, a.np2, rb, NB2 * half, li, lg, acc2);
+#pragma unroll
+    for (int i = 0; i < NB2; ++i) {
+      const int n0 = 16 * (NB2 * half + i) + 4 * lg;
+      float o[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) o[e] = acc2[i][e] + cb2[n0 + e];
+      if (vrow && !(a.dbg & 8))
+        *reinterpret_cast<float4*>(a.ms + rr * (2 * L) + n0) = make_float4(o[0], o[1], o[2], o[3]);
+      if (half == 1) *reinterpret_cast<float4*>(sx + row * sxs + (n0 - L)) = make_float4(o[0], o[1], o[2], o[3]);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) mu[i][e] = o[e];
+    }
+  }
+  __syncthreads();
+
+  // ---- 4. z = mu + eps e^s, KL, bf16 z, z sqrt(log2 e) rows, z into LDS for the transpose
+  if (half == 0) {
+    const unsigned off = a.step ? (unsigned)(*a.step) : 0u;
+    double kl = 0.0;
+#pragma unroll
+    for (int i = 0; i < NB2; ++i) {
+      const int c = 16 * i + 4 * lg;          // mu column (one Philox quad)
+      float z4[4] = {0.f, 0.f, 0.f, 0.f};
+      if (vrow) {
+        const long long ie = rr * L + c;
+        const float4 s4 = *reinterpret_cast<const float4*>(sx + row * sxs + c);
+        const float4 ep = a.eps_in ? *reinterpret_cast<const float4*>(a.eps_in + ie)
+                                   : philox_normal4(a.seed, off, (a.eps_base + (unsigned long long)ie) >> 2);
+        const float s[4] = {s4.x, s4.y, s4.z, s4.w}, e[4] = {ep.x, ep.y, ep.z, ep.w};
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const float es = __expf(s[t]);
+          z4[t] = mu[i][t] + e[t] * es;                                       // model.py:159
+          kl += (double)(1.f + 2.f * s[t] - mu[i][t] * mu[i][t] - es * es);    // optimizer.py:193
+        }
+        if (!(a.dbg & 8)) {
+          *reinterpret_cast<float4*>(a.z + ie) = make_float4(z4[0], z4[1], z4[2], z4[3]);
+          *reinterpret_cast<float4*>(a.eps_out + ie) = ep;
+          bf16x4 zb;
+#pragma unroll
+          for (int t = 0; t < 4; ++t) zb[t] = (__bf16)z4[t];
+          *reinterpret_cast<bf16x4*>(a.zb + ie) = zb;
+        }
+      }
+      bf16x4 jb;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        jb[t] = (__bf16)(z4[t] * kSqrtLog2e);
+        zt[row * zts + c + t] = z4[t];
+      }
+      *reinterpret_cast<bf16x4*>(a.jrow + ((long long)gi * a.npad + lrw) * L + c) = jb;
+    }
+    kl = wave_sum_d(kl);
+    if (lane == 0) klw[w] = kl;
+  }
+  __syncthreads();
+  // per-64-row column sums of the stored K-role values (reparam_prep order)
+  for (int i = tid; i < (HR / 64) * L; i += HT) {
+    const int h = i / L, c = i - h * L;
+    float cs = 0.f;
+    for (int q = 0; q < 64; ++q) cs += (float)(__bf16)(zt[(64 * h + q) * zts + c] * kSqrtLog2e);
+    a.colpart[((long long)gi * (a.npad / 64) + (HR / 64) * lt + h) * L + c] = cs;
+  }
+  // z^T image: 4 consecutive rows per lane
+  for (int idx = tid; idx < (HR / 4) * L; idx += HT) {
+    const int c = idx / (HR / 4), r4 = 4 * (idx % (HR / 4));
+    bf16x4 t;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) t[u] = (__bf16)zt[(r4 + u) * zts + c];
+    *reinterpret_cast<bf16x4*>(a.jt + ((long long)gi * L + c) * a.npad + lr0 + r4) = t;
+  }
+  if (tid < HR / 64)   // the 64-row block's four 16-row waves, in order
+    a.kl_part[(long long)gi * (a.npad / 64) + (HR / 64) * lt + tid] =
+        klw[4 * tid] + klw[4 * tid + 1] + klw[4 * tid + 2] + klw[4 * tid + 3];
+}
+
+template <int HR, int NB1, int NB2>
+int head_fwd_launch(const HeadFwdArgs& a, hipStream_t s) {
+  const size_t lds = (size_t)FwdLay(HR, a.kp1, a.np1, a.kp2, a.np2, a.L).total;
+  hipLaunchKernelGGL((head_fwd_kernel<HR, NB1, NB2>), dim3(a.ngraphs * (a.npad / HR)), dim3(HR * 8), lds, s, a);
+  SND_LAUNCH_CHECK("head_fwd_kernel");
+  return 0;
+}
+template <int HR>
+int head_fwd_dispatch(const HeadFwdArgs& a, hipStream_t s) {
+  const int nb1 = (a.np1 / 16 + 1) / 2, nb2 = a.np2 / 32;
+  if (nb1 == 1) return nb2 == 2 ? head_fwd_launch<HR, 1, 2>(a, s) : head_fwd_launch<HR, 1, 4>(a, s);
+  return nb2 == 2 ? head_fwd_launch<HR, 2, 2>(a, s) : head_fwd_launch<HR, 2, 4>(a, s);
+}
+
+}  // namespace
+
+
+bool head_fwd_supported(int h1, int f, int gh, int L, int kp1, int np1, int kp2, int np2) {
+  if (h1 % 8 || h1 < 8 || h1 > 64 || f < 1 || f > 8) return false;
+  if ((kp1 != 32 && kp1 != 64 && kp1 != 128) || (kp2 != 32 && kp2 != 64 && kp2 != 128)) return false;
+  if (h1 + 8 > kp1 || gh % 16 || gh < 16 || np1 != gh || np1 > 64 || gh > kp2) return false;
+  if ((L != 32 && L != 64) || np2 != 2 * L) return false;
+  const FwdLay l64(64, kp1, np1, kp2, np2, L), l128(128, kp1, np1, kp2, np2, L);
+  return l128.total <= kHeadDynLds && l64.sx_end <= l64.h && l128.sx_end <= l128.h;
+}
+
+int launch_head_fwd(const HeadFwdArgs& a, hipStream_t s) {
+  if (a.R <= 0) return 0;
+  SND_CHECK_ARG(head_fwd_supported(a.h1, a.f, a.gh, a.L, a.kp1, a.np1, a.kp2, a.np2),
+                "head_fwd: unsupported widths (h1 %d f %d gh %d L %d)", a.h1, a.f, a.gh, a.L);
+  SND_CHECK_ARG(a.npad % 128 == 0 && a.npad >= a.npg && (long long)a.npg * a.ngraphs == a.R,
+                "head_fwd: npad %% 128, R = ngraphs x npg");
+  SND_CHECK_ARG(a.ldg % 8 == 0 && a.ldg >= a.h1 + 8, "head_fwd: ldg");
+  SND_CHECK_ARG((long long)a.R * a.h1 * 2 < (1ll << 31), "head_fwd: rows x h1 beyond the 2 GB buffer range");
+  SND_CHECK_ARG(a.rowptr && (a.colidx || a.R == 0) && a.xw1 && a.g1 && a.b1 && a.x && a.ge && a.be && a.p1 &&
+                    a.g && a.wh_img && a.bh && a.hh && a.wms_img && a.bms && a.ms && a.z && a.eps_out &&
+                    a.zb && a.jrow && a.jt && a.colpart && a.kl_part,
+                "head_fwd: null operand");
+  SND_TRY(head_init_attributes());
+  return (a.dbg & 131072) ? head_fwd_dispatch<128>(a, s) : head_fwd_dispatch<kHeadRows>(a, s);
+}
+
+int head_init_attributes() {
+  static int done = 0;
+  if (done) return 0;
+  const void* ks[] = {reinterpret_cast<const void*>(head_fwd_kernel<64, 1, 2>),
+                      reinterpret_cast<const void*>(head_fwd_kernel<64, 1, 4>),
+                      reinterpret_cast<const void*>(head_fwd_kernel<64, 2, 2>),
+                      reinterpret_cast<const void*>(head_fwd_kernel<64, 2, 4>),
+                      reinterpret_cast<const void*>(head_fwd_kernel<128, 1, 2>),
+                      reinterpret_cast<const void*>(head_fwd_kernel<128, 1, 4>),
+                      reinterpret_cast<const void*>(head_fwd_kernel<128, 2, 2>),
+                      reinterpret_cast<const void*>(head_fwd_kernel<128, 2, 4>)};
+  for (const void* k : ks) {
+    if (hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, kHeadDynLds) != hipSuccess) {
+      set_error("head: hipFuncSetAttribute failed");
+      return SND_ERR_HIP;
+    }
+  }
+  done = 1;
+  return 0;
+}
+
+}  // namespace snd

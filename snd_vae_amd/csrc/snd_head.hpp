@@ -1,0 +1,39 @@
+// Fused encoder heads of the node-latent bf16 fast path (snd_head.hip): the row-local
+// chains on either side of zz^T collapsed into one launch each.
+#pragma once
+#include "snd_fast.hpp"
+
+namespace snd {
+
+// GraphConvolution 1 gather + its epilogue (layers.py:122-123, model.py:107-112),
+// h = G Wh + bh, [mu | s] = h Wms + bms (model.py:113-115), z = mu + eps e^s
+// (model.py:159) with the KL partials (optimizer.py:193) and the zz^T staging images
+// (reparam_prep semantics).  One workgroup = 128 rows of one graph.
+struct HeadFwdArgs {
+  const int* rowptr; const int* colidx;
+  int R, npg, ngraphs, npad;
+  const __bf16* xw1; int h1;                  // XW1 [R][h1] (bf16, the gathered operand)
+  const float* g1; const float* b1;           // BN1
+  const float* x; int ldx; int f;             // node features (concat X)
+  const float* ge; const float* be;           // encoder_g BN
+  float* p1;                                  // P1 [R][h1] fp32 (pre-activation)
+  __bf16* g; int ldg;                         // G [R][ldg] bf16
+  const __bf16* wh_img; int kp1, np1, gh;     // packed Wh image [np1][kp1]
+  const float* bh;
+  __bf16* hh;                                 // h [R][gh] bf16
+  const __bf16* wms_img; int kp2, np2;        // packed Wms image [np2][kp2], np2 = 2L
+  const float* bms;
+  float* ms;                                  // [mu | s] [R][2L] fp32
+  int L;
+  const float* eps_in; unsigned long long seed; const int* step; unsigned long long eps_base;
+  float* z; float* eps_out; __bf16* zb;       // z fp32 / bf16 [R][L], eps [R][L]
+  __bf16* jrow; __bf16* jt; float* colpart;   // zz^T staging (zzt_stage), DP == L
+  double* kl_part;                            // [ngraphs * npad / 64]
+  int dbg;
+};
+bool head_fwd_supported(int h1, int f, int gh, int L, int kp1, int np1, int kp2, int np2);
+int launch_head_fwd(const HeadFwdArgs& a, hipStream_t s);
+
+int head_init_attributes();
+
+}  // namespace snd

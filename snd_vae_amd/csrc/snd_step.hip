@@ -21,6 +21,7 @@
 #include "snd_elem.hpp"
 #include "snd_fast.hpp"
 #include "snd_gemm.hpp"
+#include "snd_head.hpp"
 #include "snd_spmm.hpp"
 #include "snd_tref.hpp"
 #include "snd_zzt.hpp"
@@ -86,6 +87,7 @@ struct snd_plan {
   WgGeom gK1{}, gK2s{}, gK2n{}, gK3s{};
   // ---- bf16 fast encoder (snd_fast_enc.hip + row engine)
   bool fast_enc = false;
+  bool head_fused = false;     // fused encoder forward tail (snd_head.hip): 1 launch instead of 4
   int ldh1 = 0, ldg = 0;
   Img pw1f{}, pwhf{}, pwmsf{}, pwmsb{}, pwhb{}, pw1b{};
   Img pidg{};                  // graph latent: identity [W -> W] (dG enters RC_ENC1 directly)
@@ -391,6 +393,10 @@ extern "C" int snd_plan_create(const snd_config_t* cfg, int n_graphs, snd_plan_t
       p->add_buf("FSWH", (long long)p->gWh.gx * W * wgrad_n4(gh));
       p->add_buf("FSW1", (long long)p->gW1.gx * (h0 + f) * wgrad_n4(h1));
       p->add_buf("FSW0", (long long)p->gW0.gx * f * wgrad_n4(h0));
+      // GraphConvolution 1 -> heads -> reparameterisation + zz^T staging in one launch
+      // (debug bit 65536: the four-launch chain)
+      p->head_fused = !(dbg & 65536) && zzt_dp(L) == L &&
+                      head_fwd_supported(h1, f, gh, L, p->pwhf.kp, p->pwhf.np, p->pwmsf.kp, p->pwmsf.np);
     }
   }
   *out = p;
@@ -715,6 +721,7 @@ int encoder_fast_fwd(const Ctx& x, const snd_batch_t* batch) {
     a.out = bf("FXW1"); a.ldo = h1; a.out_bf16 = 1;
     SND_TRY(launch_rowconv(a, RC_LIN, x.s));
   }
+  if (p.head_fused) return 0;   // the rest runs in head_fwd_fused (after the eps inputs are known)
   {
     SpmmBfArgs a{batch->rowptr, batch->colidx, R, bf("FXW1"), h1, h1, SND_SPMM_GCN, nullptr, 0,
                  x.f("FP1"), h1, x.w("enc.bn1.gamma"), x.w("enc.bn1.beta"), batch->features, f, f,
@@ -734,6 +741,31 @@ int encoder_fast_fwd(const Ctx& x, const snd_batch_t* batch) {
     SND_TRY(launch_rowconv(a, RC_LIN, x.s));
   }
   return 0;
+}
+
+// GraphConvolution 1 + heads + reparameterisation + zz^T staging (snd_head.hip)
+int head_fwd_fused(const Ctx& x, const snd_batch_t* batch, const float* eps, unsigned long long seed,
+                   const int* step_counter, const ZztStage& stg) {
+  const snd_plan& p = *x.p;
+  const snd_config_t& c = p.c;
+  HeadFwdArgs a{};
+  a.rowptr = batch->rowptr; a.colidx = batch->colidx;
+  a.R = p.R; a.npg = p.N; a.ngraphs = p.B; a.npad = zzt_npad(p.N);
+  a.xw1 = reinterpret_cast<const __bf16*>(x.f("FXW1")); a.h1 = c.h1;
+  a.g1 = x.w("enc.bn1.gamma"); a.b1 = x.w("enc.bn1.beta");
+  a.x = batch->features; a.ldx = c.f_in; a.f = c.f_in;
+  a.ge = x.w("enc.bne.gamma"); a.be = x.w("enc.bne.beta");
+  a.p1 = x.f("FP1"); a.g = reinterpret_cast<__bf16*>(x.f("FG")); a.ldg = p.ldg;
+  a.wh_img = reinterpret_cast<const __bf16*>(x.ws + p.pwhf.off); a.kp1 = p.pwhf.kp; a.np1 = p.pwhf.np;
+  a.gh = c.g_hidden; a.bh = x.w("enc.bh"); a.hh = reinterpret_cast<__bf16*>(x.f("FHH"));
+  a.wms_img = reinterpret_cast<const __bf16*>(x.ws + p.pwmsf.off); a.kp2 = p.pwmsf.kp; a.np2 = p.pwmsf.np;
+  a.bms = x.w("enc.bms"); a.ms = x.f("MS"); a.L = c.latent;
+  a.eps_in = eps; a.seed = seed; a.step = step_counter; a.eps_base = p.eps_base();
+  a.z = x.f("Z"); a.eps_out = x.f("EPS"); a.zb = reinterpret_cast<__bf16*>(x.f("ZB"));
+  a.jrow = reinterpret_cast<__bf16*>(stg.jrow); a.jt = reinterpret_cast<__bf16*>(stg.jt);
+  a.colpart = stg.colpart; a.kl_part = x.d("PKL");
+  a.dbg = debug_flags();
+  return launch_head_fwd(a, x.s);
 }
 
 int encoder_fast_bwd_tail(const Ctx& x, const snd_batch_t* batch);
@@ -1145,6 +1177,12 @@ extern "C" int snd_plan_launch(const snd_plan_t* plan, const snd_batch_t* batch,
       return launch_tref_proj_bwd(a, s);
     }
   }
+  if (!strcmp(kernel, "head_fwd")) {   // fused encoder forward tail (device eps, seed 0)
+    SND_CHECK_ARG(p.head_fused && p.last_params, "snd_plan_launch: head_fwd needs a fused-head step first");
+    Ctx x{&p, ws, p.last_params, p.last_grads, s};
+    const ZztStage stg = zzt_stage(ws + p.buf("ZSTAGE"), p.B, p.N, p.dj, p.c.dtype);
+    return head_fwd_fused(x, batch, nullptr, 0ull, nullptr, stg);
+  }
   if (!strncmp(kernel, "dec:", 4) || !strcmp(kernel, "pack")) {   // fast decoder kernel k
     SND_CHECK_ARG(p.fast && p.last_params, "snd_plan_launch: no fast-path step has run");
     SND_TRY(fast_init_attributes());
@@ -1237,6 +1275,8 @@ extern "C" int snd_train_step(const snd_plan_t* plan, const snd_batch_t* batch,
                         nullptr, 1};
       SND_TRY(launch_reparam_prep(a, zzt_dp(dj), x.s));
     }
+  } else if (p.head_fused) {
+    SND_TRY(head_fwd_fused(x, batch, eps, seed, step_counter, stg));
   } else if (p.fast) {   // fused with the zz^T staging images
     ReparamPrepArgs a{x.f("MS"), 2 * L, N, zzt_npad(N), p.B, L, eps, seed, step_counter, x.f("Z"),
                       x.f("EPS"), (__bf16*)x.f("ZB"), (__bf16*)stg.jrow, (__bf16*)stg.jt, stg.colpart,

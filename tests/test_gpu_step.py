@@ -340,3 +340,42 @@ def test_fused_decoder_matches_row_engine(topology, n, d, B):
     l0, l1 = o0.loss_dict(), o1.loss_dict()
     for k in ("spatial_cost", "node_cost", "cost"):
         assert l1[k] == pytest.approx(l0[k], rel=1e-6), k
+
+
+HEAD_BUFS = (("FP1", torch.float32), ("FG", torch.bfloat16), ("FHH", torch.bfloat16), ("MS", torch.float32),
+             ("Z", torch.float32), ("ZB", torch.bfloat16), ("EPS", torch.float32), ("ZSTAGE", torch.uint8),
+             ("DJD", torch.float32), ("FDP1", torch.bfloat16))
+
+
+@pytest.mark.parametrize("n,d,B", [(512, 64, 2), (300, 32, 3), (4096, 64, 2)])
+def test_fused_encoder_head_matches_chain(n, d, B):
+    """The fused encoder forward tail (snd_head.hip: GraphConvolution 1 gather + epilogue,
+    h = G Wh + bh, [mu | s] = h Wms + bms, reparameterisation and the zz^T staging images in
+    one launch) against the four-launch chain (debug bit 65536): P1, G, h, [mu | s], z,
+    eps and the staging images are bitwise equal, so is everything downstream (dJ, dP1);
+    the KL partials group rows differently (fp64 sums: the losses agree to 1e-12).
+    N = 300 covers partial 128-row tiles, d = 32 the narrower heads."""
+    from snd_vae_amd import _lib
+    from snd_vae_amd.params import init_blocks
+    cfg = tscale(n, d)
+    batch = synthetic_batch(cfg, B, seed=12)
+    p0 = init_blocks(cfg, 3)
+    runs = []
+    for flags in (65536, 0):
+        _lib.check(_lib.lib().snd_debug_set(flags))
+        try:
+            m, o, b = make(cfg, batch, p0, "bf16")
+        finally:
+            _lib.check(_lib.lib().snd_debug_set(0))
+        o.forward_backward(b)
+        torch.cuda.synchronize()
+        runs.append((m, o))
+    (m0, o0), (m1, o1) = runs
+    for name, dt in HEAD_BUFS:
+        assert torch.equal(m0.buffer(name, dt), m1.buffer(name, dt)), name
+    l0, l1 = o0.loss_dict(), o1.loss_dict()
+    for k in ("cost", "adj_cost", "kl", "acc"):
+        assert l1[k] == pytest.approx(l0[k], rel=1e-12, abs=1e-15), k
+    g0, g1 = o0.grad_blocks(), o1.grad_blocks()
+    for k in g0:
+        np.testing.assert_allclose(g1[k], g0[k], rtol=1e-5, atol=1e-6 * max(1.0, np.abs(g0[k]).max()), err_msg=k)
