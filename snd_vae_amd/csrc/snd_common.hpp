@@ -128,6 +128,18 @@ __device__ __forceinline__ float philox_normal(unsigned long long seed, unsigned
   }
 }
 
+// Reparameterisation + KL backward of one element (model.py:159, optimizer.py:193):
+// dz = adj (dJd + ej) + dz_dec; dmu = dz + kl mu; dlogstd = dz eps e^s + kl (e^2s - 1).
+// Rounding order spelled out (no contraction left to the compiler), so every kernel that
+// calls it produces the same bits.
+__device__ __forceinline__ void reparam_bwd_elem(float mu, float ls, float eps, float djd, float ej, float dzd,
+                                                 float adj, float kl, float& dm, float& dl) {
+  const float es = __expf(ls);
+  const float dz = __fmaf_rn(adj, __fadd_rn(djd, ej), dzd);
+  dm = __fmaf_rn(kl, mu, dz);
+  dl = __fmaf_rn(__fmul_rn(dz, eps), es, __fmul_rn(kl, __fmaf_rn(es, es, -1.f)));
+}
+
 inline int cdiv(long long a, long long b) { return (int)((a + b - 1) / b); }
 inline long long round_up(long long a, long long b) { return (a + b - 1) / b * b; }
 

@@ -554,10 +554,8 @@ __global__ void __launch_bounds__(NT) reparam_bwd_fast_kernel(ReparamBwdFastArgs
     bf16x4 om, os;
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
-      const float es = __expf(l[t]);
-      const float dz = a.adj_scale * (j4[t] + q4[t]) + d4[t];
-      const float dm = dz + a.kl_scale * m[t];
-      const float dl = dz * e4[t] * es + a.kl_scale * (es * es - 1.f);
+      float dm, dl;
+      reparam_bwd_elem(m[t], l[t], e4[t], j4[t], q4[t], d4[t], a.adj_scale, a.kl_scale, dm, dl);
       om[t] = (__bf16)dm;
       os[t] = (__bf16)dl;
       sm[t] += dm;

@@ -48,8 +48,9 @@ __device__ __forceinline__ void gather_rows16(const int* colidx, int s, int e, _
       for (int q = 0; q < NQ; ++q) v[u][q] = __builtin_amdgcn_raw_buffer_load_b128(rs, off + 128u * q, 0, 0);
     }
     __builtin_amdgcn_sched_barrier(0);   // all 16 requests issue before the first is consumed
+    const int nv = e - k0;               // neighbours of this round (the ids die with the loads)
 #pragma unroll
-    for (int u = 0; u < 16; ++u) fn(u, v[u], c[u] >= 0);
+    for (int u = 0; u < 16; ++u) fn(u, v[u], u < nv);
   }
 }
 

@@ -303,8 +303,351 @@ int head_fwd_dispatch(const HeadFwdArgs& a, hipStream_t s) {
   return nb2 == 2 ? head_fwd_launch<HR, 2, 2>(a, s) : head_fwd_launch<HR, 2, 4>(a, s);
 }
 
+// ---------------------------------------------------------------- backward head
+// LDS of head_bwd_kernel (bytes): Wms^T image | Wh^T image | d[mu | s] image | dh image |
+// per-wave bias sums of d[mu | s]
+struct BwdLay {
+  int w1, w2, m, h, red, total;
+  __host__ __device__ BwdLay(int kp1, int np1, int kp2, int np2, int L) {
+    w1 = 0;
+    w2 = np1 * kp1 * 2;
+    m = w2 + np2 * kp2 * 2;
+    h = m + 128 * kp1 * 2;
+    red = h + 128 * kp2 * 2;
+    total = red + 16 * 2 * L * 4;
+  }
+};
+constexpr int kBwdStaticLds = (8 * 4 * 128 + 8 * 128 + 5 * 128) * 4 + 16 * 12;
+
+__device__ __forceinline__ float shfl_rows8(float v) {   // sum over the 8 rows a wave holds per sub
+  v += __shfl_xor(v, 8, 64);
+  v += __shfl_xor(v, 16, 64);
+  v += __shfl_xor(v, 32, 64);
+  return v;
+}
+
+// NQ: 64-column chunks of z per lane (L <= 64: 1); NB1 / NB2: column blocks per wave half
+template <int NQ, int NB1, int NB2>
+__global__ void __launch_bounds__(1024) head_bwd_kernel(HeadBwdArgs a) {
+  constexpr int HT = 1024;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  __shared__ __attribute__((aligned(16))) float cps[8][4][128];   // ENC1 column partials per 16-row block
+  __shared__ __attribute__((aligned(16))) float cpb[8][128];      // dh column partials per 16-row block
+  __shared__ float colp[5][128];                                   // ENC1 per-column parameters
+  __shared__ double sl[16];
+  __shared__ unsigned stp[16];
+  const BwdLay lay(a.kp1, a.np1, a.kp2, a.np2, a.L);
+  __bf16* w1s = reinterpret_cast<__bf16*>(smem + lay.w1);
+  __bf16* w2s = reinterpret_cast<__bf16*>(smem + lay.w2);
+  __bf16* ms_img = reinterpret_cast<__bf16*>(smem + lay.m);
+  __bf16* dh_img = reinterpret_cast<__bf16*>(smem + lay.h);
+  float* bred = reinterpret_cast<float*>(smem + lay.red);
+  const int L = a.L, L2 = 2 * L;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  // tile: XCD-aware (a graph's tiles on one XCD, as the gather kernels' row blocks)
+  int t = blockIdx.x;
+  if (a.ngraphs % 8 == 0 && a.npg % 128 == 0 && a.ngraphs > 0) {
+    const int tpg = a.npg / 128, x = t & 7, sq = t >> 3;
+    const int gi = sq / tpg;
+    t = (x + 8 * gi) * tpg + (sq - gi * tpg);
+  }
+  const int r0 = t * 128;
+
+  stage_img(a.wmsb_img, a.np1 * a.kp1 * 2, reinterpret_cast<char*>(w1s), HT / 64);
+  stage_img(a.whb_img, a.np2 * a.kp2 * 2, reinterpret_cast<char*>(w2s), HT / 64);
+  // the dh image's columns [gh, kp2) are the zero k-padding the row engine stages
+  for (int i = tid; i < 128 * a.kp2 / 8; i += HT) reinterpret_cast<uint4*>(dh_img)[i] = make_uint4(0u, 0u, 0u, 0u);
+  for (int n = tid; n < 128; n += HT) {   // rowconv RC_ENC1 column parameters
+    const bool cv = n < a.W;
+    colp[1][n] = cv ? a.ge[n] * kBnC : 0.f;
+    colp[3][n] = (cv && n < a.h1) ? a.g1[n] * kBnC : 0.f;
+    colp[4][n] = (cv && n < a.h1) ? a.b1[n] : 0.f;
+  }
+
+  // ---- 1. per-edge terms of row rs (edge_bf16_kernel) + reparameterisation backward
+  {
+    const int rs = tid >> 3, sub = tid & 7;
+    const int r = r0 + rs;
+    const bool rv = r < a.R;
+    const int nch = L >> 3;
+    bool qv[NQ];
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) qv[q] = sub + 8 * q < nch;
+    float lossr = 0.f;
+    unsigned tp = 0;
+    // z_i stays packed (bf16 pairs, widened per use): the gather holds 64 VGPRs in flight
+    u32x4 zi[NQ];
+    float ej[NQ][8];
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      zi[q] = u32x4{0u, 0u, 0u, 0u};
+#pragma unroll
+      for (int j = 0; j < 8; ++j) ej[q][j] = 0.f;
+    }
+    if (rv)
+#pragma unroll
+      for (int q = 0; q < NQ; ++q)
+        if (qv[q]) zi[q] = *reinterpret_cast<const u32x4*>(a.zb + (long long)r * L + 64 * q + 8 * sub);
+    const float pw = a.pos_weight;
+    if (rv && !(a.dbg & 1)) {
+      const __amdgpu_buffer_rsrc_t rsd = rows_rsrc(a.zb, (long long)a.R * L * 2);
+      gather_rows16<NQ>(a.colidx, a.rowptr[r], a.rowptr[r + 1], rsd, 2u * L, sub,
+                        [&](int, const u32x4 (&v)[NQ], bool valid) {
+        float zj[NQ][8], dot = 0.f;
+#pragma unroll
+        for (int q = 0; q < NQ; ++q)
+#pragma unroll
+          for (int p = 0; p < 4; ++p) {
+            const unsigned wv = v[q][p];
+            zj[q][2 * p] = qv[q] ? __uint_as_float(wv << 16) : 0.f;
+            zj[q][2 * p + 1] = qv[q] ? __uint_as_float(wv & 0xFFFF0000u) : 0.f;
+          }
+#pragma unroll
+        for (int q = 0; q < NQ; ++q)
+#pragma unroll
+          for (int p = 0; p < 4; ++p) {
+            dot += __uint_as_float(zi[q][p] << 16) * zj[q][2 * p];
+            dot += __uint_as_float(zi[q][p] & 0xFFFF0000u) * zj[q][2 * p + 1];
+          }
+        const float Lij = row8_sum(dot);
+        if (!valid) return;
+        float coef = -pw;
+        if (pw != 1.f) {
+          const float sg = 1.f / (1.f + __expf(-Lij));
+          coef += (pw - 1.f) * sg;
+          lossr += (pw - 1.f) * (fmaxf(Lij, 0.f) + log1pf(__expf(-fabsf(Lij))));
+        }
+        lossr -= pw * Lij;
+        tp += Lij > 0.f ? 1u : 0u;
+#pragma unroll
+        for (int q = 0; q < NQ; ++q)
+#pragma unroll
+          for (int j = 0; j < 8; ++j) ej[q][j] += coef * zj[q][j];
+      });
+    }
+    if (sub != 0 || !rv) { lossr = 0.f; tp = 0; }   // the row's 8 lanes hold the same sums
+    // dz = adj_scale (dJd + ej) + dz_dec; dmu = dz + kl mu; dlogstd = dz eps e^s + kl (e^2s - 1)
+    float dm[NQ][8], dl[NQ][8];
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { dm[q][j] = 0.f; dl[q][j] = 0.f; }
+      const int c0 = 64 * q + 8 * sub;
+      if (rv && qv[q]) {
+        const float* msr = a.ms + (long long)r * L2;
+        const long long ie = (long long)r * L + c0;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const float4 mu = *reinterpret_cast<const float4*>(msr + c0 + 4 * h);
+          const float4 ls = *reinterpret_cast<const float4*>(msr + L + c0 + 4 * h);
+          const float4 ep = *reinterpret_cast<const float4*>(a.eps + ie + 4 * h);
+          const float4 dj = *reinterpret_cast<const float4*>(a.dJd + ie + 4 * h);
+          const float4 dd = *reinterpret_cast<const float4*>(a.dz_dec + ie + 4 * h);
+          const float m4[4] = {mu.x, mu.y, mu.z, mu.w}, l4[4] = {ls.x, ls.y, ls.z, ls.w};
+          const float e4[4] = {ep.x, ep.y, ep.z, ep.w}, j4[4] = {dj.x, dj.y, dj.z, dj.w};
+          const float d4[4] = {dd.x, dd.y, dd.z, dd.w};
+#pragma unroll
+          for (int u = 0; u < 4; ++u)
+            reparam_bwd_elem(m4[u], l4[u], e4[u], j4[u], ej[q][4 * h + u], d4[u], a.adj_scale, a.kl_scale,
+                             dm[q][4 * h + u], dl[q][4 * h + u]);
+        }
+      }
+      if (qv[q]) {
+        bf16x8 om, os;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) { om[j] = (__bf16)dm[q][j]; os[j] = (__bf16)dl[q][j]; }
+        const int cm = c0 >> 3, cs = (L + c0) >> 3;
+        *reinterpret_cast<bf16x8*>(ms_img + rs * a.kp1 + ((cm ^ hswz(rs, a.kp1)) << 3)) = om;
+        *reinterpret_cast<bf16x8*>(ms_img + rs * a.kp1 + ((cs ^ hswz(rs, a.kp1)) << 3)) = os;
+        if (rv && !(a.dbg & 8)) {
+          *reinterpret_cast<bf16x8*>(a.dms + (long long)r * L2 + c0) = om;
+          *reinterpret_cast<bf16x8*>(a.dms + (long long)r * L2 + L + c0) = os;
+        }
+        // bias gradient of the [mu | s] head: the wave's 8 rows of this lane's columns
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float sm = shfl_rows8(dm[q][j]), ss = shfl_rows8(dl[q][j]);
+          if (lane < 8) { bred[w * L2 + c0 + j] = sm; bred[w * L2 + L + c0 + j] = ss; }
+        }
+      }
+    }
+    const double lw = wave_sum_d((double)lossr);
+    const unsigned tw = wave_sum_u(tp);
+    if (lane == 0) { sl[w] = lw; stp[w] = tw; }
+  }
+  __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): weight images landed
+  __syncthreads();
+  if (tid < L2) {
+    float v = 0.f;
+    for (int k = 0; k < 16; ++k) v += bred[k * L2 + tid];
+    a.bms_part[(long long)t * L2 + tid] = v;
+  }
+  if (tid == 0) {
+    double tl = 0.0, tt = 0.0;
+    for (int k = 0; k < 16; ++k) { tl += sl[k]; tt += (double)stp[k]; }
+    a.edge_part[2 * t] = tl;
+    a.edge_part[2 * t + 1] = tt;
+  }
+
+  // ---- 2. dh = d[mu | s] Wms^T (row engine RC_LIN, no bias) + its column sums
+  const int li = lane & 15, lg = lane >> 4, rb = w & 7, half = w >> 3;
+  const int row = 16 * rb + li, r = r0 + row;
+  const bool vrow = r < a.R;
+  {
+    f32x4 acc1[NB1];
+    img_gemm<NB1>(ms_img, w1s, a.kp1, a.np1, rb, NB1 * half, li, lg, acc1);
+#pragma unroll
+    for (int i = 0; i < NB1; ++i) {
+      const int nb = NB1 * half + i;
+      if (nb >= (a.np1 >> 4)) continue;
+      const int n0 = 16 * nb + 4 * lg;
+      const bool cv = vrow && n0 < a.gh;
+      float qs[4];
+      bf16x4 v4;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float o = acc1[i][e] + 0.f;   // the row engine adds a zero bias (-0 becomes +0)
+        qs[e] = cv ? o : 0.f;
+        v4[e] = (__bf16)o;
+      }
+      if (n0 < a.gh) *img_at4(dh_img, row, n0, a.kp2) = v4;
+      if (cv && !(a.dbg & 8)) *reinterpret_cast<bf16x4*>(a.dh + (long long)r * a.gh + n0) = v4;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) qs[e] = row16_sum(qs[e]);
+      if (li == 0) *reinterpret_cast<float4*>(&cpb[rb][n0]) = make_float4(qs[0], qs[1], qs[2], qs[3]);
+    }
+  }
+  // ENC1 epilogue operands: P1 for the B1 part, X for the feature part
+  f32x4 ypf[NB2];
+  unsigned cvm[NB2];
+#pragma unroll
+  for (int i = 0; i < NB2; ++i) {
+    ypf[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    cvm[i] = 0u;
+    const int nb = NB2 * half + i;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int n = 16 * nb + 4 * lg + e;
+      if (nb < (a.np2 >> 4) && n < a.W) {
+        cvm[i] |= 1u << e;
+        if (vrow) ypf[i][e] = n < a.h1 ? a.p1[(long long)r * a.h1 + n] : a.x[(long long)r * a.ldx + (n - a.h1)];
+      }
+    }
+  }
+  __syncthreads();
+  if (tid < a.gh) {
+    float v = 0.f;
+#pragma unroll
+    for (int b = 0; b < 8; ++b) v += cpb[b][tid];
+    a.bh_part[(long long)t * a.gh + tid] = v;
+  }
+
+  // ---- 3. dG = dh Wh^T -> BNe / BN1 / lrelu backward (row engine RC_ENC1) -> dP1
+  {
+    f32x4 acc2[NB2];
+    img_gemm<NB2>(dh_img, w2s, a.kp2, a.np2, rb, NB2 * half, li, lg, acc2);
+#pragma unroll
+    for (int i = 0; i < NB2; ++i) {
+      const int nb = NB2 * half + i;
+      if (nb >= (a.np2 >> 4)) continue;
+      const int n0 = 16 * nb + 4 * lg;
+      const unsigned cm = vrow ? cvm[i] : 0u;
+      unsigned sm = cm;
+      float o[4], qs[4][4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int n = n0 + e;
+        const bool ok = cm >> e & 1u;
+        const float dg = ok ? acc2[i][e] : 0.f;
+        const bool bpart = n < a.h1;
+        const float pv = ypf[i][e];
+        const float a1 = lrelu(pv);
+        const float x2 = bpart ? a1 * colp[3][n] + colp[4][n] : pv;
+        qs[0][e] = dg * x2;
+        qs[1][e] = dg;
+        const float dh2 = dg * colp[1][n];
+        o[e] = 0.f;
+        qs[2][e] = 0.f;
+        qs[3][e] = 0.f;
+        if (bpart) {
+          qs[2][e] = dh2 * a1;
+          qs[3][e] = dh2;
+          o[e] = dh2 * colp[3][n] * lrelu_grad(pv);
+        } else {
+          sm &= ~(1u << e);
+        }
+      }
+      if (!(a.dbg & 8)) {
+        __bf16* op = a.dp1 + (long long)r * a.h1 + n0;
+        if (sm == 15u) {
+          bf16x4 v4;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v4[e] = (__bf16)o[e];
+          *reinterpret_cast<bf16x4*>(op) = v4;
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) if (sm >> e & 1u) op[e] = (__bf16)o[e];
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        float v[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = row16_sum(qs[q][e]);
+        if (li == 0) *reinterpret_cast<float4*>(&cps[rb][q][n0]) = make_float4(v[0], v[1], v[2], v[3]);
+      }
+    }
+  }
+  __syncthreads();
+  for (int i = tid; i < 4 * a.W; i += HT) {
+    const int q = i / a.W, n = i - q * a.W;
+    float v = 0.f;
+#pragma unroll
+    for (int b = 0; b < 8; ++b) v += cps[b][q][n];
+    a.enc1_part[(long long)t * 4 * a.W + i] = v;
+  }
+}
+
+template <int NQ, int NB1, int NB2>
+int head_bwd_launch(const HeadBwdArgs& a, hipStream_t s) {
+  const size_t lds = (size_t)BwdLay(a.kp1, a.np1, a.kp2, a.np2, a.L).total;
+  hipLaunchKernelGGL((head_bwd_kernel<NQ, NB1, NB2>), dim3(head_tiles(a.R)), dim3(1024), lds, s, a);
+  SND_LAUNCH_CHECK("head_bwd_kernel");
+  return 0;
+}
+
 }  // namespace
 
+int head_tiles(int R) { return cdiv(R, 128); }
+
+bool head_bwd_supported(int L, int gh, int W, int h1, int kp1, int np1, int kp2, int np2) {
+  if ((L != 16 && L != 32 && L != 64) || kp1 != 2 * L) return false;
+  if (gh % 16 || gh < 16 || np1 != gh || np1 > 64 || gh > kp2 || (kp2 != 32 && kp2 != 64 && kp2 != 128)) return false;
+  if (W > 128 || np2 != (int)round_up(W, 16) || h1 % 4 || h1 > W) return false;
+  return BwdLay(kp1, np1, kp2, np2, L).total + kBwdStaticLds <= 160 * 1024;
+}
+
+int launch_head_bwd(const HeadBwdArgs& a, hipStream_t s) {
+  if (a.R <= 0) return 0;
+  SND_CHECK_ARG(head_bwd_supported(a.L, a.gh, a.W, a.h1, a.kp1, a.np1, a.kp2, a.np2),
+                "head_bwd: unsupported widths (L %d gh %d W %d h1 %d)", a.L, a.gh, a.W, a.h1);
+  SND_CHECK_ARG((long long)a.R * a.L * 2 < (1ll << 31), "head_bwd: rows x L beyond the 2 GB buffer range");
+  SND_CHECK_ARG(a.rowptr && (a.colidx || a.R == 0) && a.zb && a.edge_part && a.ms && a.eps && a.dz_dec &&
+                    a.dJd && a.dms && a.bms_part && a.wmsb_img && a.dh && a.bh_part && a.whb_img && a.ge &&
+                    a.g1 && a.b1 && a.p1 && a.x && a.dp1 && a.enc1_part,
+                "head_bwd: null operand");
+  SND_TRY(head_init_attributes());
+  const int nb1 = (a.np1 / 16 + 1) / 2, nb2 = (a.np2 / 16 + 1) / 2;
+#define SND_HB(B1)                                   \
+  switch (nb2) {                                     \
+    case 1: return head_bwd_launch<1, B1, 1>(a, s);  \
+    case 2: return head_bwd_launch<1, B1, 2>(a, s);  \
+    case 3: return head_bwd_launch<1, B1, 3>(a, s);  \
+    default: return head_bwd_launch<1, B1, 4>(a, s); \
+  }
+  if (nb1 == 1) { SND_HB(1) } else { SND_HB(2) }
+#undef SND_HB
+}
 
 bool head_fwd_supported(int h1, int f, int gh, int L, int kp1, int np1, int kp2, int np2) {
   if (h1 % 8 || h1 < 8 || h1 > 64 || f < 1 || f > 8) return false;
@@ -342,6 +685,21 @@ int head_init_attributes() {
                       reinterpret_cast<const void*>(head_fwd_kernel<128, 1, 4>),
                       reinterpret_cast<const void*>(head_fwd_kernel<128, 2, 2>),
                       reinterpret_cast<const void*>(head_fwd_kernel<128, 2, 4>)};
+  const void* kb[] = {reinterpret_cast<const void*>(head_bwd_kernel<1, 1, 1>),
+                      reinterpret_cast<const void*>(head_bwd_kernel<1, 1, 2>),
+                      reinterpret_cast<const void*>(head_bwd_kernel<1, 1, 3>),
+                      reinterpret_cast<const void*>(head_bwd_kernel<1, 1, 4>),
+                      reinterpret_cast<const void*>(head_bwd_kernel<1, 2, 1>),
+                      reinterpret_cast<const void*>(head_bwd_kernel<1, 2, 2>),
+                      reinterpret_cast<const void*>(head_bwd_kernel<1, 2, 3>),
+                      reinterpret_cast<const void*>(head_bwd_kernel<1, 2, 4>)};
+  for (const void* k : kb) {
+    if (hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - kBwdStaticLds) !=
+        hipSuccess) {
+      set_error("head: hipFuncSetAttribute failed");
+      return SND_ERR_HIP;
+    }
+  }
   for (const void* k : ks) {
     if (hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, kHeadDynLds) != hipSuccess) {
       set_error("head: hipFuncSetAttribute failed");

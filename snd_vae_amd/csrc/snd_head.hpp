@@ -34,6 +34,32 @@ struct HeadFwdArgs {
 bool head_fwd_supported(int h1, int f, int gh, int L, int kp1, int np1, int kp2, int np2);
 int launch_head_fwd(const HeadFwdArgs& a, hipStream_t s);
 
+// Per-edge CE terms (the A = 1 pairs, optimizer.py:142-144) + the reparameterisation /
+// KL backward (model.py:159, optimizer.py:193) + dh = d[mu | s] Wms^T (model.py:114-115)
+// + dG = dh Wh^T with the encoder BN / lrelu backward down to dP1 (model.py:107-113):
+// edge_bf16 + reparam_bwd_fast + two row-engine launches in one.  One workgroup = 128
+// rows (the row engine's tiles: its column partials keep their layout and order).
+struct HeadBwdArgs {
+  const int* rowptr; const int* colidx; int R;
+  const __bf16* zb; int L; float pos_weight;   // z (bf16) [R][L]
+  double* edge_part;                           // [tiles][2] = {loss, tp}
+  const float* ms; const float* eps; const float* dz_dec; const float* dJd;
+  float adj_scale, kl_scale;
+  __bf16* dms; float* bms_part;                // d[mu | s] [R][2L] bf16; [tiles][2L]
+  const __bf16* wmsb_img; int kp1, np1, gh;    // Wms^T image [np1][kp1 = 2L]
+  __bf16* dh; float* bh_part;                  // dh [R][gh] bf16; [tiles][gh]
+  const __bf16* whb_img; int kp2, np2;         // Wh^T image [np2][kp2]
+  int W, h1;
+  const float* ge; const float* g1; const float* b1;   // BNe gamma; BN1 gamma, beta
+  const float* p1; const float* x; int ldx;            // P1 [R][h1] fp32, X [R][ldx]
+  __bf16* dp1; float* enc1_part;               // dP1 [R][h1] bf16; [tiles][4][W]
+  int npg, ngraphs;                            // XCD-aware tile order (npg % 128, ngraphs % 8)
+  int dbg;
+};
+bool head_bwd_supported(int L, int gh, int W, int h1, int kp1, int np1, int kp2, int np2);
+int head_tiles(int R);
+int launch_head_bwd(const HeadBwdArgs& a, hipStream_t s);
+
 int head_init_attributes();
 
 }  // namespace snd

@@ -88,6 +88,7 @@ struct snd_plan {
   // ---- bf16 fast encoder (snd_fast_enc.hip + row engine)
   bool fast_enc = false;
   bool head_fused = false;     // fused encoder forward tail (snd_head.hip): 1 launch instead of 4
+  bool head_bwd = false;       // fused edge terms + encoder backward head (snd_head.hip): 1 instead of 4
   int ldh1 = 0, ldg = 0;
   Img pw1f{}, pwhf{}, pwmsf{}, pwmsb{}, pwhb{}, pw1b{};
   Img pidg{};                  // graph latent: identity [W -> W] (dG enters RC_ENC1 directly)
@@ -397,6 +398,11 @@ extern "C" int snd_plan_create(const snd_config_t* cfg, int n_graphs, snd_plan_t
       // (debug bit 65536: the four-launch chain)
       p->head_fused = !(dbg & 65536) && zzt_dp(L) == L &&
                       head_fwd_supported(h1, f, gh, L, p->pwhf.kp, p->pwhf.np, p->pwmsf.kp, p->pwmsf.np);
+      // per-edge CE terms -> reparameterisation backward -> dh -> dG -> dP1 in one launch
+      // (debug bit 262144: edge_bf16 + reparam_bwd_fast + two row-engine launches)
+      p->head_bwd = !(dbg & 262144) &&
+                    head_bwd_supported(L, gh, W, h1, p->pwmsb.kp, p->pwmsb.np, p->pwhb.kp, p->pwhb.np);
+      if (p->head_bwd) p->add_buf("PHBMS", (long long)head_tiles(p->R) * 2 * L);
     }
   }
   *out = p;
@@ -768,7 +774,7 @@ int head_fwd_fused(const Ctx& x, const snd_batch_t* batch, const float* eps, uns
   return launch_head_fwd(a, x.s);
 }
 
-int encoder_fast_bwd_tail(const Ctx& x, const snd_batch_t* batch);
+int encoder_fast_bwd_tail(const Ctx& x, const snd_batch_t* batch, bool enc1_done = false);
 
 // encoder backward: reparam -> heads -> GCN1 -> GCN0 (all weight gradients as slabs)
 int encoder_fast_bwd(const Ctx& x, const snd_batch_t* batch, float adj_scale, float kl_scale) {
@@ -776,6 +782,26 @@ int encoder_fast_bwd(const Ctx& x, const snd_batch_t* batch, float adj_scale, fl
   const snd_config_t& c = p.c;
   const int R = p.R, L = c.latent, f = c.f_in, h0 = c.h0, h1 = c.h1, gh = c.g_hidden, W = p.W;
   auto bf = [&](const char* n) { return reinterpret_cast<__bf16*>(x.f(n)); };
+  if (p.head_bwd) {
+    HeadBwdArgs a{};
+    a.rowptr = batch->rowptr; a.colidx = batch->colidx; a.R = R;
+    a.zb = bf("ZB"); a.L = L; a.pos_weight = c.pos_weight; a.edge_part = x.d("PEDGE");
+    a.ms = x.f("MS"); a.eps = x.f("EPS"); a.dz_dec = x.f("DZDEC"); a.dJd = x.f("DJD");
+    a.adj_scale = adj_scale; a.kl_scale = kl_scale;
+    a.dms = bf("FDMS"); a.bms_part = x.f("PHBMS");
+    a.wmsb_img = reinterpret_cast<const __bf16*>(x.ws + p.pwmsb.off); a.kp1 = p.pwmsb.kp; a.np1 = p.pwmsb.np;
+    a.gh = gh; a.dh = bf("FDH"); a.bh_part = x.f("PFBH");
+    a.whb_img = reinterpret_cast<const __bf16*>(x.ws + p.pwhb.off); a.kp2 = p.pwhb.kp; a.np2 = p.pwhb.np;
+    a.W = W; a.h1 = h1;
+    a.ge = x.w("enc.bne.gamma"); a.g1 = x.w("enc.bn1.gamma"); a.b1 = x.w("enc.bn1.beta");
+    a.p1 = x.f("FP1"); a.x = batch->features; a.ldx = f;
+    a.dp1 = bf("FDP1"); a.enc1_part = x.f("PFENC1");
+    a.npg = p.N; a.ngraphs = p.B; a.dbg = debug_flags();
+    SND_TRY(launch_head_bwd(a, x.s));
+    SND_TRY(wgrad(x, wg_args(p, x.ws, p.gWms, bf("FHH"), gh, gh, bf("FDMS"), 2 * L, 2 * L, x.f("FSWMS"), 1), x.s));
+    SND_TRY(wgrad(x, wg_args(p, x.ws, p.gWh, bf("FG"), p.ldg, W, bf("FDH"), gh, gh, x.f("FSWH"), 1), x.s));
+    return encoder_fast_bwd_tail(x, batch, true);
+  }
   {
     ReparamBwdFastArgs a{x.f("MS"), 2 * L, R, L, x.f("EPS"), x.f("DZDEC"), x.f("DJD"), x.f("EJ"),
                          adj_scale, kl_scale, bf("FDMS"), 2 * L, x.f("PFBMS")};
@@ -796,12 +822,12 @@ int encoder_fast_bwd(const Ctx& x, const snd_batch_t* batch, float adj_scale, fl
 // encoder backward from dG: BN/lrelu backward (RC_ENC1 epilogue) -> GCN1 -> GCN0.
 // Node latent: dG = dH Wh^T is the RC_ENC1 GEMM itself; graph latent: dG (bf16,
 // from tref_head_bwd) passes through an identity image.
-int encoder_fast_bwd_tail(const Ctx& x, const snd_batch_t* batch) {
+int encoder_fast_bwd_tail(const Ctx& x, const snd_batch_t* batch, bool enc1_done) {
   const snd_plan& p = *x.p;
   const snd_config_t& c = p.c;
   const int R = p.R, f = c.f_in, h0 = c.h0, h1 = c.h1, gh = c.g_hidden, W = p.W;
   auto bf = [&](const char* n) { return reinterpret_cast<__bf16*>(x.f(n)); };
-  {
+  if (!enc1_done) {
     RcArgs a = p.tref ? rc_args(p, x.ws, p.pidg, bf("FDG"), p.ldg, W, W, colmap_plain(W))
                       : rc_args(p, x.ws, p.pwhb, bf("FDH"), gh, gh, W, colmap_plain(W));
     a.gamma = x.w("enc.bne.gamma"); a.g2 = x.w("enc.bn1.gamma"); a.b2 = x.w("enc.bn1.beta");
@@ -841,7 +867,8 @@ void encoder_fast_reduce(const Ctx& x, std::vector<ReduceDesc>& rd) {
   };
   if (!p.tref) {   // graph-latent heads are reduced by the generic path / written directly
     slab2d("FSWMS", p.gWms.gx, gh, 2 * L, "enc.Wms");
-    flat("PFBMS", reparam_bwd_fast_blocks(p.R, L), 2 * L, 2 * L, "enc.bms", 1.f);
+    if (p.head_bwd) flat("PHBMS", head_tiles(p.R), 2 * L, 2 * L, "enc.bms", 1.f);
+    else flat("PFBMS", reparam_bwd_fast_blocks(p.R, L), 2 * L, 2 * L, "enc.bms", 1.f);
     slab2d("FSWH", p.gWh.gx, W, gh, "enc.Wh");
     flat("PFBH", rcb, gh, gh, "enc.bh", 1.f);
   }
@@ -1294,7 +1321,9 @@ extern "C" int snd_train_step(const snd_plan_t* plan, const snd_batch_t* batch,
   {
     // per-edge terms on the side stream, overlapping the dense kernel / decoder
     SND_TRY(fork(x));
-    if (p.fast) {
+    if (p.head_bwd) {
+      // per-edge terms run inside head_bwd_kernel (the backward head)
+    } else if (p.fast) {
       EdgeBfArgs ea{rp, ci, R, (const __bf16*)x.f("ZB"), dj, c.pos_weight, x.f("EJ"), x.d("PEDGE"),
                     xcd_nbg(N, p.B)};
       ea.row_order = batch->row_order;
@@ -1495,7 +1524,7 @@ extern "C" int snd_train_step(const snd_plan_t* plan, const snd_batch_t* batch,
   }
   const int n_kl = (p.fast && !p.tref) ? reparam_prep_blocks(p.B, zzt_npad(N)) : reparam_blocks(RH, L);
   FinalizeArgs fa{x.d("PZZT"), zzt_dense_blocks(p.B, N, c.dtype), x.d("PEDGE"),
-                  p.fast ? edge_bf16_blocks(R) : edge_blocks(R, dj),
+                  p.head_bwd ? head_tiles(R) : (p.fast ? edge_bf16_blocks(R) : edge_blocks(R, dj)),
                   x.d("PKL"), n_kl, x.d(p.dec_fused ? "PDSSES" : "PSSES"),
                   x.d(p.dec_fused ? "PDSSEN" : "PSSEN"), p.dec_fused ? p.dtiles : nh,
                   rp, p.B, N, L, sd, nf, c.beta, c.norm, losses, grads + p.pcount, step_counter,

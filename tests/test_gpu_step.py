@@ -379,3 +379,40 @@ def test_fused_encoder_head_matches_chain(n, d, B):
     g0, g1 = o0.grad_blocks(), o1.grad_blocks()
     for k in g0:
         np.testing.assert_allclose(g1[k], g0[k], rtol=1e-5, atol=1e-6 * max(1.0, np.abs(g0[k]).max()), err_msg=k)
+
+
+@pytest.mark.parametrize("n,d,B", [(512, 64, 2), (300, 32, 3), (200, 16, 2), (4096, 64, 8)])
+def test_fused_backward_head_matches_chain(n, d, B):
+    """The fused backward head (snd_head.hip: per-edge CE terms, the reparameterisation /
+    KL backward, dh = d[mu | s] Wms^T and the encoder BN / lrelu backward to dP1 in one
+    launch) against edge_bf16 + reparam_bwd_fast + two row-engine launches (debug bit
+    262144): d[mu | s], dh and dP1 are bitwise equal and so is every weight gradient
+    computed from them; the bias gradient of the [mu | s] head and the edge loss partials
+    group rows differently (agree to fp32 / fp64 reassociation)."""
+    from snd_vae_amd import _lib
+    from snd_vae_amd.params import init_blocks
+    cfg = tscale(n, d)
+    batch = synthetic_batch(cfg, B, seed=13)
+    p0 = init_blocks(cfg, 4)
+    runs = []
+    for flags in (262144, 0):
+        _lib.check(_lib.lib().snd_debug_set(flags))
+        try:
+            m, o, b = make(cfg, batch, p0, "bf16")
+        finally:
+            _lib.check(_lib.lib().snd_debug_set(0))
+        o.forward_backward(b)
+        torch.cuda.synchronize()
+        runs.append((m, o))
+    (m0, o0), (m1, o1) = runs
+    for name, dt in (("FDMS", torch.bfloat16), ("FDH", torch.bfloat16), ("FDP1", torch.bfloat16)):
+        assert torch.equal(m0.buffer(name, dt), m1.buffer(name, dt)), name
+    l0, l1 = o0.loss_dict(), o1.loss_dict()
+    for k in ("cost", "adj_cost", "kl", "acc"):
+        assert l1[k] == pytest.approx(l0[k], rel=1e-12, abs=1e-15), k
+    g0, g1 = o0.grad_blocks(), o1.grad_blocks()
+    for k in g0:
+        if k == "enc.bms":
+            np.testing.assert_allclose(g1[k], g0[k], rtol=1e-4, atol=1e-6 * max(1.0, np.abs(g0[k]).max()), err_msg=k)
+        else:
+            assert np.array_equal(g0[k], g1[k]), k
