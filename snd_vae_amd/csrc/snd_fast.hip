@@ -419,6 +419,7 @@ __device__ __forceinline__ int tr_off(int row, int col, int kp) {
 }
 
 constexpr int WGT = 1024;   // 16 waves; wave w owns the (tap, 16-col k block) pair pg0 + w
+
 __device__ __forceinline__ int cdiv_d(int a, int b) { return (a + b - 1) / b; }
 
 struct WgUnit { int sub, s0, s1, glo, ghi; };
@@ -435,7 +436,9 @@ __device__ __forceinline__ WgUnit wg_unit(const WgArgs& a, int sub, int s0, int 
   return u;
 }
 
-template <int NBO>
+// NPW (tap, 16-column) pairs per wave: 1, or 2 (pairs w and w + 16 share every dy
+// operand read: one staging pass serves up to 32 pairs)
+template <int NBO, int NPW = 1>
 __device__ __forceinline__ void wgrad_body(const WgArgs& a, const int bx, const int by, __bf16* lds) {
   const int T = a.T, H = (T - 1) >> 1;
   const int XR = kRcRows + T - 1;
@@ -447,18 +450,27 @@ __device__ __forceinline__ void wgrad_body(const WgArgs& a, const int bx, const 
   const int li = lane & 15, lg = lane >> 4, tq = li >> 2, tp = li & 3;
   const int cbn = (a.K + 15) >> 4;
   const int P = T * cbn;
-  const int p = by * a.pairs_per_wg + w;
-  const bool pv = w < a.pairs_per_wg && p < P;
-  const int t = pv ? p / cbn : 0, cb = pv ? p - t * cbn : 0;
-
-  f32x4 acc[NBO];
+  bool pvs[NPW];
+  int ts[NPW], cbs[NPW];
 #pragma unroll
-  for (int j = 0; j < NBO; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int i = 0; i < NPW; ++i) {
+    const int wl = w + 16 * i, p = by * a.pairs_per_wg + wl;
+    pvs[i] = wl < a.pairs_per_wg && p < P;
+    ts[i] = pvs[i] ? p / cbn : 0;
+    cbs[i] = pvs[i] ? p - ts[i] * cbn : 0;
+  }
+  const bool pv = pvs[0];
+
+  f32x4 acc[NPW][NBO];
+#pragma unroll
+  for (int i = 0; i < NPW; ++i)
+#pragma unroll
+    for (int j = 0; j < NBO; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const __bf16* xg = reinterpret_cast<const __bf16*>(a.x);
   const __bf16* dg = reinterpret_cast<const __bf16*>(a.dy);
   const int c0 = bx * a.rows_per_wg, c1 = min(a.R, c0 + a.rows_per_wg);
-  auto stage = [&](const WgUnit& u, int b) {
+  auto stage = [&](const WgUnit& u, int b) __attribute__((always_inline)) {
     if (a.dbg & 2) return;
     __bf16* xs = lds + b * bufe;
     __bf16* ds = xs + (xch << 3);
@@ -486,8 +498,12 @@ __device__ __forceinline__ void wgrad_body(const WgArgs& a, const int bx, const 
 
   // per-lane tr-read offsets (elements) at k-step 0
   const int rk0 = 8 * lg + tq;
-  const int xoff = tr_off(rk0 + t, 16 * cb + 4 * tp, kpx);
-  const int xoff2 = tr_off(rk0 + t + 4, 16 * cb + 4 * tp, kpx);   // + t may carry into bit 3
+  int xoff[NPW], xoff2[NPW];
+#pragma unroll
+  for (int i = 0; i < NPW; ++i) {
+    xoff[i] = tr_off(rk0 + ts[i], 16 * cbs[i] + 4 * tp, kpx);
+    xoff2[i] = tr_off(rk0 + ts[i] + 4, 16 * cbs[i] + 4 * tp, kpx);   // + t may carry into bit 3
+  }
   const int doff = rk0 * kpy;
   int dobo[NBO];
 #pragma unroll
@@ -513,11 +529,15 @@ __device__ __forceinline__ void wgrad_body(const WgArgs& a, const int bx, const 
         for (int ks = 0; ks < kRcRows / 32; ++ks) {
           const __bf16* xb = xs + 32 * ks * kpx;
           const __bf16* db = ds + doff + 32 * ks * kpy;
-          const bf16x8 bx = tr_pair(xb + xoff, xb + xoff2);
+          bf16x8 bxv[NPW];
+#pragma unroll
+          for (int i = 0; i < NPW; ++i) bxv[i] = tr_pair(xb + xoff[i], xb + xoff2[i]);
 #pragma unroll
           for (int ob = 0; ob < NBO; ++ob) {
             const bf16x8 af = tr_pair(db + dobo[ob], db + dobo[ob] + 4 * kpy);
-            acc[ob] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bx, acc[ob], 0, 0, 0);
+#pragma unroll
+            for (int i = 0; i < NPW; ++i)
+              if (i == 0 || pvs[i]) acc[i][ob] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bxv[i], acc[i][ob], 0, 0, 0);
           }
         }
       }
@@ -526,17 +546,21 @@ __device__ __forceinline__ void wgrad_body(const WgArgs& a, const int bx, const 
     }
   }
   // D[m = n (dy col)][n = k (x col)]: lane holds k = 16cb + li, n = 16ob + 4lg + e
-  if ((a.dbg & 8) || !pv) return;
-  const int k = 16 * cb + li;
-  if (k >= a.K) return;
+  if (a.dbg & 8) return;
   // slab rows padded to a multiple of 4 floats: every store is a float4
   const int n4 = (a.N + 3) & ~3;
-  float* row = a.slab + (long long)bx * T * a.K * n4 + ((long long)t * a.K + k) * n4;
 #pragma unroll
-  for (int ob = 0; ob < NBO; ++ob) {
-    const int n0 = 16 * ob + 4 * lg;
-    if (n0 < a.N)
-      *reinterpret_cast<float4*>(row + n0) = make_float4(acc[ob][0], acc[ob][1], acc[ob][2], acc[ob][3]);
+  for (int i = 0; i < NPW; ++i) {
+    const int k = 16 * cbs[i] + li;
+    if (!pvs[i] || k >= a.K) continue;
+    float* row = a.slab + (long long)bx * T * a.K * n4 + ((long long)ts[i] * a.K + k) * n4;
+#pragma unroll
+    for (int ob = 0; ob < NBO; ++ob) {
+      const int n0 = 16 * ob + 4 * lg;
+      if (n0 < a.N)
+        *reinterpret_cast<float4*>(row + n0) =
+            make_float4(acc[i][ob][0], acc[i][ob][1], acc[i][ob][2], acc[i][ob][3]);
+    }
   }
 }
 
@@ -562,19 +586,20 @@ __global__ void __launch_bounds__(WGT) wgrad_multi_kernel(WgMultiPack m) {
   int s = 0;
   while (s + 1 < m.nseg && (int)blockIdx.x >= m.start[s + 1]) ++s;
   s = __builtin_amdgcn_readfirstlane(s);
-  const WgArgs& a = m.a[s];
+  const WgArgs a = m.a[s];   // by value: field reads stay scalar loads from the kernarg segment
   const int local = blockIdx.x - m.start[s];
   const int gx = cdiv_d(a.R, a.rows_per_wg);
   const int bx = local % gx, by = local / gx;
+  const bool two = a.pairs_per_wg > WGT / 64;
   switch ((a.N + 15) >> 4) {
-    case 1: wgrad_body<1>(a, bx, by, lds); break;
-    case 2: wgrad_body<2>(a, bx, by, lds); break;
-    case 3: wgrad_body<3>(a, bx, by, lds); break;
-    case 4: wgrad_body<4>(a, bx, by, lds); break;
-    case 5: wgrad_body<5>(a, bx, by, lds); break;
-    case 6: wgrad_body<6>(a, bx, by, lds); break;
-    case 7: wgrad_body<7>(a, bx, by, lds); break;
-    default: wgrad_body<8>(a, bx, by, lds); break;
+    case 1: if (two) wgrad_body<1, 2>(a, bx, by, lds); else wgrad_body<1>(a, bx, by, lds); break;
+    case 2: if (two) wgrad_body<2, 2>(a, bx, by, lds); else wgrad_body<2>(a, bx, by, lds); break;
+    case 3: if (two) wgrad_body<3, 2>(a, bx, by, lds); else wgrad_body<3>(a, bx, by, lds); break;
+    case 4: if (two) wgrad_body<4, 2>(a, bx, by, lds); else wgrad_body<4>(a, bx, by, lds); break;
+    case 5: if (two) wgrad_body<5, 2>(a, bx, by, lds); else wgrad_body<5>(a, bx, by, lds); break;
+    case 6: if (two) wgrad_body<6, 2>(a, bx, by, lds); else wgrad_body<6>(a, bx, by, lds); break;
+    case 7: if (two) wgrad_body<7, 2>(a, bx, by, lds); else wgrad_body<7>(a, bx, by, lds); break;
+    default: if (two) wgrad_body<8, 2>(a, bx, by, lds); else wgrad_body<8>(a, bx, by, lds); break;
   }
 }
 
@@ -737,6 +762,7 @@ int wg_launch(const WgArgs& a, dim3 grid, hipStream_t s) {
 }
 
 constexpr size_t kMaxDynLds = kRcLdsLimit;
+constexpr size_t kWgMultiLds = 160 * 1024;
 
 }  // namespace
 
@@ -836,7 +862,7 @@ int launch_wgrad_multi(const WgArgs* a, int n, hipStream_t s) {
     SND_CHECK_ARG(x.K > 0 && x.K <= 128 && x.N > 0 && x.N <= 128, "wgrad_multi: K %d N %d", x.K, x.N);
     SND_CHECK_ARG(x.ldx % 8 == 0 && x.lddy % 8 == 0 && x.x_bf16 && x.dy_bf16,
                   "wgrad_multi: bf16 operands with leading dims %% 8");
-    SND_CHECK_ARG(x.rows_per_wg % kRcRows == 0 && x.pairs_per_wg >= 1 && x.pairs_per_wg <= WGT / 64,
+    SND_CHECK_ARG(x.rows_per_wg % kRcRows == 0 && x.pairs_per_wg >= 1 && x.pairs_per_wg <= 2 * WGT / 64,
                   "wgrad_multi: geometry");
     SND_CHECK_ARG(x.x && x.dy && x.slab && x.zero && x.npg > 0, "wgrad_multi: null operand");
     const int P = x.T * cdiv(x.K, 16);
@@ -859,6 +885,8 @@ WgGeom wgrad_geom(int R, int T, int K, int N, int chunks) {
   g.pairs_per_wg = std::min(P, WGT / 64);
   g.gy = cdiv(P, g.pairs_per_wg);
   if (chunks > 0) {   // multi-segment launch: long row chunks pipeline their staging
+    g.pairs_per_wg = std::min(P, 2 * WGT / 64);   // one staging pass for up to 32 pairs
+    g.gy = cdiv(P, g.pairs_per_wg);
     g.rows_per_wg = (int)round_up(cdiv(R, chunks), kRcRows);
     g.gx = cdiv(R, g.rows_per_wg);
     return g;
@@ -913,8 +941,13 @@ int fast_init_attributes() {
 #undef SND_ATTR4
   SND_ATTR((wgrad_kernel<1>)) SND_ATTR((wgrad_kernel<2>)) SND_ATTR((wgrad_kernel<3>))
   SND_ATTR((wgrad_kernel<4>)) SND_ATTR((wgrad_kernel<5>)) SND_ATTR((wgrad_kernel<6>))
-  SND_ATTR((wgrad_kernel<7>)) SND_ATTR((wgrad_kernel<8>)) SND_ATTR(wgrad_multi_kernel)
+  SND_ATTR((wgrad_kernel<7>)) SND_ATTR((wgrad_kernel<8>))
 #undef SND_ATTR
+  if (hipFuncSetAttribute(reinterpret_cast<const void*>(wgrad_multi_kernel),
+                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)kWgMultiLds) != hipSuccess) {
+    set_error("hipFuncSetAttribute(wgrad_multi_kernel) failed");
+    return SND_ERR_HIP;
+  }
   done = 1;
   return 0;
 }

@@ -106,6 +106,7 @@ struct snd_plan {
   // parameters of the last snd_train_step (snd_plan_launch re-runs kernels on them)
   mutable const float* last_params = nullptr;
   mutable float* last_grads = nullptr;
+  mutable std::vector<WgArgs> last_wq;   // the last step's weight-gradient launch (snd_plan_launch)
   // side stream for the independent branches (edge terms, weight gradients); created
   // by the first non-capturing fast-path step, joined back before the reduction
   static constexpr int kEvents = 16;
@@ -265,7 +266,12 @@ extern "C" int snd_plan_create(const snd_config_t* cfg, int n_graphs, snd_plan_t
   // row chunks per weight gradient: the step launches them all at once (debug bit
   // 4096 or 8192: one launch each with the ~256-workgroup geometry; 16384: 32 chunks)
   const int dbg = debug_flags();
+  // row chunks per weight gradient: the step launches them all at once (debug bit
+  // 4096 or 8192: one launch each with the ~256-workgroup geometry; 16384: 32 chunks).
+  // A one-round geometry (~256 workgroups split over the segments by staged bytes) ran
+  // slower, 43 vs 29 us at C2: a workgroup's 128-row units are one DMA round trip each.
   const int wgc = (dbg & (4096 | 8192)) ? 0 : ((dbg & 16384) ? 32 : 64);
+  auto wgc_of = [&](int, int, int) { return wgc; };
   // ---- bf16 fast decoder: split [s | n] column layouts, packed weight images
   if (c.dtype == SND_BF16 && !(debug_flags() & 256)) {
     const ColMap m1 = colmap_split(c.s1, c.n1), m2 = colmap_split(c.s2, c.n2);
@@ -302,10 +308,10 @@ extern "C" int snd_plan_create(const snd_config_t* cfg, int n_graphs, snd_plan_t
       p->add_buf("PFDEC1", (long long)rcb * 3 * w1);
       p->add_buf("PFHS", (long long)hb * heads_fast_parts(c.s3, c.spatial_dim));
       p->add_buf("PFHN", (long long)hb * heads_fast_parts(c.n2, c.num_feature));
-      p->gK1 = wgrad_geom(p->R, 5, dj, w1, wgc);
-      p->gK2s = wgrad_geom(p->R, 5, c.s1, c.s2, wgc);
-      p->gK2n = wgrad_geom(p->R, 5, c.n1, c.n2, wgc);
-      p->gK3s = wgrad_geom(p->R, 5, c.s2, c.s3, wgc);
+      p->gK1 = wgrad_geom(p->R, 5, dj, w1, wgc_of(5, dj, w1));
+      p->gK2s = wgrad_geom(p->R, 5, c.s1, c.s2, wgc_of(5, c.s1, c.s2));
+      p->gK2n = wgrad_geom(p->R, 5, c.n1, c.n2, wgc_of(5, c.n1, c.n2));
+      p->gK3s = wgrad_geom(p->R, 5, c.s2, c.s3, wgc_of(5, c.s2, c.s3));
       p->add_buf("FSK1", (long long)p->gK1.gx * 5 * dj * wgrad_n4(w1));
       p->add_buf("FSK2S", (long long)p->gK2s.gx * 5 * c.s1 * wgrad_n4(c.s2));
       p->add_buf("FSK2N", (long long)p->gK2n.gx * 5 * c.n1 * wgrad_n4(c.n2));
@@ -350,8 +356,8 @@ extern "C" int snd_plan_create(const snd_config_t* cfg, int n_graphs, snd_plan_t
       const int rcb = rc_blocks(p->R);
       p->add_buf("PFENC1", (long long)rcb * 4 * W);
       p->add_buf("PFENC0", (long long)rcb * 2 * h0);
-      p->gW1 = wgrad_geom(p->R, 1, h0 + f, h1, wgc);
-      p->gW0 = wgrad_geom(p->R, 1, f, h0, wgc);
+      p->gW1 = wgrad_geom(p->R, 1, h0 + f, h1, wgc_of(1, h0 + f, h1));
+      p->gW0 = wgrad_geom(p->R, 1, f, h0, wgc_of(1, f, h0));
       p->add_buf("FSW1", (long long)p->gW1.gx * (h0 + f) * wgrad_n4(h1));
       p->add_buf("FSW0", (long long)p->gW0.gx * f * wgrad_n4(h0));
     }
@@ -386,10 +392,10 @@ extern "C" int snd_plan_create(const snd_config_t* cfg, int n_graphs, snd_plan_t
       p->add_buf("PFBH", (long long)rcb * gh);
       p->add_buf("PFENC1", (long long)rcb * 4 * W);
       p->add_buf("PFENC0", (long long)rcb * 2 * h0);
-      p->gWms = wgrad_geom(p->R, 1, gh, 2 * L, wgc);
-      p->gWh = wgrad_geom(p->R, 1, W, gh, wgc);
-      p->gW1 = wgrad_geom(p->R, 1, h0 + f, h1, wgc);
-      p->gW0 = wgrad_geom(p->R, 1, f, h0, wgc);
+      p->gWms = wgrad_geom(p->R, 1, gh, 2 * L, wgc_of(1, gh, 2 * L));
+      p->gWh = wgrad_geom(p->R, 1, W, gh, wgc_of(1, W, gh));
+      p->gW1 = wgrad_geom(p->R, 1, h0 + f, h1, wgc_of(1, h0 + f, h1));
+      p->gW0 = wgrad_geom(p->R, 1, f, h0, wgc_of(1, f, h0));
       p->add_buf("FSWMS", (long long)p->gWms.gx * gh * wgrad_n4(2 * L));
       p->add_buf("FSWH", (long long)p->gWh.gx * W * wgrad_n4(gh));
       p->add_buf("FSW1", (long long)p->gW1.gx * (h0 + f) * wgrad_n4(h1));
@@ -1204,6 +1210,12 @@ extern "C" int snd_plan_launch(const snd_plan_t* plan, const snd_batch_t* batch,
       return launch_tref_proj_bwd(a, s);
     }
   }
+  if (!strcmp(kernel, "wgrad_multi")) {   // the last step's weight gradients (current debug bits)
+    SND_CHECK_ARG(!p.last_wq.empty(), "snd_plan_launch: no multi-segment weight-gradient launch yet");
+    std::vector<WgArgs> q = p.last_wq;
+    for (auto& w : q) w.dbg = debug_flags();
+    return launch_wgrad_multi(q.data(), (int)q.size(), s);
+  }
   if (!strcmp(kernel, "head_fwd")) {   // fused encoder forward tail (device eps, seed 0)
     SND_CHECK_ARG(p.head_fused && p.last_params, "snd_plan_launch: head_fwd needs a fused-head step first");
     Ctx x{&p, ws, p.last_params, p.last_grads, s};
@@ -1466,6 +1478,7 @@ extern "C" int snd_train_step(const snd_plan_t* plan, const snd_batch_t* batch,
       return (long long)u.T * u.K * u.N > (long long)v.T * v.K * v.N;
     });
     SND_TRY(launch_wgrad_multi(x.wq->data(), (int)x.wq->size(), x.s));
+    p.last_wq = *x.wq;
   }
 
   // ======================= deterministic gradient reduction =================
