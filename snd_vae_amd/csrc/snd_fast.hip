@@ -18,6 +18,7 @@
 // 512-row chunk and a group of (tap, 16-column) pairs, and writes one
 // deterministic partial slab; snd_reduce sums the slabs in a fixed order.
 #include "snd_fast.hpp"
+#include "snd_pack.hpp"
 
 #include <algorithm>
 
@@ -49,33 +50,8 @@ struct PackPack { PackDesc d[kMaxPack]; };
 
 __global__ void __launch_bounds__(NT) pack_kernel(PackPack pk) {
   const PackDesc& d = pk.d[blockIdx.y];
-  const int kc = d.kp >> 3;
-  const int nch = d.T * d.np * kc;
-  for (int i = blockIdx.x * NT + threadIdx.x; i < nch; i += gridDim.x * NT) {
-    const int c = i % kc, tn = i / kc;
-    const int n = tn % d.np, t = tn / d.np;
-    const int lc = c ^ swz(n, d.kp);          // logical chunk stored at physical chunk c
-    bf16x8 v;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int k = 8 * lc + j;
-      float val = 0.f;
-      for (int si = 0; si < d.nsrc; ++si) {
-        const PackSrc& s = d.s[si];
-        if (s.mode == 2) {                  // identity over [a0, a1)
-          if (k == n && k >= s.a0 && k < s.a1) val = 1.f;
-          continue;
-        }
-        int aa, bb, tt;
-        if (s.mode == 0) { bb = n - s.n_off + s.b0; aa = k - s.k_off + s.a0; tt = t; }
-        else { aa = n - s.n_off + s.a0; bb = k - s.k_off + s.b0; tt = d.T - 1 - t; }
-        if (aa >= s.a0 && aa < s.a1 && bb >= s.b0 && bb < s.b1)
-          val = s.w[((long long)tt * s.A + aa) * s.B + bb];
-      }
-      v[j] = (__bf16)val;
-    }
-    *reinterpret_cast<bf16x8*>(d.dst + ((long long)(t * d.np + n) * d.kp + 8 * c)) = v;
-  }
+  const int nch = pack_chunks(d);
+  for (int i = blockIdx.x * NT + threadIdx.x; i < nch; i += gridDim.x * NT) pack_chunk(d, i);
 }
 
 // ---------------------------------------------------------------- row engine

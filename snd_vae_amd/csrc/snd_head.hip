@@ -20,6 +20,7 @@
 // for bit (tests/test_gpu_step.py); only the KL partials group their rows differently.
 #include "snd_head.hpp"
 #include "snd_gather.hpp"
+#include "snd_pack.hpp"
 
 #include <algorithm>
 
@@ -32,6 +33,7 @@ namespace {
 constexpr int kHeadRows = 64;
 constexpr int HWMAX = 16;
 constexpr float kSqrtLog2e = 1.2011224087864498f;
+__device__ __forceinline__ int cdiv_dev(int a, int b) { return (a + b - 1) / b; }
 
 typedef __attribute__((address_space(1))) const void* gptr_t;
 typedef __attribute__((address_space(3))) void* lptr_t;
@@ -616,7 +618,178 @@ int head_bwd_launch(const HeadBwdArgs& a, hipStream_t s) {
   return 0;
 }
 
+// ---------------------------------------------------------------- encoder front
+// One 128-row tile per workgroup: AX by the gcn0 gather (8 lanes per row, the fp32
+// features of the neighbours), H1 = [BN0(lrelu(AX W0)) | X] to HBM (the W1 weight
+// gradient and the backward read it) and into LDS, then XW1 = H1 W1 on MFMA with the
+// W1 image built in LDS from the fp32 weights (pack_kernel's image, bit for bit).
+// Workgroups past the tiles build the step's packed weight images (pack_chunk).
+template <int NB>
+__global__ void __launch_bounds__(1024) enc_front_kernel(FrontArgs a) {
+  const int tid = threadIdx.x;
+  const int ntiles = cdiv_dev(a.R, 128);
+  if ((int)blockIdx.x >= ntiles) {
+    const int pb = blockIdx.x - ntiles;
+    int s = 0;
+    while (s + 1 < a.npack && pb >= a.pack_wg[s + 1]) ++s;
+    s = __builtin_amdgcn_readfirstlane(s);
+    const PackDesc& d = a.pack[s];
+    const int i = (pb - a.pack_wg[s]) * 1024 + tid;
+    if (i < pack_chunks(d)) pack_chunk(d, i);
+    return;
+  }
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  __shared__ float sp[6][128];     // W0 rows (f <= 4), gamma0 * c, beta0
+  __bf16* wimg = reinterpret_cast<__bf16*>(smem);
+  __bf16* himg = reinterpret_cast<__bf16*>(smem + a.np1 * a.kp1 * 2);
+  const int r0 = blockIdx.x * 128;
+  const int K1 = a.h0 + a.f;
+  for (int i = tid; i < a.h0; i += 1024) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) sp[q][i] = q < a.f ? a.w0[q * a.h0 + i] : 0.f;
+    sp[4][i] = a.g0[i] * kBnC;
+    sp[5][i] = a.b0[i];
+  }
+  {   // W1 image [np1][kp1]: element (n, k) = W1[k][n] (pack mode 0)
+    const int kc = a.kp1 >> 3;
+    for (int i = tid; i < a.np1 * kc; i += 1024) {
+      const int c = i % kc, n = i / kc;
+      const int lc = c ^ img_swz(n, a.kp1);
+      bf16x8 v;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int k = 8 * lc + j;
+        v[j] = (__bf16)((k < K1 && n < a.n1) ? a.w1[k * a.n1 + n] : 0.f);
+      }
+      *reinterpret_cast<bf16x8*>(wimg + n * a.kp1 + 8 * c) = v;
+    }
+  }
+  __syncthreads();
+  // ---- AX for row rs (gcn0_kernel: two neighbours in flight per lane)
+  const int rs = tid >> 3, sub = tid & 7;
+  const int r = r0 + rs;
+  const bool rv = r < a.R;
+  float ax[4] = {0.f, 0.f, 0.f, 0.f};
+  if (rv) {
+    const int s = a.rowptr[r], e = a.rowptr[r + 1];
+    int k = s + sub;
+    for (; k + 8 < e; k += 16) {
+      const int c0 = a.colidx[k], c1 = a.colidx[k + 8];
+      float v0[4], v1[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        v0[j] = j < a.f ? a.x[(long long)c0 * a.ldx + j] : 0.f;
+        v1[j] = j < a.f ? a.x[(long long)c1 * a.ldx + j] : 0.f;
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) ax[j] += v0[j] + v1[j];
+    }
+    if (k < e) {
+      const int c0 = a.colidx[k];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) ax[j] += j < a.f ? a.x[(long long)c0 * a.ldx + j] : 0.f;
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) ax[j] = row8_sum(ax[j]);
+  // ---- H1 = [BN0(lrelu(AX W0)) | X]: lane sub owns chunk sub; the X chunk is chunk h0 / 8
+  const int nch = a.h0 >> 3, kc1 = a.kp1 >> 3;
+  uint4 hd = make_uint4(0u, 0u, 0u, 0u), hx = make_uint4(0u, 0u, 0u, 0u);
+  if (sub < nch) {
+    float o[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int col = 8 * sub + j;
+      float p = 0.f;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) p += ax[q] * sp[q][col];
+      o[j] = lrelu(p) * sp[4][col] + sp[5][col];
+    }
+    hd = to_bf16x8(o);
+  }
+  const int xo = (sub == nch) ? 0 : (sub + 8 == nch ? 1 : -1);
+  if (xo >= 0 && rv) {
+    float xv[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) xv[j] = j < a.f ? a.x[(long long)r * a.ldx + j] : 0.f;
+    hx = to_bf16x8(xv);
+  }
+  {
+    const bool d0 = sub < nch, x0 = xo == 0, x1 = xo == 1;
+    const uint4 v0 = make_uint4(d0 ? hd.x : (x0 ? hx.x : 0u), d0 ? hd.y : (x0 ? hx.y : 0u),
+                                d0 ? hd.z : (x0 ? hx.z : 0u), d0 ? hd.w : (x0 ? hx.w : 0u));
+    const uint4 v1 = make_uint4(x1 ? hx.x : 0u, x1 ? hx.y : 0u, x1 ? hx.z : 0u, x1 ? hx.w : 0u);
+    if (sub < kc1) *reinterpret_cast<uint4*>(himg + rs * a.kp1 + ((sub ^ hswz(rs, a.kp1)) << 3)) = v0;
+    if (sub + 8 < kc1) *reinterpret_cast<uint4*>(himg + rs * a.kp1 + (((sub + 8) ^ hswz(rs, a.kp1)) << 3)) = v1;
+  }
+  if (rv && !(a.dbg & 8)) {
+    if (sub < nch) *reinterpret_cast<uint4*>(a.h1 + (long long)r * a.ldh1 + 8 * sub) = hd;
+    if (xo >= 0) *reinterpret_cast<uint4*>(a.h1 + (long long)r * a.ldh1 + a.h0) = hx;
+    if (sub == 0) {
+      *reinterpret_cast<float4*>(a.ax + (long long)r * 4) = make_float4(ax[0], ax[1], ax[2], ax[3]);
+      const float axp[8] = {ax[0], ax[1], ax[2], ax[3], 0.f, 0.f, 0.f, 0.f};
+      *reinterpret_cast<uint4*>(a.axb + (long long)r * 8) = to_bf16x8(axp);
+    }
+  }
+  __syncthreads();
+  // ---- XW1 = H1 W1 (row engine RC_LIN, no bias)
+  const int lane = tid & 63, w = tid >> 6;
+  const int li = lane & 15, lg = lane >> 4, rb = w & 7, half = w >> 3;
+  const int row = 16 * rb + li, rr = r0 + row;
+  f32x4 acc[NB];
+  img_gemm<NB>(himg, wimg, a.kp1, a.np1, rb, NB * half, li, lg, acc);
+  if (rr >= a.R || (a.dbg & 8)) return;
+#pragma unroll
+  for (int i = 0; i < NB; ++i) {
+    const int n0 = 16 * (NB * half + i) + 4 * lg;
+    if (n0 >= a.n1) continue;
+    bf16x4 v4;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v4[e] = (__bf16)(acc[i][e] + 0.f);   // the row engine's zero bias
+    *reinterpret_cast<bf16x4*>(a.xw1 + (long long)rr * a.n1 + n0) = v4;
+  }
+}
+
 }  // namespace
+
+bool front_supported(int f, int h0, int n1, int kp1, int np1) {
+  return f >= 1 && f <= 4 && h0 % 8 == 0 && h0 >= 8 && h0 <= 64 && h0 + 8 <= kp1 && n1 % 16 == 0 &&
+         np1 == n1 && np1 <= 128 && (kp1 == 32 || kp1 == 64 || kp1 == 128) &&
+         (np1 + 128) * kp1 * 2 + 6 * 128 * 4 <= 160 * 1024;
+}
+
+int launch_front(FrontArgs& a, const PackDesc* pack, int npack, hipStream_t s) {
+  if (a.R <= 0) return 0;
+  SND_CHECK_ARG(front_supported(a.f, a.h0, a.n1, a.kp1, a.np1), "front: unsupported widths (f %d h0 %d n1 %d)",
+                a.f, a.h0, a.n1);
+  SND_CHECK_ARG(npack >= 0 && npack <= kMaxPack, "front: at most %d packed images", kMaxPack);
+  SND_CHECK_ARG(a.rowptr && (a.colidx || a.R == 0) && a.x && a.w0 && a.g0 && a.b0 && a.h1 && a.ax && a.axb &&
+                    a.w1 && a.xw1 && a.ldh1 % 8 == 0 && a.ldh1 >= a.h0 + 8,
+                "front: operands");
+  a.npack = npack;
+  int wg = 0;
+  for (int i = 0; i < npack; ++i) {
+    const PackDesc& x = pack[i];
+    SND_CHECK_ARG((x.kp == 32 || x.kp == 64 || x.kp == 128) && x.np % 16 == 0 && x.np > 0 && x.T >= 1 &&
+                      x.nsrc >= 1 && x.nsrc <= 2,
+                  "front: bad pack descriptor %d", i);
+    a.pack[i] = x;
+    a.pack_wg[i] = wg;
+    wg += cdiv(pack_chunks(x), 1024);
+  }
+  a.pack_wg[npack] = wg;
+  SND_TRY(head_init_attributes());
+  const size_t lds = (size_t)(a.np1 + 128) * a.kp1 * 2;
+  const dim3 grid(cdiv(a.R, 128) + wg);
+  switch ((a.np1 / 16 + 1) / 2) {
+    case 1: hipLaunchKernelGGL((enc_front_kernel<1>), grid, dim3(1024), lds, s, a); break;
+    case 2: hipLaunchKernelGGL((enc_front_kernel<2>), grid, dim3(1024), lds, s, a); break;
+    case 3: hipLaunchKernelGGL((enc_front_kernel<3>), grid, dim3(1024), lds, s, a); break;
+    default: hipLaunchKernelGGL((enc_front_kernel<4>), grid, dim3(1024), lds, s, a); break;
+  }
+  SND_LAUNCH_CHECK("enc_front_kernel");
+  return 0;
+}
 
 int head_tiles(int R) { return cdiv(R, 128); }
 
@@ -693,6 +866,17 @@ int head_init_attributes() {
                       reinterpret_cast<const void*>(head_bwd_kernel<1, 2, 2>),
                       reinterpret_cast<const void*>(head_bwd_kernel<1, 2, 3>),
                       reinterpret_cast<const void*>(head_bwd_kernel<1, 2, 4>)};
+  const void* kf[] = {reinterpret_cast<const void*>(enc_front_kernel<1>),
+                      reinterpret_cast<const void*>(enc_front_kernel<2>),
+                      reinterpret_cast<const void*>(enc_front_kernel<3>),
+                      reinterpret_cast<const void*>(enc_front_kernel<4>)};
+  for (const void* k : kf) {
+    if (hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 6 * 128 * 4) !=
+        hipSuccess) {
+      set_error("head: hipFuncSetAttribute failed");
+      return SND_ERR_HIP;
+    }
+  }
   for (const void* k : kb) {
     if (hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - kBwdStaticLds) !=
         hipSuccess) {

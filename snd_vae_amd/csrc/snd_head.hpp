@@ -60,6 +60,23 @@ bool head_bwd_supported(int L, int gh, int W, int h1, int kp1, int np1, int kp2,
 int head_tiles(int R);
 int launch_head_bwd(const HeadBwdArgs& a, hipStream_t s);
 
+// GraphConvolution 0 as (A X) W0 (gcn0 semantics: AX, H1 = [BN0(lrelu(AX W0)) | X]) and
+// XW1 = H1 W1 (layers.py:121, the first product of GraphConvolution 1) in one 128-row
+// tile pass; the step's packed weight images ride in the same launch as extra workgroups.
+struct FrontArgs {
+  const int* rowptr; const int* colidx; int R;
+  const float* x; int ldx; int f;
+  const float* w0; const float* g0; const float* b0; int h0;
+  __bf16* h1; int ldh1; float* ax; __bf16* axb;
+  const float* w1; int n1; int kp1, np1;     // W1 [h0 + f][n1] fp32; its image geometry
+  __bf16* xw1;                               // [R][n1]
+  PackDesc pack[kMaxPack]; int npack;        // weight images built by the extra workgroups
+  int pack_wg[kMaxPack + 1];                 // workgroup prefix per image
+  int dbg;
+};
+bool front_supported(int f, int h0, int n1, int kp1, int np1);
+int launch_front(FrontArgs& a, const PackDesc* pack, int npack, hipStream_t s);
+
 int head_init_attributes();
 
 }  // namespace snd

@@ -89,6 +89,7 @@ struct snd_plan {
   bool fast_enc = false;
   bool head_fused = false;     // fused encoder forward tail (snd_head.hip): 1 launch instead of 4
   bool head_bwd = false;       // fused edge terms + encoder backward head (snd_head.hip): 1 instead of 4
+  bool front_fused = false;    // gcn0 + H1 W1 + the weight images in one launch (snd_head.hip)
   int ldh1 = 0, ldg = 0;
   Img pw1f{}, pwhf{}, pwmsf{}, pwmsb{}, pwhb{}, pw1b{};
   Img pidg{};                  // graph latent: identity [W -> W] (dG enters RC_ENC1 directly)
@@ -411,6 +412,9 @@ extern "C" int snd_plan_create(const snd_config_t* cfg, int n_graphs, snd_plan_t
       if (p->head_bwd) p->add_buf("PHBMS", (long long)head_tiles(p->R) * 2 * L);
     }
   }
+  // GraphConvolution 0, XW1 and the packed weight images in one launch (debug bit 1048576:
+  // pack + gcn0 + a row-engine launch)
+  p->front_fused = p->fast_enc && !(dbg & 1048576) && front_supported(c.f_in, c.h0, c.h1, p->pw1f.kp, p->pw1f.np);
   *out = p;
   return 0;
 }
@@ -661,7 +665,9 @@ WgArgs wg_args(const snd_plan& p, const char* ws, const WgGeom& g, const void* x
   return a;
 }
 
-int pack_decoder(const Ctx& x) {
+// the step's packed bf16 weight images (decoder convs, and the encoder linears on the fast
+// encoder); returns the descriptor count
+int build_packs(const Ctx& x, PackDesc* e) {
   const snd_plan& p = *x.p;
   const snd_config_t& c = p.c;
   const int L = c.latent, dj = p.dj, s1 = c.s1, n1 = c.n1, s2 = c.s2, n2 = c.n2, s3 = c.s3;
@@ -684,9 +690,8 @@ int pack_decoder(const Ctx& x) {
           {src(K2s, s1, s2, 0, s1, 0, s2, 0, 0, 1), src(K2n, n1, n2, 0, n1, 0, n2, o1, o2, 1)}};
   d[5] = {dst(p.pk1b), 5, p.pk1b.kp, p.pk1b.np, 2,
           {src(K1, dj, C1, 0, dj, 0, s1, 0, 0, 1), src(K1, dj, C1, 0, dj, s1, C1, 0, o1, 1)}};
-  if (!p.fast_enc) return launch_pack(d, 6, x.s);
-  PackDesc e[12]{};
   for (int i = 0; i < 6; ++i) e[i] = d[i];
+  if (!p.fast_enc) return 6;
   const int f = c.f_in, h0 = c.h0, h1 = c.h1, gh = c.g_hidden, W = p.W;
   auto one = [&](const Img& im, PackSrc ps) { return PackDesc{dst(im), 1, im.kp, im.np, 1, {ps, {}}}; };
   if (p.tref) {
@@ -694,7 +699,7 @@ int pack_decoder(const Ctx& x) {
     e[6] = one(p.pw1f, src(W1, h0 + f, h1, 0, h0 + f, 0, h1, 0, 0, 0));
     e[7] = one(p.pw1b, src(W1, h0 + f, h1, 0, h0, 0, h1, 0, 0, 1));
     e[8] = one(p.pidg, src(nullptr, W, W, 0, W, 0, W, 0, 0, 2));
-    return launch_pack(e, 9, x.s);
+    return 9;
   }
   const float *W1 = x.w("enc.W1"), *Wh = x.w("enc.Wh"), *Wms = x.w("enc.Wms");
   e[6] = one(p.pw1f, src(W1, h0 + f, h1, 0, h0 + f, 0, h1, 0, 0, 0));
@@ -703,7 +708,12 @@ int pack_decoder(const Ctx& x) {
   e[9] = one(p.pwmsb, src(Wms, gh, 2 * L, 0, gh, 0, 2 * L, 0, 0, 1));
   e[10] = one(p.pwhb, src(Wh, W, gh, 0, W, 0, gh, 0, 0, 1));
   e[11] = one(p.pw1b, src(W1, h0 + f, h1, 0, h0, 0, h1, 0, 0, 1));
-  return launch_pack(e, 12, x.s);
+  return 12;
+}
+
+int pack_decoder(const Ctx& x) {
+  PackDesc e[kMaxPack]{};
+  return launch_pack(e, build_packs(x, e), x.s);
 }
 
 // optional row tiles of the batch (snd_row_tiles_t): the SpMM stages neighbour rows in LDS
@@ -721,14 +731,26 @@ int encoder_fast_fwd(const Ctx& x, const snd_batch_t* batch) {
   const snd_config_t& c = p.c;
   const int R = p.R, L = c.latent, f = c.f_in, h0 = c.h0, h1 = c.h1, gh = c.g_hidden, W = p.W;
   auto bf = [&](const char* n) { return reinterpret_cast<__bf16*>(x.f(n)); };
-  {
+  if (p.front_fused) {   // gcn0 + XW1 + the packed weight images: one launch
+    FrontArgs a{};
+    a.rowptr = batch->rowptr; a.colidx = batch->colidx; a.R = R;
+    a.x = batch->features; a.ldx = f; a.f = f;
+    a.w0 = x.w("enc.W0"); a.g0 = x.w("enc.bn0.gamma"); a.b0 = x.w("enc.bn0.beta"); a.h0 = h0;
+    a.h1 = bf("FH1"); a.ldh1 = p.ldh1; a.ax = x.f("AX"); a.axb = bf("AXB");
+    a.w1 = x.w("enc.W1"); a.n1 = h1; a.kp1 = p.pw1f.kp; a.np1 = p.pw1f.np;
+    a.xw1 = bf("FXW1"); a.dbg = debug_flags();
+    PackDesc e[kMaxPack]{};
+    const int ne = build_packs(x, e);
+    SND_TRY(launch_front(a, e, ne, x.s));
+  }
+  if (!p.front_fused) {
     Gcn0Args a{batch->rowptr, batch->colidx, R, batch->features, f, f, x.w("enc.W0"),
                x.w("enc.bn0.gamma"), x.w("enc.bn0.beta"), h0, bf("FH1"), p.ldh1, x.f("AX"), bf("AXB"),
                xcd_nbg(p.N, p.B)};
     a.row_order = batch->row_order;
     SND_TRY(launch_gcn0(a, x.s));
   }
-  {
+  if (!p.front_fused) {
     RcArgs a = rc_args(p, x.ws, p.pw1f, bf("FH1"), p.ldh1, h0 + f, h1, colmap_plain(h1));
     a.out = bf("FXW1"); a.ldo = h1; a.out_bf16 = 1;
     SND_TRY(launch_rowconv(a, RC_LIN, x.s));
@@ -1276,7 +1298,8 @@ extern "C" int snd_train_step(const snd_plan_t* plan, const snd_batch_t* batch,
   const float* X = batch->features;
   if (p.fast) {
     SND_TRY(fast_init_attributes());
-    SND_TRY(pack_decoder(x));   // bf16 weight images of this step's parameters
+    // bf16 weight images of this step's parameters (inside the encoder front when fused)
+    if (!p.front_fused) SND_TRY(pack_decoder(x));
   }
 
   // =============================== forward ===============================

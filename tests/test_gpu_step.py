@@ -416,3 +416,42 @@ def test_fused_backward_head_matches_chain(n, d, B):
             np.testing.assert_allclose(g1[k], g0[k], rtol=1e-4, atol=1e-6 * max(1.0, np.abs(g0[k]).max()), err_msg=k)
         else:
             assert np.array_equal(g0[k], g1[k]), k
+
+
+FRONT_BUFS = (("FH1", torch.bfloat16), ("AX", torch.float32), ("AXB", torch.bfloat16), ("FXW1", torch.bfloat16),
+              ("PK1F", torch.uint8), ("PK2F", torch.uint8), ("PK3F", torch.uint8), ("PK3B", torch.uint8),
+              ("PK2B", torch.uint8), ("PK1B", torch.uint8), ("PW1F", torch.uint8), ("PW1B", torch.uint8))
+
+
+@pytest.mark.parametrize("topology,n,d,B", [("tscale", 512, 64, 2), ("tscale", 300, 32, 3),
+                                            ("tscale", 200, 16, 2), ("tref", 300, 32, 2)])
+def test_fused_encoder_front_matches_chain(topology, n, d, B):
+    """The fused encoder front (snd_head.hip: the gcn0 gather, H1 = [BN0(lrelu(AX W0)) | X],
+    XW1 = H1 W1 and the step's packed weight images in one launch) against pack + gcn0 +
+    a row-engine launch (debug bit 1048576): H1, AX, XW1 and every weight image are
+    bitwise equal, and so is the whole step downstream."""
+    from snd_vae_amd import _lib
+    from snd_vae_amd.params import init_blocks
+    cfg = tscale(n, d) if topology == "tscale" else tref(n, d, g_hidden=16, latent=8)
+    batch = synthetic_batch(cfg, B, seed=14)
+    p0 = init_blocks(cfg, 5)
+    runs = []
+    for flags in (1048576, 0):
+        _lib.check(_lib.lib().snd_debug_set(flags))
+        try:
+            m, o, b = make(cfg, batch, p0, "bf16")
+        finally:
+            _lib.check(_lib.lib().snd_debug_set(0))
+        o.forward_backward(b)
+        torch.cuda.synchronize()
+        runs.append((m, o))
+    (m0, o0), (m1, o1) = runs
+    names = [nm for nm in FRONT_BUFS if not (topology == "tref" and nm[0] in ("PWHF",))]
+    for name, dt in names:
+        assert torch.equal(m0.buffer(name, dt), m1.buffer(name, dt)), name
+    l0, l1 = o0.loss_dict(), o1.loss_dict()
+    for k in l0:
+        assert l1[k] == l0[k], k
+    g0, g1 = o0.grad_blocks(), o1.grad_blocks()
+    for k in g0:
+        assert np.array_equal(g0[k], g1[k]), k
