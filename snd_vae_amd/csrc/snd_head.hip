@@ -46,8 +46,8 @@ __host__ __device__ __forceinline__ int hswz(int row, int kp) {
   return kp == 128 ? (row & 15) : (kp == 64 ? ((row >> 1) & 7) : 0);
 }
 
-// LDS layout (bytes) of head_fwd_kernel, shared by host and device.  The s exchange
-// buffer (fp32 [128][L + 4]) reuses the Wh image and the G image, dead after step 2.
+// LDS layout (bytes) of head_fwd_kernel, shared by host and device.  The [mu | s]
+// exchange (fp32 2 x [HR][L + 4]) reuses the weight, G and h images, dead after step 3.
 struct FwdLay {
   int w2, w1, g, h, zt, total, sx_end;
   __host__ __device__ FwdLay(int HR, int kp1, int np1, int kp2, int np2, int L) {
@@ -57,10 +57,10 @@ struct FwdLay {
     h = g + HR * kp1 * 2;
     zt = h + HR * kp2 * 2;
     total = zt + HR * (L + 1) * 4;
-    sx_end = w1 + HR * (L + 4) * 4;
+    sx_end = 2 * HR * (L + 4) * 4;
   }
 };
-constexpr int kHeadStaticLds = 2 * 128 * 4 + HWMAX * 8;
+constexpr int kHeadStaticLds = 2 * 128 * 4 + 2 * HWMAX * 8;
 constexpr int kHeadDynLds = 160 * 1024 - kHeadStaticLds - 512;
 
 // LDS-DMA a packed [np][kp] bf16 weight image (whole 1 KB pieces)
@@ -106,13 +106,14 @@ __global__ void __launch_bounds__(HR * 8) head_fwd_kernel(HeadFwdArgs a) {
   constexpr int HT = HR * 8, HW = HT / 64, NRB = HR / 16;   // threads, waves, 16-row blocks
   extern __shared__ __attribute__((aligned(16))) char smem[];
   __shared__ float cb1[128], cb2[128];   // bh, bms per physical column
-  __shared__ double klw[HWMAX];
+  __shared__ double klw[2 * HWMAX];
   const FwdLay lay(HR, a.kp1, a.np1, a.kp2, a.np2, a.L);
   __bf16* w2s = reinterpret_cast<__bf16*>(smem + lay.w2);
   __bf16* w1s = reinterpret_cast<__bf16*>(smem + lay.w1);
   __bf16* gs = reinterpret_cast<__bf16*>(smem + lay.g);
   __bf16* hs = reinterpret_cast<__bf16*>(smem + lay.h);
-  float* sx = reinterpret_cast<float*>(smem + lay.w1);
+  float* mx = reinterpret_cast<float*>(smem);                        // [HR][L + 4] mu, then
+  float* sx = reinterpret_cast<float*>(smem + HR * (a.L + 4) * 4);   // s: over the dead images
   float* zt = reinterpret_cast<float*>(smem + lay.zt);
   const int L = a.L, sxs = L + 4, zts = L + 1;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -196,7 +197,8 @@ __global__ void __launch_bounds__(HR * 8) head_fwd_kernel(HeadFwdArgs a) {
   const long long rr = gr0 + lrw;
   {
     f32x4 acc1[NB1];
-    img_gemm<NB1>(gs, w1s, a.kp1, a.np1, rb, NB1 * half, li, lg, acc1);
+    if (a.dbg & 16) { for (int i = 0; i < NB1; ++i) acc1[i] = f32x4{0.f, 0.f, 0.f, 0.f}; }
+    else img_gemm<NB1>(gs, w1s, a.kp1, a.np1, rb, NB1 * half, li, lg, acc1);
 #pragma unroll
     for (int i = 0; i < NB1; ++i) {
       const int n0 = 16 * (NB1 * half + i) + 4 * lg;
@@ -210,46 +212,59 @@ __global__ void __launch_bounds__(HR * 8) head_fwd_kernel(HeadFwdArgs a) {
   }
   __syncthreads();
 
-  // ---- 3. [mu | s] = h Wms + bms: the s half (waves NRB..) crosses to the mu waves
-  float mu[NB2][4];
+  // ---- 3. [mu | s] = h Wms + bms; both halves go to LDS (the weight and h images are dead)
   {
     f32x4 acc2[NB2];
-    img_gemm<NB2>(hs, w2s, a.kp2, a.np2, rb, NB2 * half, li, lg, acc2);
+    if (a.dbg & 16) { for (int i = 0; i < NB2; ++i) acc2[i] = f32x4{0.f, 0.f, 0.f, 0.f}; }
+    else img_gemm<NB2>(hs, w2s, a.kp2, a.np2, rb, NB2 * half, li, lg, acc2);
+    float o[NB2][4];
 #pragma unroll
     for (int i = 0; i < NB2; ++i) {
       const int n0 = 16 * (NB2 * half + i) + 4 * lg;
-      float o[4];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) o[e] = acc2[i][e] + cb2[n0 + e];
+      for (int e = 0; e < 4; ++e) o[i][e] = acc2[i][e] + cb2[n0 + e];
       if (vrow && !(a.dbg & 8))
-        *reinterpret_cast<float4*>(a.ms + rr * (2 * L) + n0) = make_float4(o[0], o[1], o[2], o[3]);
-      if (half == 1) *reinterpret_cast<float4*>(sx + row * sxs + (n0 - L)) = make_float4(o[0], o[1], o[2], o[3]);
+        *reinterpret_cast<float4*>(a.ms + rr * (2 * L) + n0) = make_float4(o[i][0], o[i][1], o[i][2], o[i][3]);
+    }
+    __syncthreads();   // every wave is past its MFMA reads of the Wms and h images
 #pragma unroll
-      for (int e = 0; e < 4; ++e) mu[i][e] = o[e];
+    for (int i = 0; i < NB2; ++i) {
+      const int n0 = 16 * (NB2 * half + i) + 4 * lg;   // half 0: mu columns, half 1: s columns
+      *reinterpret_cast<float4*>((half ? sx : mx) + row * sxs + (n0 - half * L)) =
+          make_float4(o[i][0], o[i][1], o[i][2], o[i][3]);
     }
   }
   __syncthreads();
 
-  // ---- 4. z = mu + eps e^s, KL, bf16 z, z sqrt(log2 e) rows, z into LDS for the transpose
-  if (half == 0) {
+  // ---- 4. z = mu + eps e^s, KL, bf16 z, z sqrt(log2 e) rows, z into LDS for the transpose;
+  // every wave takes rows x Philox quads of the tile
+  {
     const unsigned off = a.step ? (unsigned)(*a.step) : 0u;
-    double kl = 0.0;
+    const int nq = L >> 2;
+    double kl[HR / 64];
 #pragma unroll
-    for (int i = 0; i < NB2; ++i) {
-      const int c = 16 * i + 4 * lg;          // mu column (one Philox quad)
+    for (int h = 0; h < HR / 64; ++h) kl[h] = 0.0;
+    for (int it = (a.dbg & 32) ? HR * nq : tid; it < HR * nq; it += HT) {
+      const int zr = it / nq, c = 4 * (it - zr * nq);
+      const int zl = lr0 + zr;
       float z4[4] = {0.f, 0.f, 0.f, 0.f};
-      if (vrow) {
-        const long long ie = rr * L + c;
-        const float4 s4 = *reinterpret_cast<const float4*>(sx + row * sxs + c);
+      if (zl < a.npg) {
+        const long long ie = (gr0 + zl) * L + c;
+        const float4 m4 = *reinterpret_cast<const float4*>(mx + zr * sxs + c);
+        const float4 s4 = *reinterpret_cast<const float4*>(sx + zr * sxs + c);
         const float4 ep = a.eps_in ? *reinterpret_cast<const float4*>(a.eps_in + ie)
                                    : philox_normal4(a.seed, off, (a.eps_base + (unsigned long long)ie) >> 2);
-        const float s[4] = {s4.x, s4.y, s4.z, s4.w}, e[4] = {ep.x, ep.y, ep.z, ep.w};
+        const float mu[4] = {m4.x, m4.y, m4.z, m4.w}, s[4] = {s4.x, s4.y, s4.z, s4.w};
+        const float e[4] = {ep.x, ep.y, ep.z, ep.w};
+        double kq = 0.0;
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
           const float es = __expf(s[t]);
-          z4[t] = mu[i][t] + e[t] * es;                                       // model.py:159
-          kl += (double)(1.f + 2.f * s[t] - mu[i][t] * mu[i][t] - es * es);    // optimizer.py:193
+          z4[t] = mu[t] + e[t] * es;                                          // model.py:159
+          kq += (double)(1.f + 2.f * s[t] - mu[t] * mu[t] - es * es);        // optimizer.py:193
         }
+#pragma unroll
+        for (int h = 0; h < HR / 64; ++h) kl[h] += (zr >> 6) == h ? kq : 0.0;
         if (!(a.dbg & 8)) {
           *reinterpret_cast<float4*>(a.z + ie) = make_float4(z4[0], z4[1], z4[2], z4[3]);
           *reinterpret_cast<float4*>(a.eps_out + ie) = ep;
@@ -263,32 +278,43 @@ __global__ void __launch_bounds__(HR * 8) head_fwd_kernel(HeadFwdArgs a) {
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
         jb[t] = (__bf16)(z4[t] * kSqrtLog2e);
-        zt[row * zts + c + t] = z4[t];
+        zt[zr * zts + c + t] = z4[t];
       }
-      *reinterpret_cast<bf16x4*>(a.jrow + ((long long)gi * a.npad + lrw) * L + c) = jb;
+      *reinterpret_cast<bf16x4*>(a.jrow + ((long long)gi * a.npad + zl) * L + c) = jb;
     }
-    kl = wave_sum_d(kl);
-    if (lane == 0) klw[w] = kl;
+#pragma unroll
+    for (int h = 0; h < HR / 64; ++h) {
+      const double v = wave_sum_d(kl[h]);
+      if (lane == 0) klw[h * HWMAX + w] = v;
+    }
   }
   __syncthreads();
   // per-64-row column sums of the stored K-role values (reparam_prep order)
-  for (int i = tid; i < (HR / 64) * L; i += HT) {
+  for (int i = (a.dbg & 64) ? HT * HR : tid; i < (HR / 64) * L; i += HT) {
     const int h = i / L, c = i - h * L;
     float cs = 0.f;
-    for (int q = 0; q < 64; ++q) cs += (float)(__bf16)(zt[(64 * h + q) * zts + c] * kSqrtLog2e);
+    for (int q0 = 0; q0 < 64; q0 += 16) {   // 16 reads in flight, the sum in row order
+      float t[16];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) t[u] = zt[(64 * h + q0 + u) * zts + c];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) cs += (float)(__bf16)(t[u] * kSqrtLog2e);
+    }
     a.colpart[((long long)gi * (a.npad / 64) + (HR / 64) * lt + h) * L + c] = cs;
   }
   // z^T image: 4 consecutive rows per lane
-  for (int idx = tid; idx < (HR / 4) * L; idx += HT) {
+  for (int idx = (a.dbg & 64) ? HT * HR : tid; idx < (HR / 4) * L; idx += HT) {
     const int c = idx / (HR / 4), r4 = 4 * (idx % (HR / 4));
     bf16x4 t;
 #pragma unroll
     for (int u = 0; u < 4; ++u) t[u] = (__bf16)zt[(r4 + u) * zts + c];
     *reinterpret_cast<bf16x4*>(a.jt + ((long long)gi * L + c) * a.npad + lr0 + r4) = t;
   }
-  if (tid < HR / 64)   // the 64-row block's four 16-row waves, in order
-    a.kl_part[(long long)gi * (a.npad / 64) + (HR / 64) * lt + tid] =
-        klw[4 * tid] + klw[4 * tid + 1] + klw[4 * tid + 2] + klw[4 * tid + 3];
+  if (tid < HR / 64) {   // the 64-row block's partial: every wave's share, in wave order
+    double v = 0.0;
+    for (int k = 0; k < HW; ++k) v += klw[tid * HWMAX + k];
+    a.kl_part[(long long)gi * (a.npad / 64) + (HR / 64) * lt + tid] = v;
+  }
 }
 
 template <int HR, int NB1, int NB2>
@@ -828,7 +854,7 @@ bool head_fwd_supported(int h1, int f, int gh, int L, int kp1, int np1, int kp2,
   if (h1 + 8 > kp1 || gh % 16 || gh < 16 || np1 != gh || np1 > 64 || gh > kp2) return false;
   if ((L != 32 && L != 64) || np2 != 2 * L) return false;
   const FwdLay l64(64, kp1, np1, kp2, np2, L), l128(128, kp1, np1, kp2, np2, L);
-  return l128.total <= kHeadDynLds && l64.sx_end <= l64.h && l128.sx_end <= l128.h;
+  return l128.total <= kHeadDynLds && l64.sx_end <= l64.zt && l128.sx_end <= l128.zt;
 }
 
 int launch_head_fwd(const HeadFwdArgs& a, hipStream_t s) {
