@@ -211,16 +211,67 @@ def test_zzt_ce_f32(n, d, B, kbar):
     assert rel(dz.cpu().numpy(), rdz) < 1e-5
 
 
-@pytest.mark.parametrize("n,d,B", [(300, 64, 2), (128, 128, 2)])
-def test_zzt_ce_bf16(n, d, B):
+@pytest.mark.parametrize("n,d,B,scale", [(300, 64, 2, 0.25), (128, 128, 2, 0.25), (300, 32, 3, 0.3),
+                                         (700, 64, 1, 0.25), (257, 64, 2, 1.0), (130, 16, 2, 0.5)])
+def test_zzt_ce_bf16(n, d, B, scale):
+    """bf16 zz^T + CE (v4 for d <= 64: 32x32x16 MFMA, select-free epilogue; v3 for d = 128).
+    (700, 64, 1): column splits; scale 1.0: logits up to |L| ~ 40."""
     from snd_vae_amd import layers
-    rp, ci, dense, z = _zzt_case(n, d, B, 10.0, 7, 0.25)
+    rp, ci, dense, z = _zzt_case(n, d, B, 10.0, 7, scale)
     ce, correct, dz = layers.inner_product_ce(cu(z), B, cu(rp, torch.int32), cu(ci, torch.int32),
                                               dtype="bf16")
     rce, rdz, rcorrect = R.adj_ce(z.astype(np.float64), dense, n)
     assert ce == pytest.approx(rce, rel=2e-3)
     assert abs(correct - rcorrect) <= 0.01 * B * n * n
     assert rel(dz.cpu().numpy(), rdz) < 2e-2
+
+
+def test_zzt_ce_bf16_extreme_logits():
+    """Planted blocks of logits far beyond the v4 pair-product range (L = -100 between
+    rows 0-3 and 4-7, +100 inside each block): the overflow fallback keeps the CE exact."""
+    from snd_vae_amd import layers
+    n, d, B = 200, 64, 2
+    rp, ci, dense, z = _zzt_case(n, d, B, 8.0, 11, 0.25)
+    a = np.zeros(d, np.float32)
+    a[:4] = 5.0                                   # |a|^2 = 100
+    for b in range(B):
+        z[b * n:b * n + 4] = a
+        z[b * n + 4:b * n + 8] = -a
+    ce, correct, dz = layers.inner_product_ce(cu(z), B, cu(rp, torch.int32), cu(ci, torch.int32),
+                                              dtype="bf16")
+    rce, rdz, rcorrect = R.adj_ce(z.astype(np.float64), dense, n)
+    assert np.isfinite(ce)
+    assert ce == pytest.approx(rce, rel=2e-3)
+    assert abs(correct - rcorrect) <= 0.01 * B * n * n
+    assert rel(dz.cpu().numpy(), rdz) < 2e-2
+
+
+def test_zzt_v4_matches_v3_in_step():
+    """The step's zz^T launch: v4 (default) against v3 on the same staged z (C2 shapes,
+    8 graphs): loss and count agree to bf16 rounding, dJ within bf16 operand rounding."""
+    from snd_vae_amd import _lib
+    from snd_vae_amd.model import DeviceBatch, SGCNModelVAE
+    from snd_vae_amd.optimizer import OptimizerVAE
+    cfg = tscale(4096, 64)
+    db = DeviceBatch(synthetic_batch(cfg, 8, seed=1000))
+    model = SGCNModelVAE(cfg, 8, dtype="bf16")
+    opt = OptimizerVAE(model)
+    opt.step(db)
+    torch.cuda.synchronize()
+    L = _lib.lib()
+    bc = db.c_struct()
+    pz = model.buffer("PZZT", torch.float64)
+    djd = model.buffer("DJD")
+    out = {}
+    for name in ("zzt_dense_v3", "zzt_dense"):
+        _lib.check(L.snd_plan_launch(model.plan, bc, model.workspace.data_ptr(), name.encode(),
+                                     _lib.stream_ptr()))
+        torch.cuda.synchronize()
+        out[name] = (pz.view(-1, 2).sum(0).cpu().numpy(), djd.clone().cpu().numpy())
+    (s3, d3), (s4, d4) = out["zzt_dense_v3"], out["zzt_dense"]
+    assert s4[0] == pytest.approx(s3[0], rel=1e-4)
+    assert abs(s4[1] - s3[1]) <= 1e-4 * 8 * 4096 * 4096
+    assert rel(d4, d3) < 1e-2
 
 
 def test_zzt_ce_weighted_bce():
