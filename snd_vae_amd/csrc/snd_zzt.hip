@@ -867,35 +867,39 @@ __global__ void __launch_bounds__(NTH) zzt_dense_f32(ZztArgs a) {
 // blocks (32 j of every 128-column tile): each wave owns one 32 x 32 logit
 // block per tile.  A 32x32x16 MFMA holds the SIMD's vector issue for 8 of its
 // 32 cycles (16x16x32: 8 of 16), and a block needs half v3's LDS operand reads.
-//   fwd   Y[j][i] = -c - x_ij        A = z_j rows (LDS tile), B = -z_i (LDS image
+//   fwd   Y[j][i] = -x_ij            A = z_j rows (LDS tile), B = -z_i (LDS image
 //                                    of the workgroup's rows, negated; registers
-//                                    are the scarce resource at 4 waves per SIMD),
-//                                    C = -c (an inline constant: c = 4)
+//                                    are the scarce resource at 4 waves per SIMD)
 //   bwd   dJ'[i][c] += S'[i][j] z_j[c] A = S' packed straight from Y's registers
 //                                    (its column i is on the lane), B = z^T
 //                                    (LDS, j order permuted to match)
-// Epilogue per logit (EPI 0), y = -x - c:
-//   e = 2^y; q = e + 2^-c; s' = 1/q = 2^c sigmoid(x); pos = (y < -c);
-//   per PAIR of logits one log2(q_a q_b) (q >= 2^-c: the product stays normal).
-// softplus2(x) = x + log2(q) + c with sum_j x_ij = z_i . colsum (analytic): no
-// |x| and no select per logit.  sigmoid(x) = 1 / (1 + 2^-x) is exact and finite
-// for every x (q = inf -> 0); s' carries 2^c through bf16 (exact) and the MFMA,
-// removed once at the end.  A pair product overflows only when x_a + x_b <
-// -(128 + 2c) (L_a + L_b < -94): that lane recomputes the block's loss terms in
-// the |x| form (one wave-uniform test per block when nothing overflows).
-// Measured cost model of the epilogue (phase-skip builds): ~8 issue cycles per
-// transcendental and ~4 per other VALU op per wave, so EPI 0 (2.5 transcendentals
-// + ~3.3 other ops per logit) beats v3's |x| form (EPI 1: 2.125 + ~6.9).
+// Epilogue per logit (EPI 0), y = -x:
+//   e = 2^y; q = 1 + e; s = 1/q = sigmoid(x); per PAIR of logits one
+//   log2(q_a q_b); #{x > 0} = #{sign(y)}: sign bytes of 4 logits gathered by two
+//   v_perm and popcounted (1 op per logit instead of a compare + SALU ballot).
+// softplus2(x) = x + log2(q) with sum_j x_ij = z_i . colsum (analytic): no |x|
+// and no select per logit.  sigmoid(x) = 1 / (1 + 2^-x) is exact and finite for
+// every x (q = inf -> 0).  A pair product overflows only when x_a + x_b < -128
+// (L_a + L_b < -88.7): that lane recomputes the block's loss terms in the |x|
+// form (one wave-uniform test per block when nothing overflows).
+// Measured rates (tools/micro/valu_rate.hip, 4 waves per SIMD): a transcendental
+// costs ~3.4 FMAs of issue and does not co-issue with them; compare + ballot ~2
+// FMAs.  EPI 0 (2.5 transcendentals + ~2.5 other ops per logit) beats v3's |x|
+// form (EPI 1: 2.125 + ~6.9).  c (kZ4C) stays a parameter: a nonzero c needs the
+// ballot count (y < -c) back.
 // Tiles are triple-buffered (global loads two tiles ahead).  MODE 1 issues tile
 // t+1's forward MFMAs before tile t's epilogue (matrix pipe beside the wave's own
-// VALU); MODE 2 runs odd column-block waves' backward MFMAs one tile late.
+// VALU; it spills at d = 64); MODE 2 runs odd column-block waves' backward MFMAs
+// one tile late.  Measured at C2 within one run: MODE 0 62.1 us, MODE 2 63.3,
+// MODE 1 67.0, v3 65.1 (phase split of MODE 0, stamps: prologue 3.2 us, tile
+// loop ~48 us of which the epilogue VALU ~60 %, corrections + stores 2.4 us).
 // LDS images carry one 16 B pad per row: every operand read of a lane group
 // lands on 16 distinct 4-bank groups and all k-steps / output blocks of a lane
 // share one address register.  The diagonal correction reads z_i[c] from a
 // transposed LDS copy of the workgroup's z^T columns (one coalesced load).
-constexpr float kZ4C = 4.f;             // c: an inline constant of the MFMA's C operand
-constexpr float kZ4Q = 0.0625f;          // 2^-c
-constexpr float kZ4S = 0.0625f;          // dJ scale 2^-c
+constexpr float kZ4C = 0.f;             // c (an inline constant of the MFMA's C operand)
+constexpr float kZ4Q = 1.f;              // 2^-c
+constexpr float kZ4S = 1.f;              // dJ scale 2^-c
 
 template <int DP, int MODE, int EPI, bool MEAS>
 __global__ void __launch_bounds__(NTH2) zzt_dense_bf16_v4(ZztArgs a) {
@@ -911,6 +915,7 @@ __global__ void __launch_bounds__(NTH2) zzt_dense_bf16_v4(ZztArgs a) {
   constexpr int JCH = TJ2 * CPR, TCH = DP * TCPR;
   constexpr int JPT = (JCH + NT - 1) / NT, TPT = (TCH + NT - 1) / NT;
   constexpr float C4 = EPI == 0 ? kZ4C : 0.f;
+  static_assert(kZ4C == 0.f, "EPI 0 counts x > 0 by the sign of y = -x - c: c must be 0");
   constexpr unsigned NEG = EPI == 0 ? 0x80008000u : 0u;   // B operand sign
   __shared__ __attribute__((aligned(16))) __bf16 lds[3 * BUF];
   __shared__ __attribute__((aligned(16))) __bf16 brows[ROWS * JST];   // (-)z_i rows (scaled)
@@ -1039,7 +1044,7 @@ __global__ void __launch_bounds__(NTH2) zzt_dense_bf16_v4(ZztArgs a) {
   };
   float lacc = 0.f, labs = 0.f;
   double ltot = 0.0;
-  unsigned wcnt = 0;
+  unsigned wcnt = 0, lcnt = 0;   // per wave (EPI 1 ballots) / per lane (EPI 0 sign bits)
   auto epi = [&](const f32x16& Y, bf16x8 (&sA)[2]) {
     if constexpr (EPI == 0) {
       float q[16], lt = 0.f;
@@ -1048,7 +1053,16 @@ __global__ void __launch_bounds__(NTH2) zzt_dense_bf16_v4(ZztArgs a) {
         const float e = __builtin_amdgcn_exp2f(Y[v]);
         q[v] = e + kZ4Q;
         sA[v >> 3][v & 7] = (__bf16)__builtin_amdgcn_rcpf(q[v]);
-        wcnt += (unsigned)__popcll(__ballot(Y[v] < -kZ4C));
+      }
+      // #{x > 0} = #{y < 0} (c = 0; y = +0 where x = 0): the sign bytes of four y's
+      // gathered by two v_perm, masked, popcounted into a per-lane count
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const unsigned t01 = __builtin_amdgcn_perm(__float_as_uint(Y[4 * g4 + 1]),
+                                                   __float_as_uint(Y[4 * g4]), 0x0C0C0703u);
+        const unsigned t23 = __builtin_amdgcn_perm(__float_as_uint(Y[4 * g4 + 3]),
+                                                   __float_as_uint(Y[4 * g4 + 2]), 0x07030C0Cu);
+        lcnt += (unsigned)__builtin_popcount((t01 | t23) & 0x80808080u);
       }
 #pragma unroll
       for (int p = 0; p < 8; ++p) lt += __builtin_amdgcn_logf(q[2 * p] * q[2 * p + 1]);
@@ -1227,6 +1241,7 @@ __global__ void __launch_bounds__(NTH2) zzt_dense_bf16_v4(ZztArgs a) {
     }
   }
   const double l = wave_sum_d(ltot);
+  if constexpr (EPI == 0) wcnt = wave_sum_u(lcnt);
   if (lane == 0) { sl[w] = l; sc[w] = wcnt - dpos; }
   __syncthreads();
   if (tid == 0) {
@@ -1339,12 +1354,12 @@ int launch_zzt_dense(const ZztArgs& a, int dtype, hipStream_t s) {
     else if (dp == 64) hipLaunchKernelGGL((zzt_dense_bf16_v2<64>), grid, dim3(NTH2), 0, s, a);
     else hipLaunchKernelGGL((zzt_dense_bf16_v2<128>), grid, dim3(NTH2), 0, s, a);
   } else if (dtype == SND_BF16 && dp <= 64 && (a.variant & 255) != 3) {   // v4 (default, d <= 64)
-    // default: signed epilogue, pipelined forward; A/B: variant 10 + 3 EPI + MODE;
+    // default: signed epilogue, plain tile order; A/B: variant 10 + 3 EPI + MODE;
     // variant >= 256: the measurement build of the default (phase skips / stamps)
     const int v = a.variant & 255;
-    const int cfg = (a.variant >= 256 || v < 10 || v > 15) ? 1 : v - 10;
+    const int cfg = (a.variant >= 256 || v < 10 || v > 15) ? 0 : v - 10;
 #define SND_V4(DPV)                                                                              \
-  if (a.variant >= 256) hipLaunchKernelGGL((zzt_dense_bf16_v4<DPV, 1, 0, true>), grid, dim3(NTH2), 0, s, a); \
+  if (a.variant >= 256) hipLaunchKernelGGL((zzt_dense_bf16_v4<DPV, 0, 0, true>), grid, dim3(NTH2), 0, s, a); \
   else if (cfg == 0) hipLaunchKernelGGL((zzt_dense_bf16_v4<DPV, 0, 0, false>), grid, dim3(NTH2), 0, s, a); \
   else if (cfg == 1) hipLaunchKernelGGL((zzt_dense_bf16_v4<DPV, 1, 0, false>), grid, dim3(NTH2), 0, s, a); \
   else if (cfg == 2) hipLaunchKernelGGL((zzt_dense_bf16_v4<DPV, 2, 0, false>), grid, dim3(NTH2), 0, s, a); \
