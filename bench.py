@@ -189,8 +189,9 @@ def kernel_timer(model, bc, reps):
 def spmm_batched(host, width, copies, reps):
     """The bf16 SpMM on `copies` x the bench batch stacked block-diagonally (8 x copies
     graphs): a working set above the 256 MB Infinity Cache, so the HBM fraction is not
-    a cache artefact.  Headline: the row-tiled kernel
-    (snd_csr_spmm_bf16_tiled, neighbour rows staged in LDS); previous_variant: the
+    a cache artefact.  Headline: the sliding-window kernel
+    (snd_csr_spmm_bf16_window, every h row DMA'd once into an LDS ring);
+    previous_variant: the row-tile kernel (snd_csr_spmm_bf16_tiled) and, under it, the
     register-gather kernel (snd_csr_spmm_bf16) on the same input."""
     import ctypes
 
@@ -220,21 +221,37 @@ def spmm_batched(host, width, copies, reps):
     out = torch.empty_like(h)
     L = _lib.lib()
     ng = host.n_graphs * copies
-    ms = time_launches(lambda sp: _lib.check(L.snd_csr_spmm_bf16_tiled(
+    ms_tiled = time_launches(lambda sp: _lib.check(L.snd_csr_spmm_bf16_tiled(
         d_rp.data_ptr(), d_ci.data_ptr(), R, ctypes.byref(tiles), h.data_ptr(), width, width,
         out.data_ptr(), width, host.n_nodes, ng, d_order.data_ptr(), sp)), reps)
-    ms_prev = time_launches(lambda sp: _lib.check(L.snd_csr_spmm_bf16(
+    ms_reg = time_launches(lambda sp: _lib.check(L.snd_csr_spmm_bf16(
         d_rp.data_ptr(), d_ci.data_ptr(), R, h.data_ptr(), width, width, out.data_ptr(), width,
         host.n_nodes, ng, d_order.data_ptr(), sp)), reps)
     byts = 4 * (R + 1) + 4 * len(ci) + 2 * 2 * R * width
+    frac = lambda t: round(byts / (t * 1e-3) / 1e9 / PEAK_HBM_GBS, 4)
+    tiled = {"kernel": f"csr_spmm_bf16_tiled ({tr}-row tiles, sets <= {rt.ustride} rows)",
+             "avg_launch_ms": round(ms_tiled, 5), "frac": frac(ms_tiled)}
+    reg = {"kernel": "csr_spmm_bf16 (register gathers)", "avg_launch_ms": round(ms_reg, 5),
+           "frac": frac(ms_reg)}
+    # headline: the sliding-window kernel (h rows DMA'd once into an LDS ring) when the
+    # schedule's bandwidth fits its ring, else the row-tile kernel
+    from snd_vae_amd.data import window_plan
+    from snd_vae_amd.layers import DeviceWindowPlan
+    wp = window_plan(big, order.astype(np.int32))
+    if (wp.beta + 7) // 8 * 8 <= 352 and width == 64:
+        dw = DeviceWindowPlan(wp)
+        ms = time_launches(lambda sp: _lib.check(L.snd_csr_spmm_bf16_window(
+            dw.meta.data_ptr(), dw.slots.data_ptr(), dw.rows.data_ptr(), dw.order.data_ptr(), R, host.n_nodes, ng, wp.beta,
+            h.data_ptr(), width, width, out.data_ptr(), width, sp)), reps)
+        kern = (f"csr_spmm_bf16_window (A @ H, width {width}, {ng} graphs block-diagonal, {len(ci)} nnz, "
+                f"RCM schedule, beta {wp.beta}, 1096-row LDS ring)")
+        prev = dict(tiled, previous_variant=reg)
+    else:
+        ms, kern, prev = ms_tiled, "csr_spmm_bf16_tiled (A @ H, width %d, %d graphs)" % (width, ng), reg
     gbs = byts / (ms * 1e-3) / 1e9
-    return {"kernel": f"csr_spmm_bf16_tiled (A @ H, width {width}, {ng} graphs "
-                      f"block-diagonal, {len(ci)} nnz, {tr}-row tiles, sets <= {rt.ustride} rows)",
-            "bound": "hbm", "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+    return {"kernel": kern, "bound": "hbm", "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
             "frac": round(gbs / PEAK_HBM_GBS, 4), "avg_launch_ms": round(ms, 5),
-            "bytes_per_launch": byts,
-            "previous_variant": {"kernel": "csr_spmm_bf16 (register gathers)", "avg_launch_ms": round(ms_prev, 5),
-                                 "frac": round(byts / (ms_prev * 1e-3) / 1e9 / PEAK_HBM_GBS, 4)}}
+            "bytes_per_launch": byts, "previous_variant": prev}
 
 
 def extra_workload(name, args, info):

@@ -121,6 +121,28 @@ int snd_csr_spmm_bf16_tiled(const int* rowptr, const int* colidx, int n_rows,
                             const snd_row_tiles_t* tiles, const void* h, int ldh,
                             int width, void* out, int ldo, int n_per_graph,
                             int n_graphs, const int* row_order, snd_stream_t stream);
+/* snd_csr_spmm_bf16 streamed through a sliding window (ABI 7): out = A @ h,
+ * width 64, bf16 rows, fp32 sums in colidx order (bitwise equal to
+ * snd_csr_spmm_bf16).  A workgroup walks one graph's schedule positions (e.g.
+ * the per-graph RCM order) in steps of 128 rows and keeps the h rows of
+ * positions [p - beta, p + 127 + beta] in a 1096-row LDS ring, filled by
+ * LDS-DMA two steps ahead: every h row is read from HBM once.  The plan
+ * (snd_vae_amd/data.py window_plan, host-built once per batch):
+ *   meta[q]  = (start8 << 6) | degree of the row at position q (degree <= 63)
+ *   slots[]  = u16 ring slot (neighbour position % 1096) per neighbour, each
+ *              row's list at 8 * start8, padded to 8 entries
+ *   rows[q]  = the row whose sums position q computes, and meta[q] its meta:
+ *              inside each aligned 128-position block listed by degree,
+ *              descending (a wave's 8 rows then share their neighbour count)
+ *   order[q] = the row at position q (the h row held at ring slot q % 1096)
+ * beta = max |neighbour position - row position|; ceil8(beta) <= 352, else
+ * SND_ERR_ARG (use snd_csr_spmm_bf16_tiled).  Replaces layers.py:122 (tf.matmul
+ * of the dense adjacency). */
+int snd_csr_spmm_bf16_window(const int* meta, const uint16_t* slots, const int* rows,
+                             const int* order,
+                             int n_rows, int n_per_graph, int n_graphs, int beta,
+                             const void* h, int ldh, int width, void* out, int ldo,
+                             snd_stream_t stream);
 /* ---- a5: linear / dense GEMM on MFMA ---------------------------------------
  * Replaces linear() (layers.py:566-576) and the X@w of GraphConvolution
  * (layers.py:120-121; the tile() copy is not needed):

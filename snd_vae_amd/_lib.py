@@ -17,7 +17,7 @@ c_int, c_ll, c_float, c_size, c_ull = C.c_int, C.c_longlong, C.c_float, C.c_size
 vp = C.c_void_p
 
 
-ABI_VERSION = 6
+ABI_VERSION = 7
 GEN_MODES = {"sample": 0, "mean": 1, "prior": 2, "given": 3}
 TOPOLOGY = {"tscale": 0, "tref": 1}
 
@@ -67,6 +67,8 @@ _SIGS = {
     "snd_spmm_tile_plan": (c_ll, [vp, vp, c_int, vp, c_int, vp, vp, vp, vp, C.POINTER(c_int)]),
     "snd_csr_spmm_bf16_tiled": (c_int, [vp, vp, c_int, C.POINTER(RowTiles), vp, c_int, c_int, vp,
                                         c_int, c_int, c_int, vp, vp]),
+    "snd_csr_spmm_bf16_window": (c_int, [vp, vp, vp, vp, c_int, c_int, c_int, c_int, vp, c_int, c_int,
+                                         vp, c_int, vp]),
     "snd_gemm": (c_int, [c_int, c_int, c_int, c_int, c_int, vp, c_int, vp, c_int, vp, c_int,
                          vp, c_int, vp]),
     "snd_conv1d_same_fwd": (c_int, [vp, c_int, c_int, c_int, c_int, vp, c_int, vp, vp, vp,

@@ -23,6 +23,7 @@ from dataclasses import dataclass
 from typing import List, Optional, Sequence
 
 import numpy as np
+from typing import NamedTuple
 
 from .config import SNDConfig
 
@@ -232,6 +233,63 @@ def row_tiles(batch: GraphBatch, order: Optional[np.ndarray], tile_rows: int) ->
     if n2 != n:
         raise _lib.SNDError(f"snd_spmm_tile_plan failed ({n2}): {_lib.last_error()}")
     return RowTiles(rows, trp, lcol, ucol, tile_rows, int(ust.value))
+
+
+class WindowPlan(NamedTuple):
+    """Sliding-window SpMM plan (snd_csr_spmm_bf16_window), one per batch."""
+    meta: np.ndarray     # int32 [R]: (start8 << 6) | degree, rows by degree inside each 128-position block
+    slots: np.ndarray    # uint16 [8 * sum(ceil8(degree))]: ring slot (position % 1096) per neighbour
+    rows: np.ndarray     # int32 [R]: the row of each meta entry
+    order: np.ndarray    # int32 [R]: the row at each position (the schedule)
+    beta: int            # largest |position(neighbour) - position(row)|
+    max_degree: int
+
+
+def window_plan(batch: GraphBatch, order: np.ndarray, ring: int = 1096) -> WindowPlan:
+    """Position-ordered neighbour lists for the window SpMM.
+
+    Position q (per graph, in the schedule ``order``, e.g. locality_order) holds
+    row order[q]; its neighbours (colidx order, so the kernel's fp32 sums are the
+    register kernel's) are stored as ring slots (neighbour position mod ``ring``)
+    in a list padded to 8 entries.  beta bounds |position distance| over all
+    edges; the kernel needs ceil8(beta) <= 352 (snd_csr_spmm_bf16_window).
+    meta / rows list each aligned block of 128 positions (one kernel step) by
+    degree, descending (ties by position): a wavefront's 8 rows then have
+    similar lengths, and the SIMD's four wavefronts together about the mean.
+    """
+    n, B = batch.n_nodes, batch.n_graphs
+    R = n * B
+    order = np.ascontiguousarray(order, np.int64)
+    rp = batch.rowptr.astype(np.int64)
+    ci = batch.colidx.astype(np.int64)
+    pos = np.empty(R, np.int64)
+    pos[order] = np.arange(R) % n                 # graph-local position of every row
+    deg = np.diff(rp)[order]                      # degree of the row at each position
+    if deg.size and deg.max() > 63:
+        raise ValueError("window_plan: degree > 63 does not fit the metadata word")
+    pad = (deg + 7) // 8 * 8
+    start = np.zeros(R + 1, np.int64)
+    np.cumsum(pad, out=start[1:])
+    if start[-1] // 8 >= (1 << 25):
+        raise ValueError("window_plan: slot lists exceed the 25-bit offset")
+    nnz = int(deg.sum())
+    slots = np.zeros(max(int(start[-1]), 8), np.uint16)
+    beta = 0
+    if nnz:
+        excl = np.cumsum(deg) - deg               # exclusive prefix of degrees
+        run = np.arange(nnz) - np.repeat(excl, deg)   # index within the row's list
+        src = np.repeat(rp[order], deg) + run     # colidx entries in position order
+        npos = pos[ci[src]]
+        qpos = np.repeat(np.arange(R) % n, deg)
+        beta = int(np.abs(npos - qpos).max())
+        slots[np.repeat(start[:-1], deg) + run] = (npos % ring).astype(np.uint16)
+    meta = ((start[:-1] // 8) << 6 | deg).astype(np.int32)
+    # per aligned 128-position block of each graph: degree descending, ties by position
+    q = np.arange(R)
+    blk = (q // n) * ((n + 127) // 128) + (q % n) // 128
+    srt = np.lexsort((q, -deg, blk))
+    return WindowPlan(meta[srt], slots, order[srt].astype(np.int32), order.astype(np.int32), beta,
+                      int(deg.max()) if deg.size else 0)
 
 
 def shard(batch: GraphBatch, rank: int, world: int) -> GraphBatch:

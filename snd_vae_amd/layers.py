@@ -14,6 +14,7 @@ from __future__ import annotations
 
 import ctypes as C
 
+import numpy as np
 import torch
 
 from . import _lib
@@ -94,6 +95,30 @@ def spmm_bf16_tiled(rowptr, colidx, tiles, h, n_per_graph=0, n_graphs=0, row_ord
     _lib.check(_lib.lib().snd_csr_spmm_bf16_tiled(
         _P(rowptr), _P(colidx), rows, C.byref(t), _P(h), width, width, _P(out), width,
         n_per_graph, n_graphs, _P(row_order), _lib.stream_ptr()), "snd_csr_spmm_bf16_tiled")
+    return out
+
+
+class DeviceWindowPlan:
+    """data.WindowPlan on the device (meta, slots, rows, order) for spmm_bf16_window."""
+
+    def __init__(self, plan, device="cuda"):
+        self.meta = torch.from_numpy(plan.meta).to(device)
+        self.slots = torch.from_numpy(plan.slots.view(np.int16)).to(device)
+        self.rows = torch.from_numpy(plan.rows).to(device)
+        self.order = torch.from_numpy(plan.order).to(device)
+        self.beta = plan.beta
+
+
+def spmm_bf16_window(wplan, h, n_per_graph, n_graphs):
+    """spmm_bf16 streamed through an LDS window (snd_csr_spmm_bf16_window);
+    bit-identical to spmm_bf16.  wplan: DeviceWindowPlan."""
+    if not (h.is_cuda and h.is_contiguous() and h.dtype == torch.bfloat16):
+        raise ValueError("spmm_bf16_window: expected a contiguous bfloat16 device tensor")
+    rows, width = h.shape
+    out = torch.empty_like(h)
+    _lib.check(_lib.lib().snd_csr_spmm_bf16_window(
+        _P(wplan.meta), _P(wplan.slots), _P(wplan.rows), _P(wplan.order), rows, n_per_graph, n_graphs, wplan.beta,
+        _P(h), width, width, _P(out), width, _lib.stream_ptr()), "snd_csr_spmm_bf16_window")
     return out
 
 

@@ -133,6 +133,51 @@ def test_spmm_bf16_tiled_bitwise(n, B, kbar, width, tile_rows, locality):
         assert np.abs(out.float().cpu().numpy() - r64).max() <= 2 ** -7 * max(np.abs(r64).max(), 1.0)
 
 
+@pytest.mark.parametrize("n,B,kbar,seed", [(4096, 8, 16.0, 9), (4096, 64, 16.0, 9), (4096, 1, 16.0, 3),
+                                             (1000, 3, 16.0, 4), (300, 3, 10.0, 5), (96, 2, 0.0, 6),
+                                             (256, 4, 40.0, 7), (200, 1, 50.0, 8), (130, 5, 3.0, 2)])
+def test_spmm_bf16_window_bitwise(n, B, kbar, seed):
+    """The sliding-window SpMM (h rows DMA'd once into a 1096-row LDS ring, two
+    128-row steps ahead) sums every row's neighbours in colidx order: bitwise equal
+    to spmm_bf16.  64 graphs: one workgroup per graph, 32 steps; 8 graphs: 32
+    one-step segments per graph; n = 1000 / 130: partial last steps; kbar 40 / 50:
+    rows past 32 neighbours; kbar 0: empty rows."""
+    from snd_vae_amd import layers
+    from snd_vae_amd.data import GraphBatch, locality_order, window_plan
+    rp, ci, dense = rand_batch(n, B, kbar, seed) if B <= 8 else rand_batch_csr(n, B, kbar, seed)
+    gb = GraphBatch(B, n, rp, ci, np.zeros((n * B, 1), np.float32), np.zeros((n * B, 1), np.float32),
+                    np.zeros((n * B, 2), np.float32))
+    order = locality_order(gb)
+    wp = window_plan(gb, order)
+    assert (wp.beta + 7) // 8 * 8 <= 352
+    if kbar >= 40:
+        assert wp.max_degree > 32
+    hb = torch.from_numpy(np.random.default_rng(seed).standard_normal((n * B, 64)).astype(np.float32)).to(torch.bfloat16)
+    d_rp, d_ci = cu(rp, torch.int32), cu(ci if len(ci) else np.zeros(1, np.int32), torch.int32)
+    ref = layers.spmm_bf16(d_rp, d_ci, hb.cuda(), n, B, cu(order, torch.int32))
+    out = layers.spmm_bf16_window(layers.DeviceWindowPlan(wp), hb.cuda(), n, B)
+    torch.cuda.synchronize()
+    assert torch.equal(out.view(torch.int16), ref.view(torch.int16))
+    if dense is not None:
+        r64 = R.spmm(dense, hb.float().numpy().astype(np.float64), n)
+        assert np.abs(out.float().cpu().numpy() - r64).max() <= 2 ** -7 * max(np.abs(r64).max(), 1.0)
+
+
+def test_spmm_bf16_window_rejects_wide_window():
+    """Natural (generator) order puts neighbours ~N apart: the window plan's beta
+    exceeds the ring and the launch refuses (the caller keeps the tiled kernel)."""
+    from snd_vae_amd import _lib, layers
+    from snd_vae_amd.data import GraphBatch, window_plan
+    n, B = 4096, 1
+    rp, ci = rand_batch_csr(n, B, 16.0, 1)[:2]
+    gb = GraphBatch(B, n, rp, ci, np.zeros((n, 1), np.float32), np.zeros((n, 1), np.float32),
+                    np.zeros((n, 2), np.float32))
+    wp = window_plan(gb, np.arange(n, dtype=np.int32))
+    assert wp.beta > 352
+    with pytest.raises(_lib.SNDError):
+        layers.spmm_bf16_window(layers.DeviceWindowPlan(wp), torch.zeros(n, 64, dtype=torch.bfloat16, device="cuda"), n, B)
+
+
 def test_graph_convolution_epilogue():
     from snd_vae_amd import layers
     n, B, f, w = 150, 2, 3, 64

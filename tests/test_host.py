@@ -209,3 +209,38 @@ def test_reference_checkpoint_names_roundtrip(topology):
     del bad["encoder/g_g0_conv/w"]
     with pytest.raises(KeyError):
         checkpoint.reference_to_blocks(cfg, bad)
+
+
+@pytest.mark.parametrize("n,B,kbar", [(500, 3, 8.0), (4096, 2, 16.0), (97, 4, 5.0)])
+def test_window_plan_matches_literal(n, B, kbar):
+    """data.window_plan (sliding-window SpMM plan) against a per-row restatement:
+    position q holds row order[q]; its list = ring slots of its neighbours'
+    positions in colidx order, padded to 8; meta = (start8 << 6) | degree, listed
+    (with rows) by degree descending inside every aligned 128-position block."""
+    from snd_vae_amd.config import tscale
+    from snd_vae_amd.data import locality_order, synthetic_batch, window_plan
+    b = synthetic_batch(tscale(n, 16, mean_degree=kbar), B, seed=n)
+    order = locality_order(b)
+    wp = window_plan(b, order)
+    R = n * B
+    pos = np.empty(R, np.int64)
+    pos[order] = np.arange(R) % n
+    start, beta = 0, 0
+    meta = np.zeros(R, np.int64)
+    for q in range(R):
+        row = int(order[q])
+        nb = b.colidx[b.rowptr[row]:b.rowptr[row + 1]].astype(np.int64)
+        meta[q] = (start // 8) << 6 | len(nb)
+        np.testing.assert_array_equal(wp.slots[start:start + len(nb)], pos[nb] % 1096)
+        assert all(nb // n == row // n)                       # block diagonal
+        if len(nb):
+            beta = max(beta, int(np.abs(pos[nb] - q % n).max()))
+        start += (len(nb) + 7) // 8 * 8
+    assert wp.beta == beta
+    np.testing.assert_array_equal(wp.order, order)
+    for g in range(B):
+        for lo in range(0, n, 128):
+            qs = list(range(g * n + lo, g * n + min(lo + 128, n)))
+            key = sorted(qs, key=lambda q: (-(meta[q] & 63), q))
+            np.testing.assert_array_equal(wp.meta[qs[0]:qs[-1] + 1], meta[key])
+            np.testing.assert_array_equal(wp.rows[qs[0]:qs[-1] + 1], order[key])

@@ -53,6 +53,23 @@ __global__ void kern(float* out, int iters) {
       c += __popcll(__ballot(a4 > 0.5f)); c += __popcll(__ballot(a5 > 0.5f));
       c += __popcll(__ballot(a6 > 0.5f)); c += __popcll(__ballot(a7 > 0.5f));
       a0 += (float)c;
+    } else if constexpr (KIND == 8) {   // 8 v_dot2_f32_bf16 (accumulating)
+      typedef __bf16 bf2 __attribute__((ext_vector_type(2)));
+      bf2 x = {av[0], av[1]}, one = {(__bf16)1.f, (__bf16)0.f};
+      a0 = __builtin_amdgcn_fdot2_f32_bf16(x, one, a0, false);
+      a1 = __builtin_amdgcn_fdot2_f32_bf16(x, one, a1, false);
+      a2 = __builtin_amdgcn_fdot2_f32_bf16(x, one, a2, false);
+      a3 = __builtin_amdgcn_fdot2_f32_bf16(x, one, a3, false);
+      a4 = __builtin_amdgcn_fdot2_f32_bf16(x, one, a4, false);
+      a5 = __builtin_amdgcn_fdot2_f32_bf16(x, one, a5, false);
+      a6 = __builtin_amdgcn_fdot2_f32_bf16(x, one, a6, false);
+      a7 = __builtin_amdgcn_fdot2_f32_bf16(x, one, a7, false);
+      av[0] = (__bf16)a7;
+    } else if constexpr (KIND == 9) {   // 8 v_pk_add_f32 (2 floats each)
+      typedef float f2 __attribute__((ext_vector_type(2)));
+      f2 p0 = {a0, a1}, p1 = {a2, a3}, p2 = {a4, a5}, p3 = {a6, a7}, k = {0.5f, 0.25f};
+      for (int u = 0; u < 2; ++u) { p0 += k; p1 += k; p2 += k; p3 += k; }
+      a0 = p0[0]; a1 = p0[1]; a2 = p1[0]; a3 = p1[1]; a4 = p2[0]; a5 = p2[1]; a6 = p3[0]; a7 = p3[1];
     } else if constexpr (KIND == 7) {   // 4 rcp + 4 exp2
       a0 = __builtin_amdgcn_exp2f(a0); a1 = __builtin_amdgcn_rcpf(a1);
       a2 = __builtin_amdgcn_exp2f(a2); a3 = __builtin_amdgcn_rcpf(a3);
@@ -70,7 +87,7 @@ void run(const char* name, int ninstr) {
   float* out;
   hipMalloc(&out, 256 * 1024 * sizeof(float));
   const int iters = 4000;
-  for (int wps : {1, 2, 4, 8}) {
+  for (int wps : {1, 2, 4}) {
     const int threads = 256 * wps;   // wps waves per SIMD
     hipEvent_t e0, e1;
     hipEventCreate(&e0); hipEventCreate(&e1);
@@ -98,5 +115,7 @@ int main() {
   run<4>("mfma32 + exp2 x8", 1);
   run<5>("mfma32 + fma x8", 1);
   run<6>("cmp+ballot x8", 8);
+  run<8>("dot2_f32_bf16 x8", 8);
+  run<9>("pk_add_f32 x8", 8);
   return 0;
 }
