@@ -18,7 +18,9 @@
 //             offset in 16-byte units (lists padded to 8 entries)
 //   slots[]   u16 ring slot (neighbour position % 1096) of every neighbour, in
 //             colidx order: the fp32 sums are the register kernel's, in the same
-//             order, so the result is bitwise equal to snd_csr_spmm_bf16
+//             order, so the result is bitwise equal to snd_csr_spmm_bf16; each
+//             list is padded with the zero row's slot (1096) to a multiple of 8
+//             and to the largest degree of its wavefront's 8 rows (<= 32)
 //   rows[q]   the row whose sums position q computes: inside every aligned
 //             128-position block the rows (and their meta) are listed by degree,
 //             descending, so the 8 rows of a wave have near-equal degrees and the
@@ -77,7 +79,7 @@ struct WinArgs {
   int ldo;
   int n, spg, seg, beta8;
   int dbg;   // measurement only (snd_debug_set >> 16): 1 no sums, 2 no window DMA, 4 no slot DMA,
-             // 8 neighbour groups of 8 (default 4)
+             // 8 neighbour groups of 8 (default 4), 16 shift/and unpack + packed adds (default dot2)
 };
 
 __device__ __forceinline__ void acc8(float (&f)[8], const uint4 d) {
@@ -87,6 +89,38 @@ __device__ __forceinline__ void acc8(float (&f)[8], const uint4 d) {
     f[2 * j] += __uint_as_float(v[j] << 16);
     f[2 * j + 1] += __uint_as_float(v[j] & 0xFFFF0000u);
   }
+}
+
+// the same fp32 sums without unpacking: v_dot2c_f32_bf16 with (1, 0) / (0, 1) adds
+// the low / high bf16 of a word to an fp32 accumulator (x * 1 and y * 0 are exact,
+// one rounding: the add of acc8), 8 VALU per neighbour instead of 12
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void acc8_dot(float (&f)[8], const uint4 d) {
+  const unsigned v[4] = {d.x, d.y, d.z, d.w};
+  // (1, 0) and (0, 1) through SGPRs: hipcc encodes the bf16 pair (1, 0) as the inline
+  // constant 1.0, which the hardware reads as the fp32 word 0x3F800000 = (0, 1)
+  unsigned lo1u, hi1u;
+  asm volatile("s_mov_b32 %0, 0x3f80" : "=s"(lo1u));
+  asm volatile("s_mov_b32 %0, 0x3f800000" : "=s"(hi1u));
+  const bf16x2_t lo1 = __builtin_bit_cast(bf16x2_t, lo1u);
+  const bf16x2_t hi1 = __builtin_bit_cast(bf16x2_t, hi1u);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const bf16x2_t x = __builtin_bit_cast(bf16x2_t, v[j]);
+    f[2 * j] = __builtin_amdgcn_fdot2_f32_bf16(x, lo1, f[2 * j], false);
+    f[2 * j + 1] = __builtin_amdgcn_fdot2_f32_bf16(x, hi1, f[2 * j + 1], false);
+  }
+}
+
+// LDS byte address of ring slot (the low or high u16 of w) for a lane at column
+// offset `base`: slot * 128 + base in one v_mad_u32_u16 (op_sel picks the half).
+// Entries past a row's degree hold the zero row's slot (the plan pads every list
+// to its wavefront group's largest degree), so no per-entry compare or select.
+__device__ __forceinline__ unsigned slot_addr(unsigned w, int hi, unsigned base) {
+  unsigned r;
+  if (hi) asm("v_mad_u32_u16 %0, %1, %2, %3 op_sel:[1,0,0,0]" : "=v"(r) : "v"(w), "s"(WIDTH * 2), "v"(base));
+  else asm("v_mad_u32_u16 %0, %1, %2, %3" : "=v"(r) : "v"(w), "s"(WIDTH * 2), "v"(base));
+  return r;
 }
 
 constexpr int vmcnt_imm(int n) { return (n & 15) | (7 << 4) | (15 << 8) | ((n >> 4) << 14); }
@@ -112,7 +146,7 @@ __device__ __forceinline__ void raw_barrier() {
   asm volatile("" ::: "memory");
 }
 
-template <int GK>
+template <int GK, bool DOT>
 __global__ void __launch_bounds__(WT) spmm_win_kernel(WinArgs a) {
   __shared__ __attribute__((aligned(16))) char lds[LDS_BYTES];
   const unsigned lds0 = (unsigned)(uintptr_t)(lptr_t)lds;   // LDS byte address of lds[0]
@@ -190,9 +224,12 @@ __global__ void __launch_bounds__(WT) spmm_win_kernel(WinArgs a) {
     __builtin_amdgcn_s_waitcnt(vmcnt_imm(5));
     raw_barrier();
 
-    // sum the row's neighbours from the ring (colidx order, fp32); entries past the
-    // row's degree read the zero row, so a group of GK reads is issued before the
-    // first add; the wave leaves the loop after its rows' largest degree
+    // sum the row's neighbours from the ring (colidx order, fp32).  The wave's 8 rows
+    // are one degree-sorted group and every list is padded with the zero row to the
+    // group's largest degree (exact +0 adds past a row's own degree): a chunk of GK
+    // reads is issued before the first add; the wave leaves the loop after the
+    // group's largest degree.  (Reads of the next chunk issued before the adds of
+    // the current one measured slower: 101 vs 96 us.)
     const int m0 = lds_i32(idx_blk(s) + 4 * r8);
     const int row0 = lds_i32(idx_blk(s) + 32 + 4 * r8);
     const int deg = m0 & 63;
@@ -210,18 +247,21 @@ __global__ void __launch_bounds__(WT) spmm_win_kernel(WinArgs a) {
 #pragma unroll
       for (int j = 0; j < GK; ++j) {
         const int k = k0 + j;
-        const unsigned sk = (k & 1) ? (sv[k >> 1] >> 16) : (sv[k >> 1] & 0xFFFFu);
-        const unsigned slot = k < deg ? sk : (unsigned)ZROW;
-        d[j] = *reinterpret_cast<const uint4*>(lds + slot * (WIDTH * 2) + base);
+        d[j] = *reinterpret_cast<const uint4*>(lds + slot_addr(sv[k >> 1], k & 1, base));
       }
 #pragma unroll
-      for (int j = 0; j < GK; ++j) acc8(f, d[j]);
+      for (int j = 0; j < GK; ++j) {
+        if constexpr (DOT) acc8_dot(f, d[j]);
+        else acc8(f, d[j]);
+      }
     }
     if (__builtin_amdgcn_ballot_w64(deg > 32)) {   // rows past 32 neighbours (rare)
       const int k0 = (m0 >> 6) * 8;
       for (int k = 32; k < deg; ++k) {
         const unsigned slot = a.slots[k0 + k];
-        acc8(f, *reinterpret_cast<const uint4*>(lds + slot * (WIDTH * 2) + base));
+        const uint4 dv = *reinterpret_cast<const uint4*>(lds + slot * (WIDTH * 2) + base);
+        if constexpr (DOT) acc8_dot(f, dv);
+        else acc8(f, dv);
       }
     }
     bf16x8 o;
@@ -263,10 +303,15 @@ extern "C" int snd_csr_spmm_bf16_window(const int* meta, const uint16_t* slots, 
   WinArgs a{meta, slots, rows, order, reinterpret_cast<const __bf16*>(h), ldh,
             reinterpret_cast<__bf16*>(out), ldo, n_per_graph, cdiv(n_per_graph, seg), seg, beta8,
             debug_flags() >> 16};
-  if (a.dbg & 8)
-    hipLaunchKernelGGL(spmm_win_kernel<8>, dim3(n_graphs * a.spg), dim3(WT), 0, (hipStream_t)stream, a);
-  else
-    hipLaunchKernelGGL(spmm_win_kernel<4>, dim3(n_graphs * a.spg), dim3(WT), 0, (hipStream_t)stream, a);
+  const dim3 grid(n_graphs * a.spg);
+  const hipStream_t st = (hipStream_t)stream;
+  if (a.dbg & 8) {
+    if (a.dbg & 16) hipLaunchKernelGGL((spmm_win_kernel<8, false>), grid, dim3(WT), 0, st, a);
+    else hipLaunchKernelGGL((spmm_win_kernel<8, true>), grid, dim3(WT), 0, st, a);
+  } else {
+    if (a.dbg & 16) hipLaunchKernelGGL((spmm_win_kernel<4, false>), grid, dim3(WT), 0, st, a);
+    else hipLaunchKernelGGL((spmm_win_kernel<4, true>), grid, dim3(WT), 0, st, a);
+  }
   SND_LAUNCH_CHECK("spmm_win_kernel");
   return 0;
 }

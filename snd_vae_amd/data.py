@@ -267,13 +267,27 @@ def window_plan(batch: GraphBatch, order: np.ndarray, ring: int = 1096) -> Windo
     deg = np.diff(rp)[order]                      # degree of the row at each position
     if deg.size and deg.max() > 63:
         raise ValueError("window_plan: degree > 63 does not fit the metadata word")
-    pad = (deg + 7) // 8 * 8
+    # per aligned 128-position block of each graph: degree descending, ties by position
+    q = np.arange(R)
+    blk = (q // n) * ((n + 127) // 128) + (q % n) // 128
+    srt = np.lexsort((q, -deg, blk))
+    # a wavefront sums the 8 rows of one sorted group together up to their largest
+    # degree: every list is padded (with the ring's zero row, slot ``ring``) to its
+    # group's largest degree (at most the 32 entries the kernel stages), in 8s
+    rank = np.empty(R, np.int64)
+    bs = blk[srt]
+    first = np.searchsorted(bs, bs, side="left")          # sorted index of the block's first row
+    rank[srt] = np.arange(R) - first                       # rank of a position inside its block
+    gfirst = np.empty(R, np.int64)
+    gfirst[srt] = first + (rank[srt] // 8) * 8             # sorted index of its group's first row
+    gmax = deg[srt][gfirst] if R else deg
+    pad = (np.maximum(deg, np.minimum(gmax, 32)) + 7) // 8 * 8
     start = np.zeros(R + 1, np.int64)
     np.cumsum(pad, out=start[1:])
     if start[-1] // 8 >= (1 << 25):
         raise ValueError("window_plan: slot lists exceed the 25-bit offset")
     nnz = int(deg.sum())
-    slots = np.zeros(max(int(start[-1]), 8), np.uint16)
+    slots = np.full(max(int(start[-1]), 8), ring, np.uint16)
     beta = 0
     if nnz:
         excl = np.cumsum(deg) - deg               # exclusive prefix of degrees
@@ -284,10 +298,6 @@ def window_plan(batch: GraphBatch, order: np.ndarray, ring: int = 1096) -> Windo
         beta = int(np.abs(npos - qpos).max())
         slots[np.repeat(start[:-1], deg) + run] = (npos % ring).astype(np.uint16)
     meta = ((start[:-1] // 8) << 6 | deg).astype(np.int32)
-    # per aligned 128-position block of each graph: degree descending, ties by position
-    q = np.arange(R)
-    blk = (q // n) * ((n + 127) // 128) + (q % n) // 128
-    srt = np.lexsort((q, -deg, blk))
     return WindowPlan(meta[srt], slots, order[srt].astype(np.int32), order.astype(np.int32), beta,
                       int(deg.max()) if deg.size else 0)
 

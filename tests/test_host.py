@@ -215,8 +215,10 @@ def test_reference_checkpoint_names_roundtrip(topology):
 def test_window_plan_matches_literal(n, B, kbar):
     """data.window_plan (sliding-window SpMM plan) against a per-row restatement:
     position q holds row order[q]; its list = ring slots of its neighbours'
-    positions in colidx order, padded to 8; meta = (start8 << 6) | degree, listed
-    (with rows) by degree descending inside every aligned 128-position block."""
+    positions in colidx order, then the zero row's slot 1096 up to its wavefront
+    group's largest degree (at most 32), in 8s; meta = (start8 << 6) | degree,
+    listed (with rows) by degree descending inside every aligned 128-position
+    block, a group = 8 consecutive rows of that listing."""
     from snd_vae_amd.config import tscale
     from snd_vae_amd.data import locality_order, synthetic_batch, window_plan
     b = synthetic_batch(tscale(n, 16, mean_degree=kbar), B, seed=n)
@@ -225,22 +227,30 @@ def test_window_plan_matches_literal(n, B, kbar):
     R = n * B
     pos = np.empty(R, np.int64)
     pos[order] = np.arange(R) % n
+    deg = np.array([b.rowptr[r + 1] - b.rowptr[r] for r in order], np.int64)
+    keys, gmax = {}, np.zeros(R, np.int64)
+    for g in range(B):
+        for lo in range(0, n, 128):
+            qs = list(range(g * n + lo, g * n + min(lo + 128, n)))
+            key = sorted(qs, key=lambda q: (-deg[q], q))
+            keys[(g, lo)] = (qs, key)
+            for i, q in enumerate(key):
+                gmax[q] = deg[key[i - i % 8]]
     start, beta = 0, 0
     meta = np.zeros(R, np.int64)
     for q in range(R):
         row = int(order[q])
         nb = b.colidx[b.rowptr[row]:b.rowptr[row + 1]].astype(np.int64)
         meta[q] = (start // 8) << 6 | len(nb)
+        plen = (max(len(nb), min(int(gmax[q]), 32)) + 7) // 8 * 8
         np.testing.assert_array_equal(wp.slots[start:start + len(nb)], pos[nb] % 1096)
+        assert (wp.slots[start + len(nb):start + plen] == 1096).all()
         assert all(nb // n == row // n)                       # block diagonal
         if len(nb):
             beta = max(beta, int(np.abs(pos[nb] - q % n).max()))
-        start += (len(nb) + 7) // 8 * 8
+        start += plen
     assert wp.beta == beta
     np.testing.assert_array_equal(wp.order, order)
-    for g in range(B):
-        for lo in range(0, n, 128):
-            qs = list(range(g * n + lo, g * n + min(lo + 128, n)))
-            key = sorted(qs, key=lambda q: (-(meta[q] & 63), q))
-            np.testing.assert_array_equal(wp.meta[qs[0]:qs[-1] + 1], meta[key])
-            np.testing.assert_array_equal(wp.rows[qs[0]:qs[-1] + 1], order[key])
+    for qs, key in keys.values():
+        np.testing.assert_array_equal(wp.meta[qs[0]:qs[-1] + 1], meta[key])
+        np.testing.assert_array_equal(wp.rows[qs[0]:qs[-1] + 1], order[key])

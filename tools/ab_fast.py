@@ -18,6 +18,7 @@ def main():
     ap.add_argument("--flags", default="0")
     ap.add_argument("--reps", type=int, default=30)
     ap.add_argument("--graphs", type=int, default=8)
+    ap.add_argument("--keys", default="", help="snd_plan_launch keys, comma list (default: pack + dec:0..10)")
     args = ap.parse_args()
     import torch
     from snd_vae_amd import _lib
@@ -37,6 +38,9 @@ def main():
     flags = [int(f, 0) for f in args.flags.split(",")]
     keys = ["pack"] + [f"dec:{k}" for k in range(len(NAMES))]
     labels = ["pack"] + NAMES
+    if args.keys:
+        keys = args.keys.split(",")
+        labels = keys
     print("kernel".ljust(18) + "".join(f"flags={f:<4d}".rjust(12) for f in flags))
     for key, lab in zip(keys, labels):
         row = []
