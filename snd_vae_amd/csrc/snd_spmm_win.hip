@@ -43,7 +43,8 @@
 //      store of s-1 and c/d/e of s), and with them every older DMA: index(s+2)
 //      and this step's window (e of step s-2)
 //   barrier; sum from the ring; store; barrier (the next step's DMAs overwrite
-//   what this step read)
+//   what this step read).  With beta8 <= 288 the step is instead: vmcnt(2)
+//   (slots(s)); barrier; b-e; sum; store -- one barrier per step.
 // LDS (one array): ring 1096 rows x 128 B, a zero row (the slot of list entries
 // past a row's degree), 4 index blocks (16 waves x [meta 8 | row 8 | piece 8]),
 // 2 slot-list buffers (16 waves x 512 B) = 162944 B.  The window of step s+1
@@ -79,7 +80,8 @@ struct WinArgs {
   int ldo;
   int n, spg, seg, beta8;
   int dbg;   // measurement only (snd_debug_set >> 16): 1 no sums, 2 no window DMA, 4 no slot DMA,
-             // 8 neighbour groups of 8 (default 4), 16 shift/and unpack + packed adds (default dot2)
+             // 8 neighbour groups of 8 (default 4), 16 shift/and unpack + packed adds (default dot2),
+             // 32 two barriers per step at any beta
 };
 
 __device__ __forceinline__ void acc8(float (&f)[8], const uint4 d) {
@@ -212,17 +214,32 @@ __global__ void __launch_bounds__(WT) spmm_win_kernel(WinArgs a) {
   __syncthreads();
 
   const unsigned base = (unsigned)(l8 * 16);
-  for (int s = 0; s < nsteps; ++s) {
-    // b: start8 of the rows of step s+1, row id of this lane's row of the window piece
+  // b-e: the step's reads of index(s) / index(s+1) and its DMAs
+  auto issue = [&](int s) {
     const int st1 = lds_i32(idx_blk(s + 1) + 4 * (lane >> 2)) >> 6;
     const int prow = lds_i32(idx_blk(s) + 64 + 4 * r8);
-    // c, d, e
     dma_index(s + 3);
     if (!(a.dbg & 4)) dma_slots(s + 1, st1);
     if (!(a.dbg & 2)) dma_piece(dpiece(s), prow);
-    // f: slots(s), index(s+2) and this step's window are in
-    __builtin_amdgcn_s_waitcnt(vmcnt_imm(5));
-    raw_barrier();
+  };
+  // One barrier per step when the window leaves room: the DMAs of step s are issued
+  // after its barrier (every wave has finished step s-1, the last reader of the
+  // index block, slot buffer and ring rows they overwrite; the ring rows e(s)
+  // overwrites lie below every position step s reads while 2 beta8 < 592).
+  const bool one = a.beta8 <= 288 && !(a.dbg & 32);
+  for (int s = 0; s < nsteps; ++s) {
+    if (one) {
+      // slots(s) (d of step s-1, followed by e(s-1) and the store of s-1) and every
+      // older DMA are in
+      __builtin_amdgcn_s_waitcnt(vmcnt_imm(2));
+      raw_barrier();
+      issue(s);
+    } else {
+      issue(s);
+      // f: slots(s), index(s+2) and this step's window are in
+      __builtin_amdgcn_s_waitcnt(vmcnt_imm(5));
+      raw_barrier();
+    }
 
     // sum the row's neighbours from the ring (colidx order, fp32).  The wave's 8 rows
     // are one degree-sorted group and every list is padded with the zero row to the
@@ -270,7 +287,7 @@ __global__ void __launch_bounds__(WT) spmm_win_kernel(WinArgs a) {
     *reinterpret_cast<bf16x8*>(a.out + (long long)row0 * a.ldo + 8 * l8) = o;
     // every wave's LDS reads of this step are done (their values were consumed)
     // before any wave's next DMA overwrites ring rows, index blocks or slot lists
-    raw_barrier();
+    if (!one) raw_barrier();
   }
 }
 

@@ -141,7 +141,8 @@ def test_spmm_bf16_window_bitwise(n, B, kbar, seed):
     128-row steps ahead) sums every row's neighbours in colidx order: bitwise equal
     to spmm_bf16.  64 graphs: one workgroup per graph, 32 steps; 8 graphs: 32
     one-step segments per graph; n = 1000 / 130: partial last steps; kbar 40 / 50:
-    rows past 32 neighbours; kbar 0: empty rows."""
+    rows past 32 neighbours; kbar 0: empty rows.  N = 4096 (beta ~ 260): one
+    barrier per step, and (forced) the two-barrier step of wider windows."""
     from snd_vae_amd import layers
     from snd_vae_amd.data import GraphBatch, locality_order, window_plan
     rp, ci, dense = rand_batch(n, B, kbar, seed) if B <= 8 else rand_batch_csr(n, B, kbar, seed)
@@ -158,6 +159,16 @@ def test_spmm_bf16_window_bitwise(n, B, kbar, seed):
     out = layers.spmm_bf16_window(layers.DeviceWindowPlan(wp), hb.cuda(), n, B)
     torch.cuda.synchronize()
     assert torch.equal(out.view(torch.int16), ref.view(torch.int16))
+    if n == 4096 and B in (1, 8):
+        # the two-barrier step (the schedule for beta > 288), forced by debug bit 32 << 16
+        from snd_vae_amd import _lib
+        _lib.check(_lib.lib().snd_debug_set(32 << 16))
+        try:
+            out2 = layers.spmm_bf16_window(layers.DeviceWindowPlan(wp), hb.cuda(), n, B)
+            torch.cuda.synchronize()
+        finally:
+            _lib.check(_lib.lib().snd_debug_set(0))
+        assert torch.equal(out2.view(torch.int16), ref.view(torch.int16))
     if dense is not None:
         r64 = R.spmm(dense, hb.float().numpy().astype(np.float64), n)
         assert np.abs(out.float().cpu().numpy() - r64).max() <= 2 ** -7 * max(np.abs(r64).max(), 1.0)
