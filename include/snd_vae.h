@@ -122,15 +122,18 @@ int snd_csr_spmm_bf16_tiled(const int* rowptr, const int* colidx, int n_rows,
                             int width, void* out, int ldo, int n_per_graph,
                             int n_graphs, const int* row_order, snd_stream_t stream);
 /* snd_csr_spmm_bf16 streamed through a sliding window (ABI 7): out = A @ h,
- * width 64, bf16 rows, fp32 sums in colidx order (bitwise equal to
- * snd_csr_spmm_bf16).  A workgroup walks one graph's schedule positions (e.g.
+ * width 64, bf16 rows, fp32 sums in colidx order (accumulated by
+ * v_dot2c_f32_bf16: within one fp32 ulp per add of snd_csr_spmm_bf16, bitwise
+ * equal on every tested batch).  A workgroup walks one graph's schedule positions (e.g.
  * the per-graph RCM order) in steps of 128 rows and keeps the h rows of
  * positions [p - beta, p + 127 + beta] in a 1096-row LDS ring, filled by
  * LDS-DMA two steps ahead: every h row is read from HBM once.  The plan
  * (snd_vae_amd/data.py window_plan, host-built once per batch):
  *   meta[q]  = (start8 << 6) | degree of the row at position q (degree <= 63)
  *   slots[]  = u16 ring slot (neighbour position % 1096) per neighbour, each
- *              row's list at 8 * start8, padded to 8 entries
+ *              row's list at 8 * start8, padded with the zero row's slot 1096
+ *              to a multiple of 8 and to the largest degree (<= 32) of its
+ *              wavefront group (8 consecutive rows of the listing below)
  *   rows[q]  = the row whose sums position q computes, and meta[q] its meta:
  *              inside each aligned 128-position block listed by degree,
  *              descending (a wave's 8 rows then share their neighbour count)
