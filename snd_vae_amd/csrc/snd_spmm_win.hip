@@ -81,7 +81,7 @@ struct WinArgs {
   int n, spg, seg, beta8;
   int dbg;   // measurement only (snd_debug_set >> 16): 1 no sums, 2 no window DMA, 4 no slot DMA,
              // 8 neighbour groups of 8 (default 4), 16 shift/and unpack + packed adds (default dot2),
-             // 32 two barriers per step at any beta
+             // 32 two barriers per step at any beta, 64 the MFMA sums (default: VALU, 8 lanes per row)
 };
 
 __device__ __forceinline__ void acc8(float (&f)[8], const uint4 d) {
@@ -148,7 +148,17 @@ __device__ __forceinline__ void raw_barrier() {
   asm volatile("" ::: "memory");
 }
 
-template <int GK, bool DOT>
+typedef short v4s_t __attribute__((ext_vector_type(4)));
+typedef short v8s_t __attribute__((ext_vector_type(8)));
+typedef __attribute__((address_space(3))) v4s_t lds_v4s_t;
+
+// MF: the sums on MFMA (see the MF block of the step loop); the ring rows are then
+// stored with their 32-byte segments XORed by (slot >> 1) & 3.  Measured slower than
+// the VALU sums (105.6 vs 94.0 us on the 256-graph batch, 1 of 67 M outputs 1 bf16 ulp
+// apart): twice the LDS instructions (8-byte transposed reads), bank conflicts 40 % of
+// LDS-active cycles (a 32-lane half's 8 ring rows fall on 8 segment positions at
+// random), and ~10 VALU per MFMA of address arithmetic.  Kept behind debug bit 64 << 16.
+template <int GK, bool DOT, bool MF>
 __global__ void __launch_bounds__(WT) spmm_win_kernel(WinArgs a) {
   __shared__ __attribute__((aligned(16))) char lds[LDS_BYTES];
   const unsigned lds0 = (unsigned)(uintptr_t)(lptr_t)lds;   // LDS byte address of lds[0]
@@ -189,7 +199,9 @@ __global__ void __launch_bounds__(WT) spmm_win_kernel(WinArgs a) {
   };
   // e: one 8-row piece of the window (row ids from index(s))
   auto dma_piece = [&](int p0, int row) {
-    const __bf16* src = a.h + (long long)row * a.ldh + 8 * l8;
+    // MF: ring slot p0 % RR + r8 holds its segment sigma at sigma ^ ((slot >> 1) & 3)
+    const int ch16 = MF ? (l8 ^ ((((p0 % RR) + r8) >> 1 & 3) << 1)) : l8;
+    const __bf16* src = a.h + (long long)row * a.ldh + 8 * ch16;
     glds<16>(src, __builtin_amdgcn_readfirstlane(lds0 + (p0 % RR) * (WIDTH * 2)));
   };
   auto lds_i32 = [&](int off) { return *reinterpret_cast<const int*>(lds + off); };
@@ -214,6 +226,14 @@ __global__ void __launch_bounds__(WT) spmm_win_kernel(WinArgs a) {
   __syncthreads();
 
   const unsigned base = (unsigned)(l8 * 16);
+  // MF: lane (gq, li) holds B[k = 8 gq + e][n = li] = 1 iff k >> 1 == n (k = 2 n + t)
+  bf16x8 bsel;
+  {
+    const int dd = (lane & 15) - 4 * (lane >> 4);
+    const unsigned one2 = 0x3F803F80u;
+    const uint4 bw = make_uint4(dd == 0 ? one2 : 0u, dd == 1 ? one2 : 0u, dd == 2 ? one2 : 0u, dd == 3 ? one2 : 0u);
+    bsel = __builtin_bit_cast(bf16x8, bw);
+  }
   // b-e: the step's reads of index(s) / index(s+1) and its DMAs
   auto issue = [&](int s) {
     const int st1 = lds_i32(idx_blk(s + 1) + 4 * (lane >> 2)) >> 6;
@@ -241,50 +261,120 @@ __global__ void __launch_bounds__(WT) spmm_win_kernel(WinArgs a) {
       raw_barrier();
     }
 
+    if constexpr (MF) {
+      // Sums on v_mfma_f32_16x16x32_bf16 (wave = 16 degree-sorted rows x 32 columns):
+      //   D[m = column][n = row] += A[m][k] B[k][n],  k = 2 n + t (neighbour 2 j + t of row n)
+      // A: ds_read_b64_tr_b16 delivers to lane (gq, li) column li of four ring rows whose
+      //    addresses lanes 4 q + p of its 16-lane group supply -- two reads give the 8 k of
+      //    k-block gq: neighbours 2 j, 2 j + 1 of rows 4 gq + 0..3 of the group
+      // B: the constant 0/1 segment matrix (k -> its row), held in registers
+      // The plan pads every list (zero row) to the group's largest degree, so all 16
+      // rows run the same rounds; D accumulates over rounds in fp32 (products exact).
+      const int rg = w >> 1, chh = w & 1;
+      const int gq = lane >> 4, li = lane & 15, q = li >> 2, p4 = li & 3, par = q & 1;
+      const int r1 = 16 * rg + 4 * gq + (q >> 1);           // step-local rows of the two reads
+      auto slw = [&](int r) {
+        return reinterpret_cast<const uint4*>(lds + OFF_SL + (s & 1) * (16 * 512) + 512 * (r >> 3) + 64 * (r & 7));
+      };
+      const uint4* s1p = slw(r1);
+      const uint4* s2p = slw(r1 + 2);
+      const uint4 u0 = s1p[0], u1 = s1p[1], u2 = s1p[2], u3 = s1p[3];
+      const uint4 v0 = s2p[0], v1 = s2p[1], v2 = s2p[2], v3 = s2p[3];
+      const unsigned w1[16] = {u0.x, u0.y, u0.z, u0.w, u1.x, u1.y, u1.z, u1.w,
+                               u2.x, u2.y, u2.z, u2.w, u3.x, u3.y, u3.z, u3.w};
+      const unsigned w2[16] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w,
+                               v2.x, v2.y, v2.z, v2.w, v3.x, v3.y, v3.z, v3.w};
+      const int blk = OFF_IDX + (s & 3) * (16 * 96);
+      const int gdeg = __builtin_amdgcn_readfirstlane(lds_i32(blk + 96 * (2 * rg)) & 63);
+      const int nr = (a.dbg & 1) ? 0 : (min(gdeg, 32) + 1) >> 1;
+      const unsigned K = ((unsigned)chh << 6) | ((unsigned)p4 << 3);
+      const unsigned sh = 16u * (unsigned)par;
+      f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+      auto addr = [&](unsigned sl) { return (sl << 7) | (((sl << 4) & 0x60u) ^ K); };
+      auto tr = [&](unsigned off) {
+        return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s_t*)(lds + off));
+      };
+      auto round = [&](unsigned sa, unsigned sb) {
+        const unsigned a0 = addr(sa), b0 = addr(sb);
+        const v4s_t ra0 = tr(a0), rb0 = tr(b0), ra1 = tr(a0 ^ 32u), rb1 = tr(b0 ^ 32u);
+        const bf16x8 A0 = __builtin_bit_cast(bf16x8, (v8s_t)__builtin_shufflevector(ra0, rb0, 0, 1, 2, 3, 4, 5, 6, 7));
+        const bf16x8 A1 = __builtin_bit_cast(bf16x8, (v8s_t)__builtin_shufflevector(ra1, rb1, 0, 1, 2, 3, 4, 5, 6, 7));
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A0, bsel, acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A1, bsel, acc1, 0, 0, 0);
+      };
+      // rounds in pairs (lists are padded to 8 entries = 4 rounds): one uniform branch
+      // per pair, the pair's 8 transposed reads issued before its 4 MFMAs
+#pragma unroll
+      for (int jr = 0; jr < 16; jr += 2) {
+        if (jr < nr) {
+          round(__builtin_amdgcn_ubfe(w1[jr], sh, 16), __builtin_amdgcn_ubfe(w2[jr], sh, 16));
+          round(__builtin_amdgcn_ubfe(w1[jr + 1], sh, 16), __builtin_amdgcn_ubfe(w2[jr + 1], sh, 16));
+        }
+      }
+      if (gdeg > 32) {   // rows past 32 neighbours (rare): entries from the plan in HBM
+        const int m1 = lds_i32(blk + 96 * (r1 >> 3) + 4 * (r1 & 7));
+        const int m2 = lds_i32(blk + 96 * ((r1 + 2) >> 3) + 4 * ((r1 + 2) & 7));
+        for (int jr = 16; 2 * jr < gdeg; ++jr) {
+          const int k = 2 * jr + par;
+          const unsigned sa = k < (m1 & 63) ? (unsigned)a.slots[(long long)(m1 >> 6) * 8 + k] : (unsigned)ZROW;
+          const unsigned sb = k < (m2 & 63) ? (unsigned)a.slots[(long long)(m2 >> 6) * 8 + k] : (unsigned)ZROW;
+          round(sa, sb);
+        }
+      }
+      // lane (gq, li): columns 32 chh + 16 cb + 4 gq + 0..3 of the group's row li
+      const int orow = lds_i32(blk + 96 * (2 * rg + (li >> 3)) + 32 + 4 * (li & 7));
+      __bf16* op = a.out + (long long)orow * a.ldo + 32 * chh + 4 * gq;
+      bf16x4 o0, o1;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) { o0[e] = (__bf16)acc0[e]; o1[e] = (__bf16)acc1[e]; }
+      *reinterpret_cast<bf16x4*>(op) = o0;
+      *reinterpret_cast<bf16x4*>(op + 16) = o1;
+    } else {
     // sum the row's neighbours from the ring (colidx order, fp32).  The wave's 8 rows
-    // are one degree-sorted group and every list is padded with the zero row to the
-    // group's largest degree (exact +0 adds past a row's own degree): a chunk of GK
-    // reads is issued before the first add; the wave leaves the loop after the
-    // group's largest degree.  (Reads of the next chunk issued before the adds of
-    // the current one measured slower: 101 vs 96 us.)
-    const int m0 = lds_i32(idx_blk(s) + 4 * r8);
-    const int row0 = lds_i32(idx_blk(s) + 32 + 4 * r8);
-    const int deg = m0 & 63;
-    const uint4* slp = reinterpret_cast<const uint4*>(lds + sl_buf(s) + 64 * r8);
-    const uint4 sl[4] = {slp[0], slp[1], slp[2], slp[3]};
-    const unsigned sv[16] = {sl[0].x, sl[0].y, sl[0].z, sl[0].w, sl[1].x, sl[1].y, sl[1].z, sl[1].w,
-                             sl[2].x, sl[2].y, sl[2].z, sl[2].w, sl[3].x, sl[3].y, sl[3].z, sl[3].w};
-    float f[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) f[j] = 0.f;
-#pragma unroll
-    for (int k0 = 0; k0 < 32; k0 += GK) {
-      if (!__builtin_amdgcn_ballot_w64(deg > k0) || (a.dbg & 1)) break;
-      uint4 d[GK];
-#pragma unroll
-      for (int j = 0; j < GK; ++j) {
-        const int k = k0 + j;
-        d[j] = *reinterpret_cast<const uint4*>(lds + slot_addr(sv[k >> 1], k & 1, base));
+      // are one degree-sorted group and every list is padded with the zero row to the
+      // group's largest degree (exact +0 adds past a row's own degree): a chunk of GK
+      // reads is issued before the first add; the wave leaves the loop after the
+      // group's largest degree.  (Reads of the next chunk issued before the adds of
+      // the current one measured slower: 101 vs 96 us.)
+      const int m0 = lds_i32(idx_blk(s) + 4 * r8);
+      const int row0 = lds_i32(idx_blk(s) + 32 + 4 * r8);
+      const int deg = m0 & 63;
+      const uint4* slp = reinterpret_cast<const uint4*>(lds + sl_buf(s) + 64 * r8);
+      const uint4 sl[4] = {slp[0], slp[1], slp[2], slp[3]};
+      const unsigned sv[16] = {sl[0].x, sl[0].y, sl[0].z, sl[0].w, sl[1].x, sl[1].y, sl[1].z, sl[1].w,
+                               sl[2].x, sl[2].y, sl[2].z, sl[2].w, sl[3].x, sl[3].y, sl[3].z, sl[3].w};
+      float f[8];
+  #pragma unroll
+      for (int j = 0; j < 8; ++j) f[j] = 0.f;
+  #pragma unroll
+      for (int k0 = 0; k0 < 32; k0 += GK) {
+        if (!__builtin_amdgcn_ballot_w64(deg > k0) || (a.dbg & 1)) break;
+        uint4 d[GK];
+  #pragma unroll
+        for (int j = 0; j < GK; ++j) {
+          const int k = k0 + j;
+          d[j] = *reinterpret_cast<const uint4*>(lds + slot_addr(sv[k >> 1], k & 1, base));
+        }
+  #pragma unroll
+        for (int j = 0; j < GK; ++j) {
+          if constexpr (DOT) acc8_dot(f, d[j]);
+          else acc8(f, d[j]);
+        }
       }
-#pragma unroll
-      for (int j = 0; j < GK; ++j) {
-        if constexpr (DOT) acc8_dot(f, d[j]);
-        else acc8(f, d[j]);
+      if (__builtin_amdgcn_ballot_w64(deg > 32)) {   // rows past 32 neighbours (rare)
+        const int k0 = (m0 >> 6) * 8;
+        for (int k = 32; k < deg; ++k) {
+          const unsigned slot = a.slots[k0 + k];
+          const uint4 dv = *reinterpret_cast<const uint4*>(lds + slot * (WIDTH * 2) + base);
+          if constexpr (DOT) acc8_dot(f, dv);
+          else acc8(f, dv);
+        }
       }
-    }
-    if (__builtin_amdgcn_ballot_w64(deg > 32)) {   // rows past 32 neighbours (rare)
-      const int k0 = (m0 >> 6) * 8;
-      for (int k = 32; k < deg; ++k) {
-        const unsigned slot = a.slots[k0 + k];
-        const uint4 dv = *reinterpret_cast<const uint4*>(lds + slot * (WIDTH * 2) + base);
-        if constexpr (DOT) acc8_dot(f, dv);
-        else acc8(f, dv);
-      }
-    }
-    bf16x8 o;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) o[j] = (__bf16)f[j];
-    *reinterpret_cast<bf16x8*>(a.out + (long long)row0 * a.ldo + 8 * l8) = o;
+      bf16x8 o;
+  #pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = (__bf16)f[j];
+      *reinterpret_cast<bf16x8*>(a.out + (long long)row0 * a.ldo + 8 * l8) = o;    }
+
     // every wave's LDS reads of this step are done (their values were consumed)
     // before any wave's next DMA overwrites ring rows, index blocks or slot lists
     if (!one) raw_barrier();
@@ -322,12 +412,14 @@ extern "C" int snd_csr_spmm_bf16_window(const int* meta, const uint16_t* slots, 
             debug_flags() >> 16};
   const dim3 grid(n_graphs * a.spg);
   const hipStream_t st = (hipStream_t)stream;
-  if (a.dbg & 8) {
-    if (a.dbg & 16) hipLaunchKernelGGL((spmm_win_kernel<8, false>), grid, dim3(WT), 0, st, a);
-    else hipLaunchKernelGGL((spmm_win_kernel<8, true>), grid, dim3(WT), 0, st, a);
+  if (a.dbg & 64) {
+    hipLaunchKernelGGL((spmm_win_kernel<4, true, true>), grid, dim3(WT), 0, st, a);
+  } else if (a.dbg & 8) {
+    if (a.dbg & 16) hipLaunchKernelGGL((spmm_win_kernel<8, false, false>), grid, dim3(WT), 0, st, a);
+    else hipLaunchKernelGGL((spmm_win_kernel<8, true, false>), grid, dim3(WT), 0, st, a);
   } else {
-    if (a.dbg & 16) hipLaunchKernelGGL((spmm_win_kernel<4, false>), grid, dim3(WT), 0, st, a);
-    else hipLaunchKernelGGL((spmm_win_kernel<4, true>), grid, dim3(WT), 0, st, a);
+    if (a.dbg & 16) hipLaunchKernelGGL((spmm_win_kernel<4, false, false>), grid, dim3(WT), 0, st, a);
+    else hipLaunchKernelGGL((spmm_win_kernel<4, true, false>), grid, dim3(WT), 0, st, a);
   }
   SND_LAUNCH_CHECK("spmm_win_kernel");
   return 0;

@@ -271,15 +271,16 @@ def window_plan(batch: GraphBatch, order: np.ndarray, ring: int = 1096) -> Windo
     q = np.arange(R)
     blk = (q // n) * ((n + 127) // 128) + (q % n) // 128
     srt = np.lexsort((q, -deg, blk))
-    # a wavefront sums the 8 rows of one sorted group together up to their largest
-    # degree: every list is padded (with the ring's zero row, slot ``ring``) to its
-    # group's largest degree (at most the 32 entries the kernel stages), in 8s
+    # a wavefront sums the rows of one sorted group together up to their largest
+    # degree (16 rows on the MFMA sums, 8 on the VALU sums): every list is padded
+    # (with the ring's zero row, slot ``ring``) to its 16-row group's largest degree
+    # (at most the 32 entries the kernel stages), in 8s
     rank = np.empty(R, np.int64)
     bs = blk[srt]
     first = np.searchsorted(bs, bs, side="left")          # sorted index of the block's first row
     rank[srt] = np.arange(R) - first                       # rank of a position inside its block
     gfirst = np.empty(R, np.int64)
-    gfirst[srt] = first + (rank[srt] // 8) * 8             # sorted index of its group's first row
+    gfirst[srt] = first + (rank[srt] // 16) * 16           # sorted index of its group's first row
     gmax = deg[srt][gfirst] if R else deg
     pad = (np.maximum(deg, np.minimum(gmax, 32)) + 7) // 8 * 8
     start = np.zeros(R + 1, np.int64)

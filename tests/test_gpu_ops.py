@@ -169,6 +169,17 @@ def test_spmm_bf16_window_bitwise(n, B, kbar, seed):
         finally:
             _lib.check(_lib.lib().snd_debug_set(0))
         assert torch.equal(out2.view(torch.int16), ref.view(torch.int16))
+        # the MFMA sums (debug bit 64 << 16; swizzled ring, transposed reads): the same
+        # fp32 sums up to the MFMA's rounding of its two-product adds
+        _lib.check(_lib.lib().snd_debug_set(64 << 16))
+        try:
+            out3 = layers.spmm_bf16_window(layers.DeviceWindowPlan(wp), hb.cuda(), n, B)
+            torch.cuda.synchronize()
+        finally:
+            _lib.check(_lib.lib().snd_debug_set(0))
+        d = (out3.float() - ref.float()).abs()
+        assert int((out3.view(torch.int16) != ref.view(torch.int16)).sum()) <= 1e-4 * out3.numel()
+        assert float(d.max()) <= 2 ** -7 * float(ref.float().abs().max())
     if dense is not None:
         r64 = R.spmm(dense, hb.float().numpy().astype(np.float64), n)
         assert np.abs(out.float().cpu().numpy() - r64).max() <= 2 ** -7 * max(np.abs(r64).max(), 1.0)

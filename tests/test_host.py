@@ -218,7 +218,7 @@ def test_window_plan_matches_literal(n, B, kbar):
     positions in colidx order, then the zero row's slot 1096 up to its wavefront
     group's largest degree (at most 32), in 8s; meta = (start8 << 6) | degree,
     listed (with rows) by degree descending inside every aligned 128-position
-    block, a group = 8 consecutive rows of that listing."""
+    block, a group = 16 consecutive rows of that listing."""
     from snd_vae_amd.config import tscale
     from snd_vae_amd.data import locality_order, synthetic_batch, window_plan
     b = synthetic_batch(tscale(n, 16, mean_degree=kbar), B, seed=n)
@@ -235,7 +235,7 @@ def test_window_plan_matches_literal(n, B, kbar):
             key = sorted(qs, key=lambda q: (-deg[q], q))
             keys[(g, lo)] = (qs, key)
             for i, q in enumerate(key):
-                gmax[q] = deg[key[i - i % 8]]
+                gmax[q] = deg[key[i - i % 16]]
     start, beta = 0, 0
     meta = np.zeros(R, np.int64)
     for q in range(R):

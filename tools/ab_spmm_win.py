@@ -16,6 +16,7 @@ def main():
     ap.add_argument("--flags", default="0,8,1,2,4,6")
     ap.add_argument("--copies", type=int, default=32)
     ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--check", action="store_true")
     args = ap.parse_args()
     import numpy as np
     import torch
@@ -41,6 +42,22 @@ def main():
     out = torch.empty_like(h)
     L = _lib.lib()
     byts = 4 * (R + 1) + 4 * len(ci) + 2 * 2 * R * 64
+    if args.check:   # every flag's output against the register-gather kernel (fp32 sums in colidx order)
+        from snd_vae_amd import layers
+        ref = layers.spmm_bf16(torch.from_numpy(rp.astype(np.int32)).cuda(), torch.from_numpy(ci.astype(np.int32)).cuda(),
+                               h, host.n_nodes, ng, torch.from_numpy(order).cuda())
+        for f in [int(x) for x in args.flags.split(",")]:
+            _lib.check(L.snd_debug_set(f << 16))
+            out.zero_()
+            _lib.check(L.snd_csr_spmm_bf16_window(dw.meta.data_ptr(), dw.slots.data_ptr(), dw.rows.data_ptr(),
+                                                  dw.order.data_ptr(), R, host.n_nodes, ng, wp.beta, h.data_ptr(), 64, 64,
+                                                  out.data_ptr(), 64, _lib.stream_ptr()))
+            torch.cuda.synchronize()
+            neq = int((out.view(torch.int16) != ref.view(torch.int16)).sum())
+            d = (out.float() - ref.float()).abs()
+            print(f"check {f}: {neq} of {out.numel()} bf16 outputs differ, max |diff| {float(d.max()):.3e}, "
+                  f"max |ref| {float(ref.float().abs().max()):.3e}", flush=True)
+        _lib.check(L.snd_debug_set(0))
     for f in [int(x) for x in args.flags.split(",")]:
         _lib.check(L.snd_debug_set(f << 16))
         ms = bench.time_launches(lambda sp: _lib.check(L.snd_csr_spmm_bf16_window(
