@@ -275,6 +275,36 @@ int snd_sg_layer_bwd(const snd_sg_graph_t* g, const float* x, int ldx, int f, in
                      const float* dout, float* dx, int lddx, float* grads, void* workspace,
                      snd_stream_t stream);
 
+/* ---- §8f rank 4: disentangled-model pieces (not on the benchmarked path) -------
+ * e2e edge-to-edge filter of the structure decoder (layers.py:431-450), fp32:
+ *   out[b,i,j,o] = 2 b1[o] + sum_t sum_c w1[t,c,o] (x[b,i,j+t-p,c] + x[b,i+t-p,j,c])
+ * x [B, N, N, C] (NHWC), w1 [K, C, O] (the reference's [1, K, C, O] kernel; conv2
+ * uses its transpose [K, 1, C, O]: the same taps), TF SAME padding p = (K-1)/2;
+ * the decoder uses K = N (model.py:196).  Deterministic fixed-order sums. */
+int snd_e2e_fwd(const float* x, int n_graphs, int n, int c, const float* w1, const float* b1,
+                int k, int o, float* out, snd_stream_t stream);
+/* dx [B, N, N, C], dw1 [K, C, O], db1 [O] of sum(out * dout). */
+int snd_e2e_bwd(const float* x, int n_graphs, int n, int c, const float* w1, int k, int o,
+                const float* dout, float* dx, float* dw1, float* db1, snd_stream_t stream);
+/* Latent regularisers of one latent group (optimizer.py:7-58,159-190), mu / logstd /
+ * z [batch, latent] fp32:
+ *   term = w_kl kl  (cap_gamma > 0: cap_gamma relu(kl - cap_c), 'disentangled_C')
+ *        + w_dip DIP(mu; lambda_od, lambda_d) + w_tc TC(z, mu, logstd)
+ * kl = -0.5 mean(1 + 2s - mu^2 - e^{2s}) (optimizer.py:160); DIP optimizer.py:7-21;
+ * TC the minibatch estimate of optimizer.py:29-58 (logvar = 2 logstd).  Writes
+ * dmu / dlogstd = d term / d (mu, logstd) including the path through
+ * z = mu + eps e^{logstd} (model.py:155-159), and out[4] (double) =
+ * {kl, term, DIP, TC}.  One workgroup: sized for the reference's batches (<= a few
+ * hundred latents).  workspace >= snd_latent_reg_workspace(batch, latent) bytes
+ * when w_dip or w_tc is nonzero. */
+typedef struct {
+  float w_kl, cap_gamma, cap_c, w_dip, lambda_od, lambda_d, w_tc;
+} snd_latent_reg_t;
+size_t snd_latent_reg_workspace(int batch, int latent);
+int snd_latent_reg(const float* mu, const float* logstd, const float* z, int batch, int latent,
+                   const snd_latent_reg_t* w, float* dmu, float* dlogstd, double* out,
+                   void* workspace, snd_stream_t stream);
+
 /* ---- a14: the whole train step (main.py:315-334) ---------------------------
  * A plan fixes shapes; the step runs forward + backward of the SND-VAE
  * (SURVEY §8 "Composed step") for one batch in either decoder-input topology:

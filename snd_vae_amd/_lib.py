@@ -55,6 +55,11 @@ class Batch(C.Structure):
                 ("tiles", RowTiles)]
 
 
+class LatentReg(C.Structure):
+    """snd_latent_reg_t (include/snd_vae.h)."""
+    _fields_ = [(k, c_float) for k in ("w_kl", "cap_gamma", "cap_c", "w_dip", "lambda_od", "lambda_d", "w_tc")]
+
+
 # name -> (restype, argtypes)
 _SIGS = {
     "snd_last_error": (C.c_char_p, []),
@@ -95,6 +100,10 @@ _SIGS = {
                                  c_int, vp, vp, vp, vp]),
     "snd_sg_layer_bwd": (c_int, [C.POINTER(SGGraph), vp, c_int, c_int, c_int, c_int, c_int, vp,
                                  c_int, vp, vp, vp, c_int, vp, vp, vp]),
+    "snd_e2e_fwd": (c_int, [vp, c_int, c_int, c_int, vp, vp, c_int, c_int, vp, vp]),
+    "snd_e2e_bwd": (c_int, [vp, c_int, c_int, c_int, vp, c_int, c_int, vp, vp, vp, vp, vp]),
+    "snd_latent_reg_workspace": (c_size, [c_int, c_int]),
+    "snd_latent_reg": (c_int, [vp, vp, vp, c_int, c_int, C.POINTER(LatentReg), vp, vp, vp, vp, vp]),
     "snd_plan_create": (c_int, [C.POINTER(Config), c_int, C.POINTER(vp)]),
     "snd_plan_destroy": (None, [vp]),
     "snd_plan_param_count": (c_ll, [vp]),
