@@ -286,6 +286,31 @@ int snd_e2e_fwd(const float* x, int n_graphs, int n, int c, const float* w1, con
 /* dx [B, N, N, C], dw1 [K, C, O], db1 [O] of sum(out * dout). */
 int snd_e2e_bwd(const float* x, int n_graphs, int n, int c, const float* w1, int k, int o,
                 const float* dout, float* dx, float* dw1, float* db1, snd_stream_t stream);
+/* The e2e structure decoder around the filters (model.py:193-208), fp32, frozen
+ * Keras BN (y' = gamma y / sqrt(1.001) + beta) then relu:
+ *   snd_e2e_pair_fwd: x0[b,i,j,:] = relu(BN0([z_i | z_j]))  (z [B, N, D] -> x0 [B, N, N, 2D])
+ *   snd_bn_relu_fwd:  x = relu(BN(y)), y [rows, c]           (between e2e layers)
+ *   snd_e2e_head_ce:  logits = relu(BN_adj(y)) W + b (d_e_lin2, W [c][2]), the diagonal
+ *                     set to (1, 0) (model.py:200-203), CE against [1 - A, A] summed
+ *                     over B N^2 (optimizer.py:142-144) into out[0], argmax == A count
+ *                     (main.py:334) into out[1]; gradients of the MEAN CE: dy, dW, db,
+ *                     dgamma, dbeta (c <= 32; adj dense [B, N, N] 0/1 floats)
+ *   snd_bn_relu_bwd / snd_e2e_pair_bwd: the matching backward passes (per-channel
+ *                     gamma / beta gradients in fixed order; the pair backward needs
+ *                     snd_e2e_pair_bwd_workspace bytes). */
+int snd_e2e_pair_fwd(const float* z, int n_graphs, int n, int d, const float* gamma, const float* beta,
+                     float* x, snd_stream_t stream);
+size_t snd_e2e_pair_bwd_workspace(int n_graphs, int n, int d);
+int snd_e2e_pair_bwd(const float* dx0, const float* z, int n_graphs, int n, int d, const float* gamma,
+                     const float* beta, float* dz, float* dgamma, float* dbeta, void* workspace,
+                     snd_stream_t stream);
+int snd_bn_relu_fwd(const float* y, long long rows, int c, const float* gamma, const float* beta, float* x,
+                    snd_stream_t stream);
+int snd_bn_relu_bwd(const float* dx, const float* y, long long rows, int c, const float* gamma,
+                    const float* beta, float* dy, float* dgamma, float* dbeta, snd_stream_t stream);
+int snd_e2e_head_ce(const float* y, const float* adj, int n_graphs, int n, int c, const float* gamma,
+                    const float* beta, const float* w, const float* b, float* dy, float* dw, float* db,
+                    float* dgamma, float* dbeta, double* out, snd_stream_t stream);
 /* Latent regularisers of one latent group (optimizer.py:7-58,159-190), mu / logstd /
  * z [batch, latent] fp32:
  *   term = w_kl kl  (cap_gamma > 0: cap_gamma relu(kl - cap_c), 'disentangled_C')

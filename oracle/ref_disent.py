@@ -159,3 +159,41 @@ def model_type_groups(model_type, beta=1.0, gamma=1.0, c=0.0):
         return {"s": {"w_kl": beta, "w_tc": 10.0}, "g": {"w_kl": beta, "w_tc": 10.0},
                 "sg": {"w_kl": beta, "w_tc": 10.0}}
     return {"sg": {"w_kl": beta}}                               # 'base' (optimizer.py:186-188)
+
+
+# ---------------------------------------------------------------- e2e structure decoder
+BN_C = 1.0 / np.sqrt(1.0 + 1e-3)
+
+
+def structure_decoder_torch(z, adj, layers, head):
+    """model.py:193-208 + optimizer.py:142-144 literally, torch float64 (autograd-ready):
+    pairwise concat [z_i | z_j], per layer e2e(relu(BN(h))), relu(BN(h)) @ W + b, the
+    diagonal set to (1, 0), mean softmax-CE against [1 - A, A]; returns (ce, correct)."""
+    import torch
+    B, N, D = z.shape
+    h = torch.cat([z[:, :, None, :].expand(B, N, N, D), z[:, None, :, :].expand(B, N, N, D)], -1)
+    for lay in layers:
+        h = e2e_torch(torch.relu(lay["gamma"] * h * BN_C + lay["beta"]), lay["w"], lay["b"])
+    logits = torch.relu(head["gamma"] * h * BN_C + head["beta"]) @ head["w"] + head["b"]
+    diag = 1.0 - torch.eye(N, dtype=logits.dtype)[None]
+    p1 = diag * logits[..., 1]
+    p0 = diag * logits[..., 0] + (1.0 - diag)
+    prob = torch.stack([p0, p1], -1)
+    a = torch.as_tensor(adj, dtype=logits.dtype)
+    labels = torch.stack([1.0 - a, a], -1)
+    ce = torch.mean(torch.logsumexp(prob, -1) - (labels * prob).sum(-1))
+    correct = float(((p1 > p0).to(a.dtype) == a).sum())
+    return ce, correct
+
+
+def structure_decoder_grads(z, adj, layers, head):
+    """(ce, correct, dz, layer grads, head grads) by torch autograd, float64."""
+    import torch
+    t = lambda a: torch.tensor(np.asarray(a, np.float64), requires_grad=True)
+    zt = t(z)
+    lt = [{k: t(v) for k, v in lay.items()} for lay in layers]
+    ht = {k: t(v) for k, v in head.items()}
+    ce, correct = structure_decoder_torch(zt, adj, lt, ht)
+    ce.backward()
+    g = lambda d: {k: v.grad.numpy() for k, v in d.items()}
+    return float(ce.detach()), correct, zt.grad.numpy(), [g(l) for l in lt], g(ht)

@@ -102,6 +102,12 @@ _SIGS = {
                                  c_int, vp, vp, vp, c_int, vp, vp, vp]),
     "snd_e2e_fwd": (c_int, [vp, c_int, c_int, c_int, vp, vp, c_int, c_int, vp, vp]),
     "snd_e2e_bwd": (c_int, [vp, c_int, c_int, c_int, vp, c_int, c_int, vp, vp, vp, vp, vp]),
+    "snd_e2e_pair_fwd": (c_int, [vp, c_int, c_int, c_int, vp, vp, vp, vp]),
+    "snd_e2e_pair_bwd_workspace": (c_size, [c_int, c_int, c_int]),
+    "snd_e2e_pair_bwd": (c_int, [vp, vp, c_int, c_int, c_int, vp, vp, vp, vp, vp, vp, vp]),
+    "snd_bn_relu_fwd": (c_int, [vp, c_ll, c_int, vp, vp, vp, vp]),
+    "snd_bn_relu_bwd": (c_int, [vp, vp, c_ll, c_int, vp, vp, vp, vp, vp, vp]),
+    "snd_e2e_head_ce": (c_int, [vp, vp, c_int, c_int, c_int, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]),
     "snd_latent_reg_workspace": (c_size, [c_int, c_int]),
     "snd_latent_reg": (c_int, [vp, vp, vp, c_int, c_int, C.POINTER(LatentReg), vp, vp, vp, vp, vp]),
     "snd_plan_create": (c_int, [C.POINTER(Config), c_int, C.POINTER(vp)]),

@@ -22,6 +22,7 @@
 // (model.py:155-159): d mu += dz, d s += dz (z - mu).
 #include "snd_common.hpp"
 
+#include <algorithm>
 #include <cmath>
 
 namespace snd {
@@ -121,6 +122,7 @@ __global__ void __launch_bounds__(ET) e2e_bwd_w_kernel(const float* x, const flo
 // ---------------------------------------------------------------- latent regularisers
 constexpr int RT = 1024;
 
+template <int NT = RT>
 __device__ double block_sum_d(double v, double* sh) {
   v = wave_sum_d(v);
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -128,7 +130,7 @@ __device__ double block_sum_d(double v, double* sh) {
   if (lane == 0) sh[w] = v;
   __syncthreads();
   double t = 0.0;
-  for (int k = 0; k < RT / 64; ++k) t += sh[k];
+  for (int k = 0; k < NT / 64; ++k) t += sh[k];
   return t;
 }
 
@@ -279,6 +281,175 @@ __global__ void __launch_bounds__(RT) latent_reg_kernel(RegArgs a) {
   }
 }
 
+// ---------------------------------------------------------------- e2e structure decoder
+// model.py:193-208 around the e2e filters, [B, N, N, *] NHWC fp32, frozen Keras BN
+// y' = gamma c y + beta (c = 1/sqrt(1.001)) followed by relu:
+//   pair:  x0[b,i,j,c] = relu(BN0([z_i | z_j])[c])        (model.py:193-195, loop head)
+//   layer: x = relu(BN(y))                                (model.py:197-198)
+//   head:  logits = relu(BN_adj(y)) W + b (d_e_lin2), the diagonal set to (1, 0)
+//          (model.py:200-203); CE against [1 - A, A] (optimizer.py:142-144), mean over B N^2
+__global__ void __launch_bounds__(ET) pair_bn_relu_kernel(const float* z, int B, int N, int D, const float* g,
+                                                          const float* be, float* x) {
+  const long long idx = (long long)blockIdx.x * ET + threadIdx.x;
+  const int C2 = 2 * D;
+  if (idx >= (long long)B * N * N * C2) return;
+  const int c = (int)(idx % C2);
+  const long long r = idx / C2;
+  const int j = (int)(r % N), i = (int)((r / N) % N), b = (int)(r / ((long long)N * N));
+  const float v = c < D ? z[((long long)b * N + i) * D + c] : z[((long long)b * N + j) * D + c - D];
+  x[idx] = fmaxf(g[c] * kBnC * v + be[c], 0.f);
+}
+
+__global__ void __launch_bounds__(ET) bn_relu_kernel(const float* y, long long rows, int C, const float* g,
+                                                     const float* be, float* x) {
+  const long long idx = (long long)blockIdx.x * ET + threadIdx.x;
+  if (idx >= rows * C) return;
+  const int c = (int)(idx % C);
+  x[idx] = fmaxf(g[c] * kBnC * y[idx] + be[c], 0.f);
+}
+
+// d (relu(BN(y))) -> dy, and per channel dgamma = sum dt c y, dbeta = sum dt: one
+// workgroup per channel, fixed-order tree
+__global__ void __launch_bounds__(ET) bn_relu_bwd_kernel(const float* dx, const float* y, long long rows, int C,
+                                                         const float* g, const float* be, float* dy, float* dg,
+                                                         float* db) {
+  __shared__ float r1[ET], r2[ET];
+  const int c = blockIdx.x;
+  float sg = 0.f, sb = 0.f;
+  for (long long r = threadIdx.x; r < rows; r += ET) {
+    const long long e = r * C + c;
+    const float t = g[c] * kBnC * y[e] + be[c];
+    const float dt = t > 0.f ? dx[e] : 0.f;
+    dy[e] = dt * g[c] * kBnC;
+    sg = fmaf(dt, kBnC * y[e], sg);
+    sb += dt;
+  }
+  r1[threadIdx.x] = sg;
+  r2[threadIdx.x] = sb;
+  __syncthreads();
+  for (int h = ET / 2; h > 0; h >>= 1) {
+    if ((int)threadIdx.x < h) { r1[threadIdx.x] += r1[threadIdx.x + h]; r2[threadIdx.x] += r2[threadIdx.x + h]; }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) { dg[c] = r1[0]; db[c] = r2[0]; }
+}
+
+// pair stage backward: one workgroup per (b, channel c of z's 2D): dgamma/dbeta partial
+// over the graph's N^2 pairs and dz (row part: sum over j; column part: sum over i)
+__global__ void __launch_bounds__(ET) pair_bwd_kernel(const float* dx0, const float* z, int B, int N, int D,
+                                                      const float* g, const float* be, float* dz, float* pg,
+                                                      float* pb) {
+  __shared__ float r1[ET], r2[ET];
+  const int C2 = 2 * D;
+  const int b = blockIdx.x / C2, c = blockIdx.x - b * C2;
+  const int d = c < D ? c : c - D;
+  float sg = 0.f, sb = 0.f;
+  // dz[b, n, d] (this channel's half): thread n-strided, sum over the partner index
+  for (int n = threadIdx.x; n < N; n += ET) {
+    float acc = 0.f;
+    const float v = z[((long long)b * N + n) * D + d];
+    const float t = g[c] * kBnC * v + be[c];
+    for (int m = 0; m < N; ++m) {
+      const long long e = c < D ? ((((long long)b * N + n) * N + m) * C2 + c) : ((((long long)b * N + m) * N + n) * C2 + c);
+      const float dt = t > 0.f ? dx0[e] : 0.f;
+      acc += dt;
+    }
+    // every pair holding z[b, n, d] in channel c has the same pre-activation t
+    const float dzc = acc * g[c] * kBnC;
+    sg = fmaf(acc, kBnC * v, sg);
+    sb += acc;
+    if (c < D) dz[((long long)b * N + n) * D + d] = dzc;
+    else pg[(long long)B * C2 * 2 + ((long long)b * N + n) * D + d] = dzc;   // column half, added below
+  }
+  r1[threadIdx.x] = sg;
+  r2[threadIdx.x] = sb;
+  __syncthreads();
+  for (int h = ET / 2; h > 0; h >>= 1) {
+    if ((int)threadIdx.x < h) { r1[threadIdx.x] += r1[threadIdx.x + h]; r2[threadIdx.x] += r2[threadIdx.x + h]; }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) { pg[(long long)b * C2 + c] = r1[0]; pb[(long long)b * C2 + c] = r2[0]; }
+}
+
+// dz += column halves; dgamma0 / dbeta0 = sum over graphs (fixed order)
+__global__ void __launch_bounds__(ET) pair_bwd_finish_kernel(float* dz, int B, int N, int D, const float* pg,
+                                                             const float* pb, float* dg, float* db) {
+  const long long idx = (long long)blockIdx.x * ET + threadIdx.x;
+  const int C2 = 2 * D;
+  if (idx < (long long)B * N * D) dz[idx] += pg[(long long)B * C2 * 2 + idx];
+  if (idx < C2) {
+    float sg = 0.f, sb = 0.f;
+    for (int b = 0; b < B; ++b) { sg += pg[(long long)b * C2 + idx]; sb += pb[(long long)b * C2 + idx]; }
+    dg[idx] = sg;
+    db[idx] = sb;
+  }
+}
+
+// head: one workgroup walks every (b, i, j); out: [0] CE sum (double), [1] correct
+// count; dy [rows, C] and the reduced grads dW [C][2], db [2], dgamma [C], dbeta [C]
+constexpr int HC = 32;   // head input channels at most
+constexpr int HT = 256;   // head threads (32-channel register arrays per thread)
+__global__ void __launch_bounds__(HT) e2e_head_kernel(const float* y, const float* adj, int B, int N, int C,
+                                                      const float* g, const float* be, const float* W,
+                                                      const float* bl, float* dy, float* dW, float* dbl,
+                                                      float* dg, float* dbe, double* out) {
+  __shared__ double sh[HT / 64];
+  const long long rows = (long long)B * N * N;
+  const float invM = 1.f / (float)rows;
+  float aW[HC][2], aG[HC], aB[HC], ab0 = 0.f, ab1 = 0.f;
+#pragma unroll
+  for (int k = 0; k < HC; ++k) { aW[k][0] = aW[k][1] = aG[k] = aB[k] = 0.f; }
+  double ce = 0.0, cnt = 0.0;
+  for (long long e = threadIdx.x; e < rows; e += HT) {
+    const int j = (int)(e % N), i = (int)((e / N) % N);
+    const float A = adj[e];
+    float x[HC], t[HC];
+    float l0 = bl[0], l1 = bl[1];
+#pragma unroll
+    for (int k = 0; k < HC; ++k) {
+      if (k < C) {
+        t[k] = g[k] * kBnC * y[e * C + k] + be[k];
+        x[k] = fmaxf(t[k], 0.f);
+        l0 = fmaf(x[k], W[2 * k], l0);
+        l1 = fmaf(x[k], W[2 * k + 1], l1);
+      }
+    }
+    const bool dg_ = i == j;
+    if (dg_) { l0 = 1.f; l1 = 0.f; }
+    const float mx = fmaxf(l0, l1);
+    const float lse = mx + logf(expf(l0 - mx) + expf(l1 - mx));
+    ce += (double)(lse - (1.f - A) * l0 - A * l1);
+    cnt += (double)(((l1 > l0) ? 1.f : 0.f) == A);
+    const float p1 = expf(l1 - lse), p0 = expf(l0 - lse);
+    const float d0 = dg_ ? 0.f : (p0 - (1.f - A)) * invM, d1 = dg_ ? 0.f : (p1 - A) * invM;
+    ab0 += d0;
+    ab1 += d1;
+#pragma unroll
+    for (int k = 0; k < HC; ++k) {
+      if (k < C) {
+        aW[k][0] = fmaf(x[k], d0, aW[k][0]);
+        aW[k][1] = fmaf(x[k], d1, aW[k][1]);
+        const float dx = d0 * W[2 * k] + d1 * W[2 * k + 1];
+        const float dt = t[k] > 0.f ? dx : 0.f;
+        dy[e * C + k] = dt * g[k] * kBnC;
+        aG[k] = fmaf(dt, kBnC * y[e * C + k], aG[k]);
+        aB[k] += dt;
+      }
+    }
+  }
+  const double ces = block_sum_d<HT>(ce, sh), cnts = block_sum_d<HT>(cnt, sh);
+#pragma unroll
+  for (int k = 0; k < HC; ++k) {
+    if (k < C) {   // uniform
+      const double w0 = block_sum_d<HT>(aW[k][0], sh), w1 = block_sum_d<HT>(aW[k][1], sh);
+      const double gg = block_sum_d<HT>(aG[k], sh), bb = block_sum_d<HT>(aB[k], sh);
+      if (threadIdx.x == 0) { dW[2 * k] = (float)w0; dW[2 * k + 1] = (float)w1; dg[k] = (float)gg; dbe[k] = (float)bb; }
+    }
+  }
+  const double s0 = block_sum_d<HT>(ab0, sh), s1 = block_sum_d<HT>(ab1, sh);
+  if (threadIdx.x == 0) { dbl[0] = (float)s0; dbl[1] = (float)s1; out[0] = ces; out[1] = cnts; }
+}
+
 }  // namespace
 }  // namespace snd
 
@@ -326,5 +497,66 @@ extern "C" int snd_latent_reg(const float* mu, const float* logstd, const float*
             w->lambda_d, w->w_tc, dmu, dlogstd, out, (float*)workspace};
   hipLaunchKernelGGL(latent_reg_kernel, dim3(1), dim3(RT), 0, (hipStream_t)stream, a);
   SND_LAUNCH_CHECK("latent_reg_kernel");
+  return 0;
+}
+
+extern "C" int snd_e2e_pair_fwd(const float* z, int n_graphs, int n, int d, const float* gamma, const float* beta,
+                                float* x, snd_stream_t stream) {
+  SND_CHECK_ARG(z && gamma && beta && x && n_graphs > 0 && n > 0 && d > 0, "snd_e2e_pair_fwd: bad arguments");
+  const long long total = (long long)n_graphs * n * n * 2 * d;
+  hipLaunchKernelGGL(pair_bn_relu_kernel, dim3((unsigned)((total + ET - 1) / ET)), dim3(ET), 0, (hipStream_t)stream,
+                     z, n_graphs, n, d, gamma, beta, x);
+  SND_LAUNCH_CHECK("pair_bn_relu_kernel");
+  return 0;
+}
+
+extern "C" size_t snd_e2e_pair_bwd_workspace(int n_graphs, int n, int d) {
+  return 4 * ((size_t)n_graphs * 2 * d * 2 + (size_t)n_graphs * n * d);
+}
+
+extern "C" int snd_e2e_pair_bwd(const float* dx0, const float* z, int n_graphs, int n, int d, const float* gamma,
+                                const float* beta, float* dz, float* dgamma, float* dbeta, void* workspace,
+                                snd_stream_t stream) {
+  SND_CHECK_ARG(dx0 && z && gamma && beta && dz && dgamma && dbeta && workspace && n_graphs > 0 && n > 0 && d > 0,
+                "snd_e2e_pair_bwd: bad arguments");
+  float* pg = (float*)workspace;
+  float* pb = pg + (long long)n_graphs * 2 * d;
+  hipLaunchKernelGGL(pair_bwd_kernel, dim3((unsigned)(n_graphs * 2 * d)), dim3(ET), 0, (hipStream_t)stream,
+                     dx0, z, n_graphs, n, d, gamma, beta, dz, pg, pb);
+  SND_LAUNCH_CHECK("pair_bwd_kernel");
+  const long long cnt = std::max<long long>((long long)n_graphs * n * d, 2LL * d);
+  hipLaunchKernelGGL(pair_bwd_finish_kernel, dim3((unsigned)((cnt + ET - 1) / ET)), dim3(ET), 0, (hipStream_t)stream,
+                     dz, n_graphs, n, d, pg, pb, dgamma, dbeta);
+  SND_LAUNCH_CHECK("pair_bwd_finish_kernel");
+  return 0;
+}
+
+extern "C" int snd_bn_relu_fwd(const float* y, long long rows, int c, const float* gamma, const float* beta, float* x,
+                               snd_stream_t stream) {
+  SND_CHECK_ARG(y && gamma && beta && x && rows > 0 && c > 0, "snd_bn_relu_fwd: bad arguments");
+  hipLaunchKernelGGL(bn_relu_kernel, dim3((unsigned)((rows * c + ET - 1) / ET)), dim3(ET), 0, (hipStream_t)stream,
+                     y, rows, c, gamma, beta, x);
+  SND_LAUNCH_CHECK("bn_relu_kernel");
+  return 0;
+}
+
+extern "C" int snd_bn_relu_bwd(const float* dx, const float* y, long long rows, int c, const float* gamma,
+                               const float* beta, float* dy, float* dgamma, float* dbeta, snd_stream_t stream) {
+  SND_CHECK_ARG(dx && y && gamma && beta && dy && dgamma && dbeta && rows > 0 && c > 0, "snd_bn_relu_bwd: bad arguments");
+  hipLaunchKernelGGL(bn_relu_bwd_kernel, dim3((unsigned)c), dim3(ET), 0, (hipStream_t)stream, dx, y, rows, c, gamma,
+                     beta, dy, dgamma, dbeta);
+  SND_LAUNCH_CHECK("bn_relu_bwd_kernel");
+  return 0;
+}
+
+extern "C" int snd_e2e_head_ce(const float* y, const float* adj, int n_graphs, int n, int c, const float* gamma,
+                               const float* beta, const float* w, const float* b, float* dy, float* dw, float* db,
+                               float* dgamma, float* dbeta, double* out, snd_stream_t stream) {
+  SND_CHECK_ARG(y && adj && gamma && beta && w && b && dy && dw && db && dgamma && dbeta && out,
+                "snd_e2e_head_ce: null operand");
+  SND_CHECK_ARG(n_graphs > 0 && n > 0 && c > 0 && c <= HC, "snd_e2e_head_ce: channels must be in [1, %d]", HC);
+  hipLaunchKernelGGL(e2e_head_kernel, dim3(1), dim3(HT), 0, (hipStream_t)stream, y, adj, n_graphs, n, c, gamma,
+                     beta, w, b, dy, dw, db, dgamma, dbeta, out);
+  SND_LAUNCH_CHECK("e2e_head_kernel");
   return 0;
 }

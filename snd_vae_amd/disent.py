@@ -125,3 +125,68 @@ def disentangled_cost(model_type: str, groups: Dict[str, tuple], mse: Dict[str, 
     if model_type == "base":
         return [cost, mse["spatial_cost"], mse["adj_cost"], mse["node_cost"], kls["sg"]], grads
     return [cost, mse["spatial_cost"], mse["adj_cost"], mse["node_cost"], kls["g"], kls["s"], kls["sg"]], grads
+
+
+def _bn_relu(y, g, b):
+    rows, c = y.numel() // y.shape[-1], y.shape[-1]
+    x = torch.empty_like(y)
+    _lib.check(_lib.lib().snd_bn_relu_fwd(_P(y), rows, c, _P(g), _P(b), _P(x), _lib.stream_ptr()), "snd_bn_relu_fwd")
+    return x
+
+
+def structure_decoder(z, adj, layers, head):
+    """The e2e structure decoder of `model.py:193-208` with the CE of `optimizer.py:142-144`,
+    forward and backward in one call.
+
+    z [B, N, D] (z_sg_g), adj [B, N, N] 0/1 (adj_truth); layers: per e2e layer i a dict
+    {gamma, beta (d_bn_e[i], over its input channels), w [N, Cin, Cout], b [Cout]};
+    head: {gamma, beta (decoder_adj), w [Cin, 2], b [2]} (d_e_lin2).  Returns
+    (adj_cost = mean CE over B N^2, correct = #(argmax == A) (main.py:334), dz,
+    grads: a list of per-layer dicts and the head dict, same keys as the inputs)."""
+    B, N, D = z.shape
+    _f32(z, "structure_decoder z")
+    _f32(adj, "structure_decoder adj")
+    L_ = _lib.lib()
+    sp = _lib.stream_ptr()
+    # forward: x0 = relu(BN0(pair(z))), y_{i+1} = e2e(x_i), x_i = relu(BN_i(y_i))
+    x = torch.empty(B, N, N, 2 * D, device=z.device, dtype=torch.float32)
+    l0 = layers[0]
+    _lib.check(L_.snd_e2e_pair_fwd(_P(z), B, N, D, _P(l0["gamma"]), _P(l0["beta"]), _P(x), sp), "snd_e2e_pair_fwd")
+    xs, ys = [x], []
+    for i, lay in enumerate(layers):
+        y = e2e(xs[-1], lay["w"], lay["b"])
+        ys.append(y)
+        if i + 1 < len(layers):
+            nxt = layers[i + 1]
+            xs.append(_bn_relu(y, nxt["gamma"], nxt["beta"]))
+    yl = ys[-1]
+    c = yl.shape[-1]
+    dy = torch.empty_like(yl)
+    hg = {k: torch.empty_like(v) for k, v in head.items()}
+    out = torch.empty(2, device=z.device, dtype=torch.float64)
+    _lib.check(L_.snd_e2e_head_ce(_P(yl), _P(adj), B, N, c, _P(head["gamma"]), _P(head["beta"]), _P(head["w"]),
+                                  _P(head["b"]), _P(dy), _P(hg["w"]), _P(hg["b"]), _P(hg["gamma"]), _P(hg["beta"]),
+                                  _P(out), sp), "snd_e2e_head_ce")
+    # backward
+    grads = [dict() for _ in layers]
+    for i in range(len(layers) - 1, -1, -1):
+        dx, grads[i]["w"], grads[i]["b"] = e2e_bwd(xs[i], layers[i]["w"], dy)
+        if i > 0:
+            lay = layers[i]
+            dy = torch.empty_like(ys[i - 1])
+            grads[i]["gamma"] = torch.empty_like(lay["gamma"])
+            grads[i]["beta"] = torch.empty_like(lay["beta"])
+            rows, cc = ys[i - 1].numel() // ys[i - 1].shape[-1], ys[i - 1].shape[-1]
+            _lib.check(L_.snd_bn_relu_bwd(_P(dx), _P(ys[i - 1]), rows, cc, _P(lay["gamma"]), _P(lay["beta"]), _P(dy),
+                                          _P(grads[i]["gamma"]), _P(grads[i]["beta"]), sp), "snd_bn_relu_bwd")
+        else:
+            dz = torch.empty_like(z)
+            grads[0]["gamma"] = torch.empty_like(l0["gamma"])
+            grads[0]["beta"] = torch.empty_like(l0["beta"])
+            ws = torch.empty(int(L_.snd_e2e_pair_bwd_workspace(B, N, D)) // 4 + 1, device=z.device,
+                             dtype=torch.float32)
+            _lib.check(L_.snd_e2e_pair_bwd(_P(dx), _P(z), B, N, D, _P(l0["gamma"]), _P(l0["beta"]), _P(dz),
+                                           _P(grads[0]["gamma"]), _P(grads[0]["beta"]), _P(ws), sp),
+                       "snd_e2e_pair_bwd")
+    o = out.cpu().tolist()
+    return o[0] / (B * N * N), o[1], dz, grads, hg

@@ -8,7 +8,7 @@ import numpy as np
 import pytest
 import torch
 
-from oracle import ref_disent as D
+from oracle import ref_disent as RD
 
 pytestmark = pytest.mark.gpu
 
@@ -36,10 +36,10 @@ def test_e2e_fwd_bwd(B, N, C, O):
     w = (0.02 * rng.standard_normal((N, C, O))).astype(np.float32)   # truncated_normal(0.02), layers.py:434
     b = rng.standard_normal(O).astype(np.float32)
     out = disent.e2e(cu(x), cu(w), cu(b)).cpu().numpy()
-    assert rel(out, D.e2e(x, w, b)) < 1e-5
+    assert rel(out, RD.e2e(x, w, b)) < 1e-5
     dout = rng.standard_normal(out.shape).astype(np.float32)
     dx, dw, db = disent.e2e_bwd(cu(x), cu(w), cu(dout))
-    rx, rw, rb = D.e2e_grads(x, w, b, dout)
+    rx, rw, rb = RD.e2e_grads(x, w, b, dout)
     assert rel(dx.cpu().numpy(), rx) < 1e-5
     assert rel(dw.cpu().numpy(), rw) < 1e-5
     assert rel(db.cpu().numpy(), rb) < 1e-5
@@ -66,8 +66,8 @@ def test_latent_reg(B, L, name, kw):
     # the oracle with the sample exactly as the kernel sees it: eps' = (z - mu) e^-s
     eps64 = (z.astype(np.float64) - mu) * np.exp(-s.astype(np.float64))
     v, dmu, ds = disent.latent_reg(cu(mu), cu(s), cu(z), **kw)
-    ref = D.group_reg(mu, s, z, **kw)
-    val, rdmu, rds = D.group_reg_torch(mu, s, eps64, **kw)
+    ref = RD.group_reg(mu, s, z, **kw)
+    val, rdmu, rds = RD.group_reg_torch(mu, s, eps64, **kw)
     assert v["kl"] == pytest.approx(ref["kl"], rel=1e-6, abs=1e-9)
     assert v["term"] == pytest.approx(ref["term"], rel=1e-5, abs=1e-7)
     assert v["term"] == pytest.approx(val, rel=1e-5, abs=1e-7)
@@ -91,15 +91,51 @@ def test_disentangled_cost_overall_loss(mt):
         groups[g] = (cu(mu), cu(s), cu(z))
         ref_groups[g] = (mu, s, z)
     mse = {"spatial_cost": 0.08, "adj_cost": 0.7, "node_cost": 0.09}
-    c = D.capacity(5500, 25.0, 1000, 100000)
+    c = RD.capacity(5500, 25.0, 1000, 100000)
     loss, grads = disent.disentangled_cost(mt, groups, mse, beta=1.5, gamma=2.0, c=c)
-    w = D.model_type_groups(mt, 1.5, 2.0, c)
-    reg = sum(D.group_reg(*ref_groups[g], **kw)["term"] for g, kw in w.items())
+    w = RD.model_type_groups(mt, 1.5, 2.0, c)
+    reg = sum(RD.group_reg(*ref_groups[g], **kw)["term"] for g, kw in w.items())
     assert loss[0] == pytest.approx(0.87 + reg, rel=1e-5)
     assert loss[1:4] == pytest.approx([0.08, 0.7, 0.09])
-    kls = {g: D.kl(*ref_groups[g][:2]) for g in ("s", "g", "sg")}
+    kls = {g: RD.kl(*ref_groups[g][:2]) for g in ("s", "g", "sg")}
     if mt == "base":
         assert len(loss) == 5 and loss[4] == pytest.approx(kls["sg"], rel=1e-6)
     else:
         assert loss[4:] == pytest.approx([kls["g"], kls["s"], kls["sg"]], rel=1e-6)
     assert set(grads) == set(w)
+
+
+@pytest.mark.parametrize("B,N,D,hidden", [(2, 25, 6, (50, 20)), (3, 24, 4, (50, 20)), (1, 9, 3, (7, 5, 4))])
+def test_structure_decoder(B, N, D, hidden):
+    """The e2e structure decoder (model.py:193-208) + CE (optimizer.py:142-144) and its
+    backward against the literal torch float64 graph."""
+    from snd_vae_amd import disent
+    rng = np.random.default_rng(N + D)
+    z = rng.standard_normal((B, N, D)).astype(np.float32)
+    adj = np.zeros((B, N, N), np.float32)
+    for b in range(B):
+        a = (rng.random((N, N)) < 0.2).astype(np.float32)
+        a = np.triu(a, 1)
+        adj[b] = a + a.T
+    cin, layers = 2 * D, []
+    for h in hidden:
+        layers.append({"gamma": (1 + 0.1 * rng.standard_normal(cin)).astype(np.float32),
+                       "beta": (0.1 * rng.standard_normal(cin)).astype(np.float32),
+                       "w": (0.3 / np.sqrt(N * cin) * rng.standard_normal((N, cin, h))).astype(np.float32),
+                       "b": (0.1 * rng.standard_normal(h)).astype(np.float32)})
+        cin = h
+    head = {"gamma": (1 + 0.1 * rng.standard_normal(cin)).astype(np.float32),
+            "beta": (0.1 * rng.standard_normal(cin)).astype(np.float32),
+            "w": (0.5 * rng.standard_normal((cin, 2))).astype(np.float32),
+            "b": (0.1 * rng.standard_normal(2)).astype(np.float32)}
+    ce, correct, dz, grads, hg = disent.structure_decoder(
+        cu(z), cu(adj), [{k: cu(v) for k, v in l.items()} for l in layers], {k: cu(v) for k, v in head.items()})
+    rce, rcorrect, rdz, rgrads, rhg = RD.structure_decoder_grads(z, adj, layers, head)
+    assert ce == pytest.approx(rce, rel=1e-5)
+    assert abs(correct - rcorrect) <= 2
+    assert rel(dz.cpu().numpy(), rdz) < 1e-4
+    for g, rg in zip(grads, rgrads):
+        for k in ("gamma", "beta", "w", "b"):
+            assert rel(g[k].cpu().numpy(), rg[k]) < 1e-4, k
+    for k in ("gamma", "beta", "w", "b"):
+        assert rel(hg[k].cpu().numpy(), rhg[k]) < 1e-4, k
