@@ -275,7 +275,7 @@ int snd_sg_layer_bwd(const snd_sg_graph_t* g, const float* x, int ldx, int f, in
                      const float* dout, float* dx, int lddx, float* grads, void* workspace,
                      snd_stream_t stream);
 
-/* ---- §8f rank 4: disentangled-model pieces (not on the benchmarked path) -------
+/* ---- §8f rank 4: disentangled-model pieces (ABI 8; not on the benchmarked path) -
  * e2e edge-to-edge filter of the structure decoder (layers.py:431-450), fp32:
  *   out[b,i,j,o] = 2 b1[o] + sum_t sum_c w1[t,c,o] (x[b,i,j+t-p,c] + x[b,i+t-p,j,c])
  * x [B, N, N, C] (NHWC), w1 [K, C, O] (the reference's [1, K, C, O] kernel; conv2

@@ -146,16 +146,19 @@ __device__ __forceinline__ __bf16* img_at(__bf16* img, int row, int kp, int n0) 
 // o .. o + 4.  Waves are assigned column group cg = w % ncg and row blocks
 // k, k + wpc, ... (k = w / ncg); PRE(orow, nb0, yp) loads epilogue operands before
 // the MFMAs, EPI(orow, nb0, acc, yp) consumes a finished 16-row x NBH-block item.
-template <int NBH, class Pre, class Epi>
-__device__ __forceinline__ void conv_phase(const __bf16* xs, int kpx, const __bf16* ws, int kpw, int np,
-                                           int n_out, Pre&& pre, Epi&& epi, int dbg = 0) {
+// KCS = kpw / 32 k-chunks per tap as a compile-time count: the tap x chunk loop
+// unrolls whole, so the operand reads of later chunks are issued ahead of the
+// MFMAs of earlier ones (a runtime count left one LDS round trip per chunk exposed)
+template <int NBH, int KCS, class Pre, class Epi>
+__device__ __forceinline__ void conv_phase_t(const __bf16* xs, int kpx, const __bf16* ws, int kpw, int np,
+                                             int n_out, Pre&& pre, Epi&& epi, int dbg) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, li = lane & 15, lg = lane >> 4;
   const int nrb = (n_out + 15) >> 4, nbc = np >> 4;
   const int ncg = (nbc + NBH - 1) / NBH, wpc = NW / ncg;
   const int cg = w % ncg, k0 = w / ncg;
   if (k0 >= wpc) return;
   const int nb0 = cg * NBH;
-  const int kcs = (dbg & 4) ? 0 : kpw >> 5;
+  const int kcs = (dbg & 4) ? 0 : (KCS ? KCS : kpw >> 5);
   const int wsw = dswz(li, kpw);
   for (int rb = k0; rb < nrb; rb += wpc) {
     f32x4 yp[NBH];
@@ -169,7 +172,7 @@ __device__ __forceinline__ void conv_phase(const __bf16* xs, int kpx, const __bf
       const __bf16* xrp = xs + xrow * kpx;
       const int xsw = dswz(xrow, kpx);
       const __bf16* wrp = ws + (t * np + li) * kpw;
-      for (int ks = 0; ks < kcs; ++ks) {
+      auto chunk = [&](int ks) {
         const int ch = 4 * ks + lg;
         const bf16x8 bx = *reinterpret_cast<const bf16x8*>(xrp + ((ch ^ xsw) << 3));
 #pragma unroll
@@ -179,10 +182,27 @@ __device__ __forceinline__ void conv_phase(const __bf16* xs, int kpx, const __bf
             acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aw, bx, acc[i], 0, 0, 0);
           }
         }
+      };
+      if constexpr (KCS == 0) {
+        for (int ks = 0; ks < kcs; ++ks) chunk(ks);
+      } else {
+#pragma unroll
+        for (int ks = 0; ks < KCS; ++ks)
+          if (ks < kcs) chunk(ks);
       }
     }
     epi(16 * rb + li, nb0, acc, yp);
   }
+}
+// UNR false (the backward chain, at its register limit): the chunk count stays a
+// runtime value
+template <int NBH, bool UNR = true, class Pre, class Epi>
+__device__ __forceinline__ void conv_phase(const __bf16* xs, int kpx, const __bf16* ws, int kpw, int np,
+                                           int n_out, Pre&& pre, Epi&& epi, int dbg = 0) {
+  if (!UNR) conv_phase_t<NBH, 0>(xs, kpx, ws, kpw, np, n_out, pre, epi, dbg);
+  else if (kpw == 32) conv_phase_t<NBH, 1>(xs, kpx, ws, kpw, np, n_out, pre, epi, dbg);
+  else if (kpw == 64) conv_phase_t<NBH, 2>(xs, kpx, ws, kpw, np, n_out, pre, epi, dbg);
+  else conv_phase_t<NBH, 4>(xs, kpx, ws, kpw, np, n_out, pre, epi, dbg);
 }
 
 // per-column parameters of a (possibly split) layout, physical column n
@@ -562,7 +582,7 @@ __global__ void __launch_bounds__(DT) dec_bwd_kernel(DecChainBwdArgs a) {
     const int nbc = a.k3t.np >> 4, ncg = nbc, wpc = NW / ncg;
     const int nb0 = w % ncg;
     float q[3][1][4] = {};
-    conv_phase<1>(d3, a.k3t.kp, wimg, a.k3t.kp, a.k3t.np, n_out,
+    conv_phase<1, false>(d3, a.k3t.kp, wimg, a.k3t.kp, a.k3t.np, n_out,
                   [&](int orow, int nb, f32x4 (&yp)[1]) {
                     yp[0] = f32x4{0.f, 0.f, 0.f, 0.f};
                     const int gr = wr0 + orow;
@@ -619,7 +639,7 @@ __global__ void __launch_bounds__(DT) dec_bwd_kernel(DecChainBwdArgs a) {
     const int nbc = a.k2t.np >> 4, ncg = (nbc + 1) / 2, wpc = NW / ncg;
     const int nb0 = 2 * (w % ncg);
     float q[3][2][4] = {};
-    conv_phase<2>(d2, a.k2t.kp, wimg, a.k2t.kp, a.k2t.np, n_out,
+    conv_phase<2, false>(d2, a.k2t.kp, wimg, a.k2t.kp, a.k2t.np, n_out,
                   [&](int orow, int nb, f32x4 (&yp)[2]) {
                     const int gr = wr0 + orow;
                     const bool ok = orow < n_out && gr >= tl.glo && gr < tl.ghi;
@@ -685,7 +705,7 @@ __global__ void __launch_bounds__(DT) dec_bwd_kernel(DecChainBwdArgs a) {
   // ---- conv1^T: own rows -> dJ (fp32)
   {
     const int n_out = own, N = a.dj;
-    conv_phase<2>(d1, a.k1t.kp, wimg, a.k1t.kp, a.k1t.np, n_out, [](int, int, auto&) {},
+    conv_phase<2, false>(d1, a.k1t.kp, wimg, a.k1t.kp, a.k1t.np, n_out, [](int, int, auto&) {},
                   [&](int orow, int nb, f32x4 (&acc)[2], f32x4 (&)[2]) {
       if (orow >= n_out) return;
       const long long gr = tl.r0 + orow;
