@@ -194,15 +194,15 @@ __device__ __forceinline__ void conv_phase_t(const __bf16* xs, int kpx, const __
     epi(16 * rb + li, nb0, acc, yp);
   }
 }
-// UNR false (the backward chain, at its register limit): the chunk count stays a
-// runtime value
-template <int NBH, bool UNR = true, class Pre, class Epi>
+// KX: the chunk count the call site expects (the C2 decoder widths); the phase runs
+// the unrolled instantiation when kpw / 32 == KX and the runtime loop otherwise (KX 0:
+// always the runtime loop).  One unrolled instantiation per call site keeps the
+// backward chain within 128 VGPRs.
+template <int NBH, int KX, class Pre, class Epi>
 __device__ __forceinline__ void conv_phase(const __bf16* xs, int kpx, const __bf16* ws, int kpw, int np,
                                            int n_out, Pre&& pre, Epi&& epi, int dbg = 0) {
-  if (!UNR) conv_phase_t<NBH, 0>(xs, kpx, ws, kpw, np, n_out, pre, epi, dbg);
-  else if (kpw == 32) conv_phase_t<NBH, 1>(xs, kpx, ws, kpw, np, n_out, pre, epi, dbg);
-  else if (kpw == 64) conv_phase_t<NBH, 2>(xs, kpx, ws, kpw, np, n_out, pre, epi, dbg);
-  else conv_phase_t<NBH, 4>(xs, kpx, ws, kpw, np, n_out, pre, epi, dbg);
+  if (KX > 0 && kpw == 32 * KX) conv_phase_t<NBH, KX>(xs, kpx, ws, kpw, np, n_out, pre, epi, dbg);
+  else conv_phase_t<NBH, 0>(xs, kpx, ws, kpw, np, n_out, pre, epi, dbg);
 }
 
 // per-column parameters of a (possibly split) layout, physical column n
@@ -359,7 +359,7 @@ __global__ void __launch_bounds__(DT) dec_fwd_kernel(DecChainFwdArgs a) {
   // ---- conv1: window [r0 - 4, r0 + own + 4) -> U1 image (bf16), Y1 / U1 own rows to HBM
   {
     const int wr0 = tl.r0 - 4, n_out = own + 8, N = a.m1.phys(), kpo = a.k2.kp;
-    conv_phase<2>(jimg, a.k1.kp, wimg, a.k1.kp, a.k1.np, n_out, nopre,
+    conv_phase<2, 2>(jimg, a.k1.kp, wimg, a.k1.kp, a.k1.np, n_out, nopre,
                   [&](int orow, int nb0, f32x4 (&acc)[2], f32x4 (&)[2]) {
       if (orow >= n_out) return;
       const int gr = wr0 + orow;
@@ -401,7 +401,7 @@ __global__ void __launch_bounds__(DT) dec_fwd_kernel(DecChainFwdArgs a) {
   // ---- conv2: window [r0 - 2, r0 + own + 2) -> U2 image; Y2 / U2 own rows; Y2n own rows in LDS
   {
     const int wr0 = tl.r0 - 2, n_out = own + 4, N = a.m2.phys();
-    conv_phase<2>(u1img, a.k2.kp, wimg, a.k2.kp, a.k2.np, n_out, nopre,
+    conv_phase<2, 4>(u1img, a.k2.kp, wimg, a.k2.kp, a.k2.np, n_out, nopre,
                   [&](int orow, int nb0, f32x4 (&acc)[2], f32x4 (&)[2]) {
       if (orow >= n_out) return;
       const int gr = wr0 + orow;
@@ -449,7 +449,7 @@ __global__ void __launch_bounds__(DT) dec_fwd_kernel(DecChainFwdArgs a) {
   // ---- conv3 (s branch): own rows -> U3, Y3 (fp32, LDS; the spatial head's input)
   {
     const int n_out = own;
-    conv_phase<1>(u2img, kpu2, wimg, a.k3.kp, a.k3.np, n_out, nopre,
+    conv_phase<1, 2>(u2img, kpu2, wimg, a.k3.kp, a.k3.np, n_out, nopre,
                   [&](int orow, int nb0, f32x4 (&acc)[1], f32x4 (&)[1]) {
       if (orow >= n_out) return;
       const int n0 = 16 * nb0 + 4 * lg;
@@ -582,7 +582,7 @@ __global__ void __launch_bounds__(DT) dec_bwd_kernel(DecChainBwdArgs a) {
     const int nbc = a.k3t.np >> 4, ncg = nbc, wpc = NW / ncg;
     const int nb0 = w % ncg;
     float q[3][1][4] = {};
-    conv_phase<1, false>(d3, a.k3t.kp, wimg, a.k3t.kp, a.k3t.np, n_out,
+    conv_phase<1, 1>(d3, a.k3t.kp, wimg, a.k3t.kp, a.k3t.np, n_out,
                   [&](int orow, int nb, f32x4 (&yp)[1]) {
                     yp[0] = f32x4{0.f, 0.f, 0.f, 0.f};
                     const int gr = wr0 + orow;
@@ -639,7 +639,7 @@ __global__ void __launch_bounds__(DT) dec_bwd_kernel(DecChainBwdArgs a) {
     const int nbc = a.k2t.np >> 4, ncg = (nbc + 1) / 2, wpc = NW / ncg;
     const int nb0 = 2 * (w % ncg);
     float q[3][2][4] = {};
-    conv_phase<2, false>(d2, a.k2t.kp, wimg, a.k2t.kp, a.k2t.np, n_out,
+    conv_phase<2, 2>(d2, a.k2t.kp, wimg, a.k2t.kp, a.k2t.np, n_out,
                   [&](int orow, int nb, f32x4 (&yp)[2]) {
                     const int gr = wr0 + orow;
                     const bool ok = orow < n_out && gr >= tl.glo && gr < tl.ghi;
@@ -705,7 +705,7 @@ __global__ void __launch_bounds__(DT) dec_bwd_kernel(DecChainBwdArgs a) {
   // ---- conv1^T: own rows -> dJ (fp32)
   {
     const int n_out = own, N = a.dj;
-    conv_phase<2, false>(d1, a.k1t.kp, wimg, a.k1t.kp, a.k1t.np, n_out, [](int, int, auto&) {},
+    conv_phase<2, 4>(d1, a.k1t.kp, wimg, a.k1t.kp, a.k1t.np, n_out, [](int, int, auto&) {},
                   [&](int orow, int nb, f32x4 (&acc)[2], f32x4 (&)[2]) {
       if (orow >= n_out) return;
       const long long gr = tl.r0 + orow;
