@@ -305,10 +305,25 @@ __global__ void __launch_bounds__(DT) dec_fwd_kernel(DecChainFwdArgs a) {
   const int kpu2 = a.m2.phys() <= 32 ? 32 : (a.m2.phys() <= 64 ? 64 : 128);
   const int own = tl.rend - tl.r0;
 
-  // zero the activation images (pad columns and rows past a window are MFMA operands)
-  if (!(a.dbg & 32))
+  // Zero what an MFMA reads against zero weights but nobody writes: the U1 image's
+  // pad columns [k1.np, k2.kp) (conv2's last k-chunk; uninitialised LDS may hold NaN,
+  // and NaN * 0 is NaN).  Everything else a valid output reads is written first: the
+  // J window by its DMA (zeros outside the graph), U1 / U2 / U3 / Y3 / Y2n by the
+  // epilogues; rows past a window only feed discarded output rows, and U2's pad
+  // columns hold finite stale J values against zero weights.  (Zeroing the whole
+  // 148 KB measured 1.6 us of the launch.)
+  if (a.dbg & (1 << 23)) {   // test only: NaN in every activation byte first (worst-case stale LDS)
     for (int i = tid * 16; i < L.total - L.a; i += DT * 16)
-      *reinterpret_cast<uint4*>(smem + L.a + i) = make_uint4(0u, 0u, 0u, 0u);
+      *reinterpret_cast<uint4*>(smem + L.a + i) = make_uint4(~0u, ~0u, ~0u, ~0u);
+    __syncthreads();
+  }
+  if (!(a.dbg & 32)) {
+    const int kpo = a.k2.kp, npc = (kpo - a.k1.np) >> 2, nr = in_rows(TR + 4);
+    for (int i = tid; i < nr * npc; i += DT) {
+      const int row = i / npc, n0 = a.k1.np + 4 * (i - row * npc);
+      *reinterpret_cast<bf16x4*>(img_at(u1img, row, kpo, n0)) = bf16x4{};
+    }
+  }
   __syncthreads();
   // J window [r0 - 6, r0 + own + 6) and the conv1 weights
   if (!(a.dbg & 16)) stage_window(a.zb, a.ldz, a.dj, tl.r0 - 6, in_rows(TR + 8), own + 12, tl.glo, tl.ghi, a.k1.kp,

@@ -340,6 +340,21 @@ def test_fused_decoder_matches_row_engine(topology, n, d, B):
     l0, l1 = o0.loss_dict(), o1.loss_dict()
     for k in ("spatial_cost", "node_cost", "cost"):
         assert l1[k] == pytest.approx(l0[k], rel=1e-6), k
+    # the forward kernel zeroes only the LDS it must: rerun with every activation byte
+    # of its LDS set to NaN first (debug bit 1 << 23) -- same buffers, bit for bit
+    ctr = o1.step_counter.clone()            # the device Philox stream is keyed by the step
+    o1.forward_backward(b)
+    torch.cuda.synchronize()
+    snap = {name: m1.buffer(name, dt).clone() for name, dt in DEC_BUFS}
+    o1.step_counter.copy_(ctr)
+    _lib.check(_lib.lib().snd_debug_set(1 << 23))
+    try:
+        o1.forward_backward(b)
+        torch.cuda.synchronize()
+    finally:
+        _lib.check(_lib.lib().snd_debug_set(0))
+    for name, dt in DEC_BUFS:
+        assert torch.equal(m1.buffer(name, dt), snap[name]), f"{name} with NaN-poisoned LDS"
 
 
 HEAD_BUFS = (("FP1", torch.float32), ("FG", torch.bfloat16), ("FHH", torch.bfloat16), ("MS", torch.float32),
