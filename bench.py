@@ -80,8 +80,8 @@ def cpu_baseline(n_nodes, latent, budget_s):
 
 
 def load_traffic(n, d, B, dtype):
-    """HBM bytes per zz^T launch from the committed rocprofv3 PMC summary, if any."""
-    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc_zzt*.json"))):
+    """HBM bytes per zz^T launch from the newest committed rocprofv3 PMC summary, if any."""
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc_zzt*.json")), reverse=True):
         try:
             j = json.load(open(f))
         except Exception:
