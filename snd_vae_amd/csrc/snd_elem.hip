@@ -134,7 +134,10 @@ __global__ void __launch_bounds__(256) heads_kernel(HeadPack pk, int rows) {
 // ---------------------------------------------------------------- BN/lrelu bwd
 // Column-reduction kernels: block = kColRows rows x all columns; 256 threads in
 // a (RP rows) x (CP columns) layout so every row read is coalesced; per-thread
-// column sums are combined across the RP row lanes in LDS (fixed order).
+// column sums are combined across the RP row lanes in LDS (fixed order).  At the
+// widest layout (CP = 256, one row lane) a thread walks 64 rows: rows go in groups
+// of 8 whose loads are all issued before the group's stores (one row in flight per
+// thread left enc_bwd<256> at 59.5 us in the C5 step, one wave per SIMD).
 template <int CP>
 __device__ __forceinline__ float lane_rows_sum(float v, float* red) {
   constexpr int RP = 256 / CP;
@@ -158,16 +161,29 @@ __global__ void __launch_bounds__(256) dec_bwd_kernel(DecPack pk, int rows) {
   float sg = 0.f, sb = 0.f, sy = 0.f;
   const int r0 = blockIdx.x * kColRows, r1 = min(rows, r0 + kColRows);
   if (on) {
-#pragma unroll 4
-    for (int r = r0 + ty; r < r1; r += RP) {
-      const float y = a.y[(long long)r * a.ldy + c];
-      const float t = y * gc + be;
-      const float dt = a.du[(long long)r * a.lddu + c] * lrelu_grad(t);
-      const float dy = dt * gc;
-      a.dy[(long long)r * a.lddy + c] = dy;
-      sg += dt * y;
-      sb += dt;
-      sy += dy;
+    constexpr int RG = 8;   // a group's loads before its stores (see enc_bwd_kernel)
+    for (int rb = r0 + ty; rb < r1; rb += RG * RP) {
+      float yv[RG], uv[RG];
+#pragma unroll
+      for (int k = 0; k < RG; ++k) {
+        const int r = rb + k * RP;
+        const bool rv = r < r1;
+        yv[k] = rv ? a.y[(long long)r * a.ldy + c] : 0.f;
+        uv[k] = rv ? a.du[(long long)r * a.lddu + c] : 0.f;
+      }
+#pragma unroll
+      for (int k = 0; k < RG; ++k) {
+        const int r = rb + k * RP;
+        if (r >= r1) break;
+        const float y = yv[k];
+        const float t = y * gc + be;
+        const float dt = uv[k] * lrelu_grad(t);
+        const float dy = dt * gc;
+        a.dy[(long long)r * a.lddy + c] = dy;
+        sg += dt * y;
+        sb += dt;
+        sy += dy;
+      }
     }
   }
   sg = lane_rows_sum<CP>(sg, red);
@@ -193,19 +209,36 @@ __global__ void __launch_bounds__(256) enc_bwd_kernel(EncBwdArgs a, int rows) {
   float sge = 0.f, sbe = 0.f, sg = 0.f, sb = 0.f;
   const int r0 = blockIdx.x * kColRows, r1 = min(rows, r0 + kColRows);
   if (on) {
-#pragma unroll 4
-    for (int r = r0 + ty; r < r1; r += RP) {
-      float d = a.dg[(long long)r * a.lddg + c];
-      if (a.has_enc) {
-        sge += d * a.h2[(long long)r * a.ldh2 + c];
-        sbe += d;
-        d *= gec;
+    // rows in groups of RG: every input of the group is loaded before the first
+    // dp store (the store may alias the inputs as far as the compiler knows, so a
+    // plain loop keeps one row's loads in flight per thread; same sums, same order)
+    constexpr int RG = 8;
+    const bool hc = c < a.h, he = a.has_enc != 0;
+    for (int rb = r0 + ty; rb < r1; rb += RG * RP) {
+      float dv[RG], hv[RG], pv[RG];
+#pragma unroll
+      for (int k = 0; k < RG; ++k) {
+        const int r = rb + k * RP;
+        const bool rv = r < r1;
+        dv[k] = rv ? a.dg[(long long)r * a.lddg + c] : 0.f;
+        hv[k] = (rv && he) ? a.h2[(long long)r * a.ldh2 + c] : 0.f;
+        pv[k] = (rv && hc) ? a.p[(long long)r * a.ldp + c] : 0.f;
       }
-      if (c < a.h) {
-        const float p = a.p[(long long)r * a.ldp + c];
-        sg += d * lrelu(p);
-        sb += d;
-        a.dp[(long long)r * a.lddp + c] = d * gc * lrelu_grad(p);
+#pragma unroll
+      for (int k = 0; k < RG; ++k) {
+        const int r = rb + k * RP;
+        if (r >= r1) break;
+        float d = dv[k];
+        if (he) {
+          sge += d * hv[k];
+          sbe += d;
+          d *= gec;
+        }
+        if (hc) {
+          sg += d * lrelu(pv[k]);
+          sb += d;
+          a.dp[(long long)r * a.lddp + c] = d * gc * lrelu_grad(pv[k]);
+        }
       }
     }
   }
