@@ -63,6 +63,18 @@ __device__ __forceinline__ void glds16(const void* g, void* lds_base) {
   __builtin_amdgcn_global_load_lds((gptr_t)g, (lptr_t)lds_base, 16, 0, 0);
 }
 
+// The same DMA issued from inline asm: the compiler does not track it, so it does
+// not drain vmcnt before the next ds_read of a different LDS buffer (the builtin
+// makes it wait for the prefetch of chunk k+1 before reading chunk k).  The caller
+// owns the wait: s_waitcnt vmcnt(0) + barrier before the buffer is read.
+__device__ __forceinline__ void glds16_async(const void* g, void* lds_base) {
+  const unsigned dst = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(lptr_t)lds_base);
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+               "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(g), "s"(dst) : "memory");
+}
+
 __device__ __forceinline__ int rc_xchunks(int T, int lkc) {
   return (((kRcRows + T - 1) << lkc) + 63) & ~63;   // whole 1 KB pieces
 }
@@ -468,7 +480,7 @@ __device__ __forceinline__ void wgrad_body(const WgArgs& a, const int bx, const 
         const int gr = u.sub + row;
         if (gr >= u.s0 && gr < u.s1 && 8 * c < a.N) g = dg + (long long)gr * a.lddy + 8 * c;
       }
-      glds16(g, reinterpret_cast<char*>(isx ? xs : ds) + (jj << 10));
+      glds16_async(g, reinterpret_cast<char*>(isx ? xs : ds) + (jj << 10));
     }
   };
 
