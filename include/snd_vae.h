@@ -146,6 +146,20 @@ int snd_csr_spmm_bf16_window(const int* meta, const uint16_t* slots, const int* 
                              int n_rows, int n_per_graph, int n_graphs, int beta,
                              const void* h, int ldh, int width, void* out, int ldo,
                              snd_stream_t stream);
+/* The same window walk with pair sums (ABI 9; plan: data.py window_plan_pairs).
+ * A wavefront sums one row at a time, four neighbours per round as two pairs
+ * of ring rows read with ds_read_b64_tr_b16 and added by one v_dot2c with
+ * (1, 1) per pair and column: slots[] holds per row a 32-entry block, entry
+ * (round r, pair h, side t) at 8 (2h + t) + r for r < 8 and at 32 + 4 (r - 8)
+ * + 2h + t past it; side 0 prefers even ring slots, side 1 odd ones, padding
+ * uses the zero rows 1096 (even) and 1097 (odd).  meta / rows / order / beta
+ * as above.  Sums are not in colidx order: within fp32 rounding of the sums
+ * of snd_csr_spmm_bf16 (a bf16 output differs by at most one ulp). */
+int snd_csr_spmm_bf16_window_pairs(const int* meta, const uint16_t* slots, const int* rows,
+                                   const int* order,
+                                   int n_rows, int n_per_graph, int n_graphs, int beta,
+                                   const void* h, int ldh, int width, void* out, int ldo,
+                                   snd_stream_t stream);
 /* ---- a5: linear / dense GEMM on MFMA ---------------------------------------
  * Replaces linear() (layers.py:566-576) and the X@w of GraphConvolution
  * (layers.py:120-121; the tile() copy is not needed):

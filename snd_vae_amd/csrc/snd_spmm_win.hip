@@ -62,8 +62,8 @@ constexpr int WT = 1024;       // threads: 16 waves x 8 rows
 constexpr int RR = 1096;       // ring rows
 constexpr int STEP = 128;      // rows per step
 constexpr int WIDTH = 64;      // bf16 columns (128-byte rows)
-constexpr int ZROW = RR;       // the zero row's slot
-constexpr int OFF_IDX = (RR + 1) * WIDTH * 2;       // 4 x 1536 B index blocks
+constexpr int ZROW = RR;       // the zero rows' slots: RR (even) and RR + 1 (odd, pair plans)
+constexpr int OFF_IDX = (RR + 2) * WIDTH * 2;       // 4 x 1536 B index blocks
 constexpr int OFF_SL = OFF_IDX + 4 * 16 * 96;       // 2 x 8192 B slot-list buffers
 constexpr int LDS_BYTES = OFF_SL + 2 * 16 * 512;
 
@@ -158,7 +158,7 @@ typedef __attribute__((address_space(3))) v4s_t lds_v4s_t;
 // apart): twice the LDS instructions (8-byte transposed reads), bank conflicts 40 % of
 // LDS-active cycles (a 32-lane half's 8 ring rows fall on 8 segment positions at
 // random), and ~10 VALU per MFMA of address arithmetic.  Kept behind debug bit 64 << 16.
-template <int GK, bool DOT, bool MF>
+template <int GK, bool DOT, bool MF, bool PR = false>
 __global__ void __launch_bounds__(WT) spmm_win_kernel(WinArgs a) {
   __shared__ __attribute__((aligned(16))) char lds[LDS_BYTES];
   const unsigned lds0 = (unsigned)(uintptr_t)(lptr_t)lds;   // LDS byte address of lds[0]
@@ -207,7 +207,7 @@ __global__ void __launch_bounds__(WT) spmm_win_kernel(WinArgs a) {
   auto lds_i32 = [&](int off) { return *reinterpret_cast<const int*>(lds + off); };
 
   // ---- prologue: zero row, index(0..2), slots(0), window [Q0, hi(1)]
-  if (tid < WIDTH * 2 / 16)
+  if (tid < 2 * WIDTH * 2 / 16)
     reinterpret_cast<uint4*>(lds + RR * WIDTH * 2)[tid] = make_uint4(0u, 0u, 0u, 0u);
   dma_index(0);
   dma_index(1);
@@ -261,7 +261,82 @@ __global__ void __launch_bounds__(WT) spmm_win_kernel(WinArgs a) {
       raw_barrier();
     }
 
-    if constexpr (MF) {
+    if constexpr (PR) {
+      // Pair sums (plan: data.window_plan_pairs).  The wave sums its 8 rows two at a
+      // time, each row over rounds of 4 neighbours: 32-lane half h takes the round's
+      // pair h = (A, B) (an even and an odd ring slot where the row allows: the two
+      // 128-byte rows cover the 64 banks once), its 16-lane group g1 columns
+      // 32 g1 .. 32 g1 + 31.  ds_read_b64_tr_b16: lane quad qd supplies row A or B
+      // (qd & 1) at column piece (qd >> 1) + 2 g1; lane i of the group receives
+      // (A[c], B[c]) and (A[c + 16], B[c + 16]), c = 32 g1 + i, and one v_dot2c with
+      // (1, 1) adds both neighbours: 3 VALU (1 address + 2 dot2c) per 4 neighbours x
+      // 64 columns.  The halves' partial sums meet in one v_permlane32_swap.
+      const int hh = lane >> 5, g1 = (lane >> 4) & 1, qd = (lane >> 2) & 3;
+      const int cls = 2 * hh + (qd & 1);
+      const unsigned K = 32u * (unsigned)((qd >> 1) + 2 * g1) + 8u * (unsigned)(lane & 3);
+      const int col = 32 * g1 + 16 * hh + (lane & 15);
+      unsigned one2u;
+      asm volatile("s_mov_b32 %0, 0x3f803f80" : "=s"(one2u));
+      auto tr = [&](unsigned off) {
+        const v4s_t v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s_t*)(lds + off));
+        return __builtin_bit_cast(uint2, v);
+      };
+      // VOP3P v_dot2_f32_bf16 (untied accumulator): the builtin picks v_dot2c, whose
+      // tied accumulator cost one v_mov per add at every round-chunk join
+      auto add2 = [&](float& c0, float& c1, uint2 v) {
+        asm("v_dot2_f32_bf16 %0, %1, %2, %3" : "=v"(c0) : "v"(v.x), "s"(one2u), "v"(c0));
+        asm("v_dot2_f32_bf16 %0, %1, %2, %3" : "=v"(c1) : "v"(v.y), "s"(one2u), "v"(c1));
+      };
+      // The wave's 8 rows go through the rounds together (rows are listed by degree,
+      // descending, so row 0 bounds the round count; past a row's own rounds its
+      // block holds zero rows), two rounds per chunk: 16 transposed reads in flight.
+      const int blk = idx_blk(s);
+      const int deg0 = __builtin_amdgcn_readfirstlane(lds_i32(blk)) & 63;
+      const int nr = (a.dbg & 1) ? 0 : min((deg0 + 3) >> 2, 8);
+      unsigned wv[8][4];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const uint4 t = *reinterpret_cast<const uint4*>(lds + sl_buf(s) + 64 * j + 16 * cls);
+        wv[j][0] = t.x; wv[j][1] = t.y; wv[j][2] = t.z; wv[j][3] = t.w;
+      }
+      // all 32 slot words in registers before the rounds (no LDS round trip per chunk)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) asm volatile("" ::"v"(wv[j][0]), "v"(wv[j][1]), "v"(wv[j][2]), "v"(wv[j][3]));
+      float c0[8], c1[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { c0[j] = 0.f; c1[j] = 0.f; }
+#pragma unroll
+      for (int r = 0; r < 8; r += 2) {
+        if (r < nr) {
+          uint2 x[8], y[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            x[j] = tr(slot_addr(wv[j][r >> 1], 0, K));
+            y[j] = tr(slot_addr(wv[j][r >> 1], 1, K));
+          }
+#pragma unroll
+          for (int j = 0; j < 8; ++j) add2(c0[j], c1[j], x[j]);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) add2(c0[j], c1[j], y[j]);
+        }
+      }
+      // rounds past 8 (degree > 32, rare): entries 32 + 4 (r - 8) + class, from HBM
+      if (deg0 > 32 && !(a.dbg & 1)) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int mj = __builtin_amdgcn_readfirstlane(lds_i32(blk + 4 * j));
+          const int nrj = ((mj & 63) + 3) >> 2;
+          const unsigned short* e = a.slots + (long long)(mj >> 6) * 8 + 32 + cls;
+          for (int r = 8; r < nrj; ++r) add2(c0[j], c1[j], tr(e[4 * (r - 8)] * (WIDTH * 2) + K));
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const auto f = __builtin_amdgcn_permlane32_swap(__float_as_uint(c0[j]), __float_as_uint(c1[j]), false, false);
+        const int row = lds_i32(blk + 32 + 4 * j);
+        a.out[(long long)row * a.ldo + col] = (__bf16)(__uint_as_float(f[0]) + __uint_as_float(f[1]));
+      }
+    } else if constexpr (MF) {
       // Sums on v_mfma_f32_16x16x32_bf16 (wave = 16 degree-sorted rows x 32 columns):
       //   D[m = column][n = row] += A[m][k] B[k][n],  k = 2 n + t (neighbour 2 j + t of row n)
       // A: ds_read_b64_tr_b16 delivers to lane (gq, li) column li of four ring rows whose
@@ -389,11 +464,10 @@ int spmm_win_max_beta() { return 352; }   // 8-aligned, 2 beta < RR - 3 STEP (71
 
 using namespace snd;
 
-extern "C" int snd_csr_spmm_bf16_window(const int* meta, const uint16_t* slots, const int* rows,
-                                        const int* order,
-                                        int n_rows, int n_per_graph, int n_graphs, int beta,
-                                        const void* h, int ldh, int width, void* out, int ldo,
-                                        snd_stream_t stream) {
+namespace {
+int window_launch(bool pairs, const int* meta, const uint16_t* slots, const int* rows, const int* order,
+                  int n_rows, int n_per_graph, int n_graphs, int beta, const void* h, int ldh, int width,
+                  void* out, int ldo, snd_stream_t stream) {
   SND_CHECK_ARG(meta && slots && rows && order && h && out, "snd_csr_spmm_bf16_window: null operand");
   SND_CHECK_ARG(width == WIDTH, "snd_csr_spmm_bf16_window: width %d (the ring holds 64-column rows)", width);
   SND_CHECK_ARG(n_per_graph > 0 && n_graphs > 0 && (long long)n_per_graph * n_graphs == n_rows,
@@ -412,7 +486,9 @@ extern "C" int snd_csr_spmm_bf16_window(const int* meta, const uint16_t* slots, 
             debug_flags() >> 16};
   const dim3 grid(n_graphs * a.spg);
   const hipStream_t st = (hipStream_t)stream;
-  if (a.dbg & 64) {
+  if (pairs) {
+    hipLaunchKernelGGL((spmm_win_kernel<4, true, false, true>), grid, dim3(WT), 0, st, a);
+  } else if (a.dbg & 64) {
     hipLaunchKernelGGL((spmm_win_kernel<4, true, true>), grid, dim3(WT), 0, st, a);
   } else if (a.dbg & 8) {
     if (a.dbg & 16) hipLaunchKernelGGL((spmm_win_kernel<8, false, false>), grid, dim3(WT), 0, st, a);
@@ -423,4 +499,23 @@ extern "C" int snd_csr_spmm_bf16_window(const int* meta, const uint16_t* slots, 
   }
   SND_LAUNCH_CHECK("spmm_win_kernel");
   return 0;
+}
+}  // namespace
+
+extern "C" int snd_csr_spmm_bf16_window(const int* meta, const uint16_t* slots, const int* rows,
+                                        const int* order,
+                                        int n_rows, int n_per_graph, int n_graphs, int beta,
+                                        const void* h, int ldh, int width, void* out, int ldo,
+                                        snd_stream_t stream) {
+  return window_launch(false, meta, slots, rows, order, n_rows, n_per_graph, n_graphs, beta, h, ldh, width,
+                       out, ldo, stream);
+}
+
+extern "C" int snd_csr_spmm_bf16_window_pairs(const int* meta, const uint16_t* slots, const int* rows,
+                                              const int* order,
+                                              int n_rows, int n_per_graph, int n_graphs, int beta,
+                                              const void* h, int ldh, int width, void* out, int ldo,
+                                              snd_stream_t stream) {
+  return window_launch(true, meta, slots, rows, order, n_rows, n_per_graph, n_graphs, beta, h, ldh, width,
+                       out, ldo, stream);
 }

@@ -185,6 +185,38 @@ def test_spmm_bf16_window_bitwise(n, B, kbar, seed):
         assert np.abs(out.float().cpu().numpy() - r64).max() <= 2 ** -7 * max(np.abs(r64).max(), 1.0)
 
 
+@pytest.mark.parametrize("n,B,kbar,seed", [(4096, 8, 16.0, 9), (4096, 64, 16.0, 9), (4096, 1, 16.0, 3),
+                                             (1000, 3, 16.0, 4), (300, 3, 10.0, 5), (96, 2, 0.0, 6),
+                                             (256, 4, 40.0, 7), (200, 1, 50.0, 8), (130, 5, 3.0, 2)])
+def test_spmm_bf16_window_pairs(n, B, kbar, seed):
+    """The pair-sum window SpMM (rounds of 4 neighbours, two per v_dot2c) against the
+    colidx-order register kernel: the fp32 sums differ only in order and in the dot2
+    rounding, so a bf16 output differs by at most one bf16 ulp of the sum and rarely;
+    against the float64 A H within bf16 rounding.  Same batches as the bitwise test
+    (kbar 40 / 50: rounds past 8 read from HBM; kbar 0: empty rows)."""
+    from snd_vae_amd import layers
+    from snd_vae_amd.data import GraphBatch, locality_order, window_plan_pairs
+    rp, ci, dense = rand_batch(n, B, kbar, seed) if B <= 8 else rand_batch_csr(n, B, kbar, seed)
+    gb = GraphBatch(B, n, rp, ci, np.zeros((n * B, 1), np.float32), np.zeros((n * B, 1), np.float32),
+                    np.zeros((n * B, 2), np.float32))
+    order = locality_order(gb)
+    wp = window_plan_pairs(gb, order)
+    if kbar >= 40:
+        assert wp.max_degree > 32
+    hb = torch.from_numpy(np.random.default_rng(seed).standard_normal((n * B, 64)).astype(np.float32)).to(torch.bfloat16)
+    d_rp, d_ci = cu(rp, torch.int32), cu(ci if len(ci) else np.zeros(1, np.int32), torch.int32)
+    ref = layers.spmm_bf16(d_rp, d_ci, hb.cuda(), n, B, cu(order, torch.int32))
+    out = layers.spmm_bf16_window(layers.DeviceWindowPlan(wp), hb.cuda(), n, B)
+    torch.cuda.synchronize()
+    rf, of = ref.float(), out.float()
+    ulp = torch.clamp(rf.abs(), min=2 ** -100) * 2 ** -7      # one bf16 ulp bound of the sum
+    assert bool(((of - rf).abs() <= ulp).all())
+    assert int((out.view(torch.int16) != ref.view(torch.int16)).sum()) <= 2e-3 * out.numel() + 1
+    if dense is not None:
+        r64 = R.spmm(dense, hb.float().numpy().astype(np.float64), n)
+        assert np.abs(of.cpu().numpy() - r64).max() <= 2 ** -7 * max(np.abs(r64).max(), 1.0)
+
+
 def test_spmm_bf16_window_rejects_wide_window():
     """Natural (generator) order puts neighbours ~N apart: the window plan's beta
     exceeds the ring and the launch refuses (the caller keeps the tiled kernel)."""

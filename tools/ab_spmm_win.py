@@ -1,8 +1,9 @@
 """A/B of the window SpMM on the bench's 256-graph batch under measurement-only
 skip bits (snd_debug_set(bits << 16)): 1 no sums, 2 no window DMA, 4 no slot DMA,
-8 neighbour groups of 8 instead of 4.
+8 neighbour groups of 8 instead of 4.  A flag with a trailing "p" runs the pair-sum
+kernel (snd_csr_spmm_bf16_window_pairs, plan window_plan_pairs).
 
-    python tools/ab_spmm_win.py [--flags 0,1,2,4,3]
+    python tools/ab_spmm_win.py [--flags 0,1,2,4,3,0p,1p] [--check]
 """
 import argparse
 import os
@@ -23,7 +24,7 @@ def main():
     import bench
     from snd_vae_amd import _lib
     from snd_vae_amd.config import tscale
-    from snd_vae_amd.data import GraphBatch, locality_order, synthetic_batch, window_plan
+    from snd_vae_amd.data import GraphBatch, locality_order, synthetic_batch, window_plan, window_plan_pairs
     from snd_vae_amd.layers import DeviceWindowPlan
     host = synthetic_batch(tscale(4096, 64), 8, seed=0)
     rp0, ci0 = host.rowptr.astype(np.int64), host.colidx.astype(np.int64)
@@ -35,8 +36,18 @@ def main():
     order = np.concatenate([o0 + k * R0 for k in range(c)]).astype(np.int32)
     z = np.zeros((1, 1), np.float32)
     big = GraphBatch(host.n_graphs * c, host.n_nodes, rp.astype(np.int32), ci.astype(np.int32), z, z, z)
+    toks = args.flags.split(",")
     wp = window_plan(big, order)
-    dw = DeviceWindowPlan(wp)
+    plans = {False: (wp, DeviceWindowPlan(wp))}
+    if any(t.endswith("p") for t in toks):
+        wpp = window_plan_pairs(big, order)
+        plans[True] = (wpp, DeviceWindowPlan(wpp))
+
+    def launch(pairs, sp):
+        w, d = plans[pairs]
+        fn = L.snd_csr_spmm_bf16_window_pairs if pairs else L.snd_csr_spmm_bf16_window
+        _lib.check(fn(d.meta.data_ptr(), d.slots.data_ptr(), d.rows.data_ptr(), d.order.data_ptr(), R, host.n_nodes,
+                      ng, w.beta, h.data_ptr(), 64, 64, out.data_ptr(), 64, sp))
     R, ng = R0 * c, host.n_graphs * c
     h = torch.randn(R, 64, device="cuda").to(torch.bfloat16)
     out = torch.empty_like(h)
@@ -46,24 +57,21 @@ def main():
         from snd_vae_amd import layers
         ref = layers.spmm_bf16(torch.from_numpy(rp.astype(np.int32)).cuda(), torch.from_numpy(ci.astype(np.int32)).cuda(),
                                h, host.n_nodes, ng, torch.from_numpy(order).cuda())
-        for f in [int(x) for x in args.flags.split(",")]:
+        for t in toks:
+            f = int(t.rstrip("p"))
             _lib.check(L.snd_debug_set(f << 16))
             out.zero_()
-            _lib.check(L.snd_csr_spmm_bf16_window(dw.meta.data_ptr(), dw.slots.data_ptr(), dw.rows.data_ptr(),
-                                                  dw.order.data_ptr(), R, host.n_nodes, ng, wp.beta, h.data_ptr(), 64, 64,
-                                                  out.data_ptr(), 64, _lib.stream_ptr()))
+            launch(t.endswith("p"), _lib.stream_ptr())
             torch.cuda.synchronize()
             neq = int((out.view(torch.int16) != ref.view(torch.int16)).sum())
             d = (out.float() - ref.float()).abs()
-            print(f"check {f}: {neq} of {out.numel()} bf16 outputs differ, max |diff| {float(d.max()):.3e}, "
+            print(f"check {t}: {neq} of {out.numel()} bf16 outputs differ, max |diff| {float(d.max()):.3e}, "
                   f"max |ref| {float(ref.float().abs().max()):.3e}", flush=True)
         _lib.check(L.snd_debug_set(0))
-    for f in [int(x) for x in args.flags.split(",")]:
-        _lib.check(L.snd_debug_set(f << 16))
-        ms = bench.time_launches(lambda sp: _lib.check(L.snd_csr_spmm_bf16_window(
-            dw.meta.data_ptr(), dw.slots.data_ptr(), dw.rows.data_ptr(), dw.order.data_ptr(), R, host.n_nodes, ng, wp.beta,
-            h.data_ptr(), 64, 64, out.data_ptr(), 64, sp)), args.reps)
-        print(f"skip {f}: {ms * 1e3:8.1f} us  {byts / (ms * 1e-3) / 1e12:5.2f} TB/s algorithmic", flush=True)
+    for t in toks:
+        _lib.check(L.snd_debug_set(int(t.rstrip("p")) << 16))
+        ms = bench.time_launches(lambda sp: launch(t.endswith("p"), sp), args.reps)
+        print(f"skip {t}: {ms * 1e3:8.1f} us  {byts / (ms * 1e-3) / 1e12:5.2f} TB/s algorithmic", flush=True)
     _lib.check(L.snd_debug_set(0))
 
 
