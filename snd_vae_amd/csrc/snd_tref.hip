@@ -213,45 +213,65 @@ __global__ void __launch_bounds__(HB_T) tref_head_bwd_kernel(TrefHeadBwdArgs a) 
 }
 
 // ------------------------------------------------------------------ proj fwd
-__global__ void __launch_bounds__(64) tref_proj_fwd_kernel(TrefProjFwdArgs a) {
+// Block = 64 column quads x 4 waves; wave w sums latent rows [w L / 4, (w + 1) L / 4)
+// (one wave per SIMD was too few loads in flight), wave 0 adds the other waves'
+// partials in wave order and stores: J = b_p + ((S_0 + S_1) + S_2) + S_3.
+constexpr int PF_W = 4;
+__global__ void __launch_bounds__(64 * PF_W) tref_proj_fwd_kernel(TrefProjFwdArgs a) {
   __shared__ float zs[128 * B8];          // [l][8]
-  for (int i = threadIdx.x; i < a.L * B8; i += 64) {
+  __shared__ float4 part[PF_W - 1][B8][64];
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  for (int i = threadIdx.x; i < a.L * B8; i += 64 * PF_W) {
     const int l = i >> 3, b = i & 7;
     zs[i] = b < a.B ? a.z[b * a.L + l] : 0.f;
   }
   __syncthreads();
-  const long long c4 = 4LL * ((long long)blockIdx.x * 64 + threadIdx.x);
-  if (c4 >= a.Cp) return;
+  const long long c4 = 4LL * ((long long)blockIdx.x * 64 + lane);
+  const bool live = c4 < a.Cp;            // a dead lane still reaches the barrier
   float4 acc[B8];
-  const float4 bias = *reinterpret_cast<const float4*>(a.bp + c4);
 #pragma unroll
-  for (int b = 0; b < B8; ++b) acc[b] = bias;
-  const float* wcol = a.wp + c4;
-  int l = 0;
-  constexpr int U = 20;                  // one wave per SIMD: keep 20 KB of loads in flight
-  for (; l + U - 1 < a.L; l += U) {
-    float4 w[U];
+  for (int b = 0; b < B8; ++b) acc[b] = make_float4(0.f, 0.f, 0.f, 0.f);
+  const float* wcol = a.wp + (live ? c4 : 0);
+  const int l1 = (w + 1) * a.L / PF_W;
+  int l = w * a.L / PF_W;
+  constexpr int U = 10;
+  for (; l + U - 1 < l1; l += U) {
+    float4 wv[U];
 #pragma unroll
-    for (int u = 0; u < U; ++u) w[u] = *reinterpret_cast<const float4*>(wcol + (long long)(l + u) * a.Cp);
+    for (int u = 0; u < U; ++u) wv[u] = *reinterpret_cast<const float4*>(wcol + (long long)(l + u) * a.Cp);
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const float4 z0 = *reinterpret_cast<const float4*>(zs + (l + u) * B8);
       const float4 z1 = *reinterpret_cast<const float4*>(zs + (l + u) * B8 + 4);
-      fma4(acc[0], z0.x, w[u]); fma4(acc[1], z0.y, w[u]); fma4(acc[2], z0.z, w[u]);
-      fma4(acc[3], z0.w, w[u]); fma4(acc[4], z1.x, w[u]); fma4(acc[5], z1.y, w[u]);
-      fma4(acc[6], z1.z, w[u]); fma4(acc[7], z1.w, w[u]);
+      fma4(acc[0], z0.x, wv[u]); fma4(acc[1], z0.y, wv[u]); fma4(acc[2], z0.z, wv[u]);
+      fma4(acc[3], z0.w, wv[u]); fma4(acc[4], z1.x, wv[u]); fma4(acc[5], z1.y, wv[u]);
+      fma4(acc[6], z1.z, wv[u]); fma4(acc[7], z1.w, wv[u]);
     }
   }
-  for (; l < a.L; ++l) {
-    const float4 w = *reinterpret_cast<const float4*>(wcol + (long long)l * a.Cp);
+  for (; l < l1; ++l) {
+    const float4 wq = *reinterpret_cast<const float4*>(wcol + (long long)l * a.Cp);
     const float4 z0 = *reinterpret_cast<const float4*>(zs + l * B8);
     const float4 z1 = *reinterpret_cast<const float4*>(zs + l * B8 + 4);
-    fma4(acc[0], z0.x, w); fma4(acc[1], z0.y, w); fma4(acc[2], z0.z, w); fma4(acc[3], z0.w, w);
-    fma4(acc[4], z1.x, w); fma4(acc[5], z1.y, w); fma4(acc[6], z1.z, w); fma4(acc[7], z1.w, w);
+    fma4(acc[0], z0.x, wq); fma4(acc[1], z0.y, wq); fma4(acc[2], z0.z, wq); fma4(acc[3], z0.w, wq);
+    fma4(acc[4], z1.x, wq); fma4(acc[5], z1.y, wq); fma4(acc[6], z1.z, wq); fma4(acc[7], z1.w, wq);
   }
+  if (w > 0)
 #pragma unroll
-  for (int b = 0; b < B8; ++b)
-    if (b < a.B) *reinterpret_cast<float4*>(a.j + (long long)b * a.Cp + c4) = acc[b];
+    for (int b = 0; b < B8; ++b) part[w - 1][b][lane] = acc[b];
+  __syncthreads();
+  if (w > 0 || !live) return;
+  const float4 bias = *reinterpret_cast<const float4*>(a.bp + c4);
+#pragma unroll
+  for (int b = 0; b < B8; ++b) {
+    float4 s = acc[b];
+#pragma unroll
+    for (int v = 0; v < PF_W - 1; ++v) {
+      const float4 o = part[v][b][lane];
+      s.x += o.x; s.y += o.y; s.z += o.z; s.w += o.w;
+    }
+    s.x += bias.x; s.y += bias.y; s.z += bias.z; s.w += bias.w;
+    if (b < a.B) *reinterpret_cast<float4*>(a.j + (long long)b * a.Cp + c4) = s;
+  }
 }
 
 // ------------------------------------------------------------------ proj bwd
@@ -392,7 +412,7 @@ int launch_tref_proj_fwd(const TrefProjFwdArgs& a, hipStream_t s) {
   SND_CHECK_ARG(a.B >= 1 && a.B <= B8 && a.L >= 1 && a.L <= 128 && a.Cp % 4 == 0 && a.Cp > 0,
                 "tref_proj_fwd: B in 1..8, L <= 128, Cp %% 4");
   SND_CHECK_ARG(a.z && a.wp && a.bp && a.j, "tref_proj_fwd: null operand");
-  hipLaunchKernelGGL(tref_proj_fwd_kernel, dim3(cdiv(a.Cp / 4, 64)), dim3(64), 0, s, a);
+  hipLaunchKernelGGL(tref_proj_fwd_kernel, dim3(cdiv(a.Cp / 4, 64)), dim3(64 * PF_W), 0, s, a);
   SND_LAUNCH_CHECK("tref_proj_fwd_kernel");
   return 0;
 }
