@@ -45,9 +45,10 @@
 //   barrier; sum from the ring; store; barrier (the next step's DMAs overwrite
 //   what this step read).  With beta8 <= 288 the step is instead: vmcnt(2)
 //   (slots(s)); barrier; b-e; sum; store -- one barrier per step.
-// LDS (one array): ring 1096 rows x 128 B, a zero row (the slot of list entries
-// past a row's degree), 4 index blocks (16 waves x [meta 8 | row 8 | piece 8]),
-// 2 slot-list buffers (16 waves x 512 B) = 162944 B.  The window of step s+1
+// LDS (one array): ring 1096 rows x 128 B, two zero rows (the slots of list entries
+// past a row's degree; the pair plans pad the odd side with the second),
+// 4 index blocks (16 waves x [meta 8 | row 8 | piece 8]), 2 slot-list buffers
+// (16 waves x 512 B) = 163072 B.  The window of step s+1
 // (e of step s-1) is in flight while step s sums, and e(s) overwrites ring rows
 // 1096 below hi(s+2) + 8 x 15, which no later step reads while 2 beta < 712.
 #include "snd_spmm.hpp"
