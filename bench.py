@@ -91,6 +91,21 @@ def load_traffic(n, d, B, dtype):
     return None
 
 
+def load_spmm_traffic(kern, nnz):
+    """HBM bytes per window-SpMM launch (FETCH x2 + WRITE) from the committed rocprofv3
+    PMC summary of the same batch, if any (profiles/*pmc_spmm_win*.json)."""
+    if not kern.startswith("csr_spmm_bf16_window"):
+        return None
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc_spmm_win.json")), reverse=True):
+        try:
+            j = json.load(open(f))
+        except Exception:
+            continue
+        if f"{nnz} nnz" in j.get("workload", ""):
+            return j.get("hbm_bytes_per_launch")
+    return None
+
+
 def run_workload(cfg, B, args, info, steps=None, warmup=None):
     """Build B graphs per GPU, capture one full step in a HIP graph, time `steps` replays."""
     import torch
@@ -251,7 +266,7 @@ def spmm_batched(host, width, copies, reps):
     gbs = byts / (ms * 1e-3) / 1e9
     return {"kernel": kern, "bound": "hbm", "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
             "frac": round(gbs / PEAK_HBM_GBS, 4), "avg_launch_ms": round(ms, 5),
-            "bytes_per_launch": byts, "previous_variant": prev}
+            "bytes_per_launch": byts, "traffic": load_spmm_traffic(kern, len(ci)), "previous_variant": prev}
 
 
 def extra_workload(name, args, info):
