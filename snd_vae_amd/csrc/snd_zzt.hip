@@ -874,17 +874,17 @@ __global__ void __launch_bounds__(NTH) zzt_dense_f32(ZztArgs a) {
 //                                    (its column i is on the lane), B = z^T
 //                                    (LDS, j order permuted to match)
 // Epilogue per logit (EPI 0), y = -x:
-//   e = 2^y; q = 1 + e; s = 1/q = sigmoid(x); per PAIR of logits one
-//   log2(q_a q_b); #{x > 0} = #{sign(y)}: sign bytes of 4 logits gathered by two
+//   e = 2^y; q = 1 + e; s = 1/q = sigmoid(x); per QUAD of logits one
+//   log2(q_a q_b q_c q_d); #{x > 0} = #{sign(y)}: sign bytes of 4 logits gathered by two
 //   v_perm and popcounted (1 op per logit instead of a compare + SALU ballot).
 // softplus2(x) = x + log2(q) with sum_j x_ij = z_i . colsum (analytic): no |x|
 // and no select per logit.  sigmoid(x) = 1 / (1 + 2^-x) is exact and finite for
-// every x (q = inf -> 0).  A pair product overflows only when x_a + x_b < -128
-// (L_a + L_b < -88.7): that lane recomputes the block's loss terms in the |x|
+// every x (q = inf -> 0).  A quad product overflows only when x_a + .. + x_d < -128
+// (L_a + .. + L_d < -88.7): that lane recomputes the block's loss terms in the |x|
 // form (one wave-uniform test per block when nothing overflows).
 // Measured rates (tools/micro/valu_rate.hip, 4 waves per SIMD): a transcendental
 // costs ~3.4 FMAs of issue and does not co-issue with them; compare + ballot ~2
-// FMAs.  EPI 0 (2.5 transcendentals + ~2.5 other ops per logit) beats v3's |x|
+// FMAs.  EPI 0 (2.25 transcendentals + ~2.5 other ops per logit) beats v3's |x|
 // form (EPI 1: 2.125 + ~6.9).  c (kZ4C) stays a parameter: a nonzero c needs the
 // ballot count (y < -c) back.
 // Tiles are triple-buffered (global loads two tiles ahead).  MODE 1 issues tile
@@ -1065,9 +1065,10 @@ __global__ void __launch_bounds__(NTH2) zzt_dense_bf16_v4(ZztArgs a) {
         lcnt += (unsigned)__builtin_popcount((t01 | t23) & 0x80808080u);
       }
 #pragma unroll
-      for (int p = 0; p < 8; ++p) lt += __builtin_amdgcn_logf(q[2 * p] * q[2 * p + 1]);
+      for (int p = 0; p < 4; ++p)   // one log2 per 4 logits (an overflowing product: fallback below)
+        lt += __builtin_amdgcn_logf((q[4 * p] * q[4 * p + 1]) * (q[4 * p + 2] * q[4 * p + 3]));
       if (__builtin_expect(!__builtin_isfinite(lt), 0)) {
-        // a pair product overflowed: this lane's block again in the |x| form,
+        // a quad product overflowed: this lane's block again in the |x| form,
         // log2(q) = max(-x, 0) - c + log2(1 + 2^-|x|) per logit (exact for every x)
         lt = 0.f;
 #pragma unroll

@@ -326,7 +326,7 @@ def test_zzt_ce_bf16(n, d, B, scale):
 
 
 def test_zzt_ce_bf16_extreme_logits():
-    """Planted blocks of logits far beyond the v4 pair-product range (L = -100 between
+    """Planted blocks of logits far beyond the v4 quad-product range (L = -100 between
     rows 0-3 and 4-7, +100 inside each block): the overflow fallback keeps the CE exact."""
     from snd_vae_amd import layers
     n, d, B = 200, 64, 2
