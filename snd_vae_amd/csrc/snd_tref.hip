@@ -104,13 +104,18 @@ __global__ void __launch_bounds__(HF_T) tref_head_fwd_kernel(TrefHeadFwdArgs a, 
         fma4(acc[6], g1.z, w[u]); fma4(acc[7], g1.w, w[u]);
       }
     }
-    for (; kk < nk; kk += RPI) {
-      const float4 w = *reinterpret_cast<const float4*>(wrow);
-      wrow += wstep;
-      const float4 g0 = *reinterpret_cast<const float4*>(sm + kk * B8);
-      const float4 g1 = *reinterpret_cast<const float4*>(sm + kk * B8 + 4);
-      fma4(acc[0], g0.x, w); fma4(acc[1], g0.y, w); fma4(acc[2], g0.z, w); fma4(acc[3], g0.w, w);
-      fma4(acc[4], g1.x, w); fma4(acc[5], g1.y, w); fma4(acc[6], g1.z, w); fma4(acc[7], g1.w, w);
+    // the last < 8 rows: all loads issued before the first FMA (one memory round trip)
+    float4 w[7];
+#pragma unroll
+    for (int u = 0; u < 7; ++u)
+      w[u] = kk + u * RPI < nk ? *reinterpret_cast<const float4*>(wrow + u * wstep) : f4(0.f);
+#pragma unroll
+    for (int u = 0; u < 7; ++u) {
+      if (kk + u * RPI >= nk) break;
+      const float4 g0 = *reinterpret_cast<const float4*>(sm + (kk + u * RPI) * B8);
+      const float4 g1 = *reinterpret_cast<const float4*>(sm + (kk + u * RPI) * B8 + 4);
+      fma4(acc[0], g0.x, w[u]); fma4(acc[1], g0.y, w[u]); fma4(acc[2], g0.z, w[u]); fma4(acc[3], g0.w, w[u]);
+      fma4(acc[4], g1.x, w[u]); fma4(acc[5], g1.y, w[u]); fma4(acc[6], g1.z, w[u]); fma4(acc[7], g1.w, w[u]);
     }
   }
   __syncthreads();
@@ -248,12 +253,19 @@ __global__ void __launch_bounds__(64 * PF_W) tref_proj_fwd_kernel(TrefProjFwdArg
       fma4(acc[6], z1.z, wv[u]); fma4(acc[7], z1.w, wv[u]);
     }
   }
-  for (; l < l1; ++l) {
-    const float4 wq = *reinterpret_cast<const float4*>(wcol + (long long)l * a.Cp);
-    const float4 z0 = *reinterpret_cast<const float4*>(zs + l * B8);
-    const float4 z1 = *reinterpret_cast<const float4*>(zs + l * B8 + 4);
-    fma4(acc[0], z0.x, wq); fma4(acc[1], z0.y, wq); fma4(acc[2], z0.z, wq); fma4(acc[3], z0.w, wq);
-    fma4(acc[4], z1.x, wq); fma4(acc[5], z1.y, wq); fma4(acc[6], z1.z, wq); fma4(acc[7], z1.w, wq);
+  {   // the last < U rows: all loads issued before the first FMA
+    float4 wr[U - 1];
+#pragma unroll
+    for (int u = 0; u < U - 1; ++u)
+      wr[u] = l + u < l1 ? *reinterpret_cast<const float4*>(wcol + (long long)(l + u) * a.Cp) : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int u = 0; u < U - 1; ++u) {
+      if (l + u >= l1) break;
+      const float4 z0 = *reinterpret_cast<const float4*>(zs + (l + u) * B8);
+      const float4 z1 = *reinterpret_cast<const float4*>(zs + (l + u) * B8 + 4);
+      fma4(acc[0], z0.x, wr[u]); fma4(acc[1], z0.y, wr[u]); fma4(acc[2], z0.z, wr[u]); fma4(acc[3], z0.w, wr[u]);
+      fma4(acc[4], z1.x, wr[u]); fma4(acc[5], z1.y, wr[u]); fma4(acc[6], z1.z, wr[u]); fma4(acc[7], z1.w, wr[u]);
+    }
   }
   if (w > 0)
 #pragma unroll
