@@ -39,21 +39,29 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def cpu_baseline(n_nodes, latent, budget_s):
-    """Reference-formula CPU path on a bounded sample (one N-node graph per step)."""
+def _cpu_quota():
+    """CPUs the cgroup grants this process (cpu.max), or None when unlimited/unknown."""
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()
+        return None if q == "max" else round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        return None
+
+
+def cpu_leg(cfg, budget_s, max_steps=1000):
+    """Reference-formula CPU path (oracle/ref_torch.py) on one graph of `cfg` per step:
+    2 warm-up steps, then steps for ~budget_s; median and mean step time."""
     import numpy as np
     import torch
 
     from oracle import ref_torch as T
-    from snd_vae_amd.config import tscale
     from snd_vae_amd.data import synthetic_batch
     from snd_vae_amd.params import init_blocks
 
-    cores = max(1, min(len(os.sched_getaffinity(0)), int(os.environ.get("OMP_NUM_THREADS", "16"))))
-    torch.set_num_threads(cores)
-    cfg = tscale(n_nodes, latent)
+    n, lat = cfg.n_nodes, cfg.latent
     b = synthetic_batch(cfg, 1, seed=777)
-    eps = np.random.default_rng(0).standard_normal((n_nodes, latent))
+    eps_rows = 1 if cfg.topology == "tref" else n
+    eps = np.random.default_rng(0).standard_normal((eps_rows, lat))
     tensors = T.to_tensors(([b.dense_adj(0)], b.features, b.feature_truth, b.spatial_truth, eps),
                            cfg, torch.float32)
     p = T.build_params(init_blocks(cfg, 0), torch.float32)
@@ -65,18 +73,37 @@ def cpu_baseline(n_nodes, latent, budget_s):
         opt.step()
 
     t0 = time.perf_counter()
-    step()                                  # warm-up (allocations)
-    first = time.perf_counter() - t0
-    n, t0 = 0, time.perf_counter()
-    while n < 1000 and (n == 0 or time.perf_counter() - t0 + first < budget_s):
+    for _ in range(2):                      # warm-up (allocations), BASELINE.md
         step()
-        n += 1
-    dt = time.perf_counter() - t0
-    return {"value": n / dt, "unit": "graphs/s", "cores": cores, "kind": "port",
-            "sample": f"{n} train steps x 1 graph (N={n_nodes}, d={latent}) after 1 warm-up; "
-                      "reference-formula torch-CPU fp32 (dense A@(XW), [N,N,2] logits + softmax-CE, "
-                      "autograd, TF1 Adam); TF unavailable",
-            "ms_per_graph": 1000 * dt / n}
+    first = (time.perf_counter() - t0) / 2
+    times = []
+    t0 = time.perf_counter()
+    while len(times) < max_steps and (len(times) < 5 or time.perf_counter() - t0 + first < budget_s):
+        t1 = time.perf_counter()
+        step()
+        times.append(time.perf_counter() - t1)
+    med = float(np.median(times))
+    return {"graphs_per_s": round(1.0 / med, 4), "ms_per_graph_median": round(1000 * med, 3),
+            "ms_per_graph_mean": round(1000 * float(np.mean(times)), 3), "steps": len(times)}
+
+
+def cpu_baseline(n_nodes, latent, budget_s):
+    """The reference-formula CPU path on a bounded sample, threads =
+    len(os.sched_getaffinity(0)): C2 (the headline's N, d) and C1."""
+    import torch
+
+    from snd_vae_amd.config import PRESETS, tscale
+    cores = len(os.sched_getaffinity(0))
+    torch.set_num_threads(cores)
+    c2 = cpu_leg(tscale(n_nodes, latent), budget_s)
+    c1 = cpu_leg(PRESETS["C1"], min(budget_s, 5.0))
+    return {"value": c2["graphs_per_s"], "unit": "graphs/s", "cores": cores, "kind": "port",
+            "cgroup_cpu_quota": _cpu_quota(),
+            "sample": f"{c2['steps']} train steps x 1 graph (N={n_nodes}, d={latent}) after 2 warm-up, "
+                      "median step; reference-formula CPU path (TF unavailable): torch-CPU fp32, dense "
+                      "A@(XW), [N,N,2] logits + softmax-CE, autograd, TF1 Adam",
+            "ms_per_graph": c2["ms_per_graph_median"], "C2": c2,
+            "C1": dict(c1, config="N=200, d=16, graph latent (tref), F_in=1")}
 
 
 def load_traffic(n, d, B, dtype):
@@ -106,8 +133,14 @@ def load_spmm_traffic(kern, nnz):
     return None
 
 
-def run_workload(cfg, B, args, info, steps=None, warmup=None):
-    """Build B graphs per GPU, capture one full step in a HIP graph, time `steps` replays."""
+def run_workload(cfg, B, args, info, steps=None, warmup=None, dtype=None, reset_state=False):
+    """Build B graphs per GPU, capture one full step in a HIP graph, time `steps` replays.
+
+    reset_state: every timed replay starts from the state after the first step
+    (parameters, Adam moments, step counter copied back on the stream before the
+    replay; the replay alone is timed by HIP events around it).  For C4, whose
+    reference dynamics overflow within a few steps at N = 4096: the
+    timed steps then run on finite losses, the kernels' common path."""
     import torch
 
     from snd_vae_amd.data import default_tile_rows, synthetic_batch
@@ -120,7 +153,7 @@ def run_workload(cfg, B, args, info, steps=None, warmup=None):
         f"{cfg.node_h_size}, latent {cfg.latent})")
     host = synthetic_batch(cfg, B, seed=1000 + info.rank * B)
     db = DeviceBatch(host, tile_rows=0 if args.no_tiles else default_tile_rows(cfg.g_conv_hidden[1]))
-    model = SGCNModelVAE(cfg, B, dtype=args.dtype)
+    model = SGCNModelVAE(cfg, B, dtype=args.dtype if dtype is None else dtype)
     opt = OptimizerVAE(model, process_group=info.group)
     opt.step(db)          # first step (counts as warm-up): the ELBO of the initial weights
     torch.cuda.synchronize()
@@ -130,6 +163,28 @@ def run_workload(cfg, B, args, info, steps=None, warmup=None):
     else:
         opt.capture(db, warmup=2)
         run = opt.replay
+    _LIVE.append((model, opt, db))
+    if reset_state:
+        state = [t.clone() for t in (model.params, opt.m, opt.v, opt.step_counter)]
+
+        def restore():
+            for dst, src in zip((model.params, opt.m, opt.v, opt.step_counter), state):
+                dst.copy_(src, non_blocking=True)
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+              for _ in range(steps)]
+        for _ in range(warmup):
+            restore()
+            run()
+        for e0, e1 in ev:
+            restore()          # ~the parameter bytes of copies: the replay is queued behind them
+            e0.record()
+            run()
+            e1.record()
+        torch.cuda.synchronize()
+        dt = sum(e0.elapsed_time(e1) for e0, e1 in ev) / 1000.0
+        dt = max_over_ranks(dt, info, device=f"cuda:{info.local_rank}")
+        log(f"[rank {info.rank}] state-reset timing done, loss terms {opt.loss_dict()}")
+        return B * info.world * steps / dt, 1000.0 * dt / steps, model, opt, db, host
     for _ in range(warmup):
         run()
     torch.cuda.synchronize()
@@ -148,7 +203,6 @@ def run_workload(cfg, B, args, info, steps=None, warmup=None):
     torch.cuda.synchronize()
     barrier()
     dt = max_over_ranks(time.perf_counter() - t0, info, device=f"cuda:{info.local_rank}")
-    _LIVE.append((model, opt, db))
     return B * info.world * steps / dt, 1000.0 * dt / steps, model, opt, db, host
 
 
@@ -277,7 +331,8 @@ def extra_workload(name, args, info):
     B = {"C4": args.graphs_per_gpu, "C5": 1}[name]
     steps = max(5, args.steps // 5)
     value, ms, model, opt, db, host = run_workload(cfg, B, args, info, steps=steps,
-                                                   warmup=min(args.warmup, 5))
+                                                   warmup=min(args.warmup, 5),
+                                                   reset_state=cfg.topology == "tref")
     kms = kernel_timer(model, db.c_struct(), max(4, args.kernel_reps // 4))
     N, dj = cfg.n_nodes, cfg.node_h_size
     res = {"value": round(value, 3), "unit": "graphs/s", "ms_per_step": round(ms, 4),
@@ -286,10 +341,14 @@ def extra_workload(name, args, info):
            "losses_first_step": opt.first_losses,
            "losses": {k: round(v, 6) for k, v in opt.loss_dict().items()}}
     if cfg.topology == "tref":
+        res["timing"] = ("each timed HIP-graph replay starts from the state after the first step "
+                         "(params, Adam moments, step counter copied back outside the HIP events): "
+                         "the timed steps run on finite losses")
         res["losses_note"] = ("reference dynamics: TF1 Adam (lr 1e-3) moves all N*W = "
                               f"{cfg.n_nodes * cfg.enc_width} fan-in weights of the graph-latent head by ~lr per step, "
                               "so h and logstd grow by O(100) per step and the KL overflows within a few "
-                              "steps at N = 4096 (the reference model was built for N ~ 25)")
+                              "steps at N = 4096 (the reference model was built for N ~ 25); 'losses' is "
+                              "the last timed step, from the reset state")
     kern = {}
     zms = kms("zzt_dense")
     zfl = 4.0 * N * N * dj * B
@@ -333,6 +392,8 @@ def main():
                          "(the N>1 step, captured in the HIP graph) anyway")
     ap.add_argument("--spmm-copies", type=int, default=32,
                     help="secondary roofline: SpMM over this many copies of the batch (8 x 32 graphs)")
+    ap.add_argument("--no-modes", action="store_true",
+                    help="skip the fp32-mode and 1-graph (C3 per-rank) step timings")
     ap.add_argument("--extra", default="C4,C5",
                     help="other BASELINE configs timed after the headline (1 GPU only): C4,C5")
     args = ap.parse_args()
@@ -402,6 +463,22 @@ def main():
                      "avg_launch_ms": round(spmm_ms, 5), "bytes_per_launch": spmm_bytes}),
         "losses": {k: round(v, 6) for k, v in losses.items()},
     }
+    from snd_vae_amd.build import lib_status
+    out["build"] = lib_status()
+    if info.world == 1 and not args.no_modes:
+        # the same step in the fp32 parity mode (generic engine), and C3's per-rank work:
+        # one N=4096 graph per GPU (global batch 8 over 8 GPUs = strong scaling)
+        del_models()
+        v32, ms32, *_ = run_workload(cfg, B, args, info, steps=max(5, args.steps // 5),
+                                     warmup=min(args.warmup, 3), dtype="f32")
+        out["fp32_mode"] = {"value": round(v32, 3), "unit": "graphs/s", "ms_per_step": round(ms32, 4),
+                            "graphs_per_gpu": B, "note": "the parity mode (fp32 operands, generic engine)"}
+        del_models()
+        v1, ms1, *_ = run_workload(cfg, 1, args, info, steps=args.steps, warmup=args.warmup)
+        out["strong"] = {"workload": "C3 per rank: 1 graph (N=4096, d=64) per GPU, bf16, HIP-graph replay",
+                         "graphs_per_gpu": 1, "value": round(v1, 3), "unit": "graphs/s",
+                         "ms_per_step": round(ms1, 4)}
+        del_models()
     extra = [w for w in args.extra.split(",") if w] if info.world == 1 else []
     if extra:
         out["workloads"] = {}

@@ -151,7 +151,7 @@ def model_type_groups(model_type, beta=1.0, gamma=1.0, c=0.0):
     if model_type in ("disentangled", "geoGCN", "posGCN"):
         return {"s": {"w_kl": beta}, "g": {"w_kl": beta}, "sg": {"w_kl": beta}}
     if model_type == "disentangled_C":
-        return {"s": {"w_kl": 1.0}, "g": {"w_kl": 1.0}, "sg": {"cap_gamma": gamma, "cap_c": c}}
+        return {"s": {"w_kl": 1.0}, "g": {"w_kl": 1.0}, "sg": {"w_kl": 0.0, "cap_gamma": gamma, "cap_c": c}}
     if model_type == "NED-VAE-IP":
         d = {"w_kl": 1.0, "w_dip": beta, "lambda_od": 10.0, "lambda_d": 100.0}
         return {"s": dict(d), "g": dict(d), "sg": dict(d)}

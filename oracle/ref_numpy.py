@@ -105,41 +105,64 @@ def per_graph_conv_bwd(x, w, dy, n):
 
 # ----------------------------------------------------------------- adjacency
 def spmm(adj, h, n):
-    """Block-diagonal A @ H with a list of dense per-graph adjacencies."""
-    return np.concatenate([adj[b] @ h[b * n:(b + 1) * n] for b in range(len(adj))])
+    """Block-diagonal A @ H with a list of per-graph adjacencies (dense arrays or
+    scipy sparse matrices: the same product, O(nnz h) for the latter)."""
+    return np.concatenate([np.asarray(adj[b] @ h[b * n:(b + 1) * n]) for b in range(len(adj))])
 
 
-def adj_ce(J, adj, n, pos_weight=1.0, norm=1.0):
+def _dense_rows(A, lo, hi):
+    if hasattr(A, "tocsr"):
+        return A[lo:hi].toarray().astype(np.float64)
+    return A[lo:hi]
+
+
+def adj_ce(J, adj, n, pos_weight=1.0, norm=1.0, row_chunk=None, amb_tol=None):
     """Sum over graphs of the 2-class CE with the diagonal rule, plus dJ.
 
     Returns (ce_sum, dJ_of_sum, n_correct).  ce_sum / (B N^2) is adj_cost.
+    The per-pair gradient g is symmetric (L and A are), so dJ = (g + g^T) J =
+    2 g J; ``row_chunk`` rows of L at a time bound the memory (N = 16384: a
+    dense L is 2 GB in float64), and ``adj`` may hold scipy sparse matrices.
+    ``amb_tol``: also return the number of off-diagonal pairs with |L| < amb_tol
+    (pairs whose argmax may flip under rounding) as a fourth value.
     """
-    ce, correct = 0.0, 0
+    ce, correct, amb = 0.0, 0, 0
     dJ = np.zeros_like(J)
+    rc = n if row_chunk is None else row_chunk
     for b, A in enumerate(adj):
         Jb = J[b * n:(b + 1) * n]
-        L = Jb @ Jb.T
-        off = ~np.eye(n, dtype=bool)
-        sp = softplus(L)
-        # pos_weight * A * softplus(-L) + (1 - A) * softplus(L); == sp - A L at pw=1
-        term = (pos_weight * A * (sp - L) + (1.0 - A) * sp) * norm
-        ce += term[off].sum() + n * SOFTPLUS_M1 * norm
-        g = norm * (sigmoid(L) * (1.0 + A * (pos_weight - 1.0)) - A * pos_weight)
-        g[~off] = 0.0
-        dJ[b * n:(b + 1) * n] = (g + g.T) @ Jb
-        pred = (L > 0) & off                  # argmax(softmax(0, L)), tie -> 0
-        correct += int((pred == (A > 0)).sum())
+        for lo in range(0, n, rc):
+            hi = min(n, lo + rc)
+            L = Jb[lo:hi] @ Jb.T
+            Ab = _dense_rows(A, lo, hi)
+            off = np.ones(L.shape, dtype=bool)
+            off[np.arange(hi - lo), np.arange(lo, hi)] = False
+            sp = softplus(L)
+            # pos_weight * A * softplus(-L) + (1 - A) * softplus(L); == sp - A L at pw=1
+            term = (pos_weight * Ab * (sp - L) + (1.0 - Ab) * sp) * norm
+            ce += term[off].sum() + (hi - lo) * SOFTPLUS_M1 * norm
+            g = norm * (sigmoid(L) * (1.0 + Ab * (pos_weight - 1.0)) - Ab * pos_weight)
+            g[~off] = 0.0
+            dJ[b * n + lo:b * n + hi] = 2.0 * (g @ Jb)
+            pred = (L > 0) & off                  # argmax(softmax(0, L)), tie -> 0
+            correct += int((pred == (Ab > 0)).sum())
+            if amb_tol is not None:
+                amb += int(((np.abs(L) < amb_tol) & off).sum())
+    if amb_tol is not None:
+        return ce, dJ, correct, amb
     return ce, dJ, correct
 
 
 # ----------------------------------------------------------------- model
 def forward_backward(p: Dict[str, np.ndarray], adj, X, Xf, S, eps, cfg,
-                     want_grads=True):
+                     want_grads=True, row_chunk=None, amb_tol=None):
     """One training step's forward + hand-derived backward.
 
-    adj: list of B dense [N,N] 0/1 arrays; X [B*N, f_in]; Xf [B*N, nf];
+    adj: list of B [N,N] 0/1 adjacencies (dense arrays, or scipy sparse for
+    large N with ``row_chunk``, see adj_ce); X [B*N, f_in]; Xf [B*N, nf];
     S [B*N, 2]; eps [B*N, L] (tscale) or [B, L] (tref, model_joint.py:89).
-    Returns (losses dict, grads dict, cache).
+    Returns (losses dict, grads dict, cache); with ``amb_tol`` the losses hold
+    ``ambiguous`` = #{off-diagonal |L| < amb_tol}.
     """
     n = cfg.n_nodes
     R = X.shape[0]
@@ -149,7 +172,7 @@ def forward_backward(p: Dict[str, np.ndarray], adj, X, Xf, S, eps, cfg,
     s1 = cfg.s_d_channel[0]
     f64 = lambda a: np.asarray(a, np.float64)
     X, Xf, S, eps = f64(X), f64(Xf), f64(S), f64(eps)
-    adj = [f64(a) for a in adj]
+    adj = [a if hasattr(a, "tocsr") else f64(a) for a in adj]
     c = BN_C
 
     # ---- encoder (model.py:104-115)
@@ -179,7 +202,8 @@ def forward_backward(p: Dict[str, np.ndarray], adj, X, Xf, S, eps, cfg,
         J = z
 
     # ---- structure decoder + CE (layers.py:407-409, optimizer.py:144)
-    ce_sum, dJ_adj_sum, correct = adj_ce(J, adj, n, cfg.pos_weight, cfg.norm)
+    ce_out = adj_ce(J, adj, n, cfg.pos_weight, cfg.norm, row_chunk=row_chunk, amb_tol=amb_tol)
+    ce_sum, dJ_adj_sum, correct = ce_out[:3]
     adj_cost = ce_sum / (B * n * n)
     acc = correct / (B * n * n)
 
@@ -206,6 +230,8 @@ def forward_backward(p: Dict[str, np.ndarray], adj, X, Xf, S, eps, cfg,
     cost = adj_cost + node_cost + spatial_cost + cfg.beta * kl
     losses = dict(cost=cost, spatial_cost=spatial_cost, adj_cost=adj_cost,
                   node_cost=node_cost, kl=kl, acc=acc, correct=correct)
+    if amb_tol is not None:
+        losses["ambiguous"] = ce_out[3]
     cache = dict(J=J, mu=mu, s=s, z=z, G=G, h=h, Shat=Shat, Xhat=Xhat,
                  P0=P0, P1=P1, H1=H1, H2=H2, Y1=Y1, U1=U1, U2s=U2s, U3s=U3s,
                  U2n=U2n)

@@ -13,6 +13,7 @@ import dataclasses
 import json
 from typing import Optional
 
+import numpy as np
 import torch
 
 from .config import SNDConfig
@@ -101,14 +102,15 @@ def _lookup(variables: dict, name: str):
     return variables[hits[0]] if hits else None
 
 
-def reference_to_blocks(cfg: SNDConfig, variables: dict, beta1: float = 0.9):
+def reference_to_blocks(cfg: SNDConfig, variables: dict, beta1: float = 0.9, beta2: float = 0.999,
+                        global_step: Optional[int] = None):
     """{TF variable name: array} -> (blocks, adam_m, adam_v, global_step).
 
     blocks / adam_m / adam_v are dicts in the params.py layout (adam_m / adam_v /
     global_step are None when the mapping holds no Adam slots).  Raises on a
     missing variable, a shape mismatch, or BN moving statistics that are not the
-    frozen (0, 1) the hot path assumes."""
-    import numpy as np
+    frozen (0, 1) the hot path assumes, and when Adam slots come without the
+    bias-correction powers (unless ``global_step`` gives the step)."""
 
     from .params import block_shapes, logical_names
     shapes = block_shapes(cfg)
@@ -138,11 +140,41 @@ def reference_to_blocks(cfg: SNDConfig, variables: dict, beta1: float = 0.9):
                 if s is not None and not np.allclose(s, want):
                     raise ValueError(f"{scope}{stat} is not the frozen value {want}: "
                                      "the hot path runs Keras BN in inference mode (SURVEY §0.3)")
-    step = None
-    b1p = _lookup(variables, "beta1_power")
-    if b1p is not None:
-        step = int(round(np.log(float(np.asarray(b1p))) / np.log(beta1)))
+    if global_step is not None:
+        return blocks, m, v, int(global_step)
+    step = _step_from_powers(_lookup(variables, "beta1_power"), _lookup(variables, "beta2_power"),
+                             beta1, beta2)
+    if has_adam and step is None:
+        raise ValueError("reference Adam slots present but no beta1_power / beta2_power: the "
+                         "bias correction of the next step is unknown; pass global_step")
     return blocks, m, v, step
+
+
+# The smallest normal float32: TF keeps the bias-correction powers in float32, so
+# below this a power carries fewer than 24 significant bits (0.9^t at t ~ 830).
+_F32_TINY = float(np.finfo(np.float32).tiny)
+
+
+def _step_from_powers(b1p, b2p, beta1: float, beta2: float) -> Optional[int]:
+    """Completed steps t from TF1 Adam's powers.
+
+    TF1 ``AdamOptimizer`` creates beta1_power = beta1 and multiplies it by beta1
+    after every apply (optimizer.py:125,197), so after t steps it holds
+    beta1^(t+1); the step counter here holds t (Adam's step k uses beta^k).
+    beta1_power leaves the float32 normal range after ~830 steps and flushes to
+    0 near ~980, so the beta2 power (0.999^(t+1), normal until t ~ 87 K) is used
+    whenever beta1_power is subnormal or zero."""
+    for p, beta in ((b1p, beta1), (b2p, beta2)):
+        if p is None:
+            continue
+        val = float(np.asarray(p, dtype=np.float64))
+        if not (val >= _F32_TINY) or val > 1.0:
+            continue
+        return int(round(np.log(val) / np.log(beta))) - 1
+    if b1p is not None or b2p is not None:
+        raise ValueError("beta1_power and beta2_power are both zero or subnormal: the global step "
+                         "cannot be recovered; pass global_step")
+    return None
 
 
 def blocks_to_reference(cfg: SNDConfig, blocks: dict, adam_m: Optional[dict] = None,
@@ -150,7 +182,6 @@ def blocks_to_reference(cfg: SNDConfig, blocks: dict, adam_m: Optional[dict] = N
                         beta1: float = 0.9, beta2: float = 0.999) -> dict:
     """The inverse of reference_to_blocks: {TF variable name: float32 array},
     with the Adam slots, bias-correction powers and frozen BN statistics."""
-    import numpy as np
 
     from .params import logical_names
     out = {}
@@ -163,20 +194,22 @@ def blocks_to_reference(cfg: SNDConfig, blocks: dict, adam_m: Optional[dict] = N
             scope = name[:-len("gamma")]
             out[scope + "moving_mean"] = np.zeros_like(out[name])
             out[scope + "moving_variance"] = np.ones_like(out[name])
-    if global_step is not None:
-        out["beta1_power"] = np.float32(beta1 ** global_step)
-        out["beta2_power"] = np.float32(beta2 ** global_step)
+    if global_step is not None:                      # TF1: beta^(t+1) after t steps
+        out["beta1_power"] = np.float32(beta1 ** (global_step + 1))
+        out["beta2_power"] = np.float32(beta2 ** (global_step + 1))
     return out
 
 
-def load_reference(path: str, model, optimizer=None) -> Optional[int]:
+def load_reference(path: str, model, optimizer=None,
+                   global_step: Optional[int] = None) -> Optional[int]:
     """Load an .npz of reference variables (np.load, allow_pickle=False) into the
     device model (and optimizer); returns the recovered global step."""
-    import numpy as np
     with np.load(path, allow_pickle=False) as z:
         variables = {k: z[k] for k in z.files}
     b1 = optimizer.beta1 if optimizer is not None else model.cfg.adam_beta1
-    blocks, m, v, step = reference_to_blocks(model.cfg, variables, beta1=b1)
+    b2 = optimizer.beta2 if optimizer is not None else model.cfg.adam_beta2
+    blocks, m, v, step = reference_to_blocks(model.cfg, variables, beta1=b1, beta2=b2,
+                                             global_step=global_step)
     model.load_blocks(blocks)
     if optimizer is not None and m is not None:
         lay = model.layout
@@ -190,7 +223,6 @@ def load_reference(path: str, model, optimizer=None) -> Optional[int]:
 
 def save_reference(path: str, model, optimizer=None) -> None:
     """Write the device state under the reference variable names (.npz)."""
-    import numpy as np
     m = v = step = None
     if optimizer is not None:
         m, v = optimizer.state_blocks()

@@ -54,6 +54,15 @@ class GraphBatch:
         rp = self.rowptr.astype(np.int64)
         return rp[n::n] - rp[:-1:n]
 
+    def sparse_adj(self, b: int):
+        """scipy CSR [N, N] adjacency of graph b (local column ids; any N)."""
+        import scipy.sparse as sp
+        n = self.n_nodes
+        lo = b * n
+        rp = self.rowptr[lo:lo + n + 1].astype(np.int64) - int(self.rowptr[lo])
+        cols = self.colidx[int(self.rowptr[lo]):int(self.rowptr[lo + n])].astype(np.int64) - lo
+        return sp.csr_matrix((np.ones(len(cols)), cols, rp), shape=(n, n))
+
     def dense_adj(self, b: int) -> np.ndarray:
         """Dense [N, N] adjacency of graph b (small N only; tests)."""
         n = self.n_nodes

@@ -100,7 +100,7 @@ def group_weights(model_type: str, beta: float = 1.0, gamma: float = 1.0, c: flo
     if model_type in ("disentangled", "geoGCN", "posGCN"):
         return {"s": {"w_kl": beta}, "g": {"w_kl": beta}, "sg": {"w_kl": beta}}
     if model_type == "disentangled_C":
-        return {"s": {"w_kl": 1.0}, "g": {"w_kl": 1.0}, "sg": {"cap_gamma": gamma, "cap_c": c}}
+        return {"s": {"w_kl": 1.0}, "g": {"w_kl": 1.0}, "sg": {"w_kl": 0.0, "cap_gamma": gamma, "cap_c": c}}
     if model_type == "NED-VAE-IP":
         return {k: {"w_kl": 1.0, "w_dip": beta, "lambda_od": 10.0, "lambda_d": 100.0} for k in ("s", "g", "sg")}
     if model_type == "beta-TCVAE":

@@ -206,6 +206,30 @@ class SynDataset:
                           np.ascontiguousarray(x), np.ascontiguousarray(s))
 
 
+def class_balance(n_matrices: int, n_nodes: int, n_ones: int) -> Tuple[float, float]:
+    """(pos_weight, norm) of `main.py:246-247` for ``n_matrices`` N x N 0/1 matrices
+    holding ``n_ones`` ones in all:
+        pos_weight = (M N^2 - sum) / sum,  norm = M N^2 / ((M N^2 - sum) 2)."""
+    total = float(n_matrices) * n_nodes * n_nodes
+    if n_ones <= 0 or n_ones >= total:
+        raise ValueError("class balance needs both zero and nonzero adjacency entries")
+    return (total - n_ones) / n_ones, total / ((total - n_ones) * 2.0)
+
+
+def dataset_class_balance(ds: "SynDataset") -> Tuple[float, float]:
+    """`main.py:246-247` over the spanning-tree adjacency ``adj`` [G*S, N, N] that
+    `main.py:177` reshapes from load_data_syn (the trees, not adj_truth)."""
+    n = ds.n_nodes
+    mats = ones = 0
+    for g in range(ds.n_graphs):
+        for e in ds.trees[g]:
+            mats += 1
+            ones += len(np.unique(np.asarray(e[0], np.int64) * n + np.asarray(e[1], np.int64)))
+    if mats == 0:
+        raise ValueError("the dataset holds no spanning trees (sampling_num=0)")
+    return class_balance(mats, n, ones)
+
+
 def load_data_syn(type_: str, path: str, sampling_num: int = 10, num_feature: int = 1,
                   rng=None, allow_pickle: bool = False, shuffle: bool = True,
                   load_rel: bool = True) -> SynDataset:

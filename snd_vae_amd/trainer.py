@@ -28,7 +28,7 @@ import torch
 from . import checkpoint as ckpt
 from .config import SNDConfig
 from .data import default_tile_rows
-from .input_data import SynDataset
+from .input_data import SynDataset, dataset_class_balance
 from .model import DeviceBatch, SGCNModelVAE
 from .optimizer import LOSS_NAMES, OptimizerVAE
 
@@ -40,7 +40,14 @@ STORER = (("loss", "cost"), ("spatial_loss", "spatial_cost"), ("adj_loss", "adj_
 class Trainer:
     def __init__(self, cfg: SNDConfig, dataset: SynDataset, batch_size: int,
                  dtype: str = "bf16", process_group=None, seed: int = 1234,
-                 use_graphs: bool = True, locality: bool = True, blocks=None, device="cuda"):
+                 use_graphs: bool = True, locality: bool = True, blocks=None, device="cuda",
+                 weighted: bool = False):
+        """weighted: the weighted-BCE structure loss (SURVEY §8 decision ii) with the
+        dataset's pos_weight / norm of `main.py:246-247` over its spanning trees.
+        Off by default, as in the reference, whose loss ignores both (`optimizer.py:144`)."""
+        if weighted:
+            pw, nm = dataset_class_balance(dataset)
+            cfg = cfg.replace(weighted_bce=True, pos_weight=pw, norm=nm)
         world, rank = 1, 0
         if process_group is not None:
             import torch.distributed as dist

@@ -80,7 +80,7 @@ def test_group_reg_numpy_torch_fd(kw):
 def test_model_type_weights_and_capacity():
     assert RD.model_type_groups("base", beta=2.0) == {"sg": {"w_kl": 2.0}}
     g = RD.model_type_groups("disentangled_C", gamma=3.0, c=0.5)
-    assert g["sg"] == {"cap_gamma": 3.0, "cap_c": 0.5} and g["s"] == {"w_kl": 1.0}
+    assert g["sg"] == {"w_kl": 0.0, "cap_gamma": 3.0, "cap_c": 0.5} and g["s"] == {"w_kl": 1.0}
     assert RD.capacity(0, 25.0, 1000, 100000) == 0.0
     assert RD.capacity(250000, 25.0, 1000, 100000) == 25.0
     assert RD.capacity(5500, 25.0, 1000, 100000) == pytest.approx(25.0 * 1000 / 100000 * 5)

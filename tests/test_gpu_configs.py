@@ -1,0 +1,181 @@
+"""BASELINE configurations at their full sizes against the float64 oracle.
+
+The exact bench batch (C2: N=4096, d=64, 8 graphs of seed 1000, the weights of
+init seed 0), C5 (N=16384, d=128, one graph) and C3's per-rank shape (N=4096,
+one graph) run one step through snd_train_step and are compared with
+``oracle.ref_numpy.forward_backward`` on the same inputs (injected eps).  The
+oracle takes scipy-sparse adjacencies and evaluates the N^2 logits in 1024-row
+chunks (a dense float64 L is 2 GB at C5; `layers.py:407-409`,
+`optimizer.py:142-144`).
+
+Tolerances: fp32 mode -- ELBO terms within 1e-5 relative,
+gradient blocks within 2e-4 of max-abs, the accuracy count exact up to the
+off-diagonal pairs with |L| < 1e-4 (argmax under rounding); bf16 mode -- loss
+terms within 2e-2, gradients 1e-1 of max-abs, accuracy within 1e-3.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import ref_numpy as R
+from snd_vae_amd.config import tscale
+from snd_vae_amd.data import synthetic_batch
+from snd_vae_amd.params import init_blocks
+
+pytestmark = pytest.mark.gpu
+TERMS = ("cost", "spatial_cost", "adj_cost", "node_cost", "kl")
+TOL = {"f32": (1e-5, 2e-4), "bf16": (2e-2, 1e-1)}
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu(lib_built):
+    if not torch.cuda.is_available():
+        pytest.fail("GPU tests need a ROCm device")
+
+
+def block_err(g, ref):
+    return np.abs(g - ref).max() / max(np.abs(ref).max(), 1e-30)
+
+
+_CASES = {}
+
+
+def oracle_case(n, d, B, seed):
+    """Inputs and the float64 oracle step of one configuration (cached per module)."""
+    key = (n, d, B, seed)
+    if key not in _CASES:
+        cfg = tscale(n, d)
+        batch = synthetic_batch(cfg, B, seed=seed)
+        p0 = {k: v.astype(np.float32).astype(np.float64) for k, v in init_blocks(cfg, 0).items()}
+        eps = np.random.default_rng(9).standard_normal((B * n, d)).astype(np.float32)
+        adj = [batch.sparse_adj(b) for b in range(B)]
+        ref, rg, _ = R.forward_backward(p0, adj, batch.features, batch.feature_truth,
+                                        batch.spatial_truth, eps.astype(np.float64), cfg,
+                                        row_chunk=1024, amb_tol=1e-4)
+        _CASES[key] = (cfg, batch, p0, eps, ref, rg)
+    return _CASES[key]
+
+
+def run_step(cfg, batch, p0, eps, dtype):
+    from snd_vae_amd.model import DeviceBatch, SGCNModelVAE
+    from snd_vae_amd.optimizer import OptimizerVAE
+    model = SGCNModelVAE(cfg, batch.n_graphs, dtype=dtype, blocks=p0)
+    opt = OptimizerVAE(model, fuse_adam=False)
+    opt.step(DeviceBatch(batch), torch.from_numpy(eps).cuda())
+    torch.cuda.synchronize()
+    return model, opt
+
+
+def check_step(opt, ref, rg, dtype, n_pairs):
+    ltol, gtol = TOL[dtype]
+    got = opt.loss_dict()
+    for k in TERMS:
+        assert got[k] == pytest.approx(ref[k], rel=ltol), (k, got[k], ref[k])
+    if dtype == "f32":   # main.py:334 accuracy, exact away from |L| ~ 0
+        assert abs(got["correct"] - ref["correct"]) <= ref["ambiguous"], (got["correct"], ref)
+    else:
+        assert abs(got["correct"] - ref["correct"]) <= 1e-3 * n_pairs
+    g = opt.grad_blocks()
+    bad = {k: block_err(g[k], rg[k]) for k in rg if block_err(g[k], rg[k]) > gtol}
+    assert not bad, bad
+
+
+@pytest.mark.timeout(400)
+@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+def test_c2_bench_batch_vs_oracle(dtype):
+    """The bench's own batch: synthetic_batch(tscale(4096, 64), 8, seed=1000) (bench.py
+    run_workload at rank 0), init seed 0; bf16 is the benchmarked fast path."""
+    cfg, batch, p0, eps, ref, rg = oracle_case(4096, 64, 8, 1000)
+    _, opt = run_step(cfg, batch, p0, eps, dtype)
+    check_step(opt, ref, rg, dtype, 8 * 4096 * 4096)
+
+
+@pytest.mark.timeout(400)
+@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+def test_c3_per_rank_shape_vs_oracle(dtype):
+    """C3 = 8 graphs on 8 GPUs: each rank steps ONE N=4096 graph (B=1 plan; the zz^T
+    column splits fill the chip), seed 1000 + rank for rank 3."""
+    cfg, batch, p0, eps, ref, rg = oracle_case(4096, 64, 1, 1003)
+    _, opt = run_step(cfg, batch, p0, eps, dtype)
+    check_step(opt, ref, rg, dtype, 4096 * 4096)
+
+
+@pytest.mark.timeout(400)
+@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+def test_c5_step_vs_chunked_oracle(dtype):
+    """C5: N=16384, d=128, one graph (2.7e8 logits), one full step."""
+    cfg, batch, p0, eps, ref, rg = oracle_case(16384, 128, 1, 0)
+    _, opt = run_step(cfg, batch, p0, eps, dtype)
+    check_step(opt, ref, rg, dtype, 16384 * 16384)
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("dtype,scale", [("f32", 0.1), ("bf16", 0.1), ("bf16", 0.4)])
+def test_c5_zzt_ce_vs_chunked_oracle(dtype, scale):
+    """snd_zzt_ce alone at C5 (N=16384, d=128): CE sum, accuracy count and dz against
+    the row-chunked float64 adj_ce; scale 0.4 gives logits up to |L| ~ 40."""
+    from snd_vae_amd import layers
+    n, d = 16384, 128
+    batch = synthetic_batch(tscale(n, d), 1, seed=5)
+    z = (scale * np.random.default_rng(21).standard_normal((n, d))).astype(np.float32)
+    rce, rdz, rcorrect, amb = R.adj_ce(z.astype(np.float64), [batch.sparse_adj(0)], n,
+                                       row_chunk=1024, amb_tol=1e-4)
+    rp = torch.from_numpy(batch.rowptr).cuda()
+    ci = torch.from_numpy(batch.colidx).cuda()
+    ce, correct, dz = layers.inner_product_ce(torch.from_numpy(z).cuda(), 1, rp, ci, dtype=dtype)
+    dz = dz.cpu().numpy()
+    err = np.abs(dz - rdz).max() / np.abs(rdz).max()
+    if dtype == "f32":
+        assert ce == pytest.approx(rce, rel=2e-6)
+        assert abs(correct - rcorrect) <= amb
+        assert err < 1e-5
+    else:
+        assert ce == pytest.approx(rce, rel=2e-3)
+        assert abs(correct - rcorrect) <= 1e-3 * n * n
+        assert err < 2e-2
+
+
+@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+def test_dp_half_batches_sum_to_full_step(dtype):
+    """The data-parallel arithmetic of `optimizer.py:105-119` at world 2 on one GPU: two
+    half-batch plans (ranks 0 and 1, contiguous shards, each drawing its rows of the
+    device Philox stream via snd_plan_set_rng_offset), their flat gradients and loss
+    tails summed as the RCCL all-reduce would, then snd_adam_tf1 with grad_scale 1/2
+    -- against ONE full-batch step: same parameters, moments and global loss means."""
+    from snd_vae_amd import _lib
+    from snd_vae_amd.data import shard
+    from snd_vae_amd.model import DeviceBatch, SGCNModelVAE
+    from snd_vae_amd.optimizer import OptimizerVAE
+    cfg = tscale(512, 64)
+    B = 4
+    batch = synthetic_batch(cfg, B, seed=31)
+    p0 = init_blocks(cfg, 7)
+    full_m = SGCNModelVAE(cfg, B, dtype=dtype, blocks=p0)
+    full = OptimizerVAE(full_m, fuse_adam=False)
+    full.step(DeviceBatch(batch))
+    ranks = []
+    for r in range(2):
+        m = SGCNModelVAE(cfg, B // 2, dtype=dtype, blocks=p0)
+        o = OptimizerVAE(m, fuse_adam=False)
+        _lib.check(_lib.lib().snd_plan_set_rng_offset(m.plan, r * (B // 2) * cfg.n_nodes))
+        o.forward_backward(DeviceBatch(shard(batch, r, 2)))
+        ranks.append((m, o))
+    torch.cuda.synchronize()
+    (m0, o0), (m1, o1) = ranks
+    pc = m0.param_count
+    o0.grads[:pc + 8] += o1.grads[:pc + 8]       # the all-reduce (sum) of grads || loss tail
+    o0.world = 2                                 # grad_scale 1/world in snd_adam_tf1
+    o0.apply()
+    torch.cuda.synchronize()
+    tail = o0.grads[pc:pc + 6].double().cpu().numpy() / 2
+    ref = full.loss_dict()
+    for i, k in enumerate(("cost", "spatial_cost", "adj_cost", "node_cost", "kl", "acc")):
+        assert tail[i] == pytest.approx(ref[k], rel=1e-5, abs=1e-7), k
+    # gradients: the sum over two shards re-associates the full batch's sums
+    g_full = full.grads[:pc].double()
+    g_dp = o0.grads[:pc].double() / 2
+    assert float((g_dp - g_full).abs().max()) <= 1e-4 * float(g_full.abs().max())
+    # Adam normalises each update to ~lr: compare against the step size
+    dp = float((m0.params[:pc] - full_m.params[:pc]).abs().max())
+    assert dp <= 0.05 * cfg.learning_rate, dp
+    assert o0.global_step == full.global_step == 1

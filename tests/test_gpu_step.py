@@ -195,10 +195,25 @@ def test_graph_replay_is_deterministic():
     for _ in range(5):
         o1.step(b1)
     m2, o2, b2 = make(cfg, batch, p0, "bf16")
-    p_init, m_init = m2.params.clone(), o2.m.clone()
+    init = [t.clone() for t in (m2.params, o2.m, o2.v, o2.step_counter)]
+    o2.step(b2)                    # a non-trivial state to capture from (moments, step 1)
+    snap = [t.clone() for t in (m2.params, o2.m, o2.v, o2.step_counter, o2.grads, o2.losses)]
     o2.capture(b2, warmup=2)       # 2 eager warm-up steps + the capture; state restored
-    assert o2.global_step == 0
-    assert torch.equal(m2.params, p_init) and torch.equal(o2.m, m_init)
+    # capture leaves every piece of training state bit-identical
+    for name, a, b in zip(("params", "m", "v", "step", "grads", "losses"), snap,
+                          (m2.params, o2.m, o2.v, o2.step_counter, o2.grads, o2.losses)):
+        assert torch.equal(a, b), name
+    # one replay == one eager step from the same state
+    m3, o3, b3 = make(cfg, batch, p0, "bf16")
+    for dst, src in zip((m3.params, o3.m, o3.v, o3.step_counter), snap):
+        dst.copy_(src)
+    o3.step(b3)
+    o2.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(m2.params, m3.params) and torch.equal(o2.v, o3.v)
+    assert torch.equal(o2.losses, o3.losses)
+    for dst, src in zip((m2.params, o2.m, o2.v, o2.step_counter), init):
+        dst.copy_(src)             # back to the initial state: 5 replays == 5 eager steps
     for _ in range(5):
         o2.replay()
     torch.cuda.synchronize()

@@ -68,12 +68,20 @@ def test_checkpoint_resume(dataset, tmp_path):
     assert torch.equal(a.model.params, b.model.params)
 
 
-def test_first_step_matches_oracle(dataset):
+@pytest.mark.parametrize("weighted", [False, True])
+def test_first_step_matches_oracle(dataset, weighted):
+    """weighted: row a15 -- the weighted-BCE structure loss with the dataset's
+    pos_weight / norm (`main.py:246-247` over the spanning trees)."""
+    from snd_vae_amd.input_data import dataset_class_balance
     from snd_vae_amd.model import DeviceBatch
     from snd_vae_amd.trainer import Trainer
     cfg, ds = dataset
     p0 = {k: v.astype(np.float32).astype(np.float64) for k, v in init_blocks(cfg, 0).items()}
-    t = Trainer(cfg, ds, batch_size=2, dtype="f32", blocks=p0, use_graphs=False)
+    t = Trainer(cfg, ds, batch_size=2, dtype="f32", blocks=p0, use_graphs=False, weighted=weighted)
+    if weighted:
+        pw, nm = dataset_class_balance(ds)
+        assert pw > 1.0 and t.cfg.pos_weight == pw and t.cfg.norm == nm
+        cfg = t.cfg
     hb = ds.batch(cfg, [0, 1])
     eps = np.random.default_rng(4).standard_normal((2 * cfg.n_nodes, cfg.latent)).astype(np.float32)
     t.opt.step(t.batches[0], torch.from_numpy(eps).cuda())

@@ -211,6 +211,41 @@ def test_reference_checkpoint_names_roundtrip(topology):
         checkpoint.reference_to_blocks(cfg, bad)
 
 
+def test_reference_adam_power_convention():
+    """TF1 AdamOptimizer starts beta1_power at beta1 and multiplies after each
+    apply (optimizer.py:125,197): a fresh state (0.9, 0.999) is step 0, a state
+    after t steps holds beta^(t+1).  beta1_power underflows float32 after ~830
+    steps, so the step then comes from beta2_power; slots without any power raise."""
+    import numpy as np
+
+    from snd_vae_amd import checkpoint
+    from snd_vae_amd.config import tscale
+    from snd_vae_amd.params import init_blocks
+    cfg = tscale(24, 4)
+    b = init_blocks(cfg, 1)
+    m = {k: np.zeros_like(a) for k, a in b.items()}
+    ref0 = checkpoint.blocks_to_reference(cfg, b, m, m, global_step=0)
+    assert ref0["beta1_power"] == np.float32(0.9) and ref0["beta2_power"] == np.float32(0.999)
+    fresh = dict(ref0)
+    fresh["beta1_power"] = np.float32(0.9)
+    fresh["beta2_power"] = np.float32(0.999)
+    assert checkpoint.reference_to_blocks(cfg, fresh)[3] == 0
+    for t in (1, 5, 829, 1500, 20000):
+        st = dict(ref0)
+        st["beta1_power"] = np.float32(0.9) ** np.float32(t + 1)     # float32 like TF
+        st["beta2_power"] = np.float32(np.float64(0.999) ** (t + 1))
+        assert checkpoint.reference_to_blocks(cfg, st)[3] == t, t
+    dead = dict(ref0)
+    dead["beta1_power"] = np.float32(0.0)
+    dead["beta2_power"] = np.float32(0.0)
+    with pytest.raises(ValueError, match="global_step"):
+        checkpoint.reference_to_blocks(cfg, dead)
+    assert checkpoint.reference_to_blocks(cfg, dead, global_step=123456)[3] == 123456
+    nopow = {k: a for k, a in ref0.items() if not k.endswith("_power")}
+    with pytest.raises(ValueError, match="global_step"):
+        checkpoint.reference_to_blocks(cfg, nopow)
+
+
 @pytest.mark.parametrize("n,B,kbar", [(500, 3, 8.0), (4096, 2, 16.0), (97, 4, 5.0)])
 def test_window_plan_matches_literal(n, B, kbar):
     """data.window_plan (sliding-window SpMM plan) against a per-row restatement:

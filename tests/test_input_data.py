@@ -167,3 +167,27 @@ def test_checkpoint_roundtrip_metadata(tmp_path):
     m3.params = torch.zeros(m3.param_count)
     with pytest.raises(ValueError, match="layout"):
         ck.restore(fn, m3)
+
+
+def test_class_balance_matches_main_formula(ds_dir):
+    """Row a15: pos_weight / norm of `main.py:246-247`, literally, over the spanning-tree
+    adjacency `adj` [G*S, N, N] of `main.py:177` -- against dataset_class_balance on the
+    sparse ingest (same trees under the same seed)."""
+    from snd_vae_amd.input_data import class_balance, dataset_class_balance
+    cfg, root = ds_dir
+    path = os.path.join(root, "pickled")
+    np.random.seed(1)
+    _, _, trees, _ = literal_load(path, 3)
+    adj = trees.reshape(-1, trees.shape[-2], trees.shape[-1])          # main.py:177
+    pos_weight = float(adj.shape[0] * adj.shape[1] * adj.shape[1] - adj.sum()) / adj.sum()
+    norm = adj.shape[0] * adj.shape[1] * adj.shape[1] / float(
+        (adj.shape[0] * adj.shape[1] * adj.shape[1] - adj.sum()) * 2)
+    np.random.seed(1)
+    ds = load_data_syn("train", path, sampling_num=3, allow_pickle=True)
+    pw, nm = dataset_class_balance(ds)
+    assert pw == pytest.approx(pos_weight, rel=1e-12) and nm == pytest.approx(norm, rel=1e-12)
+    assert class_balance(2, 4, 4) == (7.0, 32 / 56)
+    with pytest.raises(ValueError):
+        class_balance(1, 4, 0)
+    with pytest.raises(ValueError, match="spanning"):
+        dataset_class_balance(load_data_syn("train", path, sampling_num=0, allow_pickle=True))

@@ -136,3 +136,22 @@ def test_c1_fixture_is_the_reference_topology():
     z, cfg, batch, p0 = golden_io.load("tref_c1_n200_d16")
     assert cfg.topology == "tref" and cfg.f_in == 1 and cfg.latent == 100
     assert p0["enc.Wh"].shape == (200 * 17, 100) and p0["dec.Wp"].shape == (100, 200 * 16)
+
+
+def test_adj_ce_chunked_sparse_equals_dense():
+    """adj_ce over scipy-sparse adjacencies in row chunks (the large-N oracle, N = 16384)
+    equals the dense one-shot form: same CE sum, dJ and correct count."""
+    from snd_vae_amd.config import tscale
+    from snd_vae_amd.data import synthetic_batch
+    cfg = tscale(300, 8, mean_degree=8.0)
+    b = synthetic_batch(cfg, 2, seed=3)
+    J = np.random.default_rng(1).standard_normal((600, 8))
+    dense = [b.dense_adj(g).astype(np.float64) for g in range(2)]
+    sparse = [b.sparse_adj(g) for g in range(2)]
+    for g in range(2):
+        assert np.array_equal(sparse[g].toarray(), dense[g])
+    ce0, dj0, c0 = R.adj_ce(J, dense, 300, 1.7, 0.6)
+    ce1, dj1, c1, amb = R.adj_ce(J, sparse, 300, 1.7, 0.6, row_chunk=64, amb_tol=1e-3)
+    assert abs(ce1 - ce0) <= 1e-12 * abs(ce0)
+    np.testing.assert_allclose(dj1, dj0, rtol=1e-12, atol=1e-12)
+    assert c1 == c0 and amb >= 0
