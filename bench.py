@@ -73,8 +73,9 @@ def cpu_leg(cfg, budget_s, max_steps=1000):
         opt.step()
 
     t0 = time.perf_counter()
-    for _ in range(2):                      # warm-up (allocations), BASELINE.md
+    for i in range(2):                      # warm-up (allocations), BASELINE.md
         step()
+        log(f"  cpu warm-up step {i + 1} (N={n}) done")
     first = (time.perf_counter() - t0) / 2
     times = []
     t0 = time.perf_counter()
@@ -82,6 +83,7 @@ def cpu_leg(cfg, budget_s, max_steps=1000):
         t1 = time.perf_counter()
         step()
         times.append(time.perf_counter() - t1)
+        log(f"  cpu step {len(times)}: {1000 * times[-1]:.1f} ms")
     med = float(np.median(times))
     return {"graphs_per_s": round(1.0 / med, 4), "ms_per_graph_median": round(1000 * med, 3),
             "ms_per_graph_mean": round(1000 * float(np.mean(times)), 3), "steps": len(times)}
@@ -93,12 +95,16 @@ def cpu_baseline(n_nodes, latent, budget_s):
     import torch
 
     from snd_vae_amd.config import PRESETS, tscale
-    cores = len(os.sched_getaffinity(0))
+    affinity = len(os.sched_getaffinity(0))
+    quota = _cpu_quota()
+    # threads = len(os.sched_getaffinity(0)) -- capped by the cgroup's CPU
+    # quota when one is set (the CPUs this process may actually run on at once)
+    cores = min(affinity, max(1, int(quota + 0.5))) if quota else affinity
     torch.set_num_threads(cores)
     c2 = cpu_leg(tscale(n_nodes, latent), budget_s)
     c1 = cpu_leg(PRESETS["C1"], min(budget_s, 5.0))
     return {"value": c2["graphs_per_s"], "unit": "graphs/s", "cores": cores, "kind": "port",
-            "cgroup_cpu_quota": _cpu_quota(),
+            "affinity_cpus": affinity, "cgroup_cpu_quota": quota,
             "sample": f"{c2['steps']} train steps x 1 graph (N={n_nodes}, d={latent}) after 2 warm-up, "
                       "median step; reference-formula CPU path (TF unavailable): torch-CPU fp32, dense "
                       "A@(XW), [N,N,2] logits + softmax-CE, autograd, TF1 Adam",
@@ -136,9 +142,9 @@ def load_spmm_traffic(kern, nnz):
 def run_workload(cfg, B, args, info, steps=None, warmup=None, dtype=None, reset_state=False):
     """Build B graphs per GPU, capture one full step in a HIP graph, time `steps` replays.
 
-    reset_state: every timed replay starts from the state after the first step
-    (parameters, Adam moments, step counter copied back on the stream before the
-    replay; the replay alone is timed by HIP events around it).  For C4, whose
+    reset_state: every timed replay starts from the initial state (parameters, Adam
+    moments, step counter copied back on the stream before the replay; the replay
+    alone is timed by HIP events around it), i.e. each timed step is step 1.  For C4, whose
     reference dynamics overflow within a few steps at N = 4096: the
     timed steps then run on finite losses, the kernels' common path."""
     import torch
@@ -155,6 +161,8 @@ def run_workload(cfg, B, args, info, steps=None, warmup=None, dtype=None, reset_
     db = DeviceBatch(host, tile_rows=0 if args.no_tiles else default_tile_rows(cfg.g_conv_hidden[1]))
     model = SGCNModelVAE(cfg, B, dtype=args.dtype if dtype is None else dtype)
     opt = OptimizerVAE(model, process_group=info.group)
+    if reset_state:
+        state = [t.clone() for t in (model.params, opt.m, opt.v, opt.step_counter)]
     opt.step(db)          # first step (counts as warm-up): the ELBO of the initial weights
     torch.cuda.synchronize()
     opt.first_losses = {k: round(v, 6) for k, v in opt.loss_dict().items()}
@@ -165,8 +173,6 @@ def run_workload(cfg, B, args, info, steps=None, warmup=None, dtype=None, reset_
         run = opt.replay
     _LIVE.append((model, opt, db))
     if reset_state:
-        state = [t.clone() for t in (model.params, opt.m, opt.v, opt.step_counter)]
-
         def restore():
             for dst, src in zip((model.params, opt.m, opt.v, opt.step_counter), state):
                 dst.copy_(src, non_blocking=True)
@@ -341,14 +347,14 @@ def extra_workload(name, args, info):
            "losses_first_step": opt.first_losses,
            "losses": {k: round(v, 6) for k, v in opt.loss_dict().items()}}
     if cfg.topology == "tref":
-        res["timing"] = ("each timed HIP-graph replay starts from the state after the first step "
+        res["timing"] = ("each timed HIP-graph replay is step 1: it starts from the initial state "
                          "(params, Adam moments, step counter copied back outside the HIP events): "
                          "the timed steps run on finite losses")
         res["losses_note"] = ("reference dynamics: TF1 Adam (lr 1e-3) moves all N*W = "
                               f"{cfg.n_nodes * cfg.enc_width} fan-in weights of the graph-latent head by ~lr per step, "
                               "so h and logstd grow by O(100) per step and the KL overflows within a few "
                               "steps at N = 4096 (the reference model was built for N ~ 25); 'losses' is "
-                              "the last timed step, from the reset state")
+                              "the last timed step (step 1 again, from the reset state)")
     kern = {}
     zms = kms("zzt_dense")
     zfl = 4.0 * N * N * dj * B

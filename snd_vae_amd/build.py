@@ -36,8 +36,8 @@ def _headers():
 
 def _digest(paths, extra=()):
     h = hashlib.sha256()
-    for e in extra:
-        h.update(e.encode())
+    for e in extra:                      # flags; the include paths differ per checkout
+        h.update((os.path.relpath(e, ROOT) if os.path.isabs(e) else e).encode())
     for p in sorted(paths):
         h.update(os.path.basename(p).encode())
         with open(p, "rb") as f:
