@@ -914,9 +914,9 @@ __global__ void __launch_bounds__(NTH2) zzt_dense_bf16_v4(ZztArgs a) {
   constexpr int CPR = DP / 8, TCPR = TJ2 / 8;
   constexpr int JCH = TJ2 * CPR, TCH = DP * TCPR;
   constexpr int JPT = (JCH + NT - 1) / NT, TPT = (TCH + NT - 1) / NT;
-  constexpr float C4 = EPI == 0 ? kZ4C : 0.f;
+  constexpr float C4 = EPI != 1 ? kZ4C : 0.f;
   static_assert(kZ4C == 0.f, "EPI 0 counts x > 0 by the sign of y = -x - c: c must be 0");
-  constexpr unsigned NEG = EPI == 0 ? 0x80008000u : 0u;   // B operand sign
+  constexpr unsigned NEG = EPI != 1 ? 0x80008000u : 0u;   // B operand sign
   __shared__ __attribute__((aligned(16))) __bf16 lds[3 * BUF];
   __shared__ __attribute__((aligned(16))) __bf16 brows[ROWS * JST];   // (-)z_i rows (scaled)
   __shared__ __attribute__((aligned(16))) __bf16 zown[ROWS * JST];    // z_i rows (z^T values)
@@ -1025,8 +1025,10 @@ __global__ void __launch_bounds__(NTH2) zzt_dense_bf16_v4(ZztArgs a) {
   if (skip & 32) ts[1] = __builtin_amdgcn_s_memrealtime();
 
   f32x16 cinit, acc[CB];
+  // +0 (not -0.0 = -C4 at c = 0): a zero accumulator folds into the MFMA's inline
+  // constant 0; a -0.0 splat pinned 16 VGPRs and cost 24 moves per tile
 #pragma unroll
-  for (int v = 0; v < 16; ++v) cinit[v] = -C4;
+  for (int v = 0; v < 16; ++v) cinit[v] = C4 == 0.f ? 0.f : -C4;
 #pragma unroll
   for (int q = 0; q < CB; ++q)
 #pragma unroll
@@ -1046,7 +1048,7 @@ __global__ void __launch_bounds__(NTH2) zzt_dense_bf16_v4(ZztArgs a) {
   double ltot = 0.0;
   unsigned wcnt = 0, lcnt = 0;   // per wave (EPI 1 ballots) / per lane (EPI 0 sign bits)
   auto epi = [&](const f32x16& Y, bf16x8 (&sA)[2]) {
-    if constexpr (EPI == 0) {
+    if constexpr (EPI != 1) {
       float q[16], lt = 0.f;
 #pragma unroll
       for (int v = 0; v < 16; ++v) {
@@ -1054,6 +1056,21 @@ __global__ void __launch_bounds__(NTH2) zzt_dense_bf16_v4(ZztArgs a) {
         q[v] = e + kZ4Q;
         sA[v >> 3][v & 7] = (__bf16)__builtin_amdgcn_rcpf(q[v]);
       }
+      if constexpr (EPI >= 2) {
+        // pin the packed sigmoids before the overflow test: otherwise the compiler
+        // sinks the 16 reciprocals past its branch, out of reach of the scheduler
+#pragma unroll
+        for (int h2 = 0; h2 < 2; ++h2) {
+          u32x4 t = __builtin_bit_cast(u32x4, sA[h2]);
+          asm volatile("" : "+v"(t));
+          sA[h2] = __builtin_bit_cast(bf16x8, t);
+        }
+      }
+      if constexpr (EPI == 3) {
+        // #{x > 0} = #{y < 0} by compare + ballot (SALU popcount)
+#pragma unroll
+        for (int v = 0; v < 16; ++v) wcnt += (unsigned)__popcll(__ballot(Y[v] < 0.f));
+      } else {
       // #{x > 0} = #{y < 0} (c = 0; y = +0 where x = 0): the sign bytes of four y's
       // gathered by two v_perm, masked, popcounted into a per-lane count
 #pragma unroll
@@ -1063,6 +1080,7 @@ __global__ void __launch_bounds__(NTH2) zzt_dense_bf16_v4(ZztArgs a) {
         const unsigned t23 = __builtin_amdgcn_perm(__float_as_uint(Y[4 * g4 + 3]),
                                                    __float_as_uint(Y[4 * g4 + 2]), 0x07030C0Cu);
         lcnt += (unsigned)__builtin_popcount((t01 | t23) & 0x80808080u);
+      }
       }
 #pragma unroll
       for (int p = 0; p < 4; ++p)   // one log2 per 4 logits (an overflowing product: fallback below)
@@ -1188,7 +1206,7 @@ __global__ void __launch_bounds__(NTH2) zzt_dense_bf16_v4(ZztArgs a) {
   }
   xd += __shfl_xor(xd, 32, 64);
   xs += __shfl_xor(xs, 32, 64);
-  if constexpr (EPI == 0) xs = -xs;
+  if constexpr (EPI != 1) xs = -xs;
   const bool row_valid = i_me < a.n;
   const bool corr = sp == 0;
   const bool own = cb == 0 && h == 0 && row_valid && corr;
@@ -1196,13 +1214,13 @@ __global__ void __launch_bounds__(NTH2) zzt_dense_bf16_v4(ZztArgs a) {
   if (own) {
     // EPI 0: + sum_j x_ij (softplus2(x) = x + log2(q) + c); EPI 1: + sum_j x_ij / 2
     // (the other half of max(x, 0)); both: - softplus2(x_ii)
-    ltot += (EPI == 0 ? 1.0 : 0.5) * (double)xs;
+    ltot += (EPI != 1 ? 1.0 : 0.5) * (double)xs;
     ltot -= (double)(fmaxf(xd, 0.f) + __builtin_amdgcn_logf(1.f + exd));
   }
   const unsigned dpos = (unsigned)__popcll(__ballot(own && xd > 0.f));
   if (cb == 0 && h == 0) {   // s'_ii as the backward MFMA consumed it (bf16), 0 outside split 0
     float sg;
-    if constexpr (EPI == 0) {
+    if constexpr (EPI != 1) {
       sg = __builtin_amdgcn_rcpf(__builtin_amdgcn_exp2f(-xd - kZ4C) + kZ4Q);
     } else {
       const float rcd = __builtin_amdgcn_rcpf(1.f + exd);
@@ -1223,7 +1241,7 @@ __global__ void __launch_bounds__(NTH2) zzt_dense_bf16_v4(ZztArgs a) {
   }
   __syncthreads();
   if (cb == 0 && !(skip & 32)) {
-    constexpr float scale = EPI == 0 ? kZ4S : 1.f;
+    constexpr float scale = EPI != 1 ? kZ4S : 1.f;
     float* dst = (sp == 0 ? a.dJd : a.dJd_extra + (long long)(sp - 1) * a.ngraphs * a.n * a.d) +
                  (long long)g * a.n * a.d;
 #pragma unroll
@@ -1242,7 +1260,7 @@ __global__ void __launch_bounds__(NTH2) zzt_dense_bf16_v4(ZztArgs a) {
     }
   }
   const double l = wave_sum_d(ltot);
-  if constexpr (EPI == 0) wcnt = wave_sum_u(lcnt);
+  if constexpr (EPI == 0 || EPI == 2) wcnt = wave_sum_u(lcnt);
   if (lane == 0) { sl[w] = l; sc[w] = wcnt - dpos; }
   __syncthreads();
   if (tid == 0) {
@@ -1358,7 +1376,7 @@ int launch_zzt_dense(const ZztArgs& a, int dtype, hipStream_t s) {
     // default: signed epilogue, plain tile order; A/B: variant 10 + 3 EPI + MODE;
     // variant >= 256: the measurement build of the default (phase skips / stamps)
     const int v = a.variant & 255;
-    const int cfg = (a.variant >= 256 || v < 10 || v > 15) ? 0 : v - 10;
+    const int cfg = (a.variant >= 256 || v < 10 || v > 19) ? 0 : v - 10;
 #define SND_V4(DPV)                                                                              \
   if (a.variant >= 256) hipLaunchKernelGGL((zzt_dense_bf16_v4<DPV, 0, 0, true>), grid, dim3(NTH2), 0, s, a); \
   else if (cfg == 0) hipLaunchKernelGGL((zzt_dense_bf16_v4<DPV, 0, 0, false>), grid, dim3(NTH2), 0, s, a); \
@@ -1366,7 +1384,11 @@ int launch_zzt_dense(const ZztArgs& a, int dtype, hipStream_t s) {
   else if (cfg == 2) hipLaunchKernelGGL((zzt_dense_bf16_v4<DPV, 2, 0, false>), grid, dim3(NTH2), 0, s, a); \
   else if (cfg == 3) hipLaunchKernelGGL((zzt_dense_bf16_v4<DPV, 0, 1, false>), grid, dim3(NTH2), 0, s, a); \
   else if (cfg == 4) hipLaunchKernelGGL((zzt_dense_bf16_v4<DPV, 1, 1, false>), grid, dim3(NTH2), 0, s, a); \
-  else hipLaunchKernelGGL((zzt_dense_bf16_v4<DPV, 2, 1, false>), grid, dim3(NTH2), 0, s, a);
+  else if (cfg == 5) hipLaunchKernelGGL((zzt_dense_bf16_v4<DPV, 2, 1, false>), grid, dim3(NTH2), 0, s, a); \
+  else if (cfg == 6) hipLaunchKernelGGL((zzt_dense_bf16_v4<DPV, 0, 2, false>), grid, dim3(NTH2), 0, s, a); \
+  else if (cfg == 7) hipLaunchKernelGGL((zzt_dense_bf16_v4<DPV, 0, 3, false>), grid, dim3(NTH2), 0, s, a); \
+  else if (cfg == 8) hipLaunchKernelGGL((zzt_dense_bf16_v4<DPV, 1, 2, false>), grid, dim3(NTH2), 0, s, a); \
+  else hipLaunchKernelGGL((zzt_dense_bf16_v4<DPV, 1, 3, false>), grid, dim3(NTH2), 0, s, a);
     if (dp == 32) { SND_V4(32) } else { SND_V4(64) }
 #undef SND_V4
   } else if (dtype == SND_BF16) {                     // v3: |x| formulation, 16x16x32 (d = 128)

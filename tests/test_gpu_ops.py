@@ -373,6 +373,42 @@ def test_zzt_v4_matches_v3_in_step():
     assert rel(d4, d3) < 1e-2
 
 
+@pytest.mark.parametrize("n,d,B", [(4096, 64, 8), (300, 32, 3), (4096, 64, 1), (200, 16, 2)])
+def test_zzt_variants_match_in_step(n, d, B):
+    """The step's zz^T launch in its variants on the same staged z: v4 (default and its
+    MODE 1 / ballot-count variants) against v3 (|x| form, 16x16x32):
+    loss and count agree to bf16 rounding, dJ within bf16 operand rounding.  B = 1
+    at N = 4096 runs the column splits (C3 per rank)."""
+    from snd_vae_amd import _lib
+    from snd_vae_amd.model import DeviceBatch, SGCNModelVAE
+    from snd_vae_amd.optimizer import OptimizerVAE
+    cfg = tscale(n, d)
+    db = DeviceBatch(synthetic_batch(cfg, B, seed=1000))
+    model = SGCNModelVAE(cfg, B, dtype="bf16")
+    opt = OptimizerVAE(model)
+    opt.step(db)
+    torch.cuda.synchronize()
+    L = _lib.lib()
+    bc = db.c_struct()
+    pz = model.buffer("PZZT", torch.float64)
+    djd = model.buffer("DJD")
+    out = {}
+    for name in ("zzt_dense_v3", "zzt_dense_v14", "zzt_dense_v19", "zzt_dense"):
+        pz.zero_()
+        _lib.check(L.snd_plan_launch(model.plan, bc, model.workspace.data_ptr(), name.encode(),
+                                     _lib.stream_ptr()))
+        torch.cuda.synchronize()
+        out[name] = (pz.view(-1, 2).sum(0).cpu().numpy(), djd.clone().cpu().numpy())
+    s3, d3 = out["zzt_dense_v3"]
+    for name in ("zzt_dense_v14", "zzt_dense_v19", "zzt_dense"):
+        s, dd = out[name]
+        assert s[0] == pytest.approx(s3[0], rel=1e-4), name
+        assert abs(s[1] - s3[1]) <= 1e-4 * B * n * n, name
+        assert rel(dd, d3) < 1e-2, name
+    # the ballot count (v19) and the sign-byte count (default) see the same y
+    assert out["zzt_dense_v19"][0][1] == out["zzt_dense"][0][1]
+
+
 def test_zzt_ce_weighted_bce():
     from snd_vae_amd import layers
     n, d, B = 140, 32, 2

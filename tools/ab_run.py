@@ -1,0 +1,56 @@
+"""One A/B measurement process: the C2 bench step (HIP-graph replay) and named plan
+kernels timed with HIP events, for the library SND_LIB_PATH points at.
+
+    SND_LIB_PATH=ab/x.so python tools/ab_run.py [--kernels zzt_dense,...] [--tag x]
+Prints one JSON line.
+"""
+import argparse
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--kernels", default="zzt_dense")
+    ap.add_argument("--graphs", type=int, default=8)
+    ap.add_argument("--nodes", type=int, default=4096)
+    ap.add_argument("--latent", type=int, default=64)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--tag", default=os.environ.get("SND_LIB_PATH", "default"))
+    args = ap.parse_args()
+    import torch
+
+    import bench
+    from snd_vae_amd import _lib
+    from snd_vae_amd.config import tscale
+    from snd_vae_amd.data import synthetic_batch
+    from snd_vae_amd.model import DeviceBatch, SGCNModelVAE
+    from snd_vae_amd.optimizer import OptimizerVAE
+    cfg = tscale(args.nodes, args.latent)
+    db = DeviceBatch(synthetic_batch(cfg, args.graphs, seed=1000))
+    model = SGCNModelVAE(cfg, args.graphs, dtype="bf16")
+    opt = OptimizerVAE(model)
+    opt.step(db)
+    opt.capture(db, warmup=2)
+    for _ in range(10):
+        opt.replay()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(args.steps):
+        opt.replay()
+    e1.record()
+    e1.synchronize()
+    out = {"tag": args.tag, "step_ms": round(e0.elapsed_time(e1) / args.steps, 5),
+           "losses": {k: round(v, 6) for k, v in opt.loss_dict().items()}}
+    km = bench.kernel_timer(model, db.c_struct(), args.reps)
+    for k in [k for k in args.kernels.split(",") if k]:
+        out[k + "_us"] = round(1000 * min(km(k) for _ in range(3)), 2)
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()
