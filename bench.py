@@ -319,7 +319,8 @@ def spmm_batched(host, width, copies, reps):
             dw.meta.data_ptr(), dw.slots.data_ptr(), dw.rows.data_ptr(), dw.order.data_ptr(), R, host.n_nodes, ng, wp.beta,
             h.data_ptr(), width, width, out.data_ptr(), width, sp)), reps)
         kern = (f"csr_spmm_bf16_window (A @ H, width {width}, {ng} graphs block-diagonal, {len(ci)} nnz, "
-                f"RCM schedule, beta {wp.beta}, 1096-row LDS ring)")
+                f"RCM schedule, beta {wp.beta}, 1096-row LDS ring; the kernel snd_train_step launches "
+                f"for the GraphConvolution backward A @ dP1)")
         prev = dict(tiled, previous_variant=reg)
     else:
         ms, kern, prev = ms_tiled, "csr_spmm_bf16_tiled (A @ H, width %d, %d graphs)" % (width, ng), reg
@@ -427,6 +428,7 @@ def main():
     zzt_v1_ms = kernel_ms("zzt_dense_v1") if args.dtype == "bf16" else None
     fast = args.dtype == "bf16"
     spmm_ms = kernel_ms("spmm_bf16" if fast else "spmm_dxw1")
+    spmm_tiled_ms = kernel_ms("spmm_bf16_tiled") if fast and db.tiles else None
     flops = 4.0 * N * N * d * B                       # 2N^2 d fwd + 2N^2 d bwd per graph
     achieved = flops / (zzt_ms * 1e-3) / 1e12
     peak = PEAK_TFLOPS[args.dtype]
@@ -464,9 +466,12 @@ def main():
         "secondary_roofline": dict(
             spmm_batched(host, h1, args.spmm_copies, max(4, args.kernel_reps // 2)) if fast else {},
             in_step={"kernel": f"csr_spmm (A @ dP1, width {h1}, {'bf16' if fast else 'fp32'}, "
-                               f"{B} graphs{', row tiles' if fast and db.tiles else ''})",
+                               f"{B} graphs, "
+                               f"{'window' if fast and db.window else ('row tiles' if fast and db.tiles else 'register gathers')})",
                      "achieved": round(spmm_gbs, 1), "frac": round(spmm_gbs / PEAK_HBM_GBS, 4),
-                     "avg_launch_ms": round(spmm_ms, 5), "bytes_per_launch": spmm_bytes}),
+                     "avg_launch_ms": round(spmm_ms, 5), "bytes_per_launch": spmm_bytes,
+                     "row_tiles_ms": None if spmm_tiled_ms is None else round(spmm_tiled_ms, 5),
+                     "note": "8 graphs: a 4 MB working set, L2-resident; the HBM fraction is the 256-graph line"}),
         "losses": {k: round(v, 6) for k, v in losses.items()},
     }
     from snd_vae_amd.build import lib_status

@@ -146,20 +146,6 @@ int snd_csr_spmm_bf16_window(const int* meta, const uint16_t* slots, const int* 
                              int n_rows, int n_per_graph, int n_graphs, int beta,
                              const void* h, int ldh, int width, void* out, int ldo,
                              snd_stream_t stream);
-/* The same window walk with pair sums (ABI 9; plan: data.py window_plan_pairs).
- * A wavefront sums one row at a time, four neighbours per round as two pairs
- * of ring rows read with ds_read_b64_tr_b16 and added by one v_dot2c with
- * (1, 1) per pair and column: slots[] holds per row a 32-entry block, entry
- * (round r, pair h, side t) at 8 (2h + t) + r for r < 8 and at 32 + 4 (r - 8)
- * + 2h + t past it; side 0 prefers even ring slots, side 1 odd ones, padding
- * uses the zero rows 1096 (even) and 1097 (odd).  meta / rows / order / beta
- * as above.  Sums are not in colidx order: within fp32 rounding of the sums
- * of snd_csr_spmm_bf16 (a bf16 output differs by at most one ulp). */
-int snd_csr_spmm_bf16_window_pairs(const int* meta, const uint16_t* slots, const int* rows,
-                                   const int* order,
-                                   int n_rows, int n_per_graph, int n_graphs, int beta,
-                                   const void* h, int ldh, int width, void* out, int ldo,
-                                   snd_stream_t stream);
 /* ---- a5: linear / dense GEMM on MFMA ---------------------------------------
  * Replaces linear() (layers.py:566-576) and the X@w of GraphConvolution
  * (layers.py:120-121; the tile() copy is not needed):
@@ -377,6 +363,17 @@ typedef struct snd_config {
 } snd_config_t;
 enum { SND_TSCALE = 0, SND_TREF = 1 };
 
+/* The window SpMM's plan on the device (ABI 10; data.py window_plan, see
+ * snd_csr_spmm_bf16_window): with it, the step's bf16 GraphConvolution backward
+ * SpMM (A @ dP1, width 64) runs the window kernel.  meta NULL = none. */
+typedef struct snd_window_plan {
+  const int* meta;              /* [n_rows] */
+  const uint16_t* slots;
+  const int* rows;              /* [n_rows] */
+  const int* order;             /* [n_rows] */
+  int beta;
+} snd_window_plan_t;
+
 typedef struct snd_batch {
   const int* rowptr;           /* [B*N+1] */
   const int* colidx;           /* [nnz]   */
@@ -388,6 +385,7 @@ typedef struct snd_batch {
   snd_row_tiles_t tiles;       /* optional row tiles over row_order (ABI 5; all
                                   zero = none): the bf16 encoder SpMMs stage
                                   neighbour rows in LDS */
+  snd_window_plan_t window;    /* optional window SpMM plan over row_order (ABI 10) */
 } snd_batch_t;
 
 typedef struct snd_plan snd_plan_t;

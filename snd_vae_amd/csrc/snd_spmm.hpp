@@ -25,3 +25,15 @@ int edge_blocks(int n_rows, int d);
 int launch_edge(const EdgeArgs& a, hipStream_t s);
 
 }  // namespace snd
+
+namespace snd {
+// the sliding-window bf16 SpMM (snd_spmm_win.hip; plan: data.window_plan)
+struct SpmmWinArgs {
+  const int* meta; const uint16_t* slots; const int* rows; const int* order; int beta;
+  int n_rows, n_per_graph, n_graphs;
+  const void* h; int ldh; int width;
+  void* out; int ldo;
+};
+int launch_spmm_window(const SpmmWinArgs& w, hipStream_t s);
+int spmm_win_max_beta();
+}  // namespace snd

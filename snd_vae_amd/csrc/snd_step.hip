@@ -140,7 +140,7 @@ struct snd_plan {
 };
 
 extern "C" const char* snd_last_error(void) { return g_err; }
-extern "C" int snd_abi_version(void) { return 9; }
+extern "C" int snd_abi_version(void) { return 10; }
 
 extern "C" int snd_plan_create(const snd_config_t* cfg, int n_graphs, snd_plan_t** out) {
   SND_CHECK_ARG(cfg && out && n_graphs > 0, "snd_plan_create: bad args");
@@ -715,6 +715,11 @@ int pack_decoder(const Ctx& x) {
   return launch_pack(e, build_packs(x, e), x.s);
 }
 
+// The plain bf16 SpMM A @ h (width 64) of the batch: the window kernel when the batch
+// carries a window plan that fits the ring, else the row tiles / register gathers.
+static int spmm_bf16_plain(const snd_batch_t* batch, int R, int npg, int ngraphs, const __bf16* h,
+                           int ldh, int width, __bf16* out, int ldo, hipStream_t s);
+
 // optional row tiles of the batch (snd_row_tiles_t): the SpMM stages neighbour rows in LDS
 static void use_tiles(SpmmBfArgs& a, const snd_batch_t* batch, int npg, int ngraphs) {
   a.row_order = batch->row_order;
@@ -722,6 +727,20 @@ static void use_tiles(SpmmBfArgs& a, const snd_batch_t* batch, int npg, int ngra
   a.t_rowid = batch->tiles.rows; a.t_trp = batch->tiles.trp; a.t_lcol = batch->tiles.lcol;
   a.t_ucol = batch->tiles.ucol; a.t_rows = batch->tiles.tile_rows; a.t_ustride = batch->tiles.ustride;
   a.npg = npg; a.ngraphs = ngraphs;
+}
+
+static int spmm_bf16_plain(const snd_batch_t* batch, int R, int npg, int ngraphs, const __bf16* h,
+                           int ldh, int width, __bf16* out, int ldo, hipStream_t s) {
+  const snd_window_plan_t& w = batch->window;
+  if (w.meta && width == 64 && w.beta >= 0 && ((w.beta + 7) & ~7) <= spmm_win_max_beta() &&
+      !(debug_flags() & (1 << 22))) {   // debug bit 1 << 22: the row tiles (A/B)
+    SpmmWinArgs a{w.meta, w.slots, w.rows, w.order, w.beta, R, npg, ngraphs, h, ldh, width, out, ldo};
+    return launch_spmm_window(a, s);
+  }
+  SpmmBfArgs a{batch->rowptr, batch->colidx, R, h, ldh, width, SND_SPMM_PLAIN, out, ldo};
+  a.xcd_nbg = xcd_nbg(npg, ngraphs);
+  use_tiles(a, batch, npg, ngraphs);
+  return launch_spmm_bf16(a, s);
 }
 
 // encoder forward (model.py:104-115): H1 -> XW1 -> GCN1 -> heads h, [mu | logstd]
@@ -862,12 +881,7 @@ int encoder_fast_bwd_tail(const Ctx& x, const snd_batch_t* batch, bool enc1_done
     a.out = bf("FDP1"); a.ldo = h1; a.out_bf16 = 1; a.colpart = x.f("PFENC1"); a.ncp = 4;
     SND_TRY(launch_rowconv(a, RC_ENC1, x.s));
   }
-  {
-    SpmmBfArgs a{batch->rowptr, batch->colidx, R, bf("FDP1"), h1, h1, SND_SPMM_PLAIN, bf("FDXW1"), h1};
-    a.xcd_nbg = xcd_nbg(p.N, p.B);
-    use_tiles(a, batch, p.N, p.B);
-    SND_TRY(launch_spmm_bf16(a, x.s));
-  }
+  SND_TRY(spmm_bf16_plain(batch, R, p.N, p.B, bf("FDP1"), h1, h1, bf("FDXW1"), h1, x.s));
   SND_TRY(fork(x));
   SND_TRY(wgrad(x, wg_args(p, x.ws, p.gW1, bf("FH1"), p.ldh1, h0 + f, bf("FDXW1"), h1, h1, x.f("FSW1"), 1), side(x)));
   {
@@ -1197,6 +1211,11 @@ extern "C" int snd_plan_launch(const snd_plan_t* plan, const snd_batch_t* batch,
   }
   if (!strcmp(kernel, "spmm_bf16")) {   // backward GCN1 SpMM of the fast path: A @ dP1 (bf16)
     SND_CHECK_ARG(p.fast_enc, "snd_plan_launch: spmm_bf16 needs the bf16 fast encoder");
+    return spmm_bf16_plain(batch, p.R, p.N, p.B, (const __bf16*)(ws + p.buf("FDP1")), p.c.h1, p.c.h1,
+                           (__bf16*)(ws + p.buf("FDXW1")), p.c.h1, s);
+  }
+  if (!strcmp(kernel, "spmm_bf16_tiled")) {   // the same SpMM on the row tiles (A/B)
+    SND_CHECK_ARG(p.fast_enc, "snd_plan_launch: spmm_bf16_tiled needs the bf16 fast encoder");
     SpmmBfArgs a{batch->rowptr, batch->colidx, p.R, (const __bf16*)(ws + p.buf("FDP1")), p.c.h1,
                  p.c.h1, SND_SPMM_PLAIN, (__bf16*)(ws + p.buf("FDXW1")), p.c.h1};
     a.xcd_nbg = xcd_nbg(p.N, p.B);

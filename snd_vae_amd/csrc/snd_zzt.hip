@@ -1056,21 +1056,6 @@ __global__ void __launch_bounds__(NTH2) zzt_dense_bf16_v4(ZztArgs a) {
         q[v] = e + kZ4Q;
         sA[v >> 3][v & 7] = (__bf16)__builtin_amdgcn_rcpf(q[v]);
       }
-      if constexpr (EPI >= 2) {
-        // pin the packed sigmoids before the overflow test: otherwise the compiler
-        // sinks the 16 reciprocals past its branch, out of reach of the scheduler
-#pragma unroll
-        for (int h2 = 0; h2 < 2; ++h2) {
-          u32x4 t = __builtin_bit_cast(u32x4, sA[h2]);
-          asm volatile("" : "+v"(t));
-          sA[h2] = __builtin_bit_cast(bf16x8, t);
-        }
-      }
-      if constexpr (EPI == 3) {
-        // #{x > 0} = #{y < 0} by compare + ballot (SALU popcount)
-#pragma unroll
-        for (int v = 0; v < 16; ++v) wcnt += (unsigned)__popcll(__ballot(Y[v] < 0.f));
-      } else {
       // #{x > 0} = #{y < 0} (c = 0; y = +0 where x = 0): the sign bytes of four y's
       // gathered by two v_perm, masked, popcounted into a per-lane count
 #pragma unroll
@@ -1080,7 +1065,6 @@ __global__ void __launch_bounds__(NTH2) zzt_dense_bf16_v4(ZztArgs a) {
         const unsigned t23 = __builtin_amdgcn_perm(__float_as_uint(Y[4 * g4 + 3]),
                                                    __float_as_uint(Y[4 * g4 + 2]), 0x07030C0Cu);
         lcnt += (unsigned)__builtin_popcount((t01 | t23) & 0x80808080u);
-      }
       }
 #pragma unroll
       for (int p = 0; p < 4; ++p)   // one log2 per 4 logits (an overflowing product: fallback below)
@@ -1260,7 +1244,7 @@ __global__ void __launch_bounds__(NTH2) zzt_dense_bf16_v4(ZztArgs a) {
     }
   }
   const double l = wave_sum_d(ltot);
-  if constexpr (EPI == 0 || EPI == 2) wcnt = wave_sum_u(lcnt);
+  if constexpr (EPI == 0) wcnt = wave_sum_u(lcnt);
   if (lane == 0) { sl[w] = l; sc[w] = wcnt - dpos; }
   __syncthreads();
   if (tid == 0) {
@@ -1376,7 +1360,7 @@ int launch_zzt_dense(const ZztArgs& a, int dtype, hipStream_t s) {
     // default: signed epilogue, plain tile order; A/B: variant 10 + 3 EPI + MODE;
     // variant >= 256: the measurement build of the default (phase skips / stamps)
     const int v = a.variant & 255;
-    const int cfg = (a.variant >= 256 || v < 10 || v > 19) ? 0 : v - 10;
+    const int cfg = (a.variant >= 256 || v < 10 || v > 15) ? 0 : v - 10;
 #define SND_V4(DPV)                                                                              \
   if (a.variant >= 256) hipLaunchKernelGGL((zzt_dense_bf16_v4<DPV, 0, 0, true>), grid, dim3(NTH2), 0, s, a); \
   else if (cfg == 0) hipLaunchKernelGGL((zzt_dense_bf16_v4<DPV, 0, 0, false>), grid, dim3(NTH2), 0, s, a); \
@@ -1384,11 +1368,7 @@ int launch_zzt_dense(const ZztArgs& a, int dtype, hipStream_t s) {
   else if (cfg == 2) hipLaunchKernelGGL((zzt_dense_bf16_v4<DPV, 2, 0, false>), grid, dim3(NTH2), 0, s, a); \
   else if (cfg == 3) hipLaunchKernelGGL((zzt_dense_bf16_v4<DPV, 0, 1, false>), grid, dim3(NTH2), 0, s, a); \
   else if (cfg == 4) hipLaunchKernelGGL((zzt_dense_bf16_v4<DPV, 1, 1, false>), grid, dim3(NTH2), 0, s, a); \
-  else if (cfg == 5) hipLaunchKernelGGL((zzt_dense_bf16_v4<DPV, 2, 1, false>), grid, dim3(NTH2), 0, s, a); \
-  else if (cfg == 6) hipLaunchKernelGGL((zzt_dense_bf16_v4<DPV, 0, 2, false>), grid, dim3(NTH2), 0, s, a); \
-  else if (cfg == 7) hipLaunchKernelGGL((zzt_dense_bf16_v4<DPV, 0, 3, false>), grid, dim3(NTH2), 0, s, a); \
-  else if (cfg == 8) hipLaunchKernelGGL((zzt_dense_bf16_v4<DPV, 1, 2, false>), grid, dim3(NTH2), 0, s, a); \
-  else hipLaunchKernelGGL((zzt_dense_bf16_v4<DPV, 1, 3, false>), grid, dim3(NTH2), 0, s, a);
+  else hipLaunchKernelGGL((zzt_dense_bf16_v4<DPV, 2, 1, false>), grid, dim3(NTH2), 0, s, a);
     if (dp == 32) { SND_V4(32) } else { SND_V4(64) }
 #undef SND_V4
   } else if (dtype == SND_BF16) {                     // v3: |x| formulation, 16x16x32 (d = 128)

@@ -252,7 +252,6 @@ class WindowPlan(NamedTuple):
     order: np.ndarray    # int32 [R]: the row at each position (the schedule)
     beta: int            # largest |position(neighbour) - position(row)|
     max_degree: int
-    layout: str = "groups"   # "groups": window_plan; "pairs": window_plan_pairs
 
 
 def window_plan(batch: GraphBatch, order: np.ndarray, ring: int = 1096) -> WindowPlan:
@@ -281,16 +280,15 @@ def window_plan(batch: GraphBatch, order: np.ndarray, ring: int = 1096) -> Windo
     q = np.arange(R)
     blk = (q // n) * ((n + 127) // 128) + (q % n) // 128
     srt = np.lexsort((q, -deg, blk))
-    # a wavefront sums the rows of one sorted group together up to their largest
-    # degree (16 rows on the MFMA sums, 8 on the VALU sums): every list is padded
-    # (with the ring's zero row, slot ``ring``) to its 16-row group's largest degree
-    # (at most the 32 entries the kernel stages), in 8s
+    # a wavefront sums the 8 rows of one sorted group together up to their largest
+    # degree: every list is padded (with the ring's zero row, slot ``ring``) to its
+    # group's largest degree (at most the 32 entries the kernel stages), in 8s
     rank = np.empty(R, np.int64)
     bs = blk[srt]
     first = np.searchsorted(bs, bs, side="left")          # sorted index of the block's first row
     rank[srt] = np.arange(R) - first                       # rank of a position inside its block
     gfirst = np.empty(R, np.int64)
-    gfirst[srt] = first + (rank[srt] // 16) * 16           # sorted index of its group's first row
+    gfirst[srt] = first + (rank[srt] // 8) * 8             # sorted index of its group's first row
     gmax = deg[srt][gfirst] if R else deg
     pad = (np.maximum(deg, np.minimum(gmax, 32)) + 7) // 8 * 8
     start = np.zeros(R + 1, np.int64)
@@ -311,85 +309,6 @@ def window_plan(batch: GraphBatch, order: np.ndarray, ring: int = 1096) -> Windo
     meta = ((start[:-1] // 8) << 6 | deg).astype(np.int32)
     return WindowPlan(meta[srt], slots, order[srt].astype(np.int32), order.astype(np.int32), beta,
                       int(deg.max()) if deg.size else 0)
-
-
-def window_plan_pairs(batch: GraphBatch, order: np.ndarray, ring: int = 1096) -> WindowPlan:
-    """Neighbour lists for the pair-sum window SpMM (snd_csr_spmm_bf16_window_pairs).
-
-    A wavefront sums one row at a time: per round, four neighbours as two pairs
-    (one pair per 32-lane half, each half reading both rows of its pair whole), so
-    the plan pairs an even ring slot with an odd one wherever the row allows (the
-    two 128-byte rows then cover the 64 LDS banks once).  Lists are padded to a
-    multiple of 4 with the ring's two zero rows (slot ``ring`` even, ``ring + 1``
-    odd).  Entry (round r, half h, side t) of a row sits at index 8 (2h + t) + r of
-    the row's 32-entry block for r < 8 (a lane reads its 8 rounds as one 16-byte
-    word), at 32 + 4 (r - 8) + 2h + t past it.  The summation order is not colidx
-    order: outputs agree with spmm_bf16 within fp32 rounding of the sums.
-    meta / rows / order / beta as window_plan.
-    """
-    if ring % 2:
-        raise ValueError("window_plan_pairs: the ring size must be even")
-    n, B = batch.n_nodes, batch.n_graphs
-    R = n * B
-    order = np.ascontiguousarray(order, np.int64)
-    rp = batch.rowptr.astype(np.int64)
-    ci = batch.colidx.astype(np.int64)
-    pos = np.empty(R, np.int64)
-    pos[order] = np.arange(R) % n
-    deg = np.diff(rp)[order]
-    if deg.size and deg.max() > 63:
-        raise ValueError("window_plan_pairs: degree > 63 does not fit the metadata word")
-    q = np.arange(R)
-    blk = (q // n) * ((n + 127) // 128) + (q % n) // 128
-    srt = np.lexsort((q, -deg, blk))
-    nr = (deg + 3) // 4                                   # rounds per row
-    size = 32 + 4 * np.maximum(nr - 8, 0)
-    size = (size + 7) // 8 * 8
-    start = np.zeros(R + 1, np.int64)
-    np.cumsum(size, out=start[1:])
-    if start[-1] // 8 >= (1 << 25):
-        raise ValueError("window_plan_pairs: slot lists exceed the 25-bit offset")
-    # block index of entry (round r, class c = 2h + t)
-    def slot_index(s0, r, c):
-        return s0 + np.where(r < 8, 8 * c + r, 32 + 4 * (r - 8) + c)
-    slots = np.full(max(int(start[-1]), 8), ring, np.uint16)
-    s0 = start[:-1]
-    for r_ in range(16):                                  # odd-side padding: the odd zero row
-        live = r_ < np.maximum(nr, 8)
-        for c_ in (1, 3):
-            slots[slot_index(s0[live], r_, c_)] = ring + 1
-    nnz = int(deg.sum())
-    beta = 0
-    if nnz:
-        excl = np.cumsum(deg) - deg
-        run = np.arange(nnz) - np.repeat(excl, deg)
-        src = np.repeat(rp[order], deg) + run
-        npos = pos[ci[src]]
-        rowq = np.repeat(np.arange(R), deg)
-        beta = int(np.abs(npos - rowq % n).max())
-        slot = npos % ring
-        par = slot & 1
-        # rank of each entry among its row's entries of the same parity (colidx order)
-        key = np.lexsort((run, par, rowq))
-        grp = rowq[key] * 2 + par[key]
-        gfirst = np.searchsorted(grp, grp, side="left")
-        prank = np.empty(nnz, np.int64)
-        prank[key] = np.arange(nnz) - gfirst
-        nodd = np.bincount(rowq, weights=par, minlength=R).astype(np.int64)
-        neven = deg - nodd
-        cap = 2 * nr[rowq]                                # entries per side
-        # evens fill side 0 (t = 0) first, odds side 1; an overflow goes to the other
-        # side after that side's own parity
-        even = par == 0
-        t = np.where(even, prank >= cap, prank < cap).astype(np.int64)
-        own_count = np.where(even, nodd[rowq], neven[rowq])   # entries of the other side's own parity
-        u = np.where(prank < cap, prank, own_count + prank - cap)
-        r = u >> 1
-        c = 2 * (u & 1) + t
-        slots[slot_index(start[:-1][rowq], r, c)] = slot.astype(np.uint16)
-    meta = ((start[:-1] // 8) << 6 | deg).astype(np.int32)
-    return WindowPlan(meta[srt], slots, order[srt].astype(np.int32), order.astype(np.int32), beta,
-                      int(deg.max()) if deg.size else 0, "pairs")
 
 
 def shard(batch: GraphBatch, rank: int, world: int) -> GraphBatch:

@@ -485,3 +485,33 @@ def test_fused_encoder_front_matches_chain(topology, n, d, B):
     g0, g1 = o0.grad_blocks(), o1.grad_blocks()
     for k in g0:
         assert np.array_equal(g0[k], g1[k]), k
+
+
+@pytest.mark.parametrize("n,B", [(4096, 8), (4096, 1), (1000, 3)])
+def test_step_window_spmm_matches_row_tiles(n, B):
+    """The step's GraphConvolution backward SpMM A @ dP1 on the window kernel (the batch
+    carries a window plan, snd_window_plan_t) against the row-tile kernel (debug bit
+    1 << 22): the same fp32 sums in colidx order -- dXW1 and every gradient equal."""
+    from snd_vae_amd import _lib
+    from snd_vae_amd.params import init_blocks
+    cfg = tscale(n, 64)
+    batch = synthetic_batch(cfg, B, seed=21)
+    p0 = init_blocks(cfg, 1)
+    runs = []
+    for flags in (1 << 22, 0):
+        m, o, b = make(cfg, batch, p0, "bf16")
+        assert b.window is not None and b.tiles is not None
+        _lib.check(_lib.lib().snd_debug_set(flags))
+        try:
+            o.forward_backward(b)
+            torch.cuda.synchronize()
+        finally:
+            _lib.check(_lib.lib().snd_debug_set(0))
+        runs.append((m, o))
+    (m0, o0), (m1, o1) = runs
+    a, c = m0.buffer("FDXW1", torch.bfloat16), m1.buffer("FDXW1", torch.bfloat16)
+    diff = int((a.view(torch.int16) != c.view(torch.int16)).sum())
+    assert diff <= 1e-5 * a.numel(), diff       # dot2c adds: within one fp32 ulp, bitwise in practice
+    g0, g1 = o0.grad_blocks(), o1.grad_blocks()
+    for k in g0:
+        np.testing.assert_allclose(g1[k], g0[k], rtol=1e-3, atol=1e-6 * max(1.0, np.abs(g0[k]).max()), err_msg=k)

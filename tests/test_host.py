@@ -253,7 +253,7 @@ def test_window_plan_matches_literal(n, B, kbar):
     positions in colidx order, then the zero row's slot 1096 up to its wavefront
     group's largest degree (at most 32), in 8s; meta = (start8 << 6) | degree,
     listed (with rows) by degree descending inside every aligned 128-position
-    block, a group = 16 consecutive rows of that listing."""
+    block, a group = 8 consecutive rows of that listing (one wavefront)."""
     from snd_vae_amd.config import tscale
     from snd_vae_amd.data import locality_order, synthetic_batch, window_plan
     b = synthetic_batch(tscale(n, 16, mean_degree=kbar), B, seed=n)
@@ -270,7 +270,7 @@ def test_window_plan_matches_literal(n, B, kbar):
             key = sorted(qs, key=lambda q: (-deg[q], q))
             keys[(g, lo)] = (qs, key)
             for i, q in enumerate(key):
-                gmax[q] = deg[key[i - i % 16]]
+                gmax[q] = deg[key[i - i % 8]]
     start, beta = 0, 0
     meta = np.zeros(R, np.int64)
     for q in range(R):
@@ -291,41 +291,3 @@ def test_window_plan_matches_literal(n, B, kbar):
         np.testing.assert_array_equal(wp.rows[qs[0]:qs[-1] + 1], order[key])
 
 
-@pytest.mark.parametrize("n,B,kbar", [(500, 3, 8.0), (4096, 1, 16.0), (97, 4, 5.0), (200, 2, 45.0)])
-def test_window_plan_pairs_matches_literal(n, B, kbar):
-    """data.window_plan_pairs against a per-row restatement: every round of a row's
-    block holds two pairs; the entries read (rounds < ceil(deg / 4)) are exactly its
-    neighbours' ring slots plus zero rows (1096 on side 0, 1097 on side 1); side 0 takes
-    even slots first, side 1 odd ones, so a pair mixes parities whenever the row has
-    both left; meta / rows / order / beta as window_plan."""
-    from snd_vae_amd.config import tscale
-    from snd_vae_amd.data import locality_order, synthetic_batch, window_plan, window_plan_pairs
-    b = synthetic_batch(tscale(n, 16, mean_degree=kbar), B, seed=n + 1)
-    order = locality_order(b)
-    wp = window_plan_pairs(b, order)
-    wg = window_plan(b, order)
-    assert wp.layout == "pairs" and wp.beta == wg.beta and wp.max_degree == wg.max_degree
-    np.testing.assert_array_equal(wp.rows, wg.rows)
-    np.testing.assert_array_equal(wp.order, wg.order)
-    np.testing.assert_array_equal(wp.meta & 63, wg.meta & 63)
-    R = n * B
-    pos = np.empty(R, np.int64)
-    pos[order] = np.arange(R) % n
-    idx = lambda r, c: 8 * c + r if r < 8 else 32 + 4 * (r - 8) + c
-    for m, row in zip(wp.meta, wp.rows):
-        st, d = int(m >> 6) * 8, int(m & 63)
-        nr = (d + 3) // 4
-        sides = [[int(wp.slots[st + idx(r, 2 * h + t)]) for r in range(nr) for h in range(2)] for t in range(2)]
-        for t in range(2):
-            assert all(x < 1096 or x == 1096 + t for x in sides[t])
-        got = sorted(x for s_ in sides for x in s_ if x < 1096)
-        nb = b.colidx[b.rowptr[row]:b.rowptr[row + 1]].astype(np.int64)
-        assert got == sorted((pos[nb] % 1096).tolist())
-        ev = sum(1 for x in got if x % 2 == 0)
-        od = len(got) - ev
-        # side 0 holds min(ev, 2 nr) evens, side 1 min(od, 2 nr) odds
-        assert sum(1 for x in sides[0] if x < 1096 and x % 2 == 0) == min(ev, 2 * nr)
-        assert sum(1 for x in sides[1] if x < 1096 and x % 2 == 1) == min(od, 2 * nr)
-        if nr <= 8:
-            assert (wp.slots[st + np.array([idx(r, c) for r in range(nr, 8) for c in range(4)], int)] >= 1096).all() \
-                if nr < 8 else True
