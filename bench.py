@@ -225,7 +225,9 @@ def del_models():
 def time_launches(launch, reps):
     """ms per launch: `reps` launches captured in one HIP graph (times the GPU, not the
     host launch path), replayed between HIP events recorded on the stream the kernels
-    run on.  launch(stream_ptr) enqueues one launch."""
+    run on; the best of 3 rounds of 3 replays after 3 warm replays (the first
+    measurement of a process otherwise reads high while the clocks ramp up).
+    launch(stream_ptr) enqueues one launch."""
     import torch
 
     from snd_vae_amd import _lib
@@ -237,16 +239,18 @@ def time_launches(launch, reps):
         with torch.cuda.graph(g, stream=side):
             for _ in range(reps):
                 launch(_lib.stream_ptr(side))
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    with torch.cuda.stream(side):      # warm replay + timed replays, all on `side`
-        g.replay()
-        e0.record(side)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(3)]
+    with torch.cuda.stream(side):      # warm replays (clocks up) + 3 timed rounds, all on `side`
         for _ in range(3):
             g.replay()
-        e1.record(side)
-    e1.synchronize()
+        for e0, e1 in ev:
+            e0.record(side)
+            for _ in range(3):
+                g.replay()
+            e1.record(side)
+    ev[-1][1].synchronize()
     torch.cuda.current_stream().wait_stream(side)
-    return e0.elapsed_time(e1) / (3 * reps)
+    return min(e0.elapsed_time(e1) for e0, e1 in ev) / (3 * reps)
 
 
 def kernel_timer(model, bc, reps):
