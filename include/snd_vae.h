@@ -337,7 +337,15 @@ int snd_latent_reg(const float* mu, const float* logstd, const float* z, int bat
  *   SND_TREF    graph latent (model.py:113-115, model_joint.py:87-97):
  *               h = flat(G) Wh + bh per graph, z [B, L],
  *               J = reshape(z Wp + bp, [B, N, node_h]); at most 8 graphs
- *               per plan (the weight-streaming kernels keep B in registers).
+ *               per plan (the weight-streaming kernels keep B in registers);
+ *   SND_SGJOINT the SND-VAE spatial-graph encoder (ABI 11; model_joint.py:72-85,
+ *               model.py:134-151,172-180): two SpatialGraphConvolution layers
+ *               (snd_sg_layer_fwd, BN + lrelu) over the B * sampling_num
+ *               spanning-tree copies (batch tree_rowptr / tree_colidx / rel,
+ *               features tiled per copy), flat heads per copy, z [B*S, L],
+ *               J_b = mean_s reshape(z_{b,s} Wp + bp, [N, node_h]), then the
+ *               graph-latent decoders; f_in = num_feature, h0/h1 unused, fp32
+ *               generic engine (either dtype for the GEMM operands).
  * It writes the flat
  * gradient (same layout as params), advances *step_counter and writes
  * losses[0..7] = {cost, spatial_cost, adj_cost, node_cost, kl, acc,
@@ -360,8 +368,10 @@ typedef struct snd_config {
   int dtype;        /* SND_F32 (parity) or SND_BF16 (throughput) */
   int topology;     /* SND_TSCALE or SND_TREF (ABI version 2) */
   int node_h;       /* width of J (node_h_size); == latent for SND_TSCALE */
+  int sampling_num; /* SND_SGJOINT: spanning trees per graph (main.py:100) */
+  int sg_h[6];      /* SND_SGJOINT: sg_conv_hidden [[h0,h1,h2],[h0,h1,h2]] (main.py:193) */
 } snd_config_t;
-enum { SND_TSCALE = 0, SND_TREF = 1 };
+enum { SND_TSCALE = 0, SND_TREF = 1, SND_SGJOINT = 2 };
 
 /* The window SpMM's plan on the device (ABI 10; data.py window_plan, see
  * snd_csr_spmm_bf16_window): with it, the step's bf16 GraphConvolution backward
@@ -386,6 +396,13 @@ typedef struct snd_batch {
                                   zero = none): the bf16 encoder SpMMs stage
                                   neighbour rows in LDS */
   snd_window_plan_t window;    /* optional window SpMM plan over row_order (ABI 10) */
+  /* SND_SGJOINT (ABI 11): the spanning trees of the B graphs, copy c = b * S + s of
+   * graph b (input_data.py:76-83), one symmetric block-diagonal CSR over B*S*N rows;
+   * rel [B*S, N, N] of each copy (the 'rel' feed / 600, input_data.py:59); features
+   * are then [B*S*N, num_feature] (graph b's features in each of its copies) */
+  const int* tree_rowptr;
+  const int* tree_colidx;
+  const float* rel;
 } snd_batch_t;
 
 typedef struct snd_plan snd_plan_t;

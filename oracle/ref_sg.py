@@ -111,3 +111,61 @@ def init_sg_layer(F, hidden, rng, stddev=0.02):
             "M2": rng.normal(0, stddev, (2 * F + 1 + h0, h1)), "b2": np.zeros(h1),
             "M3": rng.normal(0, stddev, (F + h1, h2)), "b3": np.zeros(h2),
             "gamma": np.ones(h2), "beta": np.zeros(h2)}
+
+
+# --------------------------------------------------------------------------- the SG-joint model
+def unpack_layer(flat, F, hidden):
+    """A layer's flat parameter vector (include/snd_vae.h layout: Matrix1, bias1, Matrix2,
+    bias2, Matrix3, bias3, BN gamma, BN beta) -> dict of views (numpy or torch)."""
+    h0, h1, h2 = hidden
+    shapes = [("M1", (3 * F + 3, h0)), ("b1", (h0,)), ("M2", (2 * F + 1 + h0, h1)), ("b2", (h1,)),
+              ("M3", (F + h1, h2)), ("b3", (h2,)), ("gamma", (h2,)), ("beta", (h2,))]
+    out, o = {}, 0
+    for name, shp in shapes:
+        n = int(np.prod(shp))
+        out[name] = flat[o:o + n].reshape(shp)
+        o += n
+    assert o == flat.shape[0], (o, flat.shape)
+    return out
+
+
+def sgjoint_loss_torch(p, trees, X, rel, adj, Xf, S, eps, cfg):
+    """The SND-VAE spatial-graph model, literally, in float64 torch ops (autograd for
+    the gradients):
+      model_joint.py:77-80   s_g = lrelu(BN(SGConv(trees, s_g, rel))) per layer, on the
+                             B*S spanning-tree copies (copy b*S + s: graph b's tree s,
+                             features and rel; main.py:254-262 feeds, aligned per graph)
+      model.py:146-151       h = flat(s_g) Wh + bh, [mu | s] per copy; z = mu + eps e^s
+      model.py:177,180       J = mean_s reshape(z Wp + bp, [B, S, N, node_h])
+      model_joint.py:112-145 decoders; optimizer.py:142-157,192-194 losses (KL over B*S*L)
+    p: torch params by block name (enc.sg0 / enc.sg1 flat); trees [B*S,N,N];
+    X [B*S,N,F]; rel [B*S,N,N]; adj / Xf / S per graph [B,N,.]; eps [B*S, L]."""
+    import torch
+
+    from oracle import ref_torch as T
+    B, n, _ = adj.shape
+    Sn, L = cfg.sampling_num, cfg.latent
+    s_g = X
+    F = X.shape[-1]
+    for i, hid in enumerate(cfg.sg_conv_hidden):
+        lp = unpack_layer(p[f"enc.sg{i}"], F, hid)
+        y = sgconv_torch(trees, s_g, rel, lp)
+        s_g = T.lrelu(T.bn(y, lp["gamma"], lp["beta"]))
+        F = hid[2]
+    h = torch.reshape(s_g, [B * Sn, -1]) @ p["enc.Wh"] + p["enc.bh"]
+    ms = h @ p["enc.Wms"] + p["enc.bms"]
+    mu, s = ms[..., :L], ms[..., L:]
+    z = mu + eps * torch.exp(s)
+    J = torch.reshape(z @ p["dec.Wp"] + p["dec.bp"], [B, Sn, n, cfg.node_h_size]).mean(1)
+    return T.decoder_losses(p, J, adj, Xf, S, mu, s, cfg)
+
+
+def sgjoint_forward_backward(blocks, trees, X, rel, adj, Xf, S, eps, cfg):
+    """(losses dict, grads dict by block) of one step, float64."""
+    import torch
+    p = {k: torch.tensor(np.asarray(v, np.float64), requires_grad=True) for k, v in blocks.items()}
+    t = lambda a: torch.tensor(np.asarray(a, np.float64))
+    cost, parts = sgjoint_loss_torch(p, t(trees), t(X), t(rel), t(adj), t(Xf), t(S), t(eps), cfg)
+    cost.backward()
+    losses = {k: float(v.detach()) for k, v in parts.items()}
+    return losses, {k: v.grad.numpy() for k, v in p.items()}

@@ -69,6 +69,16 @@ def loss_fn(p, adj, X, Xf, S, eps, cfg):
         mu, s = ms[..., :L], ms[..., L:]
         z = mu + eps * torch.exp(s)
         J = z
+    return decoder_losses(p, J, adj, Xf, S, mu, s, cfg)
+
+
+def decoder_losses(p, J, adj, Xf, S, mu, s, cfg):
+    """The decoders and the ELBO from J [B,N,node_h] (model_joint.py:112-145,
+    model.py:205-208, optimizer.py:142-157,192-194); mu / s: the latent's mean and
+    log-std over which the KL mean runs."""
+    B, n, _ = adj.shape
+    s1 = cfg.s_d_channel[0]
+    X = J
     logit = torch.matmul(J, J.transpose(1, 2))
     diag = torch.ones(n, n, dtype=X.dtype) - torch.eye(n, dtype=X.dtype)
     l0 = diag * 0.0 * logit + (1 - diag)                  # model.py:206

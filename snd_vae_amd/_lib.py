@@ -17,9 +17,9 @@ c_int, c_ll, c_float, c_size, c_ull = C.c_int, C.c_longlong, C.c_float, C.c_size
 vp = C.c_void_p
 
 
-ABI_VERSION = 10
+ABI_VERSION = 11
 GEN_MODES = {"sample": 0, "mean": 1, "prior": 2, "given": 3}
-TOPOLOGY = {"tscale": 0, "tref": 1}
+TOPOLOGY = {"tscale": 0, "tref": 1, "sgjoint": 2}
 
 
 class SNDError(RuntimeError):
@@ -32,7 +32,8 @@ class Config(C.Structure):
                 ("spatial_dim", c_int), ("h0", c_int), ("h1", c_int), ("g_hidden", c_int),
                 ("latent", c_int), ("s1", c_int), ("s2", c_int), ("s3", c_int),
                 ("n1", c_int), ("n2", c_int), ("beta", c_float), ("pos_weight", c_float),
-                ("norm", c_float), ("dtype", c_int), ("topology", c_int), ("node_h", c_int)]
+                ("norm", c_float), ("dtype", c_int), ("topology", c_int), ("node_h", c_int),
+                ("sampling_num", c_int), ("sg_h", c_int * 6)]
 
 
 class SGGraph(C.Structure):
@@ -57,7 +58,8 @@ class Batch(C.Structure):
     """snd_batch_t"""
     _fields_ = [("rowptr", vp), ("colidx", vp), ("features", vp),
                 ("feature_truth", vp), ("spatial_truth", vp), ("row_order", vp),
-                ("tiles", RowTiles), ("window", WindowPlan)]
+                ("tiles", RowTiles), ("window", WindowPlan),
+                ("tree_rowptr", vp), ("tree_colidx", vp), ("rel", vp)]
 
 
 class LatentReg(C.Structure):

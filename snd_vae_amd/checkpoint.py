@@ -47,7 +47,7 @@ def read_config(path: str) -> SNDConfig:
         d = json.loads(f.metadata()["config"])
     for k, v in d.items():
         if isinstance(v, list):
-            d[k] = tuple(v)
+            d[k] = tuple(tuple(e) if isinstance(e, list) else e for e in v)
     return SNDConfig(**d)
 
 
@@ -118,21 +118,25 @@ def reference_to_blocks(cfg: SNDConfig, variables: dict, beta1: float = 0.9, bet
     has_adam = any(_strip(k).endswith("/Adam") for k in variables)
     m = {k: np.zeros(s) for k, s in shapes.items()} if has_adam else None
     v = {k: np.zeros(s) for k, s in shapes.items()} if has_adam else None
-    for name, (blk, sl) in logical_names(cfg).items():
+    for name, entry in logical_names(cfg).items():
+        blk, sl = entry[:2]
+        flat = len(entry) == 3          # stored flattened inside the block (shape entry[2])
         val = _lookup(variables, name)
         if val is None:
             raise KeyError(f"reference variable {name!r} not found")
         val = np.asarray(val, dtype=np.float64)
         dst = blocks[blk][..., sl]
-        if val.shape != dst.shape:
-            raise ValueError(f"{name}: shape {val.shape} != {dst.shape} of {blk}")
-        blocks[blk][..., sl] = val
+        want = entry[2] if flat else dst.shape
+        if val.shape != tuple(want):
+            raise ValueError(f"{name}: shape {val.shape} != {tuple(want)} of {blk}")
+        blocks[blk][..., sl] = val.reshape(-1) if flat else val
         if has_adam:
             for slot, tgt in (("Adam", m), ("Adam_1", v)):
                 s = _lookup(variables, f"{name}/{slot}")
                 if s is None:
                     raise KeyError(f"Adam slot {name}/{slot} not found")
-                tgt[blk][..., sl] = np.asarray(s, dtype=np.float64)
+                s = np.asarray(s, dtype=np.float64)
+                tgt[blk][..., sl] = s.reshape(-1) if flat else s
         if name.endswith("/gamma"):       # Keras BN: frozen moving statistics only
             scope = name[:-len("gamma")]
             for stat, want in (("moving_mean", 0.0), ("moving_variance", 1.0)):
@@ -185,11 +189,13 @@ def blocks_to_reference(cfg: SNDConfig, blocks: dict, adam_m: Optional[dict] = N
 
     from .params import logical_names
     out = {}
-    for name, (blk, sl) in logical_names(cfg).items():
-        out[name] = np.ascontiguousarray(blocks[blk][..., sl], dtype=np.float32)
+    for name, entry in logical_names(cfg).items():
+        blk, sl = entry[:2]
+        shp = (lambda a: a.reshape(entry[2])) if len(entry) == 3 else (lambda a: a)
+        out[name] = np.ascontiguousarray(shp(blocks[blk][..., sl]), dtype=np.float32)
         if adam_m is not None:
-            out[name + "/Adam"] = np.ascontiguousarray(adam_m[blk][..., sl], dtype=np.float32)
-            out[name + "/Adam_1"] = np.ascontiguousarray(adam_v[blk][..., sl], dtype=np.float32)
+            out[name + "/Adam"] = np.ascontiguousarray(shp(adam_m[blk][..., sl]), dtype=np.float32)
+            out[name + "/Adam_1"] = np.ascontiguousarray(shp(adam_v[blk][..., sl]), dtype=np.float32)
         if name.endswith("/gamma"):
             scope = name[:-len("gamma")]
             out[scope + "moving_mean"] = np.zeros_like(out[name])

@@ -56,10 +56,16 @@ class SNDConfig:
     pos_weight: float = 1.0
     norm: float = 1.0
     encoder_coords: bool = True         # X = [x_feat || S] (decision iii)
+    # sgjoint: the spatial-graph encoder over sampling_num spanning trees per graph
+    sampling_num: int = 10              # main.py:100
+    sg_conv_hidden: Tuple[Tuple[int, int, int], ...] = ((20, 20, 20), (50, 50, 50))   # main.py:193
 
     @property
     def f_in(self) -> int:
-        """Encoder input width (coordinates appended when encoder_coords)."""
+        """Encoder input width (coordinates appended when encoder_coords; the
+        spatial-graph encoder reads the coordinates through rel instead)."""
+        if self.topology == "sgjoint":
+            return self.num_feature
         if self.encoder_coords:
             return self.num_feature + self.spatial_dim
         return self.num_feature
@@ -70,7 +76,10 @@ class SNDConfig:
 
     @property
     def enc_width(self) -> int:
-        """Width of G = BN_enc([BN(P1) || X]) (model.py:109-112)."""
+        """Width of G = BN_enc([BN(P1) || X]) (model.py:109-112); sgjoint: the last
+        spatial-graph layer's width (model_joint.py:77-80)."""
+        if self.topology == "sgjoint":
+            return self.sg_conv_hidden[-1][2]
         return self.g_conv_hidden[1] + self.f_in
 
     def replace(self, **kw) -> "SNDConfig":
@@ -92,6 +101,20 @@ def tref(n_nodes: int, node_h: int, g_hidden: int = 100, latent: int = 100,
                      node_h_size=node_h, **kw)
 
 
+def sgjoint(n_nodes: int, node_h: int, g_hidden: int = 100, latent: int = 100,
+            sampling_num: int = 10, sg_conv_hidden=((20, 20, 20), (50, 50, 50)), **kw) -> SNDConfig:
+    """The SND-VAE spatial-graph encoder (model_joint.py:72-85, model.py:134-151):
+    two SpatialGraphConvolution layers over sampling_num spanning trees per graph,
+    flat heads per tree copy (sg_hidden_size = g_hidden, sg_latent_size = latent,
+    main.py:194-195), z averaged over the copies after d_sg_lin1 (model.py:177,180),
+    then the graph-latent decoders.  Synthetic2 widths by default (main.py:173-217)."""
+    kw.setdefault("encoder_coords", False)   # coordinates enter through rel
+    return SNDConfig(n_nodes=n_nodes, g_latent_size=latent, topology="sgjoint",
+                     g_conv_hidden=(node_h, node_h), g_hidden_size=g_hidden, node_h_size=node_h,
+                     sampling_num=sampling_num,
+                     sg_conv_hidden=tuple(tuple(int(v) for v in h) for h in sg_conv_hidden), **kw)
+
+
 PRESETS = {
     # C1: N=200 d=16, reference CPU plumbing.  tref as in model.py:104.
     "C1": tref(200, 16, mean_degree=8.0, encoder_coords=False),
@@ -105,4 +128,7 @@ PRESETS = {
     "C4": tref(4096, 64),
     # C5: N=16384 d=128 inner-product decoder stress.
     "C5": tscale(16384, 128),
+    # The reference's own scale for the spatial-graph encoder: synthetic2, N=25,
+    # 10 spanning trees per graph (main.py:100,173-217).
+    "SG25": sgjoint(25, 16, mean_degree=4.0),
 }

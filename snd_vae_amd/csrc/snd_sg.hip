@@ -19,6 +19,7 @@
 #include <algorithm>
 
 #include "snd_gemm.hpp"
+#include "snd_sg.hpp"
 
 namespace snd {
 namespace {
@@ -332,6 +333,37 @@ int colsum(const Geo& G, float* ws, const float* ones, const float* B, int N, hi
 }  // namespace snd
 
 using namespace snd;
+
+namespace snd {
+namespace {
+__global__ void sg_mean_kernel(const float* z, float* zbar, int B, int S, int L) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= B * L) return;
+  const int b = i / L, l = i - b * L;
+  float acc = 0.f;
+  for (int s = 0; s < S; ++s) acc += z[((long long)b * S + s) * L + l];
+  zbar[i] = acc / (float)S;
+}
+__global__ void sg_spread_kernel(const float* dzbar, float* dz, int B, int S, int L) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long long)B * S * L) return;
+  const long long c = i / L;
+  dz[i] = dzbar[(c / S) * L + (i - c * L)] / (float)S;
+}
+}  // namespace
+
+int launch_sg_mean(const float* z, float* zbar, int B, int S, int L, hipStream_t s) {
+  hipLaunchKernelGGL(sg_mean_kernel, dim3(cdiv(B * L, 256)), dim3(256), 0, s, z, zbar, B, S, L);
+  SND_LAUNCH_CHECK("sg_mean_kernel");
+  return 0;
+}
+int launch_sg_spread(const float* dzbar, float* dz, int B, int S, int L, hipStream_t s) {
+  hipLaunchKernelGGL(sg_spread_kernel, dim3(cdiv((long long)B * S * L, 256)), dim3(256), 0, s, dzbar, dz, B,
+                     S, L);
+  SND_LAUNCH_CHECK("sg_spread_kernel");
+  return 0;
+}
+}  // namespace snd
 
 extern "C" long long snd_sg_param_count(int f, int h0, int h1, int h2) {
   if (f <= 0 || h0 <= 0 || h1 <= 0 || h2 <= 0) return -1;

@@ -24,6 +24,7 @@
 #include "snd_head.hpp"
 #include "snd_spmm.hpp"
 #include "snd_tref.hpp"
+#include "snd_sg.hpp"
 #include "snd_zzt.hpp"
 
 namespace snd {
@@ -68,7 +69,11 @@ struct snd_plan {
   snd_config_t c;
   int B, N, R;
   int W, C1;                   // enc width, fused first decoder conv width
-  bool tref = false;           // graph-latent topology (SND_TREF)
+  bool tref = false;           // graph latent (SND_TREF, and SND_SGJOINT's decoder side)
+  bool sg = false;             // SND_SGJOINT: spatial-graph encoder over B*S spanning-tree copies
+  int S = 1;                   // SND_SGJOINT: copies (spanning trees) per graph
+  long long RS = 0;            // SND_SGJOINT: encoder rows B*S*N
+  int sgf[2] = {0, 0};         // SND_SGJOINT: each SG layer's input width
   int dj = 0;                  // width of J (decoder / zz^T input)
   int RH = 0;                  // rows of the head tensors h, [mu || s], z: B (tref) or R
   std::vector<Block> blocks;
@@ -102,7 +107,7 @@ struct snd_plan {
   unsigned long long rng_row0 = 0;
   unsigned long long eps_base() const { return rng_row0 * (unsigned long long)c.latent; }
   bool block_fused(const std::string& n) const {
-    return fuse_m && tref && (n == "enc.Wh" || n == "dec.Wp");
+    return fuse_m && tref && (n == "dec.Wp" || (n == "enc.Wh" && !sg));
   }
   // parameters of the last snd_train_step (snd_plan_launch re-runs kernels on them)
   mutable const float* last_params = nullptr;
@@ -140,15 +145,24 @@ struct snd_plan {
 };
 
 extern "C" const char* snd_last_error(void) { return g_err; }
-extern "C" int snd_abi_version(void) { return 10; }
+extern "C" int snd_abi_version(void) { return 11; }
 
 extern "C" int snd_plan_create(const snd_config_t* cfg, int n_graphs, snd_plan_t** out) {
   SND_CHECK_ARG(cfg && out && n_graphs > 0, "snd_plan_create: bad args");
   const snd_config_t& c = *cfg;
-  SND_CHECK_ARG(c.n_nodes > 0 && c.f_in > 0 && c.h0 > 0 && c.h1 > 0 && c.g_hidden > 0,
+  SND_CHECK_ARG(c.topology == SND_TSCALE || c.topology == SND_TREF || c.topology == SND_SGJOINT,
+                "snd_plan_create: bad topology");
+  const bool sg = c.topology == SND_SGJOINT;
+  const bool tref = c.topology != SND_TSCALE;
+  SND_CHECK_ARG(c.n_nodes > 0 && c.f_in > 0 && (sg || (c.h0 > 0 && c.h1 > 0)) && c.g_hidden > 0,
                 "snd_plan_create: non-positive width");
-  SND_CHECK_ARG(c.topology == SND_TSCALE || c.topology == SND_TREF, "snd_plan_create: bad topology");
-  const bool tref = c.topology == SND_TREF;
+  if (sg) {
+    bool ok = c.sampling_num > 0 && c.f_in == c.num_feature;
+    for (int i = 0; i < 6; ++i) ok = ok && c.sg_h[i] > 0 && c.sg_h[i] <= 256;
+    SND_CHECK_ARG(ok, "snd_plan_create: SND_SGJOINT needs sampling_num > 0, sg_h[6] in (0, 256] and "
+                      "f_in == num_feature");
+    SND_CHECK_ARG((long long)n_graphs * c.sampling_num <= 4096, "snd_plan_create: B * sampling_num <= 4096");
+  }
   const int dj = c.node_h;
   SND_CHECK_ARG(dj == 16 || dj == 32 || dj == 64 || dj == 128,
                 "snd_plan_create: node_h %d not in {16,32,64,128}", dj);
@@ -157,8 +171,8 @@ extern "C" int snd_plan_create(const snd_config_t* cfg, int n_graphs, snd_plan_t
                           c.g_hidden <= 128),
                 "snd_plan_create: graph latent needs <= %d graphs, latent <= 128, g_hidden %% 4 <= 128",
                 kTrefMaxB);
-  SND_CHECK_ARG(c.h0 <= 128 && c.h1 <= 128, "snd_plan_create: g_conv_hidden <= 128");
-  SND_CHECK_ARG(c.h1 + c.f_in <= 256 && c.s1 + c.n1 <= 256, "snd_plan_create: width <= 256");
+  SND_CHECK_ARG(sg || (c.h0 <= 128 && c.h1 <= 128), "snd_plan_create: g_conv_hidden <= 128");
+  SND_CHECK_ARG((sg || c.h1 + c.f_in <= 256) && c.s1 + c.n1 <= 256, "snd_plan_create: width <= 256");
   SND_CHECK_ARG(c.s3 <= 64 && c.n2 <= 64 && c.spatial_dim <= 4 && c.num_feature <= 4,
                 "snd_plan_create: head widths");
   SND_CHECK_ARG(c.dtype == SND_F32 || c.dtype == SND_BF16, "snd_plan_create: bad dtype");
@@ -167,23 +181,33 @@ extern "C" int snd_plan_create(const snd_config_t* cfg, int n_graphs, snd_plan_t
   if (!p) { set_error("snd_plan_create: out of memory"); return SND_ERR_ARG; }
   p->c = c;
   p->B = n_graphs; p->N = c.n_nodes; p->R = n_graphs * c.n_nodes;
-  p->W = c.h1 + c.f_in;
+  p->W = sg ? c.sg_h[5] : c.h1 + c.f_in;
   p->C1 = c.s1 + c.n1;
   p->tref = tref;
+  p->sg = sg;
+  p->S = sg ? c.sampling_num : 1;
+  p->RS = (long long)n_graphs * p->S * c.n_nodes;
   p->dj = dj;
-  p->RH = tref ? n_graphs : p->R;
+  p->RH = tref ? n_graphs * p->S : p->R;
   const int f = c.f_in, h0 = c.h0, h1 = c.h1, gh = c.g_hidden, L = c.latent;
   const int W = p->W, C1 = p->C1;
   const long long R = p->R, RH = p->RH;
   // ---- flat parameter layout (params.py::block_shapes order)
-  p->add_block("enc.W0", (long long)f * h0);
-  p->add_block("enc.bn0.gamma", h0);
-  p->add_block("enc.bn0.beta", h0);
-  p->add_block("enc.W1", (long long)(h0 + f) * h1);
-  p->add_block("enc.bn1.gamma", h1);
-  p->add_block("enc.bn1.beta", h1);
-  p->add_block("enc.bne.gamma", W);
-  p->add_block("enc.bne.beta", W);
+  if (sg) {   // SpatialGraphConvolution layers (snd_sg_param_count layout each)
+    p->sgf[0] = f;
+    p->sgf[1] = c.sg_h[2];
+    p->add_block("enc.sg0", snd_sg_param_count(f, c.sg_h[0], c.sg_h[1], c.sg_h[2]));
+    p->add_block("enc.sg1", snd_sg_param_count(c.sg_h[2], c.sg_h[3], c.sg_h[4], c.sg_h[5]));
+  } else {
+    p->add_block("enc.W0", (long long)f * h0);
+    p->add_block("enc.bn0.gamma", h0);
+    p->add_block("enc.bn0.beta", h0);
+    p->add_block("enc.W1", (long long)(h0 + f) * h1);
+    p->add_block("enc.bn1.gamma", h1);
+    p->add_block("enc.bn1.beta", h1);
+    p->add_block("enc.bne.gamma", W);
+    p->add_block("enc.bne.beta", W);
+  }
   p->add_block("enc.Wh", (tref ? (long long)p->N * W : W) * gh);
   p->add_block("enc.bh", gh);
   p->add_block("enc.Wms", (long long)gh * 2 * L);
@@ -244,7 +268,8 @@ extern "C" int snd_plan_create(const snd_config_t* cfg, int n_graphs, snd_plan_t
   p->add_buf("PENC1", (long long)nc * (2 * W + 2 * h1)); p->add_buf("PENC0", (long long)nc * 2 * h0);
   p->sW0 = wgrad_split(f, h0, p->R);
   p->sW1 = wgrad_split(h0 + f, h1, p->R);
-  p->sWh = wgrad_split(W + 1, gh, p->R);
+  p->sWh = sg ? wgrad_split((int)std::min<long long>((long long)p->N * W + 1, 1 << 30), gh, (int)RH)
+             : wgrad_split(W + 1, gh, p->R);
   p->sWms = wgrad_split(gh + 1, 2 * L, p->RH);
   p->sK1 = wgrad_split(5 * dj, C1, p->R);
   p->sK2s = wgrad_split(5 * c.s1, c.s2, p->R);
@@ -252,9 +277,21 @@ extern "C" int snd_plan_create(const snd_config_t* cfg, int n_graphs, snd_plan_t
   p->sK3s = wgrad_split(5 * c.s2, c.s3, p->R);
   p->add_buf("SW0", (long long)p->sW0.splits * f * h0);
   p->add_buf("SW1", (long long)p->sW1.splits * (h0 + f) * h1);
-  p->add_buf("SWH", (long long)p->sWh.splits * (W + 1) * gh);
+  p->add_buf("SWH", (long long)p->sWh.splits * ((sg ? (long long)p->N * W : W) + 1) * gh);
   p->add_buf("SWMS", (long long)p->sWms.splits * (gh + 1) * 2 * L);
   p->add_buf("SK1", (long long)p->sK1.splits * 5 * dj * C1);
+  if (sg) {   // spatial-graph encoder over the B*S copies (snd_sg.hip)
+    const long long RS = p->RS, nnz = 2LL * (p->N - 1) * n_graphs * p->S;   // spanning forests
+    const int* h = c.sg_h;
+    p->add_buf("SGLR", std::max(1LL, nnz)); p->add_buf("SGQ", std::max(1LL, nnz));
+    p->add_buf("SGREV", std::max(1LL, nnz)); p->add_buf("SGDEG", RS); p->add_buf("SGE", RS);
+    p->add_buf("SGBAD", 1);
+    p->add_buf("SGY1", RS * h[2]); p->add_buf("SGX1", RS * h[2]); p->add_buf("SGDX1", RS * h[2]);
+    p->add_buf("SGY2", RS * W);    p->add_buf("SGG", RS * W);      p->add_buf("SGDG", RS * W);
+    p->add_buf("SGWS0", (long long)snd_sg_workspace((int)RS, f, h[0], h[1], h[2]), 1);
+    p->add_buf("SGWS1", (long long)snd_sg_workspace((int)RS, h[2], h[3], h[4], h[5]), 1);
+    p->add_buf("ZBAR", (long long)n_graphs * L); p->add_buf("DZBAR", (long long)n_graphs * L);
+  }
   if (tref) {   // graph-latent heads / projection (snd_tref.hip)
     p->add_buf("ZL", RH * L);   p->add_buf("DZL", RH * L);
     p->add_buf("PHF", (long long)tref_head_fwd_blocks((long long)p->N * W, gh) * RH * gh);
@@ -273,7 +310,7 @@ extern "C" int snd_plan_create(const snd_config_t* cfg, int n_graphs, snd_plan_t
   const int wgc = (dbg & (4096 | 8192)) ? 0 : ((dbg & 16384) ? 32 : 64);
   auto wgc_of = [&](int, int, int) { return wgc; };
   // ---- bf16 fast decoder: split [s | n] column layouts, packed weight images
-  if (c.dtype == SND_BF16 && !(debug_flags() & 256)) {
+  if (c.dtype == SND_BF16 && !sg && !(debug_flags() & 256)) {
     const ColMap m1 = colmap_split(c.s1, c.n1), m2 = colmap_split(c.s2, c.n2);
     const int w1 = m1.phys(), w2 = m2.phys();
     auto img = [&](int kin, int nout) {
@@ -636,6 +673,51 @@ int encoder_generic_fwd(const Ctx& x, const snd_batch_t* batch) {
   SND_TRY(gemm_fwd(x, RH, 2 * L, gh, x.f("Hh"), gh, x.w("enc.Wms"), 2 * L, B_ROW, x.f("MS"), 2 * L,
                    x.w("enc.bms")));
   return 0;
+}
+
+// SND_SGJOINT encoder (model_joint.py:72-85 / model.py:134-151): the batch's
+// spanning-tree copies through two SpatialGraphConvolution layers (lrelu(BN(.))),
+// then per copy h = flat(s_g) Wh + bh and [mu || s] = h Wms + bms (rows RH = B*S).
+snd_sg_graph_t sg_graph(const Ctx& x, const snd_batch_t* batch) {
+  const snd_plan& p = *x.p;
+  return snd_sg_graph_t{batch->tree_rowptr, batch->tree_colidx, (int)p.RS, p.N, x.f("SGLR"), x.f("SGQ"),
+                        (int*)x.f("SGREV"), x.f("SGDEG"), x.f("SGE")};
+}
+
+int encoder_sg_fwd(const Ctx& x, const snd_batch_t* batch) {
+  const snd_plan& p = *x.p;
+  const snd_config_t& c = p.c;
+  const int N = p.N, gh = c.g_hidden, L = c.latent, W = p.W, RH = p.RH;
+  const int* h = c.sg_h;
+  SND_CHECK_ARG(batch->tree_rowptr && batch->tree_colidx && batch->rel,
+                "snd_train_step: SND_SGJOINT needs the batch's spanning trees and rel");
+  const snd_sg_graph_t g = sg_graph(x, batch);
+  SND_TRY(snd_sg_prep(&g, batch->rel, (int*)x.f("SGBAD"), x.s));
+  SND_TRY(snd_sg_layer_fwd(&g, batch->features, p.sgf[0], p.sgf[0], h[0], h[1], h[2], x.w("enc.sg0"), 1,
+                           x.f("SGY1"), x.f("SGX1"), x.f("SGWS0"), x.s));
+  SND_TRY(snd_sg_layer_fwd(&g, x.f("SGX1"), h[2], h[2], h[3], h[4], h[5], x.w("enc.sg1"), 1,
+                           x.f("SGY2"), x.f("SGG"), x.f("SGWS1"), x.s));
+  const int KH = N * W;   // flat(s_g) per copy: the row-major [N, W] rows of one copy
+  SND_TRY(gemm_fwd(x, RH, gh, KH, x.f("SGG"), KH, x.w("enc.Wh"), gh, B_ROW, x.f("Hh"), gh, x.w("enc.bh")));
+  return gemm_fwd(x, RH, 2 * L, gh, x.f("Hh"), gh, x.w("enc.Wms"), 2 * L, B_ROW, x.f("MS"), 2 * L,
+                  x.w("enc.bms"));
+}
+
+// backward from DH (dL/dh per copy): dWh / dbh (split-K slab), dG = DH Wh^T, then
+// both SG layers (their gradients written straight into the flat gradient blocks)
+int encoder_sg_bwd(const Ctx& x, const snd_batch_t* batch) {
+  const snd_plan& p = *x.p;
+  const snd_config_t& c = p.c;
+  const int N = p.N, gh = c.g_hidden, W = p.W, RH = p.RH;
+  const int* h = c.sg_h;
+  const int KH = N * W;
+  SND_TRY(gemm_wgrad(x, x.f("SGG"), KH, KH, true, x.f("DH"), gh, gh, x.f("SWH"), p.sWh, RH));
+  SND_TRY(gemm_fwd(x, RH, KH, gh, x.f("DH"), gh, x.w("enc.Wh"), gh, B_COL, x.f("SGDG"), KH, nullptr));
+  const snd_sg_graph_t g = sg_graph(x, batch);
+  SND_TRY(snd_sg_layer_bwd(&g, x.f("SGX1"), h[2], h[2], h[3], h[4], h[5], x.w("enc.sg1"), 1, x.f("SGY2"),
+                           x.f("SGDG"), x.f("SGDX1"), h[2], x.g("enc.sg1"), x.f("SGWS1"), x.s));
+  return snd_sg_layer_bwd(&g, batch->features, p.sgf[0], p.sgf[0], h[0], h[1], h[2], x.w("enc.sg0"), 1,
+                          x.f("SGY1"), x.f("SGDX1"), nullptr, p.sgf[0], x.g("enc.sg0"), x.f("SGWS0"), x.s);
 }
 
 // ---- bf16 fast decoder ------------------------------------------------------
@@ -1130,7 +1212,7 @@ extern "C" int snd_generate(const snd_plan_t* plan, const snd_batch_t* batch, co
   const int sd = c.spatial_dim, nf = c.num_feature;
   const long long CP = (long long)N * dj;
   float* zl = p.tref ? x.f("ZL") : x.f("Z");
-  if (enc) SND_TRY(encoder_generic_fwd(x, batch));
+  if (enc) SND_TRY(p.sg ? encoder_sg_fwd(x, batch) : encoder_generic_fwd(x, batch));
   if (mode == SND_GEN_MEAN) {             // z = mu
     if (hipMemcpy2DAsync(zl, (size_t)L * 4, x.f("MS"), (size_t)2 * L * 4, (size_t)L * 4, RH,
                          hipMemcpyDeviceToDevice, x.s) != hipSuccess) {
@@ -1154,8 +1236,9 @@ extern "C" int snd_generate(const snd_plan_t* plan, const snd_batch_t* batch, co
     a.eps_base = p.eps_base();
     SND_TRY(launch_reparam_fwd(a, x.s));
   }
+  if (p.sg) SND_TRY(launch_sg_mean(x.f("ZL"), x.f("ZBAR"), p.B, p.S, L, x.s));   // model.py:177,180
   if (p.tref) {   // J = reshape(z Wp + bp, [B, N, node_h]) (model_joint.py:97)
-    TrefProjFwdArgs a{x.f("ZL"), p.B, L, x.w("dec.Wp"), x.w("dec.bp"), CP, x.f("Z")};
+    TrefProjFwdArgs a{x.f(p.sg ? "ZBAR" : "ZL"), p.B, L, x.w("dec.Wp"), x.w("dec.bp"), CP, x.f("Z")};
     SND_TRY(launch_tref_proj_fwd(a, x.s));
   }
   // decoders (model_joint.py:112-145): conv1d k5 SAME -> BN -> lrelu, sigmoid heads
@@ -1223,7 +1306,7 @@ extern "C" int snd_plan_launch(const snd_plan_t* plan, const snd_batch_t* batch,
     return launch_spmm_bf16(a, s);
   }
   if (!strncmp(kernel, "tref_", 5)) {   // graph-latent weight-streaming kernels
-    SND_CHECK_ARG(p.tref && p.last_params, "snd_plan_launch: no graph-latent step has run");
+    SND_CHECK_ARG(p.tref && !p.sg && p.last_params, "snd_plan_launch: no graph-latent step has run");
     Ctx x{&p, ws, p.last_params, p.last_grads, s};
     const snd_config_t& c = p.c;
     const long long KH = (long long)p.N * p.W, CP = (long long)p.N * p.dj;
@@ -1321,7 +1404,9 @@ extern "C" int snd_train_step(const snd_plan_t* plan, const snd_batch_t* batch,
   }
 
   // =============================== forward ===============================
-  if (p.fast_enc) {
+  if (p.sg) {
+    SND_TRY(encoder_sg_fwd(x, batch));
+  } else if (p.fast_enc) {
     SND_TRY(encoder_fast_fwd(x, batch));
   } else {
     SND_TRY(encoder_generic_fwd(x, batch));
@@ -1339,14 +1424,16 @@ extern "C" int snd_train_step(const snd_plan_t* plan, const snd_batch_t* batch,
   // z = mu + eps exp(s) (model.py:159); KL partials (optimizer.py:193)
   const ZztStage stg = zzt_stage(x.ws + p.buf("ZSTAGE"), p.B, N, dj, c.dtype);
   if (p.tref) {
-    {   // z [B, L] (model_joint.py:89)
+    {   // z [B, L] (model_joint.py:89); SND_SGJOINT: [B*S, L] (model.py:157)
       ReparamFwdArgs a{x.f("MS"), 2 * L, RH, L, eps, seed, step_counter, x.f("EPS"), x.f("ZL"),
                        x.d("PKL"), nullptr, L};
       a.eps_base = p.eps_base();
       SND_TRY(launch_reparam_fwd(a, x.s));
     }
+    // SND_SGJOINT: mean over the copies before the (affine) projection (model.py:177,180)
+    if (p.sg) SND_TRY(launch_sg_mean(x.f("ZL"), x.f("ZBAR"), p.B, p.S, L, x.s));
     {   // J = reshape(z Wp + bp, [B, N, node_h]) (model_joint.py:97)
-      TrefProjFwdArgs a{x.f("ZL"), p.B, L, x.w("dec.Wp"), x.w("dec.bp"), CP, x.f("Z")};
+      TrefProjFwdArgs a{x.f(p.sg ? "ZBAR" : "ZL"), p.B, L, x.w("dec.Wp"), x.w("dec.bp"), CP, x.f("Z")};
       SND_TRY(launch_tref_proj_fwd(a, x.s));
     }
     if (p.fast) {   // bf16 J for the decoder + zz^T staging images
@@ -1452,13 +1539,15 @@ extern "C" int snd_train_step(const snd_plan_t* plan, const snd_batch_t* batch,
   } else {
     if (p.tref) {
       {   // d_sg_lin1 backward: dWp, dbp written; dz partials per block
-        TrefProjBwdArgs a{x.f("ZL"), p.B, L, x.w("dec.Wp"), CP, x.f("DZDEC"), x.f("DJD"), x.f("EJ"),
-                          adj_scale, x.g("dec.Wp"), x.g("dec.bp"), x.f("PDZ")};
+        TrefProjBwdArgs a{x.f(p.sg ? "ZBAR" : "ZL"), p.B, L, x.w("dec.Wp"), CP, x.f("DZDEC"), x.f("DJD"),
+                          x.f("EJ"), adj_scale, x.g("dec.Wp"), x.g("dec.bp"), x.f("PDZ")};
         if (p.block_fused("dec.Wp")) a.adam = fused_adam(x, "dec.Wp", step_counter);
         SND_TRY(launch_tref_proj_bwd(a, x.s));
-        const ReduceDesc rd{x.f("PDZ"), x.f("DZL"), tref_proj_bwd_blocks(CP), RH * L,
-                            (long long)RH * L, 1.f, 0, 0, 0, 0};
+        const int rz = p.B;   // rows of the projection's input: B graphs
+        const ReduceDesc rd{x.f("PDZ"), x.f(p.sg ? "DZBAR" : "DZL"), tref_proj_bwd_blocks(CP), rz * L,
+                            (long long)rz * L, 1.f, 0, 0, 0, 0};
         SND_TRY(launch_reduce(&rd, 1, x.s));
+        if (p.sg) SND_TRY(launch_sg_spread(x.f("DZBAR"), x.f("DZL"), p.B, p.S, L, x.s));
       }
       ReparamBwdArgs a{x.f("MS"), 2 * L, RH, L, x.f("EPS"), x.f("DZL"), nullptr, nullptr, 0.f,
                        kl_scale, x.f("DMS"), 2 * L};
@@ -1471,7 +1560,9 @@ extern "C" int snd_train_step(const snd_plan_t* plan, const snd_batch_t* batch,
     SND_TRY(gemm_wgrad(x, x.f("Hh"), gh, gh, true, x.f("DMS"), 2 * L, 2 * L, x.f("SWMS"), p.sWms, RH));
     SND_TRY(gemm_fwd(x, RH, gh, 2 * L, x.f("DMS"), 2 * L, x.w("enc.Wms"), 2 * L, B_COL, x.f("DH"), gh,
                      nullptr));
-    if (p.tref) {   // dWh written complete; dG = dh Wh^T per graph
+    if (p.sg) {
+      SND_TRY(encoder_sg_bwd(x, batch));
+    } else if (p.tref) {   // dWh written complete; dG = dh Wh^T per graph
       TrefHeadBwdArgs a{x.f("G"), KH, p.B, x.w("enc.Wh"), gh, x.f("DH"), x.g("enc.Wh"), x.f("DG")};
       if (p.fast_enc) {   // bf16 G in, bf16 dG rows out (the fast encoder's operands)
         a.g = nullptr; a.dg = nullptr;
@@ -1487,7 +1578,7 @@ extern "C" int snd_train_step(const snd_plan_t* plan, const snd_batch_t* batch,
   }
   if (p.fast_enc && p.tref) {
     SND_TRY(encoder_fast_bwd_tail(x, batch));
-  } else if (!p.fast_enc) {
+  } else if (!p.fast_enc && !p.sg) {
     {
       EncBwdArgs a{x.f("DG"), W, x.f("H2"), W, x.w("enc.bne.gamma"), W, x.f("P1"), h1,
                    x.w("enc.bn1.gamma"), h1, x.f("DP1"), h1, x.f("PENC1"), 1};
@@ -1531,14 +1622,16 @@ extern "C" int snd_train_step(const snd_plan_t* plan, const snd_batch_t* batch,
     rd.push_back({s0, x.g(wname), sp.splits, wlen, (long long)Mtot * N_, 1.f, 0});
     if (bname) rd.push_back({s0 + wlen, x.g(bname), sp.splits, N_, (long long)Mtot * N_, 1.f, 0});
   };
-  if (p.fast_enc) {
+  if (p.sg) {
+    slab("SWH", p.sWh, (int)KH + 1, gh, "enc.Wh", (int)KH * gh, "enc.bh");
+  } else if (p.fast_enc) {
     encoder_fast_reduce(x, rd);
   } else {
     slab("SW0", p.sW0, f, h0, "enc.W0", f * h0, nullptr);
     slab("SW1", p.sW1, h0 + f, h1, "enc.W1", (h0 + f) * h1, nullptr);
     if (!p.tref) slab("SWH", p.sWh, W + 1, gh, "enc.Wh", W * gh, "enc.bh");
   }
-  if (p.tref)   // dbh = sum over graphs of dh
+  if (p.tref && !p.sg)   // dbh = sum over graphs of dh
     rd.push_back({x.f("DH"), x.g("enc.bh"), RH, gh, (long long)gh, 1.f, 0});
   if (!p.fast_enc || p.tref) slab("SWMS", p.sWms, gh + 1, 2 * L, "enc.Wms", gh * 2 * L, "enc.bms");
   if (!p.fast) {
@@ -1550,7 +1643,7 @@ extern "C" int snd_train_step(const snd_plan_t* plan, const snd_batch_t* batch,
   auto cols = [&](const char* buf, int stride, int off, int len, const char* dst) {
     rd.push_back({x.f(buf) + off, x.g(dst), nc, len, (long long)stride, 1.f, 0});
   };
-  if (!p.fast_enc) {
+  if (!p.fast_enc && !p.sg) {
     cols("PENC1", 2 * W + 2 * h1, 0, W, "enc.bne.gamma");
     cols("PENC1", 2 * W + 2 * h1, W, W, "enc.bne.beta");
     cols("PENC1", 2 * W + 2 * h1, 2 * W, h1, "enc.bn1.gamma");

@@ -74,6 +74,70 @@ class GraphBatch:
         return a
 
 
+@dataclass
+class SGBatch(GraphBatch):
+    """A batch for the spatial-graph encoder (config topology 'sgjoint').
+
+    The GraphBatch fields hold the B graphs' adj_truth CSR and decoder targets, and
+    ``features`` the encoder input of every spanning-tree copy: [B*S*N, num_feature],
+    copy c = b*S + s holding graph b's node features.  ``tree_rowptr`` /
+    ``tree_colidx``: the copies' spanning trees as one symmetric block-diagonal CSR
+    over B*S*N rows (input_data.py:76-83); ``rel`` [B*S, N, N] float32 the copies'
+    pairwise distances (2D_rel.npy / 600, input_data.py:59).  The reference feeds
+    features and rel tiled sample-major (np.tile, main.py:307-309) against graph-major
+    trees; the copies here keep each graph's own data."""
+    sampling_num: int = 1
+    tree_rowptr: np.ndarray = None
+    tree_colidx: np.ndarray = None
+    rel: np.ndarray = None
+
+
+def pairwise_rel(pos: np.ndarray) -> np.ndarray:
+    """cal_rel_dist (input_data.py:145-151): Euclidean distances between nodes."""
+    d = pos[:, None, :] - pos[None, :, :]
+    return np.sqrt((d * d).sum(-1))
+
+
+def make_sg_batch(base: GraphBatch, trees: Sequence[Sequence[np.ndarray]], rel: np.ndarray,
+                  num_feature: int) -> SGBatch:
+    """SGBatch from a GraphBatch (targets, adj_truth), per graph S spanning-tree edge
+    arrays [2, 2k] (input_data.spanning_tree_edges) and rel [B, N, N]."""
+    B, n = base.n_graphs, base.n_nodes
+    S = len(trees[0])
+    if any(len(t) != S for t in trees) or rel.shape != (B, n, n):
+        raise ValueError("make_sg_batch: every graph needs S trees and rel [B, N, N]")
+    parts = []
+    for b in range(B):
+        for e in trees[b]:
+            parts.append(csr_from_pairs(n, np.asarray(e, np.int64).T))
+    trp, tci = stack_csr(parts, n)
+    x = base.feature_truth.reshape(B, n, -1)[:, :, :num_feature]
+    xc = np.repeat(x, S, axis=0).reshape(B * S * n, -1)
+    relc = np.repeat(np.asarray(rel, np.float32), S, axis=0)
+    return SGBatch(B, n, base.rowptr, base.colidx, np.ascontiguousarray(xc, np.float32),
+                   base.feature_truth, base.spatial_truth, S, trp, tci, np.ascontiguousarray(relc))
+
+
+def sgjoint_batch(cfg: SNDConfig, n_graphs: int, seed: Optional[int] = None) -> SGBatch:
+    """B seeded RGG graphs with cfg.sampling_num scipy-MST spanning trees each under
+    U[1,2) edge weights (input_data.py:18-38, np.random.RandomState(seed)) and rel
+    from the node positions."""
+    from .input_data import spanning_tree_edges
+    seed = cfg.seed if seed is None else seed
+    base = synthetic_batch(cfg, n_graphs, seed=seed)
+    n = cfg.n_nodes
+    rs = np.random.RandomState(seed)
+    trees, rel = [], []
+    for b in range(n_graphs):
+        lo = b * n
+        rp = base.rowptr[lo:lo + n + 1].astype(np.int64) - int(base.rowptr[lo])
+        cols = base.colidx[int(base.rowptr[lo]):int(base.rowptr[lo + n])].astype(np.int64) - lo
+        raw = np.stack([np.repeat(np.arange(n), np.diff(rp)), cols], 1)
+        trees.append([spanning_tree_edges(raw, n, rs) for _ in range(cfg.sampling_num)])
+        rel.append(pairwise_rel(base.spatial_truth[lo:lo + n].astype(np.float64)))
+    return make_sg_batch(base, trees, np.stack(rel).astype(np.float32), cfg.num_feature)
+
+
 def rgg_edges(n: int, kbar: float, rng: np.random.Generator):
     """Random geometric graph: returns (positions [n,2], i<j pair array)."""
     from scipy.spatial import cKDTree

@@ -230,6 +230,21 @@ def dataset_class_balance(ds: "SynDataset") -> Tuple[float, float]:
     return class_balance(mats, n, ones)
 
 
+def dataset_sg_batch(ds: "SynDataset", cfg: SNDConfig, graphs: Sequence[int]):
+    """The SGBatch of the given graphs (main.py:316-323 slices of adj / features /
+    rel and the truths): their sampled spanning trees and rel (input_data.py:59,76-83)."""
+    from .data import make_sg_batch
+    if ds.rel is None:
+        raise ValueError("the spatial-graph encoder needs 2D_rel.npy (load_rel=True)")
+    graphs = list(graphs)
+    if any(len(ds.trees[g]) != cfg.sampling_num for g in graphs):
+        raise ValueError(f"dataset sampled {len(ds.trees[graphs[0]])} trees, config sampling_num "
+                         f"{cfg.sampling_num}")
+    base = ds.batch(cfg, graphs)
+    return make_sg_batch(base, [ds.trees[g] for g in graphs], np.asarray(ds.rel[graphs], np.float32),
+                         cfg.num_feature)
+
+
 def load_data_syn(type_: str, path: str, sampling_num: int = 10, num_feature: int = 1,
                   rng=None, allow_pickle: bool = False, shuffle: bool = True,
                   load_rel: bool = True) -> SynDataset:

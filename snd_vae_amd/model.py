@@ -24,7 +24,7 @@ import torch
 
 from . import _lib
 from .config import SNDConfig
-from .data import GraphBatch, locality_order, row_tiles, window_plan
+from .data import GraphBatch, SGBatch, locality_order, row_tiles, window_plan
 from .params import flat_layout, init_blocks
 
 DTYPES = {"f32": 0, "fp32": 0, "bf16": 1}
@@ -35,10 +35,15 @@ WINDOW_MAX_BETA = 352  # the window SpMM's ring bound (spmm_win_max_beta)
 def c_config(cfg: SNDConfig, dtype: str) -> _lib.Config:
     s1, s2, s3 = cfg.s_d_channel
     n1, n2 = cfg.n_d_channel
+    sg = cfg.topology == "sgjoint"
+    sgh = [int(v) for h in cfg.sg_conv_hidden for v in h] if sg else [0] * 6
+    if sg and len(sgh) != 6:
+        raise ValueError("sgjoint: sg_conv_hidden must hold two layers of three widths")
     return _lib.Config(cfg.n_nodes, cfg.f_in, cfg.num_feature, cfg.spatial_dim,
                        cfg.g_conv_hidden[0], cfg.g_conv_hidden[1], cfg.g_hidden_size,
                        cfg.latent, s1, s2, s3, n1, n2, cfg.beta, cfg.pos_weight, cfg.norm,
-                       DTYPES[dtype], _lib.TOPOLOGY[cfg.topology], cfg.node_h_size)
+                       DTYPES[dtype], _lib.TOPOLOGY[cfg.topology], cfg.node_h_size,
+                       cfg.sampling_num if sg else 0, (C.c_int * 6)(*sgh))
 
 
 class DeviceTiles:
@@ -68,6 +73,17 @@ class DeviceBatch:
         (with locality): the window SpMM's plan over the schedule (data.window_plan),
         used by the step's width-64 backward SpMM when its beta fits the ring."""
         t = lambda a, dt: torch.from_numpy(np.ascontiguousarray(a)).to(device=device, dtype=dt)
+        self.sg = isinstance(batch, SGBatch)
+        if self.sg:   # spatial-graph encoder: its trees and rel; the gather schedules do not apply
+            locality = False
+            tr = batch.tree_rowptr.astype(np.int64)
+            rows = np.repeat(np.arange(len(tr) - 1), np.diff(tr))
+            key = rows * len(tr) + batch.tree_colidx
+            if not np.array_equal(np.sort(key), np.sort(batch.tree_colidx.astype(np.int64) * len(tr) + rows)):
+                raise ValueError("spanning trees must be symmetric (input_data.py:31-37)")
+            self.tree_rowptr = t(batch.tree_rowptr, torch.int32)
+            self.tree_colidx = t(batch.tree_colidx if batch.tree_colidx.size else np.zeros(1), torch.int32)
+            self.rel = t(batch.rel, torch.float32)
         self.n_graphs = batch.n_graphs
         self.n_nodes = batch.n_nodes
         self.nnz = batch.nnz
@@ -97,8 +113,9 @@ class DeviceBatch:
         tl = self.tiles.c_struct() if self.tiles else _lib.RowTiles()
         w = self.window
         wp = _lib.WindowPlan(p(w[0]), p(w[1]), p(w[2]), p(w[3]), w[4]) if w else _lib.WindowPlan(None, None, None, None, -1)
+        sg = (p(self.tree_rowptr), p(self.tree_colidx), p(self.rel)) if self.sg else (None, None, None)
         return _lib.Batch(p(self.rowptr), p(self.colidx), p(self.features),
-                          p(self.feature_truth), p(self.spatial_truth), p(self.row_order), tl, wp)
+                          p(self.feature_truth), p(self.spatial_truth), p(self.row_order), tl, wp, *sg)
 
 
 class SGCNModelVAE:
@@ -162,16 +179,25 @@ class SGCNModelVAE:
         return t.view(*shape) if shape is not None else t
 
     def _rows(self, name, width, per_graph=False):
-        rows = self.n_graphs if per_graph else self.n_graphs * self.cfg.n_nodes
+        rows = self.head_rows if per_graph else self.n_graphs * self.cfg.n_nodes
         return self.buffer(name)[:rows * width].view(rows, width)
 
     @property
     def _graph_latent(self):
-        return self.cfg.topology == "tref"
+        return self.cfg.topology != "tscale"
+
+    @property
+    def head_rows(self) -> int:
+        """Rows of mu / log-std / z: B*N (node latent), B (graph latent), B*S (sgjoint:
+        one latent per spanning-tree copy, model.py:148-151)."""
+        c = self.cfg
+        if c.topology == "tscale":
+            return self.n_graphs * c.n_nodes
+        return self.n_graphs * (c.sampling_num if c.topology == "sgjoint" else 1)
 
     @property
     def z_mean_sg(self):
-        """[B, L] (graph latent) or [B*N, L] (node latent), model_joint.py:84."""
+        """[B, L] (graph latent), [B*S, L] (sgjoint) or [B*N, L] (node latent), model_joint.py:84."""
         return self._rows("MS", 2 * self.cfg.latent, self._graph_latent)[:, :self.cfg.latent]
 
     @property

@@ -64,8 +64,7 @@ class OptimizerVAE:
             import torch.distributed as dist
             self.world = dist.get_world_size(process_group)
             self.rank = dist.get_rank(process_group)
-            head_rows = model.n_graphs * (1 if cfg.topology == "tref" else cfg.n_nodes)
-            _lib.check(L.snd_plan_set_rng_offset(model.plan, self.rank * head_rows),
+            _lib.check(L.snd_plan_set_rng_offset(model.plan, self.rank * model.head_rows),
                        "snd_plan_set_rng_offset")
         self._graph = None
         self._batch_c = None

@@ -33,10 +33,25 @@ from .config import CONV_K, SNDConfig
 ALIGN = 64
 
 
+def sg_layer_shapes(f: int, hidden) -> "List[Tuple[str, Tuple[int, ...]]]":
+    """One SpatialGraphConvolution layer's variables in the flat layer layout of
+    snd_sg_param_count (include/snd_vae.h; layers.py:158-169, BN of model_joint.py:78)."""
+    h0, h1, h2 = hidden
+    return [("Matrix1", (3 * f + 3, h0)), ("bias1", (h0,)), ("Matrix2", (2 * f + 1 + h0, h1)),
+            ("bias2", (h1,)), ("Matrix3", (f + h1, h2)), ("bias3", (h2,)), ("gamma", (h2,)),
+            ("beta", (h2,))]
+
+
+def sg_layer_inputs(cfg: SNDConfig) -> List[int]:
+    """Input width of each spatial-graph layer."""
+    return [cfg.f_in] + [h[2] for h in cfg.sg_conv_hidden[:-1]]
+
+
 def block_shapes(cfg: SNDConfig) -> "OrderedDict[str, Tuple[int, ...]]":
-    if cfg.topology not in ("tscale", "tref"):
+    if cfg.topology not in ("tscale", "tref", "sgjoint"):
         raise ValueError(f"unknown topology {cfg.topology!r}")
-    tref = cfg.topology == "tref"
+    sg = cfg.topology == "sgjoint"
+    tref = cfg.topology != "tscale"
     f, (h0, h1), gh, L, nh = (cfg.f_in, cfg.g_conv_hidden, cfg.g_hidden_size,
                               cfg.latent, cfg.node_h_size)
     if not tref and nh != L:
@@ -46,15 +61,22 @@ def block_shapes(cfg: SNDConfig) -> "OrderedDict[str, Tuple[int, ...]]":
     n1, n2 = cfg.n_d_channel
     k = CONV_K
     shapes = OrderedDict()
-    shapes["enc.W0"] = (f, h0)
-    shapes["enc.bn0.gamma"] = (h0,)
-    shapes["enc.bn0.beta"] = (h0,)
-    shapes["enc.W1"] = (h0 + f, h1)
-    shapes["enc.bn1.gamma"] = (h1,)
-    shapes["enc.bn1.beta"] = (h1,)
-    shapes["enc.bne.gamma"] = (h1 + f,)
-    shapes["enc.bne.beta"] = (h1 + f,)
-    shapes["enc.Wh"] = ((n * (h1 + f)) if tref else (h1 + f), gh)
+    if sg:
+        if len(cfg.sg_conv_hidden) != 2:
+            raise ValueError("sgjoint: two spatial-graph layers (the plan's encoder)")
+        for i, (fi, hid) in enumerate(zip(sg_layer_inputs(cfg), cfg.sg_conv_hidden)):
+            shapes[f"enc.sg{i}"] = (sum(int(np.prod(sh)) for _, sh in sg_layer_shapes(fi, hid)),)
+    else:
+        shapes["enc.W0"] = (f, h0)
+        shapes["enc.bn0.gamma"] = (h0,)
+        shapes["enc.bn0.beta"] = (h0,)
+        shapes["enc.W1"] = (h0 + f, h1)
+        shapes["enc.bn1.gamma"] = (h1,)
+        shapes["enc.bn1.beta"] = (h1,)
+        shapes["enc.bne.gamma"] = (h1 + f,)
+        shapes["enc.bne.beta"] = (h1 + f,)
+    W = cfg.enc_width
+    shapes["enc.Wh"] = ((n * W) if tref else W, gh)
     shapes["enc.bh"] = (gh,)
     shapes["enc.Wms"] = (gh, 2 * L)
     shapes["enc.bms"] = (2 * L,)
@@ -84,8 +106,10 @@ def block_shapes(cfg: SNDConfig) -> "OrderedDict[str, Tuple[int, ...]]":
     return shapes
 
 
-def logical_names(cfg: SNDConfig) -> Dict[str, Tuple[str, slice]]:
-    """Reference variable name -> (physical block, slice on the last axis)."""
+def logical_names(cfg: SNDConfig) -> Dict[str, tuple]:
+    """Reference variable name -> (physical block, slice on the last axis), or for a
+    variable stored flattened inside a block (the spatial-graph layers) (block, flat
+    slice, the variable's shape)."""
     L = cfg.latent
     s1 = cfg.s_d_channel[0]
     n1 = cfg.n_d_channel[0]
@@ -132,8 +156,24 @@ def logical_names(cfg: SNDConfig) -> Dict[str, Tuple[str, slice]]:
         "decoder/d_n_lin2/Matrix": ("dec.Wn", full),
         "decoder/d_n_lin2/bias": ("dec.bn", full),
     }
-    if cfg.topology != "tref":
+    if cfg.topology == "tscale":
         del m["decoder/d_sg_lin1/Matrix"], m["decoder/d_sg_lin1/bias"]
+    if cfg.topology == "sgjoint":   # model_joint.py:72-85: g_sg<i>_conv, g_bn_sg<i>, g_sg1..3_lin
+        for k in [k for k in m if k.startswith("encoder/")]:
+            del m[k]
+        for i, (fi, hid) in enumerate(zip(sg_layer_inputs(cfg), cfg.sg_conv_hidden)):
+            o = 0
+            for name, shp in sg_layer_shapes(fi, hid):
+                size = int(np.prod(shp))
+                ref = (f"encoder/g_bn_sg{i}/{name}" if name in ("gamma", "beta")
+                       else f"encoder/g_sg{i}_conv/{name}")
+                m[ref] = (f"enc.sg{i}", slice(o, o + size), shp)
+                o += size
+        m.update({"encoder/g_sg1_lin/Matrix": ("enc.Wh", full), "encoder/g_sg1_lin/bias": ("enc.bh", full),
+                  "encoder/g_sg2_lin/Matrix": ("enc.Wms", slice(0, L)),
+                  "encoder/g_sg2_lin/bias": ("enc.bms", slice(0, L)),
+                  "encoder/g_sg3_lin/Matrix": ("enc.Wms", slice(L, 2 * L)),
+                  "encoder/g_sg3_lin/bias": ("enc.bms", slice(L, 2 * L))})
     return m
 
 
@@ -194,7 +234,17 @@ def init_blocks(cfg: SNDConfig, seed: int = 0) -> Dict[str, np.ndarray]:
     L = cfg.latent
     s1 = cfg.s_d_channel[0]
     for k, s in shapes.items():
-        if k in ("enc.W0", "enc.W1"):
+        if k.startswith("enc.sg"):                        # layers.py:158-169 + Keras BN
+            i = int(k[6:])
+            fi, hid = sg_layer_inputs(cfg)[i], cfg.sg_conv_hidden[i]
+            parts = []
+            for name, shp in sg_layer_shapes(fi, hid):
+                if name.startswith("Matrix"):
+                    parts.append(rng.normal(0.0, 0.02, shp).reshape(-1))
+                else:
+                    parts.append((np.ones(shp) if name == "gamma" else np.zeros(shp)).reshape(-1))
+            v = np.concatenate(parts)
+        elif k in ("enc.W0", "enc.W1"):
             v = _truncated_normal(rng, s, 0.02)           # GraphConvolution w
         elif k in ("enc.Wh", "dec.Ws", "dec.Wn", "dec.Wp"):
             v = rng.normal(0.0, 0.02, s)                  # linear Matrix

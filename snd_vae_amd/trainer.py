@@ -28,7 +28,7 @@ import torch
 from . import checkpoint as ckpt
 from .config import SNDConfig
 from .data import default_tile_rows
-from .input_data import SynDataset, dataset_class_balance
+from .input_data import SynDataset, dataset_class_balance, dataset_sg_batch
 from .model import DeviceBatch, SGCNModelVAE
 from .optimizer import LOSS_NAMES, OptimizerVAE
 
@@ -62,8 +62,10 @@ class Trainer:
         self.batches: List[DeviceBatch] = []
         for i in range(self.batch_num):
             lo = i * batch_size + rank * per
-            self.batches.append(DeviceBatch(dataset.batch(cfg, range(lo, lo + per)), device=device,
-                                            locality=locality,
+            graphs = range(lo, lo + per)
+            hb = (dataset_sg_batch(dataset, cfg, graphs) if cfg.topology == "sgjoint"
+                  else dataset.batch(cfg, graphs))
+            self.batches.append(DeviceBatch(hb, device=device, locality=locality,
                                             tile_rows=default_tile_rows(cfg.g_conv_hidden[1])))
         self.model = SGCNModelVAE(cfg, per, dtype=dtype, device=device, blocks=blocks)
         self.opt = OptimizerVAE(self.model, process_group=process_group, seed=seed)

@@ -112,7 +112,7 @@ def test_plan_layout_matches_python(lib_built):
     """snd_plan_create needs no GPU: check its flat layout against params.py."""
     from snd_vae_amd import _lib
     from snd_vae_amd.model import c_config
-    for preset in ("C1", "C1s", "C2", "C4", "C5"):
+    for preset in ("C1", "C1s", "C2", "C4", "C5", "SG25"):
         cfg = PRESETS[preset]
         L = _lib.lib()
         h = ctypes.c_void_p()

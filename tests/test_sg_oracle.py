@@ -125,3 +125,49 @@ def test_param_layout_matches_library():
     for f, hid in ((1, (20, 20, 20)), (20, (50, 50, 50)), (3, (4, 5, 6))):
         n = sum(int(np.prod(s)) for _, s in sg_param_shapes(f, hid))
         assert _lib.lib().snd_sg_param_count(f, *hid) == n
+
+
+def test_sgjoint_oracle_finite_differences():
+    """oracle.ref_sg.sgjoint_forward_backward (the whole SG-joint model in float64 torch
+    ops, autograd gradients) against central differences of its own cost on a small
+    case, and its decoder half against the GCN oracle's (ref_torch.decoder_losses is
+    shared with the node/graph-latent oracle)."""
+    import numpy as np
+    import torch
+
+    from oracle import ref_sg as RS
+    from snd_vae_amd.config import sgjoint
+    from snd_vae_amd.data import sgjoint_batch
+    from snd_vae_amd.params import init_blocks
+    cfg = sgjoint(8, 16, g_hidden=8, latent=4, sampling_num=2, sg_conv_hidden=((3, 4, 5), (4, 3, 6)),
+                  mean_degree=3.0, s_d_channel=(5, 4, 3), n_d_channel=(5, 4))
+    b = sgjoint_batch(cfg, 2, seed=1)
+    n, B, S = 8, 2, 2
+    trees = np.zeros((B * S, n, n))
+    rp, ci = b.tree_rowptr.astype(np.int64), b.tree_colidx.astype(np.int64)
+    for r in range(B * S * n):
+        trees[r // n, r % n, ci[rp[r]:rp[r + 1]] % n] = 1.0
+    ins = (trees, b.features.reshape(B * S, n, -1), b.rel, np.stack([b.dense_adj(g) for g in range(B)]),
+           b.feature_truth.reshape(B, n, -1), b.spatial_truth.reshape(B, n, -1))
+    p = {k: v * 5.0 for k, v in init_blocks(cfg, 3).items()}       # larger weights: non-trivial grads
+    eps = np.random.default_rng(2).standard_normal((B * S, cfg.latent))
+    losses, g = RS.sgjoint_forward_backward(p, *ins, eps, cfg)
+    rng = np.random.default_rng(0)
+
+    def cost(q):
+        t = {k: torch.tensor(v) for k, v in q.items()}
+        tt = lambda a: torch.tensor(np.asarray(a, np.float64))
+        c, _ = RS.sgjoint_loss_torch(t, tt(ins[0]), tt(ins[1]), tt(ins[2]), tt(ins[3]), tt(ins[4]),
+                                     tt(ins[5]), tt(eps), cfg)
+        return float(c)
+    for k in ("enc.sg0", "enc.sg1", "enc.Wh", "enc.Wms", "dec.Wp", "dec.K1"):
+        for _ in range(3):
+            idx = tuple(rng.integers(0, d) for d in p[k].shape)
+            h = 1e-6
+            qp = {kk: vv.copy() for kk, vv in p.items()}
+            qm = {kk: vv.copy() for kk, vv in p.items()}
+            qp[k][idx] += h
+            qm[k][idx] -= h
+            fd = (cost(qp) - cost(qm)) / (2 * h)
+            assert abs(fd - g[k][idx]) <= 1e-6 + 1e-5 * abs(fd), (k, idx, fd, g[k][idx])
+    assert np.isfinite(losses["cost"])
