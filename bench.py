@@ -403,6 +403,8 @@ def main():
                          "(the N>1 step, captured in the HIP graph) anyway")
     ap.add_argument("--spmm-copies", type=int, default=32,
                     help="secondary roofline: SpMM over this many copies of the batch (8 x 32 graphs)")
+    ap.add_argument("--batch-sweep", default="16,32",
+                    help="extra per-GPU batch sizes timed after the headline (1 GPU only)")
     ap.add_argument("--no-modes", action="store_true",
                     help="skip the fp32-mode and 1-graph (C3 per-rank) step timings")
     ap.add_argument("--extra", default="C4,C5",
@@ -494,6 +496,14 @@ def main():
                          "graphs_per_gpu": 1, "value": round(v1, 3), "unit": "graphs/s",
                          "ms_per_step": round(ms1, 4)}
         del_models()
+        # the same step at larger per-GPU batches (the headline stays at 8 graphs per GPU,
+        # C3's global batch per rank count): how far the machine is from filled at 8
+        out["batch_sweep"] = {}
+        for bs in [int(t) for t in args.batch_sweep.split(",") if t]:
+            vb, msb, *_ = run_workload(cfg, bs, args, info, steps=max(5, args.steps // 2),
+                                       warmup=min(args.warmup, 5))
+            out["batch_sweep"][str(bs)] = {"value": round(vb, 3), "unit": "graphs/s", "ms_per_step": round(msb, 4)}
+            del_models()
     extra = [w for w in args.extra.split(",") if w] if info.world == 1 else []
     if extra:
         out["workloads"] = {}
