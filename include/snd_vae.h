@@ -311,6 +311,26 @@ int snd_bn_relu_bwd(const float* dx, const float* y, long long rows, int c, cons
 int snd_e2e_head_ce(const float* y, const float* adj, int n_graphs, int n, int c, const float* gamma,
                     const float* beta, const float* w, const float* b, float* dy, float* dw, float* db,
                     float* dgamma, float* dbeta, double* out, snd_stream_t stream);
+/* Frozen Keras BN (y' = gamma y / sqrt(1.001) + beta, model.py:41) with an activation
+ * (ABI 12): act 0 identity, 1 relu, 2 lrelu(0.2) (layers.py:112-113); act_first = 1:
+ * x = BN(act(y)) (GraphConvolution then BN, model.py:107), 0: x = act(BN(y)) (the
+ * spatial encoder's relu after BN, model.py:123-124; identity for the disentangled
+ * decoders' conv + BN, model.py:190,214).  Strided rows (ld >= c).  The backward
+ * writes dy and, when non-NULL, the per-channel dgamma / dbeta (fixed-order sums). */
+int snd_bn_act_fwd(const float* y, int ldy, long long rows, int c, const float* gamma,
+                   const float* beta, int act, int act_first, float* x, int ldx, snd_stream_t stream);
+int snd_bn_act_bwd(const float* dx, int lddx, const float* y, int ldy, long long rows, int c,
+                   const float* gamma, const float* beta, int act, int act_first, float* dy, int lddy,
+                   float* dgamma, float* dbeta, snd_stream_t stream);
+/* Reparameterisation backward (model.py:155-159): dms = [dz + add_mu || dz eps e^s +
+ * add_logstd] over ms = [mu || logstd] rows (dz / add_* may be NULL: zero). */
+int snd_reparam_bwd(const float* ms, int ldms, int rows, int latent, const float* eps, const float* dz,
+                    const float* add_mu, const float* add_logstd, float* dms, int lddms,
+                    snd_stream_t stream);
+/* y[r, c] += alpha x[r, c] over a strided [rows, cols] block: gradients of one tensor
+ * reaching it along several branches (the disentangled decoders' concat inputs). */
+int snd_add_strided(long long rows, int cols, float alpha, const float* x, int ldx, float* y, int ldy,
+                    snd_stream_t stream);
 /* Latent regularisers of one latent group (optimizer.py:7-58,159-190), mu / logstd /
  * z [batch, latent] fp32:
  *   term = w_kl kl  (cap_gamma > 0: cap_gamma relu(kl - cap_c), 'disentangled_C')

@@ -1,0 +1,132 @@
+"""ORACLE -- test infrastructure only.  Never imported by the product path.
+
+The reference's disentangled SND-VAE (``SGCNModelVAE`` of `model.py:19-222` with
+`optimizer.py:123-203`) written out literally in float64 torch ops; autograd
+stands in for TF autodiff (`optimizer.py:197`).  Parity unpinned against TF
+itself (TensorFlow is unavailable); its pieces are pinned by
+ref_sg.py (the spatial-graph layer, finite differences), ref_disent.py (e2e,
+regularisers) and ref_torch.py, and the whole by finite differences
+(tests/test_disent_model_oracle.py).
+
+Graph encoder   model.py:104-115   g = BN_g_i(lrelu(A (g W_i))) || x_feat (x2), BN encoder_g,
+                                   linears g_g1_lin -> [g_g2_lin | g_g3_lin] on flat(g)
+Spatial encoder model.py:119-129   h = relu(BN_s_i(conv1d_k5_SAME(h))) (x3) from the coordinates,
+                                   BN encoder_s, g_s1_lin -> [g_s2_lin | g_s3_lin]
+SG encoder      model.py:134-151   s = lrelu(BN_sg_i(SGConv(trees, s, rel))) (x2) on the B*S
+                                   copies, BN encoder_sg, g_sg1_lin -> [g_sg2_lin | g_sg3_lin]
+get_z           model.py:153-161   z = mu + eps e^logstd per group
+decoder         model.py:172-222   J_sg = mean_s reshape(z_sg W + b), J_s, J_g (d_*_lin1);
+                                   node: BN_n_i(conv1d) (x2, no activation), BN decoder_node,
+                                   sigmoid(d_n_lin2); edges: e2e structure decoder on [J_sg | J_g];
+                                   spatial: BN_s_i(conv1d) (x3) on [J_sg | J_s], sigmoid(d_s_lin2)
+losses          optimizer.py:142-203 per model_type (ref_disent.model_type_groups)
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from oracle import ref_disent as RD
+from oracle import ref_sg as RS
+from oracle import ref_torch as T
+
+
+def disent_loss_torch(p, inp, eps, cfg):
+    """p: torch params by block name (snd_vae_amd/disent_model.py layout); inp: dict of torch
+    inputs (x [B,N,F], spatial [B,N,2], adj [B,N,N], x_sg [B*S,N,F], trees [B*S,N,N],
+    rel [B*S,N,N]); eps: {'s': [B,Ls], 'g': [B,Lg], 'sg': [B*S,Lsg]}.  Returns (cost,
+    overall_loss dict, groups)."""
+    import torch
+    bn = lambda t, k: T.bn(t, p[k + "/gamma"], p[k + "/beta"])
+    x, sp, adj = inp["x"], inp["spatial"], inp["adj"]
+    B, N, _ = x.shape
+    S = cfg.sampling_num
+    nh = cfg.node_h
+    # ---- graph encoder (model.py:104-115)
+    g = x
+    for i in range(len(cfg.g_conv_hidden)):
+        conv = T.lrelu(torch.matmul(adj, torch.matmul(g, p[f"g_g{i}_conv/w"])))   # layers.py:120-123
+        g = torch.cat([bn(conv, f"g_bn_g{i}"), x], -1)
+    g = bn(g, "encoder_g")
+    h = torch.reshape(g, [B, -1]) @ p["g_g1_lin/Matrix"] + p["g_g1_lin/bias"]
+    ms_g = h @ p["g_g23_lin/Matrix"] + p["g_g23_lin/bias"]
+    # ---- spatial encoder (model.py:119-129)
+    hs = sp
+    for i in range(len(cfg.s_channel)):
+        hs = torch.relu(bn(T.conv1d_same(hs, p[f"g_s{i + 1}_conv/kernel"], p[f"g_s{i + 1}_conv/bias"]),
+                           f"g_bn_s{i}"))
+    hs = bn(hs, "encoder_s")
+    h = torch.reshape(hs, [B, -1]) @ p["g_s1_lin/Matrix"] + p["g_s1_lin/bias"]
+    ms_s = h @ p["g_s23_lin/Matrix"] + p["g_s23_lin/bias"]
+    # ---- spatial-graph encoder (model.py:134-151)
+    s_g = inp["x_sg"]
+    F = s_g.shape[-1]
+    for i, hid in enumerate(cfg.sg_conv_hidden):
+        lp = RS.unpack_layer(p[f"g_sg{i}_conv"], F, hid)
+        s_g = T.lrelu(T.bn(RS.sgconv_torch(inp["trees"], s_g, inp["rel"], lp), lp["gamma"], lp["beta"]))
+        F = hid[2]
+    s_g = bn(s_g, "encoder_sg")
+    h = torch.reshape(s_g, [B * S, -1]) @ p["g_sg1_lin/Matrix"] + p["g_sg1_lin/bias"]
+    ms_sg = h @ p["g_sg23_lin/Matrix"] + p["g_sg23_lin/bias"]
+    groups = {}
+    for name, ms, lat in (("s", ms_s, cfg.s_latent), ("g", ms_g, cfg.g_latent), ("sg", ms_sg, cfg.sg_latent)):
+        mu, ls = ms[:, :lat], ms[:, lat:]
+        groups[name] = (mu, ls, mu + eps[name] * torch.exp(ls))          # model.py:155-159
+    # ---- decoder (model.py:172-222)
+    J_sg = torch.reshape(groups["sg"][2] @ p["d_sg_lin1/Matrix"] + p["d_sg_lin1/bias"], [B, S, N, nh]).mean(1)
+    J_s = torch.reshape(groups["s"][2] @ p["d_s_lin1/Matrix"] + p["d_s_lin1/bias"], [B, N, nh])
+    J_g = torch.reshape(groups["g"][2] @ p["d_g_lin1/Matrix"] + p["d_g_lin1/bias"], [B, N, nh])
+    z_sg_g = torch.cat([J_sg, J_g], -1)
+    u = z_sg_g
+    for i in range(len(cfg.n_d_channel)):
+        u = bn(T.conv1d_same(u, p[f"n{i}_deconv/kernel"], p[f"n{i}_deconv/bias"]), f"d_bn_n{i}")
+    xhat = torch.sigmoid(bn(u, "decoder_node") @ p["d_n_lin2/Matrix"] + p["d_n_lin2/bias"])
+    layers = [{"gamma": p[f"d_bn_e{i}/gamma"], "beta": p[f"d_bn_e{i}/beta"], "w": p[f"e{i}_deconv/w1"],
+               "b": p[f"e{i}_deconv/biases1"]} for i in range(len(cfg.e_d_hidden))]
+    head = {"gamma": p["decoder_adj/gamma"], "beta": p["decoder_adj/beta"], "w": p["d_e_lin2/Matrix"],
+            "b": p["d_e_lin2/bias"]}
+    adj_cost, correct = RD.structure_decoder_torch(z_sg_g, adj, layers, head)
+    v = torch.cat([J_sg, J_s], -1)
+    for i in range(len(cfg.s_d_channel)):
+        v = bn(T.conv1d_same(v, p[f"s{i + 1}_deconv/kernel"], p[f"s{i + 1}_deconv/bias"]), f"d_bn_s{i}")
+    shat = torch.sigmoid(v @ p["d_s_lin2/Matrix"] + p["d_s_lin2/bias"])
+    node_cost = ((inp["x"] - xhat) ** 2).mean()                           # optimizer.py:149
+    spatial_cost = ((sp - shat) ** 2).mean()                              # optimizer.py:153
+    # ---- regularisers and the cost (optimizer.py:159-203)
+    weights = RD.model_type_groups(cfg.model_type, cfg.beta, cfg.gamma, cfg.capacity)
+    reg, kls = 0.0, {}
+    for name, (mu, ls, z) in groups.items():
+        k = -0.5 * torch.mean(1 + 2 * ls - mu ** 2 - torch.exp(ls) ** 2)
+        kls[name] = k
+        if name not in weights:
+            continue
+        w = weights[name]
+        val = w.get("cap_gamma", 0.0) * torch.relu(k - w.get("cap_c", 0.0)) if w.get("cap_gamma", 0.0) > 0 \
+            else w.get("w_kl", 1.0) * k
+        if w.get("w_dip"):
+            m = mu.mean(0)
+            cov = (mu[:, None, :] * mu[:, :, None]).mean(0) - m[None, :] * m[:, None]
+            d = torch.diagonal(cov)
+            val = val + w["w_dip"] * (w.get("lambda_od", 10.0) * torch.sum((cov - torch.diag(d)) ** 2)
+                                      + w.get("lambda_d", 100.0) * torch.sum((d - 1) ** 2))
+        if w.get("w_tc"):
+            logvar = torch.log(torch.exp(ls) * torch.exp(ls))
+            tmp = z[:, None, :] - mu[None, :, :]
+            lqp = -0.5 * (tmp * tmp * torch.exp(-logvar[None]) + logvar[None] + RD.LOG_2PI)
+            val = val + w["w_tc"] * torch.mean(torch.logsumexp(lqp.sum(2), 1) - torch.logsumexp(lqp, 1).sum(1))
+        reg = reg + val
+    cost = adj_cost + node_cost + spatial_cost + reg
+    parts = {"cost": cost, "spatial_cost": spatial_cost, "adj_cost": adj_cost, "node_cost": node_cost,
+             "kl_g": kls["g"], "kl_s": kls["s"], "kl_sg": kls["sg"], "correct": correct}
+    return cost, parts, groups
+
+
+def disent_forward_backward(blocks, inputs, eps, cfg):
+    """(losses, grads by block) of one step, float64."""
+    import torch
+    p = {k: torch.tensor(np.asarray(v, np.float64), requires_grad=True) for k, v in blocks.items()}
+    t = {k: torch.tensor(np.asarray(v, np.float64)) for k, v in inputs.items()}
+    e = {k: torch.tensor(np.asarray(v, np.float64)) for k, v in eps.items()}
+    cost, parts, _ = disent_loss_torch(p, t, e, cfg)
+    cost.backward()
+    losses = {k: float(v.detach()) if hasattr(v, "detach") else float(v) for k, v in parts.items()}
+    return losses, {k: v.grad.numpy() for k, v in p.items()}

@@ -17,7 +17,7 @@ c_int, c_ll, c_float, c_size, c_ull = C.c_int, C.c_longlong, C.c_float, C.c_size
 vp = C.c_void_p
 
 
-ABI_VERSION = 11
+ABI_VERSION = 12
 GEN_MODES = {"sample": 0, "mean": 1, "prior": 2, "given": 3}
 TOPOLOGY = {"tscale": 0, "tref": 1, "sgjoint": 2}
 
@@ -117,6 +117,10 @@ _SIGS = {
     "snd_e2e_head_ce": (c_int, [vp, vp, c_int, c_int, c_int, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]),
     "snd_latent_reg_workspace": (c_size, [c_int, c_int]),
     "snd_latent_reg": (c_int, [vp, vp, vp, c_int, c_int, C.POINTER(LatentReg), vp, vp, vp, vp, vp]),
+    "snd_bn_act_fwd": (c_int, [vp, c_int, c_ll, c_int, vp, vp, c_int, c_int, vp, c_int, vp]),
+    "snd_bn_act_bwd": (c_int, [vp, c_int, vp, c_int, c_ll, c_int, vp, vp, c_int, c_int, vp, c_int, vp, vp, vp]),
+    "snd_reparam_bwd": (c_int, [vp, c_int, c_int, c_int, vp, vp, vp, vp, vp, c_int, vp]),
+    "snd_add_strided": (c_int, [c_ll, c_int, c_float, vp, c_int, vp, c_int, vp]),
     "snd_plan_create": (c_int, [C.POINTER(Config), c_int, C.POINTER(vp)]),
     "snd_plan_destroy": (None, [vp]),
     "snd_plan_param_count": (c_ll, [vp]),

@@ -560,3 +560,135 @@ extern "C" int snd_e2e_head_ce(const float* y, const float* adj, int n_graphs, i
   SND_LAUNCH_CHECK("e2e_head_kernel");
   return 0;
 }
+
+// ---- frozen Keras BN with an activation, either order (ABI 12) -----------------------
+namespace snd {
+namespace {
+__device__ __forceinline__ float act_f(float v, int act) {
+  return act == 1 ? fmaxf(v, 0.f) : (act == 2 ? fmaxf(v, kLeak * v) : v);
+}
+// d act / d v as TF routes it: relu' = 1 for v > 0; Maximum(v, 0.2 v)' = 1 for v >= 0
+__device__ __forceinline__ float act_d(float v, int act) {
+  return act == 1 ? (v > 0.f ? 1.f : 0.f) : (act == 2 ? (v >= 0.f ? 1.f : kLeak) : 1.f);
+}
+__global__ void __launch_bounds__(ET) bn_act_kernel(const float* y, int ldy, long long rows, int C,
+                                                    const float* g, const float* be, int act, int pre,
+                                                    float* x, int ldx) {
+  const long long idx = (long long)blockIdx.x * ET + threadIdx.x;
+  if (idx >= rows * C) return;
+  const int c = (int)(idx % C);
+  const long long r = idx / C;
+  const float v = y[r * ldy + c];
+  x[r * ldx + c] = pre ? g[c] * kBnC * act_f(v, act) + be[c] : act_f(g[c] * kBnC * v + be[c], act);
+}
+// one workgroup per channel, fixed-order tree: dy, dgamma = sum du c t, dbeta = sum du
+__global__ void __launch_bounds__(ET) bn_act_bwd_kernel(const float* dx, int lddx, const float* y, int ldy,
+                                                        long long rows, int C, const float* g, const float* be,
+                                                        int act, int pre, float* dy, int lddy, float* dg,
+                                                        float* db) {
+  __shared__ float r1[ET], r2[ET];
+  const int c = blockIdx.x;
+  const float gc = g[c] * kBnC;
+  float sg = 0.f, sb = 0.f;
+  for (long long r = threadIdx.x; r < rows; r += ET) {
+    const float v = y[r * ldy + c];
+    float du, t;
+    if (pre) {   // x = BN(act(y))
+      t = act_f(v, act);
+      du = dx[r * lddx + c];
+      dy[r * lddy + c] = du * gc * act_d(v, act);
+    } else {     // x = act(BN(y))
+      t = v;
+      du = dx[r * lddx + c] * act_d(gc * v + be[c], act);
+      dy[r * lddy + c] = du * gc;
+    }
+    sg = fmaf(du, kBnC * t, sg);
+    sb += du;
+  }
+  r1[threadIdx.x] = sg;
+  r2[threadIdx.x] = sb;
+  __syncthreads();
+  for (int h = ET / 2; h > 0; h >>= 1) {
+    if ((int)threadIdx.x < h) { r1[threadIdx.x] += r1[threadIdx.x + h]; r2[threadIdx.x] += r2[threadIdx.x + h]; }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    if (dg) dg[c] = r1[0];
+    if (db) db[c] = r2[0];
+  }
+}
+// z = mu + eps e^s backward: dmu = dz + add_mu, ds = dz eps e^s + add_s (model.py:155-159)
+__global__ void __launch_bounds__(ET) reparam_bwd_plain_kernel(const float* ms, int ldms, long long rows, int L,
+                                                               const float* eps, const float* dz,
+                                                               const float* add_mu, const float* add_s,
+                                                               float* dms, int lddms) {
+  const long long idx = (long long)blockIdx.x * ET + threadIdx.x;
+  if (idx >= rows * L) return;
+  const long long r = idx / L;
+  const int l = (int)(idx - r * L);
+  const float s = ms[r * ldms + L + l];
+  const float d = dz ? dz[idx] : 0.f;
+  dms[r * lddms + l] = d + (add_mu ? add_mu[idx] : 0.f);
+  dms[r * lddms + L + l] = d * eps[idx] * expf(s) + (add_s ? add_s[idx] : 0.f);
+}
+}  // namespace
+}  // namespace snd
+
+extern "C" int snd_bn_act_fwd(const float* y, int ldy, long long rows, int c, const float* gamma,
+                              const float* beta, int act, int act_first, float* x, int ldx, snd_stream_t stream) {
+  SND_CHECK_ARG(y && gamma && beta && x && rows >= 0 && c > 0 && ldy >= c && ldx >= c && act >= 0 && act <= 2,
+                "snd_bn_act_fwd: bad arguments");
+  if (rows == 0) return 0;
+  hipLaunchKernelGGL(bn_act_kernel, dim3((unsigned)((rows * c + ET - 1) / ET)), dim3(ET), 0, (hipStream_t)stream,
+                     y, ldy, rows, c, gamma, beta, act, act_first, x, ldx);
+  SND_LAUNCH_CHECK("bn_act_kernel");
+  return 0;
+}
+
+extern "C" int snd_bn_act_bwd(const float* dx, int lddx, const float* y, int ldy, long long rows, int c,
+                              const float* gamma, const float* beta, int act, int act_first, float* dy, int lddy,
+                              float* dgamma, float* dbeta, snd_stream_t stream) {
+  SND_CHECK_ARG(dx && y && gamma && beta && dy && rows >= 0 && c > 0 && lddx >= c && ldy >= c && lddy >= c &&
+                    act >= 0 && act <= 2,
+                "snd_bn_act_bwd: bad arguments");
+  hipLaunchKernelGGL(bn_act_bwd_kernel, dim3((unsigned)c), dim3(ET), 0, (hipStream_t)stream, dx, lddx, y, ldy, rows,
+                     c, gamma, beta, act, act_first, dy, lddy, dgamma, dbeta);
+  SND_LAUNCH_CHECK("bn_act_bwd_kernel");
+  return 0;
+}
+
+extern "C" int snd_reparam_bwd(const float* ms, int ldms, int rows, int latent, const float* eps, const float* dz,
+                               const float* add_mu, const float* add_logstd, float* dms, int lddms,
+                               snd_stream_t stream) {
+  SND_CHECK_ARG(ms && eps && dms && rows >= 0 && latent > 0 && ldms >= 2 * latent && lddms >= 2 * latent,
+                "snd_reparam_bwd: bad arguments");
+  const long long n = (long long)rows * latent;
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(reparam_bwd_plain_kernel, dim3((unsigned)((n + ET - 1) / ET)), dim3(ET), 0,
+                     (hipStream_t)stream, ms, ldms, (long long)rows, latent, eps, dz, add_mu, add_logstd, dms, lddms);
+  SND_LAUNCH_CHECK("reparam_bwd_plain_kernel");
+  return 0;
+}
+
+namespace snd {
+namespace {
+__global__ void __launch_bounds__(ET) add_strided_kernel(long long rows, int cols, float alpha, const float* x,
+                                                         int ldx, float* y, int ldy) {
+  const long long idx = (long long)blockIdx.x * ET + threadIdx.x;
+  if (idx >= rows * cols) return;
+  const long long r = idx / cols;
+  const int c = (int)(idx - r * cols);
+  y[r * ldy + c] += alpha * x[r * ldx + c];
+}
+}  // namespace
+}  // namespace snd
+
+extern "C" int snd_add_strided(long long rows, int cols, float alpha, const float* x, int ldx, float* y, int ldy,
+                               snd_stream_t stream) {
+  SND_CHECK_ARG(x && y && rows >= 0 && cols > 0 && ldx >= cols && ldy >= cols, "snd_add_strided: bad arguments");
+  if (rows == 0) return 0;
+  hipLaunchKernelGGL(add_strided_kernel, dim3((unsigned)((rows * cols + ET - 1) / ET)), dim3(ET), 0,
+                     (hipStream_t)stream, rows, cols, alpha, x, ldx, y, ldy);
+  SND_LAUNCH_CHECK("add_strided_kernel");
+  return 0;
+}
