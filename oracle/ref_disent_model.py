@@ -120,13 +120,15 @@ def disent_loss_torch(p, inp, eps, cfg):
     return cost, parts, groups
 
 
-def disent_forward_backward(blocks, inputs, eps, cfg):
-    """(losses, grads by block) of one step, float64."""
+def disent_forward_backward(blocks, inputs, eps, cfg, dtype=None):
+    """(losses, grads by block) of one step, float64 (dtype=torch.float32: the same graph
+    in fp32, whose distance from float64 measures a block's conditioning for tests)."""
     import torch
-    p = {k: torch.tensor(np.asarray(v, np.float64), requires_grad=True) for k, v in blocks.items()}
-    t = {k: torch.tensor(np.asarray(v, np.float64)) for k, v in inputs.items()}
-    e = {k: torch.tensor(np.asarray(v, np.float64)) for k, v in eps.items()}
+    dtype = dtype or torch.float64
+    p = {k: torch.tensor(np.asarray(v, np.float64), dtype=dtype, requires_grad=True) for k, v in blocks.items()}
+    t = {k: torch.tensor(np.asarray(v, np.float64), dtype=dtype) for k, v in inputs.items()}
+    e = {k: torch.tensor(np.asarray(v, np.float64), dtype=dtype) for k, v in eps.items()}
     cost, parts, _ = disent_loss_torch(p, t, e, cfg)
     cost.backward()
     losses = {k: float(v.detach()) if hasattr(v, "detach") else float(v) for k, v in parts.items()}
-    return losses, {k: v.grad.numpy() for k, v in p.items()}
+    return losses, {k: v.grad.double().numpy() for k, v in p.items()}
