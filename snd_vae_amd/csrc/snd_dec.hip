@@ -152,43 +152,52 @@ __device__ __forceinline__ __bf16* img_at(__bf16* img, int row, int kp, int n0) 
 template <int NBH, int KCS, class Pre, class Epi>
 __device__ __forceinline__ void conv_phase_t(const __bf16* xs, int kpx, const __bf16* ws, int kpw, int np,
                                              int n_out, Pre&& pre, Epi&& epi, int dbg) {
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, li = lane & 15, lg = lane >> 4;
+  // the wave index through readfirstlane: the row-block loop and the column-block choice
+  // are then scalar, and the MFMAs straight-line code (a per-lane view of w made every
+  // MFMA an exec-masked branch with its operand read right before it)
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int li = lane & 15, lg = lane >> 4;
   const int nrb = (n_out + 15) >> 4, nbc = np >> 4;
   const int ncg = (nbc + NBH - 1) / NBH, wpc = NW / ncg;
   const int cg = w % ncg, k0 = w / ncg;
   if (k0 >= wpc) return;
   const int nb0 = cg * NBH;
-  const int kcs = (dbg & 4) ? 0 : (KCS ? KCS : kpw >> 5);
+  const bool mm = !(dbg & 4);
+  const int kcs = KCS ? KCS : kpw >> 5;
   const int wsw = dswz(li, kpw);
+  // a column group's blocks past the image (np not a multiple of 16 NBH) repeat its last
+  // block: the MFMA runs unconditionally and the epilogue drops the columns >= np
+  int wb[NBH];
+#pragma unroll
+  for (int i = 0; i < NBH; ++i) wb[i] = 16 * min(nb0 + i, nbc - 1) * kpw;
   for (int rb = k0; rb < nrb; rb += wpc) {
     f32x4 yp[NBH];
     pre(16 * rb + li, nb0, yp);
     f32x4 acc[NBH];
 #pragma unroll
     for (int i = 0; i < NBH; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (mm) {
 #pragma unroll
-    for (int t = 0; t < 5; ++t) {
-      const int xrow = 16 * rb + li + t;
-      const __bf16* xrp = xs + xrow * kpx;
-      const int xsw = dswz(xrow, kpx);
-      const __bf16* wrp = ws + (t * np + li) * kpw;
-      auto chunk = [&](int ks) {
-        const int ch = 4 * ks + lg;
-        const bf16x8 bx = *reinterpret_cast<const bf16x8*>(xrp + ((ch ^ xsw) << 3));
+      for (int t = 0; t < 5; ++t) {
+        const int xrow = 16 * rb + li + t;
+        const __bf16* xrp = xs + xrow * kpx;
+        const int xsw = dswz(xrow, kpx);
+        const __bf16* wrp = ws + (t * np + li) * kpw;
+        auto chunk = [&](int ks) {
+          const int ch = 4 * ks + lg;
+          const bf16x8 bx = *reinterpret_cast<const bf16x8*>(xrp + ((ch ^ xsw) << 3));
 #pragma unroll
-        for (int i = 0; i < NBH; ++i) {
-          if (nb0 + i < nbc) {
-            const bf16x8 aw = *reinterpret_cast<const bf16x8*>(wrp + 16 * (nb0 + i) * kpw + ((ch ^ wsw) << 3));
+          for (int i = 0; i < NBH; ++i) {
+            const bf16x8 aw = *reinterpret_cast<const bf16x8*>(wrp + wb[i] + ((ch ^ wsw) << 3));
             acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aw, bx, acc[i], 0, 0, 0);
           }
-        }
-      };
-      if constexpr (KCS == 0) {
-        for (int ks = 0; ks < kcs; ++ks) chunk(ks);
-      } else {
+        };
+        if constexpr (KCS == 0) {
+          for (int ks = 0; ks < kcs; ++ks) chunk(ks);
+        } else {
 #pragma unroll
-        for (int ks = 0; ks < KCS; ++ks)
-          if (ks < kcs) chunk(ks);
+          for (int ks = 0; ks < KCS; ++ks) chunk(ks);
+        }
       }
     }
     epi(16 * rb + li, nb0, acc, yp);
@@ -304,6 +313,11 @@ __global__ void __launch_bounds__(DT) dec_fwd_kernel(DecChainFwdArgs a) {
   float* y2n = reinterpret_cast<float*>(smem + L.c);
   const int kpu2 = a.m2.phys() <= 32 ? 32 : (a.m2.phys() <= 64 ? 64 : 128);
   const int own = tl.rend - tl.r0;
+  // measurement only (debug bit 1 << 21): s_memrealtime at the phase boundaries, written by
+  // thread 0 over the tile's head partials at the end (results wrong); tools/dec_stamps.py
+  const bool stamp = a.dbg & (1 << 21);
+  unsigned long long ts[8] = {};
+  if (stamp) ts[0] = __builtin_amdgcn_s_memrealtime();
 
   // Zero what an MFMA reads against zero weights but nobody writes: the U1 image's
   // pad columns [k1.np, k2.kp) (conv2's last k-chunk; uninitialised LDS may hold NaN,
@@ -369,6 +383,7 @@ __global__ void __launch_bounds__(DT) dec_fwd_kernel(DecChainFwdArgs a) {
     }
   }
   wait_dma();
+  if (stamp) ts[1] = __builtin_amdgcn_s_memrealtime();
 
   auto nopre = [](int, int, auto&) {};
   // ---- conv1: window [r0 - 4, r0 + own + 4) -> U1 image (bf16), Y1 / U1 own rows to HBM
@@ -411,8 +426,10 @@ __global__ void __launch_bounds__(DT) dec_fwd_kernel(DecChainFwdArgs a) {
     }, a.dbg);
   }
   __syncthreads();
+  if (stamp) ts[2] = __builtin_amdgcn_s_memrealtime();
   stage_weights(a.k2, reinterpret_cast<char*>(wimg), a.dbg);
   wait_dma();
+  if (stamp) ts[3] = __builtin_amdgcn_s_memrealtime();
   // ---- conv2: window [r0 - 2, r0 + own + 2) -> U2 image; Y2 / U2 own rows; Y2n own rows in LDS
   {
     const int wr0 = tl.r0 - 2, n_out = own + 4, N = a.m2.phys();
@@ -459,8 +476,10 @@ __global__ void __launch_bounds__(DT) dec_fwd_kernel(DecChainFwdArgs a) {
     }, a.dbg);
   }
   __syncthreads();
+  if (stamp) ts[4] = __builtin_amdgcn_s_memrealtime();
   stage_weights(a.k3, reinterpret_cast<char*>(wimg), a.dbg);
   wait_dma();
+  if (stamp) ts[5] = __builtin_amdgcn_s_memrealtime();
   // ---- conv3 (s branch): own rows -> U3, Y3 (fp32, LDS; the spatial head's input)
   {
     const int n_out = own;
@@ -481,6 +500,7 @@ __global__ void __launch_bounds__(DT) dec_fwd_kernel(DecChainFwdArgs a) {
     }, a.dbg);
   }
   __syncthreads();
+  if (stamp) ts[6] = __builtin_amdgcn_s_memrealtime();
   // ---- heads: spatial (s3 -> sd) on threads 0..127, node (n2 -> nf) on 128..255; the
   // per-row partial quantities go to scratch over the (now idle) weight image
   const int t = blockIdx.x;
@@ -528,6 +548,14 @@ __global__ void __launch_bounds__(DT) dec_fwd_kernel(DecChainFwdArgs a) {
       (tid == 256 ? a.sse_s : a.sse_n)[t] = v;
     }
   }
+  if (stamp) {
+    __syncthreads();
+    if (tid == 0) {
+      ts[7] = __builtin_amdgcn_s_memrealtime();
+      unsigned* o = reinterpret_cast<unsigned*>(a.phs + (long long)t * NQS);
+      for (int k = 0; k < 8; ++k) o[k] = (unsigned)ts[k];
+    }
+  }
 }
 
 // ------------------------------------------------------------------ backward
@@ -560,6 +588,9 @@ __global__ void __launch_bounds__(DT) dec_bwd_kernel(DecChainBwdArgs a) {
   float* slots = reinterpret_cast<float*>(smem + L.cps);
   const int own = tl.rend - tl.r0;
   const int t = blockIdx.x;
+  const bool stamp = a.dbg & (1 << 21);   // measurement only, as dec_fwd_kernel (over pc1)
+  unsigned long long ts[8] = {};
+  if (stamp) ts[0] = __builtin_amdgcn_s_memrealtime();
 
   if (!(a.dbg & 32))
     for (int i = tid * 16; i < L.cps - L.d3; i += DT * 16)
@@ -591,6 +622,7 @@ __global__ void __launch_bounds__(DT) dec_bwd_kernel(DecChainBwdArgs a) {
     }
   }
   wait_dma();
+  if (stamp) ts[1] = __builtin_amdgcn_s_memrealtime();
   // ---- conv3^T: window [r0 - 4, r0 + own + 4): dU2s -> BN/lrelu backward -> dY2s
   {
     const int wr0 = tl.r0 - 4, n_out = own + 8, N = a.m2.a, kpo = a.k2t.kp;
@@ -646,8 +678,10 @@ __global__ void __launch_bounds__(DT) dec_bwd_kernel(DecChainBwdArgs a) {
     }
   }
   __syncthreads();
+  if (stamp) ts[2] = __builtin_amdgcn_s_memrealtime();
   stage_weights(a.k2t, reinterpret_cast<char*>(wimg), a.dbg);
   wait_dma();
+  if (stamp) ts[3] = __builtin_amdgcn_s_memrealtime();
   // ---- conv2^T: window [r0 - 2, r0 + own + 2): dU1 -> BN/lrelu backward -> dY1
   {
     const int wr0 = tl.r0 - 2, n_out = own + 4, W1 = a.m1.phys(), kpo = a.k1t.kp;
@@ -715,8 +749,10 @@ __global__ void __launch_bounds__(DT) dec_bwd_kernel(DecChainBwdArgs a) {
     }
   }
   __syncthreads();
+  if (stamp) ts[4] = __builtin_amdgcn_s_memrealtime();
   stage_weights(a.k1t, reinterpret_cast<char*>(wimg), a.dbg);
   wait_dma();
+  if (stamp) ts[5] = __builtin_amdgcn_s_memrealtime();
   // ---- conv1^T: own rows -> dJ (fp32)
   {
     const int n_out = own, N = a.dj;
@@ -732,6 +768,15 @@ __global__ void __launch_bounds__(DT) dec_bwd_kernel(DecChainBwdArgs a) {
             make_float4(acc[i][0], acc[i][1], acc[i][2], acc[i][3]);
       }
     }, a.dbg);
+  }
+  if (stamp) {
+    ts[6] = __builtin_amdgcn_s_memrealtime();
+    __syncthreads();
+    if (tid == 0) {
+      ts[7] = __builtin_amdgcn_s_memrealtime();
+      unsigned* o = reinterpret_cast<unsigned*>(a.pc1 + (long long)t * 3 * a.m1.phys());
+      for (int k = 0; k < 8; ++k) o[k] = (unsigned)ts[k];
+    }
   }
 }
 

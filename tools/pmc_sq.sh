@@ -2,8 +2,8 @@
 # SQ counters of one kernel launched alone (tools/prof_zzt.py --kernel $KERNEL), in
 # three rocprofv3 --pmc passes (<= 8 SQ + 2 GRBM counters each), then a JSON summary:
 #   KERNEL=zzt_dense TAG=v4 bash tools/pmc_sq.sh   -> gpurun_out/pmc_$TAG.json
-# (CMD overrides the launcher, e.g. CMD="python tools/ab_spmm_win.py --flags 0 --reps 2"
-#  KERNEL=spmm_win_kernel)
+# (CMD overrides the launcher, e.g. CMD="python tools/ab_fast.py --keys dec:fwd --reps 2"
+#  KERNEL=dec_fwd_kernel)
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 K=${KERNEL:-zzt_dense}; T=${TAG:-$K}
