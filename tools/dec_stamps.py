@@ -22,6 +22,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--graphs", type=int, default=8)
     ap.add_argument("--keys", default="dec:fwd,dec:bwd")
+    ap.add_argument("--flags", default="0", help="extra measurement-only debug bits, comma list (one run each)")
     args = ap.parse_args()
     import numpy as np
     import torch
@@ -39,9 +40,9 @@ def main():
     bc = db.c_struct()
     L = _lib.lib()
     nb = args.graphs * 4096 // 128
-    for key in args.keys.split(","):
+    for key, fl in [(k, int(f, 0)) for k in args.keys.split(",") for f in args.flags.split(",")]:
         buf, stride, names = KERNELS[key]
-        _lib.check(L.snd_debug_set(1 << 21))
+        _lib.check(L.snd_debug_set((1 << 21) | fl))
         for _ in range(5):
             _lib.check(L.snd_plan_launch(model.plan, bc, model.workspace.data_ptr(), key.encode(), _lib.stream_ptr()))
         torch.cuda.synchronize()
@@ -49,7 +50,7 @@ def main():
         raw = model.buffer(buf, torch.float32).view(torch.int32)[:nb * stride].cpu().numpy().astype(np.int64)
         st = (raw.reshape(nb, stride)[:, :len(names)] & 0xFFFFFFFF).astype(np.float64)
         rel = (st - st[:, 0].min()) * 0.01   # 100 MHz ticks -> us
-        print(f"== {key} ({nb} workgroups)")
+        print(f"== {key} flags {fl} ({nb} workgroups)")
         for k, n in enumerate(names):
             c = rel[:, k]
             print(f"  {n:18s} min {c.min():7.2f}  median {np.median(c):7.2f}  max {c.max():7.2f} us")

@@ -24,7 +24,7 @@ for s in $STAGES; do
     tests) step pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread ;;
     bench) step bench 600 python bench.py ;;
     prof)  step rocprof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run \
-             --output-format csv -- python bench.py --steps 20 --warmup 5 --no-cpu-baseline --extra "" ;;
+             --output-format csv -- python bench.py --steps 20 --warmup 5 --no-cpu-baseline --extra "" --batch-sweep "" --no-modes ;;
     pmc1)  step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc1 -o run \
              --output-format csv -- python bench.py --steps 5 --warmup 2 --no-cpu-baseline ;;
     pmc2)  step pmc_write 600 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc2 -o run \

@@ -23,7 +23,7 @@ def load(d):
         names[did] = r["Kernel_Name"]
     ids = sorted(by)
     # last step = dispatches after the second-to-last adam kernel
-    ad = [i for i in ids if "adam_kernel" in names[i]]
+    ad = [i for i in ids if "adam" in names[i]]
     lo = ad[-2] if len(ad) >= 2 else ids[0] - 1
     step = [i for i in ids if lo < i <= ad[-1]]
     return [(names[i], by[i]) for i in step]
