@@ -43,7 +43,8 @@ constexpr float kLog2e = 1.4426950408889634f;
 constexpr float kLn2 = 0.69314718055994531f;
 constexpr double kSoftplusM1 = 0.31326168751822286;  // CE of a diagonal pair: logsumexp(1,0) - 1
 
-__device__ __forceinline__ float lrelu(float x) { return x >= 0.f ? x : kLeak * x; }
+// max(x, 0.2 x) == (x >= 0 ? x : 0.2 x) for every x (both zeros keep their sign): 2 ops, not 3
+__device__ __forceinline__ float lrelu(float x) { return fmaxf(x, kLeak * x); }
 // TF Maximum gradient: routed to x where x >= 0.2x  =>  1 for x >= 0.
 __device__ __forceinline__ float lrelu_grad(float x) { return x >= 0.f ? 1.f : kLeak; }
 

@@ -299,7 +299,7 @@ __device__ __forceinline__ void head_tile(int hi, int orow, bool rv, long long g
 // ------------------------------------------------------------------ forward
 __global__ void __launch_bounds__(DT) dec_fwd_kernel(DecChainFwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  __shared__ float cp1[3][128], cp2[3][128], cp3[3][16];
+  __shared__ __attribute__((aligned(16))) float cp1[3][128], cp2[3][128], cp3[3][16];
   __shared__ float hp[2][64];   // head parameters (head_tile layout)
   const FwdLay L(a);
   const Tile tl = tile_of(blockIdx.x, a.npg);
@@ -388,7 +388,12 @@ __global__ void __launch_bounds__(DT) dec_fwd_kernel(DecChainFwdArgs a) {
   auto nopre = [](int, int, auto&) {};
   // ---- conv1: window [r0 - 4, r0 + own + 4) -> U1 image (bf16), Y1 / U1 own rows to HBM
   {
-    const int wr0 = tl.r0 - 4, n_out = own + 8, N = a.m1.phys(), kpo = a.k2.kp;
+    // Columns outside the split layout (the [s | n] gap, the pad to np) need no mask:
+    // their packed weights and column parameters are zero, so y = +0 and lrelu(BN(y)) = +0
+    // there, which is what the zero-filled Y1 / U1 pads and the image already hold; every
+    // column group is a whole float4 inside np = ld1.  Only rows outside the graph (TF
+    // SAME padding) are zeroed.
+    const int wr0 = tl.r0 - 4, n_out = own + 8, kpo = a.k2.kp, nbc = a.k1.np >> 4;
     conv_phase<2, 2>(jimg, a.k1.kp, wimg, a.k1.kp, a.k1.np, n_out, nopre,
                   [&](int orow, int nb0, f32x4 (&acc)[2], f32x4 (&)[2]) {
       if (orow >= n_out) return;
@@ -396,31 +401,22 @@ __global__ void __launch_bounds__(DT) dec_fwd_kernel(DecChainFwdArgs a) {
       const bool ing = gr >= tl.glo && gr < tl.ghi, mine = gr >= tl.r0 && gr < tl.rend;
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
+        if (nb0 + i >= nbc) continue;
         const int n0 = 16 * (nb0 + i) + 4 * lg;
-        if (n0 >= a.k1.np) continue;
-        float yv[4], o[4];
-        unsigned cm = 0u;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int n = n0 + e;
-          if (n < N && a.m1.valid(n)) cm |= 1u << e;
-          yv[e] = acc[i][e] + cp1[0][n];
-          o[e] = lrelu(yv[e] * cp1[1][n] + cp1[2][n]);
-        }
+        const f32x4 b = *reinterpret_cast<const f32x4*>(&cp1[0][n0]);
+        const f32x4 g = *reinterpret_cast<const f32x4*>(&cp1[1][n0]);
+        const f32x4 be = *reinterpret_cast<const f32x4*>(&cp1[2][n0]);
+        f32x4 yv;
         bf16x4 ub;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) ub[e] = (__bf16)((ing && (cm >> e & 1u)) ? o[e] : 0.f);
+        for (int e = 0; e < 4; ++e) {
+          yv[e] = acc[i][e] + b[e];
+          ub[e] = (__bf16)(ing ? lrelu(yv[e] * g[e] + be[e]) : 0.f);
+        }
         *reinterpret_cast<bf16x4*>(img_at(u1img, orow, kpo, n0)) = ub;
-        if (mine && cm && !(a.dbg & 8)) {
-          float* yp = a.y1 + (long long)gr * a.ldy1 + n0;
-          __bf16* up = a.u1 + (long long)gr * a.ldy1 + n0;
-          if (cm == 15u) {
-            *reinterpret_cast<float4*>(yp) = make_float4(yv[0], yv[1], yv[2], yv[3]);
-            *reinterpret_cast<bf16x4*>(up) = ub;
-          } else {
-#pragma unroll
-            for (int e = 0; e < 4; ++e) if (cm >> e & 1u) { yp[e] = yv[e]; up[e] = ub[e]; }
-          }
+        if (mine && !(a.dbg & 8)) {
+          *reinterpret_cast<f32x4*>(a.y1 + (long long)gr * a.ldy1 + n0) = yv;
+          *reinterpret_cast<bf16x4*>(a.u1 + (long long)gr * a.ldy1 + n0) = ub;
         }
       }
     }, a.dbg);
@@ -432,7 +428,9 @@ __global__ void __launch_bounds__(DT) dec_fwd_kernel(DecChainFwdArgs a) {
   if (stamp) ts[3] = __builtin_amdgcn_s_memrealtime();
   // ---- conv2: window [r0 - 2, r0 + own + 2) -> U2 image; Y2 / U2 own rows; Y2n own rows in LDS
   {
-    const int wr0 = tl.r0 - 2, n_out = own + 4, N = a.m2.phys();
+    // as conv1: no column masks (zero weights and parameters outside the layout)
+    const int wr0 = tl.r0 - 2, n_out = own + 4, nbc = a.k2.np >> 4;
+    const int nlo = a.m2.b ? a.m2.offb : 1 << 30, nhi = a.m2.offb + a.m2.b;
     conv_phase<2, 4>(u1img, a.k2.kp, wimg, a.k2.kp, a.k2.np, n_out, nopre,
                   [&](int orow, int nb0, f32x4 (&acc)[2], f32x4 (&)[2]) {
       if (orow >= n_out) return;
@@ -440,37 +438,24 @@ __global__ void __launch_bounds__(DT) dec_fwd_kernel(DecChainFwdArgs a) {
       const bool ing = gr >= tl.glo && gr < tl.ghi, mine = gr >= tl.r0 && gr < tl.rend;
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
+        if (nb0 + i >= nbc) continue;
         const int n0 = 16 * (nb0 + i) + 4 * lg;
-        if (n0 >= a.k2.np) continue;
-        float yv[4], o[4];
-        unsigned cm = 0u;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int n = n0 + e;
-          if (n < N && a.m2.valid(n)) cm |= 1u << e;
-          yv[e] = acc[i][e] + cp2[0][n];
-          o[e] = lrelu(yv[e] * cp2[1][n] + cp2[2][n]);
-        }
+        const f32x4 b = *reinterpret_cast<const f32x4*>(&cp2[0][n0]);
+        const f32x4 g = *reinterpret_cast<const f32x4*>(&cp2[1][n0]);
+        const f32x4 be = *reinterpret_cast<const f32x4*>(&cp2[2][n0]);
+        f32x4 yv;
         bf16x4 ub;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) ub[e] = (__bf16)((ing && (cm >> e & 1u)) ? o[e] : 0.f);
+        for (int e = 0; e < 4; ++e) {
+          yv[e] = acc[i][e] + b[e];
+          ub[e] = (__bf16)(ing ? lrelu(yv[e] * g[e] + be[e]) : 0.f);
+        }
         *reinterpret_cast<bf16x4*>(img_at(u2img, orow, kpu2, n0)) = ub;
-        if (mine && cm && !(a.dbg & 8)) {
-          float* yp = a.y2 + (long long)gr * a.ldy2 + n0;
-          __bf16* up = a.u2 + (long long)gr * a.ldy2 + n0;
-          if (cm == 15u) {
-            *reinterpret_cast<float4*>(yp) = make_float4(yv[0], yv[1], yv[2], yv[3]);
-            *reinterpret_cast<bf16x4*>(up) = ub;
-          } else {
-#pragma unroll
-            for (int e = 0; e < 4; ++e) if (cm >> e & 1u) { yp[e] = yv[e]; up[e] = ub[e]; }
-          }
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const int n = n0 + e;
-            if ((cm >> e & 1u) && n >= a.m2.offb && a.m2.b)
-              y2n[(gr - tl.r0) * L.ldY2n + (n - a.m2.offb)] = yv[e];
-          }
+        if (mine && !(a.dbg & 8)) {
+          *reinterpret_cast<f32x4*>(a.y2 + (long long)gr * a.ldy2 + n0) = yv;
+          *reinterpret_cast<bf16x4*>(a.u2 + (long long)gr * a.ldy2 + n0) = ub;
+          if (n0 >= nlo && n0 < nhi)   // the n branch's columns: whole float4 groups (b % 4 == 0)
+            *reinterpret_cast<f32x4*>(&y2n[(gr - tl.r0) * L.ldY2n + (n0 - a.m2.offb)]) = yv;
         }
       }
     }, a.dbg);
@@ -489,11 +474,10 @@ __global__ void __launch_bounds__(DT) dec_fwd_kernel(DecChainFwdArgs a) {
       const int n0 = 16 * nb0 + 4 * lg;
       float yv[4], o[4];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
+      for (int e = 0; e < 4; ++e) {   // columns >= s3: zero weights and parameters, y = o = +0
         const int n = n0 + e;
-        const bool cv = n < a.s3;
-        yv[e] = cv ? acc[0][e] + cp3[0][n] : 0.f;
-        o[e] = cv ? lrelu(yv[e] * cp3[1][n] + cp3[2][n]) : 0.f;
+        yv[e] = acc[0][e] + cp3[0][n];
+        o[e] = lrelu(yv[e] * cp3[1][n] + cp3[2][n]);
       }
       *reinterpret_cast<float4*>(u3 + orow * 16 + n0) = make_float4(o[0], o[1], o[2], o[3]);
       *reinterpret_cast<float4*>(y3 + orow * 16 + n0) = make_float4(yv[0], yv[1], yv[2], yv[3]);
@@ -577,7 +561,7 @@ __device__ __forceinline__ void colpart_flush(float (&q)[3][NBH][4], float* slot
 
 __global__ void __launch_bounds__(DT) dec_bwd_kernel(DecChainBwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  __shared__ float cpa[2][128], cpb[2][128];   // conv2-s BN (gamma c, beta), conv1 BN
+  __shared__ __attribute__((aligned(16))) float cpa[2][128], cpb[2][128];   // conv2-s BN (gamma c, beta), conv1 BN
   const BwdLay L(a);
   const Tile tl = tile_of(blockIdx.x, a.npg);
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, lg = lane >> 4;
@@ -645,14 +629,14 @@ __global__ void __launch_bounds__(DT) dec_bwd_kernel(DecChainBwdArgs a) {
       const int gr = wr0 + orow;
       const bool ing = gr >= tl.glo && gr < tl.ghi, mine = gr >= tl.r0 && gr < tl.rend;
       const int n0 = 16 * nb + 4 * lg;
+      // columns >= N: zero weights, gamma and beta, so dt = +0 there without a mask
+      const f32x4 ga = *reinterpret_cast<const f32x4*>(&cpa[0][n0]);
+      const f32x4 be = *reinterpret_cast<const f32x4*>(&cpa[1][n0]);
       float o[4];
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const int n = n0 + e;
-        const bool cv = n < N && ing;
-        const float ga = cpa[0][n], be = cpa[1][n];
-        const float dt = cv ? acc[0][e] * lrelu_grad(yp[0][e] * ga + be) : 0.f;
-        o[e] = dt * ga;
+        const float dt = ing ? acc[0][e] * lrelu_grad(yp[0][e] * ga[e] + be[e]) : 0.f;
+        o[e] = dt * ga[e];
         if (mine) { q[0][0][e] += dt * yp[0][e]; q[1][0][e] += dt; q[2][0][e] += o[e]; }
       }
       bf16x4 ob;
@@ -693,16 +677,10 @@ __global__ void __launch_bounds__(DT) dec_bwd_kernel(DecChainBwdArgs a) {
                     const int gr = wr0 + orow;
                     const bool ok = orow < n_out && gr >= tl.glo && gr < tl.ghi;
 #pragma unroll
-                    for (int i = 0; i < 2; ++i) {
+                    for (int i = 0; i < 2; ++i) {   // Y1's gap / pad columns hold +0 (np = ld1)
                       yp[i] = f32x4{0.f, 0.f, 0.f, 0.f};
                       const int n0 = 16 * (nb + i) + 4 * lg;
-                      if (ok && n0 < W1) {
-                        const float* p = a.y1 + (long long)gr * a.ldy1 + n0;
-                        if (n0 + 3 < W1) yp[i] = *reinterpret_cast<const f32x4*>(p);
-                        else
-#pragma unroll
-                          for (int e = 0; e < 4; ++e) if (n0 + e < W1) yp[i][e] = p[e];
-                      }
+                      if (ok && nb + i < nbc) yp[i] = *reinterpret_cast<const f32x4*>(a.y1 + (long long)gr * a.ldy1 + n0);
                     }
                   },
                   [&](int orow, int nb, f32x4 (&acc)[2], f32x4 (&yp)[2]) {
@@ -711,31 +689,23 @@ __global__ void __launch_bounds__(DT) dec_bwd_kernel(DecChainBwdArgs a) {
       const bool ing = gr >= tl.glo && gr < tl.ghi, mine = gr >= tl.r0 && gr < tl.rend;
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
+        if (nb + i >= nbc) continue;
         const int n0 = 16 * (nb + i) + 4 * lg;
-        if (n0 >= a.k2t.np) continue;
+        // the U1 layout's gap / pad columns: zero weights, gamma, beta and Y1, so dt = +0
+        const f32x4 ga = *reinterpret_cast<const f32x4*>(&cpb[0][n0]);
+        const f32x4 be = *reinterpret_cast<const f32x4*>(&cpb[1][n0]);
         float o[4];
-        unsigned cm = 0u;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          const int n = n0 + e;
-          const bool cv = n < W1 && a.m1.valid(n);
-          if (cv) cm |= 1u << e;
-          const float ga = cpb[0][n], be = cpb[1][n];
-          const float dt = (cv && ing) ? acc[i][e] * lrelu_grad(yp[i][e] * ga + be) : 0.f;
-          o[e] = dt * ga;
+          const float dt = ing ? acc[i][e] * lrelu_grad(yp[i][e] * ga[e] + be[e]) : 0.f;
+          o[e] = dt * ga[e];
           if (mine) { q[0][i][e] += dt * yp[i][e]; q[1][i][e] += dt; q[2][i][e] += o[e]; }
         }
         bf16x4 ob;
 #pragma unroll
         for (int e = 0; e < 4; ++e) ob[e] = (__bf16)o[e];
         *reinterpret_cast<bf16x4*>(img_at(d1, orow, kpo, n0)) = ob;
-        if (mine && cm && !(a.dbg & 8)) {
-          __bf16* dp = a.dy1 + (long long)gr * a.lddy1 + n0;
-          if (cm == 15u) *reinterpret_cast<bf16x4*>(dp) = ob;
-          else
-#pragma unroll
-            for (int e = 0; e < 4; ++e) if (cm >> e & 1u) dp[e] = ob[e];
-        }
+        if (mine && !(a.dbg & 8)) *reinterpret_cast<bf16x4*>(a.dy1 + (long long)gr * a.lddy1 + n0) = ob;
       }
     }, a.dbg);
     __syncthreads();   // slots: the conv3^T partials were consumed above
@@ -798,6 +768,9 @@ bool dec_fused_supported(int dj, const ColMap& m1, const ColMap& m2, int s3, int
   if (FwdLay(f).total > lim || BwdLay(b).total > lim) return false;
   // image kp: conv inputs must match the packed images
   if (k3.kp > 64 || k3t.np != 32 || k2t.np > 128 || k1t.np != ((dj + 15) / 16) * 16) return false;
+  // the epilogues move whole 16-column groups of Y1 / U1 / dY1 (Y2 / U2): every image
+  // column must lie inside the row's leading dimension (round_up(phys, 8))
+  if (k1.np > rup(m1.phys(), 8) || k2t.np > rup(m1.phys(), 8) || k2.np > rup(m2.phys(), 8)) return false;
   return 16 % ((k2t.np / 16 + 1) / 2) == 0 && 16 % (k3t.np / 16) == 0;
 }
 
