@@ -316,7 +316,7 @@ __global__ void __launch_bounds__(DT) dec_fwd_kernel(DecChainFwdArgs a) {
   // measurement only (debug bit 1 << 21): s_memrealtime at the phase boundaries, written by
   // thread 0 over the tile's head partials at the end (results wrong); tools/dec_stamps.py
   const bool stamp = a.dbg & (1 << 21);
-  unsigned long long ts[8] = {};
+  unsigned long long ts[9] = {};
   if (stamp) ts[0] = __builtin_amdgcn_s_memrealtime();
 
   // Zero what an MFMA reads against zero weights but nobody writes: the U1 image's
@@ -331,11 +331,11 @@ __global__ void __launch_bounds__(DT) dec_fwd_kernel(DecChainFwdArgs a) {
       *reinterpret_cast<uint4*>(smem + L.a + i) = make_uint4(~0u, ~0u, ~0u, ~0u);
     __syncthreads();
   }
-  if (!(a.dbg & 32)) {
+  if (!(a.dbg & 32)) {   // (kp - np) / 4 <= 4 groups of 4 columns per row: no division
     const int kpo = a.k2.kp, npc = (kpo - a.k1.np) >> 2, nr = in_rows(TR + 4);
-    for (int i = tid; i < nr * npc; i += DT) {
-      const int row = i / npc, n0 = a.k1.np + 4 * (i - row * npc);
-      *reinterpret_cast<bf16x4*>(img_at(u1img, row, kpo, n0)) = bf16x4{};
+    for (int i = tid; i < nr * 4; i += DT) {
+      const int row = i >> 2, q = i & 3;
+      if (q < npc) *reinterpret_cast<bf16x4*>(img_at(u1img, row, kpo, a.k1.np + 4 * q)) = bf16x4{};
     }
   }
   __syncthreads();
@@ -516,6 +516,7 @@ __global__ void __launch_bounds__(DT) dec_fwd_kernel(DecChainFwdArgs a) {
       }
     }
     __syncthreads();
+    if (stamp) ts[7] = __builtin_amdgcn_s_memrealtime();
     // tile partials: each quantity summed over the 128 rows in order
     if (tid < NQS + NQN) {
       const float* src = scr + tid * kScr;
@@ -535,9 +536,9 @@ __global__ void __launch_bounds__(DT) dec_fwd_kernel(DecChainFwdArgs a) {
   if (stamp) {
     __syncthreads();
     if (tid == 0) {
-      ts[7] = __builtin_amdgcn_s_memrealtime();
+      ts[8] = __builtin_amdgcn_s_memrealtime();
       unsigned* o = reinterpret_cast<unsigned*>(a.phs + (long long)t * NQS);
-      for (int k = 0; k < 8; ++k) o[k] = (unsigned)ts[k];
+      for (int k = 0; k < 9; ++k) o[k] = (unsigned)ts[k];
     }
   }
 }
@@ -766,6 +767,7 @@ bool dec_fused_supported(int dj, const ColMap& m1, const ColMap& m2, int s3, int
   b.k3t = k3t; b.k2t = k2t; b.k1t = k1t; b.m1 = m1; b.m2 = m2; b.s3 = s3; b.dj = dj;
   const int lim = kDynLds;
   if (FwdLay(f).total > lim || BwdLay(b).total > lim) return false;
+  if (k2.kp - k1.np > 16) return false;   // dec_fwd zeroes at most 4 pad groups of U1 per row
   // image kp: conv inputs must match the packed images
   if (k3.kp > 64 || k3t.np != 32 || k2t.np > 128 || k1t.np != ((dj + 15) / 16) * 16) return false;
   // the epilogues move whole 16-column groups of Y1 / U1 / dY1 (Y2 / U2): every image

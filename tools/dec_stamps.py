@@ -12,7 +12,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 KERNELS = {
     # key: (plan buffer, stride in 32-bit words per workgroup (dec:bwd: 3 x the 106-wide U1 layout), labels)
     "dec:fwd": ("PDHS", 52, ["start", "J+W1 staged", "conv1 done", "W2 staged", "conv2 done",
-                             "W3 staged", "conv3 done", "heads done"]),
+                             "W3 staged", "conv3 done", "head rows done", "partials done"]),
     "dec:bwd": ("PDC1", 3 * 106, ["start", "dY3+W3t staged", "conv3T done", "W2t staged", "conv2T done",
                                "W1t staged", "conv1T (wave 0)", "end"]),
 }
