@@ -928,7 +928,8 @@ __global__ void __launch_bounds__(NTH2) zzt_dense_bf16_v4(ZztArgs a) {
 
   // measurement only (MEAS builds, variant >> 8): phase-skip bits 1 epilogue,
   // 2 forward MFMAs, 4 backward MFMAs, 8 tile staging, 16 the tile loop, 64 the
-  // tile barrier (with 8); 32 s_memrealtime stamps over part[] (results wrong)
+  // tile barrier (with 8); 32 s_memrealtime stamps over part[] (results wrong);
+  // 128 (with 32) the tile loop's shader-clock cycles instead (tools/zzt_stamps.py)
   const int skip = MEAS ? __builtin_amdgcn_readfirstlane(a.variant >> 8) : 0;
   unsigned long long ts[4] = {0, 0, 0, 0};
   if (skip & 32) ts[0] = __builtin_amdgcn_s_memrealtime();
@@ -1022,7 +1023,8 @@ __global__ void __launch_bounds__(NTH2) zzt_dense_bf16_v4(ZztArgs a) {
     for (int p = 0; p < NT / DP; ++p) s += csred[p][tid];
     colsum[tid] = s;
   }
-  if (skip & 32) ts[1] = __builtin_amdgcn_s_memrealtime();
+  unsigned long long tcy[2] = {0, 0};   // shader-clock cycles (s_memtime) over the tile loop
+  if (skip & 32) { ts[1] = __builtin_amdgcn_s_memrealtime(); tcy[0] = __builtin_amdgcn_s_memtime(); }
 
   f32x16 cinit, acc[CB];
   // +0 (not -0.0 = -C4 at c = 0): a zero accumulator folds into the MFMA's inline
@@ -1174,7 +1176,7 @@ __global__ void __launch_bounds__(NTH2) zzt_dense_bf16_v4(ZztArgs a) {
     labs = 0.f;
   }
   if (late && tl1 > t0 && !(skip & 4)) bwd(lds + ((tl1 - 1 - t0) % 3) * BUF, sPrev);
-  if (skip & 32) ts[2] = __builtin_amdgcn_s_memrealtime();
+  if (skip & 32) { ts[2] = __builtin_amdgcn_s_memrealtime(); tcy[1] = __builtin_amdgcn_s_memtime(); }
 
   // ---- per-row corrections (row i_me; lanes r and r + 32 hold its two k halves)
   float xd = 0.f, xs = 0.f;
@@ -1258,6 +1260,9 @@ __global__ void __launch_bounds__(NTH2) zzt_dense_bf16_v4(ZztArgs a) {
       ts[3] = __builtin_amdgcn_s_memrealtime();
       unsigned* o = reinterpret_cast<unsigned*>(a.part + 2 * blockIdx.x);
       for (int k = 0; k < 4; ++k) o[k] = (unsigned)ts[k];
+      if (skip & 128) {   // tile loop: 100 MHz stamps and shader-clock cycles instead
+        o[0] = (unsigned)ts[1]; o[1] = (unsigned)ts[2]; o[2] = (unsigned)tcy[0]; o[3] = (unsigned)tcy[1];
+      }
     }
   }
 }

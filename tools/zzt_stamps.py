@@ -41,6 +41,16 @@ def main():
     for k, n in enumerate(names):
         c = rel[:, k]
         print(f"{n:16s} min {c.min():7.2f}  median {np.median(c):7.2f}  max {c.max():7.2f} us")
+    name = f"zzt_dense_v{(32 | 128 | args.skip) << 8}".encode()
+    for _ in range(3):
+        _lib.check(L.snd_plan_launch(model.plan, bc, model.workspace.data_ptr(), name, _lib.stream_ptr()))
+    torch.cuda.synchronize()
+    rc = model.buffer("PZZT", torch.float64).view(torch.int32)[:4 * nb].cpu().numpy().astype(np.int64)
+    rc = (rc & 0xFFFFFFFF).reshape(nb, 4)
+    us = ((rc[:, 1] - rc[:, 0]) % 2**32) * 0.01
+    cyc = ((rc[:, 3] - rc[:, 2]) % 2**32).astype(np.float64)
+    print(f"tile loop: median {np.median(cyc):.0f} shader cycles in {np.median(us):.2f} us "
+          f"-> clock {np.median(cyc / us) / 1e3:.3f} GHz")
     d = np.diff(rel, axis=1)
     for k in range(3):
         print(f"phase {names[k]:>16s} -> {names[k+1]:16s} median {np.median(d[:, k]):7.2f}  max {d[:, k].max():7.2f} us")
