@@ -160,7 +160,8 @@ def run_workload(cfg, B, args, info, steps=None, warmup=None, dtype=None, reset_
     host = synthetic_batch(cfg, B, seed=1000 + info.rank * B)
     db = DeviceBatch(host, tile_rows=0 if args.no_tiles else default_tile_rows(cfg.g_conv_hidden[1]))
     model = SGCNModelVAE(cfg, B, dtype=args.dtype if dtype is None else dtype)
-    opt = OptimizerVAE(model, process_group=info.group)
+    opt = OptimizerVAE(model, process_group=info.group,
+                       bucketed=False if getattr(args, "no_buckets", False) else None)
     if reset_state:
         state = [t.clone() for t in (model.params, opt.m, opt.v, opt.step_counter)]
     opt.step(db)          # first step (counts as warm-up): the ELBO of the initial weights
@@ -401,6 +402,9 @@ def main():
     ap.add_argument("--force-dist", action="store_true",
                     help="under torchrun with one rank: init RCCL and run the gradient all-reduce "
                          "(the N>1 step, captured in the HIP graph) anyway")
+    ap.add_argument("--no-buckets", action="store_true",
+                    help="data parallel: one all-reduce of the whole gradient + one Adam pass "
+                         "instead of the bucketed exchange (A/B)")
     ap.add_argument("--spmm-copies", type=int, default=32,
                     help="secondary roofline: SpMM over this many copies of the batch (8 x 32 graphs)")
     ap.add_argument("--batch-sweep", default="16,32",

@@ -444,6 +444,18 @@ size_t snd_plan_workspace_bytes(const snd_plan_t* plan);
 int snd_plan_fuse_adam(snd_plan_t* plan, float* m, float* v, float lr, float beta1,
                        float beta2, float eps);
 int snd_plan_block_fused(const snd_plan_t* plan, int idx);
+/* Bucketed data parallel (ABI 13).  Registers `event` (a hipEvent_t created by the
+ * caller) to be recorded on the step's stream right after the kernel that writes
+ * block idx's gradient complete, so the caller can start that bucket's collective on
+ * another stream while the backward pass goes on (DP of optimizer.py:125,197 with
+ * main.py:331's single update): the graph-latent d_sg_lin1 weight and
+ * bias complete after the projection backward, the graph-latent head weight after
+ * the head backward.  Returns k > 0, the block's completion point (blocks with the
+ * same k complete together and share one event; points are reached in increasing k),
+ * when it has one (the event is kept for every later snd_train_step; NULL unregisters
+ * it), 0 when the block's gradient is completed by the step's final reduction
+ * (nothing kept), <0 on a bad index. */
+int snd_plan_grad_event(snd_plan_t* plan, int idx, void* event);
 /* Data parallel (ABI 6): the device Philox normals of this plan's head rows start at
  * global head row `head_row_offset` (rank * n_graphs for SND_TREF, rank * n_graphs *
  * n_nodes for SND_TSCALE), so every rank of a sharded global batch draws exactly the

@@ -30,7 +30,9 @@ def _meta(model) -> dict:
 
 
 def save(path: str, model, optimizer=None) -> None:
-    """Write params (+ Adam m, v, global step when ``optimizer`` is given)."""
+    """Write params (+ Adam m, v, global step when ``optimizer`` is given).  With a
+    bucketed data-parallel optimizer whose large buckets keep sharded Adam moments,
+    call ``optimizer.sync_state()`` on every rank first (a collective)."""
     from safetensors.torch import save_file
     pc = model.param_count
     t = {"params": model.params[:pc].detach().cpu().contiguous()}

@@ -102,6 +102,16 @@ struct snd_plan {
   // fused TF1 Adam (snd_plan_fuse_adam): Adam state of the blocks updated inside the step
   float* fuse_m = nullptr; float* fuse_v = nullptr;
   float fuse_lr = 0.f, fuse_b1 = 0.f, fuse_b2 = 0.f, fuse_eps = 0.f;
+  // bucketed data parallel (snd_plan_grad_event): events recorded on the step stream
+  // right after the kernel that writes a block's gradient complete (graph latent:
+  // tref_proj_bwd -> dec.Wp, dec.bp; tref_head_bwd -> enc.Wh)
+  hipEvent_t ev_proj = nullptr, ev_head = nullptr;
+  int grad_point(const std::string& n) const {   // 1 proj, 2 head, 0 the final reduction
+    if (!tref) return 0;
+    if (n == "dec.Wp" || n == "dec.bp") return 1;
+    if (n == "enc.Wh" && !sg) return 2;
+    return 0;
+  }
   // Philox row offset of this plan's head rows (snd_plan_set_rng_offset): a data-parallel
   // rank draws the normals a single device would draw for its rows of the global batch
   unsigned long long rng_row0 = 0;
@@ -145,7 +155,7 @@ struct snd_plan {
 };
 
 extern "C" const char* snd_last_error(void) { return g_err; }
-extern "C" int snd_abi_version(void) { return 12; }
+extern "C" int snd_abi_version(void) { return 13; }
 
 extern "C" int snd_plan_create(const snd_config_t* cfg, int n_graphs, snd_plan_t** out) {
   SND_CHECK_ARG(cfg && out && n_graphs > 0, "snd_plan_create: bad args");
@@ -482,6 +492,13 @@ extern "C" int snd_plan_set_rng_offset(snd_plan_t* p, long long head_row_offset)
   return 0;
 }
 
+extern "C" int snd_plan_grad_event(snd_plan_t* p, int idx, void* event) {
+  SND_CHECK_ARG(p && idx >= 0 && idx < (int)p->blocks.size(), "snd_plan_grad_event: bad index");
+  const int pt = p->grad_point(p->blocks[idx].name);
+  if (pt == 1) p->ev_proj = (hipEvent_t)event;
+  if (pt == 2) p->ev_head = (hipEvent_t)event;
+  return pt;
+}
 extern "C" int snd_plan_block_fused(const snd_plan_t* p, int idx) {
   SND_CHECK_ARG(p && idx >= 0 && idx < (int)p->blocks.size(), "snd_plan_block_fused: bad index");
   return p->block_fused(p->blocks[idx].name) ? 1 : 0;
@@ -1543,6 +1560,10 @@ extern "C" int snd_train_step(const snd_plan_t* plan, const snd_batch_t* batch,
                           x.f("EJ"), adj_scale, x.g("dec.Wp"), x.g("dec.bp"), x.f("PDZ")};
         if (p.block_fused("dec.Wp")) a.adam = fused_adam(x, "dec.Wp", step_counter);
         SND_TRY(launch_tref_proj_bwd(a, x.s));
+        if (p.ev_proj && hipEventRecord(p.ev_proj, x.s) != hipSuccess) {
+          set_error("train step: grad event (dec.Wp) record failed");
+          return SND_ERR_HIP;
+        }
         const int rz = p.B;   // rows of the projection's input: B graphs
         const ReduceDesc rd{x.f("PDZ"), x.f(p.sg ? "DZBAR" : "DZL"), tref_proj_bwd_blocks(CP), rz * L,
                             (long long)rz * L, 1.f, 0, 0, 0, 0};
@@ -1571,6 +1592,10 @@ extern "C" int snd_train_step(const snd_plan_t* plan, const snd_batch_t* batch,
       }
       if (p.block_fused("enc.Wh")) a.adam = fused_adam(x, "enc.Wh", step_counter);
       SND_TRY(launch_tref_head_bwd(a, x.s));
+      if (p.ev_head && hipEventRecord(p.ev_head, x.s) != hipSuccess) {
+        set_error("train step: grad event (enc.Wh) record failed");
+        return SND_ERR_HIP;
+      }
     } else {
       SND_TRY(gemm_wgrad(x, x.f("G"), W, W, true, x.f("DH"), gh, gh, x.f("SWH"), p.sWh));
       SND_TRY(gemm_fwd(x, R, W, gh, x.f("DH"), gh, x.w("enc.Wh"), gh, B_COL, x.f("DG"), W, nullptr));

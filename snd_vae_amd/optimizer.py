@@ -6,7 +6,10 @@ Mirror of `optimizer.py:123-203` (``OptimizerVAE``, model_type 'base'):
 one iteration of the reference train loop (`main.py:315-334`):
 
     snd_train_step   forward + backward, flat gradient, loss terms
-    all-reduce       (data parallel only) one RCCL call on the flat gradient
+    exchange         (data parallel only) RCCL over the gradient buckets
+                     (parallel.plan_buckets): early buckets overlap the backward
+                     pass on a communication stream, large ones are
+                     reduce-scattered, updated as shards and all-gathered
     snd_adam_tf1     tf.train.AdamOptimizer(lr).minimize (`optimizer.py:125,197`)
 
 All three are stream-ordered device work, so a step can be captured in a
@@ -31,7 +34,8 @@ class OptimizerVAE:
     def __init__(self, model: SGCNModelVAE, learning_rate: Optional[float] = None,
                  beta1: Optional[float] = None, beta2: Optional[float] = None,
                  epsilon: Optional[float] = None, process_group=None, seed: int = 1234,
-                 fuse_adam: Optional[bool] = None):
+                 fuse_adam: Optional[bool] = None, bucketed: Optional[bool] = None,
+                 shard_min: Optional[int] = None):
         """fuse_adam (default: on without a process group): blocks whose gradient one
         kernel produces complete (graph-latent heads / d_sg_lin1) take their Adam
         update inside the step (snd_plan_fuse_adam); their gradient is then not written.
@@ -41,7 +45,13 @@ class OptimizerVAE:
         forced world of 1 executes exactly the N > 1 code path.  The device Philox
         stream is offset to this rank's rows of the global batch
         (snd_plan_set_rng_offset), so the ranks draw the normals one device would
-        draw for the whole batch."""
+        draw for the whole batch.
+
+        bucketed (default: on with a process group): the exchange of
+        parallel.run_buckets instead of one all-reduce of the whole gradient; a model
+        without early completion points or large blocks (C2) has one bucket, i.e. the
+        same single all-reduce.  shard_min: floats from which a bucket is sharded
+        (parallel.SHARD_MIN)."""
         cfg = model.cfg
         self.model = model
         self.lr = cfg.learning_rate if learning_rate is None else learning_rate
@@ -90,6 +100,44 @@ class OptimizerVAE:
                 self._adam_ranges[-1][1] += end - off
             else:
                 self._adam_ranges.append([off, end - off])
+        self.bucketed = self.distributed and (bucketed is None or bool(bucketed))
+        self.buckets = []
+        if self.bucketed:
+            self._init_buckets(shard_min)
+
+    def _init_buckets(self, shard_min):
+        """Bucket plan, completion events and chunk buffers of the bucketed exchange."""
+        from .parallel import SHARD_MIN, plan_buckets
+        m, L = self.model, _lib.lib()
+        lay = m.layout
+        names = list(lay.shapes)
+        blocks, points = [], []
+        for i, k in enumerate(names):
+            off = lay.offsets[k]
+            end = lay.offsets[names[i + 1]] if i + 1 < len(names) else m.param_count
+            blocks.append((off, end - off))
+            pt = int(L.snd_plan_grad_event(m.plan, i, None))
+            if pt < 0:
+                _lib.check(pt, "snd_plan_grad_event")
+            points.append(pt)
+        total = m.param_count + 8       # + the loss terms the step writes (TAIL layout)
+        self.buckets = plan_buckets(blocks, points, m.param_count, total, self.world,
+                                    SHARD_MIN if shard_min is None else shard_min)
+        # one event per early point, recorded by snd_train_step after the kernel that
+        # completes it (created now: torch creates events lazily on their first record)
+        self._events = {}
+        for i, pt in enumerate(points):
+            if pt and any(b.point == pt for b in self.buckets):
+                if pt not in self._events:
+                    ev = torch.cuda.Event()
+                    ev.record()
+                    self._events[pt] = ev
+                if L.snd_plan_grad_event(m.plan, i, C.c_void_p(self._events[pt].cuda_event)) != pt:
+                    raise _lib.SNDError(f"snd_plan_grad_event: block {k}: {_lib.last_error()}")
+        self._shard_grads = [torch.empty((b.hi - b.lo) // self.world if b.sharded else 0,
+                                         dtype=torch.float32, device=m.device) for b in self.buckets]
+        self._comm = torch.cuda.Stream(device=m.device) if self._events else None
+        self.step_next = torch.zeros(1, dtype=torch.int32, device=m.device)
 
     # ------------------------------------------------------------------ step
     def forward_backward(self, batch: DeviceBatch, eps: Optional[torch.Tensor] = None,
@@ -107,21 +155,76 @@ class OptimizerVAE:
             import torch.distributed as dist
             dist.all_reduce(self.grads[:self.model.param_count + 8], group=self.group)
 
+    def _adam(self, off: int, n: int, grad: torch.Tensor, stream=None, step=None):
+        """snd_adam_tf1 on params/m/v[off:off+n] with the gradient at `grad`; `step`:
+        the device global step it reads (default the step counter)."""
+        m, b = self.model, 4 * off
+        _lib.check(_lib.lib().snd_adam_tf1(
+            _lib.ptr(m.params) + b, _lib.ptr(grad), _lib.ptr(self.m) + b, _lib.ptr(self.v) + b,
+            n, self.lr, self.beta1, self.beta2, self.eps, 1.0 / self.world,
+            _lib.ptr(self.step_counter if step is None else step), _lib.stream_ptr(stream)),
+            "snd_adam_tf1")
+
     def apply(self, stream=None):
-        m = self.model
         for off, n in self._adam_ranges:
-            b = 4 * off
-            _lib.check(_lib.lib().snd_adam_tf1(
-                _lib.ptr(m.params) + b, _lib.ptr(self.grads) + b, _lib.ptr(self.m) + b,
-                _lib.ptr(self.v) + b, n, self.lr, self.beta1, self.beta2, self.eps,
-                1.0 / self.world, _lib.ptr(self.step_counter), _lib.stream_ptr(stream)),
-                "snd_adam_tf1")
+            self._adam(off, n, self.grads[off:off + n], stream)
+
+    def exchange_apply(self):
+        """The bucketed exchange + update (parallel.run_buckets) after forward_backward:
+        early buckets on the communication stream, ordered after their completion
+        events, the rest after the step; the step's stream then waits for all of it."""
+        import torch.distributed as dist
+
+        from .parallel import run_buckets
+        g = self.group
+        main = torch.cuda.current_stream()
+        comm = self._comm if self._comm is not None else main
+
+        def wait(b):
+            if comm is main:
+                return
+            if b.point:
+                self._events[b.point].wait(comm)
+            else:
+                comm.wait_stream(main)
+
+        with torch.cuda.stream(comm):
+            # an early bucket's update may run before the step's final reduction
+            # increments the global step: it reads step_next (set before the step)
+            run_buckets(self.buckets, self.grads, self.model.params, self.model.param_count,
+                        self.world, self.rank,
+                        lambda off, n, gr, b: self._adam(off, n, gr, step=self.step_next if b.point else None),
+                        self._shard_grads,
+                        lambda out, inp: dist.reduce_scatter_tensor(out, inp, group=g),
+                        lambda out, inp: dist.all_gather_into_tensor(out, inp, group=g),
+                        lambda t: dist.all_reduce(t, group=g), wait)
+        if comm is not main:
+            main.wait_stream(comm)
 
     def step(self, batch: DeviceBatch, eps: Optional[torch.Tensor] = None):
-        """One optimisation step (`main.py:331`): fwd+bwd, all-reduce, Adam."""
+        """One optimisation step (`main.py:331`): fwd+bwd, gradient exchange, Adam."""
+        if self.bucketed:
+            if self._events:   # the global step the early buckets' Adam updates use
+                torch.add(self.step_counter, 1, out=self.step_next)
+            self.forward_backward(batch, eps)
+            self.exchange_apply()
+            return
         self.forward_backward(batch, eps)
         self.allreduce()
         self.apply()
+
+    def sync_state(self):
+        """All-gather the Adam moments of the sharded buckets (each rank keeps only its
+        chunk current) so that m and v are complete on every rank, e.g. before a
+        checkpoint.  No-op without sharded buckets."""
+        if not self.bucketed:
+            return
+        import torch.distributed as dist
+        for b in self.buckets:
+            if b.sharded:
+                lo, c = b.shard(self.world, self.rank)
+                for t in (self.m, self.v):
+                    dist.all_gather_into_tensor(t[b.lo:b.hi], t[lo:lo + c].clone(), group=self.group)
 
     # ------------------------------------------------------------ HIP graph
     def _state(self):
@@ -184,6 +287,7 @@ class OptimizerVAE:
         return m.layout.unpack(self.grads[:m.param_count].double().cpu().numpy())
 
     def state_blocks(self):
+        self.sync_state()
         m = self.model
         pc = m.param_count
         return (m.layout.unpack(self.m[:pc].double().cpu().numpy()),

@@ -1,13 +1,19 @@
-"""Data parallelism over graphs: one process per GPU, one all-reduce per step.
+"""Data parallelism over graphs: one process per GPU, bucketed gradient exchange.
 
 The reference is single-device (`main.py:34` pins CUDA_VISIBLE_DEVICES=1;
 there is no collective anywhere).  SURVEY.md §8e: graphs are independent, so
 the batch is sharded contiguously over ranks; every loss term is a mean over
 equal-size per-graph sets, hence the global gradient is the mean of the rank
-gradients.  The exchange is ONE all-reduce(sum) of the flat fp32 gradient
-buffer with the loss terms appended; the 1/world scale is folded into the
-Adam kernel.  Frozen-stat BN needs no cross-rank sync.  Backend "nccl" is
-RCCL over xGMI on MI355X; "gloo" serves the CPU tests.
+gradients.  The exchange is a sum over ranks of the flat fp32 gradient buffer
+with the loss terms appended; the 1/world scale is folded into the Adam kernel.
+It runs in buckets (plan_buckets / run_buckets): a block whose gradient one
+kernel completes early in the backward pass (the graph-latent head and
+d_sg_lin1 weights, 216 MB at C4) starts its exchange on a communication stream
+while the backward pass goes on, and large buckets are reduce-scattered, updated
+as per-rank shards (1/world of the Adam traffic) and all-gathered; the rest (all
+of C2's ~245 KB) is ONE all-reduce at the end of the step.  Frozen-stat BN needs
+no cross-rank sync.  Backend "nccl" is RCCL over xGMI on MI355X; "gloo"
+serves the CPU tests.
 """
 from __future__ import annotations
 
@@ -43,6 +49,92 @@ def init_from_env(backend: str = "nccl", force: bool = False) -> DistInfo:
         dist.init_process_group(backend=backend, rank=rank, world_size=world,
                                 device_id=torch.device("cuda", local) if backend == "nccl" else None)
     return DistInfo(rank, world, local, dist.group.WORLD)
+
+
+# buckets at least this many floats are reduce-scattered and updated as per-rank
+# shards (ZeRO-1); smaller ones are all-reduced and updated on every rank
+SHARD_MIN = 1 << 20
+
+
+@dataclass
+class Bucket:
+    """A contiguous range [lo, hi) of the flat gradient / parameter buffer whose
+    gradient is complete at one point of the step: `point` 0 = after the step's final
+    reduction, k > 0 = the plan's k-th early point (snd_plan_grad_event)."""
+    lo: int
+    hi: int
+    point: int
+    sharded: bool
+
+    def shard(self, world: int, rank: int):
+        """[lo, lo + c) of this rank's chunk of a sharded bucket."""
+        c = (self.hi - self.lo) // world
+        return self.lo + rank * c, c
+
+
+def plan_buckets(blocks, points, param_count: int, total: int, world: int,
+                 shard_min: int = SHARD_MIN):
+    """Buckets of the flat buffer [0, total) (parameters, then the loss tail).
+
+    blocks: [(offset, padded_length)] in layout order (contiguous, lengths % 64 == 0);
+    points[i]: completion point of block i.  A bucket is a maximal run of consecutive
+    blocks with one point; a run of at least `shard_min` floats whose length splits
+    into world 16-byte-aligned chunks is sharded.  The loss tail [param_count, total)
+    joins the last run when that run is all-reduced, else it is a bucket of its own
+    (every rank reads the summed loss terms).  Issue order: the early points in the
+    order the step reaches them, then the end of the step."""
+    runs = []
+    for (off, n), pt in zip(blocks, points):
+        if runs and runs[-1][2] == pt and runs[-1][1] == off:
+            runs[-1][1] = off + n
+        else:
+            runs.append([off, off + n, pt])
+    if not runs or runs[-1][1] != param_count:
+        raise ValueError("plan_buckets: blocks do not tile [0, param_count)")
+    out = []
+    for lo, hi, pt in runs:
+        n = hi - lo
+        sharded = n >= shard_min and n % (4 * world) == 0
+        out.append(Bucket(lo, hi, pt, sharded))
+    last = out[-1]
+    if total > param_count:
+        if last.point == 0 and not last.sharded:
+            last.hi = total
+        else:
+            out.append(Bucket(param_count, total, 0, False))
+    out.sort(key=lambda b: (b.point == 0, b.point, b.lo))
+    return out
+
+
+def run_buckets(buckets, grads, params, param_count: int, world: int, rank: int, adam,
+                shard_grads, reduce_scatter, all_gather, all_reduce, wait=None):
+    """The data-parallel exchange + update of one step over `buckets`:
+
+      sharded bucket:  reduce-scatter(sum) its gradient -> this rank's chunk,
+                       adam(lo, n, chunk gradient) on the chunk's parameters,
+                       all-gather the updated chunks (in place) into every rank;
+      other bucket:    all-reduce(sum) its gradient, adam over its parameters.
+
+    adam(lo, n, g, bucket) updates params/m/v[lo:lo+n] with gradient g (1/world folded
+    in by the caller); shard_grads[i]: the chunk buffer of bucket i; wait(bucket) orders
+    the bucket after its gradient is complete (the GPU path: a stream wait on the
+    bucket's event).  The collectives are parameters so the same schedule runs on
+    RCCL (product) and gloo (CPU tests)."""
+    for i, b in enumerate(buckets):
+        if wait is not None:
+            wait(b)
+        if b.sharded:
+            lo, c = b.shard(world, rank)
+            reduce_scatter(shard_grads[i], grads[b.lo:b.hi])
+            n = max(0, min(lo + c, param_count) - lo)
+            if n:
+                adam(lo, n, shard_grads[i][:n], b)
+            all_gather(params[b.lo:b.hi], params[lo:lo + c])
+        else:
+            all_reduce(grads[b.lo:b.hi])
+            n = max(0, min(b.hi, param_count) - b.lo)
+            if n:
+                adam(b.lo, n, grads[b.lo:b.lo + n], b)
 
 
 def allreduce_mean_(flat: torch.Tensor, info: DistInfo) -> torch.Tensor:

@@ -142,9 +142,11 @@ class Trainer:
         for _ in range(epochs):
             e = self.epoch
             out.append(self.train_epoch(verbose))
-            if checkpoint_dir and e % save_every == 0 and self.rank == 0:
-                os.makedirs(checkpoint_dir, exist_ok=True)
-                self.save(os.path.join(checkpoint_dir, f"model_dgt_global_{e}.safetensors"))
+            if checkpoint_dir and e % save_every == 0:
+                self.opt.sync_state()   # collective: sharded Adam moments onto every rank
+                if self.rank == 0:
+                    os.makedirs(checkpoint_dir, exist_ok=True)
+                    self.save(os.path.join(checkpoint_dir, f"model_dgt_global_{e}.safetensors"))
         return out
 
     def save(self, path: str):

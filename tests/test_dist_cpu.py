@@ -144,3 +144,102 @@ def test_force_dist_init(world):
         assert w == world and has_group
         assert t == 1.5 + (world - 1)
         assert flat == [world * (world + 1) / 2] * 4
+
+
+# ---------------------------------------------------------------- bucketed exchange
+def _adam_tf1(p, m, v, g, t, lr=1e-3, b1=0.9, b2=0.999, eps=1e-8, scale=1.0):
+    """TF1 Adam in float32 torch ops, the snd_adam_tf1 formula (optimizer.py:125,197)."""
+    lrt = lr * np.sqrt(1.0 - b2 ** t) / (1.0 - b1 ** t)
+    gc = g * scale
+    m.mul_(b1).add_((1.0 - b1) * gc)
+    v.mul_(b2).add_((1.0 - b2) * gc * gc)
+    p.sub_(np.float32(lrt) * m / (v.sqrt() + eps))
+
+
+def _bucket_case(world):
+    """A flat layout with a d_sg_lin1-like early pair (point 1), a head-like early
+    block (point 2) and small end-of-step blocks between them, plus the loss tail."""
+    from snd_vae_amd.parallel import plan_buckets
+    lens = [64, 128, 4096, 64, 192, 2048, 64, 128]
+    pts = [0, 0, 2, 0, 0, 1, 1, 0]
+    offs = np.cumsum([0] + lens[:-1]).tolist()
+    P = sum(lens)
+    return P, plan_buckets(list(zip(offs, lens)), pts, P, P + 8, world, shard_min=1024)
+
+
+def _bucket_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    from snd_vae_amd.parallel import init_from_env, run_buckets
+    info = init_from_env("gloo")
+    P, buckets = _bucket_case(world)
+    gen = torch.Generator().manual_seed(7)
+    params = torch.randn(P + 8, generator=gen)            # the same initial state on every rank
+    m = torch.randn(P + 8, generator=gen).abs() * 1e-3
+    v = torch.randn(P + 8, generator=gen).abs() * 1e-6
+    grads = torch.randn(P + 8, generator=torch.Generator().manual_seed(100 + rank))
+    g0 = grads.clone()
+    shard_grads = [torch.empty((b.hi - b.lo) // world if b.sharded else 0) for b in buckets]
+    order = []
+
+    def adam(off, n, g, b):
+        _adam_tf1(params[off:off + n], m[off:off + n], v[off:off + n], g, t=3, scale=1.0 / world)
+
+    run_buckets(buckets, grads, params, P, world, rank, adam, shard_grads,
+                lambda out, inp: dist.reduce_scatter_tensor(out, inp, group=info.group),
+                lambda out, inp: dist.all_gather_into_tensor(out, inp, group=info.group),
+                lambda t: dist.all_reduce(t, group=info.group), wait=lambda b: order.append(b.point))
+    # the sharded buckets' moments are current on the owner's chunk only: gather them
+    for b in buckets:
+        if b.sharded:
+            lo, c = b.shard(world, rank)
+            for t in (m, v):
+                dist.all_gather_into_tensor(t[b.lo:b.hi], t[lo:lo + c].clone(), group=info.group)
+    q.put((rank, g0.numpy(), params[:P].numpy(), m[:P].numpy(), v[:P].numpy(),
+           grads[P:].numpy(), order))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_bucket_plan_shapes():
+    """Early points first (in the order the step reaches them), runs of one point
+    merged, large runs sharded, the loss tail on an all-reduced bucket."""
+    P, bk = _bucket_case(2)
+    got = [(b.lo, b.hi, b.point, b.sharded) for b in bk]
+    assert got == [(4544, 6656, 1, True), (192, 4288, 2, True), (0, 192, 0, False),
+                   (4288, 4544, 0, False), (6656, P + 8, 0, False)]
+    # a model without early points or large blocks (C2): one all-reduce of everything
+    from snd_vae_amd.parallel import plan_buckets
+    one = plan_buckets([(0, 64), (64, 128)], [0, 0], 192, 200, 8)
+    assert [(b.lo, b.hi, b.point, b.sharded) for b in one] == [(0, 200, 0, False)]
+
+
+@pytest.mark.parametrize("world", [2])
+def test_bucketed_exchange_equals_allreduce_adam(world):
+    """parallel.run_buckets (reduce-scatter + per-rank shard Adam + all-gather for
+    large buckets, all-reduce + Adam for the rest, the order OptimizerVAE issues them)
+    gives every rank exactly the parameters of one all-reduce of the whole gradient
+    followed by one Adam pass, and the summed loss tail."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_bucket_worker, args=(r, world, port, q)) for r in range(world)]
+    for pr in procs:
+        pr.start()
+    res = sorted([q.get(timeout=180) for _ in range(world)], key=lambda x: x[0])
+    for pr in procs:
+        pr.join(timeout=60)
+        assert pr.exitcode == 0
+    P, buckets = _bucket_case(world)
+    gsum = sum(torch.from_numpy(r[1]) for r in res)
+    gen = torch.Generator().manual_seed(7)
+    params = torch.randn(P + 8, generator=gen)
+    m = torch.randn(P + 8, generator=gen).abs() * 1e-3
+    v = torch.randn(P + 8, generator=gen).abs() * 1e-6
+    _adam_tf1(params[:P], m[:P], v[:P], gsum[:P], t=3, scale=1.0 / world)
+    for r in res:
+        assert np.array_equal(r[2], params[:P].numpy())
+        assert np.array_equal(r[3], m[:P].numpy())
+        assert np.array_equal(r[4], v[:P].numpy())
+        assert np.array_equal(r[5], gsum[P:].numpy())       # loss terms summed everywhere
+        assert r[6] == [b.point for b in buckets] == [1, 2, 0, 0, 0]

@@ -291,3 +291,41 @@ def test_window_plan_matches_literal(n, B, kbar):
         np.testing.assert_array_equal(wp.rows[qs[0]:qs[-1] + 1], order[key])
 
 
+
+
+def test_grad_event_points_and_buckets(lib_built):
+    """snd_plan_grad_event (ABI 13): the graph-latent d_sg_lin1 weight and bias complete
+    at point 1 (after the projection backward), the graph-latent head weight at point 2
+    (after the head backward), everything else at the final reduction; the bucket plan
+    of C4 at 8 ranks shards the two 100 MB runs and all-reduces the small rest; C2 is one
+    all-reduce of the whole gradient and the loss tail."""
+    from snd_vae_amd import _lib
+    from snd_vae_amd.model import c_config
+    from snd_vae_amd.parallel import plan_buckets
+    for preset in ("C4", "C2"):
+        cfg = PRESETS[preset]
+        L = _lib.lib()
+        h = ctypes.c_void_p()
+        cc = c_config(cfg, "bf16")
+        rc = L.snd_plan_create(ctypes.byref(cc), 8, ctypes.byref(h))
+        if rc != 0 and "hipFuncSetAttribute" in _lib.last_error():
+            pytest.skip("HIP runtime unavailable on this host")
+        _lib.check(rc)
+        lay = flat_layout(cfg)
+        names = list(lay.shapes)
+        pts = [L.snd_plan_grad_event(h, i, None) for i in range(len(names))]
+        want = {"dec.Wp": 1, "dec.bp": 1, "enc.Wh": 2} if preset == "C4" else {}
+        assert pts == [want.get(k, 0) for k in names]
+        assert L.snd_plan_grad_event(h, len(names), None) < 0
+        blocks = [(lay.offsets[k], (lay.offsets[names[i + 1]] if i + 1 < len(names) else lay.total)
+                   - lay.offsets[k]) for i, k in enumerate(names)]
+        bk = plan_buckets(blocks, pts, lay.total, lay.total + 8, 8)
+        if preset == "C4":
+            assert [(b.point, b.sharded) for b in bk] == [(1, True), (2, True), (0, False), (0, False),
+                                                          (0, False)]
+            assert (bk[0].lo, bk[0].hi) == (lay.offsets["dec.Wp"], lay.offsets["dec.K1"])
+            assert (bk[1].lo, bk[1].hi) == (lay.offsets["enc.Wh"], lay.offsets["enc.bh"])
+            assert bk[-1].hi == lay.total + 8
+        else:
+            assert [(b.lo, b.hi, b.point, b.sharded) for b in bk] == [(0, lay.total + 8, 0, False)]
+        L.snd_plan_destroy(h)
