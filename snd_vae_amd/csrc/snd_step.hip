@@ -1290,7 +1290,7 @@ extern "C" int snd_plan_launch(const snd_plan_t* plan, const snd_batch_t* batch,
   char* ws = (char*)workspace;
   hipStream_t s = (hipStream_t)stream;
   const int L = p.dj;
-  if (!strncmp(kernel, "zzt_dense", 9)) {   // zzt_dense | zzt_dense_v1 | zzt_dense_v2
+  if (!strncmp(kernel, "zzt_dense", 9)) {   // zzt_dense | zzt_dense_v<variant> (ZztArgs.variant)
     const ZztStage stg = zzt_stage(ws + p.buf("ZSTAGE"), p.B, p.N, L, p.c.dtype);
     const int variant = kernel[9] == '_' ? atoi(kernel + 11) : 0;   // zzt_dense_v<N>
     ZztArgs za{stg.jrow, stg.jt, p.N, zzt_npad(p.N), p.B, L, (float*)(ws + p.buf("DJD")),

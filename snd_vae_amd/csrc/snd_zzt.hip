@@ -258,218 +258,18 @@ __global__ void __launch_bounds__(NTH) zzt_dense_bf16(ZztArgs a) {
   block_reduce_write(st, a.part);
 }
 
-// ---------------------------------------------------------------- bf16 MFMA, v2
-// 1024-thread workgroup = 8 row groups (16 rows each, 128 rows) x 2 column
-// halves: 16 waves per CU (4 per SIMD) so one wave's VALU epilogue overlaps
-// another's MFMAs.  Column tile TJ2 = 128 staged once per workgroup; half h
-// takes chunks {2h, 2h+1} (32 columns each) of every tile, and issues the
-// second chunk's QK-MFMAs before the first chunk's epilogue (independent
-// work for the scheduler).  The halves' partial dJ are summed through LDS at
-// the end.  The logit-sign count uses a wave ballot (SALU popcount) that
-// shares its compare with the sigmoid select.
+// ---------------------------------------------------------------- v3 / v4 geometry
+// 1024-thread workgroup over 128 rows of one graph: 16 waves per CU (4 per SIMD)
+// so one wave's VALU epilogue overlaps another's MFMAs; column tiles of TJ2 = 128.
+// (Round 1's v2, 8 row groups x 2 column halves with a masked epilogue, is gone:
+// v3 replaced it with the mask-free loop below.)
 constexpr int TJ2 = 128;
 constexpr int NTH2 = 1024;
 
-struct WaveStats {
-  double loss2;     // per lane
-  unsigned wcnt;    // per wave (uniform)
-};
-
-// x[8] of this lane for a chunk; element e <-> j = jbase + 16*(e>>2) + 4*q4 + (e&3)
-template <bool SPECIAL>
-__device__ __forceinline__ void chunk_epilogue2(const f32x4& X0, const f32x4& X1, bf16x8& sb,
-                                                WaveStats& st, int jbase, int q4, int i, int n) {
-  float cs = 0.f, prod = 1.f;
-  unsigned wc = 0;
-#pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    const float xv = e < 4 ? X0[e] : X1[e - 4];
-    const float ex = __builtin_amdgcn_exp2f(-fabsf(xv));
-    const float qd = 1.f + ex;
-    const float rc = __builtin_amdgcn_rcpf(qd);
-    bool pos = xv > 0.f;
-    if constexpr (SPECIAL) {
-      const int j = jbase + 16 * (e >> 2) + 4 * q4 + (e & 3);
-      const bool valid = (j < n) && (i < n) && (j != i);
-      pos = pos && valid;
-      prod *= valid ? qd : 1.f;
-      cs += pos ? xv : 0.f;
-      sb[e] = (__bf16)(valid ? (xv > 0.f ? rc : ex * rc) : 0.f);
-    } else {
-      prod *= qd;
-      cs += pos ? xv : 0.f;      // max(x, 0) sharing the sign compare (no fmaxf canonicalise)
-      sb[e] = (__bf16)(pos ? rc : ex * rc);
-    }
-    wc += (unsigned)__popcll(__ballot(pos));
-  }
-  st.loss2 += (double)(cs + __builtin_amdgcn_logf(prod));
-  st.wcnt += wc;
-}
-
-template <int DP>
-__global__ void __launch_bounds__(NTH2) zzt_dense_bf16_v2(ZztArgs a) {
-  constexpr int JS = TJ2 * DP;         // z rows image (elements)
-  constexpr int TS = DP * TJ2;         // z^T image
-  constexpr int KS = DP / 32;
-  constexpr int CT = DP / 16;
-  constexpr int CPR = DP / 8;          // 16 B chunks per z row
-  constexpr int TCPR = TJ2 / 8;        // 16 B chunks per z^T row
-  constexpr int JCH = TJ2 * CPR, TCH = DP * TCPR;
-  constexpr int JPT = (JCH + NTH2 - 1) / NTH2, TPT = (TCH + NTH2 - 1) / NTH2;
-  __shared__ __attribute__((aligned(16))) __bf16 lds[2][JS + TS];
-
-  const int g = blockIdx.x % a.ngraphs, rb = blockIdx.x / a.ngraphs;
-  const __bf16* Jg = reinterpret_cast<const __bf16*>(a.jrow) + (long long)g * a.npad * DP;
-  const __bf16* JTg = reinterpret_cast<const __bf16*>(a.jt) + (long long)g * DP * a.npad;
-  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, r = lane & 15, q4 = lane >> 4;
-  const int rg = w & 7, half = w >> 3;
-  // wave-uniform by construction; readfirstlane lets the compiler branch on SCC
-  const int i0 = __builtin_amdgcn_readfirstlane(rb * ROWS + 16 * rg);
-  const int i_me = i0 + r;
-
-  bf16x8 bI[KS];
-#pragma unroll
-  for (int ks = 0; ks < KS; ++ks)
-    bI[ks] = *reinterpret_cast<const bf16x8*>(Jg + (long long)i_me * DP + 32 * ks + 8 * q4);
-  // Retire the z_i loads before the loop: otherwise the waitcnt pass merges
-  // them with the loop-carried prefetch and waits vmcnt(0) ahead of every
-  // tile's first MFMA, serialising the global prefetch with compute.
-  __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0)
-  f32x4 acc[CT];
-#pragma unroll
-  for (int ct = 0; ct < CT; ++ct) acc[ct] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  uint4 rj[JPT], rt[TPT];
-  auto gload = [&](int t) {
-#pragma unroll
-    for (int p = 0; p < JPT; ++p) {
-      const int idx = tid + p * NTH2;
-      if (idx < JCH) {
-        const int row = idx / CPR, ch = idx - row * CPR;
-        rj[p] = *reinterpret_cast<const uint4*>(Jg + (long long)(t * TJ2 + row) * DP + ch * 8);
-      }
-    }
-#pragma unroll
-    for (int p = 0; p < TPT; ++p) {
-      const int idx = tid + p * NTH2;
-      if (idx < TCH) {
-        const int c = idx / TCPR, ch = idx - c * TCPR;
-        rt[p] = *reinterpret_cast<const uint4*>(JTg + (long long)c * a.npad + t * TJ2 + ch * 8);
-      }
-    }
-  };
-  auto sstore = [&](int buf) {
-#pragma unroll
-    for (int p = 0; p < JPT; ++p) {
-      const int idx = tid + p * NTH2;
-      if (idx < JCH) {
-        const int row = idx / CPR, ch = idx - row * CPR;
-        *reinterpret_cast<uint4*>(&lds[buf][row * DP + ((ch ^ Swz<DP>::j(row)) * 8)]) = rj[p];
-      }
-    }
-#pragma unroll
-    for (int p = 0; p < TPT; ++p) {
-      const int idx = tid + p * NTH2;
-      if (idx < TCH) {
-        const int c = idx / TCPR, ch = idx - c * TCPR;
-        // 16 B chunk swizzle: 8 B unit u -> u ^ 2(c & 15) keeps unit pairs together
-        *reinterpret_cast<uint4*>(&lds[buf][JS + c * TJ2 + ((ch ^ (c & 15)) * 8)]) = rt[p];
-      }
-    }
-  };
-
-  auto qk = [&](const __bf16* Ls, int q, f32x4& X0, f32x4& X1) {
-    X0 = f32x4{0.f, 0.f, 0.f, 0.f};
-    X1 = f32x4{0.f, 0.f, 0.f, 0.f};
-    const int ra = 32 * q + r, rb2 = 32 * q + 16 + r;
-#pragma unroll
-    for (int ks = 0; ks < KS; ++ks) {
-      const bf16x8 a0 = *reinterpret_cast<const bf16x8*>(
-          &Ls[ra * DP + (((4 * ks + q4) ^ Swz<DP>::j(ra)) * 8)]);
-      const bf16x8 a1 = *reinterpret_cast<const bf16x8*>(
-          &Ls[rb2 * DP + (((4 * ks + q4) ^ Swz<DP>::j(rb2)) * 8)]);
-      X0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, bI[ks], X0, 0, 0, 0);
-      X1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, bI[ks], X1, 0, 0, 0);
-    }
-  };
-  auto pv = [&](const __bf16* Ls, int q, const bf16x8& sb) {
-#pragma unroll
-    for (int ct = 0; ct < CT; ++ct) {
-      const int c = 16 * ct + r;
-      const int sw = (c & 15) << 1;
-      const int u0 = 8 * q + q4, u1 = 8 * q + 4 + q4;     // 8 B units of 4 j
-      const bf16x4 lo = *reinterpret_cast<const bf16x4*>(&Ls[JS + c * TJ2 + ((u0 ^ sw) * 4)]);
-      const bf16x4 hi = *reinterpret_cast<const bf16x4*>(&Ls[JS + c * TJ2 + ((u1 ^ sw) * 4)]);
-      const bf16x8 a2 = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-      acc[ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a2, sb, acc[ct], 0, 0, 0);
-    }
-  };
-  auto epi = [&](int t, int q, const f32x4& X0, const f32x4& X1, bf16x8& sb, WaveStats& st) {
-    const int jbase = t * TJ2 + 32 * q;
-    const bool special = (jbase + 32 > a.n) || (i0 + 16 > a.n) ||
-                         (i0 >= jbase && i0 < jbase + 32);
-    if (special) chunk_epilogue2<true>(X0, X1, sb, st, jbase, q4, i_me, a.n);
-    else chunk_epilogue2<false>(X0, X1, sb, st, jbase, q4, i_me, a.n);
-  };
-
-  const int ntiles = a.npad / TJ2;
-  gload(0);
-  sstore(0);
-  __syncthreads();
-  WaveStats st{0.0, 0u};
-  const int qa = 2 * half, qb = 2 * half + 1;
-  for (int t = 0; t < ntiles; ++t) {
-    const int cur = t & 1;
-    if (t + 1 < ntiles) gload(t + 1);
-    const __bf16* Ls = lds[cur];
-    f32x4 Xa0, Xa1, Xb0, Xb1;
-    bf16x8 sa, sbv;
-    qk(Ls, qa, Xa0, Xa1);
-    qk(Ls, qb, Xb0, Xb1);           // independent of chunk a's epilogue
-    epi(t, qa, Xa0, Xa1, sa, st);
-    pv(Ls, qa, sa);
-    epi(t, qb, Xb0, Xb1, sbv, st);
-    pv(Ls, qb, sbv);
-    if (t + 1 < ntiles) sstore(cur ^ 1);
-    __syncthreads();
-  }
-
-  // combine the two column halves' partial dJ through LDS (staging is free now)
-  float* red = reinterpret_cast<float*>(&lds[0][0]);
-  const int slot = (rg * 64 + lane) * (4 * CT);
-  if (half == 1) {
-#pragma unroll
-    for (int ct = 0; ct < CT; ++ct)
-      *reinterpret_cast<f32x4*>(&red[slot + 4 * ct]) = acc[ct];
-  }
-  __syncthreads();
-  if (half == 0 && i_me < a.n) {
-    float* dst = a.dJd + ((long long)g * a.n + i_me) * a.d;
-#pragma unroll
-    for (int ct = 0; ct < CT; ++ct) {
-      const f32x4 o = *reinterpret_cast<const f32x4*>(&red[slot + 4 * ct]);
-      const int c0 = 16 * ct + 4 * q4;
-      if (c0 < a.d)
-        *reinterpret_cast<float4*>(dst + c0) =
-            make_float4(acc[ct][0] + o[0], acc[ct][1] + o[1], acc[ct][2] + o[2], acc[ct][3] + o[3]);
-    }
-  }
-  // statistics: per-lane loss, per-wave count
-  __shared__ double sl[NTH2 / 64];
-  __shared__ unsigned sc[NTH2 / 64];
-  const double l = wave_sum_d(st.loss2);
-  if (lane == 0) { sl[w] = l; sc[w] = st.wcnt; }
-  __syncthreads();
-  if (tid == 0) {
-    double tl = 0.0, tc = 0.0;
-    for (int k = 0; k < NTH2 / 64; ++k) { tl += sl[k]; tc += (double)sc[k]; }
-    a.part[2 * blockIdx.x] = tl * (double)kLn2;
-    a.part[2 * blockIdx.x + 1] = tc;
-  }
-}
 
 // ---------------------------------------------------------------- bf16 MFMA, v3
-// v2's structure with a mask-free main loop.  Every (i, j) of the padded
+// 8 row groups (16 rows) x 2 column halves (32-column chunks of every tile),
+// with a mask-free main loop.  Every (i, j) of the padded
 // npad x npad square is evaluated; afterwards
 //   * padded pairs (zero rows, x = 0 exactly: 1 log2-unit of loss each, no
 //     sign count, sigma * 0 = 0 into dJ) are subtracted analytically;
@@ -1357,10 +1157,6 @@ int launch_zzt_dense(const ZztArgs& a, int dtype, hipStream_t s) {
     if (dp == 32) hipLaunchKernelGGL((zzt_dense_bf16<32>), grid, dim3(NTH), 0, s, a);
     else if (dp == 64) hipLaunchKernelGGL((zzt_dense_bf16<64>), grid, dim3(NTH), 0, s, a);
     else hipLaunchKernelGGL((zzt_dense_bf16<128>), grid, dim3(NTH), 0, s, a);
-  } else if (dtype == SND_BF16 && a.variant == 2) {   // v2: masked epilogue
-    if (dp == 32) hipLaunchKernelGGL((zzt_dense_bf16_v2<32>), grid, dim3(NTH2), 0, s, a);
-    else if (dp == 64) hipLaunchKernelGGL((zzt_dense_bf16_v2<64>), grid, dim3(NTH2), 0, s, a);
-    else hipLaunchKernelGGL((zzt_dense_bf16_v2<128>), grid, dim3(NTH2), 0, s, a);
   } else if (dtype == SND_BF16 && dp <= 64 && (a.variant & 255) != 3) {   // v4 (default, d <= 64)
     // default: signed epilogue, plain tile order; A/B: variant 10 + 3 EPI + MODE;
     // variant >= 256: the measurement build of the default (phase skips / stamps)

@@ -134,8 +134,6 @@ class OptimizerVAE:
                     self._events[pt] = ev
                 if L.snd_plan_grad_event(m.plan, i, C.c_void_p(self._events[pt].cuda_event)) != pt:
                     raise _lib.SNDError(f"snd_plan_grad_event: block {k}: {_lib.last_error()}")
-        self._shard_grads = [torch.empty((b.hi - b.lo) // self.world if b.sharded else 0,
-                                         dtype=torch.float32, device=m.device) for b in self.buckets]
         self._comm = torch.cuda.Stream(device=m.device) if self._events else None
         self.step_next = torch.zeros(1, dtype=torch.int32, device=m.device)
 
@@ -194,7 +192,7 @@ class OptimizerVAE:
             run_buckets(self.buckets, self.grads, self.model.params, self.model.param_count,
                         self.world, self.rank,
                         lambda off, n, gr, b: self._adam(off, n, gr, step=self.step_next if b.point else None),
-                        self._shard_grads,
+                        None,   # in-place reduce-scatter into this rank's chunk of grads
                         lambda out, inp: dist.reduce_scatter_tensor(out, inp, group=g),
                         lambda out, inp: dist.all_gather_into_tensor(out, inp, group=g),
                         lambda t: dist.all_reduce(t, group=g), wait)

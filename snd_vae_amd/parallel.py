@@ -116,7 +116,9 @@ def run_buckets(buckets, grads, params, param_count: int, world: int, rank: int,
       other bucket:    all-reduce(sum) its gradient, adam over its parameters.
 
     adam(lo, n, g, bucket) updates params/m/v[lo:lo+n] with gradient g (1/world folded
-    in by the caller); shard_grads[i]: the chunk buffer of bucket i; wait(bucket) orders
+    in by the caller); shard_grads[i]: the chunk buffer of bucket i, or None for an
+    in-place reduce-scatter into this rank's chunk of the gradient buffer (no copy,
+    a no-op at world 1); wait(bucket) orders
     the bucket after its gradient is complete (the GPU path: a stream wait on the
     bucket's event).  The collectives are parameters so the same schedule runs on
     RCCL (product) and gloo (CPU tests)."""
@@ -125,10 +127,11 @@ def run_buckets(buckets, grads, params, param_count: int, world: int, rank: int,
             wait(b)
         if b.sharded:
             lo, c = b.shard(world, rank)
-            reduce_scatter(shard_grads[i], grads[b.lo:b.hi])
+            out = grads[lo:lo + c] if shard_grads is None else shard_grads[i]
+            reduce_scatter(out, grads[b.lo:b.hi])
             n = max(0, min(lo + c, param_count) - lo)
             if n:
-                adam(lo, n, shard_grads[i][:n], b)
+                adam(lo, n, out[:n], b)
             all_gather(params[b.lo:b.hi], params[lo:lo + c])
         else:
             all_reduce(grads[b.lo:b.hi])

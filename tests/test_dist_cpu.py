@@ -167,7 +167,7 @@ def _bucket_case(world):
     return P, plan_buckets(list(zip(offs, lens)), pts, P, P + 8, world, shard_min=1024)
 
 
-def _bucket_worker(rank, world, port, q):
+def _bucket_worker(rank, world, port, q, inplace):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
     from snd_vae_amd.parallel import init_from_env, run_buckets
@@ -185,7 +185,7 @@ def _bucket_worker(rank, world, port, q):
     def adam(off, n, g, b):
         _adam_tf1(params[off:off + n], m[off:off + n], v[off:off + n], g, t=3, scale=1.0 / world)
 
-    run_buckets(buckets, grads, params, P, world, rank, adam, shard_grads,
+    run_buckets(buckets, grads, params, P, world, rank, adam, shard_grads if inplace is False else None,
                 lambda out, inp: dist.reduce_scatter_tensor(out, inp, group=info.group),
                 lambda out, inp: dist.all_gather_into_tensor(out, inp, group=info.group),
                 lambda t: dist.all_reduce(t, group=info.group), wait=lambda b: order.append(b.point))
@@ -214,8 +214,8 @@ def test_bucket_plan_shapes():
     assert [(b.lo, b.hi, b.point, b.sharded) for b in one] == [(0, 200, 0, False)]
 
 
-@pytest.mark.parametrize("world", [2])
-def test_bucketed_exchange_equals_allreduce_adam(world):
+@pytest.mark.parametrize("world,inplace", [(2, True), (2, False)])
+def test_bucketed_exchange_equals_allreduce_adam(world, inplace):
     """parallel.run_buckets (reduce-scatter + per-rank shard Adam + all-gather for
     large buckets, all-reduce + Adam for the rest, the order OptimizerVAE issues them)
     gives every rank exactly the parameters of one all-reduce of the whole gradient
@@ -223,7 +223,7 @@ def test_bucketed_exchange_equals_allreduce_adam(world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_bucket_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_bucket_worker, args=(r, world, port, q, inplace)) for r in range(world)]
     for pr in procs:
         pr.start()
     res = sorted([q.get(timeout=180) for _ in range(world)], key=lambda x: x[0])
@@ -242,4 +242,5 @@ def test_bucketed_exchange_equals_allreduce_adam(world):
         assert np.array_equal(r[3], m[:P].numpy())
         assert np.array_equal(r[4], v[:P].numpy())
         assert np.array_equal(r[5], gsum[P:].numpy())       # loss terms summed everywhere
+        assert len(r[6]) == len(buckets)
         assert r[6] == [b.point for b in buckets] == [1, 2, 0, 0, 0]

@@ -16,7 +16,7 @@ def main():
     ap.add_argument("--graphs", type=int, default=8)
     ap.add_argument("--nodes", type=int, default=4096)
     ap.add_argument("--latent", type=int, default=64)
-    ap.add_argument("--variants", default="zzt_dense,zzt_dense_v2,zzt_dense_v1")
+    ap.add_argument("--variants", default="zzt_dense,zzt_dense_v1")
     args = ap.parse_args()
     import torch
     from snd_vae_amd import _lib
