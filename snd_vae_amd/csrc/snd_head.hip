@@ -469,7 +469,11 @@ __global__ void __launch_bounds__(1024) head_bwd_kernel(HeadBwdArgs a) {
           const float4 mu = *reinterpret_cast<const float4*>(msr + c0 + 4 * h);
           const float4 ls = *reinterpret_cast<const float4*>(msr + L + c0 + 4 * h);
           const float4 ep = *reinterpret_cast<const float4*>(a.eps + ie + 4 * h);
-          const float4 dj = *reinterpret_cast<const float4*>(a.dJd + ie + 4 * h);
+          float4 dj = *reinterpret_cast<const float4*>(a.dJd + ie + 4 * h);
+          for (int sx = 0; sx < a.nextra; ++sx) {   // zzt_split_sum_kernel's order
+            const float4 e = *reinterpret_cast<const float4*>(a.dJd_extra + (long long)sx * a.R * L + ie + 4 * h);
+            dj.x += e.x; dj.y += e.y; dj.z += e.z; dj.w += e.w;
+          }
           const float4 dd = *reinterpret_cast<const float4*>(a.dz_dec + ie + 4 * h);
           const float m4[4] = {mu.x, mu.y, mu.z, mu.w}, l4[4] = {ls.x, ls.y, ls.z, ls.w};
           const float e4[4] = {ep.x, ep.y, ep.z, ep.w}, j4[4] = {dj.x, dj.y, dj.z, dj.w};

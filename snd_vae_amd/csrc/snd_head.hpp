@@ -44,6 +44,7 @@ struct HeadBwdArgs {
   const __bf16* zb; int L; float pos_weight;   // z (bf16) [R][L]
   double* edge_part;                           // [tiles][2] = {loss, tp}
   const float* ms; const float* eps; const float* dz_dec; const float* dJd;
+  const float* dJd_extra; int nextra;          // zz^T column-split partials, added in order
   float adj_scale, kl_scale;
   __bf16* dms; float* bms_part;                // d[mu | s] [R][2L] bf16; [tiles][2L]
   const __bf16* wmsb_img; int kp1, np1, gh;    // Wms^T image [np1][kp1 = 2L]

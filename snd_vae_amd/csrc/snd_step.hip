@@ -932,6 +932,7 @@ int encoder_fast_bwd(const Ctx& x, const snd_batch_t* batch, float adj_scale, fl
     a.rowptr = batch->rowptr; a.colidx = batch->colidx; a.R = R;
     a.zb = bf("ZB"); a.L = L; a.pos_weight = c.pos_weight; a.edge_part = x.d("PEDGE");
     a.ms = x.f("MS"); a.eps = x.f("EPS"); a.dz_dec = x.f("DZDEC"); a.dJd = x.f("DJD");
+    a.dJd_extra = x.f("DJDX"); a.nextra = zzt_tsplit(p.B, p.N, c.dtype) - 1;   // deferred split sum
     a.adj_scale = adj_scale; a.kl_scale = kl_scale;
     a.dms = bf("FDMS"); a.bms_part = x.f("PHBMS");
     a.wmsb_img = reinterpret_cast<const __bf16*>(x.ws + p.pwmsb.off); a.kp1 = p.pwmsb.kp; a.np1 = p.pwmsb.np;
@@ -1494,7 +1495,8 @@ extern "C" int snd_train_step(const snd_plan_t* plan, const snd_batch_t* batch,
     if (!p.fast) SND_TRY(launch_zzt_prep(x.f("Z"), p.B, N, dj, c.dtype, stg, x.s));
     ZztArgs za{stg.jrow, stg.jt, N, zzt_npad(N), p.B, dj, x.f("DJD"), x.d("PZZT"), stg.colpart, 0,
                x.f("DJDX")};
-    SND_TRY(launch_zzt_dense(za, c.dtype, x.s));
+    // the fused head backward adds the column-split partials itself (one launch fewer)
+    SND_TRY(launch_zzt_dense(za, c.dtype, x.s, p.fast_enc && !p.tref && p.head_bwd));
   }
   if (p.fast) {
     SND_TRY(decoder_fast(x, batch));

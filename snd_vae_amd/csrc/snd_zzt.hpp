@@ -34,6 +34,9 @@ ZztStage zzt_stage(void* base, int ngraphs, int n, int d, int dtype);
 int zzt_init_attributes();
 int launch_zzt_prep(const float* z, int ngraphs, int n, int d, int dtype, const ZztStage& st,
                     hipStream_t s);
-int launch_zzt_dense(const ZztArgs& a, int dtype, hipStream_t s);
+// defer_split: column splits (zzt_tsplit > 1) leave their partial dJ in dJd_extra for
+// the consumer to add (head_bwd_kernel, in the same fixed order) instead of launching
+// zzt_split_sum_kernel
+int launch_zzt_dense(const ZztArgs& a, int dtype, hipStream_t s, bool defer_split = false);
 
 }  // namespace snd
