@@ -300,7 +300,11 @@ def test_forced_world1_process_group_runs_the_distributed_step():
         finally:
             dist.all_reduce = real
         torch.cuda.synchronize()
-        assert calls == [ma.param_count + 8] * 3
+        # the bucketed exchange (parallel.plan_buckets): every bucket is all-reduced once per
+        # step at this size (no bucket reaches SHARD_MIN), together exactly grads || loss terms
+        nb = len(oa.buckets)
+        assert nb > 1 and not any(b.sharded for b in oa.buckets)
+        assert len(calls) == 3 * nb and sum(calls) == 3 * (ma.param_count + 8)
         assert torch.equal(ma.params, mb.params)
         assert torch.equal(oa.losses, ob.losses)
     finally:
