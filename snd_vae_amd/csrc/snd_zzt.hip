@@ -1067,6 +1067,340 @@ __global__ void __launch_bounds__(NTH2) zzt_dense_bf16_v4(ZztArgs a) {
   }
 }
 
+// ---------------------------------------------------------------- bf16 MFMA, v7 (d = 128)
+// v4's work split and signed (EPI 0) epilogue at d = 128, where v4's two LDS images
+// per tile (z rows and z^T, 2 x 35 KB) cannot be triple-buffered beside the
+// workgroup's own rows.  One image per tile serves both products:
+//   * layout: 8-row x 32-column subtiles of 512 B, 16-byte chunks XOR-swizzled
+//     (zoa; MI355X guide T10 "one image for row reads AND transposed reads"): the
+//     forward A operand (z_j rows) is a ds_read_b128 row read, the backward B operand
+//     (z_j[c] for the 8 j of a k-slot, column c on the lane) two ds_read_b64_tr_b16
+//     transposed reads of the same image; both conflict-free, 2 address bases each;
+//   * the image holds z * sqrt(log2 e) (the forward's scaled rows), so the backward
+//     sums scaled z_j and the result is divided by sqrt(log2 e) once at the end
+//     (within bf16 rounding of v3's unscaled z^T operand);
+//   * tiles arrive by LDS-DMA (asm-issued, counted vmcnt) into a 3-deep ring, the
+//     workgroup's -z_i rows sit in a fourth image: 128 KB of LDS;
+//   * the four column blocks' partial dJ are combined through LDS in two passes
+//     (two 32-column output blocks each: 98 KB).
+// Per wave and tile: 8 forward + 8 backward v_mfma_f32_32x32x16_bf16, the same
+// epilogue VALU as v4 at d = 64: twice v4's MFMA work per logit.
+typedef short zv4s __attribute__((ext_vector_type(4)));
+typedef short zv8s __attribute__((ext_vector_type(8)));
+typedef __attribute__((address_space(3))) zv4s zlds_v4s;
+typedef __attribute__((address_space(3))) void* zlptr_t;
+
+__device__ __forceinline__ int zoa(int row, int ch) {   // byte offset of (row, 16-byte chunk ch)
+  return 2048 * (row >> 3) + 512 * (ch >> 2) + 64 * (row & 7) + 16 * ((ch & 3) ^ ((row >> 2) & 3));
+}
+// one 16-byte LDS-DMA per lane to the wave-uniform LDS byte address dst + 16 lane,
+// issued from inline asm: the compiler neither tracks nor drains it
+__device__ __forceinline__ void zdma16(const void* g, unsigned dst) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+               "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(g), "s"(dst) : "memory");
+}
+__device__ __forceinline__ bf16x8 ztr_pair(const char* p0, const char* p1) {
+  const zv4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((zlds_v4s*)(p0));
+  const zv4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((zlds_v4s*)(p1));
+  const zv8s c = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+  return __builtin_bit_cast(bf16x8, c);
+}
+constexpr float kInvSqrtLog2e = 0.8325546111576977f;   // 1 / sqrt(log2 e)
+
+template <bool MEAS, bool STAG>
+__global__ void __launch_bounds__(NTH2) zzt_dense_bf16_v7(ZztArgs a) {
+  constexpr int DP = 128, NT = NTH2, NW = NT / 64;
+  constexpr int KS = DP / 16;          // forward k-steps
+  constexpr int CB = DP / 32;          // backward 32-column output blocks
+  constexpr int IMG = TJ2 * DP * 2;    // one [128][128] bf16 image, 32 KB
+  __shared__ __attribute__((aligned(16))) char lds[4 * IMG];   // 3 tile buffers, -z_i rows
+  __shared__ float colsum[DP];
+  __shared__ float csred[NT / DP][DP];
+  __shared__ float dsg[4][32];
+  __shared__ double sl[NW];
+  __shared__ unsigned sc[NW];
+  char* brows = lds + 3 * IMG;
+  const unsigned lds0 = (unsigned)(uintptr_t)(zlptr_t)lds;
+
+  // measurement only (MEAS, variant >> 8): 1 skips the epilogue, 2 the forward MFMAs,
+  // 4 the backward MFMAs, 8 the tile DMAs (results wrong)
+  const int skip = MEAS ? __builtin_amdgcn_readfirstlane(a.variant >> 8) : 0;
+  const int wgs = a.ngraphs * (a.npad / ROWS);
+  const int sp = blockIdx.x / wgs, bx = blockIdx.x - sp * wgs;
+  const int nsplit = gridDim.x / wgs;
+  const int g = bx % a.ngraphs, rb = bx / a.ngraphs;
+  const __bf16* Jg = reinterpret_cast<const __bf16*>(a.jrow) + (long long)g * a.npad * DP;
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, r = lane & 31, h = lane >> 5;
+  const int rg = w & 3, cb = w >> 2;
+  const int i0 = __builtin_amdgcn_readfirstlane(rb * ROWS + 32 * rg);
+  const int i_me = i0 + r;
+  const int ntot = a.npad / TJ2;
+  const int t0 = sp * ntot / nsplit, t1 = (sp + 1) * ntot / nsplit;
+
+  // tile t -> ring buffer b: 32 pieces of 1 KB, wave w issues pieces w and w + 16.
+  // Piece P, lane l lands at 1024 P + 16 l = row 8 (P >> 1) + ((l >> 2) & 7), chunk
+  // 4 (2 (P & 1) + (l >> 5)) + ((l & 3) ^ ((row >> 2) & 3)) of the image (zoa inverse)
+  int dsrc[2];
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int P = w + 16 * k;
+    const int row = 8 * (P >> 1) + ((lane >> 2) & 7);
+    const int ch = 4 * (2 * (P & 1) + (lane >> 5)) + ((lane & 3) ^ ((row >> 2) & 3));
+    dsrc[k] = row * DP + 8 * ch;
+  }
+  auto dma = [&](int t, int b) {
+    if (MEAS && (skip & 8)) return;
+#pragma unroll
+    for (int k = 0; k < 2; ++k)
+      zdma16(Jg + (long long)t * TJ2 * DP + dsrc[k],
+             __builtin_amdgcn_readfirstlane(lds0 + b * IMG + 1024 * (w + 16 * k)));
+  };
+
+  // ---- prologue: tiles t0, t0+1 in flight (STAG: t0 only); -z_i rows; column sums
+  dma(t0, 0);
+  if (!STAG) dma(min(t0 + 1, t1 - 1), 1);
+  for (int idx = tid; idx < ROWS * (DP / 8); idx += NT) {
+    const int row = idx >> 4, ch = idx & 15;
+    const uint4 u = *reinterpret_cast<const uint4*>(Jg + (long long)(rb * ROWS + row) * DP + ch * 8);
+    *reinterpret_cast<uint4*>(brows + zoa(row, ch)) =
+        make_uint4(u.x ^ 0x80008000u, u.y ^ 0x80008000u, u.z ^ 0x80008000u, u.w ^ 0x80008000u);
+  }
+  {
+    const int nrb = a.npad / 64;
+    const int k = tid % DP, grp = tid / DP;
+    float s = 0.f;
+    for (int p = grp; p < nrb; p += NT / DP) s += a.colpart[((long long)g * nrb + p) * DP + k];
+    csred[grp][k] = s;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid < DP) {
+    float s = 0.f;
+    for (int p = 0; p < NT / DP; ++p) s += csred[p][tid];
+    colsum[tid] = s;
+  }
+
+  f32x16 acc[CB];
+#pragma unroll
+  for (int q = 0; q < CB; ++q)
+#pragma unroll
+    for (int v = 0; v < 16; ++v) acc[q][v] = 0.f;
+  // forward operand bases (k-step s: base[s & 1] + 512 (s >> 1))
+  const int ja = 32 * cb + r, ia = 32 * rg + r;
+  const int fa0 = zoa(ja, h), fa1 = zoa(ja, 2 + h);
+  const int fb0 = zoa(ia, h), fb1 = zoa(ia, 2 + h);
+  // backward transposed-read bases: lane 4 qq + pp of group gq supplies row
+  // 32 cb + 16 s + 8 t + 4 (gq >> 1) + qq, columns 32 q + 16 (gq & 1) + 4 pp .. + 3
+  const int gq = lane >> 4, qq = (lane >> 2) & 3, pp = lane & 3;
+  const int c0 = 2 * (gq & 1) + (pp >> 1);
+  const int tb0 = 2048 * (4 * cb) + 64 * (4 * (gq >> 1) + qq) + 16 * (c0 ^ (gq >> 1)) + 8 * (pp & 1);
+  const int tb1 = 2048 * (4 * cb + 1) + 64 * (4 * (gq >> 1) + qq) + 16 * (c0 ^ ((gq >> 1) + 2)) + 8 * (pp & 1);
+  auto fwd = [&](int b) {
+    f32x16 X;
+#pragma unroll
+    for (int v = 0; v < 16; ++v) X[v] = 0.f;
+    if (MEAS && (skip & 2)) return X;
+    const char* T = lds + b * IMG;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      const bf16x8 av = *reinterpret_cast<const bf16x8*>(T + ((s & 1) ? fa1 : fa0) + 512 * (s >> 1));
+      const bf16x8 bv = *reinterpret_cast<const bf16x8*>(brows + ((s & 1) ? fb1 : fb0) + 512 * (s >> 1));
+      X = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, bv, X, 0, 0, 0);
+    }
+    return X;
+  };
+  float lacc = 0.f;
+  double ltot = 0.0;
+  unsigned lcnt = 0;
+  auto epi = [&](const f32x16& Y, bf16x8 (&sA)[2]) {   // v4 EPI 0, y = -x
+    if (MEAS && (skip & 1)) {
+#pragma unroll
+      for (int v = 0; v < 16; ++v) sA[v >> 3][v & 7] = (__bf16)Y[v];
+      return;
+    }
+    float q[16], lt = 0.f;
+#pragma unroll
+    for (int v = 0; v < 16; ++v) {
+      const float e = __builtin_amdgcn_exp2f(Y[v]);
+      q[v] = e + 1.f;
+      sA[v >> 3][v & 7] = (__bf16)__builtin_amdgcn_rcpf(q[v]);
+    }
+#pragma unroll
+    for (int g4 = 0; g4 < 4; ++g4) {
+      const unsigned t01 = __builtin_amdgcn_perm(__float_as_uint(Y[4 * g4 + 1]),
+                                                 __float_as_uint(Y[4 * g4]), 0x0C0C0703u);
+      const unsigned t23 = __builtin_amdgcn_perm(__float_as_uint(Y[4 * g4 + 3]),
+                                                 __float_as_uint(Y[4 * g4 + 2]), 0x07030C0Cu);
+      lcnt += (unsigned)__builtin_popcount((t01 | t23) & 0x80808080u);
+    }
+#pragma unroll
+    for (int p = 0; p < 4; ++p)
+      lt += __builtin_amdgcn_logf((q[4 * p] * q[4 * p + 1]) * (q[4 * p + 2] * q[4 * p + 3]));
+    if (__builtin_expect(!__builtin_isfinite(lt), 0)) {   // a quad product overflowed
+      lt = 0.f;
+#pragma unroll
+      for (int v = 0; v < 16; ++v) {
+        const float xn = Y[v];
+        lt += fmaxf(xn, 0.f) + __builtin_amdgcn_logf(1.f + __builtin_amdgcn_exp2f(-fabsf(xn)));
+      }
+    }
+    lacc += lt;
+  };
+  auto bwd = [&](int b, const bf16x8 (&sA)[2]) {
+    if (MEAS && (skip & 4)) { lacc += (float)sA[0][0]; return; }
+    const char* T = lds + b * IMG;
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int q = 0; q < CB; ++q) {
+        const bf16x8 bv = ztr_pair(T + tb0 + 4096 * s + 512 * q, T + tb1 + 4096 * s + 512 * q);
+        acc[q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(sA[s], bv, acc[q], 0, 0, 0);
+      }
+  };
+
+  // tile t in ring slot CUR: DMA of tile t+2 into the slot tile t-1 left, forward,
+  // epilogue, backward; wait for tile t+1 (its 2 DMAs per wave; t+2's may fly), barrier.
+  // STAG: the odd column-block waves (two of the four waves of every SIMD: waves w and
+  // w + 4k share one) run one tile late -- tile t-1's epilogue and backward, then tile
+  // t's forward -- so after every barrier half of each SIMD's waves start on the VALU
+  // while the other half starts on the matrix pipe (the phases otherwise serialise:
+  // all four waves open a tile with their forward MFMAs and close it with the
+  // backward ones).  Three slots hold tiles t-1 (late backward), t and t+1 (DMA'd
+  // one tile ahead into the slot of tile t-2).
+  // (the two roles run separate loops, so the early waves do not keep the late waves'
+  // carried logits live)
+  auto run = [&](auto late_c) {
+    constexpr bool LATE = decltype(late_c)::value;
+    f32x16 Yp;
+#pragma unroll
+    for (int v = 0; v < 16; ++v) Yp[v] = 0.f;
+    auto tile = [&](int t, auto cc) {
+      constexpr int CUR = decltype(cc)::value, NN = (CUR + 2) % 3;
+      if constexpr (STAG) {
+        if (t + 1 < t1) dma(t + 1, (CUR + 1) % 3);
+        if constexpr (LATE) {
+          if (t > t0) {
+            bf16x8 sA[2];
+            epi(Yp, sA);
+            bwd(NN, sA);   // tile t-1's slot
+          }
+          Yp = fwd(CUR);
+        } else {
+          const f32x16 Y = fwd(CUR);
+          bf16x8 sA[2];
+          epi(Y, sA);
+          bwd(CUR, sA);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // tile t+1 landed
+      } else {
+        dma(min(t + 2, t1 - 1), NN);
+        const f32x16 Y = fwd(CUR);
+        bf16x8 sA[2];
+        epi(Y, sA);
+        bwd(CUR, sA);
+        asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+      }
+      __syncthreads();
+    };
+    for (int t = t0; t < t1; t += 3) {
+      tile(t, std::integral_constant<int, 0>{});
+      if (t + 1 < t1) tile(t + 1, std::integral_constant<int, 1>{});
+      if (t + 2 < t1) tile(t + 2, std::integral_constant<int, 2>{});
+      ltot += (double)lacc;
+      lacc = 0.f;
+    }
+    if (LATE && t1 > t0) {   // the late waves' last tile (its slot is intact: no DMA after the loop)
+      bf16x8 sA[2];
+      epi(Yp, sA);
+      bwd((t1 - 1 - t0) % 3, sA);
+      ltot += (double)lacc;
+      lacc = 0.f;
+    }
+  };
+  if (STAG && (cb & 1)) run(std::true_type{});
+  else run(std::false_type{});
+
+  // ---- per-row corrections (row i_me; lanes r and r + 32 hold its two k halves)
+  float xd = 0.f, xs = 0.f;
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+    const bf16x8 bv = *reinterpret_cast<const bf16x8*>(brows + ((s & 1) ? fb1 : fb0) + 512 * (s >> 1));
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float bb = (float)bv[e];
+      xd += bb * bb;
+      xs += bb * colsum[16 * s + 8 * h + e];
+    }
+  }
+  xd += __shfl_xor(xd, 32, 64);
+  xs += __shfl_xor(xs, 32, 64);
+  xs = -xs;
+  const bool row_valid = i_me < a.n;
+  const bool corr = sp == 0;
+  const bool own = cb == 0 && h == 0 && row_valid && corr;
+  const float exd = __builtin_amdgcn_exp2f(-fabsf(xd));
+  if (own) {
+    ltot += (double)xs;
+    ltot -= (double)(fmaxf(xd, 0.f) + __builtin_amdgcn_logf(1.f + exd));
+  }
+  const unsigned dpos = (unsigned)__popcll(__ballot(own && xd > 0.f));
+  if (cb == 0 && h == 0) {   // s'_ii as the backward MFMA consumed it (bf16), 0 outside split 0
+    const float sg = __builtin_amdgcn_rcpf(__builtin_amdgcn_exp2f(-xd) + 1.f);
+    dsg[rg][r] = corr ? (float)(__bf16)sg : 0.f;
+  }
+
+  // ---- combine the four column blocks' partial dJ' (fixed order) through LDS, two
+  // 32-column output blocks per pass; the diagonal term subtracted with the same
+  // scaled z_i the backward products used, then the sqrt(log2 e) scale removed
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no DMA may land in red
+  __syncthreads();
+  float* red = reinterpret_cast<float*>(lds);        // [cb-1][rg][2 * 16][64]
+  float* dst = (sp == 0 ? a.dJd : a.dJd_extra + (long long)(sp - 1) * a.ngraphs * a.n * a.d) +
+               (long long)g * a.n * a.d;
+  const __bf16* zi = Jg + (long long)(rb * ROWS + 32 * rg) * DP;
+#pragma unroll
+  for (int pass = 0; pass < 2; ++pass) {
+    if (cb > 0) {
+#pragma unroll
+      for (int qh = 0; qh < 2; ++qh)
+#pragma unroll
+        for (int v = 0; v < 16; ++v)
+          red[(((cb - 1) * 4 + rg) * 32 + qh * 16 + v) * 64 + lane] = acc[2 * pass + qh][v];
+    }
+    __syncthreads();
+    if (cb == 0) {
+#pragma unroll
+      for (int qh = 0; qh < 2; ++qh) {
+        const int c = 32 * (2 * pass + qh) + r;
+#pragma unroll
+        for (int v = 0; v < 16; ++v) {
+          float o = acc[2 * pass + qh][v];
+#pragma unroll
+          for (int k = 0; k < 3; ++k) o += red[((k * 4 + rg) * 32 + qh * 16 + v) * 64 + lane];
+          const int il = (v & 3) + 8 * (v >> 2) + 4 * h;   // D row within the row group
+          const int i = i0 + il;
+          if (i < a.n && c < a.d)
+            dst[(long long)i * a.d + c] = (o - dsg[rg][il] * (float)zi[il * DP + c]) * kInvSqrtLog2e;
+        }
+      }
+    }
+    __syncthreads();
+  }
+  const double l = wave_sum_d(ltot);
+  const unsigned wcnt = wave_sum_u(lcnt);
+  if (lane == 0) { sl[w] = l; sc[w] = wcnt - dpos; }
+  __syncthreads();
+  if (tid == 0) {
+    double tl = 0.0, tc = 0.0;
+    for (int k = 0; k < NW; ++k) { tl += sl[k]; tc += (double)sc[k]; }
+    if (rb == 0 && corr) tl -= (double)a.npad * a.npad - (double)a.n * a.n;
+    a.part[2 * blockIdx.x] = tl * (double)kLn2;
+    a.part[2 * blockIdx.x + 1] = tc;
+  }
+}
+
 // dJd += sum of the column-split partials (fixed order)
 __global__ void zzt_split_sum_kernel(float* dJd, const float* extra, long long n, int nextra) {
   long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1174,7 +1508,13 @@ int launch_zzt_dense(const ZztArgs& a, int dtype, hipStream_t s, bool defer_spli
   else hipLaunchKernelGGL((zzt_dense_bf16_v4<DPV, 2, 1, false>), grid, dim3(NTH2), 0, s, a);
     if (dp == 32) { SND_V4(32) } else { SND_V4(64) }
 #undef SND_V4
-  } else if (dtype == SND_BF16) {                     // v3: |x| formulation, 16x16x32 (d = 128)
+  } else if (dtype == SND_BF16 && dp == 128 && (a.variant & 255) != 3) {   // v7 (default, d = 128)
+    const bool stag = (a.variant & 255) != 17;   // 17: v7 without the wave stagger (A/B)
+    if (a.variant >= 256 && stag) hipLaunchKernelGGL((zzt_dense_bf16_v7<true, true>), grid, dim3(NTH2), 0, s, a);
+    else if (a.variant >= 256) hipLaunchKernelGGL((zzt_dense_bf16_v7<true, false>), grid, dim3(NTH2), 0, s, a);
+    else if (stag) hipLaunchKernelGGL((zzt_dense_bf16_v7<false, true>), grid, dim3(NTH2), 0, s, a);
+    else hipLaunchKernelGGL((zzt_dense_bf16_v7<false, false>), grid, dim3(NTH2), 0, s, a);
+  } else if (dtype == SND_BF16) {                     // v3: |x| formulation, 16x16x32 (A/B: variant 3)
     if (dp == 32) hipLaunchKernelGGL((zzt_dense_bf16_v3<32>), grid, dim3(NTH2), 0, s, a);
     else if (dp == 64) hipLaunchKernelGGL((zzt_dense_bf16_v3<64>), grid, dim3(NTH2), 0, s, a);
     else hipLaunchKernelGGL((zzt_dense_bf16_v3<128>), grid, dim3(NTH2), 0, s, a);

@@ -279,10 +279,12 @@ def test_zzt_ce_f32(n, d, B, kbar):
 
 
 @pytest.mark.parametrize("n,d,B,scale", [(300, 64, 2, 0.25), (128, 128, 2, 0.25), (300, 32, 3, 0.3),
-                                         (700, 64, 1, 0.25), (257, 64, 2, 1.0), (130, 16, 2, 0.5)])
+                                         (700, 64, 1, 0.25), (257, 64, 2, 1.0), (130, 16, 2, 0.5),
+                                         (700, 128, 1, 0.25), (257, 128, 2, 0.7), (1100, 128, 3, 0.2)])
 def test_zzt_ce_bf16(n, d, B, scale):
-    """bf16 zz^T + CE (v4 for d <= 64: 32x32x16 MFMA, select-free epilogue; v3 for d = 128).
-    (700, 64, 1): column splits; scale 1.0: logits up to |L| ~ 40."""
+    """bf16 zz^T + CE (v4 for d <= 64: 32x32x16 MFMA, select-free epilogue; v7 for d = 128:
+    one dual-use LDS image per tile, transposed reads for the backward operand).
+    (700, d, 1): column splits; scale 1.0: logits up to |L| ~ 40."""
     from snd_vae_amd import layers
     rp, ci, dense, z = _zzt_case(n, d, B, 10.0, 7, scale)
     ce, correct, dz = layers.inner_product_ce(cu(z), B, cu(rp, torch.int32), cu(ci, torch.int32),
@@ -293,11 +295,12 @@ def test_zzt_ce_bf16(n, d, B, scale):
     assert rel(dz.cpu().numpy(), rdz) < 2e-2
 
 
-def test_zzt_ce_bf16_extreme_logits():
-    """Planted blocks of logits far beyond the v4 quad-product range (L = -100 between
+@pytest.mark.parametrize("d", [64, 128])
+def test_zzt_ce_bf16_extreme_logits(d):
+    """Planted blocks of logits far beyond the v4/v7 quad-product range (L = -100 between
     rows 0-3 and 4-7, +100 inside each block): the overflow fallback keeps the CE exact."""
     from snd_vae_amd import layers
-    n, d, B = 200, 64, 2
+    n, B = 200, 2
     rp, ci, dense, z = _zzt_case(n, d, B, 8.0, 11, 0.25)
     a = np.zeros(d, np.float32)
     a[:4] = 5.0                                   # |a|^2 = 100
