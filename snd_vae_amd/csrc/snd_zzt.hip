@@ -1319,8 +1319,15 @@ __global__ void __launch_bounds__(NTH2) zzt_dense_bf16_v7(ZztArgs a) {
       lacc = 0.f;
     }
   };
-  if (STAG && (cb & 1)) run(std::true_type{});
-  else run(std::false_type{});
+  // static priority 1 for the late waves (MI355X guide, two waves per SIMD item 4):
+  // 324 vs 330 us at 2 graphs; priority 1 for the early waves instead 331
+  if (STAG && (cb & 1)) {
+    __builtin_amdgcn_s_setprio(1);
+    run(std::true_type{});
+    __builtin_amdgcn_s_setprio(0);
+  } else {
+    run(std::false_type{});
+  }
 
   // ---- per-row corrections (row i_me; lanes r and r + 32 hold its two k halves)
   float xd = 0.f, xs = 0.f;
