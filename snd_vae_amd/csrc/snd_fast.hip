@@ -106,34 +106,41 @@ __global__ void __launch_bounds__(RCT) rowconv_kernel(RcArgs a) {
   const int rb = w & 7, nb0 = NBH * (w >> 3);
   const int r0 = blockIdx.x * kRcRows;
   const int rend = min(r0 + kRcRows, a.R);
-  const int nbc = np >> 4;
+  // column window of this workgroup: image columns [nbase, nbase + nloc); LDS, colp and
+  // cps are indexed by the local column, global memory by nbase + local
+  const int nbase = blockIdx.y * a.npb;
+  const int nloc = min(a.npb, np - nbase);
+  const int nbc = nloc >> 4;
   const bool use_cp = NCP > 0 && a.colpart != nullptr && !(a.dbg & 64);
 
   // ---- packed weight image (LDS-DMA, 1 KB per wave instruction)
   if (!(a.dbg & 1)) {
-    const int npc = (T * np * kp) >> 9;
+    const int segc = (nloc * kp) >> 9, npc = T * segc;   // 1 KB pieces per tap, in all
     const char* g = reinterpret_cast<const char*>(a.wpk) + lane * 16;
-    for (int j = w; j < npc; j += RCT / 64) glds16(g + (j << 10), reinterpret_cast<char*>(ws) + (j << 10));
+    for (int j = w; j < npc; j += RCT / 64) {
+      const int t = j / segc, jj = j - t * segc;
+      glds16(g + ((long long)(t * np + nbase) * kp * 2) + (jj << 10), reinterpret_cast<char*>(ws) + (j << 10));
+    }
   }
   // ---- per-column parameters
-  if (tid < np) {
-    const int n = tid;
+  if (tid < nloc) {
+    const int nl = tid, n = nbase + tid;
     const bool cv = n < a.N && a.cols.valid(n) && !(a.dbg & 16);
     const bool pa = n < a.cols.a;
     const int ia = pa ? n : a.cols.logical(n), ib = n - a.cols.offb;
     auto par = [&](const float* A, const float* Bv) {
       return !cv || !A ? 0.f : (pa || !Bv ? A[ia] : Bv[ib]);
     };
-    colp[0][n] = par(a.bias, a.bias_b);
-    colp[1][n] = par(a.gamma, a.gamma_b) * kBnC;
-    colp[2][n] = par(a.beta, a.beta_b);
+    colp[0][nl] = par(a.bias, a.bias_b);
+    colp[1][nl] = par(a.gamma, a.gamma_b) * kBnC;
+    colp[2][nl] = par(a.beta, a.beta_b);
     if constexpr (EPI == RC_ENC1) {
-      colp[3][n] = (cv && n < a.h) ? a.g2[n] * kBnC : 0.f;
-      colp[4][n] = (cv && n < a.h) ? a.b2[n] : 0.f;
+      colp[3][nl] = (cv && n < a.h) ? a.g2[n] * kBnC : 0.f;
+      colp[4][nl] = (cv && n < a.h) ? a.b2[n] : 0.f;
     }
     if constexpr (EPI == RC_ENC0) {
 #pragma unroll
-      for (int k = 0; k < 4; ++k) colp[3 + k][n] = (cv && k < a.f) ? a.w0[k * a.N + n] : 0.f;
+      for (int k = 0; k < 4; ++k) colp[3 + k][nl] = (cv && k < a.f) ? a.w0[k * a.N + n] : 0.f;
     }
   }
 
@@ -143,7 +150,7 @@ __global__ void __launch_bounds__(RCT) rowconv_kernel(RcArgs a) {
     cvm[i] = 0u;
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      const int n = 16 * (nb0 + i) + 4 * lg + e;
+      const int n = nbase + 16 * (nb0 + i) + 4 * lg + e;
       if (nb0 + i < nbc && n < a.N && a.cols.valid(n)) cvm[i] |= 1u << e;
     }
   }
@@ -185,7 +192,7 @@ __global__ void __launch_bounds__(RCT) rowconv_kernel(RcArgs a) {
       if (rv && !(a.dbg & 32)) {
 #pragma unroll
         for (int i = 0; i < NBH; ++i) {
-          const int n0 = 16 * (nb0 + i) + 4 * lg;
+          const int n0 = nbase + 16 * (nb0 + i) + 4 * lg;
           if constexpr (EPI == RC_DECBWD) {
             const float* yp = a.y + (long long)r * a.ldy + n0;
             if (cvm[i] == 15u) ypf[i] = *reinterpret_cast<const f32x4*>(yp);
@@ -220,7 +227,7 @@ __global__ void __launch_bounds__(RCT) rowconv_kernel(RcArgs a) {
       const int xrow = 16 * rb + li + t;
       const __bf16* xrp = xs + xrow * kp;
       const int xsw = swz(xrow, kp);
-      const __bf16* wrp = ws + (t * np + li) * kp;
+      const __bf16* wrp = ws + (t * nloc + li) * kp;
       for (int ks = 0; ks < kcs; ++ks) {
         const int ch = 4 * ks + lg;
         const bf16x8 bx = *reinterpret_cast<const bf16x8*>(xrp + ((ch ^ xsw) << 3));
@@ -240,16 +247,16 @@ __global__ void __launch_bounds__(RCT) rowconv_kernel(RcArgs a) {
     for (int i = 0; i < NBH; ++i) {
       const int nb = nb0 + i;
       if (nb >= nbc || (a.dbg & 128)) continue;
-      const int n0 = 16 * nb + 4 * lg;
+      const int nl0 = 16 * nb + 4 * lg, n0 = nbase + nl0;
       const unsigned cm = rv ? cvm[i] : 0u;
       float o[4], qs[NCP > 0 ? NCP : 1][4];
 #pragma unroll
       for (int q = 0; q < (NCP > 0 ? NCP : 1); ++q)
 #pragma unroll
         for (int e = 0; e < 4; ++e) qs[q][e] = 0.f;
-      const float4 bia = *reinterpret_cast<const float4*>(&colp[0][n0]);
-      const float4 gam = *reinterpret_cast<const float4*>(&colp[1][n0]);
-      const float4 bet = *reinterpret_cast<const float4*>(&colp[2][n0]);
+      const float4 bia = *reinterpret_cast<const float4*>(&colp[0][nl0]);
+      const float4 gam = *reinterpret_cast<const float4*>(&colp[1][nl0]);
+      const float4 bet = *reinterpret_cast<const float4*>(&colp[2][nl0]);
       const float bi[4] = {bia.x, bia.y, bia.z, bia.w};
       const float ga[4] = {gam.x, gam.y, gam.z, gam.w};
       const float be[4] = {bet.x, bet.y, bet.z, bet.w};
@@ -280,13 +287,13 @@ __global__ void __launch_bounds__(RCT) rowconv_kernel(RcArgs a) {
       } else if constexpr (EPI == RC_ENC1) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          const int n = n0 + e;
+          const int n = n0 + e, nl = nl0 + e;
           const bool ok = cm >> e & 1u;
           const float dg = ok ? acc[i][e] : 0.f;
           const bool bpart = n < a.h;
           const float pv = ypf[i][e];
           const float a1 = lrelu(pv);
-          const float x2 = bpart ? a1 * colp[3][n] + colp[4][n] : pv;
+          const float x2 = bpart ? a1 * colp[3][nl] + colp[4][nl] : pv;
           qs[0][e] = dg * x2;
           qs[1][e] = dg;
           const float dh2 = dg * ga[e];
@@ -296,7 +303,7 @@ __global__ void __launch_bounds__(RCT) rowconv_kernel(RcArgs a) {
           if (bpart) {
             qs[2][e] = dh2 * a1;
             qs[3][e] = dh2;
-            o[e] = dh2 * colp[3][n] * lrelu_grad(pv);
+            o[e] = dh2 * colp[3][nl] * lrelu_grad(pv);
           } else {
             sm &= ~(1u << e);
           }
@@ -306,7 +313,7 @@ __global__ void __launch_bounds__(RCT) rowconv_kernel(RcArgs a) {
         for (int e = 0; e < 4; ++e) {
           float pv = 0.f;
 #pragma unroll
-          for (int k = 0; k < 4; ++k) pv += ax[k] * colp[3 + k][n0 + e];
+          for (int k = 0; k < 4; ++k) pv += ax[k] * colp[3 + k][nl0 + e];
           const float db = (cm >> e & 1u) ? acc[i][e] : 0.f;
           qs[0][e] = db * lrelu(pv);
           qs[1][e] = db;
@@ -340,7 +347,7 @@ __global__ void __launch_bounds__(RCT) rowconv_kernel(RcArgs a) {
 #pragma unroll
             for (int e = 0; e < 4; ++e) v[e] = row16_sum(qs[q][e]);
             if (li == 0) {
-              float4* cp = reinterpret_cast<float4*>(&cps[rb][q][n0]);
+              float4* cp = reinterpret_cast<float4*>(&cps[rb][q][nl0]);
               if (first) *cp = make_float4(v[0], v[1], v[2], v[3]);
               else { float4 o4 = *cp; o4.x += v[0]; o4.y += v[1]; o4.z += v[2]; o4.w += v[3]; *cp = o4; }
             }
@@ -354,12 +361,13 @@ __global__ void __launch_bounds__(RCT) rowconv_kernel(RcArgs a) {
   if constexpr (NCP > 0) {
     if (use_cp) {
       __syncthreads();
-      for (int i = tid; i < NCP * a.N; i += RCT) {
-        const int q = i / a.N, n = i - q * a.N;
+      for (int i = tid; i < NCP * nloc; i += RCT) {
+        const int q = i / nloc, nl = i - q * nloc, n = nbase + nl;
+        if (n >= a.N) continue;
         float t = 0.f;
 #pragma unroll
-        for (int b = 0; b < 8; ++b) t += cps[b][q][n];
-        a.colpart[(long long)blockIdx.x * NCP * a.N + i] = t;
+        for (int b = 0; b < 8; ++b) t += cps[b][q][nl];
+        a.colpart[((long long)blockIdx.x * NCP + q) * a.N + n] = t;
       }
     }
   }
@@ -723,9 +731,9 @@ __global__ void __launch_bounds__(NT) heads_fast_kernel(HeadFastPack pk, int R) 
 
 template <int EPI>
 int rc_launch_epi(const RcArgs& a, hipStream_t s) {
-  const size_t lds = rc_lds_bytes(a.T, a.kp, a.np);
-  const dim3 grid(rc_blocks(a.R)), block(RCT);
-  switch ((a.np / 16 + 1) / 2) {
+  const size_t lds = rc_lds_bytes(a.T, a.kp, a.npb);
+  const dim3 grid(rc_blocks(a.R), cdiv(a.np, a.npb)), block(RCT);
+  switch ((a.npb / 16 + 1) / 2) {
     case 1: hipLaunchKernelGGL((rowconv_kernel<EPI, 1>), grid, block, lds, s, a); break;
     case 2: hipLaunchKernelGGL((rowconv_kernel<EPI, 2>), grid, block, lds, s, a); break;
     case 3: hipLaunchKernelGGL((rowconv_kernel<EPI, 3>), grid, block, lds, s, a); break;
@@ -807,14 +815,24 @@ size_t rc_lds_bytes(int T, int kp, int np) {
   return (xch * 8 + (size_t)T * np * kp) * 2;
 }
 
-int launch_rowconv(const RcArgs& a, int epi, hipStream_t s) {
-  if (a.R <= 0) return 0;
+int rc_cols_per_block(int T, int kp, int np) {
+  for (int s = cdiv(np, 128); s <= 8; ++s) {
+    const int npb = (int)round_up(cdiv(np, s), 16);
+    if (npb <= 128 && rc_lds_bytes(T, kp, npb) <= kMaxDynLds) return npb;
+  }
+  return 0;
+}
+
+int launch_rowconv(const RcArgs& a0, int epi, hipStream_t s) {
+  if (a0.R <= 0) return 0;
+  RcArgs a = a0;
   SND_CHECK_ARG(a.T == 1 || a.T == 5, "rowconv: T must be 1 or 5");
   SND_CHECK_ARG(a.kp == 32 || a.kp == 64 || a.kp == 128, "rowconv: kp %d", a.kp);
-  SND_CHECK_ARG(a.np % 16 == 0 && a.np >= 16 && a.np <= 128, "rowconv: np %d", a.np);
+  SND_CHECK_ARG(a.np % 16 == 0 && a.np >= 16 && a.np <= 256, "rowconv: np %d", a.np);
   SND_CHECK_ARG(a.K <= a.kp && a.N <= a.np && a.N > 0, "rowconv: K %d / N %d exceed image", a.K, a.N);
   SND_CHECK_ARG(a.ldx % 8 == 0 && a.ldo % 4 == 0, "rowconv: ldx %% 8 / ldo %% 4");
-  SND_CHECK_ARG(rc_lds_bytes(a.T, a.kp, a.np) <= kMaxDynLds, "rowconv: LDS image too large");
+  a.npb = rc_cols_per_block(a.T, a.kp, a.np);
+  SND_CHECK_ARG(a.npb > 0, "rowconv: LDS image too large (T %d kp %d np %d)", a.T, a.kp, a.np);
   SND_CHECK_ARG(a.x && a.wpk && a.out && a.zero && a.x_bf16, "rowconv: null operand / fp32 x");
   SND_CHECK_ARG(!a.colpart || (a.ncp >= 1 && a.ncp <= 4), "rowconv: ncp");
   SND_CHECK_ARG(a.npg > 0, "rowconv: npg");

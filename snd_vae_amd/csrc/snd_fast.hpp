@@ -74,11 +74,17 @@ struct RcArgs {
   int h;                        // ENC1: h1
   const void* zero;             // >= 16 zero bytes in device memory (LDS-DMA fill source)
   int dbg;                      // measurement only: bits skip phases (see snd_debug_set)
+  int npb;                      // image columns per workgroup (set by launch_rowconv: np, or a
+                                // 16-multiple window when the whole image exceeds the LDS budget;
+                                // blockIdx.y selects the window)
 };
 constexpr int kRcRows = 128;    // rows per workgroup tile
 constexpr size_t kRcLdsLimit = 136 * 1024;   // dynamic LDS (static partials use the rest)
 int rc_blocks(int R);
 size_t rc_lds_bytes(int T, int kp, int np);
+// columns per workgroup for an image: np if it fits kRcLdsLimit, else the widest
+// 16-multiple window that does (0: none does)
+int rc_cols_per_block(int T, int kp, int np);
 int launch_rowconv(const RcArgs& a, int epi, hipStream_t s);
 
 // ---- weight-gradient engine ----------------------------------------------

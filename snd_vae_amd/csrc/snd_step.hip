@@ -330,8 +330,8 @@ extern "C" int snd_plan_create(const snd_config_t* cfg, int n_graphs, snd_plan_t
     Img ims[6] = {img(dj, w1), img(w1, w2), img(c.s2, c.s3), img(c.s3, c.s2), img(w2, w1), img(w1, dj)};
     bool ok = heads_fast_supported(c.s3, c.spatial_dim) && heads_fast_supported(c.n2, c.num_feature) &&
               w1 <= 128;
-    for (auto& m : ims)
-      ok = ok && m.kp > 0 && m.np <= 128 && rc_lds_bytes(m.T, m.kp, m.np) <= kRcLdsLimit;
+    for (auto& m : ims)   // images over the LDS budget run in column windows (rc_cols_per_block)
+      ok = ok && m.kp > 0 && m.np <= 128 && rc_cols_per_block(m.T, m.kp, m.np) > 0;
     if (ok) {
       p->fast = true;
       p->m1 = m1; p->m2 = m2;

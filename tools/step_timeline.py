@@ -20,7 +20,7 @@ def main(path):
         busy += e - s
         n = r["Kernel_Name"].replace("snd::(anonymous namespace)::", "").replace("_ZN3snd12_GLOBAL__N_1", "")
         print(f"{(s - t0) / 1e3:8.1f} {(e - s) / 1e3:7.2f}  grid {r['Grid_Size_X']:>7}x{r['Grid_Size_Y']:>3}"
-              f" lds {r['LDS_Block_Size']:>6} vgpr {r['VGPR_Count']:>3}/{r['Accum_VGPR_Count']:>3}  {n[:70]}")
+              f"x{r.get('Grid_Size_Z', '1'):>3} lds {r['LDS_Block_Size']:>6} vgpr {r['VGPR_Count']:>3}/{r['Accum_VGPR_Count']:>3}  {n[:70]}")
     end = int(rows[b - 1]["End_Timestamp"])
     print(f"step span {(end - t0) / 1e3:.1f} us, kernel busy {busy / 1e3:.1f} us, {b - a} launches")
 
