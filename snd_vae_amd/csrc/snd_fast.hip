@@ -35,7 +35,7 @@ typedef __attribute__((address_space(3))) v4s lds_v4s;
 // 16-byte chunk XOR of a [row][kp] bf16 image read by ds_read_b128 with lane
 // row = l & 15, chunk = 4 ks + (l >> 4) (conflict-free; as the zz^T images).
 __device__ __forceinline__ int swz(int row, int kp) {
-  return kp == 128 ? (row & 15) : (kp == 64 ? ((row >> 1) & 7) : 0);
+  return kp >= 128 ? (row & 15) : (kp == 64 ? ((row >> 1) & 7) : 0);
 }
 
 __device__ __forceinline__ uint4 pack8(float4 lo, float4 hi) {
@@ -96,7 +96,7 @@ __global__ void __launch_bounds__(RCT) rowconv_kernel(RcArgs a) {
   __shared__ float colp[8][128];   // bias, gamma*c, beta, g2*c | W0 rows, b2 per physical column
   constexpr int NCP = RcNcp<EPI>::v;
   const int T = a.T, H = (T - 1) >> 1, kp = a.kp, np = a.np;
-  const int lkc = kp == 128 ? 4 : (kp == 64 ? 3 : 2);   // log2(kp / 8)
+  const int lkc = kp == 256 ? 5 : (kp == 128 ? 4 : (kp == 64 ? 3 : 2));   // log2(kp / 8)
   const int XR = kRcRows + T - 1;
   const int xch = rc_xchunks(T, lkc);
   __bf16* xs = lds;
@@ -141,6 +141,10 @@ __global__ void __launch_bounds__(RCT) rowconv_kernel(RcArgs a) {
     if constexpr (EPI == RC_ENC0) {
 #pragma unroll
       for (int k = 0; k < 4; ++k) colp[3 + k][nl] = (cv && k < a.f) ? a.w0[k * a.N + n] : 0.f;
+    }
+    if constexpr (EPI == RC_LIN || EPI == RC_FWD) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) colp[3 + k][nl] = (cv && k < a.ktail) ? a.wtail[k * a.ldwt + n] : 0.f;
     }
   }
 
@@ -216,6 +220,13 @@ __global__ void __launch_bounds__(RCT) rowconv_kernel(RcArgs a) {
 #pragma unroll
         for (int k = 0; k < 4; ++k) if (k < a.f) ax[k] = a.p[(long long)r * a.ldp + k];
     }
+    if constexpr (EPI == RC_LIN || EPI == RC_FWD) {   // the x columns past the image
+      if (rv && a.ktail > 0) {
+        const __bf16* xt = reinterpret_cast<const __bf16*>(a.x) + (long long)r * a.ldx + a.K;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) if (k < a.ktail) ax[k] = (float)xt[k];
+      }
+    }
     __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): staging DMA landed
     __syncthreads();
 
@@ -258,6 +269,13 @@ __global__ void __launch_bounds__(RCT) rowconv_kernel(RcArgs a) {
       const float4 gam = *reinterpret_cast<const float4*>(&colp[1][nl0]);
       const float4 bet = *reinterpret_cast<const float4*>(&colp[2][nl0]);
       const float bi[4] = {bia.x, bia.y, bia.z, bia.w};
+      if constexpr (EPI == RC_LIN || EPI == RC_FWD) {
+        if (a.ktail > 0)
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+#pragma unroll
+            for (int k = 0; k < 4; ++k) acc[i][e] += ax[k] * colp[3 + k][nl0 + e];
+      }
       const float ga[4] = {gam.x, gam.y, gam.z, gam.w};
       const float be[4] = {bet.x, bet.y, bet.z, bet.w};
       unsigned sm = cm;    // columns stored
@@ -770,7 +788,7 @@ int launch_pack(const PackDesc* d, int n, hipStream_t s) {
   int maxch = 0;
   for (int i = 0; i < n; ++i) {
     const PackDesc& x = d[i];
-    if (!(x.kp == 32 || x.kp == 64 || x.kp == 128) || x.np % 16 || x.np <= 0 || x.T < 1 ||
+    if (!(x.kp == 32 || x.kp == 64 || x.kp == 128 || x.kp == 256) || x.np % 16 || x.np <= 0 || x.T < 1 ||
         x.nsrc < 1 || x.nsrc > 2) {
       set_error("pack: bad descriptor %d (kp %d np %d T %d)", i, x.kp, x.np, x.T);
       return SND_ERR_ARG;
@@ -827,7 +845,10 @@ int launch_rowconv(const RcArgs& a0, int epi, hipStream_t s) {
   if (a0.R <= 0) return 0;
   RcArgs a = a0;
   SND_CHECK_ARG(a.T == 1 || a.T == 5, "rowconv: T must be 1 or 5");
-  SND_CHECK_ARG(a.kp == 32 || a.kp == 64 || a.kp == 128, "rowconv: kp %d", a.kp);
+  SND_CHECK_ARG(a.kp == 32 || a.kp == 64 || a.kp == 128 || a.kp == 256, "rowconv: kp %d", a.kp);
+  SND_CHECK_ARG(a.ktail == 0 || ((epi == RC_LIN || epi == RC_FWD) && a.ktail <= 4 && a.wtail && a.ldwt >= a.N &&
+                                 a.cols.b == 0),
+                "rowconv: K tail needs RC_LIN / RC_FWD, <= 4 columns, a plain layout");
   SND_CHECK_ARG(a.np % 16 == 0 && a.np >= 16 && a.np <= 256, "rowconv: np %d", a.np);
   SND_CHECK_ARG(a.K <= a.kp && a.N <= a.np && a.N > 0, "rowconv: K %d / N %d exceed image", a.K, a.N);
   SND_CHECK_ARG(a.ldx % 8 == 0 && a.ldo % 4 == 0, "rowconv: ldx %% 8 / ldo %% 4");

@@ -74,6 +74,10 @@ struct RcArgs {
   int h;                        // ENC1: h1
   const void* zero;             // >= 16 zero bytes in device memory (LDS-DMA fill source)
   int dbg;                      // measurement only: bits skip phases (see snd_debug_set)
+  // RC_LIN / RC_FWD: x columns [K, K + ktail) (bf16, ktail <= 4) beyond the image enter in
+  // the epilogue: acc[r][n] += sum_j x[r][K + j] * wtail[j * ldwt + n] (a [B | X] input one
+  // feature column wider than 128)
+  int ktail; const float* wtail; int ldwt;
   int npb;                      // image columns per workgroup (set by launch_rowconv: np, or a
                                 // 16-multiple window when the whole image exceeds the LDS budget;
                                 // blockIdx.y selects the window)

@@ -8,7 +8,7 @@ namespace snd {
 // 16-byte chunk XOR of a [row][kp] bf16 image read by ds_read_b128 with lane
 // row = l & 15, chunk = 4 ks + (l >> 4) (conflict-free; as the zz^T images).
 __host__ __device__ __forceinline__ int img_swz(int row, int kp) {
-  return kp == 128 ? (row & 15) : (kp == 64 ? ((row >> 1) & 7) : 0);
+  return kp >= 128 ? (row & 15) : (kp == 64 ? ((row >> 1) & 7) : 0);
 }
 
 // physical chunk i of image d: dst[t][n][8 c .. 8 c + 7] = W values of logical chunk c ^ swz

@@ -99,6 +99,12 @@ struct snd_plan {
   Img pw1f{}, pwhf{}, pwmsf{}, pwmsb{}, pwhb{}, pw1b{};
   Img pidg{};                  // graph latent: identity [W -> W] (dG enters RC_ENC1 directly)
   WgGeom gWms{}, gWh{}, gW1{}, gW0{};
+  // wide encoders (d = 128, C5): H1 = [B0 | X] and G are h + f > 128 columns wide -- the
+  // images hold the first kw1 / kwh input rows, the f feature rows enter as the row
+  // engine's K tail and as separate tail weight gradients; [mu | logstd] (2L = 256) is
+  // differentiated in nms-column halves
+  int kw1 = 0, kwh = 0, nms = 0;
+  WgGeom gW1t{}, gWht{};
   // fused TF1 Adam (snd_plan_fuse_adam): Adam state of the blocks updated inside the step
   float* fuse_m = nullptr; float* fuse_v = nullptr;
   float fuse_lr = 0.f, fuse_b1 = 0.f, fuse_b2 = 0.f, fuse_eps = 0.f;
@@ -387,6 +393,7 @@ extern "C" int snd_plan_create(const snd_config_t* cfg, int n_graphs, snd_plan_t
       ok = ok && m.kp > 0 && m.np <= 128 && rc_lds_bytes(m.T, m.kp, m.np) <= kRcLdsLimit;
     if (ok) {
       p->fast_enc = true;
+      p->kw1 = h0 + f; p->kwh = W; p->nms = 2 * L;
       p->ldh1 = (int)round_up(h0 + f, 8);
       p->ldg = (int)round_up(W, 8);
       const char* nm[3] = {"PW1F", "PW1B", "PIDG"};
@@ -411,13 +418,16 @@ extern "C" int snd_plan_create(const snd_config_t* cfg, int n_graphs, snd_plan_t
   }
   // ---- bf16 fast encoder: GraphConvolution 0 as (A X) W0, bf16 operands throughout
   if (p->fast && !tref && !(debug_flags() & 512)) {
-    auto img1 = [&](int kin, int nout) { return Img{1, kp_of(kin), (int)round_up(nout, 16), 0}; };
-    Img ims[6] = {img1(h0 + f, h1), img1(W, gh), img1(gh, 2 * L), img1(2 * L, gh), img1(gh, W), img1(h1, h0)};
-    bool ok = h0 % 8 == 0 && h1 % 8 == 0 && h1 <= 128 && f <= 4 && W <= 128 && h0 + f <= 128 &&
-              gh <= 128 && 2 * L <= 128;
-    for (auto& m : ims)
-      ok = ok && m.kp > 0 && m.np <= 128 && rc_lds_bytes(m.T, m.kp, m.np) <= kRcLdsLimit;
+    auto img1 = [&](int kin, int nout) { return Img{1, kin <= 128 ? kp_of(kin) : (kin <= 256 ? 256 : -1),
+                                                    (int)round_up(nout, 16), 0}; };
+    const int kw1 = h0 + f <= 128 ? h0 + f : h0, kwh = W <= 128 ? W : h1;   // the rest: K tails
+    Img ims[6] = {img1(kw1, h1), img1(kwh, gh), img1(gh, 2 * L), img1(2 * L, gh), img1(gh, W), img1(h1, h0)};
+    bool ok = h0 % 8 == 0 && h1 % 8 == 0 && h1 <= 128 && f <= 4 && W == h1 + f && h0 <= 128 &&
+              gh <= 128 && 2 * L <= 256 && (2 * L <= 128 || L % 8 == 0) && ims[0].kp <= 128 && ims[1].kp <= 128;
+    for (auto& m : ims)   // images over the LDS budget run in column windows
+      ok = ok && m.kp > 0 && m.np <= 256 && rc_cols_per_block(m.T, m.kp, m.np) > 0;
     if (ok) {
+      p->kw1 = kw1; p->kwh = kwh; p->nms = 2 * L <= 128 ? 2 * L : L;
       p->fast_enc = true;
       p->ldh1 = (int)round_up(h0 + f, 8);
       p->ldg = (int)round_up(W, 8);
@@ -439,14 +449,23 @@ extern "C" int snd_plan_create(const snd_config_t* cfg, int n_graphs, snd_plan_t
       p->add_buf("PFBH", (long long)rcb * gh);
       p->add_buf("PFENC1", (long long)rcb * 4 * W);
       p->add_buf("PFENC0", (long long)rcb * 2 * h0);
-      p->gWms = wgrad_geom(p->R, 1, gh, 2 * L, wgc_of(1, gh, 2 * L));
-      p->gWh = wgrad_geom(p->R, 1, W, gh, wgc_of(1, W, gh));
-      p->gW1 = wgrad_geom(p->R, 1, h0 + f, h1, wgc_of(1, h0 + f, h1));
+      const int nms = p->nms;
+      p->gWms = wgrad_geom(p->R, 1, gh, nms, wgc_of(1, gh, nms));
+      p->gWh = wgrad_geom(p->R, 1, kwh, gh, wgc_of(1, kwh, gh));
+      p->gW1 = wgrad_geom(p->R, 1, kw1, h1, wgc_of(1, kw1, h1));
       p->gW0 = wgrad_geom(p->R, 1, f, h0, wgc_of(1, f, h0));
-      p->add_buf("FSWMS", (long long)p->gWms.gx * gh * wgrad_n4(2 * L));
-      p->add_buf("FSWH", (long long)p->gWh.gx * W * wgrad_n4(gh));
-      p->add_buf("FSW1", (long long)p->gW1.gx * (h0 + f) * wgrad_n4(h1));
+      p->add_buf("FSWMS", (long long)p->gWms.gx * gh * wgrad_n4(nms) * (2 * L / nms));
+      p->add_buf("FSWH", (long long)p->gWh.gx * kwh * wgrad_n4(gh));
+      p->add_buf("FSW1", (long long)p->gW1.gx * kw1 * wgrad_n4(h1));
       p->add_buf("FSW0", (long long)p->gW0.gx * f * wgrad_n4(h0));
+      if (kwh < W) {
+        p->gWht = wgrad_geom(p->R, 1, W - kwh, gh, wgc_of(1, W - kwh, gh));
+        p->add_buf("FSWHT", (long long)p->gWht.gx * (W - kwh) * wgrad_n4(gh));
+      }
+      if (kw1 < h0 + f) {
+        p->gW1t = wgrad_geom(p->R, 1, h0 + f - kw1, h1, wgc_of(1, h0 + f - kw1, h1));
+        p->add_buf("FSW1T", (long long)p->gW1t.gx * (h0 + f - kw1) * wgrad_n4(h1));
+      }
       // GraphConvolution 1 -> heads -> reparameterisation + zz^T staging in one launch
       // (debug bit 65536: the four-launch chain)
       p->head_fused = !(dbg & 65536) && zzt_dp(L) == L &&
@@ -867,8 +886,9 @@ int encoder_fast_fwd(const Ctx& x, const snd_batch_t* batch) {
     a.row_order = batch->row_order;
     SND_TRY(launch_gcn0(a, x.s));
   }
-  if (!p.front_fused) {
-    RcArgs a = rc_args(p, x.ws, p.pw1f, bf("FH1"), p.ldh1, h0 + f, h1, colmap_plain(h1));
+  if (!p.front_fused) {   // p.kw1 < h0 + f: the X columns as the K tail
+    RcArgs a = rc_args(p, x.ws, p.pw1f, bf("FH1"), p.ldh1, p.kw1, h1, colmap_plain(h1));
+    a.ktail = h0 + f - p.kw1; a.wtail = x.w("enc.W1") + (long long)p.kw1 * h1; a.ldwt = h1;
     a.out = bf("FXW1"); a.ldo = h1; a.out_bf16 = 1;
     SND_TRY(launch_rowconv(a, RC_LIN, x.s));
   }
@@ -882,7 +902,8 @@ int encoder_fast_fwd(const Ctx& x, const snd_batch_t* batch) {
   }
   if (p.tref) return 0;   // graph heads: snd_tref.hip on bf16 flat(G)
   {
-    RcArgs a = rc_args(p, x.ws, p.pwhf, bf("FG"), p.ldg, W, gh, colmap_plain(gh));
+    RcArgs a = rc_args(p, x.ws, p.pwhf, bf("FG"), p.ldg, p.kwh, gh, colmap_plain(gh));
+    a.ktail = W - p.kwh; a.wtail = x.w("enc.Wh") + (long long)p.kwh * gh; a.ldwt = gh;
     a.bias = x.w("enc.bh"); a.out = bf("FHH"); a.ldo = gh; a.out_bf16 = 1;
     SND_TRY(launch_rowconv(a, RC_LIN, x.s));
   }
@@ -954,14 +975,20 @@ int encoder_fast_bwd(const Ctx& x, const snd_batch_t* batch, float adj_scale, fl
     SND_TRY(launch_reparam_bwd_fast(a, x.s));
   }
   SND_TRY(fork(x));
-  SND_TRY(wgrad(x, wg_args(p, x.ws, p.gWms, bf("FHH"), gh, gh, bf("FDMS"), 2 * L, 2 * L, x.f("FSWMS"), 1), side(x)));
+  for (int h = 0; h < 2 * L; h += p.nms)   // [mu | logstd] in nms-column halves
+    SND_TRY(wgrad(x, wg_args(p, x.ws, p.gWms, bf("FHH"), gh, gh, bf("FDMS") + h, 2 * L, p.nms,
+                             x.f("FSWMS") + (long long)(h / p.nms) * p.gWms.gx * gh * wgrad_n4(p.nms), 1),
+                  side(x)));
   {
     RcArgs a = rc_args(p, x.ws, p.pwmsb, bf("FDMS"), 2 * L, 2 * L, gh, colmap_plain(gh));
     a.out = bf("FDH"); a.ldo = gh; a.out_bf16 = 1; a.colpart = x.f("PFBH"); a.ncp = 1;
     SND_TRY(launch_rowconv(a, RC_LIN, x.s));
   }
   SND_TRY(fork(x));
-  SND_TRY(wgrad(x, wg_args(p, x.ws, p.gWh, bf("FG"), p.ldg, W, bf("FDH"), gh, gh, x.f("FSWH"), 1), side(x)));
+  SND_TRY(wgrad(x, wg_args(p, x.ws, p.gWh, bf("FG"), p.ldg, p.kwh, bf("FDH"), gh, gh, x.f("FSWH"), 1), side(x)));
+  if (p.kwh < W)
+    SND_TRY(wgrad(x, wg_args(p, x.ws, p.gWht, bf("FG") + p.kwh, p.ldg, W - p.kwh, bf("FDH"), gh, gh,
+                             x.f("FSWHT"), 1), side(x)));
   return encoder_fast_bwd_tail(x, batch);
 }
 
@@ -983,7 +1010,10 @@ int encoder_fast_bwd_tail(const Ctx& x, const snd_batch_t* batch, bool enc1_done
   }
   SND_TRY(spmm_bf16_plain(batch, R, p.N, p.B, bf("FDP1"), h1, h1, bf("FDXW1"), h1, x.s));
   SND_TRY(fork(x));
-  SND_TRY(wgrad(x, wg_args(p, x.ws, p.gW1, bf("FH1"), p.ldh1, h0 + f, bf("FDXW1"), h1, h1, x.f("FSW1"), 1), side(x)));
+  SND_TRY(wgrad(x, wg_args(p, x.ws, p.gW1, bf("FH1"), p.ldh1, p.kw1, bf("FDXW1"), h1, h1, x.f("FSW1"), 1), side(x)));
+  if (p.kw1 < h0 + f)
+    SND_TRY(wgrad(x, wg_args(p, x.ws, p.gW1t, bf("FH1") + p.kw1, p.ldh1, h0 + f - p.kw1, bf("FDXW1"), h1, h1,
+                             x.f("FSW1T"), 1), side(x)));
   {
     RcArgs a = rc_args(p, x.ws, p.pw1b, bf("FDXW1"), h1, h1, h0, colmap_plain(h0));
     a.gamma = x.w("enc.bn0.gamma"); a.p = x.f("AX"); a.ldp = 4; a.w0 = x.w("enc.W0"); a.f = f;
@@ -1006,14 +1036,23 @@ void encoder_fast_reduce(const Ctx& x, std::vector<ReduceDesc>& rd) {
     const int n4 = wgrad_n4(N);
     rd.push_back({x.f(buf), x.g(dst), parts, N, (long long)rows * n4, 1.f, 0, rows, n4, N});
   };
+  // slab [parts][rows][n4] -> rows [rows][N] of a weight with row stride dst_rs, at dst
+  auto slab_at = [&](const float* src, int parts, int rows, int N, float* dst, long long dst_rs) {
+    const int n4 = wgrad_n4(N);
+    rd.push_back({src, dst, parts, N, (long long)rows * n4, 1.f, 0, rows, n4, dst_rs});
+  };
   if (!p.tref) {   // graph-latent heads are reduced by the generic path / written directly
-    slab2d("FSWMS", p.gWms.gx, gh, 2 * L, "enc.Wms");
+    for (int h = 0; h < 2 * L; h += p.nms)
+      slab_at(x.f("FSWMS") + (long long)(h / p.nms) * p.gWms.gx * gh * wgrad_n4(p.nms), p.gWms.gx, gh, p.nms,
+              x.g("enc.Wms") + h, 2 * L);
     if (p.head_bwd) flat("PHBMS", head_tiles(p.R), 2 * L, 2 * L, "enc.bms", 1.f);
     else flat("PFBMS", reparam_bwd_fast_blocks(p.R, L), 2 * L, 2 * L, "enc.bms", 1.f);
-    slab2d("FSWH", p.gWh.gx, W, gh, "enc.Wh");
+    slab2d("FSWH", p.gWh.gx, p.kwh, gh, "enc.Wh");
+    if (p.kwh < W) slab_at(x.f("FSWHT"), p.gWht.gx, W - p.kwh, gh, x.g("enc.Wh") + (long long)p.kwh * gh, gh);
     flat("PFBH", rcb, gh, gh, "enc.bh", 1.f);
   }
-  slab2d("FSW1", p.gW1.gx, h0 + f, h1, "enc.W1");
+  slab2d("FSW1", p.gW1.gx, p.kw1, h1, "enc.W1");
+  if (p.kw1 < h0 + f) slab_at(x.f("FSW1T"), p.gW1t.gx, h0 + f - p.kw1, h1, x.g("enc.W1") + (long long)p.kw1 * h1, h1);
   slab2d("FSW0", p.gW0.gx, f, h0, "enc.W0");
   const float* e1 = x.f("PFENC1");
   rd.push_back({e1, x.g("enc.bne.gamma"), rcb, W, 4LL * W, kBnC, 0, 0, 0, 0});

@@ -109,6 +109,30 @@ def test_c5_step_vs_chunked_oracle(dtype):
     check_step(opt, ref, rg, dtype, 16384 * 16384)
 
 
+def test_c5_wide_encoder_parts_vs_chunked_oracle():
+    """C5 runs the bf16 fast encoder with 129-wide H1 / G (the feature column as the row
+    engine's K tail and a separate tail weight gradient) and 256-wide [mu | logstd]
+    (two 128-column weight-gradient halves, a kp = 256 image for dH): each of those
+    pieces against the oracle on its own, so a dropped tail or half cannot hide under a
+    whole-block tolerance (`model.py:104-115`, `layers.py:566-576`)."""
+    cfg, batch, p0, eps, ref, rg = oracle_case(16384, 128, 1, 0)
+    model, opt = run_step(cfg, batch, p0, eps, "bf16")
+    g = opt.grad_blocks()
+    h0, h1, L = cfg.g_conv_hidden[0], cfg.g_conv_hidden[1], cfg.g_latent_size
+    parts = {"enc.W1 B0 rows": ("enc.W1", np.s_[:h0]), "enc.W1 X rows": ("enc.W1", np.s_[h0:]),
+             "enc.Wh B1 rows": ("enc.Wh", np.s_[:h1]), "enc.Wh X rows": ("enc.Wh", np.s_[h1:]),
+             "enc.Wms mu": ("enc.Wms", np.s_[:, :L]), "enc.Wms logstd": ("enc.Wms", np.s_[:, L:]),
+             "enc.bms mu": ("enc.bms", np.s_[:L]), "enc.bms logstd": ("enc.bms", np.s_[L:])}
+    bad = {}
+    for nm, (k, sl) in parts.items():
+        a, r = np.asarray(g[k])[sl], np.asarray(rg[k])[sl]
+        assert np.abs(r).max() > 0, nm
+        e = block_err(a, r)
+        if e > 1e-1:
+            bad[nm] = e
+    assert not bad, bad
+
+
 @pytest.mark.timeout(300)
 @pytest.mark.parametrize("dtype,scale", [("f32", 0.1), ("bf16", 0.1), ("bf16", 0.4)])
 def test_c5_zzt_ce_vs_chunked_oracle(dtype, scale):
