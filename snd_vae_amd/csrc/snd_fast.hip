@@ -854,6 +854,13 @@ int launch_rowconv(const RcArgs& a0, int epi, hipStream_t s) {
   SND_CHECK_ARG(a.ldx % 8 == 0 && a.ldo % 4 == 0, "rowconv: ldx %% 8 / ldo %% 4");
   a.npb = rc_cols_per_block(a.T, a.kp, a.np);
   SND_CHECK_ARG(a.npb > 0, "rowconv: LDS image too large (T %d kp %d np %d)", a.T, a.kp, a.np);
+  // fill the chip: under 256 row tiles (R < 32768, e.g. C5's one graph) the column
+  // windows split further, down to 32 columns (debug bit 1 << 19: off)
+  for (;;) {
+    const int nb = (int)round_up(cdiv(a.npb, 2), 16);
+    if ((a.dbg & (1 << 19)) || rc_blocks(a.R) * cdiv(a.np, a.npb) >= 256 || nb < 32 || nb >= a.npb) break;
+    a.npb = nb;
+  }
   SND_CHECK_ARG(a.x && a.wpk && a.out && a.zero && a.x_bf16, "rowconv: null operand / fp32 x");
   SND_CHECK_ARG(!a.colpart || (a.ncp >= 1 && a.ncp <= 4), "rowconv: ncp");
   SND_CHECK_ARG(a.npg > 0, "rowconv: npg");

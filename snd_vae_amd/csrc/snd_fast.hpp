@@ -181,6 +181,8 @@ struct ReparamBwdFastArgs {
   float adj_scale, kl_scale;
   __bf16* dms; int lddms;
   float* colpart;             // [blocks][2L]
+  // zz^T column-split partials [nextra][R][L] added to dJd here (launch_zzt_dense defer_split)
+  const float* dJd_extra = nullptr; int nextra = 0;
 };
 int reparam_bwd_fast_blocks(int R, int L);
 

@@ -545,7 +545,11 @@ __global__ void __launch_bounds__(NT) reparam_bwd_fast_kernel(ReparamBwdFastArgs
     const float4 mu = *reinterpret_cast<const float4*>(a.ms + (long long)r * a.ldms + 4 * c4);
     const float4 ls = *reinterpret_cast<const float4*>(a.ms + (long long)r * a.ldms + a.L + 4 * c4);
     const float4 ep = *reinterpret_cast<const float4*>(a.eps + i);
-    const float4 dj = *reinterpret_cast<const float4*>(a.dJd + i);
+    float4 dj = *reinterpret_cast<const float4*>(a.dJd + i);
+    for (int sx = 0; sx < a.nextra; ++sx) {   // zzt_split_sum_kernel's order
+      const float4 e = *reinterpret_cast<const float4*>(a.dJd_extra + (long long)sx * a.R * a.L + i);
+      dj.x += e.x; dj.y += e.y; dj.z += e.z; dj.w += e.w;
+    }
     const float4 ej = *reinterpret_cast<const float4*>(a.ej + i);
     const float4 dd = *reinterpret_cast<const float4*>(a.dz_dec + i);
     const float m[4] = {mu.x, mu.y, mu.z, mu.w}, l[4] = {ls.x, ls.y, ls.z, ls.w};

@@ -323,7 +323,9 @@ extern "C" int snd_plan_create(const snd_config_t* cfg, int n_graphs, snd_plan_t
   // 64 chunks measured best at C2 (32: 35.0 vs 28.8 us; 128: step 0.260 vs 0.252 ms).
   // A one-round geometry (~256 workgroups split over the segments by staged bytes) ran
   // slower, 43 vs 29 us at C2: a workgroup's 128-row units are one DMA round trip each.
-  const int wgc = (dbg & (4096 | 8192)) ? 0 : ((dbg & 16384) ? 32 : 64);
+  // Under 32768 rows (C5's one N = 16384 graph) 32 chunks: half the slab bytes for the
+  // reduction, still >= 384 workgroups (C5 step 0.417 vs 0.403 ms).
+  const int wgc = (dbg & (4096 | 8192)) ? 0 : (((dbg & 16384) || R < 32768) ? 32 : 64);
   auto wgc_of = [&](int, int, int) { return wgc; };
   // ---- bf16 fast decoder: split [s | n] column layouts, packed weight images
   if (c.dtype == SND_BF16 && !sg && !(debug_flags() & 256)) {
@@ -972,6 +974,7 @@ int encoder_fast_bwd(const Ctx& x, const snd_batch_t* batch, float adj_scale, fl
   {
     ReparamBwdFastArgs a{x.f("MS"), 2 * L, R, L, x.f("EPS"), x.f("DZDEC"), x.f("DJD"), x.f("EJ"),
                          adj_scale, kl_scale, bf("FDMS"), 2 * L, x.f("PFBMS")};
+    a.dJd_extra = x.f("DJDX"); a.nextra = zzt_tsplit(p.B, p.N, c.dtype) - 1;   // deferred split sum
     SND_TRY(launch_reparam_bwd_fast(a, x.s));
   }
   SND_TRY(fork(x));
@@ -1535,7 +1538,8 @@ extern "C" int snd_train_step(const snd_plan_t* plan, const snd_batch_t* batch,
     ZztArgs za{stg.jrow, stg.jt, N, zzt_npad(N), p.B, dj, x.f("DJD"), x.d("PZZT"), stg.colpart, 0,
                x.f("DJDX")};
     // the fused head backward adds the column-split partials itself (one launch fewer)
-    SND_TRY(launch_zzt_dense(za, c.dtype, x.s, p.fast_enc && !p.tref && p.head_bwd));
+    // the column-split sum is folded into head_bwd / reparam_bwd_fast (node latent, fast encoder)
+    SND_TRY(launch_zzt_dense(za, c.dtype, x.s, p.fast_enc && !p.tref));
   }
   if (p.fast) {
     SND_TRY(decoder_fast(x, batch));

@@ -18,13 +18,16 @@ def main():
     ap.add_argument("--flags", default="0")
     ap.add_argument("--kernels", default="zzt_dense")
     ap.add_argument("--graphs", default="8", help="graphs per GPU, comma list")
+    ap.add_argument("--config", default="", help="preset (C5, ...) instead of tscale(4096, 64)")
     ns = ap.parse_args()
     args = argparse.Namespace(steps=50, warmup=10, no_graph=False, dtype="bf16", no_tiles=False)
     info = init_from_env("nccl")
     for B in [int(x) for x in ns.graphs.split(",")]:
         for f in [int(x) for x in ns.flags.split(",")]:
             _lib.check(_lib.lib().snd_debug_set(f))
-            v, ms, model, opt, db, host = bench.run_workload(tscale(4096, 64), B, args, info)
+            from snd_vae_amd.config import PRESETS
+            cfg = PRESETS[ns.config] if ns.config else tscale(4096, 64)
+            v, ms, model, opt, db, host = bench.run_workload(cfg, B, args, info)
             kms = bench.kernel_timer(model, db.c_struct(), 20)
             ks = {k: round(kms(k), 5) for k in ns.kernels.split(",") if k}
             _lib.check(_lib.lib().snd_debug_set(0))
