@@ -1537,7 +1537,6 @@ extern "C" int snd_train_step(const snd_plan_t* plan, const snd_batch_t* batch,
     if (!p.fast) SND_TRY(launch_zzt_prep(x.f("Z"), p.B, N, dj, c.dtype, stg, x.s));
     ZztArgs za{stg.jrow, stg.jt, N, zzt_npad(N), p.B, dj, x.f("DJD"), x.d("PZZT"), stg.colpart, 0,
                x.f("DJDX")};
-    // the fused head backward adds the column-split partials itself (one launch fewer)
     // the column-split sum is folded into head_bwd / reparam_bwd_fast (node latent, fast encoder)
     SND_TRY(launch_zzt_dense(za, c.dtype, x.s, p.fast_enc && !p.tref));
   }
