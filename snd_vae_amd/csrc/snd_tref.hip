@@ -49,23 +49,34 @@ __device__ __forceinline__ float g_at(const A& a, int b, long long k) {
   return a.g[(long long)b * a.K + k];
 }
 
+__device__ __forceinline__ float4 ld_nt(const float* p) {
+  const f32x4 v = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p));
+  return make_float4(v[0], v[1], v[2], v[3]);
+}
+__device__ __forceinline__ void st_nt(float* p, const float4& x) {
+  const f32x4 v = {x.x, x.y, x.z, x.w};
+  __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(p));
+}
+
 // fused TF1 Adam on 4 consecutive elements; g is the (complete) gradient
 __device__ __forceinline__ float adam_lrt(const AdamFuse& f) {
   const int t = *f.step + 1;
   return (float)((double)f.lr * sqrt(1.0 - pow((double)f.b2, t)) / (1.0 - pow((double)f.b1, t)));
 }
+// m, v, p: the moments and parameters as already loaded (issued with the weight loads,
+// so a row's update does not wait a memory round trip of its own)
 __device__ __forceinline__ void adam4(const AdamFuse& f, float lrt, long long i, const float4& g,
-                                      float4 p) {   // p: the parameters as already loaded
-  float4 m = *reinterpret_cast<const float4*>(f.m + i), v = *reinterpret_cast<const float4*>(f.v + i);
+                                      float4 p, float4 m, float4 v) {
 #define SND_ADAM_C(c)                                        \
   m.c = f.b1 * m.c + (1.f - f.b1) * g.c;                     \
   v.c = f.b2 * v.c + (1.f - f.b2) * g.c * g.c;               \
   p.c -= lrt * m.c / (sqrtf(v.c) + f.eps);
   SND_ADAM_C(x) SND_ADAM_C(y) SND_ADAM_C(z) SND_ADAM_C(w)
 #undef SND_ADAM_C
-  *reinterpret_cast<float4*>(f.m + i) = m;
-  *reinterpret_cast<float4*>(f.v + i) = v;
-  *reinterpret_cast<float4*>(f.p + i) = p;
+  // streamed once per step: non-temporal stores (no L2 / Infinity Cache allocation)
+  st_nt(f.m + i, m);
+  st_nt(f.v + i, v);
+  st_nt(f.p + i, p);
 }
 
 // ------------------------------------------------------------------ head fwd
@@ -171,12 +182,18 @@ __global__ void __launch_bounds__(HB_T) tref_head_bwd_kernel(TrefHeadBwdArgs a) 
   constexpr int U = 4;                   // row pairs in flight per wave
   const int r0 = 2 * wv + h;             // row slot of this lane; 8 rows per block pass
   for (int base = 0; base < nk; base += 8 * U) {
-    float4 w[U];
+    float4 w[U], am[U], av[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int kk = base + 8 * u + r0;
-      w[u] = (qa && kk < nk) ? *reinterpret_cast<const float4*>(a.wh + (k0 + kk) * a.gh + 4 * q)
-                             : f4(0.f);
+      const bool ld = qa && kk < nk;
+      const long long i = (k0 + (ld ? kk : 0)) * a.gh + 4 * q;
+      w[u] = ld ? ld_nt(a.wh + i) : f4(0.f);
+      am[u] = av[u] = f4(0.f);
+      if (fused && ld) {
+        am[u] = ld_nt(a.adam.m + i);
+        av[u] = ld_nt(a.adam.v + i);
+      }
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -190,7 +207,7 @@ __global__ void __launch_bounds__(HB_T) tref_head_bwd_kernel(TrefHeadBwdArgs a) 
 #pragma unroll
       for (int b = 0; b < B8; ++b) fma4(dw, gb[b], dh[b]);
       if (qa && rv) {
-        if (fused) adam4(a.adam, lrt, (k0 + kk) * a.gh + 4 * q, dw, w[u]);
+        if (fused) adam4(a.adam, lrt, (k0 + kk) * a.gh + 4 * q, dw, w[u], am[u], av[u]);
         else *reinterpret_cast<float4*>(a.dwh + (k0 + kk) * a.gh + 4 * q) = dw;
       }
       float p[B8];
@@ -328,11 +345,18 @@ __global__ void __launch_bounds__(PB_T) tref_proj_bwd_kernel(TrefProjBwdArgs a) 
   const float lrt = fused ? adam_lrt(a.adam) : 0.f;
   constexpr int U = 5;
   for (int l0 = wv; l0 < a.L; l0 += PB_W * U) {
-    float4 w[U];
+    float4 w[U], am[U], av[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int l = l0 + PB_W * u;
-      w[u] = (cv && l < a.L) ? *reinterpret_cast<const float4*>(a.wp + (long long)l * a.Cp + c4) : f4(0.f);
+      const bool ld = cv && l < a.L;
+      const long long i = (long long)(ld ? l : 0) * a.Cp + (cv ? c4 : 0);
+      w[u] = ld ? ld_nt(a.wp + i) : f4(0.f);
+      am[u] = av[u] = f4(0.f);
+      if (fused && ld) {
+        am[u] = ld_nt(a.adam.m + i);
+        av[u] = ld_nt(a.adam.v + i);
+      }
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -344,7 +368,7 @@ __global__ void __launch_bounds__(PB_T) tref_proj_bwd_kernel(TrefProjBwdArgs a) 
       fma4(dw, z0.x, d[0]); fma4(dw, z0.y, d[1]); fma4(dw, z0.z, d[2]); fma4(dw, z0.w, d[3]);
       fma4(dw, z1.x, d[4]); fma4(dw, z1.y, d[5]); fma4(dw, z1.z, d[6]); fma4(dw, z1.w, d[7]);
       if (cv) {
-        if (fused) adam4(a.adam, lrt, (long long)l * a.Cp + c4, dw, w[u]);
+        if (fused) adam4(a.adam, lrt, (long long)l * a.Cp + c4, dw, w[u], am[u], av[u]);
         else *reinterpret_cast<float4*>(a.dwp + (long long)l * a.Cp + c4) = dw;
       }
 #pragma unroll

@@ -21,6 +21,7 @@ def main():
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--tag", default=os.environ.get("SND_LIB_PATH", "default"))
+    ap.add_argument("--config", default="", help="preset (C4, C5, ...) instead of --nodes/--latent")
     args = ap.parse_args()
     import torch
 
@@ -30,7 +31,8 @@ def main():
     from snd_vae_amd.data import synthetic_batch
     from snd_vae_amd.model import DeviceBatch, SGCNModelVAE
     from snd_vae_amd.optimizer import OptimizerVAE
-    cfg = tscale(args.nodes, args.latent)
+    from snd_vae_amd.config import PRESETS
+    cfg = PRESETS[args.config] if args.config else tscale(args.nodes, args.latent)
     db = DeviceBatch(synthetic_batch(cfg, args.graphs, seed=1000))
     model = SGCNModelVAE(cfg, args.graphs, dtype="bf16")
     opt = OptimizerVAE(model)
