@@ -872,14 +872,12 @@ __global__ void __launch_bounds__(NTH2) zzt_dense_bf16_v4(ZztArgs a) {
       for (int p = 0; p < 4; ++p)   // one log2 per 4 logits (an overflowing product: fallback below)
         lt += __builtin_amdgcn_logf((q[4 * p] * q[4 * p + 1]) * (q[4 * p + 2] * q[4 * p + 3]));
       if (__builtin_expect(!__builtin_isfinite(lt), 0)) {
-        // a quad product overflowed: this lane's block again in the |x| form,
-        // log2(q) = max(-x, 0) - c + log2(1 + 2^-|x|) per logit (exact for every x)
+        // a quad product overflowed: this lane's block again one logit at a time,
+        // log2(q) = y for y > 24 (1 + 2^y rounds to 2^y; q may be inf), else log2(q)
+        // (one transcendental per logit on the q already computed; c = 0)
         lt = 0.f;
 #pragma unroll
-        for (int v = 0; v < 16; ++v) {
-          const float xn = Y[v] + kZ4C;   // -x
-          lt += fmaxf(xn, 0.f) - kZ4C + __builtin_amdgcn_logf(1.f + __builtin_amdgcn_exp2f(-fabsf(xn)));
-        }
+        for (int v = 0; v < 16; ++v) lt += Y[v] > 24.f ? Y[v] : __builtin_amdgcn_logf(q[v]);
       }
       lacc += lt + 16.f * kZ4C;   // + c per logit: the sum stays small in fp32
     } else {   // v3's |x| form: sigma = x > 0 ? r : e r, one log2 per 8 logits
@@ -1239,12 +1237,9 @@ __global__ void __launch_bounds__(NTH2) zzt_dense_bf16_v7(ZztArgs a) {
     for (int p = 0; p < 4; ++p)
       lt += __builtin_amdgcn_logf((q[4 * p] * q[4 * p + 1]) * (q[4 * p + 2] * q[4 * p + 3]));
     if (__builtin_expect(!__builtin_isfinite(lt), 0)) {   // a quad product overflowed
-      lt = 0.f;
+      lt = 0.f;   // log2(q) per logit: y past 24 exactly, else log2 of the q already computed
 #pragma unroll
-      for (int v = 0; v < 16; ++v) {
-        const float xn = Y[v];
-        lt += fmaxf(xn, 0.f) + __builtin_amdgcn_logf(1.f + __builtin_amdgcn_exp2f(-fabsf(xn)));
-      }
+      for (int v = 0; v < 16; ++v) lt += Y[v] > 24.f ? Y[v] : __builtin_amdgcn_logf(q[v]);
     }
     lacc += lt;
   };
