@@ -265,6 +265,9 @@ __global__ void __launch_bounds__(256) enc_bwd_kernel(EncBwdArgs a, int rows) {
 }
 
 // ---------------------------------------------------------------- reduce
+#ifndef SND_RED_PL
+#define SND_RED_PL 16   // part lanes of a >= 64-part slab (A/B builds: -DSND_RED_PL=4 / 8)
+#endif
 struct ReducePack {
   ReduceDesc d[kMaxReduce];
   int bstart[kMaxReduce + 1];   // first block of each descriptor (flattened 1-D grid)
@@ -286,7 +289,7 @@ __global__ void __launch_bounds__(256) reduce_kernel(ReducePack pk, FinalizeArgs
   __shared__ double red[256];
   const int rows = d.rows > 0 ? d.rows : 1;
   const long long items = (long long)rows * d.len;
-  const int PL = d.nparts >= 64 ? 16 : 4;        // part lanes
+  const int PL = d.nparts >= 64 ? SND_RED_PL : 4;   // part lanes
   const int IPB = 256 / PL;                      // items per block
   const int it = threadIdx.x % IPB, pl = threadIdx.x / IPB;
   const long long j = (long long)bx * IPB + it;
@@ -466,7 +469,7 @@ int launch_reduce(const ReduceDesc* d, int n, hipStream_t s, const FinalizeArgs*
       if (i < cnt) {
         pk.d[i] = d[base + i];
         const long long items = (long long)(pk.d[i].rows > 0 ? pk.d[i].rows : 1) * pk.d[i].len;
-        const int ipb = pk.d[i].nparts >= 64 ? 16 : 64;
+        const int ipb = pk.d[i].nparts >= 64 ? 256 / SND_RED_PL : 64;
         nb += (items + ipb - 1) / ipb;
       }
     }
