@@ -266,7 +266,7 @@ __global__ void __launch_bounds__(256) enc_bwd_kernel(EncBwdArgs a, int rows) {
 
 // ---------------------------------------------------------------- reduce
 #ifndef SND_RED_PL
-#define SND_RED_PL 16   // part lanes of a >= 64-part slab (A/B builds: -DSND_RED_PL=4 / 8)
+#define SND_RED_PL 8   // part lanes of a >= 64-part slab (C2 step 0.2368 vs 0.2389 ms at 16, 0.2380 at 4)
 #endif
 struct ReducePack {
   ReduceDesc d[kMaxReduce];
