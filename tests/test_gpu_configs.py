@@ -109,6 +109,47 @@ def test_c5_step_vs_chunked_oracle(dtype):
     check_step(opt, ref, rg, dtype, 16384 * 16384)
 
 
+WIDE_PARTS = lambda h0, h1, L: {
+    "enc.W1 B0 rows": ("enc.W1", np.s_[:h0]), "enc.W1 X rows": ("enc.W1", np.s_[h0:]),
+    "enc.Wh B1 rows": ("enc.Wh", np.s_[:h1]), "enc.Wh X rows": ("enc.Wh", np.s_[h1:]),
+    "enc.Wms mu": ("enc.Wms", np.s_[:, :L]), "enc.Wms logstd": ("enc.Wms", np.s_[:, L:]),
+    "enc.bms mu": ("enc.bms", np.s_[:L]), "enc.bms logstd": ("enc.bms", np.s_[L:])}
+
+
+@pytest.mark.parametrize("n,B", [(512, 2), (384, 1)])
+def test_wide_fast_path_small_vs_oracle(n, B):
+    """The d = 128 fast path (C5's widths: row-engine column windows, K tails, kp = 256
+    images, Wms halves, occupancy windows under 256 row tiles) at small N against the
+    float64 oracle: the whole step and each wide piece on its own."""
+    from snd_vae_amd import _lib
+    from snd_vae_amd.model import c_config
+    import ctypes
+    cfg, batch, p0, eps, ref, rg = oracle_case(n, 128, B, 40 + n)
+    h = ctypes.c_void_p()   # the plan takes the fast encoder and decoder at these widths
+    _lib.check(_lib.lib().snd_plan_create(ctypes.byref(c_config(cfg, "bf16")), B, ctypes.byref(h)))
+    off, cnt = ctypes.c_longlong(), ctypes.c_longlong()
+    have = {nm: _lib.lib().snd_plan_buffer(h, nm.encode(), ctypes.byref(off), ctypes.byref(cnt)) == 0
+            for nm in ("FY1", "FH1", "FSW1T", "FSWHT")}
+    _lib.lib().snd_plan_destroy(h)
+    assert all(have.values()), have
+    _, opt = run_step(cfg, batch, p0, eps, "bf16")
+    got = opt.loss_dict()
+    for k in TERMS:
+        assert got[k] == pytest.approx(ref[k], rel=2e-2), (k, got[k], ref[k])
+    g = opt.grad_blocks()
+    # every block within 0.15 of max-abs: at N <= 512 the decoder's conv weight gradients
+    # sum few rows and carry ~10 % bf16 noise on any engine (dec.K2s 0.1006 here, 0.1003 on
+    # the generic bf16 engine, debug bit 256; 0.048 at N = 4096: tools/wide_check.py)
+    loose = {k: block_err(g[k], rg[k]) for k in rg if block_err(g[k], rg[k]) > 0.15}
+    assert not loose, loose
+    bad = {}
+    for nm, (k, sl) in WIDE_PARTS(cfg.g_conv_hidden[0], cfg.g_conv_hidden[1], cfg.g_latent_size).items():
+        e = block_err(np.asarray(g[k])[sl], np.asarray(rg[k])[sl])
+        if e > 1e-1:
+            bad[nm] = e
+    assert not bad, bad
+
+
 def test_c5_wide_encoder_parts_vs_chunked_oracle():
     """C5 runs the bf16 fast encoder with 129-wide H1 / G (the feature column as the row
     engine's K tail and a separate tail weight gradient) and 256-wide [mu | logstd]
@@ -118,13 +159,8 @@ def test_c5_wide_encoder_parts_vs_chunked_oracle():
     cfg, batch, p0, eps, ref, rg = oracle_case(16384, 128, 1, 0)
     model, opt = run_step(cfg, batch, p0, eps, "bf16")
     g = opt.grad_blocks()
-    h0, h1, L = cfg.g_conv_hidden[0], cfg.g_conv_hidden[1], cfg.g_latent_size
-    parts = {"enc.W1 B0 rows": ("enc.W1", np.s_[:h0]), "enc.W1 X rows": ("enc.W1", np.s_[h0:]),
-             "enc.Wh B1 rows": ("enc.Wh", np.s_[:h1]), "enc.Wh X rows": ("enc.Wh", np.s_[h1:]),
-             "enc.Wms mu": ("enc.Wms", np.s_[:, :L]), "enc.Wms logstd": ("enc.Wms", np.s_[:, L:]),
-             "enc.bms mu": ("enc.bms", np.s_[:L]), "enc.bms logstd": ("enc.bms", np.s_[L:])}
     bad = {}
-    for nm, (k, sl) in parts.items():
+    for nm, (k, sl) in WIDE_PARTS(cfg.g_conv_hidden[0], cfg.g_conv_hidden[1], cfg.g_latent_size).items():
         a, r = np.asarray(g[k])[sl], np.asarray(rg[k])[sl]
         assert np.abs(r).max() > 0, nm
         e = block_err(a, r)
