@@ -81,7 +81,8 @@ struct WinArgs {
   int ldo;
   int n, spg, seg, beta8;
   int dbg;   // measurement only (snd_debug_set >> 24): 1 no sums, 2 no window DMA, 4 no slot DMA,
-             // 32 two barriers per step at any beta
+             // 8 non-temporal output stores, 16 non-temporal window DMA, 32 two barriers
+             // per step at any beta
 };
 
 // fp32 sums without unpacking: v_dot2c_f32_bf16 with (1, 0) / (0, 1) adds the low /
@@ -120,10 +121,14 @@ constexpr int vmcnt_imm(int n) { return (n & 15) | (7 << 4) | (15 << 8) | ((n >>
 
 // global -> LDS DMA of `bytes` (4 or 16) per active lane to the wave-uniform LDS
 // address `dst` + 4/16 x lane (the compiler does not see it: vmcnt counted by hand)
-template <int BYTES>
+template <int BYTES, bool NT = false>
 __device__ __forceinline__ void glds(const void* src, unsigned dst) {
   unsigned keep;
-  if constexpr (BYTES == 16)
+  if constexpr (BYTES == 16 && NT)   // streamed once: non-temporal
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+                 "global_load_lds_dwordx4 %1, off nt\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(src), "s"(dst) : "memory");
+  else if constexpr (BYTES == 16)
     asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
                  "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
                  : "=&s"(keep) : "v"(src), "s"(dst) : "memory");
@@ -181,7 +186,12 @@ __global__ void __launch_bounds__(WT) spmm_win_kernel(WinArgs a) {
   // e: one 8-row piece of the window (row ids from index(s))
   auto dma_piece = [&](int p0, int row) {
     const __bf16* src = a.h + (long long)row * a.ldh + 8 * l8;
-    glds<16>(src, __builtin_amdgcn_readfirstlane(lds0 + (p0 % RR) * (WIDTH * 2)));
+    const unsigned dst = __builtin_amdgcn_readfirstlane(lds0 + (p0 % RR) * (WIDTH * 2));
+    // A/B (debug 16): non-temporal window DMA.  Within noise on the 256-graph batch
+    // (77-82 us either way), 1.5-4 us slower in the C2 step, where h was just written
+    // and still sits in L2 / the Infinity Cache: allocating loads stay the default
+    if (a.dbg & 16) glds<16, true>(src, dst);
+    else glds<16>(src, dst);
   };
   auto lds_i32 = [&](int off) { return *reinterpret_cast<const int*>(lds + off); };
 
@@ -274,7 +284,14 @@ __global__ void __launch_bounds__(WT) spmm_win_kernel(WinArgs a) {
       bf16x8 o;
   #pragma unroll
       for (int j = 0; j < 8; ++j) o[j] = (__bf16)f[j];
-      *reinterpret_cast<bf16x8*>(a.out + (long long)row0 * a.ldo + 8 * l8) = o;    }
+      __bf16* op = a.out + (long long)row0 * a.ldo + 8 * l8;
+      if (!(a.dbg & 8)) {
+        *reinterpret_cast<bf16x8*>(op) = o;
+      } else {   // A/B: non-temporal output stores
+        typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+        __builtin_nontemporal_store(__builtin_bit_cast(u32x4_t, o), reinterpret_cast<u32x4_t*>(op));
+      }
+    }
 
     // every wave's LDS reads of this step are done (their values were consumed)
     // before any wave's next DMA overwrites ring rows, index blocks or slot lists
