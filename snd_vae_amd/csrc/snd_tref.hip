@@ -401,12 +401,17 @@ __global__ void __launch_bounds__(256) adam_vec_kernel(float4* p, const float4* 
                                                        float4* v, long long n4, float lr, float b1,
                                                        float b2, float eps, float gscale,
                                                        const int* step) {
+  // the first element's loads go out before the bias-correction arithmetic (f64 pow)
+  // so its memory round trip overlaps it (small buffers: one element per thread)
+  const long long i0 = (long long)blockIdx.x * 256 + threadIdx.x;
+  const long long st = (long long)gridDim.x * 256;
+  float4 gi, mi, vi, pi;
+  if (i0 < n4) { gi = g[i0]; mi = m[i0]; vi = v[i0]; pi = p[i0]; }
   const int t = *step;
   const double lr_t = (double)lr * sqrt(1.0 - pow((double)b2, t)) / (1.0 - pow((double)b1, t));
   const float lrt = (float)lr_t;
-  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n4; i += (long long)gridDim.x * 256) {
-    const float4 gi = g[i];
-    float4 mi = m[i], vi = v[i], pi = p[i];
+  for (long long i = i0; i < n4; i += st) {
+    if (i != i0) { gi = g[i]; mi = m[i]; vi = v[i]; pi = p[i]; }
 #define SND_ADAM_LANE(c)                                   \
     {                                                      \
       const float gc = gi.c * gscale;                      \
