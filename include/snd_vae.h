@@ -235,6 +235,16 @@ int snd_adam_tf1(float* param, const float* grad, float* m, float* v,
                  long long n, float lr, float beta1, float beta2, float eps,
                  float grad_scale, const int* step_counter,
                  snd_stream_t stream);
+/* The same update over n_ranges disjoint [offsets[k], offsets[k] + counts[k]) element
+ * ranges of the same flat buffers in one launch (ABI 14; host arrays, read at call
+ * time): the blocks a fused in-step update (snd_plan_fuse_adam) leaves to the caller
+ * are not contiguous (C4: three ranges).  Offsets and counts that are multiples of 4
+ * on 16-byte aligned buffers take one float4 launch for up to 16 ranges; anything
+ * else falls back to one snd_adam_tf1 per range.  Same arithmetic either way. */
+int snd_adam_tf1_ranges(float* param, const float* grad, float* m, float* v,
+                        const long long* offsets, const long long* counts, int n_ranges,
+                        float lr, float beta1, float beta2, float eps, float grad_scale,
+                        const int* step_counter, snd_stream_t stream);
 
 /* ---- SpatialGraphConvolution (layers.py:143-198) and the model_joint
  * spatial-graph encoder layer s' = lrelu(BN(SGConv(adj, s, rel)))

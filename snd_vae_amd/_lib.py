@@ -17,7 +17,7 @@ c_int, c_ll, c_float, c_size, c_ull = C.c_int, C.c_longlong, C.c_float, C.c_size
 vp = C.c_void_p
 
 
-ABI_VERSION = 13
+ABI_VERSION = 14
 GEN_MODES = {"sample": 0, "mean": 1, "prior": 2, "given": 3}
 TOPOLOGY = {"tscale": 0, "tref": 1, "sgjoint": 2}
 
@@ -100,6 +100,8 @@ _SIGS = {
                                 vp, c_int, vp, vp, vp, c_size, vp]),
     "snd_adam_tf1": (c_int, [vp, vp, vp, vp, c_ll, c_float, c_float, c_float, c_float,
                              c_float, vp, vp]),
+    "snd_adam_tf1_ranges": (c_int, [vp, vp, vp, vp, vp, vp, c_int, c_float, c_float, c_float,
+                                    c_float, c_float, vp, vp]),
     "snd_sg_prep": (c_int, [C.POINTER(SGGraph), vp, vp, vp]),
     "snd_sg_param_count": (c_ll, [c_int, c_int, c_int, c_int]),
     "snd_sg_workspace": (c_size, [c_int, c_int, c_int, c_int, c_int]),

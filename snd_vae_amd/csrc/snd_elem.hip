@@ -529,6 +529,25 @@ extern "C" int snd_reparam_kl(const float* ms, int ldms, int rows, int latent,
   return launch_reparam_fwd(a, (hipStream_t)stream);
 }
 
+extern "C" int snd_adam_tf1_ranges(float* param, const float* grad, float* m, float* v,
+                                   const long long* offsets, const long long* counts, int n_ranges,
+                                   float lr, float beta1, float beta2, float eps, float grad_scale,
+                                   const int* step_counter, snd_stream_t stream) {
+  SND_CHECK_ARG(param && grad && m && v && step_counter && offsets && counts && n_ranges >= 0,
+                "snd_adam_tf1_ranges: bad args");
+  if (n_ranges == 0) return 0;
+  bool vec = n_ranges <= kAdamMaxRanges &&
+             ((uintptr_t)param | (uintptr_t)grad | (uintptr_t)m | (uintptr_t)v) % 16 == 0;
+  for (int k = 0; k < n_ranges && vec; ++k) vec = offsets[k] % 4 == 0 && counts[k] % 4 == 0;
+  if (vec)
+    return launch_adam_ranges(param, grad, m, v, offsets, counts, n_ranges, lr, beta1,
+                              beta2, eps, grad_scale, step_counter, (hipStream_t)stream);
+  for (int k = 0; k < n_ranges; ++k)   // unaligned ranges: one launch each
+    SND_TRY(snd_adam_tf1(param + offsets[k], grad + offsets[k], m + offsets[k], v + offsets[k], counts[k],
+                         lr, beta1, beta2, eps, grad_scale, step_counter, stream));
+  return 0;
+}
+
 extern "C" int snd_adam_tf1(float* param, const float* grad, float* m, float* v, long long n,
                             float lr, float beta1, float beta2, float eps, float grad_scale,
                             const int* step_counter, snd_stream_t stream) {

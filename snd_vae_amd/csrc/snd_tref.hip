@@ -427,7 +427,70 @@ __global__ void __launch_bounds__(256) adam_vec_kernel(float4* p, const float4* 
   }
 }
 
+// several disjoint float4 ranges of the same flat buffers in one launch (the blocks an
+// in-step fused update leaves: C4 has three); same arithmetic as adam_vec_kernel
+struct AdamRanges {
+  long long off4[kAdamMaxRanges], start4[kAdamMaxRanges + 1];
+  int n;
+};
+__global__ void __launch_bounds__(256) adam_ranges_kernel(float4* p, const float4* g, float4* m, float4* v,
+                                                          AdamRanges rg, float lr, float b1, float b2,
+                                                          float eps, float gscale, const int* step) {
+  const long long tot = rg.start4[rg.n];
+  const long long j = (long long)blockIdx.x * 256 + threadIdx.x;
+  long long i = -1;
+  if (j < tot) {
+    int r = 0;
+    while (r + 1 < rg.n && j >= rg.start4[r + 1]) ++r;
+    i = rg.off4[r] + (j - rg.start4[r]);
+  }
+  float4 gi, mi, vi, pi;
+  if (i >= 0) { gi = g[i]; mi = m[i]; vi = v[i]; pi = p[i]; }
+  const int t = *step;
+  const double lr_t = (double)lr * sqrt(1.0 - pow((double)b2, t)) / (1.0 - pow((double)b1, t));
+  const float lrt = (float)lr_t;
+  if (i < 0) return;
+#define SND_ADAM_LANE(c)                                 \
+  {                                                      \
+    const float gc = gi.c * gscale;                      \
+    mi.c = b1 * mi.c + (1.f - b1) * gc;                  \
+    vi.c = b2 * vi.c + (1.f - b2) * gc * gc;             \
+    pi.c -= lrt * mi.c / (sqrtf(vi.c) + eps);            \
+  }
+  SND_ADAM_LANE(x) SND_ADAM_LANE(y) SND_ADAM_LANE(z) SND_ADAM_LANE(w)
+#undef SND_ADAM_LANE
+  m[i] = mi;
+  v[i] = vi;
+  p[i] = pi;
+}
+
 }  // namespace
+
+int launch_adam_ranges(float* p, const float* g, float* m, float* v, const long long* off,
+                       const long long* cnt, int n, float lr, float b1, float b2, float eps, float gscale,
+                       const int* step, hipStream_t s) {
+  SND_CHECK_ARG(n >= 1 && n <= kAdamMaxRanges, "adam_ranges: 1..%d ranges", kAdamMaxRanges);
+  SND_CHECK_ARG(((uintptr_t)p | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v) % 16 == 0,
+                "adam_ranges: 16-byte aligned buffers");
+  AdamRanges rg{};
+  rg.n = n;
+  long long acc = 0;
+  for (int k = 0; k < n; ++k) {
+    SND_CHECK_ARG(off[k] >= 0 && cnt[k] >= 0 && off[k] % 4 == 0 && cnt[k] % 4 == 0,
+                  "adam_ranges: offsets and counts must be multiples of 4");
+    rg.off4[k] = off[k] / 4;
+    rg.start4[k] = acc;
+    acc += cnt[k] / 4;
+  }
+  rg.start4[n] = acc;
+  if (acc == 0) return 0;
+  hipLaunchKernelGGL(adam_ranges_kernel, dim3((unsigned)cdiv(acc, 256)), dim3(256), 0, s,
+                     reinterpret_cast<float4*>(p), reinterpret_cast<const float4*>(g),
+                     reinterpret_cast<float4*>(m), reinterpret_cast<float4*>(v), rg, lr, b1, b2, eps, gscale,
+                     step);
+  SND_LAUNCH_CHECK("adam_ranges_kernel");
+  return 0;
+}
 
 int tref_head_fwd_blocks(long long K, int gh) { return cdiv(K, head_fwd_rpb(K, gh)); }
 

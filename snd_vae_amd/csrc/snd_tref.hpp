@@ -69,5 +69,10 @@ int launch_tref_proj_bwd(const TrefProjBwdArgs& a, hipStream_t s);
 // Vectorised TF1 Adam (float4 streams; n % 4 == 0, 16-byte aligned buffers)
 int launch_adam_vec(float* p, const float* g, float* m, float* v, long long n, float lr,
                     float b1, float b2, float eps, float gscale, const int* step, hipStream_t s);
+// the same update over up to kAdamMaxRanges disjoint [off, off + cnt) ranges (multiples of 4)
+constexpr int kAdamMaxRanges = 16;
+int launch_adam_ranges(float* p, const float* g, float* m, float* v, const long long* off,
+                       const long long* cnt, int n, float lr, float b1, float b2, float eps, float gscale,
+                       const int* step, hipStream_t s);
 
 }  // namespace snd

@@ -100,6 +100,9 @@ class OptimizerVAE:
                 self._adam_ranges[-1][1] += end - off
             else:
                 self._adam_ranges.append([off, end - off])
+        # host copies for snd_adam_tf1_ranges (read at call time, so the arrays outlive it)
+        self._roff = (C.c_longlong * max(1, len(self._adam_ranges)))(*[o for o, _ in self._adam_ranges])
+        self._rcnt = (C.c_longlong * max(1, len(self._adam_ranges)))(*[n for _, n in self._adam_ranges])
         self.bucketed = self.distributed and (bucketed is None or bool(bucketed))
         self.buckets = []
         if self.bucketed:
@@ -164,6 +167,14 @@ class OptimizerVAE:
             "snd_adam_tf1")
 
     def apply(self, stream=None):
+        if len(self._adam_ranges) > 1:   # the blocks a fused update leaves: one launch
+            m = self.model
+            _lib.check(_lib.lib().snd_adam_tf1_ranges(
+                _lib.ptr(m.params), _lib.ptr(self.grads), _lib.ptr(self.m), _lib.ptr(self.v),
+                self._roff, self._rcnt, len(self._adam_ranges), self.lr, self.beta1, self.beta2,
+                self.eps, 1.0 / self.world, _lib.ptr(self.step_counter), _lib.stream_ptr(stream)),
+                "snd_adam_tf1_ranges")
+            return
         for off, n in self._adam_ranges:
             self._adam(off, n, self.grads[off:off + n], stream)
 

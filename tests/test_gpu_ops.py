@@ -436,6 +436,43 @@ def test_adam_tf1_matches_oracle():
     assert np.abs(tp.cpu().numpy() - po["w"]).max() < 1e-6
 
 
+@pytest.mark.parametrize("ranges", [[(0, 1000), (2000, 400), (4096, 3000)],   # float4 launch
+                                    [(3, 997), (2001, 398)]])                  # per-range fallback
+def test_adam_tf1_ranges_equals_per_range_updates(ranges):
+    """snd_adam_tf1_ranges (one launch over the blocks a fused update leaves) equals one
+    snd_adam_tf1 per range, and leaves everything outside the ranges untouched."""
+    import ctypes
+    from snd_vae_amd import _lib
+    L = _lib.lib()
+    rng = np.random.default_rng(3)
+    n = 8192
+    p, g = rng.standard_normal(n).astype(np.float32), rng.standard_normal(n).astype(np.float32)
+    m0, v0 = 0.1 * rng.standard_normal(n).astype(np.float32), rng.random(n).astype(np.float32)
+    step = torch.full((1,), 5, dtype=torch.int32, device=DEV)
+    out = []
+    for multi in (False, True):
+        tp, tg, tm, tv = cu(p), cu(g), cu(m0), cu(v0)
+        if multi:
+            off = (ctypes.c_longlong * len(ranges))(*[o for o, _ in ranges])
+            cnt = (ctypes.c_longlong * len(ranges))(*[c for _, c in ranges])
+            _lib.check(L.snd_adam_tf1_ranges(tp.data_ptr(), tg.data_ptr(), tm.data_ptr(), tv.data_ptr(),
+                                             off, cnt, len(ranges), 0.0008, 0.9, 0.999, 1e-8, 0.5,
+                                             step.data_ptr(), _lib.stream_ptr()))
+        else:
+            for o, c in ranges:
+                _lib.check(L.snd_adam_tf1(tp.data_ptr() + 4 * o, tg.data_ptr() + 4 * o, tm.data_ptr() + 4 * o,
+                                          tv.data_ptr() + 4 * o, c, 0.0008, 0.9, 0.999, 1e-8, 0.5,
+                                          step.data_ptr(), _lib.stream_ptr()))
+        torch.cuda.synchronize()
+        out.append([t.cpu().numpy() for t in (tp, tm, tv)])
+    inside = np.zeros(n, bool)
+    for o, c in ranges:
+        inside[o:o + c] = True
+    for a, b, init in zip(out[0], out[1], (p, m0, v0)):
+        assert np.array_equal(a, b)
+        assert np.array_equal(b[~inside], init[~inside])
+
+
 def test_reparam_injected_and_philox():
     from snd_vae_amd import _lib
     rows, L = 2000, 64

@@ -22,6 +22,8 @@ def main():
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--tag", default=os.environ.get("SND_LIB_PATH", "default"))
     ap.add_argument("--config", default="", help="preset (C4, C5, ...) instead of --nodes/--latent")
+    ap.add_argument("--adam-per-range", action="store_true",
+                    help="A/B: one snd_adam_tf1 launch per unfused range instead of snd_adam_tf1_ranges")
     args = ap.parse_args()
     import torch
 
@@ -36,6 +38,12 @@ def main():
     db = DeviceBatch(synthetic_batch(cfg, args.graphs, seed=1000))
     model = SGCNModelVAE(cfg, args.graphs, dtype="bf16")
     opt = OptimizerVAE(model)
+    if args.adam_per_range:
+        def per_range(stream=None):
+            for off, n in opt._adam_ranges:
+                opt._adam(off, n, opt.grads[off:off + n], stream)
+        opt.apply = per_range
+        args.tag += " per-range"
     opt.step(db)
     opt.capture(db, warmup=2)
     for _ in range(10):
