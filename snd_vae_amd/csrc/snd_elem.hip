@@ -268,6 +268,12 @@ __global__ void __launch_bounds__(256) enc_bwd_kernel(EncBwdArgs a, int rows) {
 #ifndef SND_RED_PL
 #define SND_RED_PL 8   // part lanes of a >= 64-part slab (C2 step 0.2368 vs 0.2389 ms at 16, 0.2380 at 4)
 #endif
+// part lanes of a descriptor (uniform per block): a thread sums nparts / PL parts in a
+// dependent chain, so the many-part partials (C4's split-K head / projection slabs, ~1000
+// parts) take wider lane groups and more blocks
+__host__ __device__ __forceinline__ int red_pl(int nparts) {
+  return nparts >= 1024 ? 64 : (nparts >= 256 ? 32 : (nparts >= 64 ? SND_RED_PL : 4));
+}
 struct ReducePack {
   ReduceDesc d[kMaxReduce];
   int bstart[kMaxReduce + 1];   // first block of each descriptor (flattened 1-D grid)
@@ -289,7 +295,7 @@ __global__ void __launch_bounds__(256) reduce_kernel(ReducePack pk, FinalizeArgs
   __shared__ double red[256];
   const int rows = d.rows > 0 ? d.rows : 1;
   const long long items = (long long)rows * d.len;
-  const int PL = d.nparts >= 64 ? SND_RED_PL : 4;   // part lanes
+  const int PL = red_pl(d.nparts);               // part lanes
   const int IPB = 256 / PL;                      // items per block
   const int it = threadIdx.x % IPB, pl = threadIdx.x / IPB;
   const long long j = (long long)bx * IPB + it;
@@ -469,7 +475,7 @@ int launch_reduce(const ReduceDesc* d, int n, hipStream_t s, const FinalizeArgs*
       if (i < cnt) {
         pk.d[i] = d[base + i];
         const long long items = (long long)(pk.d[i].rows > 0 ? pk.d[i].rows : 1) * pk.d[i].len;
-        const int ipb = pk.d[i].nparts >= 64 ? 256 / SND_RED_PL : 64;
+        const int ipb = 256 / red_pl(pk.d[i].nparts);
         nb += (items + ipb - 1) / ipb;
       }
     }
