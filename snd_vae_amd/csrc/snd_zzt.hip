@@ -849,6 +849,9 @@ __global__ void __launch_bounds__(NTH2) zzt_dense_bf16_v4(ZztArgs a) {
   float lacc = 0.f, labs = 0.f;
   double ltot = 0.0;
   unsigned wcnt = 0, lcnt = 0;   // per wave (EPI 1 ballots) / per lane (EPI 0 sign bits)
+  // sticky, wave-uniform: once a quad product of this wave overflowed, later tiles skip
+  // the products (logits that large, e.g. C4's graph-latent heads at init, recur)
+  bool ovf = false;
   auto epi = [&](const f32x16& Y, bf16x8 (&sA)[2]) {
     if constexpr (EPI != 1) {
       float q[16], lt = 0.f;
@@ -868,11 +871,14 @@ __global__ void __launch_bounds__(NTH2) zzt_dense_bf16_v4(ZztArgs a) {
                                                    __float_as_uint(Y[4 * g4 + 2]), 0x07030C0Cu);
         lcnt += (unsigned)__builtin_popcount((t01 | t23) & 0x80808080u);
       }
+      if (!ovf) {
 #pragma unroll
-      for (int p = 0; p < 4; ++p)   // one log2 per 4 logits (an overflowing product: fallback below)
-        lt += __builtin_amdgcn_logf((q[4 * p] * q[4 * p + 1]) * (q[4 * p + 2] * q[4 * p + 3]));
-      if (__builtin_expect(!__builtin_isfinite(lt), 0)) {
-        // a quad product overflowed: this lane's block again one logit at a time,
+        for (int p = 0; p < 4; ++p)   // one log2 per 4 logits (an overflowing product: fallback below)
+          lt += __builtin_amdgcn_logf((q[4 * p] * q[4 * p + 1]) * (q[4 * p + 2] * q[4 * p + 3]));
+        ovf = __builtin_amdgcn_ballot_w64(!__builtin_isfinite(lt)) != 0;
+      }
+      if (__builtin_expect(ovf, 0)) {
+        // a quad product overflowed: the block one logit at a time,
         // log2(q) = y for y > 24 (1 + 2^y rounds to 2^y; q may be inf), else log2(q)
         // (one transcendental per logit on the q already computed; c = 0)
         lt = 0.f;
