@@ -392,7 +392,7 @@ __global__ void __launch_bounds__(256) adam_kernel(float* p, const float* g, flo
     const float vi = b2 * v[i] + (1.f - b2) * gi * gi;
     m[i] = mi;
     v[i] = vi;
-    p[i] -= lrt * mi / (sqrtf(vi) + eps);
+    p[i] -= lrt * mi * __builtin_amdgcn_rcpf(__builtin_amdgcn_sqrtf(vi) + eps);
   }
 }
 
