@@ -174,7 +174,7 @@ constexpr int HB_T = 256, HB_RPB = SND_HB_RPB;   // A/B builds: -DSND_HB_RPB=...
 
 __global__ void __launch_bounds__(HB_T) tref_head_bwd_kernel(TrefHeadBwdArgs a) {
   __shared__ float gs[HB_RPB * B8];      // G[b, k0 + kk] as [kk][8]
-  __shared__ float dgs[B8 * HB_RPB];     // dG[b, k0 + kk] as [b][kk]
+  __shared__ float dgs[2][B8 * HB_RPB];  // dG[b, k0 + kk] as [b][kk]: the two 16-lane halves' sums
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const int h = lane >> 5, q = lane & 31;
   const int TPR = a.gh >> 2;
@@ -222,26 +222,26 @@ __global__ void __launch_bounds__(HB_T) tref_head_bwd_kernel(TrefHeadBwdArgs a) 
         if (fused) adam4(a.adam, lrt, (k0 + kk) * a.gh + 4 * q, dw, w[u], am[u], av[u]);
         else *reinterpret_cast<float4*>(a.dwh + (k0 + kk) * a.gh + 4 * q) = dw;
       }
+      // all lanes active: inactive quads hold 0.  Each 16-lane half parks its sum; the
+      // halves are added at the store (same order as a cross-half swizzle, no LDS permute)
       float p[B8];
 #pragma unroll
-      for (int b = 0; b < B8; ++b) {
-        p[b] = row16_sum(dot4(dh[b], w[u]));          // all lanes active: inactive quads hold 0
-        p[b] += __shfl_xor(p[b], 16, 64);
-      }
-      if (q == 0 && rv)
+      for (int b = 0; b < B8; ++b) p[b] = row16_sum(dot4(dh[b], w[u]));
+      if ((q & 15) == 0 && rv)
 #pragma unroll
-        for (int b = 0; b < B8; ++b) dgs[b * HB_RPB + kk] = p[b];
+        for (int b = 0; b < B8; ++b) dgs[q >> 4][b * HB_RPB + kk] = p[b];
     }
   }
   __syncthreads();
   for (int b = 0; b < a.B; ++b)
     for (int kk = t; kk < nk; kk += HB_T) {
       const long long k = k0 + kk;
+      const float v = dgs[0][b * HB_RPB + kk] + dgs[1][b * HB_RPB + kk];
       if (a.dgb) {
         const long long n = k / a.W;
-        a.dgb[((long long)b * a.npg + n) * a.ldg + (k - n * a.W)] = (__bf16)dgs[b * HB_RPB + kk];
+        a.dgb[((long long)b * a.npg + n) * a.ldg + (k - n * a.W)] = (__bf16)v;
       } else {
-        a.dg[(long long)b * a.K + k] = dgs[b * HB_RPB + kk];
+        a.dg[(long long)b * a.K + k] = v;
       }
     }
 }
@@ -325,7 +325,7 @@ constexpr int PB_T = 256, PB_W = PB_T / 64;
 
 __global__ void __launch_bounds__(PB_T) tref_proj_bwd_kernel(TrefProjBwdArgs a) {
   __shared__ float zs[128 * B8];         // z as [l][8]
-  __shared__ float red[128 * B8];        // dz partial as [l][8]
+  __shared__ float red[4][128 * B8];     // dz partials as [16-lane row][l][8]
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   for (int i = t; i < a.L * B8; i += PB_T) {
     const int l = i >> 3, b = i & 7;
@@ -384,18 +384,17 @@ __global__ void __launch_bounds__(PB_T) tref_proj_bwd_kernel(TrefProjBwdArgs a) 
         else *reinterpret_cast<float4*>(a.dwp + (long long)l * a.Cp + c4) = dw;
       }
 #pragma unroll
-      for (int b = 0; b < B8; ++b) {
-        float p = row16_sum(dot4(d[b], w[u]));
-        p += __shfl_xor(p, 16, 64);
-        p += __shfl_xor(p, 32, 64);
-        if (lane == 0) red[l * B8 + b] = p;
+      for (int b = 0; b < B8; ++b) {   // each 16-lane row parks its sum (no LDS permutes)
+        const float p = row16_sum(dot4(d[b], w[u]));
+        if ((lane & 15) == 0) red[lane >> 4][l * B8 + b] = p;
       }
     }
   }
   __syncthreads();
   for (int i = t; i < a.L * a.B; i += PB_T) {
     const int b = i / a.L, l = i - b * a.L;
-    a.slab[(long long)blockIdx.x * a.B * a.L + i] = red[l * B8 + b];
+    const int j = l * B8 + b;   // (R0 + R1) + (R2 + R3): the order of the xor-16 / xor-32 swizzles
+    a.slab[(long long)blockIdx.x * a.B * a.L + i] = (red[0][j] + red[1][j]) + (red[2][j] + red[3][j]);
   }
 }
 
