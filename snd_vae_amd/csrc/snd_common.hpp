@@ -145,4 +145,17 @@ __device__ __forceinline__ void reparam_bwd_elem(float mu, float ls, float eps, 
 inline int cdiv(long long a, long long b) { return (int)((a + b - 1) / b); }
 inline long long round_up(long long a, long long b) { return (a + b - 1) / b * b; }
 
+// One TF1 Adam element update (optimizer.py:125,197), shared by every Adam kernel (the
+// separate float4 / range / scalar passes and the updates fused into the graph-latent
+// streams) with every rounding explicit, so no kernel's FMA contraction differs: a fused
+// and a separate update of the same gradient are bitwise equal.  The division is
+// v_rcp_f32 of v_sqrt_f32 (1 ulp each) instead of the ~15-VALU IEEE sequences.
+__device__ __forceinline__ void adam_elem(float& p, float& m, float& v, float g, float b1, float b2,
+                                          float eps, float lrt) {
+  m = __fmaf_rn(b1, m, __fmul_rn(1.f - b1, g));
+  v = __fmaf_rn(b2, v, __fmul_rn(__fmul_rn(1.f - b2, g), g));
+  p = __fsub_rn(p, __fmul_rn(__fmul_rn(lrt, m),
+                             __builtin_amdgcn_rcpf(__fadd_rn(__builtin_amdgcn_sqrtf(v), eps))));
+}
+
 }  // namespace snd

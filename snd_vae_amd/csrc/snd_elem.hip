@@ -68,6 +68,96 @@ __global__ void __launch_bounds__(256) reparam_bwd_kernel(ReparamBwdArgs a) {
   }
 }
 
+// ---------------------------------------------------------------- graph-latent small heads
+constexpr int kSHC = 8;        // latent columns per forward block (mu and logstd: 2 x 8 of Wms)
+constexpr int kSHK = 128;      // gh limit
+constexpr int kSHN = 64;       // columns of [mu || s] per backward block
+constexpr int kSHD = 16;       // h columns per dh block
+constexpr int kSHL2 = 256;     // 2L limit
+
+__global__ void __launch_bounds__(256) small_head_fwd_kernel(SmallHeadFwdArgs a) {
+  __shared__ float ws[kSHK][2 * kSHC];            // Wms columns c0.. (mu) and L + c0.. (logstd)
+  __shared__ float hs[kSmallHeadRows][kSHK];
+  const int c0 = blockIdx.x * kSHC, L2 = 2 * a.L, t = threadIdx.x;
+  for (int i = t; i < a.gh * 2 * kSHC; i += 256) {
+    const int k = i / (2 * kSHC), j = i - k * 2 * kSHC;
+    const int c = c0 + (j & (kSHC - 1));
+    ws[k][j] = c < a.L ? a.wms[k * L2 + (j < kSHC ? c : a.L + c)] : 0.f;
+  }
+  for (int i = t; i < a.rows * a.gh; i += 256) hs[i / a.gh][i % a.gh] = a.hh[i];
+  __syncthreads();
+  const unsigned off = a.step ? (unsigned)(*a.step) : 0u;
+  const int b = t / kSHC, j = t - b * kSHC, c = c0 + j;
+  double kl = 0.0;
+  if (b < a.rows && c < a.L) {
+    float mu = 0.f, ls = 0.f;
+    for (int k = 0; k < a.gh; ++k) {
+      mu = fmaf(hs[b][k], ws[k][j], mu);
+      ls = fmaf(hs[b][k], ws[k][kSHC + j], ls);
+    }
+    mu += a.bms[c];
+    ls += a.bms[a.L + c];
+    a.ms[b * L2 + c] = mu;
+    a.ms[b * L2 + a.L + c] = ls;
+    const int i = b * a.L + c;
+    const float eps = a.eps_in ? a.eps_in[i] : philox_normal(a.seed, off, a.eps_base + (unsigned long long)i);
+    const float es = __expf(ls);
+    a.z[i] = mu + eps * es;                // model.py:159
+    if (a.eps_out) a.eps_out[i] = eps;
+    kl = (double)(1.f + 2.f * ls - mu * mu - es * es);   // optimizer.py:193
+  }
+  const double s = block_sum(kl);
+  if (t == 0) a.kl_part[blockIdx.x] = s;
+}
+
+// d[mu || s] of the block's 64 columns for every row, then their Wms / bms slab columns
+__global__ void __launch_bounds__(256) small_head_dms_kernel(SmallHeadBwdArgs a) {
+  __shared__ float dm[kSmallHeadRows][kSHN];
+  __shared__ float hs[kSmallHeadRows][kSHK];
+  const int L2 = 2 * a.L, t = threadIdx.x, nl = t & (kSHN - 1), grp = t >> 6;
+  const int n = blockIdx.x * kSHN + nl;
+  for (int i = t; i < a.rows * a.gh; i += 256) hs[i / a.gh][i % a.gh] = a.hh[i];
+  if (n < L2) {
+    const int c = n < a.L ? n : n - a.L;
+    for (int b = grp; b < a.rows; b += 4) {
+      const float mu = a.ms[b * L2 + c], ls = a.ms[b * L2 + a.L + c];
+      const float es = __expf(ls);
+      const float dz = a.dz[b * a.L + c];
+      const float v = n < a.L ? dz + a.kl_scale * mu : dz * a.eps[b * a.L + c] * es + a.kl_scale * (es * es - 1.f);
+      a.dms[b * L2 + n] = v;
+      dm[b][nl] = v;
+    }
+  }
+  __syncthreads();
+  if (n >= L2) return;
+  for (int k = grp; k <= a.gh; k += 4) {
+    float acc = 0.f;
+    if (k < a.gh)
+      for (int b = 0; b < a.rows; ++b) acc = fmaf(hs[b][k], dm[b][nl], acc);
+    else
+      for (int b = 0; b < a.rows; ++b) acc += dm[b][nl];
+    a.slab[k * L2 + n] = acc;
+  }
+}
+
+// dh[b][k] = sum_n d[mu || s][b][n] Wms[k][n] for the block's 16 h columns
+__global__ void __launch_bounds__(256) small_head_dh_kernel(SmallHeadBwdArgs a) {
+  __shared__ float dm[kSmallHeadRows][kSHL2 + 1];
+  __shared__ float ws[kSHD][kSHL2 + 1];
+  const int L2 = 2 * a.L, t = threadIdx.x, k0 = blockIdx.x * kSHD;
+  for (int i = t; i < a.rows * L2; i += 256) dm[i / L2][i % L2] = a.dms[i];
+  for (int i = t; i < kSHD * L2; i += 256) {
+    const int kk = i / L2, n = i - kk * L2;
+    ws[kk][n] = k0 + kk < a.gh ? a.wms[(k0 + kk) * L2 + n] : 0.f;
+  }
+  __syncthreads();
+  const int b = t / kSHD, kk = t - b * kSHD, k = k0 + kk;
+  if (b >= a.rows || k >= a.gh) return;
+  float acc = 0.f;
+  for (int n = 0; n < L2; ++n) acc = fmaf(dm[b][n], ws[kk][n], acc);
+  a.dh[b * a.gh + k] = acc;
+}
+
 // ---------------------------------------------------------------- heads
 constexpr int kHeadRows = 256;
 constexpr int kHeadK = 64, kHeadO = 4;
@@ -387,12 +477,11 @@ __global__ void __launch_bounds__(256) adam_kernel(float* p, const float* g, flo
   const float lrt = (float)lr_t;
   for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n;
        i += (long long)gridDim.x * 256) {
-    const float gi = g[i] * gscale;
-    const float mi = b1 * m[i] + (1.f - b1) * gi;
-    const float vi = b2 * v[i] + (1.f - b2) * gi * gi;
+    float pi = p[i], mi = m[i], vi = v[i];
+    adam_elem(pi, mi, vi, __fmul_rn(g[i], gscale), b1, b2, eps, lrt);
     m[i] = mi;
     v[i] = vi;
-    p[i] -= lrt * mi * __builtin_amdgcn_rcpf(__builtin_amdgcn_sqrtf(vi) + eps);
+    p[i] = pi;
   }
 }
 
@@ -410,6 +499,28 @@ int launch_reparam_fwd(const ReparamFwdArgs& a, hipStream_t s) {
 int launch_reparam_bwd(const ReparamBwdArgs& a, hipStream_t s) {
   hipLaunchKernelGGL(reparam_bwd_kernel, dim3(reparam_blocks(a.rows, a.L)), dim3(256), 0, s, a);
   SND_LAUNCH_CHECK("reparam_bwd_kernel");
+  return 0;
+}
+
+bool small_head_supported(int rows, int gh, int L) {
+  return rows >= 1 && rows <= kSmallHeadRows && rows * kSHC <= 256 && gh >= 1 && gh <= kSHK && L >= 1 &&
+         2 * L <= kSHL2 && rows * kSHD <= 256;
+}
+int small_head_fwd_blocks(int L) { return cdiv(L, kSHC); }
+int launch_small_head_fwd(const SmallHeadFwdArgs& a, hipStream_t s) {
+  SND_CHECK_ARG(small_head_supported(a.rows, a.gh, a.L), "small_head: rows <= 16, gh <= 128, 2L <= 256");
+  SND_CHECK_ARG(a.hh && a.wms && a.bms && a.ms && a.z && a.kl_part, "small_head_fwd: operands");
+  hipLaunchKernelGGL(small_head_fwd_kernel, dim3(small_head_fwd_blocks(a.L)), dim3(256), 0, s, a);
+  SND_LAUNCH_CHECK("small_head_fwd_kernel");
+  return 0;
+}
+int launch_small_head_bwd(const SmallHeadBwdArgs& a, hipStream_t s) {
+  SND_CHECK_ARG(small_head_supported(a.rows, a.gh, a.L), "small_head: rows <= 16, gh <= 128, 2L <= 256");
+  SND_CHECK_ARG(a.hh && a.wms && a.ms && a.eps && a.dz && a.dms && a.slab && a.dh, "small_head_bwd: operands");
+  hipLaunchKernelGGL(small_head_dms_kernel, dim3(cdiv(2 * a.L, kSHN)), dim3(256), 0, s, a);
+  SND_LAUNCH_CHECK("small_head_dms_kernel");
+  hipLaunchKernelGGL(small_head_dh_kernel, dim3(cdiv(a.gh, kSHD)), dim3(256), 0, s, a);
+  SND_LAUNCH_CHECK("small_head_dh_kernel");
   return 0;
 }
 

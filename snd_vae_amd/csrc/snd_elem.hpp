@@ -15,6 +15,35 @@ struct ReparamFwdArgs {
 int reparam_blocks(int rows, int L);
 int launch_reparam_fwd(const ReparamFwdArgs& a, hipStream_t s);
 
+// Graph-latent heads on <= kSmallHeadRows rows (B graphs): [mu || s] = h Wms + bms fused
+// with the reparameterisation + KL (model.py:114-115,153-161; optimizer.py:193), and the
+// backward as two launches: d[mu || s] (reparam/KL backward) with the Wms / bms slab of
+// one split ([gh + 1][2L], bias row last, as the generic split-K wgrad writes it), then
+// dh = d[mu || s] Wms^T.  Each block stages its operand slice in LDS first, so no thread
+// walks a chain of dependent global loads (the generic GEMMs ran ~6 us apiece here).
+constexpr int kSmallHeadRows = 32;
+struct SmallHeadFwdArgs {
+  const float* hh; int rows; int gh;          // [rows][gh]
+  const float* wms; const float* bms; int L;  // [gh][2L], [2L]
+  float* ms;                                  // [rows][2L] out
+  const float* eps_in; unsigned long long seed; const int* step; unsigned long long eps_base;
+  float* eps_out; float* z;                   // [rows][L]
+  double* kl_part;                            // [small_head_fwd_blocks(L)]
+};
+struct SmallHeadBwdArgs {
+  const float* hh; int rows; int gh;
+  const float* wms; int L;
+  const float* ms; const float* eps; const float* dz;   // dz: [rows][L]
+  float kl_scale;
+  float* dms;                                 // [rows][2L]
+  float* slab;                                // [gh + 1][2L]
+  float* dh;                                  // [rows][gh]
+};
+bool small_head_supported(int rows, int gh, int L);
+int small_head_fwd_blocks(int L);
+int launch_small_head_fwd(const SmallHeadFwdArgs& a, hipStream_t s);
+int launch_small_head_bwd(const SmallHeadBwdArgs& a, hipStream_t s);
+
 struct ReparamBwdArgs {
   const float* ms; int ldms; int rows; int L;
   const float* eps;

@@ -95,6 +95,7 @@ struct snd_plan {
   bool head_fused = false;     // fused encoder forward tail (snd_head.hip): 1 launch instead of 4
   bool head_bwd = false;       // fused edge terms + encoder backward head (snd_head.hip): 1 instead of 4
   bool front_fused = false;    // gcn0 + H1 W1 + the weight images in one launch (snd_head.hip)
+  bool small_head = false;     // graph latent: [mu || s] head + reparameterisation (snd_elem.hip small_head_*)
   int ldh1 = 0, ldg = 0;
   Img pw1f{}, pwhf{}, pwmsf{}, pwmsb{}, pwhb{}, pw1b{};
   Img pidg{};                  // graph latent: identity [W -> W] (dG enters RC_ENC1 directly)
@@ -275,7 +276,7 @@ extern "C" int snd_plan_create(const snd_config_t* cfg, int n_graphs, snd_plan_t
   p->add_buf("DP0", R * h0);  p->add_buf("DXW0", R * h0);
   const int nz = zzt_dense_blocks(p->B, p->N, c.dtype), ne = edge_blocks(p->R, dj);
   const int nk = reparam_blocks(p->RH, L), nh = head_blocks(p->R), nc = col_blocks(p->R);
-  p->add_buf("PZZT", 2LL * nz, 8); p->add_buf("PEDGE", 2LL * std::max(ne, edge_bf16_blocks(p->R)), 8); p->add_buf("PKL", std::max(nk, reparam_prep_blocks(p->B, zzt_npad(p->N))), 8);
+  p->add_buf("PZZT", 2LL * nz, 8); p->add_buf("PEDGE", 2LL * std::max(ne, edge_bf16_blocks(p->R)), 8); p->add_buf("PKL", std::max({nk, reparam_prep_blocks(p->B, zzt_npad(p->N)), small_head_fwd_blocks(c.latent)}), 8);
   p->add_buf("PSSES", nh, 8); p->add_buf("PSSEN", nh, 8);
   p->add_buf("PHS", (long long)nh * (c.s3 * c.spatial_dim + c.spatial_dim));
   p->add_buf("PHN", (long long)nh * (c.n2 * c.num_feature + c.num_feature));
@@ -287,6 +288,9 @@ extern "C" int snd_plan_create(const snd_config_t* cfg, int n_graphs, snd_plan_t
   p->sWh = sg ? wgrad_split((int)std::min<long long>((long long)p->N * W + 1, 1 << 30), gh, (int)RH)
              : wgrad_split(W + 1, gh, p->R);
   p->sWms = wgrad_split(gh + 1, 2 * L, p->RH);
+  // graph latent on <= 16 head rows: the Wms GEMM with the reparameterisation (one launch)
+  // and their backward (two launches) instead of five generic launches
+  p->small_head = tref && small_head_supported(p->RH, gh, L) && p->sWms.splits == 1;
   p->sK1 = wgrad_split(5 * dj, C1, p->R);
   p->sK2s = wgrad_split(5 * c.s1, c.s2, p->R);
   p->sK2n = wgrad_split(5 * c.n1, c.n2, p->R);
@@ -707,9 +711,10 @@ int encoder_generic_fwd(const Ctx& x, const snd_batch_t* batch) {
     SND_TRY(gemm_fwd(x, R, gh, W, x.f("G"), W, x.w("enc.Wh"), gh, B_ROW, x.f("Hh"), gh,
                      x.w("enc.bh")));
   }
-  // [mu || s] = h Wms + bms (model.py:114-115)
-  SND_TRY(gemm_fwd(x, RH, 2 * L, gh, x.f("Hh"), gh, x.w("enc.Wms"), 2 * L, B_ROW, x.f("MS"), 2 * L,
-                   x.w("enc.bms")));
+  // [mu || s] = h Wms + bms (model.py:114-115; small_head: with the reparameterisation)
+  if (!p.small_head)
+    SND_TRY(gemm_fwd(x, RH, 2 * L, gh, x.f("Hh"), gh, x.w("enc.Wms"), 2 * L, B_ROW, x.f("MS"), 2 * L,
+                     x.w("enc.bms")));
   return 0;
 }
 
@@ -737,6 +742,7 @@ int encoder_sg_fwd(const Ctx& x, const snd_batch_t* batch) {
                            x.f("SGY2"), x.f("SGG"), x.f("SGWS1"), x.s));
   const int KH = N * W;   // flat(s_g) per copy: the row-major [N, W] rows of one copy
   SND_TRY(gemm_fwd(x, RH, gh, KH, x.f("SGG"), KH, x.w("enc.Wh"), gh, B_ROW, x.f("Hh"), gh, x.w("enc.bh")));
+  if (p.small_head) return 0;   // with the reparameterisation
   return gemm_fwd(x, RH, 2 * L, gh, x.f("Hh"), gh, x.w("enc.Wms"), 2 * L, B_ROW, x.f("MS"), 2 * L,
                   x.w("enc.bms"));
 }
@@ -1273,6 +1279,9 @@ extern "C" int snd_generate(const snd_plan_t* plan, const snd_batch_t* batch, co
   const long long CP = (long long)N * dj;
   float* zl = p.tref ? x.f("ZL") : x.f("Z");
   if (enc) SND_TRY(p.sg ? encoder_sg_fwd(x, batch) : encoder_generic_fwd(x, batch));
+  if (enc && p.small_head)   // the step folds [mu || s] into small_head_fwd; here it is read directly
+    SND_TRY(gemm_fwd(x, RH, 2 * L, c.g_hidden, x.f("Hh"), c.g_hidden, x.w("enc.Wms"), 2 * L, B_ROW, x.f("MS"),
+                     2 * L, x.w("enc.bms")));
   if (mode == SND_GEN_MEAN) {             // z = mu
     if (hipMemcpy2DAsync(zl, (size_t)L * 4, x.f("MS"), (size_t)2 * L * 4, (size_t)L * 4, RH,
                          hipMemcpyDeviceToDevice, x.s) != hipSuccess) {
@@ -1478,13 +1487,18 @@ extern "C" int snd_train_step(const snd_plan_t* plan, const snd_batch_t* batch,
     const ReduceDesc rd{x.f("PHF"), x.f("Hh"), tref_head_fwd_blocks(KH, gh), RH * gh,
                         (long long)RH * gh, 1.f, 0, 0, 0, 0};
     SND_TRY(launch_reduce(&rd, 1, x.s));
-    SND_TRY(gemm_fwd(x, RH, 2 * L, gh, x.f("Hh"), gh, x.w("enc.Wms"), 2 * L, B_ROW, x.f("MS"), 2 * L,
-                     x.w("enc.bms")));
+    if (!p.small_head)
+      SND_TRY(gemm_fwd(x, RH, 2 * L, gh, x.f("Hh"), gh, x.w("enc.Wms"), 2 * L, B_ROW, x.f("MS"), 2 * L,
+                       x.w("enc.bms")));
   }
   // z = mu + eps exp(s) (model.py:159); KL partials (optimizer.py:193)
   const ZztStage stg = zzt_stage(x.ws + p.buf("ZSTAGE"), p.B, N, dj, c.dtype);
   if (p.tref) {
-    {   // z [B, L] (model_joint.py:89); SND_SGJOINT: [B*S, L] (model.py:157)
+    if (p.small_head) {   // [mu || s] = h Wms + bms, z and the KL terms in one launch
+      SmallHeadFwdArgs a{x.f("Hh"), RH, gh, x.w("enc.Wms"), x.w("enc.bms"), L, x.f("MS"), eps, seed,
+                         step_counter, p.eps_base(), x.f("EPS"), x.f("ZL"), x.d("PKL")};
+      SND_TRY(launch_small_head_fwd(a, x.s));
+    } else {   // z [B, L] (model_joint.py:89); SND_SGJOINT: [B*S, L] (model.py:157)
       ReparamFwdArgs a{x.f("MS"), 2 * L, RH, L, eps, seed, step_counter, x.f("EPS"), x.f("ZL"),
                        x.d("PKL"), nullptr, L};
       a.eps_base = p.eps_base();
@@ -1614,17 +1628,25 @@ extern "C" int snd_train_step(const snd_plan_t* plan, const snd_batch_t* batch,
         SND_TRY(launch_reduce(&rd, 1, x.s));
         if (p.sg) SND_TRY(launch_sg_spread(x.f("DZBAR"), x.f("DZL"), p.B, p.S, L, x.s));
       }
-      ReparamBwdArgs a{x.f("MS"), 2 * L, RH, L, x.f("EPS"), x.f("DZL"), nullptr, nullptr, 0.f,
-                       kl_scale, x.f("DMS"), 2 * L};
-      SND_TRY(launch_reparam_bwd(a, x.s));
+      if (p.small_head) {   // reparam/KL backward + the Wms slab, then dh
+        SmallHeadBwdArgs a{x.f("Hh"), RH, gh, x.w("enc.Wms"), L, x.f("MS"), x.f("EPS"), x.f("DZL"), kl_scale,
+                           x.f("DMS"), x.f("SWMS"), x.f("DH")};
+        SND_TRY(launch_small_head_bwd(a, x.s));
+      } else {
+        ReparamBwdArgs a{x.f("MS"), 2 * L, RH, L, x.f("EPS"), x.f("DZL"), nullptr, nullptr, 0.f,
+                         kl_scale, x.f("DMS"), 2 * L};
+        SND_TRY(launch_reparam_bwd(a, x.s));
+      }
     } else {
       ReparamBwdArgs a{x.f("MS"), 2 * L, R, L, x.f("EPS"), x.f("DZDEC"), x.f("DJD"), x.f("EJ"),
                        adj_scale, kl_scale, x.f("DMS"), 2 * L};
       SND_TRY(launch_reparam_bwd(a, x.s));
     }
-    SND_TRY(gemm_wgrad(x, x.f("Hh"), gh, gh, true, x.f("DMS"), 2 * L, 2 * L, x.f("SWMS"), p.sWms, RH));
-    SND_TRY(gemm_fwd(x, RH, gh, 2 * L, x.f("DMS"), 2 * L, x.w("enc.Wms"), 2 * L, B_COL, x.f("DH"), gh,
-                     nullptr));
+    if (!p.small_head) {
+      SND_TRY(gemm_wgrad(x, x.f("Hh"), gh, gh, true, x.f("DMS"), 2 * L, 2 * L, x.f("SWMS"), p.sWms, RH));
+      SND_TRY(gemm_fwd(x, RH, gh, 2 * L, x.f("DMS"), 2 * L, x.w("enc.Wms"), 2 * L, B_COL, x.f("DH"), gh,
+                       nullptr));
+    }
     if (p.sg) {
       SND_TRY(encoder_sg_bwd(x, batch));
     } else if (p.tref) {   // dWh written complete; dG = dh Wh^T per graph
@@ -1738,7 +1760,8 @@ extern "C" int snd_train_step(const snd_plan_t* plan, const snd_batch_t* batch,
     rd.push_back({x.f("PHN"), x.g("dec.Wn"), nh, n2 * nf, (long long)hn, 1.f, 0});
     rd.push_back({x.f("PHN") + n2 * nf, x.g("dec.bn"), nh, nf, (long long)hn, 1.f, 0});
   }
-  const int n_kl = (p.fast && !p.tref) ? reparam_prep_blocks(p.B, zzt_npad(N)) : reparam_blocks(RH, L);
+  const int n_kl = (p.fast && !p.tref) ? reparam_prep_blocks(p.B, zzt_npad(N))
+                   : (p.small_head ? small_head_fwd_blocks(L) : reparam_blocks(RH, L));
   FinalizeArgs fa{x.d("PZZT"), zzt_dense_blocks(p.B, N, c.dtype), x.d("PEDGE"),
                   p.head_bwd ? head_tiles(R) : (p.fast ? edge_bf16_blocks(R) : edge_blocks(R, dj)),
                   x.d("PKL"), n_kl, x.d(p.dec_fused ? "PDSSES" : "PSSES"),

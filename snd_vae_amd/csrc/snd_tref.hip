@@ -70,12 +70,10 @@ __device__ __forceinline__ float adam_lrt(const AdamFuse& f) {
 // so a row's update does not wait a memory round trip of its own)
 __device__ __forceinline__ void adam4(const AdamFuse& f, float lrt, long long i, const float4& g,
                                       float4 p, float4 m, float4 v) {
-#define SND_ADAM_C(c)                                        \
-  m.c = f.b1 * m.c + (1.f - f.b1) * g.c;                     \
-  v.c = f.b2 * v.c + (1.f - f.b2) * g.c * g.c;               \
-  p.c -= lrt * m.c * __builtin_amdgcn_rcpf(__builtin_amdgcn_sqrtf(v.c) + f.eps);
-  SND_ADAM_C(x) SND_ADAM_C(y) SND_ADAM_C(z) SND_ADAM_C(w)
-#undef SND_ADAM_C
+  adam_elem(p.x, m.x, v.x, g.x, f.b1, f.b2, f.eps, lrt);
+  adam_elem(p.y, m.y, v.y, g.y, f.b1, f.b2, f.eps, lrt);
+  adam_elem(p.z, m.z, v.z, g.z, f.b1, f.b2, f.eps, lrt);
+  adam_elem(p.w, m.w, v.w, g.w, f.b1, f.b2, f.eps, lrt);
   // streamed once per step: non-temporal stores (no L2 / Infinity Cache allocation)
   st_nt(f.m + i, m);
   st_nt(f.v + i, v);
@@ -414,15 +412,10 @@ __global__ void __launch_bounds__(256) adam_vec_kernel(float4* p, const float4* 
   const float lrt = (float)lr_t;
   for (long long i = i0; i < n4; i += st) {
     if (i != i0) { gi = g[i]; mi = m[i]; vi = v[i]; pi = p[i]; }
-#define SND_ADAM_LANE(c)                                   \
-    {                                                      \
-      const float gc = gi.c * gscale;                      \
-      mi.c = b1 * mi.c + (1.f - b1) * gc;                  \
-      vi.c = b2 * vi.c + (1.f - b2) * gc * gc;             \
-      pi.c -= lrt * mi.c * __builtin_amdgcn_rcpf(__builtin_amdgcn_sqrtf(vi.c) + eps);          \
-    }
-    SND_ADAM_LANE(x) SND_ADAM_LANE(y) SND_ADAM_LANE(z) SND_ADAM_LANE(w)
-#undef SND_ADAM_LANE
+    adam_elem(pi.x, mi.x, vi.x, __fmul_rn(gi.x, gscale), b1, b2, eps, lrt);
+    adam_elem(pi.y, mi.y, vi.y, __fmul_rn(gi.y, gscale), b1, b2, eps, lrt);
+    adam_elem(pi.z, mi.z, vi.z, __fmul_rn(gi.z, gscale), b1, b2, eps, lrt);
+    adam_elem(pi.w, mi.w, vi.w, __fmul_rn(gi.w, gscale), b1, b2, eps, lrt);
     m[i] = mi;
     v[i] = vi;
     p[i] = pi;
@@ -452,15 +445,10 @@ __global__ void __launch_bounds__(256) adam_ranges_kernel(float4* p, const float
   const double lr_t = (double)lr * sqrt(1.0 - pow((double)b2, t)) / (1.0 - pow((double)b1, t));
   const float lrt = (float)lr_t;
   if (i < 0) return;
-#define SND_ADAM_LANE(c)                                 \
-  {                                                      \
-    const float gc = gi.c * gscale;                      \
-    mi.c = b1 * mi.c + (1.f - b1) * gc;                  \
-    vi.c = b2 * vi.c + (1.f - b2) * gc * gc;             \
-    pi.c -= lrt * mi.c * __builtin_amdgcn_rcpf(__builtin_amdgcn_sqrtf(vi.c) + eps);          \
-  }
-  SND_ADAM_LANE(x) SND_ADAM_LANE(y) SND_ADAM_LANE(z) SND_ADAM_LANE(w)
-#undef SND_ADAM_LANE
+  adam_elem(pi.x, mi.x, vi.x, __fmul_rn(gi.x, gscale), b1, b2, eps, lrt);
+  adam_elem(pi.y, mi.y, vi.y, __fmul_rn(gi.y, gscale), b1, b2, eps, lrt);
+  adam_elem(pi.z, mi.z, vi.z, __fmul_rn(gi.z, gscale), b1, b2, eps, lrt);
+  adam_elem(pi.w, mi.w, vi.w, __fmul_rn(gi.w, gscale), b1, b2, eps, lrt);
   m[i] = mi;
   v[i] = vi;
   p[i] = pi;
