@@ -950,13 +950,13 @@ int head_fwd_fused(const Ctx& x, const snd_batch_t* batch, const float* eps, uns
 
 int encoder_fast_bwd_tail(const Ctx& x, const snd_batch_t* batch, bool enc1_done = false);
 
-// encoder backward: reparam -> heads -> GCN1 -> GCN0 (all weight gradients as slabs)
-int encoder_fast_bwd(const Ctx& x, const snd_batch_t* batch, float adj_scale, float kl_scale) {
+// the fused backward head alone (encoder_fast_bwd; snd_plan_launch "head_bwd")
+int head_bwd_fused(const Ctx& x, const snd_batch_t* batch, float adj_scale, float kl_scale) {
   const snd_plan& p = *x.p;
   const snd_config_t& c = p.c;
-  const int R = p.R, L = c.latent, f = c.f_in, h0 = c.h0, h1 = c.h1, gh = c.g_hidden, W = p.W;
+  const int R = p.R, L = c.latent, f = c.f_in, h1 = c.h1, gh = c.g_hidden, W = p.W;
   auto bf = [&](const char* n) { return reinterpret_cast<__bf16*>(x.f(n)); };
-  if (p.head_bwd) {
+  {
     HeadBwdArgs a{};
     a.rowptr = batch->rowptr; a.colidx = batch->colidx; a.R = R;
     a.zb = bf("ZB"); a.L = L; a.pos_weight = c.pos_weight; a.edge_part = x.d("PEDGE");
@@ -972,7 +972,18 @@ int encoder_fast_bwd(const Ctx& x, const snd_batch_t* batch, float adj_scale, fl
     a.p1 = x.f("FP1"); a.x = batch->features; a.ldx = f;
     a.dp1 = bf("FDP1"); a.enc1_part = x.f("PFENC1");
     a.npg = p.N; a.ngraphs = p.B; a.dbg = debug_flags();
-    SND_TRY(launch_head_bwd(a, x.s));
+    return launch_head_bwd(a, x.s);
+  }
+}
+
+// encoder backward: reparam -> heads -> GCN1 -> GCN0 (all weight gradients as slabs)
+int encoder_fast_bwd(const Ctx& x, const snd_batch_t* batch, float adj_scale, float kl_scale) {
+  const snd_plan& p = *x.p;
+  const snd_config_t& c = p.c;
+  const int R = p.R, L = c.latent, f = c.f_in, h0 = c.h0, h1 = c.h1, gh = c.g_hidden, W = p.W;
+  auto bf = [&](const char* n) { return reinterpret_cast<__bf16*>(x.f(n)); };
+  if (p.head_bwd) {
+    SND_TRY(head_bwd_fused(x, batch, adj_scale, kl_scale));
     SND_TRY(wgrad(x, wg_args(p, x.ws, p.gWms, bf("FHH"), gh, gh, bf("FDMS"), 2 * L, 2 * L, x.f("FSWMS"), 1), x.s));
     SND_TRY(wgrad(x, wg_args(p, x.ws, p.gWh, bf("FG"), p.ldg, W, bf("FDH"), gh, gh, x.f("FSWH"), 1), x.s));
     return encoder_fast_bwd_tail(x, batch, true);
@@ -1407,6 +1418,13 @@ extern "C" int snd_plan_launch(const snd_plan_t* plan, const snd_batch_t* batch,
     std::vector<WgArgs> q = p.last_wq;
     for (auto& w : q) w.dbg = debug_flags();
     return launch_wgrad_multi(q.data(), (int)q.size(), s);
+  }
+  if (!strcmp(kernel, "head_bwd")) {   // fused backward head (the step's scales)
+    SND_CHECK_ARG(p.head_bwd && p.last_params, "snd_plan_launch: head_bwd needs a fused-head step first");
+    Ctx x{&p, ws, p.last_params, p.last_grads, s};
+    const double pairs = (double)p.B * p.N * (double)p.N;
+    return head_bwd_fused(x, batch, (float)(2.0 * (double)p.c.norm / pairs),
+                          (float)((double)p.c.beta / ((double)p.RH * p.c.latent)));
   }
   if (!strcmp(kernel, "head_fwd")) {   // fused encoder forward tail (device eps, seed 0)
     SND_CHECK_ARG(p.head_fused && p.last_params, "snd_plan_launch: head_fwd needs a fused-head step first");
