@@ -833,6 +833,9 @@ size_t rc_lds_bytes(int T, int kp, int np) {
   return (xch * 8 + (size_t)T * np * kp) * 2;
 }
 
+#ifndef SND_RC_FILL
+#define SND_RC_FILL 256   // row-engine workgroups the column windows aim for (A/B: -DSND_RC_FILL=512)
+#endif
 int rc_cols_per_block(int T, int kp, int np) {
   for (int s = cdiv(np, 128); s <= 8; ++s) {
     const int npb = (int)round_up(cdiv(np, s), 16);
@@ -858,7 +861,7 @@ int launch_rowconv(const RcArgs& a0, int epi, hipStream_t s) {
   // windows split further, down to 32 columns (debug bit 1 << 19: off)
   for (;;) {
     const int nb = (int)round_up(cdiv(a.npb, 2), 16);
-    if ((a.dbg & (1 << 19)) || rc_blocks(a.R) * cdiv(a.np, a.npb) >= 256 || nb < 32 || nb >= a.npb) break;
+    if ((a.dbg & (1 << 19)) || rc_blocks(a.R) * cdiv(a.np, a.npb) >= SND_RC_FILL || nb < 32 || nb >= a.npb) break;
     a.npb = nb;
   }
   SND_CHECK_ARG(a.x && a.wpk && a.out && a.zero && a.x_bf16, "rowconv: null operand / fp32 x");
