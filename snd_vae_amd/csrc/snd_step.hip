@@ -329,7 +329,10 @@ extern "C" int snd_plan_create(const snd_config_t* cfg, int n_graphs, snd_plan_t
   // slower, 43 vs 29 us at C2: a workgroup's 128-row units are one DMA round trip each.
   // Under 32768 rows (C5's one N = 16384 graph) 32 chunks: half the slab bytes for the
   // reduction, still >= 384 workgroups (C5 step 0.417 vs 0.403 ms).
-  const int wgc = (dbg & (4096 | 8192)) ? 0 : (((dbg & 16384) || R < 32768) ? 32 : 64);
+#ifndef SND_WGC_SMALL
+#define SND_WGC_SMALL 32   // A/B builds: -DSND_WGC_SMALL=16
+#endif
+  const int wgc = (dbg & (4096 | 8192)) ? 0 : ((dbg & 16384) ? 32 : (R < 32768 ? SND_WGC_SMALL : 64));
   auto wgc_of = [&](int, int, int) { return wgc; };
   // ---- bf16 fast decoder: split [s | n] column layouts, packed weight images
   if (c.dtype == SND_BF16 && !sg && !(debug_flags() & 256)) {
