@@ -169,14 +169,16 @@ def _step_from_powers(b1p, b2p, beta1: float, beta2: float) -> Optional[int]:
     beta1^(t+1); the step counter here holds t (Adam's step k uses beta^k).
     beta1_power leaves the float32 normal range after ~830 steps and flushes to
     0 near ~980, so the beta2 power (0.999^(t+1), normal until t ~ 87 K) is used
-    whenever beta1_power is subnormal or zero."""
+    whenever beta1_power is subnormal or zero.  TF multiplies by float32(beta)
+    (0.999 -> 0.99900001287), so the logarithm is taken of that float32 value:
+    with float64 0.999 the estimate drifts by a whole step from t ~ 39 K."""
     for p, beta in ((b1p, beta1), (b2p, beta2)):
         if p is None:
             continue
         val = float(np.asarray(p, dtype=np.float64))
         if not (val >= _F32_TINY) or val > 1.0:
             continue
-        return int(round(np.log(val) / np.log(beta))) - 1
+        return int(round(np.log(val) / np.log(float(np.float32(beta))))) - 1
     if b1p is not None or b2p is not None:
         raise ValueError("beta1_power and beta2_power are both zero or subnormal: the global step "
                          "cannot be recovered; pass global_step")
@@ -203,9 +205,23 @@ def blocks_to_reference(cfg: SNDConfig, blocks: dict, adam_m: Optional[dict] = N
             out[scope + "moving_mean"] = np.zeros_like(out[name])
             out[scope + "moving_variance"] = np.ones_like(out[name])
     if global_step is not None:                      # TF1: beta^(t+1) after t steps
-        out["beta1_power"] = np.float32(beta1 ** (global_step + 1))
-        out["beta2_power"] = np.float32(beta2 ** (global_step + 1))
+        out["beta1_power"] = tf_power(beta1, global_step)
+        out["beta2_power"] = tf_power(beta2, global_step)
     return out
+
+
+def tf_power(beta: float, steps: int) -> np.float32:
+    """TF1 Adam's bias-correction power after `steps` applies: float32(beta) times
+    float32(beta) `steps` times, every product rounded to float32 (optimizer.py:125,197;
+    the variable starts at beta).  Past 2^18 steps (both powers long subnormal) the
+    float64 closed form."""
+    b = np.float32(beta)
+    if steps > (1 << 18):
+        return np.float32(float(b) ** (steps + 1))
+    p = b
+    for _ in range(steps):
+        p = np.float32(p * b)
+    return p
 
 
 def load_reference(path: str, model, optimizer=None,

@@ -47,11 +47,13 @@ class OptimizerVAE:
         (snd_plan_set_rng_offset), so the ranks draw the normals one device would
         draw for the whole batch.
 
-        bucketed (default: on with a process group): the exchange of
-        parallel.run_buckets instead of one all-reduce of the whole gradient; a model
-        without early completion points or large blocks (C2) has one bucket, i.e. the
-        same single all-reduce.  shard_min: floats from which a bucket is sharded
-        (parallel.SHARD_MIN)."""
+        bucketed (default OFF, opt-in): the exchange of parallel.run_buckets instead of
+        one all-reduce of the whole gradient; a model without early completion points or
+        large blocks (C2) has one bucket, i.e. the same single all-reduce.  Its
+        side-stream overlap of early buckets with the backward pass has been checked
+        bit for bit at world 1 (RCCL) and world 2 (gloo, CPU) only, never on 2+ GPUs, so
+        the default stays the single all-reduce.  shard_min: floats from
+        which a bucket is sharded (parallel.SHARD_MIN)."""
         cfg = model.cfg
         self.model = model
         self.lr = cfg.learning_rate if learning_rate is None else learning_rate
@@ -103,10 +105,35 @@ class OptimizerVAE:
         # host copies for snd_adam_tf1_ranges (read at call time, so the arrays outlive it)
         self._roff = (C.c_longlong * max(1, len(self._adam_ranges)))(*[o for o, _ in self._adam_ranges])
         self._rcnt = (C.c_longlong * max(1, len(self._adam_ranges)))(*[n for _, n in self._adam_ranges])
-        self.bucketed = self.distributed and (bucketed is None or bool(bucketed))
+        self.bucketed = self.distributed and bool(bucketed)
         self.buckets = []
+        self._events = {}
+        # the plan records raw hipEvent_t pointers for the early buckets: drop whatever a
+        # previous optimizer of this plan registered (its torch events may be freed)
+        self._unregister_events()
         if self.bucketed:
             self._init_buckets(shard_min)
+
+    def _unregister_events(self):
+        plan = getattr(self.model, "plan", None)
+        if plan is None:
+            return
+        L = _lib.lib()
+        for i in range(len(self.model.layout.shapes)):
+            L.snd_plan_grad_event(plan, i, None)
+
+    def close(self):
+        """Unregister this optimizer's completion events from the plan (idempotent);
+        called by __del__, so a freed optimizer never leaves dangling events behind."""
+        if getattr(self, "_events", None):
+            self._unregister_events()
+            self._events = {}
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
     def _init_buckets(self, shard_min):
         """Bucket plan, completion events and chunk buffers of the bucketed exchange."""
@@ -128,7 +155,6 @@ class OptimizerVAE:
                                     SHARD_MIN if shard_min is None else shard_min)
         # one event per early point, recorded by snd_train_step after the kernel that
         # completes it (created now: torch creates events lazily on their first record)
-        self._events = {}
         for i, pt in enumerate(points):
             if pt and any(b.point == pt for b in self.buckets):
                 if pt not in self._events:
@@ -291,11 +317,17 @@ class OptimizerVAE:
         return int(self.step_counter.item())
 
     def grad_blocks(self):
-        """Flat gradient by block (fused-Adam blocks are updated in the step, not stored)."""
+        """Flat gradient by block (fused-Adam blocks are updated in the step, not stored).
+
+        With sharded buckets (bucketed exchange) only this rank's chunk of each sharded
+        bucket holds the reduced gradient; the rest of such a bucket is this rank's local,
+        unreduced gradient."""
         m = self.model
         return m.layout.unpack(self.grads[:m.param_count].double().cpu().numpy())
 
     def state_blocks(self):
+        """Adam moments by block.  COLLECTIVE under the bucketed exchange (sync_state
+        all-gathers the sharded moments): call it on every rank, not on rank 0 only."""
         self.sync_state()
         m = self.model
         pc = m.param_count

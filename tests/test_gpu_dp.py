@@ -89,6 +89,6 @@ def test_c2_distributed_is_one_allreduce(pg):
     from snd_vae_amd.model import SGCNModelVAE
     from snd_vae_amd.optimizer import OptimizerVAE
     m = SGCNModelVAE(tscale(4096, 64), 8, dtype="bf16")
-    o = OptimizerVAE(m, process_group=pg)
+    o = OptimizerVAE(m, process_group=pg, bucketed=True)
     assert [(b.lo, b.hi, b.point, b.sharded) for b in o.buckets] == [(0, m.param_count + 8, 0, False)]
     assert o._comm is None

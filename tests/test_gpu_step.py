@@ -282,7 +282,7 @@ def test_forced_world1_process_group_runs_the_distributed_step():
         batch = synthetic_batch(cfg, 2, seed=4)
         p0 = init_blocks(cfg, 0)
         ma = SGCNModelVAE(cfg, 2, dtype="bf16", blocks=p0)
-        oa = OptimizerVAE(ma, process_group=dist.group.WORLD)
+        oa = OptimizerVAE(ma, process_group=dist.group.WORLD, bucketed=True)
         assert oa.distributed and not oa.fused
         mb, ob, bb = make(cfg, batch, p0, "bf16", fuse_adam=False)
         ba = DeviceBatch(batch)

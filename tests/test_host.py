@@ -230,11 +230,13 @@ def test_reference_adam_power_convention():
     fresh["beta1_power"] = np.float32(0.9)
     fresh["beta2_power"] = np.float32(0.999)
     assert checkpoint.reference_to_blocks(cfg, fresh)[3] == 0
-    for t in (1, 5, 829, 1500, 20000):
+    for t in (1, 5, 829, 1500, 20000, 50000, 86000):
         st = dict(ref0)
-        st["beta1_power"] = np.float32(0.9) ** np.float32(t + 1)     # float32 like TF
-        st["beta2_power"] = np.float32(np.float64(0.999) ** (t + 1))
+        # as TF builds them: repeated float32 multiplication by float32(beta)
+        st["beta1_power"] = checkpoint.tf_power(0.9, t)
+        st["beta2_power"] = checkpoint.tf_power(0.999, t)
         assert checkpoint.reference_to_blocks(cfg, st)[3] == t, t
+        assert checkpoint.blocks_to_reference(cfg, b, m, m, global_step=t)["beta2_power"] == st["beta2_power"]
     dead = dict(ref0)
     dead["beta1_power"] = np.float32(0.0)
     dead["beta2_power"] = np.float32(0.0)
