@@ -1071,6 +1071,335 @@ __global__ void __launch_bounds__(NTH2) zzt_dense_bf16_v4(ZztArgs a) {
   }
 }
 
+// ---------------------------------------------------------------- bf16 MFMA, v8 (d <= 64)
+// v8: ONE wave per SIMD (256-thread workgroup, up to 512 registers per lane) that
+// interleaves its own epilogue VALU with its own MFMAs (MI355X_MICROARCH.md constants,
+// 'single-issue instructions HIDDEN per v_mfma_f32_32x32x16_bf16 gap': a gap of 32
+// cycles hides ~24 cycles of issue).  v4's four waves per SIMD ran the matrix phase
+// and the VALU phase of a tile back to back (2,432 VALU + 1,024 MFMA cycles per tile
+// and SIMD = the measured 3,456): here the per-block software pipeline puts every
+// MFMA next to independent VALU of the same wave.
+//
+// Work split: wave w owns rows i0 + 32 w .. +31 of the workgroup's 128 rows and ALL
+// four 32-column blocks of every 128-column tile (no cross-wave combine of partial
+// dJ).  Logit block k = 4 t + cb; per block, in one straight-line region:
+//   fwd(k+1)  Y'[j][i] = -x_ij        4 MFMAs, A = z_j rows (LDS), B = -z_i (REGISTERS)
+//   epi(k)    sigma, log2 of quad products, sign count (v4's EPI 0, same arithmetic)
+//   bwd(k-1)  dJ'[i][c] += S'[i][j] z_j[c]   4 MFMAs, A = S' (registers), B = z^T (LDS)
+// so each 32x32 block's epilogue runs beside 8 MFMAs it does not depend on.
+// LDS: v4's two images per tile, triple-buffered; the tile barrier sits after block
+// cb0 of tile t (the last reader of tile t-1, bwd(t-1, cb3), is done), then tile t+2
+// is stored from registers into t-1's buffer and tile t+3 is loaded into registers.
+// Results: v4's per-logit arithmetic in v4's order per (i, j); the dJ sums run over
+// j in the same k order per 32-column block, blocks in ascending order (v4 summed the
+// four column blocks' partials at the end: dJ differs from v4 by fp32 reassociation).
+// SCHED 1 shapes each block with sched_group_barrier (MFMA, then VALU fillers).
+template <int DP, int SCHED>
+__global__ void __launch_bounds__(256) zzt_dense_bf16_v8(ZztArgs a) {
+  constexpr int NT = 256, NW = 4;
+  constexpr int KS = DP / 16;          // forward k-steps
+  constexpr int CB = DP / 32;          // backward 32-column output blocks
+  constexpr int JST = DP + 8;          // J / row image stride (elements)
+  constexpr int TST = TJ2 + 8;         // z^T image stride
+  constexpr int JS = TJ2 * JST;
+  constexpr int TS = DP * TST;
+  constexpr int BUF = JS + TS;
+  constexpr int CPR = DP / 8, TCPR = TJ2 / 8;
+  constexpr int JCH = TJ2 * CPR, TCH = DP * TCPR;
+  constexpr int JPT = (JCH + NT - 1) / NT, TPT = (TCH + NT - 1) / NT;
+  __shared__ __attribute__((aligned(16))) __bf16 lds[3 * BUF];
+  __shared__ __attribute__((aligned(16))) __bf16 zown[ROWS * JST];    // z_i rows (z^T values)
+  __shared__ float colsum[DP];
+  __shared__ float csred[NT / DP][DP];
+  __shared__ float dsg[NW][32];
+  __shared__ double sl[NW];
+  __shared__ unsigned sc[NW];
+
+  const int wgs = a.ngraphs * (a.npad / ROWS);
+  const int sp = blockIdx.x / wgs, bx = blockIdx.x - sp * wgs;
+  const int nsplit = gridDim.x / wgs;
+  const int g = bx % a.ngraphs, rb = bx / a.ngraphs;
+  const __bf16* Jg = reinterpret_cast<const __bf16*>(a.jrow) + (long long)g * a.npad * DP;
+  const __bf16* JTg = reinterpret_cast<const __bf16*>(a.jt) + (long long)g * DP * a.npad;
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, r = lane & 31, h = lane >> 5;
+  const int i0 = __builtin_amdgcn_readfirstlane(rb * ROWS + 32 * w);
+  const int i_me = i0 + r;
+  const int ntot = a.npad / TJ2;
+  const int t0 = sp * ntot / nsplit, t1 = (sp + 1) * ntot / nsplit;
+
+  uint4 rj[JPT], rt[TPT];
+  auto gload = [&](int t) {
+#pragma unroll
+    for (int p = 0; p < JPT; ++p) {
+      const int idx = tid + p * NT;
+      if (JCH % NT == 0 || idx < JCH) {
+        const int row = idx / CPR, ch = idx - row * CPR;
+        rj[p] = *reinterpret_cast<const uint4*>(Jg + (long long)(t * TJ2 + row) * DP + ch * 8);
+      }
+    }
+#pragma unroll
+    for (int p = 0; p < TPT; ++p) {
+      const int idx = tid + p * NT;
+      if (TCH % NT == 0 || idx < TCH) {
+        const int c = idx / TCPR, ch = idx - c * TCPR;
+        rt[p] = *reinterpret_cast<const uint4*>(JTg + (long long)c * a.npad + t * TJ2 + ch * 8);
+      }
+    }
+  };
+  // J rows: [row][k].  z^T: row c holds, per 32-j block jb and k-step s, chunk
+  // 4 jb + 2 s + h = {j = 32 jb + 16 s + 4 h + 0..3, + 8 + 0..3} (the k order of
+  // the packed S' operand) -- v4's layout
+  auto sstore = [&](__bf16* L) {
+#pragma unroll
+    for (int p = 0; p < JPT; ++p) {
+      const int idx = tid + p * NT;
+      if (JCH % NT == 0 || idx < JCH) {
+        const int row = idx / CPR, ch = idx - row * CPR;
+        *reinterpret_cast<uint4*>(&L[row * JST + ch * 8]) = rj[p];
+      }
+    }
+#pragma unroll
+    for (int p = 0; p < TPT; ++p) {
+      const int idx = tid + p * NT;
+      if (TCH % NT == 0 || idx < TCH) {
+        const int c = idx / TCPR, ch = idx - c * TCPR;
+        const int jb = ch >> 2, m = ch & 3, s = m >> 1, a8 = (m & 1) * 4;
+        __bf16* row = &L[JS + c * TST + (4 * jb + 2 * s) * 8 + a8];
+        *reinterpret_cast<uint2*>(row) = make_uint2(rt[p].x, rt[p].y);
+        *reinterpret_cast<uint2*>(row + 8) = make_uint2(rt[p].z, rt[p].w);
+      }
+    }
+  };
+
+  // ---- prologue: tiles t0, t0+1 staged, t0+2 in registers; the wave's -z_i rows in
+  // registers (the forward B operand); z_i^T columns -> zown; graph column sums
+  gload(t0);
+  bf16x8 zi[KS];   // -z_i (scaled): row i0 + r, k = 16 s + 8 h .. + 7
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+    const uint4 u = *reinterpret_cast<const uint4*>(Jg + (long long)(i0 + r) * DP + 16 * s + 8 * h);
+    const uint4 v = make_uint4(u.x ^ 0x80008000u, u.y ^ 0x80008000u, u.z ^ 0x80008000u, u.w ^ 0x80008000u);
+    zi[s] = __builtin_bit_cast(bf16x8, v);
+  }
+  for (int idx = tid; idx < DP * (ROWS / 8); idx += NT) {   // z^T[c][rb*128 + 8u ..] -> zown[i][c]
+    const int c = idx / (ROWS / 8), u = idx - c * (ROWS / 8);
+    const bf16x8 v = *reinterpret_cast<const bf16x8*>(JTg + (long long)c * a.npad + rb * ROWS + 8 * u);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) zown[(8 * u + e) * JST + c] = v[e];
+  }
+  {   // graph column sums S_k = sum_j zs_jk (fixed order over the 64-row partials)
+    const int nrb = a.npad / 64;
+    const int k = tid % DP, grp = tid / DP;
+    float s = 0.f;
+    for (int p = grp; p < nrb; p += NT / DP) s += a.colpart[((long long)g * nrb + p) * DP + k];
+    csred[grp][k] = s;
+  }
+  sstore(lds);
+  gload(min(t0 + 1, t1 - 1));
+  sstore(lds + BUF);
+  gload(min(t0 + 2, t1 - 1));
+  // buffer 2's z^T image is read (times S' = 0) by the first block's bwd(t0 - 1): finite
+  for (int idx = tid; idx < TS / 8; idx += NT)
+    *reinterpret_cast<uint4*>(&lds[2 * BUF + JS + 8 * idx]) = make_uint4(0u, 0u, 0u, 0u);
+  __syncthreads();
+  if (tid < DP) {
+    float s = 0.f;
+    for (int p = 0; p < NT / DP; ++p) s += csred[p][tid];
+    colsum[tid] = s;
+  }
+
+  f32x16 acc[CB];
+#pragma unroll
+  for (int q = 0; q < CB; ++q)
+#pragma unroll
+    for (int v = 0; v < 16; ++v) acc[q][v] = 0.f;
+  // operands are read from LDS one block before the MFMAs that use them (one wave per
+  // SIMD: nothing else hides the LDS latency)
+  struct FOp { bf16x8 v[KS]; };
+  struct BOp { bf16x8 v[2][CB]; };
+  auto fload = [&](const __bf16* L, int cb) {
+    FOp o;
+    const int j = 32 * cb + r;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) o.v[s] = *reinterpret_cast<const bf16x8*>(&L[j * JST + (2 * s + h) * 8]);
+    return o;
+  };
+  auto bload = [&](const __bf16* L, int cb) {
+    BOp o;
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int q = 0; q < CB; ++q)
+        o.v[s][q] = *reinterpret_cast<const bf16x8*>(&L[JS + (32 * q + r) * TST + (4 * cb + 2 * s + h) * 8]);
+    return o;
+  };
+  auto fwd = [&](const FOp& o) {
+    f32x16 X;
+#pragma unroll
+    for (int v = 0; v < 16; ++v) X[v] = 0.f;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) X = __builtin_amdgcn_mfma_f32_32x32x16_bf16(o.v[s], zi[s], X, 0, 0, 0);
+    return X;
+  };
+  auto bwd = [&](const BOp& o, const bf16x8 (&sA)[2]) {
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int q = 0; q < CB; ++q)
+        acc[q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(sA[s], o.v[s][q], acc[q], 0, 0, 0);
+  };
+  float lacc = 0.f;
+  double ltot = 0.0;
+  unsigned lcnt = 0;
+  // v4 EPI 0 on one 32x32 block (y = -x): sigma, one log2 per quad, sign count; the
+  // quad products' overflow fallback is a wave-uniform branch after the block's MFMAs
+  auto epi = [&](const f32x16& Y, bf16x8 (&sA)[2], float (&q)[16]) {
+    float lt = 0.f;
+#pragma unroll
+    for (int v = 0; v < 16; ++v) {
+      const float e = __builtin_amdgcn_exp2f(Y[v]);
+      q[v] = e + kZ4Q;
+      sA[v >> 3][v & 7] = (__bf16)__builtin_amdgcn_rcpf(q[v]);
+    }
+#pragma unroll
+    for (int g4 = 0; g4 < 4; ++g4) {
+      const unsigned t01 = __builtin_amdgcn_perm(__float_as_uint(Y[4 * g4 + 1]),
+                                                 __float_as_uint(Y[4 * g4]), 0x0C0C0703u);
+      const unsigned t23 = __builtin_amdgcn_perm(__float_as_uint(Y[4 * g4 + 3]),
+                                                 __float_as_uint(Y[4 * g4 + 2]), 0x07030C0Cu);
+      lcnt += (unsigned)__builtin_popcount((t01 | t23) & 0x80808080u);
+    }
+#pragma unroll
+    for (int p = 0; p < 4; ++p)
+      lt += __builtin_amdgcn_logf((q[4 * p] * q[4 * p + 1]) * (q[4 * p + 2] * q[4 * p + 3]));
+    return lt;
+  };
+  auto epi_fix = [&](const f32x16& Y, const float (&q)[16], float lt) {
+    if (__builtin_expect(__builtin_amdgcn_ballot_w64(!__builtin_isfinite(lt)) != 0, 0)) {
+      lt = 0.f;   // a quad product overflowed: the block one logit at a time (v4)
+#pragma unroll
+      for (int v = 0; v < 16; ++v) lt += Y[v] > 24.f ? Y[v] : __builtin_amdgcn_logf(q[v]);
+    }
+    lacc += lt;
+  };
+  auto shape = [&]() {
+    if constexpr (SCHED == 1) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // one MFMA
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);   // one DS read
+        __builtin_amdgcn_sched_group_barrier(0x002, 8, 0);   // VALU fillers
+      }
+    }
+  };
+
+  // pipeline state: Y = fwd(k), fA = operands of fwd(k + 1), bB = operands of
+  // bwd(k - 1), sPrev = S'(k - 1)
+  f32x16 Y = fwd(fload(lds, 0));
+  FOp fA = fload(lds, 1);
+  BOp bB = bload(lds + 2 * BUF, 3);   // zeroed image: bwd(t0 - 1) adds S' = 0 times 0
+  bf16x8 sPrev[2];
+#pragma unroll
+  for (int s = 0; s < 2; ++s)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) sPrev[s][e] = (__bf16)0.f;
+
+  // one block k = (tile of L, cb): fwd(k + 1) | loads for k + 2 and bwd(k) | epi(k) | bwd(k - 1)
+  auto block = [&](const __bf16* Lf2, int cbf2, const __bf16* Lk, int cb) {
+    float q[16];
+    bf16x8 sA[2];
+    const f32x16 Yn = fwd(fA);
+    const FOp fN = fload(Lf2, cbf2);
+    const BOp bN = bload(Lk, cb);
+    const float lt = epi(Y, sA, q);
+    bwd(bB, sPrev);
+    shape();
+    epi_fix(Y, q, lt);
+    Y = Yn;
+    fA = fN;
+    bB = bN;
+    sPrev[0] = sA[0];
+    sPrev[1] = sA[1];
+  };
+  // one tile; buffer indices compile-time (tile t in buffer CUR = (t - t0) % 3)
+  auto tile = [&](int t, auto cc) {
+    constexpr int CUR = decltype(cc)::value, NXT = (CUR + 1) % 3, PRV = (CUR + 2) % 3;
+    const __bf16* const Lc = lds + CUR * BUF;
+    const __bf16* const Ln = lds + NXT * BUF;
+    block(Lc, 2, Lc, 0);
+    __syncthreads();                   // every wave is past bwd(t - 1, 3): PRV is free
+    sstore(lds + PRV * BUF);           // tile t + 2
+    gload(min(t + 3, t1 - 1));
+    block(Lc, 3, Lc, 1);
+    block(Ln, 0, Lc, 2);               // tile t + 1: visible since the barrier above
+    block(Ln, 1, Lc, 3);
+  };
+  for (int t = t0; t < t1; t += 3) {
+    tile(t, std::integral_constant<int, 0>{});
+    if (t + 1 < t1) tile(t + 1, std::integral_constant<int, 1>{});
+    if (t + 2 < t1) tile(t + 2, std::integral_constant<int, 2>{});
+    ltot += (double)lacc;   // keep the fp32 partial sums short
+    lacc = 0.f;
+  }
+  bwd(bB, sPrev);
+
+  // ---- per-row corrections (row i_me; lanes r and r + 32 hold its two k halves)
+  float xd = 0.f, xs = 0.f;
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float bb = (float)zi[s][e];   // (-)z_i: the products below do not see the sign
+      xd += bb * bb;
+      xs += bb * colsum[16 * s + 8 * h + e];
+    }
+  }
+  xd += __shfl_xor(xd, 32, 64);
+  xs += __shfl_xor(xs, 32, 64);
+  xs = -xs;
+  const bool row_valid = i_me < a.n;
+  const bool corr = sp == 0;
+  const bool own = h == 0 && row_valid && corr;
+  const float exd = __builtin_amdgcn_exp2f(-fabsf(xd));
+  if (own) {   // + sum_j x_ij (softplus2(x) = x + log2(q)) - softplus2(x_ii)
+    ltot += (double)xs;
+    ltot -= (double)(fmaxf(xd, 0.f) + __builtin_amdgcn_logf(1.f + exd));
+  }
+  const unsigned dpos = (unsigned)__popcll(__ballot(own && xd > 0.f));
+  if (h == 0) {   // s'_ii as the backward MFMA consumed it (bf16), 0 outside split 0
+    const float sg = __builtin_amdgcn_rcpf(__builtin_amdgcn_exp2f(-xd) + kZ4Q);
+    dsg[w][r] = corr ? (float)(__bf16)sg : 0.f;
+  }
+  __syncthreads();
+  {
+    float* dst = (sp == 0 ? a.dJd : a.dJd_extra + (long long)(sp - 1) * a.ngraphs * a.n * a.d) +
+                 (long long)g * a.n * a.d;
+#pragma unroll
+    for (int q = 0; q < CB; ++q) {
+      const int c = 32 * q + r;
+#pragma unroll
+      for (int v = 0; v < 16; ++v) {
+        const int il = (v & 3) + 8 * (v >> 2) + 4 * h;   // D row within the wave's 32 rows
+        const int i = i0 + il;
+        if (i < a.n && c < a.d)
+          dst[(long long)i * a.d + c] = acc[q][v] - dsg[w][il] * (float)zown[(32 * w + il) * JST + c];
+      }
+    }
+  }
+  const double l = wave_sum_d(ltot);
+  const unsigned wcnt = wave_sum_u(lcnt);
+  if (lane == 0) { sl[w] = l; sc[w] = wcnt - dpos; }
+  __syncthreads();
+  if (tid == 0) {
+    double tl = 0.0, tc = 0.0;
+    for (int k = 0; k < NW; ++k) { tl += sl[k]; tc += (double)sc[k]; }
+    if (rb == 0 && corr)   // padded pairs of this graph: x = 0 exactly, softplus2(0) = 1 each
+      tl -= (double)a.npad * a.npad - (double)a.n * a.n;
+    a.part[2 * blockIdx.x] = tl * (double)kLn2;
+    a.part[2 * blockIdx.x + 1] = tc;
+  }
+}
+
 // ---------------------------------------------------------------- bf16 MFMA, v7 (d = 128)
 // v4's work split and signed (EPI 0) epilogue at d = 128, where v4's two LDS images
 // per tile (z rows and z^T, 2 x 35 KB) cannot be triple-buffered beside the
@@ -1501,6 +1830,14 @@ int launch_zzt_dense(const ZztArgs& a, int dtype, hipStream_t s, bool defer_spli
     if (dp == 32) hipLaunchKernelGGL((zzt_dense_bf16<32>), grid, dim3(NTH), 0, s, a);
     else if (dp == 64) hipLaunchKernelGGL((zzt_dense_bf16<64>), grid, dim3(NTH), 0, s, a);
     else hipLaunchKernelGGL((zzt_dense_bf16<128>), grid, dim3(NTH), 0, s, a);
+  } else if (dtype == SND_BF16 && dp <= 64 && (a.variant == 20 || a.variant == 21)) {   // v8 A/B
+    if (dp == 32) {
+      if (a.variant == 20) hipLaunchKernelGGL((zzt_dense_bf16_v8<32, 0>), grid, dim3(256), 0, s, a);
+      else hipLaunchKernelGGL((zzt_dense_bf16_v8<32, 1>), grid, dim3(256), 0, s, a);
+    } else {
+      if (a.variant == 20) hipLaunchKernelGGL((zzt_dense_bf16_v8<64, 0>), grid, dim3(256), 0, s, a);
+      else hipLaunchKernelGGL((zzt_dense_bf16_v8<64, 1>), grid, dim3(256), 0, s, a);
+    }
   } else if (dtype == SND_BF16 && dp <= 64 && (a.variant & 255) != 3) {   // v4 (default, d <= 64)
     // default: signed epilogue, plain tile order; A/B: variant 10 + 3 EPI + MODE;
     // variant >= 256: the measurement build of the default (phase skips / stamps)
