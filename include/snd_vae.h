@@ -211,6 +211,23 @@ int snd_zzt_ce(const float* z, int n_graphs, int n, int d,
                float norm, double* stats, float* dz, void* workspace,
                size_t workspace_bytes, int dtype, snd_stream_t stream);
 
+/* ---- a7/a10 row-sharded (SURVEY §8e "beyond DP": one N = 16384 graph over ranks) --
+ * The same CE and gradient for the rows [row0, row1) of ONE graph against all N
+ * columns (layers.py:407-409, optimizer.py:142-144 restricted to a row block):
+ *   z       [n, d] the whole graph's latent (all-gathered by the caller);
+ *   rowptr  [row1 - row0 + 1] the range's CSR row pointers (a slice of the graph's
+ *           CSR is fine: offsets index colidx), colidx global column ids;
+ *   stats[0] = sum CE over the range's rows x N pairs, stats[1] = #correct there;
+ *   dz [row1 - row0, d] = d(sum CE over ALL pairs)/dz for the range's rows -- L is
+ *   symmetric, so a rank's rows need no reduction across ranks.
+ * row0 % 128 == 0 and (row1 % 128 == 0 or row1 == n).  Summing stats over a
+ * partition of [0, n) gives snd_zzt_ce's stats for the graph. */
+size_t snd_zzt_ce_rows_workspace(int n, int d, int row0, int row1, int dtype);
+int snd_zzt_ce_rows(const float* z, int n, int d, int row0, int row1,
+                    const int* rowptr, const int* colidx, float pos_weight, float norm,
+                    double* stats, float* dz, void* workspace, size_t workspace_bytes,
+                    int dtype, snd_stream_t stream);
+
 /* ---- a11: sigmoid head + MSE ----------------------------------------------
  * Replaces tf.nn.sigmoid(linear(...)) (model_joint.py:121,144) and the
  * squared-difference means (optimizer.py:149,153) with their gradients:

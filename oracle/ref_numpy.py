@@ -153,6 +153,29 @@ def adj_ce(J, adj, n, pos_weight=1.0, norm=1.0, row_chunk=None, amb_tol=None):
     return ce, dJ, correct
 
 
+def adj_ce_rows(J, A, n, r0, r1, pos_weight=1.0, norm=1.0, row_chunk=1024):
+    """adj_ce of ONE graph restricted to its rows [r0, r1) (the row-sharded zz^T of
+    SURVEY §8e): (ce over the range's rows x n pairs, dJ rows [r1 - r0, d] of the
+    whole sum's gradient, #correct over the range).  Over a partition of [0, n) the
+    ce and correct sum to adj_ce's and the dJ rows concatenate to its dJ."""
+    ce, correct = 0.0, 0
+    dJ = np.zeros((r1 - r0, J.shape[1]))
+    for lo in range(r0, r1, row_chunk):
+        hi = min(r1, lo + row_chunk)
+        L = J[lo:hi] @ J.T
+        Ab = _dense_rows(A, lo, hi)
+        off = np.ones(L.shape, dtype=bool)
+        off[np.arange(hi - lo), np.arange(lo, hi)] = False
+        sp = softplus(L)
+        term = (pos_weight * Ab * (sp - L) + (1.0 - Ab) * sp) * norm
+        ce += term[off].sum() + (hi - lo) * SOFTPLUS_M1 * norm
+        g = norm * (sigmoid(L) * (1.0 + Ab * (pos_weight - 1.0)) - Ab * pos_weight)
+        g[~off] = 0.0
+        dJ[lo - r0:hi - r0] = 2.0 * (g @ J)
+        correct += int((((L > 0) & off) == (Ab > 0)).sum())
+    return ce, dJ, correct
+
+
 # ----------------------------------------------------------------- model
 def forward_backward(p: Dict[str, np.ndarray], adj, X, Xf, S, eps, cfg,
                      want_grads=True, row_chunk=None, amb_tol=None):

@@ -95,6 +95,9 @@ _SIGS = {
     "snd_zzt_ce_workspace": (c_size, [c_int, c_int, c_int, c_int]),
     "snd_zzt_ce": (c_int, [vp, c_int, c_int, c_int, vp, vp, c_float, c_float, vp, vp, vp,
                            c_size, c_int, vp]),
+    "snd_zzt_ce_rows_workspace": (c_size, [c_int, c_int, c_int, c_int, c_int]),
+    "snd_zzt_ce_rows": (c_int, [vp, c_int, c_int, c_int, c_int, vp, vp, c_float, c_float, vp,
+                                vp, vp, c_size, c_int, vp]),
     "snd_sigmoid_mse_blocks": (c_int, [c_int]),
     "snd_sigmoid_mse": (c_int, [vp, c_int, c_int, c_int, vp, vp, c_int, vp, c_int, vp, vp,
                                 vp, c_int, vp, vp, vp, c_size, vp]),

@@ -124,7 +124,7 @@ __global__ void __launch_bounds__(256) edge_kernel(EdgeArgs a) {
     float4 zi[NV], acc[NV];
 #pragma unroll
     for (int v = 0; v < NV; ++v) {
-      zi[v] = *reinterpret_cast<const float4*>(a.z + (long long)r * a.d + 4 * (sub + LPR * v));
+      zi[v] = *reinterpret_cast<const float4*>(a.z + ((long long)a.row0 + r) * a.d + 4 * (sub + LPR * v));
       acc[v] = make_float4(0.f, 0.f, 0.f, 0.f);
     }
     const int s = a.rowptr[r], e = a.rowptr[r + 1];

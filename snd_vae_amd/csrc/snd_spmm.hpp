@@ -20,6 +20,7 @@ struct EdgeArgs {
   float pos_weight;
   float* ej;                    // [n_rows, d]
   double* part;                 // [blocks][2] = {loss, tp}
+  int row0 = 0;                 // z row of local row 0 (row-sharded zz^T): z_i = z[row0 + r]
 };
 int edge_blocks(int n_rows, int d);
 int launch_edge(const EdgeArgs& a, hipStream_t s);

@@ -43,6 +43,15 @@ constexpr int TJ = 64;      // columns per LDS tile
 constexpr int ROWS = 128;   // rows per workgroup
 constexpr int NTH = 512;
 
+// row blocks a launch covers (ZztArgs.nrb; 0 = every row block of the graphs)
+__host__ __device__ __forceinline__ int zrb(const ZztArgs& a) { return a.nrb ? a.nrb : a.npad / ROWS; }
+// pairs (i, j) of row block rb with i or j a padding row: the mask-free kernels evaluate
+// them as x = 0 (softplus2(0) = 1 each) and subtract them per row block
+__device__ __forceinline__ double zzt_padded_pairs(const ZztArgs& a, int rb) {
+  const int valid = max(0, min(ROWS, a.n - rb * ROWS));
+  return (double)ROWS * a.npad - (double)valid * a.n;
+}
+
 // ---------------------------------------------------------------- prep
 template <typename T, int DP>
 __global__ void __launch_bounds__(256) zzt_prep_kernel(const float* z, int n, int npad,
@@ -146,7 +155,7 @@ __global__ void __launch_bounds__(NTH) zzt_dense_bf16(ZztArgs a) {
   constexpr int JPT = (JCH + NTH - 1) / NTH, TPT = (TCH + NTH - 1) / NTH;
   __shared__ __attribute__((aligned(16))) __bf16 lds[2][JS + TS];
 
-  const int g = blockIdx.x % a.ngraphs, rb = blockIdx.x / a.ngraphs;
+  const int g = blockIdx.x % a.ngraphs, rb = a.rb0 + blockIdx.x / a.ngraphs;
   const __bf16* Jg = reinterpret_cast<const __bf16*>(a.jrow) + (long long)g * a.npad * DP;
   const __bf16* JTg = reinterpret_cast<const __bf16*>(a.jt) + (long long)g * DP * a.npad;
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, r = lane & 15, q4 = lane >> 4;
@@ -319,10 +328,10 @@ __global__ void __launch_bounds__(NTH2) zzt_dense_bf16_v3(ZztArgs a) {
   __shared__ float csred[NTH2 / DP][DP];
 
   // block -> (column split sp, graph g, row block rb)
-  const int wgs = a.ngraphs * (a.npad / ROWS);
+  const int wgs = a.ngraphs * zrb(a);
   const int sp = blockIdx.x / wgs, bx = blockIdx.x - sp * wgs;
   const int nsplit = gridDim.x / wgs;
-  const int g = bx % a.ngraphs, rb = bx / a.ngraphs;
+  const int g = bx % a.ngraphs, rb = a.rb0 + bx / a.ngraphs;
   const __bf16* Jg = reinterpret_cast<const __bf16*>(a.jrow) + (long long)g * a.npad * DP;
   const __bf16* JTg = reinterpret_cast<const __bf16*>(a.jt) + (long long)g * DP * a.npad;
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, r = lane & 15, q4 = lane >> 4;
@@ -522,8 +531,8 @@ __global__ void __launch_bounds__(NTH2) zzt_dense_bf16_v3(ZztArgs a) {
   if (tid == 0) {
     double tl = 0.0, tc = 0.0;
     for (int k = 0; k < NTH2 / 64; ++k) { tl += sl[k]; tc += (double)sc[k]; }
-    if (rb == 0 && corr)   // padded pairs of this graph: x = 0 exactly, log2(1 + 1) = 1 each
-      tl -= (double)a.npad * a.npad - (double)a.n * a.n;
+    if (corr)   // padded pairs of this row block: x = 0 exactly, log2(1 + 1) = 1 each
+      tl -= zzt_padded_pairs(a, rb);
     a.part[2 * blockIdx.x] = tl * (double)kLn2;
     a.part[2 * blockIdx.x + 1] = tc;
   }
@@ -544,7 +553,7 @@ __global__ void __launch_bounds__(NTH) zzt_dense_f32(ZztArgs a) {
   float* lds0 = dyn;
   float* lds1 = dyn + JS + TS;
 
-  const int g = blockIdx.x % a.ngraphs, rb = blockIdx.x / a.ngraphs;
+  const int g = blockIdx.x % a.ngraphs, rb = a.rb0 + blockIdx.x / a.ngraphs;
   const float* Jg = reinterpret_cast<const float*>(a.jrow) + (long long)g * a.npad * DP;
   const float* JTg = reinterpret_cast<const float*>(a.jt) + (long long)g * DP * a.npad;
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, r = lane & 15, q4 = lane >> 4;
@@ -733,10 +742,10 @@ __global__ void __launch_bounds__(NTH2) zzt_dense_bf16_v4(ZztArgs a) {
   const int skip = MEAS ? __builtin_amdgcn_readfirstlane(a.variant >> 8) : 0;
   unsigned long long ts[4] = {0, 0, 0, 0};
   if (skip & 32) ts[0] = __builtin_amdgcn_s_memrealtime();
-  const int wgs = a.ngraphs * (a.npad / ROWS);
+  const int wgs = a.ngraphs * zrb(a);
   const int sp = blockIdx.x / wgs, bx = blockIdx.x - sp * wgs;
   const int nsplit = gridDim.x / wgs;
-  const int g = bx % a.ngraphs, rb = bx / a.ngraphs;
+  const int g = bx % a.ngraphs, rb = a.rb0 + bx / a.ngraphs;
   const __bf16* Jg = reinterpret_cast<const __bf16*>(a.jrow) + (long long)g * a.npad * DP;
   const __bf16* JTg = reinterpret_cast<const __bf16*>(a.jt) + (long long)g * DP * a.npad;
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, r = lane & 31, h = lane >> 5;
@@ -1056,8 +1065,8 @@ __global__ void __launch_bounds__(NTH2) zzt_dense_bf16_v4(ZztArgs a) {
   if (tid == 0) {
     double tl = 0.0, tc = 0.0;
     for (int k = 0; k < NW; ++k) { tl += sl[k]; tc += (double)sc[k]; }
-    if (rb == 0 && corr)   // padded pairs of this graph: x = 0 exactly, softplus2(0) = 1 each
-      tl -= (double)a.npad * a.npad - (double)a.n * a.n;
+    if (corr)   // padded pairs of this row block: x = 0 exactly, softplus2(0) = 1 each
+      tl -= zzt_padded_pairs(a, rb);
     a.part[2 * blockIdx.x] = tl * (double)kLn2;
     a.part[2 * blockIdx.x + 1] = tc;
     if (skip & 32) {
@@ -1115,10 +1124,10 @@ __global__ void __launch_bounds__(256) zzt_dense_bf16_v8(ZztArgs a) {
   __shared__ double sl[NW];
   __shared__ unsigned sc[NW];
 
-  const int wgs = a.ngraphs * (a.npad / ROWS);
+  const int wgs = a.ngraphs * zrb(a);
   const int sp = blockIdx.x / wgs, bx = blockIdx.x - sp * wgs;
   const int nsplit = gridDim.x / wgs;
-  const int g = bx % a.ngraphs, rb = bx / a.ngraphs;
+  const int g = bx % a.ngraphs, rb = a.rb0 + bx / a.ngraphs;
   const __bf16* Jg = reinterpret_cast<const __bf16*>(a.jrow) + (long long)g * a.npad * DP;
   const __bf16* JTg = reinterpret_cast<const __bf16*>(a.jt) + (long long)g * DP * a.npad;
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, r = lane & 31, h = lane >> 5;
@@ -1393,8 +1402,8 @@ __global__ void __launch_bounds__(256) zzt_dense_bf16_v8(ZztArgs a) {
   if (tid == 0) {
     double tl = 0.0, tc = 0.0;
     for (int k = 0; k < NW; ++k) { tl += sl[k]; tc += (double)sc[k]; }
-    if (rb == 0 && corr)   // padded pairs of this graph: x = 0 exactly, softplus2(0) = 1 each
-      tl -= (double)a.npad * a.npad - (double)a.n * a.n;
+    if (corr)   // padded pairs of this row block: x = 0 exactly, softplus2(0) = 1 each
+      tl -= zzt_padded_pairs(a, rb);
     a.part[2 * blockIdx.x] = tl * (double)kLn2;
     a.part[2 * blockIdx.x + 1] = tc;
   }
@@ -1460,10 +1469,10 @@ __global__ void __launch_bounds__(NTH2) zzt_dense_bf16_v7(ZztArgs a) {
   // measurement only (MEAS, variant >> 8): 1 skips the epilogue, 2 the forward MFMAs,
   // 4 the backward MFMAs, 8 the tile DMAs (results wrong)
   const int skip = MEAS ? __builtin_amdgcn_readfirstlane(a.variant >> 8) : 0;
-  const int wgs = a.ngraphs * (a.npad / ROWS);
+  const int wgs = a.ngraphs * zrb(a);
   const int sp = blockIdx.x / wgs, bx = blockIdx.x - sp * wgs;
   const int nsplit = gridDim.x / wgs;
-  const int g = bx % a.ngraphs, rb = bx / a.ngraphs;
+  const int g = bx % a.ngraphs, rb = a.rb0 + bx / a.ngraphs;
   const __bf16* Jg = reinterpret_cast<const __bf16*>(a.jrow) + (long long)g * a.npad * DP;
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, r = lane & 31, h = lane >> 5;
   const int rg = w & 3, cb = w >> 2;
@@ -1732,18 +1741,19 @@ __global__ void __launch_bounds__(NTH2) zzt_dense_bf16_v7(ZztArgs a) {
   if (tid == 0) {
     double tl = 0.0, tc = 0.0;
     for (int k = 0; k < NW; ++k) { tl += sl[k]; tc += (double)sc[k]; }
-    if (rb == 0 && corr) tl -= (double)a.npad * a.npad - (double)a.n * a.n;
+    if (corr) tl -= zzt_padded_pairs(a, rb);
     a.part[2 * blockIdx.x] = tl * (double)kLn2;
     a.part[2 * blockIdx.x + 1] = tc;
   }
 }
 
 // dJd += sum of the column-split partials (fixed order)
-__global__ void zzt_split_sum_kernel(float* dJd, const float* extra, long long n, int nextra) {
+__global__ void zzt_split_sum_kernel(float* dJd, const float* extra, long long n, long long stride,
+                                     int nextra) {
   long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   for (; i < n; i += (long long)gridDim.x * blockDim.x) {
     float v = dJd[i];
-    for (int s = 0; s < nextra; ++s) v += extra[(long long)s * n + i];
+    for (int s = 0; s < nextra; ++s) v += extra[(long long)s * stride + i];
     dJd[i] = v;
   }
 }
@@ -1752,6 +1762,25 @@ __global__ void zzt_split_sum_kernel(float* dJd, const float* extra, long long n
 __global__ void zzt_combine_kernel(float* dz, const float* ej, long long n, float norm) {
   long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   for (; i < n; i += (long long)gridDim.x * blockDim.x) dz[i] = norm * (dz[i] + ej[i]);
+}
+
+// out = scale * (a + b)   (row-sharded combine: dJd rows of the range + edge terms)
+__global__ void zzt_combine2_kernel(float* out, const float* a, const float* b, long long n, float scale) {
+  long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  for (; i < n; i += (long long)gridDim.x * blockDim.x) out[i] = scale * (a[i] + b[i]);
+}
+
+// stats of a row range: rows * n pairs, the range's edges (rowptr[rows] - rowptr[0])
+__global__ void zzt_stats_rows_kernel(const double* pd, int nd, const double* pe, int ne,
+                                      const int* rowptr, int rows, int n, float norm,
+                                      double* stats) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  double dl = 0.0, dc = 0.0, el = 0.0, tp = 0.0;
+  for (int k = 0; k < nd; ++k) { dl += pd[2 * k]; dc += pd[2 * k + 1]; }
+  for (int k = 0; k < ne; ++k) { el += pe[2 * k]; tp += pe[2 * k + 1]; }
+  const double nnz = (double)(rowptr[rows] - rowptr[0]);
+  stats[0] = (double)norm * (dl + el + (double)rows * kSoftplusM1);
+  stats[1] = (double)rows * n - nnz - dc + 2.0 * tp;
 }
 
 __global__ void zzt_stats_kernel(const double* pd, int nd, const double* pe, int ne,
@@ -1777,7 +1806,10 @@ int zzt_dp(int d) {
 }
 int zzt_npad(int n) { return (int)round_up(n, ROWS); }
 int zzt_tsplit(int ngraphs, int n, int dtype) {
-  const int wgs = ngraphs * (zzt_npad(n) / ROWS), ntiles = zzt_npad(n) / TJ2;
+  return zzt_tsplit_blocks(ngraphs * (zzt_npad(n) / ROWS), n, dtype);
+}
+int zzt_tsplit_blocks(int wgs, int n, int dtype) {
+  const int ntiles = zzt_npad(n) / TJ2;
   if (dtype != SND_BF16 || wgs >= 256) return 1;
   // up to 8 column splits: one C2 graph (32 row blocks) then fills 256 CUs (B = 1 step
   // 0.1546 -> 0.1512 ms against 4 splits; B = 2 unchanged at 4)
@@ -1823,9 +1855,13 @@ int launch_zzt_prep(const float* z, int ngraphs, int n, int d, int dtype, const 
 
 int launch_zzt_dense(const ZztArgs& a, int dtype, hipStream_t s, bool defer_split) {
   const int dp = zzt_dp(a.d);
-  const int ts = (dtype == SND_BF16 && a.variant == 0) ? zzt_tsplit(a.ngraphs, a.n, dtype) : 1;
+  SND_CHECK_ARG(a.rb0 >= 0 && a.nrb >= 0 && a.rb0 + zrb(a) <= a.npad / ROWS,
+                "zzt_dense: row blocks [%d, %d) outside the %d of the graph", a.rb0, a.rb0 + zrb(a),
+                a.npad / ROWS);
+  const int ts = (dtype == SND_BF16 && a.variant == 0) ? zzt_tsplit_blocks(a.ngraphs * zrb(a), a.n, dtype) : 1;
   SND_CHECK_ARG(ts == 1 || a.dJd_extra, "zzt_dense: column splits need dJd_extra");
-  dim3 grid(a.ngraphs * (a.npad / ROWS) * ts);
+  SND_CHECK_ARG(a.nrb == 0 || a.ngraphs == 1, "zzt_dense: a row-block range needs one graph");
+  dim3 grid(a.ngraphs * zrb(a) * ts);
   if (dtype == SND_BF16 && a.variant == 1) {          // v1: 8 waves x 16 rows, TJ 64
     if (dp == 32) hipLaunchKernelGGL((zzt_dense_bf16<32>), grid, dim3(NTH), 0, s, a);
     else if (dp == 64) hipLaunchKernelGGL((zzt_dense_bf16<64>), grid, dim3(NTH), 0, s, a);
@@ -1871,9 +1907,12 @@ int launch_zzt_dense(const ZztArgs& a, int dtype, hipStream_t s, bool defer_spli
   }
   SND_LAUNCH_CHECK("zzt_dense");
   if (ts > 1 && !defer_split) {
-    const long long cnt = (long long)a.ngraphs * a.n * a.d;
+    // the launch's rows only (a row-block range writes no other rows of the slabs)
+    const long long r0 = (long long)a.rb0 * ROWS;
+    const long long r1 = a.nrb ? std::min<long long>(a.n, r0 + (long long)a.nrb * ROWS) : a.n;
+    const long long cnt = (long long)a.ngraphs * (r1 - r0) * a.d, total = (long long)a.ngraphs * a.n * a.d;
     hipLaunchKernelGGL(zzt_split_sum_kernel, dim3((unsigned)std::min<long long>(cdiv(cnt, 256), 4096)),
-                       dim3(256), 0, s, a.dJd, a.dJd_extra, cnt, ts - 1);
+                       dim3(256), 0, s, a.dJd + r0 * a.d, a.dJd_extra + r0 * a.d, cnt, total, ts - 1);
     SND_LAUNCH_CHECK("zzt_split_sum_kernel");
   }
   return 0;
@@ -1951,5 +1990,73 @@ extern "C" int snd_zzt_ce(const float* z, int n_graphs, int n, int d, const int*
                      zzt_dense_blocks(n_graphs, n, dtype), pe, edge_blocks((int)rows, d), rowptr,
                      n_graphs, n, norm, stats);
   SND_LAUNCH_CHECK("zzt_stats_kernel");
+  return 0;
+}
+
+// ---------------------------------------------------------------- row-sharded CE
+// One graph's rows [row0, row1) against all of its columns: every rank of a
+// row-sharded zz^T owns a contiguous row range, and because L is symmetric its
+// dz rows need no reduction across ranks (d CE / dz_i = 2 norm sum_j G_ij z_j).
+static void zrows_layout(int n, int d, int row0, int row1, int dtype, size_t* off, size_t* total) {
+  const int rows = row1 - row0;
+  const int rb0 = row0 / 128, nrb = (int)cdiv(row1, 128) - rb0;
+  const int ts = zzt_tsplit_blocks(nrb, n, dtype);
+  size_t b = 0;
+  off[0] = b; b += round_up(zzt_staging_bytes(1, n, d, dtype), 256);              // images
+  off[1] = b; b += round_up((size_t)n * d * sizeof(float), 256);                  // dJd (full rows)
+  off[2] = b; b += round_up((size_t)rows * d * sizeof(float), 256);               // ej
+  off[3] = b; b += round_up(2 * sizeof(double) * (size_t)nrb * ts, 256);          // dense partials
+  off[4] = b; b += round_up(2 * sizeof(double) * (size_t)edge_blocks(rows, d), 256);
+  off[5] = b; b += round_up((size_t)std::max(0, ts - 1) * n * d * sizeof(float), 256);   // splits
+  *total = b;
+}
+
+extern "C" size_t snd_zzt_ce_rows_workspace(int n, int d, int row0, int row1, int dtype) {
+  if (zzt_dp(d) < 0 || n <= 0 || row0 < 0 || row1 <= row0 || row1 > n) return 0;
+  size_t off[6], total;
+  zrows_layout(n, d, row0, row1, dtype, off, &total);
+  return total;
+}
+
+extern "C" int snd_zzt_ce_rows(const float* z, int n, int d, int row0, int row1,
+                               const int* rowptr, const int* colidx, float pos_weight, float norm,
+                               double* stats, float* dz, void* ws, size_t ws_bytes, int dtype,
+                               snd_stream_t stream) {
+  SND_CHECK_ARG(z && rowptr && stats && dz, "snd_zzt_ce_rows: null operand");
+  SND_CHECK_ARG(d == 16 || d == 32 || d == 64 || d == 128, "snd_zzt_ce_rows: d=%d not in {16,32,64,128}", d);
+  SND_CHECK_ARG(n > 0 && 0 <= row0 && row0 < row1 && row1 <= n,
+                "snd_zzt_ce_rows: rows [%d, %d) outside [0, %d)", row0, row1, n);
+  SND_CHECK_ARG(row0 % 128 == 0 && (row1 % 128 == 0 || row1 == n),
+                "snd_zzt_ce_rows: row range [%d, %d) not on 128-row blocks", row0, row1);
+  SND_CHECK_ARG(dtype == SND_F32 || dtype == SND_BF16, "snd_zzt_ce_rows: bad dtype");
+  size_t off[6], need;
+  zrows_layout(n, d, row0, row1, dtype, off, &need);
+  SND_CHECK_ARG(ws && ws_bytes >= need, "snd_zzt_ce_rows: workspace %zu < %zu", ws_bytes, need);
+  SND_TRY(zzt_init_attributes());
+  hipStream_t s = (hipStream_t)stream;
+  char* p = (char*)ws;
+  const int rows = row1 - row0;
+  const int rb0 = row0 / 128, nrb = (int)cdiv(row1, 128) - rb0;
+  const ZztStage stg = zzt_stage(p + off[0], 1, n, d, dtype);
+  float* djd = (float*)(p + off[1]);
+  float* ej = (float*)(p + off[2]);
+  double* pd = (double*)(p + off[3]);
+  double* pe = (double*)(p + off[4]);
+  SND_TRY(launch_zzt_prep(z, 1, n, d, dtype, stg, s));
+  ZztArgs a{stg.jrow, stg.jt, n, zzt_npad(n), 1, d, djd, pd, stg.colpart, 0, (float*)(p + off[5])};
+  a.rb0 = rb0;
+  a.nrb = nrb;
+  SND_TRY(launch_zzt_dense(a, dtype, s));
+  EdgeArgs e{rowptr, colidx, rows, z, d, pos_weight, ej, pe};
+  e.row0 = row0;
+  SND_TRY(launch_edge(e, s));
+  hipLaunchKernelGGL(zzt_combine2_kernel, dim3(1024), dim3(256), 0, s, dz, djd + (long long)row0 * d, ej,
+                     (long long)rows * d, 2.f * norm);
+  SND_LAUNCH_CHECK("zzt_combine2_kernel");
+  const int ts = zzt_tsplit_blocks(nrb, n, dtype == SND_BF16 ? SND_BF16 : dtype);
+  hipLaunchKernelGGL(zzt_stats_rows_kernel, dim3(1), dim3(64), 0, s, pd,
+                     nrb * ((dtype == SND_BF16) ? ts : 1), pe, edge_blocks(rows, d), rowptr, rows, n,
+                     norm, stats);
+  SND_LAUNCH_CHECK("zzt_stats_rows_kernel");
   return 0;
 }

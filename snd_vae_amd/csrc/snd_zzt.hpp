@@ -13,6 +13,8 @@ struct ZztArgs {
   int variant;           // bf16 kernel: 0 = default (v4 for d <= 64, else v3), 1 = v1,
                          // 3 = v3, 10..15 = v4 (epilogue, mode) A/B; >= 256 v4 measurement build
   float* dJd_extra;      // v3 column splits 1.. (zzt_tsplit > 1): [(tsplit-1)][B*n][d] scratch
+  int rb0 = 0;           // first 128-row block of the launch (row-sharded zz^T, snd_zzt_ce_rows)
+  int nrb = 0;           // row blocks of the launch; 0 = every row block
 };
 
 // Staging buffers carved from one workspace region.
@@ -28,6 +30,7 @@ int zzt_npad(int n);
 // block over zzt_tsplit() workgroups (bf16 only); their partial dJ rows are summed
 // in fixed order by launch_zzt_dense.  Loss partials: zzt_dense_blocks() entries.
 int zzt_tsplit(int ngraphs, int n, int dtype);
+int zzt_tsplit_blocks(int row_blocks, int n, int dtype);   // the same for a row-block count
 int zzt_dense_blocks(int ngraphs, int n, int dtype);
 size_t zzt_staging_bytes(int ngraphs, int n, int d, int dtype);
 ZztStage zzt_stage(void* base, int ngraphs, int n, int d, int dtype);

@@ -186,6 +186,29 @@ def inner_product_ce(z, n_graphs, rowptr, colidx, pos_weight=1.0, norm=1.0, dtyp
     return float(s[0]), float(s[1]), dz
 
 
+def inner_product_ce_rows(z, row0, row1, rowptr, colidx, pos_weight=1.0, norm=1.0, dtype="bf16"):
+    """The fused CE of one graph's rows [row0, row1) against all its columns
+    (snd_zzt_ce_rows; the row-sharded zz^T of SURVEY §8e): z [n, d] is the WHOLE graph,
+    rowptr the range's row pointers (a slice of the graph's CSR), colidx global ids.
+
+    Returns (stats, dz_rows): stats a float64 device tensor [ce_sum, n_correct] over the
+    range (left on the device for the caller's all-reduce); dz_rows [row1 - row0, d] is
+    d(ce_sum over ALL pairs)/dz for those rows (L symmetric: no reduction needed)."""
+    _need(z, "inner_product_ce_rows z")
+    n, d = z.shape
+    L = _lib.lib()
+    wsb = L.snd_zzt_ce_rows_workspace(n, d, row0, row1, _dt(dtype))
+    if wsb == 0:
+        raise _lib.SNDError(f"snd_zzt_ce_rows_workspace: bad shape n={n} d={d} rows [{row0}, {row1})")
+    ws = torch.empty(wsb, dtype=torch.uint8, device=z.device)
+    stats = torch.zeros(2, dtype=torch.float64, device=z.device)
+    dz = torch.empty(row1 - row0, d, dtype=torch.float32, device=z.device)
+    _lib.check(L.snd_zzt_ce_rows(_P(z), n, d, row0, row1, _P(rowptr), _P(colidx), pos_weight, norm,
+                                 _P(stats), _P(dz), _P(ws), wsb, _dt(dtype), _lib.stream_ptr()),
+               "snd_zzt_ce_rows")
+    return stats, dz
+
+
 def dense_to_csr(adj):
     """Reference dense adj_truth [B,N,N] -> (rowptr, colidx) on the device."""
     b, n, _ = adj.shape

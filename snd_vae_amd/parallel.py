@@ -156,3 +156,82 @@ def max_over_ranks(x: float, info: DistInfo, device="cpu") -> float:
     t = torch.tensor([x], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX, group=info.group)
     return float(t.item())
+
+
+# ---------------------------------------------------------------- row sharding (§8e)
+# One graph too large for one device's step (C5: N = 16384, 2.7e8 logits) split by
+# ROWS over the ranks instead of by graphs.  zz^T: every rank owns a contiguous
+# 128-row-aligned row range, all-gathers z once, evaluates its rows against every
+# column (snd_zzt_ce_rows) and keeps its dz rows -- L is symmetric, so dz needs no
+# reduction; only the two loss scalars are all-reduced.  Encoder SpMM: under the
+# RCM row order every neighbour of a row lies within +-beta rows, so a rank needs
+# only a halo of beta rows from each neighbouring range (halo_rows).
+
+def row_ranges(n: int, world: int, block: int = 128):
+    """Contiguous row ranges of one n-row graph over `world` ranks, cut on `block`-row
+    boundaries (the zz^T kernel's row blocks); the last range ends at n."""
+    nb = -(-n // block)
+    out = []
+    for r in range(world):
+        b0, b1 = r * nb // world, (r + 1) * nb // world
+        out.append((min(n, b0 * block), min(n, b1 * block)))
+    return out
+
+
+def allgather_rows(x_local: torch.Tensor, ranges, group) -> torch.Tensor:
+    """The whole [n, ...] matrix from every rank's contiguous row range (ranges may
+    differ in size by a block: shards are padded to the largest for the collective)."""
+    import torch.distributed as dist
+    world = len(ranges)
+    rmax = max(r1 - r0 for r0, r1 in ranges)
+    pad = torch.zeros((rmax,) + tuple(x_local.shape[1:]), dtype=x_local.dtype, device=x_local.device)
+    pad[:x_local.shape[0]] = x_local
+    parts = [torch.empty_like(pad) for _ in range(world)]
+    dist.all_gather(parts, pad, group=group)
+    return torch.cat([parts[r][:r1 - r0] for r, (r0, r1) in enumerate(ranges)])
+
+
+def halo_rows(x_local: torch.Tensor, ranges, rank: int, halo: int, group) -> torch.Tensor:
+    """Rows [row0 - halo, row1 + halo) clipped to [0, n) of a contiguously row-sharded
+    matrix, on this rank: its own rows plus `halo` boundary rows from each side
+    (every rank contributes its first and last `halo` rows to one all-gather)."""
+    import torch.distributed as dist
+    world = len(ranges)
+    h = halo
+    rows = x_local.shape[0]
+    tail = tuple(x_local.shape[1:])
+    edge = torch.zeros((2, h) + tail, dtype=x_local.dtype, device=x_local.device)
+    k = min(h, rows)
+    edge[0, :k] = x_local[:k]                # first rows (the lower neighbour's upper halo)
+    edge[1, h - k:] = x_local[rows - k:]     # last rows, right-aligned
+    parts = [torch.empty_like(edge) for _ in range(world)]
+    dist.all_gather(parts, edge, group=group)
+    r0, r1 = ranges[rank]
+    lo = max(0, r0 - h)
+    hi = min(ranges[-1][1], r1 + h)
+    below = parts[rank - 1][1][h - (r0 - lo):] if rank > 0 and r0 > lo else x_local[:0]
+    above = parts[rank + 1][0][:hi - r1] if rank + 1 < world and hi > r1 else x_local[:0]
+    if rank > 0 and (r0 - lo) > ranges[rank - 1][1] - ranges[rank - 1][0]:
+        raise ValueError("halo wider than the neighbouring range")
+    if rank + 1 < world and (hi - r1) > ranges[rank + 1][1] - ranges[rank + 1][0]:
+        raise ValueError("halo wider than the neighbouring range")
+    return torch.cat([below, x_local, above]), lo
+
+
+def row_sharded_adj_ce(z_local: torch.Tensor, ranges, rank: int, rowptr, colidx, group,
+                       compute=None, **kw):
+    """The structure decoder's CE (layers.py:407-409, optimizer.py:142-144) of ONE
+    graph row-sharded over the ranks: all-gather z, this rank's rows against every
+    column, all-reduce (sum) of [ce_sum, n_correct].  rowptr/colidx: this rank's
+    rows of the graph's CSR (global column ids).  Returns (stats, dz_rows) with
+    stats the global [ce_sum, n_correct] and dz_rows this rank's rows of d ce_sum/dz.
+    compute(z_full, row0, row1, rowptr, colidx, **kw) -> (stats, dz_rows) defaults to
+    the HIP kernel (layers.inner_product_ce_rows)."""
+    import torch.distributed as dist
+    if compute is None:
+        from .layers import inner_product_ce_rows as compute
+    z_full = allgather_rows(z_local, ranges, group)
+    r0, r1 = ranges[rank]
+    stats, dz = compute(z_full, r0, r1, rowptr, colidx, **kw)
+    dist.all_reduce(stats, group=group)
+    return stats, dz
