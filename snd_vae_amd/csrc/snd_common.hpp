@@ -43,6 +43,17 @@ constexpr float kLog2e = 1.4426950408889634f;
 constexpr float kLn2 = 0.69314718055994531f;
 constexpr double kSoftplusM1 = 0.31326168751822286;  // CE of a diagonal pair: logsumexp(1,0) - 1
 
+// Measurement-only debug bits (phase skips, in-kernel clock stamps; snd_debug_set) are
+// compiled into the measurement build only (-DSND_MEAS=1, tools/build_exp.sh).  In the
+// shipped library kdbg() keeps just kKeepDbg -- the bit a parity test needs (1 << 23:
+// poison the decoder's LDS activations before staging) -- so every other debug branch
+// in the hot kernels folds away at compile time.
+#ifndef SND_MEAS
+#define SND_MEAS 0
+#endif
+constexpr int kKeepDbg = 1 << 23;
+__host__ __device__ __forceinline__ constexpr int kdbg(int dbg) { return SND_MEAS ? dbg : (dbg & kKeepDbg); }
+
 // max(x, 0.2 x) == (x >= 0 ? x : 0.2 x) for every x (both zeros keep their sign): 2 ops, not 3
 __device__ __forceinline__ float lrelu(float x) { return fmaxf(x, kLeak * x); }
 // TF Maximum gradient: routed to x where x >= 0.2x  =>  1 for x >= 0.

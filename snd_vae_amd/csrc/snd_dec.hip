@@ -315,7 +315,7 @@ __global__ void __launch_bounds__(DT) dec_fwd_kernel(DecChainFwdArgs a) {
   const int own = tl.rend - tl.r0;
   // measurement only (debug bit 1 << 21): s_memrealtime at the phase boundaries, written by
   // thread 0 over the tile's head partials at the end (results wrong); tools/dec_stamps.py
-  const bool stamp = a.dbg & (1 << 21);
+  const bool stamp = kdbg(a.dbg) & (1 << 21);
   unsigned long long ts[9] = {};
   if (stamp) ts[0] = __builtin_amdgcn_s_memrealtime();
 
@@ -326,12 +326,12 @@ __global__ void __launch_bounds__(DT) dec_fwd_kernel(DecChainFwdArgs a) {
   // epilogues; rows past a window only feed discarded output rows, and U2's pad
   // columns hold finite stale J values against zero weights.  (Zeroing the whole
   // 148 KB measured 1.6 us of the launch.)
-  if (a.dbg & (1 << 23)) {   // test only: NaN in every activation byte first (worst-case stale LDS)
+  if (kdbg(a.dbg) & (1 << 23)) {   // test only: NaN in every activation byte first (worst-case stale LDS)
     for (int i = tid * 16; i < L.total - L.a; i += DT * 16)
       *reinterpret_cast<uint4*>(smem + L.a + i) = make_uint4(~0u, ~0u, ~0u, ~0u);
     __syncthreads();
   }
-  if (!(a.dbg & 32)) {   // (kp - np) / 4 <= 4 groups of 4 columns per row: no division
+  if (!(kdbg(a.dbg) & 32)) {   // (kp - np) / 4 <= 4 groups of 4 columns per row: no division
     const int kpo = a.k2.kp, npc = (kpo - a.k1.np) >> 2, nr = in_rows(TR + 4);
     for (int i = tid; i < nr * 4; i += DT) {
       const int row = i >> 2, q = i & 3;
@@ -340,9 +340,9 @@ __global__ void __launch_bounds__(DT) dec_fwd_kernel(DecChainFwdArgs a) {
   }
   __syncthreads();
   // J window [r0 - 6, r0 + own + 6) and the conv1 weights
-  if (!(a.dbg & 16)) stage_window(a.zb, a.ldz, a.dj, tl.r0 - 6, in_rows(TR + 8), own + 12, tl.glo, tl.ghi, a.k1.kp,
+  if (!(kdbg(a.dbg) & 16)) stage_window(a.zb, a.ldz, a.dj, tl.r0 - 6, in_rows(TR + 8), own + 12, tl.glo, tl.ghi, a.k1.kp,
                reinterpret_cast<char*>(jimg), a.zero);
-  stage_weights(a.k1, reinterpret_cast<char*>(wimg), a.dbg);
+  stage_weights(a.k1, reinterpret_cast<char*>(wimg), kdbg(a.dbg));
   // head parameters and the tile's targets, fetched now so their latency hides under the convs
   if (tid >= 512 && tid < 512 + 128) {
     const int i = tid - 512, hh = i >> 6, j = i & 63;
@@ -414,16 +414,16 @@ __global__ void __launch_bounds__(DT) dec_fwd_kernel(DecChainFwdArgs a) {
           ub[e] = (__bf16)(ing ? lrelu(yv[e] * g[e] + be[e]) : 0.f);
         }
         *reinterpret_cast<bf16x4*>(img_at(u1img, orow, kpo, n0)) = ub;
-        if (mine && !(a.dbg & 8)) {
+        if (mine && !(kdbg(a.dbg) & 8)) {
           *reinterpret_cast<f32x4*>(a.y1 + (long long)gr * a.ldy1 + n0) = yv;
           *reinterpret_cast<bf16x4*>(a.u1 + (long long)gr * a.ldy1 + n0) = ub;
         }
       }
-    }, a.dbg);
+    }, kdbg(a.dbg));
   }
   __syncthreads();
   if (stamp) ts[2] = __builtin_amdgcn_s_memrealtime();
-  stage_weights(a.k2, reinterpret_cast<char*>(wimg), a.dbg);
+  stage_weights(a.k2, reinterpret_cast<char*>(wimg), kdbg(a.dbg));
   wait_dma();
   if (stamp) ts[3] = __builtin_amdgcn_s_memrealtime();
   // ---- conv2: window [r0 - 2, r0 + own + 2) -> U2 image; Y2 / U2 own rows; Y2n own rows in LDS
@@ -451,18 +451,18 @@ __global__ void __launch_bounds__(DT) dec_fwd_kernel(DecChainFwdArgs a) {
           ub[e] = (__bf16)(ing ? lrelu(yv[e] * g[e] + be[e]) : 0.f);
         }
         *reinterpret_cast<bf16x4*>(img_at(u2img, orow, kpu2, n0)) = ub;
-        if (mine && !(a.dbg & 8)) {
+        if (mine && !(kdbg(a.dbg) & 8)) {
           *reinterpret_cast<f32x4*>(a.y2 + (long long)gr * a.ldy2 + n0) = yv;
           *reinterpret_cast<bf16x4*>(a.u2 + (long long)gr * a.ldy2 + n0) = ub;
           if (n0 >= nlo && n0 < nhi)   // the n branch's columns: whole float4 groups (b % 4 == 0)
             *reinterpret_cast<f32x4*>(&y2n[(gr - tl.r0) * L.ldY2n + (n0 - a.m2.offb)]) = yv;
         }
       }
-    }, a.dbg);
+    }, kdbg(a.dbg));
   }
   __syncthreads();
   if (stamp) ts[4] = __builtin_amdgcn_s_memrealtime();
-  stage_weights(a.k3, reinterpret_cast<char*>(wimg), a.dbg);
+  stage_weights(a.k3, reinterpret_cast<char*>(wimg), kdbg(a.dbg));
   wait_dma();
   if (stamp) ts[5] = __builtin_amdgcn_s_memrealtime();
   // ---- conv3 (s branch): own rows -> U3, Y3 (fp32, LDS; the spatial head's input)
@@ -481,7 +481,7 @@ __global__ void __launch_bounds__(DT) dec_fwd_kernel(DecChainFwdArgs a) {
       }
       *reinterpret_cast<float4*>(u3 + orow * 16 + n0) = make_float4(o[0], o[1], o[2], o[3]);
       *reinterpret_cast<float4*>(y3 + orow * 16 + n0) = make_float4(yv[0], yv[1], yv[2], yv[3]);
-    }, a.dbg);
+    }, kdbg(a.dbg));
   }
   __syncthreads();
   if (stamp) ts[6] = __builtin_amdgcn_s_memrealtime();
@@ -491,7 +491,7 @@ __global__ void __launch_bounds__(DT) dec_fwd_kernel(DecChainFwdArgs a) {
   constexpr int NQS = head_nq(10, 2), NQN = head_nq(20, 1);
   float* scr = reinterpret_cast<float*>(smem + L.w);
   double* sscr = reinterpret_cast<double*>(smem + L.w + (NQS + NQN) * kScr * 4);
-  if (!(a.dbg & 2)) {
+  if (!(kdbg(a.dbg) & 2)) {
     if (tid < 256) {
       const int hi = tid >> 7, orow = tid & 127;
       const bool rv = orow < own;
@@ -573,18 +573,18 @@ __global__ void __launch_bounds__(DT) dec_bwd_kernel(DecChainBwdArgs a) {
   float* slots = reinterpret_cast<float*>(smem + L.cps);
   const int own = tl.rend - tl.r0;
   const int t = blockIdx.x;
-  const bool stamp = a.dbg & (1 << 21);   // measurement only, as dec_fwd_kernel (over pc1)
+  const bool stamp = kdbg(a.dbg) & (1 << 21);   // measurement only, as dec_fwd_kernel (over pc1)
   unsigned long long ts[8] = {};
   if (stamp) ts[0] = __builtin_amdgcn_s_memrealtime();
 
-  if (!(a.dbg & 32))
+  if (!(kdbg(a.dbg) & 32))
     for (int i = tid * 16; i < L.cps - L.d3; i += DT * 16)
       *reinterpret_cast<uint4*>(smem + L.d3 + i) = make_uint4(0u, 0u, 0u, 0u);
   __syncthreads();
   // dY3 window [r0 - 6, r0 + own + 6), conv3^T weights
-  if (!(a.dbg & 16)) stage_window(a.dy3, a.lddy3, a.s3, tl.r0 - 6, in_rows(TR + 8), own + 12, tl.glo, tl.ghi, a.k3t.kp,
+  if (!(kdbg(a.dbg) & 16)) stage_window(a.dy3, a.lddy3, a.s3, tl.r0 - 6, in_rows(TR + 8), own + 12, tl.glo, tl.ghi, a.k3t.kp,
                reinterpret_cast<char*>(d3), a.zero);
-  stage_weights(a.k3t, reinterpret_cast<char*>(wimg), a.dbg);
+  stage_weights(a.k3t, reinterpret_cast<char*>(wimg), kdbg(a.dbg));
   if (tid < 128) {
     const int n = tid;
     const ColMap ms{a.m2.a, 0, a.m2.a};
@@ -597,7 +597,7 @@ __global__ void __launch_bounds__(DT) dec_bwd_kernel(DecChainBwdArgs a) {
   {
     const int wr0 = tl.r0 - 4, nv = own + 8, kp2 = a.k2t.kp;
     const int nq = (a.m2.b + 3) / 4;             // 4-column groups of the n part
-    for (int i = tid; i < ((a.dbg & 16) ? 0 : nv * nq); i += DT) {
+    for (int i = tid; i < ((kdbg(a.dbg) & 16) ? 0 : nv * nq); i += DT) {
       const int row = i / nq, q = i - row * nq;
       const int gr = wr0 + row;
       if (gr < tl.glo || gr >= tl.ghi) continue;
@@ -645,14 +645,14 @@ __global__ void __launch_bounds__(DT) dec_bwd_kernel(DecChainBwdArgs a) {
       for (int e = 0; e < 4; ++e) ob[e] = (__bf16)o[e];
       if (n0 < a.m2.offb || !a.m2.b)    // s part only (the n part came from the heads)
         *reinterpret_cast<bf16x4*>(img_at(d2, orow, kpo, n0)) = ob;
-      if (mine && !(a.dbg & 8)) {
+      if (mine && !(kdbg(a.dbg) & 8)) {
         __bf16* dp = a.dy2 + (long long)gr * a.lddy2 + n0;
         if (n0 + 3 < N) *reinterpret_cast<bf16x4*>(dp) = ob;
         else
 #pragma unroll
           for (int e = 0; e < 4; ++e) if (n0 + e < N) dp[e] = ob[e];
       }
-    }, a.dbg);
+    }, kdbg(a.dbg));
     if (w / ncg < wpc) colpart_flush<1>(q, slots, a.k3t.np, nb0, nbc, w / ncg);
     __syncthreads();
     for (int i = tid; i < 3 * N; i += DT) {
@@ -664,7 +664,7 @@ __global__ void __launch_bounds__(DT) dec_bwd_kernel(DecChainBwdArgs a) {
   }
   __syncthreads();
   if (stamp) ts[2] = __builtin_amdgcn_s_memrealtime();
-  stage_weights(a.k2t, reinterpret_cast<char*>(wimg), a.dbg);
+  stage_weights(a.k2t, reinterpret_cast<char*>(wimg), kdbg(a.dbg));
   wait_dma();
   if (stamp) ts[3] = __builtin_amdgcn_s_memrealtime();
   // ---- conv2^T: window [r0 - 2, r0 + own + 2): dU1 -> BN/lrelu backward -> dY1
@@ -706,9 +706,9 @@ __global__ void __launch_bounds__(DT) dec_bwd_kernel(DecChainBwdArgs a) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) ob[e] = (__bf16)o[e];
         *reinterpret_cast<bf16x4*>(img_at(d1, orow, kpo, n0)) = ob;
-        if (mine && !(a.dbg & 8)) *reinterpret_cast<bf16x4*>(a.dy1 + (long long)gr * a.lddy1 + n0) = ob;
+        if (mine && !(kdbg(a.dbg) & 8)) *reinterpret_cast<bf16x4*>(a.dy1 + (long long)gr * a.lddy1 + n0) = ob;
       }
-    }, a.dbg);
+    }, kdbg(a.dbg));
     __syncthreads();   // slots: the conv3^T partials were consumed above
     if (w / ncg < wpc) colpart_flush<2>(q, slots, a.k2t.np, nb0, nbc, w / ncg);
     __syncthreads();
@@ -721,7 +721,7 @@ __global__ void __launch_bounds__(DT) dec_bwd_kernel(DecChainBwdArgs a) {
   }
   __syncthreads();
   if (stamp) ts[4] = __builtin_amdgcn_s_memrealtime();
-  stage_weights(a.k1t, reinterpret_cast<char*>(wimg), a.dbg);
+  stage_weights(a.k1t, reinterpret_cast<char*>(wimg), kdbg(a.dbg));
   wait_dma();
   if (stamp) ts[5] = __builtin_amdgcn_s_memrealtime();
   // ---- conv1^T: own rows -> dJ (fp32)
@@ -734,11 +734,11 @@ __global__ void __launch_bounds__(DT) dec_bwd_kernel(DecChainBwdArgs a) {
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
         const int n0 = 16 * (nb + i) + 4 * lg;
-        if (n0 >= N || (a.dbg & 8)) continue;
+        if (n0 >= N || (kdbg(a.dbg) & 8)) continue;
         *reinterpret_cast<float4*>(a.dz + gr * a.lddz + n0) =
             make_float4(acc[i][0], acc[i][1], acc[i][2], acc[i][3]);
       }
-    }, a.dbg);
+    }, kdbg(a.dbg));
   }
   if (stamp) {
     ts[6] = __builtin_amdgcn_s_memrealtime();

@@ -111,10 +111,10 @@ __global__ void __launch_bounds__(RCT) rowconv_kernel(RcArgs a) {
   const int nbase = blockIdx.y * a.npb;
   const int nloc = min(a.npb, np - nbase);
   const int nbc = nloc >> 4;
-  const bool use_cp = NCP > 0 && a.colpart != nullptr && !(a.dbg & 64);
+  const bool use_cp = NCP > 0 && a.colpart != nullptr && !(kdbg(a.dbg) & 64);
 
   // ---- packed weight image (LDS-DMA, 1 KB per wave instruction)
-  if (!(a.dbg & 1)) {
+  if (!(kdbg(a.dbg) & 1)) {
     const int segc = (nloc * kp) >> 9, npc = T * segc;   // 1 KB pieces per tap, in all
     const char* g = reinterpret_cast<const char*>(a.wpk) + lane * 16;
     for (int j = w; j < npc; j += RCT / 64) {
@@ -125,7 +125,7 @@ __global__ void __launch_bounds__(RCT) rowconv_kernel(RcArgs a) {
   // ---- per-column parameters
   if (tid < nloc) {
     const int nl = tid, n = nbase + tid;
-    const bool cv = n < a.N && a.cols.valid(n) && !(a.dbg & 16);
+    const bool cv = n < a.N && a.cols.valid(n) && !(kdbg(a.dbg) & 16);
     const bool pa = n < a.cols.a;
     const int ia = pa ? n : a.cols.logical(n), ib = n - a.cols.offb;
     auto par = [&](const float* A, const float* Bv) {
@@ -173,7 +173,7 @@ __global__ void __launch_bounds__(RCT) rowconv_kernel(RcArgs a) {
     }
     if (!first) __syncthreads();
     // ---- x rows [r0 - H, r0 - H + XR), zero outside [glo, ghi)
-    if (!(a.dbg & 2)) {
+    if (!(kdbg(a.dbg) & 2)) {
       const int kc = 1 << lkc;
       for (int j = w; j < (xch >> 6); j += RCT / 64) {
         const int q = (j << 6) + lane;
@@ -193,7 +193,7 @@ __global__ void __launch_bounds__(RCT) rowconv_kernel(RcArgs a) {
 #pragma unroll
     for (int i = 0; i < NBH; ++i) ypf[i] = f32x4{0.f, 0.f, 0.f, 0.f};
     if constexpr (EPI == RC_DECBWD || EPI == RC_ENC1) {
-      if (rv && !(a.dbg & 32)) {
+      if (rv && !(kdbg(a.dbg) & 32)) {
 #pragma unroll
         for (int i = 0; i < NBH; ++i) {
           const int n0 = nbase + 16 * (nb0 + i) + 4 * lg;
@@ -233,7 +233,7 @@ __global__ void __launch_bounds__(RCT) rowconv_kernel(RcArgs a) {
     f32x4 acc[NBH];
 #pragma unroll
     for (int i = 0; i < NBH; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-    const int kcs = (a.dbg & 4) ? 0 : kp >> 5;
+    const int kcs = (kdbg(a.dbg) & 4) ? 0 : kp >> 5;
     for (int t = 0; t < T; ++t) {
       const int xrow = 16 * rb + li + t;
       const __bf16* xrp = xs + xrow * kp;
@@ -257,7 +257,7 @@ __global__ void __launch_bounds__(RCT) rowconv_kernel(RcArgs a) {
 #pragma unroll
     for (int i = 0; i < NBH; ++i) {
       const int nb = nb0 + i;
-      if (nb >= nbc || (a.dbg & 128)) continue;
+      if (nb >= nbc || (kdbg(a.dbg) & 128)) continue;
       const int nl0 = 16 * nb + 4 * lg, n0 = nbase + nl0;
       const unsigned cm = rv ? cvm[i] : 0u;
       float o[4], qs[NCP > 0 ? NCP : 1][4];
@@ -287,7 +287,7 @@ __global__ void __launch_bounds__(RCT) rowconv_kernel(RcArgs a) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) { yv[e] = acc[i][e] + bi[e]; o[e] = lrelu(yv[e] * ga[e] + be[e]); }
         float* yp = a.y + (long long)r * a.ldy + n0;
-        if (a.dbg & 8) {
+        if (kdbg(a.dbg) & 8) {
         } else if (cm == 15u) *reinterpret_cast<float4*>(yp) = make_float4(yv[0], yv[1], yv[2], yv[3]);
         else
 #pragma unroll
@@ -338,7 +338,7 @@ __global__ void __launch_bounds__(RCT) rowconv_kernel(RcArgs a) {
           o[e] = db * ga[e] * lrelu_grad(pv);
         }
       }
-      if (a.dbg & 8) sm = 0u;
+      if (kdbg(a.dbg) & 8) sm = 0u;
       if (a.out_bf16) {
         __bf16* op = reinterpret_cast<__bf16*>(a.out) + (long long)r * a.ldo + n0;
         if (sm == 15u) {
@@ -485,7 +485,7 @@ __device__ __forceinline__ void wgrad_body(const WgArgs& a, const int bx, const 
   const __bf16* dg = reinterpret_cast<const __bf16*>(a.dy);
   const int c0 = bx * a.rows_per_wg, c1 = min(a.R, c0 + a.rows_per_wg);
   auto stage = [&](const WgUnit& u, int b) __attribute__((always_inline)) {
-    if (a.dbg & 2) return;
+    if (kdbg(a.dbg) & 2) return;
     __bf16* xs = lds + b * bufe;
     __bf16* ds = xs + (xch << 3);
     // wave-strided LDS-DMA over the 16 waves
@@ -536,7 +536,7 @@ __device__ __forceinline__ void wgrad_body(const WgArgs& a, const int bx, const 
       if (more) { un = wg_unit(a, nsub, ns0, c1); stage(un, (k + 1) & 1); }
       const __bf16* xs = lds + (k & 1) * bufe;
       const __bf16* ds = xs + (xch << 3);
-      if (!(a.dbg & 4) && pv) {
+      if (!(kdbg(a.dbg) & 4) && pv) {
         // the tr-read swizzle of rows rk, rk + 4, rk + 32 j (+ t) is the same: offsets
         // advance by constants across the 4 k-steps
 #pragma unroll
@@ -560,7 +560,7 @@ __device__ __forceinline__ void wgrad_body(const WgArgs& a, const int bx, const 
     }
   }
   // D[m = n (dy col)][n = k (x col)]: lane holds k = 16cb + li, n = 16ob + 4lg + e
-  if (a.dbg & 8) return;
+  if (kdbg(a.dbg) & 8) return;
   // slab rows padded to a multiple of 4 floats: every store is a float4
   const int n4 = (a.N + 3) & ~3;
 #pragma unroll

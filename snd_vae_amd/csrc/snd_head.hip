@@ -139,7 +139,7 @@ __global__ void __launch_bounds__(HR * 8) head_fwd_kernel(HeadFwdArgs a) {
   float acc[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) acc[j] = 0.f;
-  if (rv && !(a.dbg & 1)) {
+  if (rv && !(kdbg(a.dbg) & 1)) {
     const __amdgpu_buffer_rsrc_t rsd = rows_rsrc(a.xw1, (long long)a.R * a.h1 * 2);
     gather_rows16<1>(a.colidx, a.rowptr[r], a.rowptr[r + 1], rsd, 2u * a.h1, sub,
                      [&](int, const u32x4 (&v)[1], bool) { acc8v(acc, v[0]); });
@@ -180,7 +180,7 @@ __global__ void __launch_bounds__(HR * 8) head_fwd_kernel(HeadFwdArgs a) {
   __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): weight images landed (gathers consumed)
   __syncthreads();
   // P1 and G leave for the backward pass while the heads run
-  if (rv && !(a.dbg & 8)) {
+  if (rv && !(kdbg(a.dbg) & 8)) {
     if (sub < nch) {
       float* pp = a.p1 + r * a.h1 + 8 * sub;
       *reinterpret_cast<float4*>(pp) = make_float4(acc[0], acc[1], acc[2], acc[3]);
@@ -197,7 +197,7 @@ __global__ void __launch_bounds__(HR * 8) head_fwd_kernel(HeadFwdArgs a) {
   const long long rr = gr0 + lrw;
   {
     f32x4 acc1[NB1];
-    if (a.dbg & 16) { for (int i = 0; i < NB1; ++i) acc1[i] = f32x4{0.f, 0.f, 0.f, 0.f}; }
+    if (kdbg(a.dbg) & 16) { for (int i = 0; i < NB1; ++i) acc1[i] = f32x4{0.f, 0.f, 0.f, 0.f}; }
     else img_gemm<NB1>(gs, w1s, a.kp1, a.np1, rb, NB1 * half, li, lg, acc1);
 #pragma unroll
     for (int i = 0; i < NB1; ++i) {
@@ -207,7 +207,7 @@ __global__ void __launch_bounds__(HR * 8) head_fwd_kernel(HeadFwdArgs a) {
 #pragma unroll
       for (int e = 0; e < 4; ++e) v4[e] = (__bf16)(acc1[i][e] + cb1[n0 + e]);
       *img_at4(hs, row, n0, a.kp2) = v4;
-      if (vrow && !(a.dbg & 8)) *reinterpret_cast<bf16x4*>(a.hh + rr * a.gh + n0) = v4;
+      if (vrow && !(kdbg(a.dbg) & 8)) *reinterpret_cast<bf16x4*>(a.hh + rr * a.gh + n0) = v4;
     }
   }
   __syncthreads();
@@ -215,7 +215,7 @@ __global__ void __launch_bounds__(HR * 8) head_fwd_kernel(HeadFwdArgs a) {
   // ---- 3. [mu | s] = h Wms + bms; both halves go to LDS (the weight and h images are dead)
   {
     f32x4 acc2[NB2];
-    if (a.dbg & 16) { for (int i = 0; i < NB2; ++i) acc2[i] = f32x4{0.f, 0.f, 0.f, 0.f}; }
+    if (kdbg(a.dbg) & 16) { for (int i = 0; i < NB2; ++i) acc2[i] = f32x4{0.f, 0.f, 0.f, 0.f}; }
     else img_gemm<NB2>(hs, w2s, a.kp2, a.np2, rb, NB2 * half, li, lg, acc2);
     float o[NB2][4];
 #pragma unroll
@@ -223,7 +223,7 @@ __global__ void __launch_bounds__(HR * 8) head_fwd_kernel(HeadFwdArgs a) {
       const int n0 = 16 * (NB2 * half + i) + 4 * lg;
 #pragma unroll
       for (int e = 0; e < 4; ++e) o[i][e] = acc2[i][e] + cb2[n0 + e];
-      if (vrow && !(a.dbg & 8))
+      if (vrow && !(kdbg(a.dbg) & 8))
         *reinterpret_cast<float4*>(a.ms + rr * (2 * L) + n0) = make_float4(o[i][0], o[i][1], o[i][2], o[i][3]);
     }
     __syncthreads();   // every wave is past its MFMA reads of the Wms and h images
@@ -244,7 +244,7 @@ __global__ void __launch_bounds__(HR * 8) head_fwd_kernel(HeadFwdArgs a) {
     double kl[HR / 64];
 #pragma unroll
     for (int h = 0; h < HR / 64; ++h) kl[h] = 0.0;
-    for (int it = (a.dbg & 32) ? HR * nq : tid; it < HR * nq; it += HT) {
+    for (int it = (kdbg(a.dbg) & 32) ? HR * nq : tid; it < HR * nq; it += HT) {
       const int zr = it / nq, c = 4 * (it - zr * nq);
       const int zl = lr0 + zr;
       float z4[4] = {0.f, 0.f, 0.f, 0.f};
@@ -265,7 +265,7 @@ __global__ void __launch_bounds__(HR * 8) head_fwd_kernel(HeadFwdArgs a) {
         }
 #pragma unroll
         for (int h = 0; h < HR / 64; ++h) kl[h] += (zr >> 6) == h ? kq : 0.0;
-        if (!(a.dbg & 8)) {
+        if (!(kdbg(a.dbg) & 8)) {
           *reinterpret_cast<float4*>(a.z + ie) = make_float4(z4[0], z4[1], z4[2], z4[3]);
           *reinterpret_cast<float4*>(a.eps_out + ie) = ep;
           bf16x4 zb;
@@ -290,7 +290,7 @@ __global__ void __launch_bounds__(HR * 8) head_fwd_kernel(HeadFwdArgs a) {
   }
   __syncthreads();
   // per-64-row column sums of the stored K-role values (reparam_prep order)
-  for (int i = (a.dbg & 64) ? HT * HR : tid; i < (HR / 64) * L; i += HT) {
+  for (int i = (kdbg(a.dbg) & 64) ? HT * HR : tid; i < (HR / 64) * L; i += HT) {
     const int h = i / L, c = i - h * L;
     float cs = 0.f;
     for (int q0 = 0; q0 < 64; q0 += 16) {   // 16 reads in flight, the sum in row order
@@ -303,7 +303,7 @@ __global__ void __launch_bounds__(HR * 8) head_fwd_kernel(HeadFwdArgs a) {
     a.colpart[((long long)gi * (a.npad / 64) + (HR / 64) * lt + h) * L + c] = cs;
   }
   // z^T image: 4 consecutive rows per lane
-  for (int idx = (a.dbg & 64) ? HT * HR : tid; idx < (HR / 4) * L; idx += HT) {
+  for (int idx = (kdbg(a.dbg) & 64) ? HT * HR : tid; idx < (HR / 4) * L; idx += HT) {
     const int c = idx / (HR / 4), r4 = 4 * (idx % (HR / 4));
     bf16x4 t;
 #pragma unroll
@@ -417,7 +417,7 @@ __global__ void __launch_bounds__(1024) head_bwd_kernel(HeadBwdArgs a) {
       for (int q = 0; q < NQ; ++q)
         if (qv[q]) zi[q] = *reinterpret_cast<const u32x4*>(a.zb + (long long)r * L + 64 * q + 8 * sub);
     const float pw = a.pos_weight;
-    if (rv && !(a.dbg & 1)) {
+    if (rv && !(kdbg(a.dbg) & 1)) {
       const __amdgpu_buffer_rsrc_t rsd = rows_rsrc(a.zb, (long long)a.R * L * 2);
       gather_rows16<NQ>(a.colidx, a.rowptr[r], a.rowptr[r + 1], rsd, 2u * L, sub,
                         [&](int, const u32x4 (&v)[NQ], bool valid) {
@@ -491,7 +491,7 @@ __global__ void __launch_bounds__(1024) head_bwd_kernel(HeadBwdArgs a) {
         const int cm = c0 >> 3, cs = (L + c0) >> 3;
         *reinterpret_cast<bf16x8*>(ms_img + rs * a.kp1 + ((cm ^ hswz(rs, a.kp1)) << 3)) = om;
         *reinterpret_cast<bf16x8*>(ms_img + rs * a.kp1 + ((cs ^ hswz(rs, a.kp1)) << 3)) = os;
-        if (rv && !(a.dbg & 8)) {
+        if (rv && !(kdbg(a.dbg) & 8)) {
           *reinterpret_cast<bf16x8*>(a.dms + (long long)r * L2 + c0) = om;
           *reinterpret_cast<bf16x8*>(a.dms + (long long)r * L2 + L + c0) = os;
         }
@@ -543,7 +543,7 @@ __global__ void __launch_bounds__(1024) head_bwd_kernel(HeadBwdArgs a) {
         v4[e] = (__bf16)o;
       }
       if (n0 < a.gh) *img_at4(dh_img, row, n0, a.kp2) = v4;
-      if (cv && !(a.dbg & 8)) *reinterpret_cast<bf16x4*>(a.dh + (long long)r * a.gh + n0) = v4;
+      if (cv && !(kdbg(a.dbg) & 8)) *reinterpret_cast<bf16x4*>(a.dh + (long long)r * a.gh + n0) = v4;
 #pragma unroll
       for (int e = 0; e < 4; ++e) qs[e] = row16_sum(qs[e]);
       if (li == 0) *reinterpret_cast<float4*>(&cpb[rb][n0]) = make_float4(qs[0], qs[1], qs[2], qs[3]);
@@ -609,7 +609,7 @@ __global__ void __launch_bounds__(1024) head_bwd_kernel(HeadBwdArgs a) {
           sm &= ~(1u << e);
         }
       }
-      if (!(a.dbg & 8)) {
+      if (!(kdbg(a.dbg) & 8)) {
         __bf16* op = a.dp1 + (long long)r * a.h1 + n0;
         if (sm == 15u) {
           bf16x4 v4;
@@ -752,7 +752,7 @@ __global__ void __launch_bounds__(1024) enc_front_kernel(FrontArgs a) {
     if (sub < kc1) *reinterpret_cast<uint4*>(himg + rs * a.kp1 + ((sub ^ hswz(rs, a.kp1)) << 3)) = v0;
     if (sub + 8 < kc1) *reinterpret_cast<uint4*>(himg + rs * a.kp1 + (((sub + 8) ^ hswz(rs, a.kp1)) << 3)) = v1;
   }
-  if (rv && !(a.dbg & 8)) {
+  if (rv && !(kdbg(a.dbg) & 8)) {
     if (sub < nch) *reinterpret_cast<uint4*>(a.h1 + (long long)r * a.ldh1 + 8 * sub) = hd;
     if (xo >= 0) *reinterpret_cast<uint4*>(a.h1 + (long long)r * a.ldh1 + a.h0) = hx;
     if (sub == 0) {
@@ -768,7 +768,7 @@ __global__ void __launch_bounds__(1024) enc_front_kernel(FrontArgs a) {
   const int row = 16 * rb + li, rr = r0 + row;
   f32x4 acc[NB];
   img_gemm<NB>(himg, wimg, a.kp1, a.np1, rb, NB * half, li, lg, acc);
-  if (rr >= a.R || (a.dbg & 8)) return;
+  if (rr >= a.R || (kdbg(a.dbg) & 8)) return;
 #pragma unroll
   for (int i = 0; i < NB; ++i) {
     const int n0 = 16 * (NB * half + i) + 4 * lg;

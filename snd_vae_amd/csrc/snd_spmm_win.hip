@@ -80,9 +80,9 @@ struct WinArgs {
   __bf16* out;
   int ldo;
   int n, spg, seg, beta8;
-  int dbg;   // measurement only (snd_debug_set >> 24): 1 no sums, 2 no window DMA, 4 no slot DMA,
-             // 8 non-temporal output stores, 16 non-temporal window DMA, 32 two barriers
-             // per step at any beta
+  int dbg;   // snd_debug_set >> 24.  A/B (both builds): 32 two barriers per step at any beta,
+             // 64 wave w sums group w (no SIMD balancing).  Measurement build only
+             // (MEAS, any of bits 1-4 set): 1 no sums, 2 no window DMA, 4 no slot DMA
 };
 
 // fp32 sums without unpacking: v_dot2c_f32_bf16 with (1, 0) / (0, 1) adds the low /
@@ -121,14 +121,10 @@ constexpr int vmcnt_imm(int n) { return (n & 15) | (7 << 4) | (15 << 8) | ((n >>
 
 // global -> LDS DMA of `bytes` (4 or 16) per active lane to the wave-uniform LDS
 // address `dst` + 4/16 x lane (the compiler does not see it: vmcnt counted by hand)
-template <int BYTES, bool NT = false>
+template <int BYTES>
 __device__ __forceinline__ void glds(const void* src, unsigned dst) {
   unsigned keep;
-  if constexpr (BYTES == 16 && NT)   // streamed once: non-temporal
-    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
-                 "global_load_lds_dwordx4 %1, off nt\n\ts_mov_b32 m0, %0"
-                 : "=&s"(keep) : "v"(src), "s"(dst) : "memory");
-  else if constexpr (BYTES == 16)
+  if constexpr (BYTES == 16)
     asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
                  "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
                  : "=&s"(keep) : "v"(src), "s"(dst) : "memory");
@@ -144,8 +140,10 @@ __device__ __forceinline__ void raw_barrier() {
   asm volatile("" ::: "memory");
 }
 
-template <int GK>
+template <int GK, bool MEAS>
 __global__ void __launch_bounds__(WT) spmm_win_kernel(WinArgs a) {
+  // the phase-skip bits exist in the measurement instantiation only
+  const int skip = MEAS ? (a.dbg & 7) : 0;
   __shared__ __attribute__((aligned(16))) char lds[LDS_BYTES];
   const unsigned lds0 = (unsigned)(uintptr_t)(lptr_t)lds;   // LDS byte address of lds[0]
   const int g = blockIdx.x / a.spg, sg = blockIdx.x - g * a.spg;
@@ -158,8 +156,13 @@ __global__ void __launch_bounds__(WT) spmm_win_kernel(WinArgs a) {
   const int Q1 = min(a.n, P1 + a.beta8);          // window end (exclusive)
   // last window position step s reads
   auto hi = [&](int s) { return min(P0 + STEP * s + STEP - 1 + a.beta8, Q1 - 1); };
+  // the 8-row group this wave sums: groups are listed by degree (descending) inside
+  // each step, and wave w runs on SIMD w % 4, so the snake {s, 7 - s, 8 + s, 15 - s}
+  // gives every SIMD the same share of the step's neighbours (w % 4 = s; dbg 64: group w)
+  const int sm = w & 3, wk = w >> 2;
+  const int grp = (a.dbg & 64) ? w : (wk == 0 ? sm : wk == 1 ? 7 - sm : wk == 2 ? 8 + sm : 15 - sm);
   // graph-local position of row j (0..7) of this wave at step s (clamped: duplicates are benign)
-  auto rpos = [&](int s, int j) { return min(P0 + STEP * s + 8 * w + j, P1 - 1); };
+  auto rpos = [&](int s, int j) { return min(P0 + STEP * s + 8 * grp + j, P1 - 1); };
   // first position of the 8-row piece this wave DMAs at step s (8-aligned; past the
   // window end it lands in dead ring rows)
   auto dpiece = [&](int s) { return ((hi(s + 1) + 8) & ~7) + 8 * w; };
@@ -187,11 +190,10 @@ __global__ void __launch_bounds__(WT) spmm_win_kernel(WinArgs a) {
   auto dma_piece = [&](int p0, int row) {
     const __bf16* src = a.h + (long long)row * a.ldh + 8 * l8;
     const unsigned dst = __builtin_amdgcn_readfirstlane(lds0 + (p0 % RR) * (WIDTH * 2));
-    // A/B (debug 16): non-temporal window DMA.  Within noise on the 256-graph batch
-    // (77-82 us either way), 1.5-4 us slower in the C2 step, where h was just written
-    // and still sits in L2 / the Infinity Cache: allocating loads stay the default
-    if (a.dbg & 16) glds<16, true>(src, dst);
-    else glds<16>(src, dst);
+    // allocating loads: non-temporal window DMA measured within noise on the 256-graph
+    // batch and 1.5-4 us slower in the C2 step, where h was just written and still sits
+    // in L2 / the Infinity Cache (retired A/B)
+    glds<16>(src, dst);
   };
   auto lds_i32 = [&](int off) { return *reinterpret_cast<const int*>(lds + off); };
 
@@ -220,8 +222,8 @@ __global__ void __launch_bounds__(WT) spmm_win_kernel(WinArgs a) {
     const int st1 = lds_i32(idx_blk(s + 1) + 4 * (lane >> 2)) >> 6;
     const int prow = lds_i32(idx_blk(s) + 64 + 4 * r8);
     dma_index(s + 3);
-    if (!(a.dbg & 4)) dma_slots(s + 1, st1);
-    if (!(a.dbg & 2)) dma_piece(dpiece(s), prow);
+    if (!(skip & 4)) dma_slots(s + 1, st1);
+    if (!(skip & 2)) dma_piece(dpiece(s), prow);
   };
   // One barrier per step when the window leaves room: the DMAs of step s are issued
   // after its barrier (every wave has finished step s-1, the last reader of the
@@ -261,7 +263,7 @@ __global__ void __launch_bounds__(WT) spmm_win_kernel(WinArgs a) {
       for (int j = 0; j < 8; ++j) f[j] = 0.f;
   #pragma unroll
       for (int k0 = 0; k0 < 32; k0 += GK) {
-        if (!__builtin_amdgcn_ballot_w64(deg > k0) || (a.dbg & 1)) break;
+        if (!__builtin_amdgcn_ballot_w64(deg > k0) || (skip & 1)) break;
         uint4 d[GK];
   #pragma unroll
         for (int j = 0; j < GK; ++j) {
@@ -284,13 +286,8 @@ __global__ void __launch_bounds__(WT) spmm_win_kernel(WinArgs a) {
       bf16x8 o;
   #pragma unroll
       for (int j = 0; j < 8; ++j) o[j] = (__bf16)f[j];
-      __bf16* op = a.out + (long long)row0 * a.ldo + 8 * l8;
-      if (!(a.dbg & 8)) {
-        *reinterpret_cast<bf16x8*>(op) = o;
-      } else {   // A/B: non-temporal output stores
-        typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
-        __builtin_nontemporal_store(__builtin_bit_cast(u32x4_t, o), reinterpret_cast<u32x4_t*>(op));
-      }
+      // (non-temporal output stores measured no faster: retired A/B)
+      *reinterpret_cast<bf16x8*>(a.out + (long long)row0 * a.ldo + 8 * l8) = o;
     }
 
     // every wave's LDS reads of this step are done (their values were consumed)
@@ -325,7 +322,8 @@ int launch_spmm_window(const SpmmWinArgs& w, hipStream_t st) {
   WinArgs a{w.meta, w.slots, w.rows, w.order, reinterpret_cast<const __bf16*>(w.h), w.ldh,
             reinterpret_cast<__bf16*>(w.out), w.ldo, w.n_per_graph, cdiv(w.n_per_graph, seg), seg, beta8,
             debug_flags() >> 24};
-  hipLaunchKernelGGL((spmm_win_kernel<4>), dim3(w.n_graphs * a.spg), dim3(WT), 0, st, a);
+  if (a.dbg & 7) hipLaunchKernelGGL((spmm_win_kernel<4, true>), dim3(w.n_graphs * a.spg), dim3(WT), 0, st, a);
+  else hipLaunchKernelGGL((spmm_win_kernel<4, false>), dim3(w.n_graphs * a.spg), dim3(WT), 0, st, a);
   SND_LAUNCH_CHECK("spmm_win_kernel");
   return 0;
 }

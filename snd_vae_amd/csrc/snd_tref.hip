@@ -159,16 +159,8 @@ int head_fwd_rpb(long long K, int gh) {
 // per-row dot products dG[b, k] = dh[b, :] . Wh[k, :] are reduced over the 32
 // lanes of the half with DPP (row16) + one xor-16 swizzle, and parked in LDS so
 // dG leaves the block as coalesced rows.
-#ifndef SND_HB_RPB
-#define SND_HB_RPB 256
-#endif
-#ifndef SND_HB_U
-#define SND_HB_U 4
-#endif
-#ifndef SND_PB_U
-#define SND_PB_U 5
-#endif
-constexpr int HB_T = 256, HB_RPB = SND_HB_RPB;   // A/B builds: -DSND_HB_RPB=... (tools/build_ab.sh)
+// (rows per block, row pairs / rows in flight: other values measured flat or worse, round 3)
+constexpr int HB_T = 256, HB_RPB = 256;
 
 __global__ void __launch_bounds__(HB_T) tref_head_bwd_kernel(TrefHeadBwdArgs a) {
   __shared__ float gs[HB_RPB * B8];      // G[b, k0 + kk] as [kk][8]
@@ -189,7 +181,7 @@ __global__ void __launch_bounds__(HB_T) tref_head_bwd_kernel(TrefHeadBwdArgs a) 
   __syncthreads();
   const bool fused = a.adam.p != nullptr;
   const float lrt = fused ? adam_lrt(a.adam) : 0.f;
-  constexpr int U = SND_HB_U;            // row pairs in flight per wave
+  constexpr int U = 4;                   // row pairs in flight per wave
   const int r0 = 2 * wv + h;             // row slot of this lane; 8 rows per block pass
   for (int base = 0; base < nk; base += 8 * U) {
     float4 w[U], am[U], av[U];
@@ -353,7 +345,7 @@ __global__ void __launch_bounds__(PB_T) tref_proj_bwd_kernel(TrefProjBwdArgs a) 
   __syncthreads();
   const bool fused = a.adam.p != nullptr;
   const float lrt = fused ? adam_lrt(a.adam) : 0.f;
-  constexpr int U = SND_PB_U;
+  constexpr int U = 5;                   // weight rows in flight per thread
   for (int l0 = wv; l0 < a.L; l0 += PB_W * U) {
     float4 w[U], am[U], av[U];
 #pragma unroll

@@ -267,276 +267,13 @@ __global__ void __launch_bounds__(NTH) zzt_dense_bf16(ZztArgs a) {
   block_reduce_write(st, a.part);
 }
 
-// ---------------------------------------------------------------- v3 / v4 geometry
+// ---------------------------------------------------------------- v4 / v7 geometry
 // 1024-thread workgroup over 128 rows of one graph: 16 waves per CU (4 per SIMD)
 // so one wave's VALU epilogue overlaps another's MFMAs; column tiles of TJ2 = 128.
-// (Round 1's v2, 8 row groups x 2 column halves with a masked epilogue, is gone:
-// v3 replaced it with the mask-free loop below.)
+// (Round 1's v2 and round 2's v3 -- 16x16x32 MFMAs, the |x| epilogue -- are retired.)
 constexpr int TJ2 = 128;
 constexpr int NTH2 = 1024;
 
-
-// ---------------------------------------------------------------- bf16 MFMA, v3
-// 8 row groups (16 rows) x 2 column halves (32-column chunks of every tile),
-// with a mask-free main loop.  Every (i, j) of the padded
-// npad x npad square is evaluated; afterwards
-//   * padded pairs (zero rows, x = 0 exactly: 1 log2-unit of loss each, no
-//     sign count, sigma * 0 = 0 into dJ) are subtracted analytically;
-//   * the diagonal (x_ii from the wave's own z_i registers) is subtracted
-//     from loss, count and dJ_i (sigma rounded to bf16 as the MFMA saw it).
-// max(x, 0) = (x + |x|) / 2 with sum_j x_ij = z_i . sum_j z_j computed from
-// per-64-row column sums written by the prep kernel: one |x| add per logit.
-// Per logit: exp2, rcp (transcendental), q = 1 + e, running product, |x|
-// add, sign compare (its mask feeds the sigma select and a SALU popcount),
-// sigma multiply + select, bf16 pack.
-__device__ __forceinline__ void chunk_epilogue3(const f32x4& X0, const f32x4& X1, bf16x8& sb,
-                                                float& labs, float& llog, unsigned& wcnt) {
-  float prod0 = 1.f, prod1 = 1.f, sa = 0.f;
-  unsigned wc = 0;
-#pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    const float xv = e < 4 ? X0[e] : X1[e - 4];
-    // (an inline-asm v_exp_f32 with the -|x| modifier would drop the v_and hipcc
-    // keeps for |x|, but the hazard recognizer does not see a transcendental inside
-    // asm: a dependent VALU may read the result without the required wait states)
-    const float ex = __builtin_amdgcn_exp2f(-fabsf(xv));
-    const float qd = 1.f + ex;
-    const float rc = __builtin_amdgcn_rcpf(qd);
-    const bool pos = xv > 0.f;
-    if (e & 1) prod1 *= qd; else prod0 *= qd;
-    sa = __builtin_fmaf(fabsf(xv), 0.5f, sa);   // v_fma_f32 takes |x| as a source modifier (an add gets a v_and)
-    sb[e] = (__bf16)(pos ? rc : ex * rc);
-    wc += (unsigned)__popcll(__ballot(pos));
-  }
-  labs += sa;
-  llog += __builtin_amdgcn_logf(prod0 * prod1);
-  wcnt += wc;
-}
-
-template <int DP>
-__global__ void __launch_bounds__(NTH2) zzt_dense_bf16_v3(ZztArgs a) {
-  constexpr int JS = TJ2 * DP;
-  constexpr int TS = DP * TJ2;
-  constexpr int KS = DP / 32;
-  constexpr int CT = DP / 16;
-  constexpr int CPR = DP / 8;
-  constexpr int TCPR = TJ2 / 8;
-  constexpr int JCH = TJ2 * CPR, TCH = DP * TCPR;
-  constexpr int JPT = (JCH + NTH2 - 1) / NTH2, TPT = (TCH + NTH2 - 1) / NTH2;
-  __shared__ __attribute__((aligned(16))) __bf16 lds[2][JS + TS];
-  __shared__ float colsum[DP];
-  __shared__ float csred[NTH2 / DP][DP];
-
-  // block -> (column split sp, graph g, row block rb)
-  const int wgs = a.ngraphs * zrb(a);
-  const int sp = blockIdx.x / wgs, bx = blockIdx.x - sp * wgs;
-  const int nsplit = gridDim.x / wgs;
-  const int g = bx % a.ngraphs, rb = a.rb0 + bx / a.ngraphs;
-  const __bf16* Jg = reinterpret_cast<const __bf16*>(a.jrow) + (long long)g * a.npad * DP;
-  const __bf16* JTg = reinterpret_cast<const __bf16*>(a.jt) + (long long)g * DP * a.npad;
-  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, r = lane & 15, q4 = lane >> 4;
-  const int rg = w & 7, half = w >> 3;
-  const int i0 = __builtin_amdgcn_readfirstlane(rb * ROWS + 16 * rg);
-  const int i_me = i0 + r;
-
-  bf16x8 bI[KS];
-#pragma unroll
-  for (int ks = 0; ks < KS; ++ks)
-    bI[ks] = *reinterpret_cast<const bf16x8*>(Jg + (long long)i_me * DP + 32 * ks + 8 * q4);
-  // graph column sums S_k = sum_j zs_jk (fixed order over the 64-row partials)
-  {
-    const int nrb = a.npad / 64;
-    const int k = tid % DP, grp = tid / DP;
-    constexpr int NG = NTH2 / DP;
-    float s = 0.f;
-    for (int p = grp; p < nrb; p += NG) s += a.colpart[((long long)g * nrb + p) * DP + k];
-    csred[grp][k] = s;
-  }
-  __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): see v2
-  __syncthreads();
-  if (tid < DP) {
-    float s = 0.f;
-    for (int p = 0; p < NTH2 / DP; ++p) s += csred[p][tid];
-    colsum[tid] = s;
-  }
-  f32x4 acc[CT];
-#pragma unroll
-  for (int ct = 0; ct < CT; ++ct) acc[ct] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  uint4 rj[JPT], rt[TPT];
-  auto gload = [&](int t) {
-#pragma unroll
-    for (int p = 0; p < JPT; ++p) {
-      const int idx = tid + p * NTH2;
-      if (idx < JCH) {
-        const int row = idx / CPR, ch = idx - row * CPR;
-        rj[p] = *reinterpret_cast<const uint4*>(Jg + (long long)(t * TJ2 + row) * DP + ch * 8);
-      }
-    }
-#pragma unroll
-    for (int p = 0; p < TPT; ++p) {
-      const int idx = tid + p * NTH2;
-      if (idx < TCH) {
-        const int c = idx / TCPR, ch = idx - c * TCPR;
-        rt[p] = *reinterpret_cast<const uint4*>(JTg + (long long)c * a.npad + t * TJ2 + ch * 8);
-      }
-    }
-  };
-  auto sstore = [&](int buf) {
-#pragma unroll
-    for (int p = 0; p < JPT; ++p) {
-      const int idx = tid + p * NTH2;
-      if (idx < JCH) {
-        const int row = idx / CPR, ch = idx - row * CPR;
-        *reinterpret_cast<uint4*>(&lds[buf][row * DP + ((ch ^ Swz<DP>::j(row)) * 8)]) = rj[p];
-      }
-    }
-    // z^T image for the PV A-operand: inside every 32-column block the two
-    // 4-column groups a lane needs (j = 4g.., 16 + 4g..) are stored as one 16 B
-    // chunk g, so the operand is ONE ds_read_b128; chunks XOR-swizzled by
-    // (c & 15), conflict-free over the b128 lane groups.
-#pragma unroll
-    for (int p = 0; p < TPT; ++p) {
-      const int idx = tid + p * NTH2;
-      if (idx < TCH) {
-        const int c = idx / TCPR, ch = idx - c * TCPR;
-        const int blk = ch >> 2, m = ch & 3, hsel = m >> 1;
-        const int c0 = ((4 * blk + ((2 * m) & 3)) ^ (c & 15)) * 8 + 4 * hsel;
-        const int c1 = ((4 * blk + ((2 * m + 1) & 3)) ^ (c & 15)) * 8 + 4 * hsel;
-        __bf16* row = &lds[buf][JS + c * TJ2];
-        *reinterpret_cast<uint2*>(row + c0) = make_uint2(rt[p].x, rt[p].y);
-        *reinterpret_cast<uint2*>(row + c1) = make_uint2(rt[p].z, rt[p].w);
-      }
-    }
-  };
-  auto qk = [&](const __bf16* Ls, int q, f32x4& X0, f32x4& X1) {
-    X0 = f32x4{0.f, 0.f, 0.f, 0.f};
-    X1 = f32x4{0.f, 0.f, 0.f, 0.f};
-    const int ra = 32 * q + r, rb2 = 32 * q + 16 + r;
-#pragma unroll
-    for (int ks = 0; ks < KS; ++ks) {
-      const bf16x8 a0 = *reinterpret_cast<const bf16x8*>(
-          &Ls[ra * DP + (((4 * ks + q4) ^ Swz<DP>::j(ra)) * 8)]);
-      const bf16x8 a1 = *reinterpret_cast<const bf16x8*>(
-          &Ls[rb2 * DP + (((4 * ks + q4) ^ Swz<DP>::j(rb2)) * 8)]);
-      X0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, bI[ks], X0, 0, 0, 0);
-      X1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, bI[ks], X1, 0, 0, 0);
-    }
-  };
-  auto pv = [&](const __bf16* Ls, int q, const bf16x8& sb) {
-#pragma unroll
-    for (int ct = 0; ct < CT; ++ct) {
-      const int c = 16 * ct + r;
-      const bf16x8 a2 = *reinterpret_cast<const bf16x8*>(
-          &Ls[JS + c * TJ2 + (((4 * q + q4) ^ (c & 15)) * 8)]);
-      acc[ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a2, sb, acc[ct], 0, 0, 0);
-    }
-  };
-
-  const int ntot = a.npad / TJ2;
-  const int t0 = sp * ntot / nsplit, ntiles = (sp + 1) * ntot / nsplit;
-  gload(t0);
-  sstore(0);
-  __syncthreads();
-  float labs = 0.f, llog = 0.f;
-  double ltot = 0.0;
-  unsigned wcnt = 0;
-  const int qa = 2 * half, qb = 2 * half + 1;
-  // one tile out of LDS buffer CUR (a compile-time constant: the loop runs two
-  // tiles per trip, so every LDS address is a per-lane base + an immediate)
-  auto tile = [&](int t, auto curc) {
-    constexpr int cur = decltype(curc)::value;
-    // branch-free body (the last tile reloads itself into the idle buffer): one
-    // basic block, so |x| folds into the accumulate as a source modifier
-    gload(min(t + 1, ntiles - 1));
-    const __bf16* Ls = lds[cur];
-    f32x4 Xa0, Xa1, Xb0, Xb1;
-    bf16x8 sa, sbv;
-    qk(Ls, qa, Xa0, Xa1);
-    qk(Ls, qb, Xb0, Xb1);
-    chunk_epilogue3(Xa0, Xa1, sa, labs, llog, wcnt);
-    pv(Ls, qa, sa);
-    chunk_epilogue3(Xb0, Xb1, sbv, labs, llog, wcnt);
-    pv(Ls, qb, sbv);
-    sstore(cur ^ 1);
-    __syncthreads();
-  };
-  for (int t = t0; t < ntiles; t += 2) {
-    tile(t, std::integral_constant<int, 0>{});
-    if (t + 1 < ntiles) tile(t + 1, std::integral_constant<int, 1>{});
-    if (((t - t0) & 7) == 6) {      // keep the fp32 partial sums short
-      ltot += (double)(labs + llog);
-      labs = 0.f;
-      llog = 0.f;
-    }
-  }
-  ltot += (double)(labs + llog);
-
-  // ---- corrections (row i = i_me; the 4 q4-lanes of a row share them)
-  float xd = 0.f, xs = 0.f;           // x_ii and sum_j x_ij (this lane's k-slice)
-#pragma unroll
-  for (int ks = 0; ks < KS; ++ks)
-#pragma unroll
-    for (int jj = 0; jj < 8; ++jj) {
-      const float b = (float)bI[ks][jj];
-      xd += b * b;
-      xs += b * colsum[32 * ks + 8 * q4 + jj];
-    }
-  xd += __shfl_xor(xd, 16, 64);
-  xd += __shfl_xor(xd, 32, 64);
-  xs += __shfl_xor(xs, 16, 64);
-  xs += __shfl_xor(xs, 32, 64);
-  const bool row_valid = i_me < a.n;
-  const bool corr = sp == 0;           // analytic corrections: once per row, in split 0
-  const float exd = __builtin_amdgcn_exp2f(-fabsf(xd));
-  const float sgd = xd > 0.f ? 1.f / (1.f + exd) : exd / (1.f + exd);
-  if (half == 0 && q4 == 0 && row_valid && corr) {
-    // + sum_j x_ij / 2 (the other half of max(x,0)); - softplus2(x_ii)
-    ltot += 0.5 * (double)xs;
-    ltot -= (double)(fmaxf(xd, 0.f) + __builtin_amdgcn_logf(1.f + exd));
-  }
-  const unsigned dpos = (unsigned)__popcll(__ballot(half == 0 && q4 == 0 && row_valid && corr && xd > 0.f));
-
-  // ---- combine the two column halves' partial dJ, subtract the diagonal term
-  float* red = reinterpret_cast<float*>(&lds[0][0]);
-  const int slot = (rg * 64 + lane) * (4 * CT);
-  if (half == 1) {
-#pragma unroll
-    for (int ct = 0; ct < CT; ++ct)
-      *reinterpret_cast<f32x4*>(&red[slot + 4 * ct]) = acc[ct];
-  }
-  __syncthreads();
-  if (half == 0 && row_valid) {
-    const float sgb = corr ? (float)(__bf16)sgd : 0.f;   // sigma as the PV-MFMA consumed it
-    float* dst = (sp == 0 ? a.dJd : a.dJd_extra + (long long)(sp - 1) * a.ngraphs * a.n * a.d) +
-                 ((long long)g * a.n + i_me) * a.d;
-#pragma unroll
-    for (int ct = 0; ct < CT; ++ct) {
-      const f32x4 o = *reinterpret_cast<const f32x4*>(&red[slot + 4 * ct]);
-      const int c0 = 16 * ct + 4 * q4;
-      if (c0 < a.d) {
-        float v[4];
-#pragma unroll
-        for (int e = 0; e < 4; ++e)
-          v[e] = acc[ct][e] + o[e] - sgb * (float)JTg[(long long)(c0 + e) * a.npad + i_me];
-        *reinterpret_cast<float4*>(dst + c0) = make_float4(v[0], v[1], v[2], v[3]);
-      }
-    }
-  }
-  __shared__ double sl[NTH2 / 64];
-  __shared__ unsigned sc[NTH2 / 64];
-  const double l = wave_sum_d(ltot);
-  if (lane == 0) { sl[w] = l; sc[w] = wcnt - dpos; }
-  __syncthreads();
-  if (tid == 0) {
-    double tl = 0.0, tc = 0.0;
-    for (int k = 0; k < NTH2 / 64; ++k) { tl += sl[k]; tc += (double)sc[k]; }
-    if (corr)   // padded pairs of this row block: x = 0 exactly, log2(1 + 1) = 1 each
-      tl -= zzt_padded_pairs(a, rb);
-    a.part[2 * blockIdx.x] = tl * (double)kLn2;
-    a.part[2 * blockIdx.x + 1] = tc;
-  }
-}
 
 // ---------------------------------------------------------------- f32 MFMA
 __device__ __forceinline__ int hJ(int row) { return ((row & 1) << 1) | (((row >> 1) & 7) << 2); }
@@ -682,7 +419,7 @@ __global__ void __launch_bounds__(NTH) zzt_dense_f32(ZztArgs a) {
 //   bwd   dJ'[i][c] += S'[i][j] z_j[c] A = S' packed straight from Y's registers
 //                                    (its column i is on the lane), B = z^T
 //                                    (LDS, j order permuted to match)
-// Epilogue per logit (EPI 0), y = -x:
+// Epilogue per logit, y = -x:
 //   e = 2^y; q = 1 + e; s = 1/q = sigmoid(x); per QUAD of logits one
 //   log2(q_a q_b q_c q_d); #{x > 0} = #{sign(y)}: sign bytes of 4 logits gathered by two
 //   v_perm and popcounted (1 op per logit instead of a compare + SALU ballot).
@@ -692,25 +429,19 @@ __global__ void __launch_bounds__(NTH) zzt_dense_f32(ZztArgs a) {
 // (L_a + .. + L_d < -88.7): that lane recomputes the block's loss terms in the |x|
 // form (one wave-uniform test per block when nothing overflows).
 // Measured rates (tools/micro/valu_rate.hip, 4 waves per SIMD): a transcendental
-// costs ~3.4 FMAs of issue and does not co-issue with them; compare + ballot ~2
-// FMAs.  EPI 0 (2.25 transcendentals + ~2.5 other ops per logit) beats v3's |x|
-// form (EPI 1: 2.125 + ~6.9).  c (kZ4C) stays a parameter: a nonzero c needs the
-// ballot count (y < -c) back.
-// Tiles are triple-buffered (global loads two tiles ahead).  MODE 1 issues tile
-// t+1's forward MFMAs before tile t's epilogue (matrix pipe beside the wave's own
-// VALU; it spills at d = 64); MODE 2 runs odd column-block waves' backward MFMAs
-// one tile late.  Measured at C2 within one run: MODE 0 62.1 us, MODE 2 63.3,
-// MODE 1 67.0, v3 65.1 (phase split of MODE 0, stamps: prologue 3.2 us, tile
-// loop ~48 us of which the epilogue VALU ~60 %, corrections + stores 2.4 us).
+// costs ~3.4 FMAs of issue and does not co-issue with them.  This signed epilogue
+// (2.25 transcendentals + ~2.5 other ops per logit) beat round 1's |x| form
+// (2.125 + ~6.9).  Tiles are triple-buffered (global loads two tiles ahead).
+// Variants measured slower and retired: the next tile's forward MFMAs
+// before this tile's epilogue (spills at d = 64), odd column blocks' backward one
+// tile late, the |x| epilogue, one wave per SIMD with a block-level software
+// pipeline (v8: 89-95 us against 60 us).
 // LDS images carry one 16 B pad per row: every operand read of a lane group
 // lands on 16 distinct 4-bank groups and all k-steps / output blocks of a lane
 // share one address register.  The diagonal correction reads z_i[c] from a
 // transposed LDS copy of the workgroup's z^T columns (one coalesced load).
-constexpr float kZ4C = 0.f;             // c (an inline constant of the MFMA's C operand)
-constexpr float kZ4Q = 1.f;              // 2^-c
-constexpr float kZ4S = 1.f;              // dJ scale 2^-c
 
-template <int DP, int MODE, int EPI, bool MEAS>
+template <int DP, bool MEAS>
 __global__ void __launch_bounds__(NTH2) zzt_dense_bf16_v4(ZztArgs a) {
   constexpr int NT = NTH2, NW = NT / 64;
   constexpr int KS = DP / 16;          // forward k-steps
@@ -723,9 +454,7 @@ __global__ void __launch_bounds__(NTH2) zzt_dense_bf16_v4(ZztArgs a) {
   constexpr int CPR = DP / 8, TCPR = TJ2 / 8;
   constexpr int JCH = TJ2 * CPR, TCH = DP * TCPR;
   constexpr int JPT = (JCH + NT - 1) / NT, TPT = (TCH + NT - 1) / NT;
-  constexpr float C4 = EPI != 1 ? kZ4C : 0.f;
-  static_assert(kZ4C == 0.f, "EPI 0 counts x > 0 by the sign of y = -x - c: c must be 0");
-  constexpr unsigned NEG = EPI != 1 ? 0x80008000u : 0u;   // B operand sign
+  constexpr unsigned NEG = 0x80008000u;   // B operand sign: the forward computes y = -x
   __shared__ __attribute__((aligned(16))) __bf16 lds[3 * BUF];
   __shared__ __attribute__((aligned(16))) __bf16 brows[ROWS * JST];   // (-)z_i rows (scaled)
   __shared__ __attribute__((aligned(16))) __bf16 zown[ROWS * JST];    // z_i rows (z^T values)
@@ -822,10 +551,8 @@ __global__ void __launch_bounds__(NTH2) zzt_dense_bf16_v4(ZztArgs a) {
     csred[grp][k] = s;
   }
   sstore(lds);
-  if (MODE != 2) {
-    gload(min(t0 + 1, t1 - 1));
-    sstore(lds + BUF);
-  }
+  gload(min(t0 + 1, t1 - 1));
+  sstore(lds + BUF);
   __syncthreads();
   if (tid < DP) {
     float s = 0.f;
@@ -836,10 +563,10 @@ __global__ void __launch_bounds__(NTH2) zzt_dense_bf16_v4(ZztArgs a) {
   if (skip & 32) { ts[1] = __builtin_amdgcn_s_memrealtime(); tcy[0] = __builtin_amdgcn_s_memtime(); }
 
   f32x16 cinit, acc[CB];
-  // +0 (not -0.0 = -C4 at c = 0): a zero accumulator folds into the MFMA's inline
-  // constant 0; a -0.0 splat pinned 16 VGPRs and cost 24 moves per tile
+  // +0 accumulator init: a zero accumulator folds into the MFMA's inline constant 0 (a
+  // -0.0 splat pinned 16 VGPRs and cost 24 moves per tile)
 #pragma unroll
-  for (int v = 0; v < 16; ++v) cinit[v] = C4 == 0.f ? 0.f : -C4;
+  for (int v = 0; v < 16; ++v) cinit[v] = 0.f;
 #pragma unroll
   for (int q = 0; q < CB; ++q)
 #pragma unroll
@@ -855,66 +582,45 @@ __global__ void __launch_bounds__(NTH2) zzt_dense_bf16_v4(ZztArgs a) {
     }
     return X;
   };
-  float lacc = 0.f, labs = 0.f;
+  float lacc = 0.f;
   double ltot = 0.0;
-  unsigned wcnt = 0, lcnt = 0;   // per wave (EPI 1 ballots) / per lane (EPI 0 sign bits)
+  unsigned lcnt = 0;   // per lane: sign bits counted
   // sticky, wave-uniform: once a quad product of this wave overflowed, later tiles skip
   // the products (logits that large, e.g. C4's graph-latent heads at init, recur)
   bool ovf = false;
   auto epi = [&](const f32x16& Y, bf16x8 (&sA)[2]) {
-    if constexpr (EPI != 1) {
-      float q[16], lt = 0.f;
+    float q[16], lt = 0.f;
 #pragma unroll
-      for (int v = 0; v < 16; ++v) {
-        const float e = __builtin_amdgcn_exp2f(Y[v]);
-        q[v] = e + kZ4Q;
-        sA[v >> 3][v & 7] = (__bf16)__builtin_amdgcn_rcpf(q[v]);
-      }
-      // #{x > 0} = #{y < 0} (c = 0; y = +0 where x = 0): the sign bytes of four y's
-      // gathered by two v_perm, masked, popcounted into a per-lane count
-#pragma unroll
-      for (int g4 = 0; g4 < 4; ++g4) {
-        const unsigned t01 = __builtin_amdgcn_perm(__float_as_uint(Y[4 * g4 + 1]),
-                                                   __float_as_uint(Y[4 * g4]), 0x0C0C0703u);
-        const unsigned t23 = __builtin_amdgcn_perm(__float_as_uint(Y[4 * g4 + 3]),
-                                                   __float_as_uint(Y[4 * g4 + 2]), 0x07030C0Cu);
-        lcnt += (unsigned)__builtin_popcount((t01 | t23) & 0x80808080u);
-      }
-      if (!ovf) {
-#pragma unroll
-        for (int p = 0; p < 4; ++p)   // one log2 per 4 logits (an overflowing product: fallback below)
-          lt += __builtin_amdgcn_logf((q[4 * p] * q[4 * p + 1]) * (q[4 * p + 2] * q[4 * p + 3]));
-        ovf = __builtin_amdgcn_ballot_w64(!__builtin_isfinite(lt)) != 0;
-      }
-      if (__builtin_expect(ovf, 0)) {
-        // a quad product overflowed: the block one logit at a time,
-        // log2(q) = y for y > 24 (1 + 2^y rounds to 2^y; q may be inf), else log2(q)
-        // (one transcendental per logit on the q already computed; c = 0)
-        lt = 0.f;
-#pragma unroll
-        for (int v = 0; v < 16; ++v) lt += Y[v] > 24.f ? Y[v] : __builtin_amdgcn_logf(q[v]);
-      }
-      lacc += lt + 16.f * kZ4C;   // + c per logit: the sum stays small in fp32
-    } else {   // v3's |x| form: sigma = x > 0 ? r : e r, one log2 per 8 logits
-#pragma unroll
-      for (int hb = 0; hb < 2; ++hb) {
-        float prod0 = 1.f, prod1 = 1.f, sa = 0.f;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const float xv = Y[8 * hb + e];
-          const float ex = __builtin_amdgcn_exp2f(-fabsf(xv));
-          const float qd = 1.f + ex;
-          const float rc = __builtin_amdgcn_rcpf(qd);
-          const bool pos = xv > 0.f;
-          if (e & 1) prod1 *= qd; else prod0 *= qd;
-          sa = __builtin_fmaf(fabsf(xv), 0.5f, sa);
-          sA[hb][e] = (__bf16)(pos ? rc : ex * rc);
-          wcnt += (unsigned)__popcll(__ballot(pos));
-        }
-        labs += sa;
-        lacc += __builtin_amdgcn_logf(prod0 * prod1);
-      }
+    for (int v = 0; v < 16; ++v) {
+      const float e = __builtin_amdgcn_exp2f(Y[v]);
+      q[v] = e + 1.f;
+      sA[v >> 3][v & 7] = (__bf16)__builtin_amdgcn_rcpf(q[v]);
     }
+    // #{x > 0} = #{y < 0} (y = +0 where x = 0): the sign bytes of four y's gathered
+    // by two v_perm, masked, popcounted into a per-lane count
+#pragma unroll
+    for (int g4 = 0; g4 < 4; ++g4) {
+      const unsigned t01 = __builtin_amdgcn_perm(__float_as_uint(Y[4 * g4 + 1]),
+                                                 __float_as_uint(Y[4 * g4]), 0x0C0C0703u);
+      const unsigned t23 = __builtin_amdgcn_perm(__float_as_uint(Y[4 * g4 + 3]),
+                                                 __float_as_uint(Y[4 * g4 + 2]), 0x07030C0Cu);
+      lcnt += (unsigned)__builtin_popcount((t01 | t23) & 0x80808080u);
+    }
+    if (!ovf) {
+#pragma unroll
+      for (int p = 0; p < 4; ++p)   // one log2 per 4 logits (an overflowing product: fallback below)
+        lt += __builtin_amdgcn_logf((q[4 * p] * q[4 * p + 1]) * (q[4 * p + 2] * q[4 * p + 3]));
+      ovf = __builtin_amdgcn_ballot_w64(!__builtin_isfinite(lt)) != 0;
+    }
+    if (__builtin_expect(ovf, 0)) {
+      // a quad product overflowed: the block one logit at a time,
+      // log2(q) = y for y > 24 (1 + 2^y rounds to 2^y; q may be inf), else log2(q)
+      // (one transcendental per logit on the q already computed)
+      lt = 0.f;
+#pragma unroll
+      for (int v = 0; v < 16; ++v) lt += Y[v] > 24.f ? Y[v] : __builtin_amdgcn_logf(q[v]);
+    }
+    lacc += lt;
   };
   auto bwd = [&](const __bf16* L, const bf16x8 (&sA)[2]) {
 #pragma unroll
@@ -928,55 +634,22 @@ __global__ void __launch_bounds__(NTH2) zzt_dense_bf16_v4(ZztArgs a) {
   };
 
   f32x16 Y;
-  bf16x8 sPrev[2];
-  const bool late = MODE == 2 && (cb & 1);
-  if constexpr (MODE == 1) Y = fwd(lds);
   // one tile; buffer indices are compile-time, the last tiles re-stage the final
-  // tile (branch-free body); the extra MODE-1 forward result is dropped
+  // tile (branch-free body)
   auto tile = [&](int t, auto cc) {
-    constexpr int CUR = decltype(cc)::value, NXT = (CUR + 1) % 3, NN = (CUR + 2) % 3;
-    if constexpr (MODE == 2) {
-      // buffers: CUR = tile t, NN = tile t-1 (read late), NXT <- tile t+1
-      if (!(skip & 8)) gload(min(t + 1, t1 - 1));
-      if (late) {
-        if (t > t0 && !(skip & 4)) bwd(lds + NN * BUF, sPrev);
-        Y = (skip & 2) ? cinit : fwd(lds + CUR * BUF);
-        if (skip & 1) {
+    constexpr int CUR = decltype(cc)::value, NN = (CUR + 2) % 3;
+    if (!(skip & 8)) gload(min(t + 2, t1 - 1));
+    Y = (skip & 2) ? cinit : fwd(lds + CUR * BUF);
+    bf16x8 sA[2];
+    if (skip & 1) {
 #pragma unroll
-          for (int v = 0; v < 16; ++v) sPrev[v >> 3][v & 7] = (__bf16)Y[v];
-        } else {
-          epi(Y, sPrev);
-        }
-      } else {
-        Y = (skip & 2) ? cinit : fwd(lds + CUR * BUF);
-        bf16x8 sA[2];
-        if (skip & 1) {
-#pragma unroll
-          for (int v = 0; v < 16; ++v) sA[v >> 3][v & 7] = (__bf16)Y[v];
-        } else {
-          epi(Y, sA);
-        }
-        if (!(skip & 4)) bwd(lds + CUR * BUF, sA);
-        else lacc += (float)sA[0][0];
-      }
-      if (!(skip & 8)) sstore(lds + NXT * BUF);
+      for (int v = 0; v < 16; ++v) sA[v >> 3][v & 7] = (__bf16)Y[v];
     } else {
-      if (!(skip & 8)) gload(min(t + 2, t1 - 1));
-      f32x16 Yn;
-      if constexpr (MODE == 1) Yn = (skip & 2) ? cinit : fwd(lds + NXT * BUF);
-      else Y = (skip & 2) ? cinit : fwd(lds + CUR * BUF);
-      bf16x8 sA[2];
-      if (skip & 1) {
-#pragma unroll
-        for (int v = 0; v < 16; ++v) sA[v >> 3][v & 7] = (__bf16)Y[v];
-      } else {
-        epi(Y, sA);
-      }
-      if (!(skip & 4)) bwd(lds + CUR * BUF, sA);
-      else lacc += (float)sA[0][0];
-      if (!(skip & 8)) sstore(lds + NN * BUF);
-      if constexpr (MODE == 1) Y = Yn;
+      epi(Y, sA);
     }
+    if (!(skip & 4)) bwd(lds + CUR * BUF, sA);
+    else lacc += (float)sA[0][0];
+    if (!(skip & 8)) sstore(lds + NN * BUF);
     if (!(skip & 64)) __syncthreads();
   };
   const int tl1 = (skip & 16) ? t0 : t1;
@@ -984,11 +657,9 @@ __global__ void __launch_bounds__(NTH2) zzt_dense_bf16_v4(ZztArgs a) {
     tile(t, std::integral_constant<int, 0>{});
     if (t + 1 < tl1) tile(t + 1, std::integral_constant<int, 1>{});
     if (t + 2 < tl1) tile(t + 2, std::integral_constant<int, 2>{});
-    ltot += (double)(lacc + labs);   // keep the fp32 partial sums short
+    ltot += (double)lacc;   // keep the fp32 partial sums short
     lacc = 0.f;
-    labs = 0.f;
   }
-  if (late && tl1 > t0 && !(skip & 4)) bwd(lds + ((tl1 - 1 - t0) % 3) * BUF, sPrev);
   if (skip & 32) { ts[2] = __builtin_amdgcn_s_memrealtime(); tcy[1] = __builtin_amdgcn_s_memtime(); }
 
   // ---- per-row corrections (row i_me; lanes r and r + 32 hold its two k halves)
@@ -1005,26 +676,18 @@ __global__ void __launch_bounds__(NTH2) zzt_dense_bf16_v4(ZztArgs a) {
   }
   xd += __shfl_xor(xd, 32, 64);
   xs += __shfl_xor(xs, 32, 64);
-  if constexpr (EPI != 1) xs = -xs;
+  xs = -xs;
   const bool row_valid = i_me < a.n;
   const bool corr = sp == 0;
   const bool own = cb == 0 && h == 0 && row_valid && corr;
   const float exd = __builtin_amdgcn_exp2f(-fabsf(xd));
-  if (own) {
-    // EPI 0: + sum_j x_ij (softplus2(x) = x + log2(q) + c); EPI 1: + sum_j x_ij / 2
-    // (the other half of max(x, 0)); both: - softplus2(x_ii)
-    ltot += (EPI != 1 ? 1.0 : 0.5) * (double)xs;
+  if (own) {   // + sum_j x_ij (softplus2(x) = x + log2(q)), - softplus2(x_ii)
+    ltot += (double)xs;
     ltot -= (double)(fmaxf(xd, 0.f) + __builtin_amdgcn_logf(1.f + exd));
   }
   const unsigned dpos = (unsigned)__popcll(__ballot(own && xd > 0.f));
   if (cb == 0 && h == 0) {   // s'_ii as the backward MFMA consumed it (bf16), 0 outside split 0
-    float sg;
-    if constexpr (EPI != 1) {
-      sg = __builtin_amdgcn_rcpf(__builtin_amdgcn_exp2f(-xd - kZ4C) + kZ4Q);
-    } else {
-      const float rcd = __builtin_amdgcn_rcpf(1.f + exd);
-      sg = xd > 0.f ? rcd : exd * rcd;
-    }
+    const float sg = __builtin_amdgcn_rcpf(__builtin_amdgcn_exp2f(-xd) + 1.f);
     dsg[rg][r] = corr ? (float)(__bf16)sg : 0.f;
   }
 
@@ -1040,7 +703,6 @@ __global__ void __launch_bounds__(NTH2) zzt_dense_bf16_v4(ZztArgs a) {
   }
   __syncthreads();
   if (cb == 0 && !(skip & 32)) {
-    constexpr float scale = EPI != 1 ? kZ4S : 1.f;
     float* dst = (sp == 0 ? a.dJd : a.dJd_extra + (long long)(sp - 1) * a.ngraphs * a.n * a.d) +
                  (long long)g * a.n * a.d;
 #pragma unroll
@@ -1054,12 +716,12 @@ __global__ void __launch_bounds__(NTH2) zzt_dense_bf16_v4(ZztArgs a) {
         const int il = (v & 3) + 8 * (v >> 2) + 4 * h;   // D row within the row group
         const int i = i0 + il;
         if (i < a.n && c < a.d)
-          dst[(long long)i * a.d + c] = scale * (o - dsg[rg][il] * (float)zown[(32 * rg + il) * JST + c]);
+          dst[(long long)i * a.d + c] = o - dsg[rg][il] * (float)zown[(32 * rg + il) * JST + c];
       }
     }
   }
   const double l = wave_sum_d(ltot);
-  if constexpr (EPI == 0) wcnt = wave_sum_u(lcnt);
+  const unsigned wcnt = wave_sum_u(lcnt);
   if (lane == 0) { sl[w] = l; sc[w] = wcnt - dpos; }
   __syncthreads();
   if (tid == 0) {
@@ -1080,337 +742,8 @@ __global__ void __launch_bounds__(NTH2) zzt_dense_bf16_v4(ZztArgs a) {
   }
 }
 
-// ---------------------------------------------------------------- bf16 MFMA, v8 (d <= 64)
-// v8: ONE wave per SIMD (256-thread workgroup, up to 512 registers per lane) that
-// interleaves its own epilogue VALU with its own MFMAs (MI355X_MICROARCH.md constants,
-// 'single-issue instructions HIDDEN per v_mfma_f32_32x32x16_bf16 gap': a gap of 32
-// cycles hides ~24 cycles of issue).  v4's four waves per SIMD ran the matrix phase
-// and the VALU phase of a tile back to back (2,432 VALU + 1,024 MFMA cycles per tile
-// and SIMD = the measured 3,456): here the per-block software pipeline puts every
-// MFMA next to independent VALU of the same wave.
-//
-// Work split: wave w owns rows i0 + 32 w .. +31 of the workgroup's 128 rows and ALL
-// four 32-column blocks of every 128-column tile (no cross-wave combine of partial
-// dJ).  Logit block k = 4 t + cb; per block, in one straight-line region:
-//   fwd(k+1)  Y'[j][i] = -x_ij        4 MFMAs, A = z_j rows (LDS), B = -z_i (REGISTERS)
-//   epi(k)    sigma, log2 of quad products, sign count (v4's EPI 0, same arithmetic)
-//   bwd(k-1)  dJ'[i][c] += S'[i][j] z_j[c]   4 MFMAs, A = S' (registers), B = z^T (LDS)
-// so each 32x32 block's epilogue runs beside 8 MFMAs it does not depend on.
-// LDS: v4's two images per tile, triple-buffered; the tile barrier sits after block
-// cb0 of tile t (the last reader of tile t-1, bwd(t-1, cb3), is done), then tile t+2
-// is stored from registers into t-1's buffer and tile t+3 is loaded into registers.
-// Results: v4's per-logit arithmetic in v4's order per (i, j); the dJ sums run over
-// j in the same k order per 32-column block, blocks in ascending order (v4 summed the
-// four column blocks' partials at the end: dJ differs from v4 by fp32 reassociation).
-// SCHED 1 shapes each block with sched_group_barrier (MFMA, then VALU fillers).
-template <int DP, int SCHED>
-__global__ void __launch_bounds__(256) zzt_dense_bf16_v8(ZztArgs a) {
-  constexpr int NT = 256, NW = 4;
-  constexpr int KS = DP / 16;          // forward k-steps
-  constexpr int CB = DP / 32;          // backward 32-column output blocks
-  constexpr int JST = DP + 8;          // J / row image stride (elements)
-  constexpr int TST = TJ2 + 8;         // z^T image stride
-  constexpr int JS = TJ2 * JST;
-  constexpr int TS = DP * TST;
-  constexpr int BUF = JS + TS;
-  constexpr int CPR = DP / 8, TCPR = TJ2 / 8;
-  constexpr int JCH = TJ2 * CPR, TCH = DP * TCPR;
-  constexpr int JPT = (JCH + NT - 1) / NT, TPT = (TCH + NT - 1) / NT;
-  __shared__ __attribute__((aligned(16))) __bf16 lds[3 * BUF];
-  __shared__ __attribute__((aligned(16))) __bf16 zown[ROWS * JST];    // z_i rows (z^T values)
-  __shared__ float colsum[DP];
-  __shared__ float csred[NT / DP][DP];
-  __shared__ float dsg[NW][32];
-  __shared__ double sl[NW];
-  __shared__ unsigned sc[NW];
-
-  const int wgs = a.ngraphs * zrb(a);
-  const int sp = blockIdx.x / wgs, bx = blockIdx.x - sp * wgs;
-  const int nsplit = gridDim.x / wgs;
-  const int g = bx % a.ngraphs, rb = a.rb0 + bx / a.ngraphs;
-  const __bf16* Jg = reinterpret_cast<const __bf16*>(a.jrow) + (long long)g * a.npad * DP;
-  const __bf16* JTg = reinterpret_cast<const __bf16*>(a.jt) + (long long)g * DP * a.npad;
-  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, r = lane & 31, h = lane >> 5;
-  const int i0 = __builtin_amdgcn_readfirstlane(rb * ROWS + 32 * w);
-  const int i_me = i0 + r;
-  const int ntot = a.npad / TJ2;
-  const int t0 = sp * ntot / nsplit, t1 = (sp + 1) * ntot / nsplit;
-
-  uint4 rj[JPT], rt[TPT];
-  auto gload = [&](int t) {
-#pragma unroll
-    for (int p = 0; p < JPT; ++p) {
-      const int idx = tid + p * NT;
-      if (JCH % NT == 0 || idx < JCH) {
-        const int row = idx / CPR, ch = idx - row * CPR;
-        rj[p] = *reinterpret_cast<const uint4*>(Jg + (long long)(t * TJ2 + row) * DP + ch * 8);
-      }
-    }
-#pragma unroll
-    for (int p = 0; p < TPT; ++p) {
-      const int idx = tid + p * NT;
-      if (TCH % NT == 0 || idx < TCH) {
-        const int c = idx / TCPR, ch = idx - c * TCPR;
-        rt[p] = *reinterpret_cast<const uint4*>(JTg + (long long)c * a.npad + t * TJ2 + ch * 8);
-      }
-    }
-  };
-  // J rows: [row][k].  z^T: row c holds, per 32-j block jb and k-step s, chunk
-  // 4 jb + 2 s + h = {j = 32 jb + 16 s + 4 h + 0..3, + 8 + 0..3} (the k order of
-  // the packed S' operand) -- v4's layout
-  auto sstore = [&](__bf16* L) {
-#pragma unroll
-    for (int p = 0; p < JPT; ++p) {
-      const int idx = tid + p * NT;
-      if (JCH % NT == 0 || idx < JCH) {
-        const int row = idx / CPR, ch = idx - row * CPR;
-        *reinterpret_cast<uint4*>(&L[row * JST + ch * 8]) = rj[p];
-      }
-    }
-#pragma unroll
-    for (int p = 0; p < TPT; ++p) {
-      const int idx = tid + p * NT;
-      if (TCH % NT == 0 || idx < TCH) {
-        const int c = idx / TCPR, ch = idx - c * TCPR;
-        const int jb = ch >> 2, m = ch & 3, s = m >> 1, a8 = (m & 1) * 4;
-        __bf16* row = &L[JS + c * TST + (4 * jb + 2 * s) * 8 + a8];
-        *reinterpret_cast<uint2*>(row) = make_uint2(rt[p].x, rt[p].y);
-        *reinterpret_cast<uint2*>(row + 8) = make_uint2(rt[p].z, rt[p].w);
-      }
-    }
-  };
-
-  // ---- prologue: tiles t0, t0+1 staged, t0+2 in registers; the wave's -z_i rows in
-  // registers (the forward B operand); z_i^T columns -> zown; graph column sums
-  gload(t0);
-  bf16x8 zi[KS];   // -z_i (scaled): row i0 + r, k = 16 s + 8 h .. + 7
-#pragma unroll
-  for (int s = 0; s < KS; ++s) {
-    const uint4 u = *reinterpret_cast<const uint4*>(Jg + (long long)(i0 + r) * DP + 16 * s + 8 * h);
-    const uint4 v = make_uint4(u.x ^ 0x80008000u, u.y ^ 0x80008000u, u.z ^ 0x80008000u, u.w ^ 0x80008000u);
-    zi[s] = __builtin_bit_cast(bf16x8, v);
-  }
-  for (int idx = tid; idx < DP * (ROWS / 8); idx += NT) {   // z^T[c][rb*128 + 8u ..] -> zown[i][c]
-    const int c = idx / (ROWS / 8), u = idx - c * (ROWS / 8);
-    const bf16x8 v = *reinterpret_cast<const bf16x8*>(JTg + (long long)c * a.npad + rb * ROWS + 8 * u);
-#pragma unroll
-    for (int e = 0; e < 8; ++e) zown[(8 * u + e) * JST + c] = v[e];
-  }
-  {   // graph column sums S_k = sum_j zs_jk (fixed order over the 64-row partials)
-    const int nrb = a.npad / 64;
-    const int k = tid % DP, grp = tid / DP;
-    float s = 0.f;
-    for (int p = grp; p < nrb; p += NT / DP) s += a.colpart[((long long)g * nrb + p) * DP + k];
-    csred[grp][k] = s;
-  }
-  sstore(lds);
-  gload(min(t0 + 1, t1 - 1));
-  sstore(lds + BUF);
-  gload(min(t0 + 2, t1 - 1));
-  // buffer 2's z^T image is read (times S' = 0) by the first block's bwd(t0 - 1): finite
-  for (int idx = tid; idx < TS / 8; idx += NT)
-    *reinterpret_cast<uint4*>(&lds[2 * BUF + JS + 8 * idx]) = make_uint4(0u, 0u, 0u, 0u);
-  __syncthreads();
-  if (tid < DP) {
-    float s = 0.f;
-    for (int p = 0; p < NT / DP; ++p) s += csred[p][tid];
-    colsum[tid] = s;
-  }
-
-  f32x16 acc[CB];
-#pragma unroll
-  for (int q = 0; q < CB; ++q)
-#pragma unroll
-    for (int v = 0; v < 16; ++v) acc[q][v] = 0.f;
-  // operands are read from LDS one block before the MFMAs that use them (one wave per
-  // SIMD: nothing else hides the LDS latency)
-  struct FOp { bf16x8 v[KS]; };
-  struct BOp { bf16x8 v[2][CB]; };
-  auto fload = [&](const __bf16* L, int cb) {
-    FOp o;
-    const int j = 32 * cb + r;
-#pragma unroll
-    for (int s = 0; s < KS; ++s) o.v[s] = *reinterpret_cast<const bf16x8*>(&L[j * JST + (2 * s + h) * 8]);
-    return o;
-  };
-  auto bload = [&](const __bf16* L, int cb) {
-    BOp o;
-#pragma unroll
-    for (int s = 0; s < 2; ++s)
-#pragma unroll
-      for (int q = 0; q < CB; ++q)
-        o.v[s][q] = *reinterpret_cast<const bf16x8*>(&L[JS + (32 * q + r) * TST + (4 * cb + 2 * s + h) * 8]);
-    return o;
-  };
-  auto fwd = [&](const FOp& o) {
-    f32x16 X;
-#pragma unroll
-    for (int v = 0; v < 16; ++v) X[v] = 0.f;
-#pragma unroll
-    for (int s = 0; s < KS; ++s) X = __builtin_amdgcn_mfma_f32_32x32x16_bf16(o.v[s], zi[s], X, 0, 0, 0);
-    return X;
-  };
-  auto bwd = [&](const BOp& o, const bf16x8 (&sA)[2]) {
-#pragma unroll
-    for (int s = 0; s < 2; ++s)
-#pragma unroll
-      for (int q = 0; q < CB; ++q)
-        acc[q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(sA[s], o.v[s][q], acc[q], 0, 0, 0);
-  };
-  float lacc = 0.f;
-  double ltot = 0.0;
-  unsigned lcnt = 0;
-  // v4 EPI 0 on one 32x32 block (y = -x): sigma, one log2 per quad, sign count; the
-  // quad products' overflow fallback is a wave-uniform branch after the block's MFMAs
-  auto epi = [&](const f32x16& Y, bf16x8 (&sA)[2], float (&q)[16]) {
-    float lt = 0.f;
-#pragma unroll
-    for (int v = 0; v < 16; ++v) {
-      const float e = __builtin_amdgcn_exp2f(Y[v]);
-      q[v] = e + kZ4Q;
-      sA[v >> 3][v & 7] = (__bf16)__builtin_amdgcn_rcpf(q[v]);
-    }
-#pragma unroll
-    for (int g4 = 0; g4 < 4; ++g4) {
-      const unsigned t01 = __builtin_amdgcn_perm(__float_as_uint(Y[4 * g4 + 1]),
-                                                 __float_as_uint(Y[4 * g4]), 0x0C0C0703u);
-      const unsigned t23 = __builtin_amdgcn_perm(__float_as_uint(Y[4 * g4 + 3]),
-                                                 __float_as_uint(Y[4 * g4 + 2]), 0x07030C0Cu);
-      lcnt += (unsigned)__builtin_popcount((t01 | t23) & 0x80808080u);
-    }
-#pragma unroll
-    for (int p = 0; p < 4; ++p)
-      lt += __builtin_amdgcn_logf((q[4 * p] * q[4 * p + 1]) * (q[4 * p + 2] * q[4 * p + 3]));
-    return lt;
-  };
-  auto epi_fix = [&](const f32x16& Y, const float (&q)[16], float lt) {
-    if (__builtin_expect(__builtin_amdgcn_ballot_w64(!__builtin_isfinite(lt)) != 0, 0)) {
-      lt = 0.f;   // a quad product overflowed: the block one logit at a time (v4)
-#pragma unroll
-      for (int v = 0; v < 16; ++v) lt += Y[v] > 24.f ? Y[v] : __builtin_amdgcn_logf(q[v]);
-    }
-    lacc += lt;
-  };
-  auto shape = [&]() {
-    if constexpr (SCHED == 1) {
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // one MFMA
-        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);   // one DS read
-        __builtin_amdgcn_sched_group_barrier(0x002, 8, 0);   // VALU fillers
-      }
-    }
-  };
-
-  // pipeline state: Y = fwd(k), fA = operands of fwd(k + 1), bB = operands of
-  // bwd(k - 1), sPrev = S'(k - 1)
-  f32x16 Y = fwd(fload(lds, 0));
-  FOp fA = fload(lds, 1);
-  BOp bB = bload(lds + 2 * BUF, 3);   // zeroed image: bwd(t0 - 1) adds S' = 0 times 0
-  bf16x8 sPrev[2];
-#pragma unroll
-  for (int s = 0; s < 2; ++s)
-#pragma unroll
-    for (int e = 0; e < 8; ++e) sPrev[s][e] = (__bf16)0.f;
-
-  // one block k = (tile of L, cb): fwd(k + 1) | loads for k + 2 and bwd(k) | epi(k) | bwd(k - 1)
-  auto block = [&](const __bf16* Lf2, int cbf2, const __bf16* Lk, int cb) {
-    float q[16];
-    bf16x8 sA[2];
-    const f32x16 Yn = fwd(fA);
-    const FOp fN = fload(Lf2, cbf2);
-    const BOp bN = bload(Lk, cb);
-    const float lt = epi(Y, sA, q);
-    bwd(bB, sPrev);
-    shape();
-    epi_fix(Y, q, lt);
-    Y = Yn;
-    fA = fN;
-    bB = bN;
-    sPrev[0] = sA[0];
-    sPrev[1] = sA[1];
-  };
-  // one tile; buffer indices compile-time (tile t in buffer CUR = (t - t0) % 3)
-  auto tile = [&](int t, auto cc) {
-    constexpr int CUR = decltype(cc)::value, NXT = (CUR + 1) % 3, PRV = (CUR + 2) % 3;
-    const __bf16* const Lc = lds + CUR * BUF;
-    const __bf16* const Ln = lds + NXT * BUF;
-    block(Lc, 2, Lc, 0);
-    __syncthreads();                   // every wave is past bwd(t - 1, 3): PRV is free
-    sstore(lds + PRV * BUF);           // tile t + 2
-    gload(min(t + 3, t1 - 1));
-    block(Lc, 3, Lc, 1);
-    block(Ln, 0, Lc, 2);               // tile t + 1: visible since the barrier above
-    block(Ln, 1, Lc, 3);
-  };
-  for (int t = t0; t < t1; t += 3) {
-    tile(t, std::integral_constant<int, 0>{});
-    if (t + 1 < t1) tile(t + 1, std::integral_constant<int, 1>{});
-    if (t + 2 < t1) tile(t + 2, std::integral_constant<int, 2>{});
-    ltot += (double)lacc;   // keep the fp32 partial sums short
-    lacc = 0.f;
-  }
-  bwd(bB, sPrev);
-
-  // ---- per-row corrections (row i_me; lanes r and r + 32 hold its two k halves)
-  float xd = 0.f, xs = 0.f;
-#pragma unroll
-  for (int s = 0; s < KS; ++s) {
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const float bb = (float)zi[s][e];   // (-)z_i: the products below do not see the sign
-      xd += bb * bb;
-      xs += bb * colsum[16 * s + 8 * h + e];
-    }
-  }
-  xd += __shfl_xor(xd, 32, 64);
-  xs += __shfl_xor(xs, 32, 64);
-  xs = -xs;
-  const bool row_valid = i_me < a.n;
-  const bool corr = sp == 0;
-  const bool own = h == 0 && row_valid && corr;
-  const float exd = __builtin_amdgcn_exp2f(-fabsf(xd));
-  if (own) {   // + sum_j x_ij (softplus2(x) = x + log2(q)) - softplus2(x_ii)
-    ltot += (double)xs;
-    ltot -= (double)(fmaxf(xd, 0.f) + __builtin_amdgcn_logf(1.f + exd));
-  }
-  const unsigned dpos = (unsigned)__popcll(__ballot(own && xd > 0.f));
-  if (h == 0) {   // s'_ii as the backward MFMA consumed it (bf16), 0 outside split 0
-    const float sg = __builtin_amdgcn_rcpf(__builtin_amdgcn_exp2f(-xd) + kZ4Q);
-    dsg[w][r] = corr ? (float)(__bf16)sg : 0.f;
-  }
-  __syncthreads();
-  {
-    float* dst = (sp == 0 ? a.dJd : a.dJd_extra + (long long)(sp - 1) * a.ngraphs * a.n * a.d) +
-                 (long long)g * a.n * a.d;
-#pragma unroll
-    for (int q = 0; q < CB; ++q) {
-      const int c = 32 * q + r;
-#pragma unroll
-      for (int v = 0; v < 16; ++v) {
-        const int il = (v & 3) + 8 * (v >> 2) + 4 * h;   // D row within the wave's 32 rows
-        const int i = i0 + il;
-        if (i < a.n && c < a.d)
-          dst[(long long)i * a.d + c] = acc[q][v] - dsg[w][il] * (float)zown[(32 * w + il) * JST + c];
-      }
-    }
-  }
-  const double l = wave_sum_d(ltot);
-  const unsigned wcnt = wave_sum_u(lcnt);
-  if (lane == 0) { sl[w] = l; sc[w] = wcnt - dpos; }
-  __syncthreads();
-  if (tid == 0) {
-    double tl = 0.0, tc = 0.0;
-    for (int k = 0; k < NW; ++k) { tl += sl[k]; tc += (double)sc[k]; }
-    if (corr)   // padded pairs of this row block: x = 0 exactly, softplus2(0) = 1 each
-      tl -= zzt_padded_pairs(a, rb);
-    a.part[2 * blockIdx.x] = tl * (double)kLn2;
-    a.part[2 * blockIdx.x + 1] = tc;
-  }
-}
-
 // ---------------------------------------------------------------- bf16 MFMA, v7 (d = 128)
-// v4's work split and signed (EPI 0) epilogue at d = 128, where v4's two LDS images
+// v4's work split and signed epilogue at d = 128, where v4's two LDS images
 // per tile (z rows and z^T, 2 x 35 KB) cannot be triple-buffered beside the
 // workgroup's own rows.  One image per tile serves both products:
 //   * layout: 8-row x 32-column subtiles of 512 B, 16-byte chunks XOR-swizzled
@@ -1451,7 +784,7 @@ __device__ __forceinline__ bf16x8 ztr_pair(const char* p0, const char* p1) {
 }
 constexpr float kInvSqrtLog2e = 0.8325546111576977f;   // 1 / sqrt(log2 e)
 
-template <bool MEAS, bool STAG>
+template <bool MEAS>
 __global__ void __launch_bounds__(NTH2) zzt_dense_bf16_v7(ZztArgs a) {
   constexpr int DP = 128, NT = NTH2, NW = NT / 64;
   constexpr int KS = DP / 16;          // forward k-steps
@@ -1500,9 +833,8 @@ __global__ void __launch_bounds__(NTH2) zzt_dense_bf16_v7(ZztArgs a) {
              __builtin_amdgcn_readfirstlane(lds0 + b * IMG + 1024 * (w + 16 * k)));
   };
 
-  // ---- prologue: tiles t0, t0+1 in flight (STAG: t0 only); -z_i rows; column sums
+  // ---- prologue: tile t0 in flight; -z_i rows; column sums
   dma(t0, 0);
-  if (!STAG) dma(min(t0 + 1, t1 - 1), 1);
   for (int idx = tid; idx < ROWS * (DP / 8); idx += NT) {
     const int row = idx >> 4, ch = idx & 15;
     const uint4 u = *reinterpret_cast<const uint4*>(Jg + (long long)(rb * ROWS + row) * DP + ch * 8);
@@ -1556,7 +888,7 @@ __global__ void __launch_bounds__(NTH2) zzt_dense_bf16_v7(ZztArgs a) {
   float lacc = 0.f;
   double ltot = 0.0;
   unsigned lcnt = 0;
-  auto epi = [&](const f32x16& Y, bf16x8 (&sA)[2]) {   // v4 EPI 0, y = -x
+  auto epi = [&](const f32x16& Y, bf16x8 (&sA)[2]) {   // v4's epilogue, y = -x
     if (MEAS && (skip & 1)) {
 #pragma unroll
       for (int v = 0; v < 16; ++v) sA[v >> 3][v & 7] = (__bf16)Y[v];
@@ -1601,7 +933,7 @@ __global__ void __launch_bounds__(NTH2) zzt_dense_bf16_v7(ZztArgs a) {
 
   // tile t in ring slot CUR: DMA of tile t+2 into the slot tile t-1 left, forward,
   // epilogue, backward; wait for tile t+1 (its 2 DMAs per wave; t+2's may fly), barrier.
-  // STAG: the odd column-block waves (two of the four waves of every SIMD: waves w and
+  // Stagger: the odd column-block waves (two of the four waves of every SIMD: waves w and
   // w + 4k share one) run one tile late -- tile t-1's epilogue and backward, then tile
   // t's forward -- so after every barrier half of each SIMD's waves start on the VALU
   // while the other half starts on the matrix pipe (the phases otherwise serialise:
@@ -1617,30 +949,21 @@ __global__ void __launch_bounds__(NTH2) zzt_dense_bf16_v7(ZztArgs a) {
     for (int v = 0; v < 16; ++v) Yp[v] = 0.f;
     auto tile = [&](int t, auto cc) {
       constexpr int CUR = decltype(cc)::value, NN = (CUR + 2) % 3;
-      if constexpr (STAG) {
-        if (t + 1 < t1) dma(t + 1, (CUR + 1) % 3);
-        if constexpr (LATE) {
-          if (t > t0) {
-            bf16x8 sA[2];
-            epi(Yp, sA);
-            bwd(NN, sA);   // tile t-1's slot
-          }
-          Yp = fwd(CUR);
-        } else {
-          const f32x16 Y = fwd(CUR);
+      if (t + 1 < t1) dma(t + 1, (CUR + 1) % 3);
+      if constexpr (LATE) {
+        if (t > t0) {
           bf16x8 sA[2];
-          epi(Y, sA);
-          bwd(CUR, sA);
+          epi(Yp, sA);
+          bwd(NN, sA);   // tile t-1's slot
         }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // tile t+1 landed
+        Yp = fwd(CUR);
       } else {
-        dma(min(t + 2, t1 - 1), NN);
         const f32x16 Y = fwd(CUR);
         bf16x8 sA[2];
         epi(Y, sA);
         bwd(CUR, sA);
-        asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
       }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // tile t+1 landed
       __syncthreads();
     };
     for (int t = t0; t < t1; t += 3) {
@@ -1660,7 +983,7 @@ __global__ void __launch_bounds__(NTH2) zzt_dense_bf16_v7(ZztArgs a) {
   };
   // static priority 1 for the late waves (MI355X guide, two waves per SIMD item 4):
   // 324 vs 330 us at 2 graphs; priority 1 for the early waves instead 331
-  if (STAG && (cb & 1)) {
+  if (cb & 1) {
     __builtin_amdgcn_s_setprio(1);
     run(std::true_type{});
     __builtin_amdgcn_s_setprio(0);
@@ -1866,39 +1189,18 @@ int launch_zzt_dense(const ZztArgs& a, int dtype, hipStream_t s, bool defer_spli
     if (dp == 32) hipLaunchKernelGGL((zzt_dense_bf16<32>), grid, dim3(NTH), 0, s, a);
     else if (dp == 64) hipLaunchKernelGGL((zzt_dense_bf16<64>), grid, dim3(NTH), 0, s, a);
     else hipLaunchKernelGGL((zzt_dense_bf16<128>), grid, dim3(NTH), 0, s, a);
-  } else if (dtype == SND_BF16 && dp <= 64 && (a.variant == 20 || a.variant == 21)) {   // v8 A/B
-    if (dp == 32) {
-      if (a.variant == 20) hipLaunchKernelGGL((zzt_dense_bf16_v8<32, 0>), grid, dim3(256), 0, s, a);
-      else hipLaunchKernelGGL((zzt_dense_bf16_v8<32, 1>), grid, dim3(256), 0, s, a);
+  } else if (dtype == SND_BF16 && dp <= 64) {         // v4 (default, d <= 64)
+    // variant >= 256: the measurement build (phase skips / stamps, variant >> 8)
+    if (a.variant >= 256) {
+      if (dp == 32) hipLaunchKernelGGL((zzt_dense_bf16_v4<32, true>), grid, dim3(NTH2), 0, s, a);
+      else hipLaunchKernelGGL((zzt_dense_bf16_v4<64, true>), grid, dim3(NTH2), 0, s, a);
     } else {
-      if (a.variant == 20) hipLaunchKernelGGL((zzt_dense_bf16_v8<64, 0>), grid, dim3(256), 0, s, a);
-      else hipLaunchKernelGGL((zzt_dense_bf16_v8<64, 1>), grid, dim3(256), 0, s, a);
+      if (dp == 32) hipLaunchKernelGGL((zzt_dense_bf16_v4<32, false>), grid, dim3(NTH2), 0, s, a);
+      else hipLaunchKernelGGL((zzt_dense_bf16_v4<64, false>), grid, dim3(NTH2), 0, s, a);
     }
-  } else if (dtype == SND_BF16 && dp <= 64 && (a.variant & 255) != 3) {   // v4 (default, d <= 64)
-    // default: signed epilogue, plain tile order; A/B: variant 10 + 3 EPI + MODE;
-    // variant >= 256: the measurement build of the default (phase skips / stamps)
-    const int v = a.variant & 255;
-    const int cfg = (a.variant >= 256 || v < 10 || v > 15) ? 0 : v - 10;
-#define SND_V4(DPV)                                                                              \
-  if (a.variant >= 256) hipLaunchKernelGGL((zzt_dense_bf16_v4<DPV, 0, 0, true>), grid, dim3(NTH2), 0, s, a); \
-  else if (cfg == 0) hipLaunchKernelGGL((zzt_dense_bf16_v4<DPV, 0, 0, false>), grid, dim3(NTH2), 0, s, a); \
-  else if (cfg == 1) hipLaunchKernelGGL((zzt_dense_bf16_v4<DPV, 1, 0, false>), grid, dim3(NTH2), 0, s, a); \
-  else if (cfg == 2) hipLaunchKernelGGL((zzt_dense_bf16_v4<DPV, 2, 0, false>), grid, dim3(NTH2), 0, s, a); \
-  else if (cfg == 3) hipLaunchKernelGGL((zzt_dense_bf16_v4<DPV, 0, 1, false>), grid, dim3(NTH2), 0, s, a); \
-  else if (cfg == 4) hipLaunchKernelGGL((zzt_dense_bf16_v4<DPV, 1, 1, false>), grid, dim3(NTH2), 0, s, a); \
-  else hipLaunchKernelGGL((zzt_dense_bf16_v4<DPV, 2, 1, false>), grid, dim3(NTH2), 0, s, a);
-    if (dp == 32) { SND_V4(32) } else { SND_V4(64) }
-#undef SND_V4
-  } else if (dtype == SND_BF16 && dp == 128 && (a.variant & 255) != 3) {   // v7 (default, d = 128)
-    const bool stag = (a.variant & 255) != 17;   // 17: v7 without the wave stagger (A/B)
-    if (a.variant >= 256 && stag) hipLaunchKernelGGL((zzt_dense_bf16_v7<true, true>), grid, dim3(NTH2), 0, s, a);
-    else if (a.variant >= 256) hipLaunchKernelGGL((zzt_dense_bf16_v7<true, false>), grid, dim3(NTH2), 0, s, a);
-    else if (stag) hipLaunchKernelGGL((zzt_dense_bf16_v7<false, true>), grid, dim3(NTH2), 0, s, a);
-    else hipLaunchKernelGGL((zzt_dense_bf16_v7<false, false>), grid, dim3(NTH2), 0, s, a);
-  } else if (dtype == SND_BF16) {                     // v3: |x| formulation, 16x16x32 (A/B: variant 3)
-    if (dp == 32) hipLaunchKernelGGL((zzt_dense_bf16_v3<32>), grid, dim3(NTH2), 0, s, a);
-    else if (dp == 64) hipLaunchKernelGGL((zzt_dense_bf16_v3<64>), grid, dim3(NTH2), 0, s, a);
-    else hipLaunchKernelGGL((zzt_dense_bf16_v3<128>), grid, dim3(NTH2), 0, s, a);
+  } else if (dtype == SND_BF16) {                     // v7 (d = 128)
+    if (a.variant >= 256) hipLaunchKernelGGL((zzt_dense_bf16_v7<true>), grid, dim3(NTH2), 0, s, a);
+    else hipLaunchKernelGGL((zzt_dense_bf16_v7<false>), grid, dim3(NTH2), 0, s, a);
   } else {
     const size_t shm = 2 * 2 * (size_t)TJ * dp * sizeof(float);
     if (dp == 32) hipLaunchKernelGGL((zzt_dense_f32<32>), grid, dim3(NTH), shm, s, a);

@@ -10,8 +10,9 @@ struct ZztArgs {
   float* dJd;            // [B*n][d]  sum_{j != i} sigmoid(L_ij) z_j
   double* part;          // [blocks][2] = {sum softplus over valid pairs, #{L > 0}}
   const float* colpart;  // [B][npad/64][DP] column sums of jrow (bf16 values), per 64 rows
-  int variant;           // bf16 kernel: 0 = default (v4 for d <= 64, else v3), 1 = v1,
-                         // 3 = v3, 10..15 = v4 (epilogue, mode) A/B; >= 256 v4 measurement build
+  int variant;           // bf16 kernel: 0 = default (v4 for d <= 64, v7 for d = 128), 1 = v1
+                         // (the bench's previous variant); >= 256 the measurement build of the
+                         // default (phase-skip / stamp bits variant >> 8, tools/zzt_stamps.py)
   float* dJd_extra;      // v3 column splits 1.. (zzt_tsplit > 1): [(tsplit-1)][B*n][d] scratch
   int rb0 = 0;           // first 128-row block of the launch (row-sharded zz^T, snd_zzt_ce_rows)
   int nrb = 0;           // row blocks of the launch; 0 = every row block
