@@ -162,7 +162,7 @@ struct snd_plan {
 };
 
 extern "C" const char* snd_last_error(void) { return g_err; }
-extern "C" int snd_abi_version(void) { return 14; }
+extern "C" int snd_abi_version(void) { return 15; }
 
 extern "C" int snd_plan_create(const snd_config_t* cfg, int n_graphs, snd_plan_t** out) {
   SND_CHECK_ARG(cfg && out && n_graphs > 0, "snd_plan_create: bad args");
