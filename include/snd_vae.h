@@ -530,6 +530,14 @@ int snd_plan_launch(const snd_plan_t* plan, const snd_batch_t* batch,
  * terms and weight gradients on a side stream.  0 (default) = normal. */
 int snd_debug_set(int flags);
 
+/* Plan options (round 4).  "conc_decoder": 1 = run the fused decoder on a side stream
+ * beside the zz^T kernel (whose column splits then leave the decoder's tiles their CUs);
+ * for small batches (C3: one graph per rank), where neither kernel fills the chip.  The
+ * side stream is created by the first non-capturing step.  Returns 1 when the option
+ * is in effect for this plan, 0 when the plan cannot use it, SND_ERR_ARG for an
+ * unknown option. */
+int snd_plan_set_option(snd_plan_t* plan, const char* name, int value);
+
 #ifdef __cplusplus
 }
 #endif

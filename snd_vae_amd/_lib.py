@@ -71,6 +71,7 @@ class LatentReg(C.Structure):
 _SIGS = {
     "snd_last_error": (C.c_char_p, []),
     "snd_abi_version": (c_int, []),
+    "snd_plan_set_option": (c_int, [vp, C.c_char_p, c_int]),
     "snd_dense_to_csr_workspace": (c_size, [c_int, c_int]),
     "snd_dense_to_csr": (c_int, [vp, c_int, c_int, vp, vp, c_ll, vp, vp, c_size, vp]),
     "snd_csr_spmm": (c_int, [vp, vp, c_int, vp, c_int, c_int, vp, c_int, c_int, vp, vp, vp,

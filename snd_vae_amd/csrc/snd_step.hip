@@ -132,6 +132,13 @@ struct snd_plan {
   mutable std::vector<WgArgs> last_wq;   // the last step's weight-gradient launch (snd_plan_launch)
   // side stream for the independent branches (edge terms, weight gradients); created
   // by the first non-capturing fast-path step, joined back before the reduction
+  // concurrent decoder (snd_plan_set_option "conc_decoder"): with B small the zz^T
+  // kernel's column splits and the decoder's 32-64 tiles do not both fill the chip, so the
+  // fused decoder runs on the side stream beside zz^T, which leaves it dec_tiles CUs
+  // (zzt_ts: the column splits every zz^T consumer uses -- launch, split sum, finalize)
+  int conc_dec = 0;
+  int zzt_ts = 1;
+  bool conc_dec_on() const { return conc_dec > 0 && fast && dec_fused && !tref; }
   static constexpr int kEvents = 16;
   mutable hipStream_t side = nullptr;
   mutable hipEvent_t ev[kEvents] = {};
@@ -489,6 +496,7 @@ extern "C" int snd_plan_create(const snd_config_t* cfg, int n_graphs, snd_plan_t
   // GraphConvolution 0, XW1 and the packed weight images in one launch (debug bit 1048576:
   // pack + gcn0 + a row-engine launch)
   p->front_fused = p->fast_enc && !(dbg & 1048576) && front_supported(c.f_in, c.h0, c.h1, p->pw1f.kp, p->pw1f.np);
+  p->zzt_ts = zzt_tsplit(p->B, p->N, c.dtype);
   *out = p;
   return 0;
 }
@@ -505,6 +513,26 @@ extern "C" int snd_plan_param_block(const snd_plan_t* p, int idx, const char** n
   return 0;
 }
 extern "C" size_t snd_plan_workspace_bytes(const snd_plan_t* p) { return p ? (size_t)p->ws : 0; }
+
+// zz^T column splits with the concurrent decoder on: zz^T keeps the CUs the decoder's
+// tiles do not take (one 1024-thread workgroup per CU for either kernel)
+static int conc_zzt_ts(const snd_plan& p) {
+  const int full = zzt_tsplit(p.B, p.N, p.c.dtype);
+  if (!p.conc_dec_on()) return full;
+  const int wgs = p.B * (zzt_npad(p.N) / 128);
+  return std::max(1, std::min(full, (256 - p.dtiles) / wgs));
+}
+
+extern "C" int snd_plan_set_option(snd_plan_t* p, const char* name, int value) {
+  SND_CHECK_ARG(p && name, "snd_plan_set_option: bad args");
+  if (!strcmp(name, "conc_decoder")) {
+    p->conc_dec = value;
+    p->zzt_ts = conc_zzt_ts(*p);
+    return p->conc_dec_on() ? 1 : 0;
+  }
+  set_error("snd_plan_set_option: unknown option '%s'", name);
+  return SND_ERR_ARG;
+}
 
 extern "C" int snd_plan_fuse_adam(snd_plan_t* p, float* m, float* v, float lr, float beta1,
                                   float beta2, float eps) {
@@ -593,6 +621,25 @@ int join(const Ctx& x) {
   return 0;
 }
 hipStream_t side(const Ctx& x) { return x.side ? x.side : x.s; }
+// fork_to / join_from: the same on an explicit stream (the concurrent decoder's)
+int fork_to(const Ctx& x, hipStream_t o) {
+  SND_CHECK_ARG(x.nev && *x.nev < snd_plan::kEvents, "train step: out of fork events");
+  hipEvent_t e = x.p->ev[(*x.nev)++];
+  if (hipEventRecord(e, x.s) != hipSuccess || hipStreamWaitEvent(o, e, 0) != hipSuccess) {
+    set_error("train step: fork failed");
+    return SND_ERR_HIP;
+  }
+  return 0;
+}
+int join_from(const Ctx& x, hipStream_t o) {
+  SND_CHECK_ARG(x.nev && *x.nev < snd_plan::kEvents, "train step: out of join events");
+  hipEvent_t e = x.p->ev[(*x.nev)++];
+  if (hipEventRecord(e, o) != hipSuccess || hipStreamWaitEvent(x.s, e, 0) != hipSuccess) {
+    set_error("train step: join failed");
+    return SND_ERR_HIP;
+  }
+  return 0;
+}
 // a weight gradient: queued for the step's single multi-segment launch, or launched now
 int wgrad(const Ctx& x, const WgArgs& a, hipStream_t s) {
   if (x.wq) { x.wq->push_back(a); return 0; }
@@ -964,7 +1011,7 @@ int head_bwd_fused(const Ctx& x, const snd_batch_t* batch, float adj_scale, floa
     a.rowptr = batch->rowptr; a.colidx = batch->colidx; a.R = R;
     a.zb = bf("ZB"); a.L = L; a.pos_weight = c.pos_weight; a.edge_part = x.d("PEDGE");
     a.ms = x.f("MS"); a.eps = x.f("EPS"); a.dz_dec = x.f("DZDEC"); a.dJd = x.f("DJD");
-    a.dJd_extra = x.f("DJDX"); a.nextra = zzt_tsplit(p.B, p.N, c.dtype) - 1;   // deferred split sum
+    a.dJd_extra = x.f("DJDX"); a.nextra = p.zzt_ts - 1;   // deferred split sum
     a.adj_scale = adj_scale; a.kl_scale = kl_scale;
     a.dms = bf("FDMS"); a.bms_part = x.f("PHBMS");
     a.wmsb_img = reinterpret_cast<const __bf16*>(x.ws + p.pwmsb.off); a.kp1 = p.pwmsb.kp; a.np1 = p.pwmsb.np;
@@ -994,7 +1041,7 @@ int encoder_fast_bwd(const Ctx& x, const snd_batch_t* batch, float adj_scale, fl
   {
     ReparamBwdFastArgs a{x.f("MS"), 2 * L, R, L, x.f("EPS"), x.f("DZDEC"), x.f("DJD"), x.f("EJ"),
                          adj_scale, kl_scale, bf("FDMS"), 2 * L, x.f("PFBMS")};
-    a.dJd_extra = x.f("DJDX"); a.nextra = zzt_tsplit(p.B, p.N, c.dtype) - 1;   // deferred split sum
+    a.dJd_extra = x.f("DJDX"); a.nextra = p.zzt_ts - 1;   // deferred split sum
     SND_TRY(launch_reparam_bwd_fast(a, x.s));
   }
   SND_TRY(fork(x));
@@ -1472,6 +1519,13 @@ extern "C" int snd_train_step(const snd_plan_t* plan, const snd_batch_t* batch,
     init_concurrency(p, x.s);
     if (p.conc == 1) { x.side = p.side; x.nev = &nev; }
   }
+  // the concurrent decoder needs the side stream, created by a non-capturing step
+  bool cdec = false;
+  if (p.conc_dec_on() && !x.side) {
+    init_concurrency(p, x.s);
+    cdec = p.conc == 1;
+    if (cdec) x.nev = &nev;
+  }
   // single stream: every fast-path weight gradient waits for one launch before the
   // reduction (debug bit 4096: one launch per weight, as before)
   std::vector<WgArgs> wq;
@@ -1572,11 +1626,22 @@ extern "C" int snd_train_step(const snd_plan_t* plan, const snd_batch_t* batch,
     if (!p.fast) SND_TRY(launch_zzt_prep(x.f("Z"), p.B, N, dj, c.dtype, stg, x.s));
     ZztArgs za{stg.jrow, stg.jt, N, zzt_npad(N), p.B, dj, x.f("DJD"), x.d("PZZT"), stg.colpart, 0,
                x.f("DJDX")};
+    za.tsplit = p.zzt_ts;
+    // concurrent decoder: the fused decoder on the side stream beside zz^T (forked after
+    // the staging that both read, joined before the backward head that reads both)
+    if (cdec) {
+      SND_TRY(fork_to(x, p.side));
+      Ctx xd = x;
+      xd.s = p.side;
+      xd.side = nullptr;
+      SND_TRY(decoder_fast(xd, batch));
+    }
     // the column-split sum is folded into head_bwd / reparam_bwd_fast (node latent, fast encoder)
     SND_TRY(launch_zzt_dense(za, c.dtype, x.s, p.fast_enc && !p.tref));
+    if (cdec) SND_TRY(join_from(x, p.side));
   }
   if (p.fast) {
-    SND_TRY(decoder_fast(x, batch));
+    if (!cdec) SND_TRY(decoder_fast(x, batch));
   } else {
     // decoders (model_joint.py:112-145): conv1d k5 SAME -> BN -> lrelu
     SND_TRY(conv_fwd(x, x.f("Z"), dj, dj, "dec.K1", C1, "dec.b1", "dec.bn1.gamma", "dec.bn1.beta",
@@ -1783,7 +1848,7 @@ extern "C" int snd_train_step(const snd_plan_t* plan, const snd_batch_t* batch,
   }
   const int n_kl = (p.fast && !p.tref) ? reparam_prep_blocks(p.B, zzt_npad(N))
                    : (p.small_head ? small_head_fwd_blocks(L) : reparam_blocks(RH, L));
-  FinalizeArgs fa{x.d("PZZT"), zzt_dense_blocks(p.B, N, c.dtype), x.d("PEDGE"),
+  FinalizeArgs fa{x.d("PZZT"), p.B * (zzt_npad(N) / 128) * (c.dtype == SND_BF16 ? p.zzt_ts : 1), x.d("PEDGE"),
                   p.head_bwd ? head_tiles(R) : (p.fast ? edge_bf16_blocks(R) : edge_blocks(R, dj)),
                   x.d("PKL"), n_kl, x.d(p.dec_fused ? "PDSSES" : "PSSES"),
                   x.d(p.dec_fused ? "PDSSEN" : "PSSEN"), p.dec_fused ? p.dtiles : nh,

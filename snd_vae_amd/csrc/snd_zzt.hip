@@ -1181,7 +1181,11 @@ int launch_zzt_dense(const ZztArgs& a, int dtype, hipStream_t s, bool defer_spli
   SND_CHECK_ARG(a.rb0 >= 0 && a.nrb >= 0 && a.rb0 + zrb(a) <= a.npad / ROWS,
                 "zzt_dense: row blocks [%d, %d) outside the %d of the graph", a.rb0, a.rb0 + zrb(a),
                 a.npad / ROWS);
-  const int ts = (dtype == SND_BF16 && a.variant == 0) ? zzt_tsplit_blocks(a.ngraphs * zrb(a), a.n, dtype) : 1;
+  const int ts = (dtype == SND_BF16 && a.variant == 0)
+                     ? (a.tsplit > 0 ? a.tsplit : zzt_tsplit_blocks(a.ngraphs * zrb(a), a.n, dtype)) : 1;
+  SND_CHECK_ARG(ts <= std::max(1, zzt_tsplit_blocks(a.ngraphs * zrb(a), a.n, dtype)),
+                "zzt_dense: %d column splits > the %d the scratch is sized for", ts,
+                zzt_tsplit_blocks(a.ngraphs * zrb(a), a.n, dtype));
   SND_CHECK_ARG(ts == 1 || a.dJd_extra, "zzt_dense: column splits need dJd_extra");
   SND_CHECK_ARG(a.nrb == 0 || a.ngraphs == 1, "zzt_dense: a row-block range needs one graph");
   dim3 grid(a.ngraphs * zrb(a) * ts);

@@ -16,6 +16,7 @@ struct ZztArgs {
   float* dJd_extra;      // v3 column splits 1.. (zzt_tsplit > 1): [(tsplit-1)][B*n][d] scratch
   int rb0 = 0;           // first 128-row block of the launch (row-sharded zz^T, snd_zzt_ce_rows)
   int nrb = 0;           // row blocks of the launch; 0 = every row block
+  int tsplit = 0;        // column splits of the default bf16 kernel; 0 = zzt_tsplit's choice
 };
 
 // Staging buffers carved from one workspace region.

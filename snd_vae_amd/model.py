@@ -169,6 +169,14 @@ class SGCNModelVAE:
     def blocks(self) -> Dict[str, np.ndarray]:
         return self.layout.unpack(self.params[:self.param_count].double().cpu().numpy())
 
+    def set_option(self, name: str, value: int) -> bool:
+        """A plan option (snd_plan_set_option): True when it is in effect for this plan.
+        "conc_decoder": the fused decoder on a side stream beside zz^T (small batches)."""
+        r = _lib.lib().snd_plan_set_option(self.plan, name.encode(), int(value))
+        if r < 0:
+            _lib.check(r, "snd_plan_set_option")
+        return r == 1
+
     # ---- workspace views (intermediates of the last step)
     def buffer(self, name: str, dtype=torch.float32, shape=None) -> torch.Tensor:
         off, n = C.c_longlong(), C.c_longlong()

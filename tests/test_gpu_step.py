@@ -218,6 +218,46 @@ def test_graph_replay_is_deterministic():
     assert torch.equal(o1.losses, o2.losses)
 
 
+@pytest.mark.parametrize("B", [1, 2])
+def test_concurrent_decoder_replays_like_eager(B):
+    """Plan option "conc_decoder" (the fused decoder on a side stream beside zz^T, whose
+    column splits then leave the decoder's tiles their CUs): captured replays equal eager
+    steps bit for bit, and the step equals the serial step's up to the zz^T split sums'
+    fp32 re-association."""
+    from snd_vae_amd.params import init_blocks
+    cfg = tscale(4096, 64)
+    batch = synthetic_batch(cfg, B, seed=8)
+    p0 = init_blocks(cfg, 0)
+    runs = []
+    for conc in (0, 1):
+        m, o, b = make(cfg, batch, p0, "bf16")
+        assert m.set_option("conc_decoder", conc) == bool(conc)
+        for _ in range(3):
+            o.step(b)                 # eager (the first creates the side stream)
+        torch.cuda.synchronize()
+        runs.append((m, o, b))
+    (ms, os_, _), (mc, oc, bc) = runs
+    for k in ("cost", "adj_cost", "kl", "spatial_cost"):
+        assert oc.loss_dict()[k] == pytest.approx(os_.loss_dict()[k], rel=1e-4), k
+    gs, gc = os_.grads[:ms.param_count], oc.grads[:mc.param_count]
+    assert float((gs - gc).abs().max()) <= 2e-2 * float(gs.abs().max())
+    # replay == eager from the same state
+    m2, o2, b2 = make(cfg, batch, p0, "bf16")
+    m2.set_option("conc_decoder", 1)
+    o2.step(b2)
+    o2.capture(b2, warmup=1)
+    snap = [t.clone() for t in (m2.params, o2.m, o2.v, o2.step_counter)]
+    o2.replay()
+    m3, o3, b3 = make(cfg, batch, p0, "bf16")
+    m3.set_option("conc_decoder", 1)
+    o3.step(b3)                       # creates the side stream; then reset to the snapshot
+    for dst, src in zip((m3.params, o3.m, o3.v, o3.step_counter), snap):
+        dst.copy_(src)
+    o3.step(b3)
+    torch.cuda.synchronize()
+    assert torch.equal(m2.params, m3.params) and torch.equal(o2.losses, o3.losses)
+
+
 def test_training_reduces_cost():
     cfg = tscale(1024, 64)
     batch = synthetic_batch(cfg, 4, seed=3)
