@@ -26,6 +26,9 @@ for s in $STAGES; do
     prof)  step rocprof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run \
              --output-format csv -- python bench.py --steps 20 --warmup 5 --no-cpu-baseline --extra "" --batch-sweep "" --no-modes ;;
     abzzt) step ab_zzt 300 python tools/ab_zzt.py --variants ${ZZT_VARIANTS:-zzt_dense} --rounds 5 ;;
+    abspmm) step ab_spmm 300 python tools/ab_spmm_win.py --flags ${SPMM_FLAGS:-0} --rounds 6 ;;
+    some) step pytest_some 600 python -u -m pytest ${TESTS} -x -v --timeout 300 --timeout-method thread ;;
+    strong) step strong 400 python bench.py --steps 50 --warmup 10 --no-cpu-baseline --batch-sweep "" --extra "" ;;
   esac
 done
 echo "== done"
