@@ -531,8 +531,10 @@ int snd_plan_launch(const snd_plan_t* plan, const snd_batch_t* batch,
 int snd_debug_set(int flags);
 
 /* Plan options (round 4).  "conc_decoder": 1 = run the fused decoder on a side stream
- * beside the zz^T kernel (whose column splits then leave the decoder's tiles their CUs);
- * for small batches (C3: one graph per rank), where neither kernel fills the chip.  The
+ * beside the zz^T kernel (whose column splits then leave the decoder's tiles their CUs),
+ * 0 = serial, -1 = auto (the default: on for graphs of N >= 2048 with at most 64
+ * decoder tiles -- one or two N = 4096 graphs, C3's per-rank batch -- where neither
+ * kernel fills the chip).  The
  * side stream is created by the first non-capturing step.  Returns 1 when the option
  * is in effect for this plan, 0 when the plan cannot use it, SND_ERR_ARG for an
  * unknown option. */

@@ -136,9 +136,14 @@ struct snd_plan {
   // kernel's column splits and the decoder's 32-64 tiles do not both fill the chip, so the
   // fused decoder runs on the side stream beside zz^T, which leaves it dec_tiles CUs
   // (zzt_ts: the column splits every zz^T consumer uses -- launch, split sum, finalize)
-  int conc_dec = 0;
+  // (default -1 = auto: on for graphs of N >= 2048 with at most 64 decoder tiles, i.e. one
+  // or two N = 4096 graphs; C3's one-graph step 0.1704 -> 0.1626 ms,
+  // profiles/r04_bench_strong_conc.json.  Small graphs stay serial: launch-bound)
+  int conc_dec = -1;
   int zzt_ts = 1;
-  bool conc_dec_on() const { return conc_dec > 0 && fast && dec_fused && !tref; }
+  bool conc_dec_on() const {
+    return (conc_dec > 0 || (conc_dec < 0 && dtiles <= 64 && N >= 2048)) && fast && dec_fused && !tref;
+  }
   static constexpr int kEvents = 16;
   mutable hipStream_t side = nullptr;
   mutable hipEvent_t ev[kEvents] = {};
@@ -170,6 +175,15 @@ struct snd_plan {
 
 extern "C" const char* snd_last_error(void) { return g_err; }
 extern "C" int snd_abi_version(void) { return 15; }
+
+// zz^T column splits with the concurrent decoder on: zz^T keeps the CUs the decoder's
+// tiles do not take (one 1024-thread workgroup per CU for either kernel)
+static int conc_zzt_ts(const snd_plan& p) {
+  const int full = zzt_tsplit(p.B, p.N, p.c.dtype);
+  if (!p.conc_dec_on()) return full;
+  const int wgs = p.B * (zzt_npad(p.N) / 128);
+  return std::max(1, std::min(full, (256 - p.dtiles) / wgs));
+}
 
 extern "C" int snd_plan_create(const snd_config_t* cfg, int n_graphs, snd_plan_t** out) {
   SND_CHECK_ARG(cfg && out && n_graphs > 0, "snd_plan_create: bad args");
@@ -496,7 +510,7 @@ extern "C" int snd_plan_create(const snd_config_t* cfg, int n_graphs, snd_plan_t
   // GraphConvolution 0, XW1 and the packed weight images in one launch (debug bit 1048576:
   // pack + gcn0 + a row-engine launch)
   p->front_fused = p->fast_enc && !(dbg & 1048576) && front_supported(c.f_in, c.h0, c.h1, p->pw1f.kp, p->pw1f.np);
-  p->zzt_ts = zzt_tsplit(p->B, p->N, c.dtype);
+  p->zzt_ts = conc_zzt_ts(*p);
   *out = p;
   return 0;
 }
@@ -513,15 +527,6 @@ extern "C" int snd_plan_param_block(const snd_plan_t* p, int idx, const char** n
   return 0;
 }
 extern "C" size_t snd_plan_workspace_bytes(const snd_plan_t* p) { return p ? (size_t)p->ws : 0; }
-
-// zz^T column splits with the concurrent decoder on: zz^T keeps the CUs the decoder's
-// tiles do not take (one 1024-thread workgroup per CU for either kernel)
-static int conc_zzt_ts(const snd_plan& p) {
-  const int full = zzt_tsplit(p.B, p.N, p.c.dtype);
-  if (!p.conc_dec_on()) return full;
-  const int wgs = p.B * (zzt_npad(p.N) / 128);
-  return std::max(1, std::min(full, (256 - p.dtiles) / wgs));
-}
 
 extern "C" int snd_plan_set_option(snd_plan_t* p, const char* name, int value) {
   SND_CHECK_ARG(p && name, "snd_plan_set_option: bad args");

@@ -61,7 +61,8 @@ def run_step(cfg, batch, p0, eps, dtype, options=None):
     from snd_vae_amd.optimizer import OptimizerVAE
     model = SGCNModelVAE(cfg, batch.n_graphs, dtype=dtype, blocks=p0)
     for k, v in (options or {}).items():
-        assert model.set_option(k, v) == (dtype == "bf16"), (k, dtype)
+        on = model.set_option(k, v)
+        assert on == (dtype == "bf16" and v == 1), (k, v, dtype)
     opt = OptimizerVAE(model, fuse_adam=False)
     opt.step(DeviceBatch(batch), torch.from_numpy(eps).cuda())
     torch.cuda.synchronize()
@@ -108,9 +109,10 @@ def test_c2_bench_batch_vs_oracle(dtype):
 def test_c3_per_rank_shape_vs_oracle(dtype, conc):
     """C3 = 8 graphs on 8 GPUs: each rank steps ONE N=4096 graph (B=1 plan; the zz^T
     column splits fill the chip), seed 1000 + rank for rank 3.  conc: the fused decoder
-    on a side stream beside zz^T (plan option "conc_decoder", 7 column splits)."""
+    on a side stream beside zz^T (plan option "conc_decoder", 7 column splits; the
+    default at one graph) or serial (8 splits)."""
     cfg, batch, p0, eps, ref, rg = oracle_case(4096, 64, 1, 1003)
-    _, opt = run_step(cfg, batch, p0, eps, dtype, {"conc_decoder": 1} if conc else None)
+    _, opt = run_step(cfg, batch, p0, eps, dtype, {"conc_decoder": conc})
     check_step(opt, ref, rg, dtype, 4096 * 4096, name=f"c3_per_rank{'_conc' if conc else ''}")
 
 

@@ -231,7 +231,7 @@ def test_concurrent_decoder_replays_like_eager(B):
     runs = []
     for conc in (0, 1):
         m, o, b = make(cfg, batch, p0, "bf16")
-        assert m.set_option("conc_decoder", conc) == bool(conc)
+        assert m.set_option("conc_decoder", conc) == bool(conc)   # explicit, not the auto default
         for _ in range(3):
             o.step(b)                 # eager (the first creates the side stream)
         torch.cuda.synchronize()
