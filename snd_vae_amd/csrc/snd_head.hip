@@ -334,18 +334,21 @@ int head_fwd_dispatch(const HeadFwdArgs& a, hipStream_t s) {
 // ---------------------------------------------------------------- backward head
 // LDS of head_bwd_kernel (bytes): Wms^T image | Wh^T image | d[mu | s] image | dh image |
 // per-wave bias sums of d[mu | s]
+// Rows per backward-head tile (kHeadBwdRows, snd_head.hpp): 128 rows x 1024 threads, or 64
+// rows x 512 threads (two workgroups per CU, A/B build -DSND_HB_ROWS=64)
 struct BwdLay {
   int w1, w2, m, h, red, total;
-  __host__ __device__ BwdLay(int kp1, int np1, int kp2, int np2, int L) {
+  __host__ __device__ BwdLay(int kp1, int np1, int kp2, int np2, int L, int hr = kHeadBwdRows) {
     w1 = 0;
     w2 = np1 * kp1 * 2;
     m = w2 + np2 * kp2 * 2;
-    h = m + 128 * kp1 * 2;
-    red = h + 128 * kp2 * 2;
-    total = red + 16 * 2 * L * 4;
+    h = m + hr * kp1 * 2;
+    red = h + hr * kp2 * 2;
+    total = red + (hr / 8) * 2 * L * 4;
   }
 };
-constexpr int kBwdStaticLds = (8 * 4 * 128 + 8 * 128 + 5 * 128) * 4 + 16 * 12;
+constexpr int kBwdStaticLds = ((kHeadBwdRows / 16) * 4 * 128 + (kHeadBwdRows / 16) * 128 + 5 * 128) * 4 +
+                              (kHeadBwdRows / 8) * 12;
 
 __device__ __forceinline__ float shfl_rows8(float v) {   // sum over the 8 rows a wave holds per sub
   v += __shfl_xor(v, 8, 64);
@@ -355,16 +358,16 @@ __device__ __forceinline__ float shfl_rows8(float v) {   // sum over the 8 rows 
 }
 
 // NQ: 64-column chunks of z per lane (L <= 64: 1); NB1 / NB2: column blocks per wave half
-template <int NQ, int NB1, int NB2>
-__global__ void __launch_bounds__(1024) head_bwd_kernel(HeadBwdArgs a) {
-  constexpr int HT = 1024;
+template <int HR, int NQ, int NB1, int NB2>
+__global__ void __launch_bounds__(HR * 8) head_bwd_kernel(HeadBwdArgs a) {
+  constexpr int HT = HR * 8, HW = HT / 64, NRB = HR / 16;   // threads, waves, 16-row blocks
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  __shared__ __attribute__((aligned(16))) float cps[8][4][128];   // ENC1 column partials per 16-row block
-  __shared__ __attribute__((aligned(16))) float cpb[8][128];      // dh column partials per 16-row block
-  __shared__ float colp[5][128];                                   // ENC1 per-column parameters
-  __shared__ double sl[16];
-  __shared__ unsigned stp[16];
-  const BwdLay lay(a.kp1, a.np1, a.kp2, a.np2, a.L);
+  __shared__ __attribute__((aligned(16))) float cps[NRB][4][128];   // ENC1 column partials per 16-row block
+  __shared__ __attribute__((aligned(16))) float cpb[NRB][128];      // dh column partials per 16-row block
+  __shared__ float colp[5][128];                                     // ENC1 per-column parameters
+  __shared__ double sl[HW];
+  __shared__ unsigned stp[HW];
+  const BwdLay lay(a.kp1, a.np1, a.kp2, a.np2, a.L, HR);
   __bf16* w1s = reinterpret_cast<__bf16*>(smem + lay.w1);
   __bf16* w2s = reinterpret_cast<__bf16*>(smem + lay.w2);
   __bf16* ms_img = reinterpret_cast<__bf16*>(smem + lay.m);
@@ -374,17 +377,17 @@ __global__ void __launch_bounds__(1024) head_bwd_kernel(HeadBwdArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   // tile: XCD-aware (a graph's tiles on one XCD, as the gather kernels' row blocks)
   int t = blockIdx.x;
-  if (a.ngraphs % 8 == 0 && a.npg % 128 == 0 && a.ngraphs > 0) {
-    const int tpg = a.npg / 128, x = t & 7, sq = t >> 3;
+  if (a.ngraphs % 8 == 0 && a.npg % HR == 0 && a.ngraphs > 0) {
+    const int tpg = a.npg / HR, x = t & 7, sq = t >> 3;
     const int gi = sq / tpg;
     t = (x + 8 * gi) * tpg + (sq - gi * tpg);
   }
-  const int r0 = t * 128;
+  const int r0 = t * HR;
 
-  stage_img(a.wmsb_img, a.np1 * a.kp1 * 2, reinterpret_cast<char*>(w1s), HT / 64);
-  stage_img(a.whb_img, a.np2 * a.kp2 * 2, reinterpret_cast<char*>(w2s), HT / 64);
+  stage_img(a.wmsb_img, a.np1 * a.kp1 * 2, reinterpret_cast<char*>(w1s), HW);
+  stage_img(a.whb_img, a.np2 * a.kp2 * 2, reinterpret_cast<char*>(w2s), HW);
   // the dh image's columns [gh, kp2) are the zero k-padding the row engine stages
-  for (int i = tid; i < 128 * a.kp2 / 8; i += HT) reinterpret_cast<uint4*>(dh_img)[i] = make_uint4(0u, 0u, 0u, 0u);
+  for (int i = tid; i < HR * a.kp2 / 8; i += HT) reinterpret_cast<uint4*>(dh_img)[i] = make_uint4(0u, 0u, 0u, 0u);
   for (int n = tid; n < 128; n += HT) {   // rowconv RC_ENC1 column parameters
     const bool cv = n < a.W;
     colp[1][n] = cv ? a.ge[n] * kBnC : 0.f;
@@ -511,18 +514,18 @@ __global__ void __launch_bounds__(1024) head_bwd_kernel(HeadBwdArgs a) {
   __syncthreads();
   if (tid < L2) {
     float v = 0.f;
-    for (int k = 0; k < 16; ++k) v += bred[k * L2 + tid];
+    for (int k = 0; k < HW; ++k) v += bred[k * L2 + tid];
     a.bms_part[(long long)t * L2 + tid] = v;
   }
   if (tid == 0) {
     double tl = 0.0, tt = 0.0;
-    for (int k = 0; k < 16; ++k) { tl += sl[k]; tt += (double)stp[k]; }
+    for (int k = 0; k < HW; ++k) { tl += sl[k]; tt += (double)stp[k]; }
     a.edge_part[2 * t] = tl;
     a.edge_part[2 * t + 1] = tt;
   }
 
   // ---- 2. dh = d[mu | s] Wms^T (row engine RC_LIN, no bias) + its column sums
-  const int li = lane & 15, lg = lane >> 4, rb = w & 7, half = w >> 3;
+  const int li = lane & 15, lg = lane >> 4, rb = w % NRB, half = w / NRB;
   const int row = 16 * rb + li, r = r0 + row;
   const bool vrow = r < a.R;
   {
@@ -570,7 +573,7 @@ __global__ void __launch_bounds__(1024) head_bwd_kernel(HeadBwdArgs a) {
   if (tid < a.gh) {
     float v = 0.f;
 #pragma unroll
-    for (int b = 0; b < 8; ++b) v += cpb[b][tid];
+    for (int b = 0; b < NRB; ++b) v += cpb[b][tid];
     a.bh_part[(long long)t * a.gh + tid] = v;
   }
 
@@ -635,7 +638,7 @@ __global__ void __launch_bounds__(1024) head_bwd_kernel(HeadBwdArgs a) {
     const int q = i / a.W, n = i - q * a.W;
     float v = 0.f;
 #pragma unroll
-    for (int b = 0; b < 8; ++b) v += cps[b][q][n];
+    for (int b = 0; b < NRB; ++b) v += cps[b][q][n];
     a.enc1_part[(long long)t * 4 * a.W + i] = v;
   }
 }
@@ -643,7 +646,8 @@ __global__ void __launch_bounds__(1024) head_bwd_kernel(HeadBwdArgs a) {
 template <int NQ, int NB1, int NB2>
 int head_bwd_launch(const HeadBwdArgs& a, hipStream_t s) {
   const size_t lds = (size_t)BwdLay(a.kp1, a.np1, a.kp2, a.np2, a.L).total;
-  hipLaunchKernelGGL((head_bwd_kernel<NQ, NB1, NB2>), dim3(head_tiles(a.R)), dim3(1024), lds, s, a);
+  hipLaunchKernelGGL((head_bwd_kernel<kHeadBwdRows, NQ, NB1, NB2>), dim3(head_tiles(a.R)),
+                     dim3(kHeadBwdRows * 8), lds, s, a);
   SND_LAUNCH_CHECK("head_bwd_kernel");
   return 0;
 }
@@ -821,7 +825,7 @@ int launch_front(FrontArgs& a, const PackDesc* pack, int npack, hipStream_t s) {
   return 0;
 }
 
-int head_tiles(int R) { return cdiv(R, 128); }
+int head_tiles(int R) { return cdiv(R, kHeadBwdRows); }
 
 bool head_bwd_supported(int L, int gh, int W, int h1, int kp1, int np1, int kp2, int np2) {
   if ((L != 16 && L != 32 && L != 64) || kp1 != 2 * L) return false;
@@ -888,14 +892,14 @@ int head_init_attributes() {
                       reinterpret_cast<const void*>(head_fwd_kernel<128, 1, 4>),
                       reinterpret_cast<const void*>(head_fwd_kernel<128, 2, 2>),
                       reinterpret_cast<const void*>(head_fwd_kernel<128, 2, 4>)};
-  const void* kb[] = {reinterpret_cast<const void*>(head_bwd_kernel<1, 1, 1>),
-                      reinterpret_cast<const void*>(head_bwd_kernel<1, 1, 2>),
-                      reinterpret_cast<const void*>(head_bwd_kernel<1, 1, 3>),
-                      reinterpret_cast<const void*>(head_bwd_kernel<1, 1, 4>),
-                      reinterpret_cast<const void*>(head_bwd_kernel<1, 2, 1>),
-                      reinterpret_cast<const void*>(head_bwd_kernel<1, 2, 2>),
-                      reinterpret_cast<const void*>(head_bwd_kernel<1, 2, 3>),
-                      reinterpret_cast<const void*>(head_bwd_kernel<1, 2, 4>)};
+  const void* kb[] = {reinterpret_cast<const void*>(head_bwd_kernel<kHeadBwdRows, 1, 1, 1>),
+                      reinterpret_cast<const void*>(head_bwd_kernel<kHeadBwdRows, 1, 1, 2>),
+                      reinterpret_cast<const void*>(head_bwd_kernel<kHeadBwdRows, 1, 1, 3>),
+                      reinterpret_cast<const void*>(head_bwd_kernel<kHeadBwdRows, 1, 1, 4>),
+                      reinterpret_cast<const void*>(head_bwd_kernel<kHeadBwdRows, 1, 2, 1>),
+                      reinterpret_cast<const void*>(head_bwd_kernel<kHeadBwdRows, 1, 2, 2>),
+                      reinterpret_cast<const void*>(head_bwd_kernel<kHeadBwdRows, 1, 2, 3>),
+                      reinterpret_cast<const void*>(head_bwd_kernel<kHeadBwdRows, 1, 2, 4>)};
   const void* kf[] = {reinterpret_cast<const void*>(enc_front_kernel<1>),
                       reinterpret_cast<const void*>(enc_front_kernel<2>),
                       reinterpret_cast<const void*>(enc_front_kernel<3>),

@@ -58,7 +58,11 @@ struct HeadBwdArgs {
   int dbg;
 };
 bool head_bwd_supported(int L, int gh, int W, int h1, int kp1, int np1, int kp2, int np2);
-int head_tiles(int R);
+#ifndef SND_HB_ROWS
+#define SND_HB_ROWS 128   // rows per backward-head tile (A/B build: -DSND_HB_ROWS=64)
+#endif
+constexpr int kHeadBwdRows = SND_HB_ROWS;
+int head_tiles(int R);   // backward-head tiles (kHeadBwdRows rows each)
 int launch_head_bwd(const HeadBwdArgs& a, hipStream_t s);
 
 // GraphConvolution 0 as (A X) W0 (gcn0 semantics: AX, H1 = [BN0(lrelu(AX W0)) | X]) and

@@ -474,7 +474,8 @@ extern "C" int snd_plan_create(const snd_config_t* cfg, int n_graphs, snd_plan_t
       p->add_buf("FHH", R * gh, 2);       p->add_buf("FDMS", R * 2 * L, 2);
       p->add_buf("FDH", R * gh, 2);       p->add_buf("FDP1", R * h1, 2);
       p->add_buf("FDXW1", R * h1, 2);     p->add_buf("FDP0", R * h0, 2);
-      const int rcb = rc_blocks(p->R);
+      // column partials: the row engine's 128-row blocks, or the backward head's tiles
+      const int rcb = std::max(rc_blocks(p->R), head_tiles(p->R));
       p->add_buf("PFBMS", (long long)reparam_bwd_fast_blocks(p->R, L) * 2 * L);
       p->add_buf("PFBH", (long long)rcb * gh);
       p->add_buf("PFENC1", (long long)rcb * 4 * W);
@@ -1104,6 +1105,8 @@ void encoder_fast_reduce(const Ctx& x, std::vector<ReduceDesc>& rd) {
   const snd_config_t& c = p.c;
   const int L = c.latent, f = c.f_in, h0 = c.h0, h1 = c.h1, gh = c.g_hidden, W = p.W;
   const int rcb = rc_blocks(p.R);
+  // PFBH / PFENC1 come from the fused backward head (its tiles) or the row engine (rcb)
+  const int hcb = p.head_bwd ? head_tiles(p.R) : rcb;
   auto flat = [&](const char* buf, int parts, long long len, long long stride, const char* dst, float sc) {
     rd.push_back({x.f(buf), x.g(dst), parts, (int)len, stride, sc, 0, 0, 0, 0});
   };
@@ -1124,16 +1127,16 @@ void encoder_fast_reduce(const Ctx& x, std::vector<ReduceDesc>& rd) {
     else flat("PFBMS", reparam_bwd_fast_blocks(p.R, L), 2 * L, 2 * L, "enc.bms", 1.f);
     slab2d("FSWH", p.gWh.gx, p.kwh, gh, "enc.Wh");
     if (p.kwh < W) slab_at(x.f("FSWHT"), p.gWht.gx, W - p.kwh, gh, x.g("enc.Wh") + (long long)p.kwh * gh, gh);
-    flat("PFBH", rcb, gh, gh, "enc.bh", 1.f);
+    flat("PFBH", hcb, gh, gh, "enc.bh", 1.f);
   }
   slab2d("FSW1", p.gW1.gx, p.kw1, h1, "enc.W1");
   if (p.kw1 < h0 + f) slab_at(x.f("FSW1T"), p.gW1t.gx, h0 + f - p.kw1, h1, x.g("enc.W1") + (long long)p.kw1 * h1, h1);
   slab2d("FSW0", p.gW0.gx, f, h0, "enc.W0");
   const float* e1 = x.f("PFENC1");
-  rd.push_back({e1, x.g("enc.bne.gamma"), rcb, W, 4LL * W, kBnC, 0, 0, 0, 0});
-  rd.push_back({e1 + W, x.g("enc.bne.beta"), rcb, W, 4LL * W, 1.f, 0, 0, 0, 0});
-  rd.push_back({e1 + 2 * W, x.g("enc.bn1.gamma"), rcb, h1, 4LL * W, kBnC, 0, 0, 0, 0});
-  rd.push_back({e1 + 3 * W, x.g("enc.bn1.beta"), rcb, h1, 4LL * W, 1.f, 0, 0, 0, 0});
+  rd.push_back({e1, x.g("enc.bne.gamma"), hcb, W, 4LL * W, kBnC, 0, 0, 0, 0});
+  rd.push_back({e1 + W, x.g("enc.bne.beta"), hcb, W, 4LL * W, 1.f, 0, 0, 0, 0});
+  rd.push_back({e1 + 2 * W, x.g("enc.bn1.gamma"), hcb, h1, 4LL * W, kBnC, 0, 0, 0, 0});
+  rd.push_back({e1 + 3 * W, x.g("enc.bn1.beta"), hcb, h1, 4LL * W, 1.f, 0, 0, 0, 0});
   const float* e0 = x.f("PFENC0");
   rd.push_back({e0, x.g("enc.bn0.gamma"), rcb, h0, 2LL * h0, kBnC, 0, 0, 0, 0});
   rd.push_back({e0 + h0, x.g("enc.bn0.beta"), rcb, h0, 2LL * h0, 1.f, 0, 0, 0, 0});

@@ -28,6 +28,7 @@ for s in $STAGES; do
     abzzt) step ab_zzt 300 python tools/ab_zzt.py --variants ${ZZT_VARIANTS:-zzt_dense} --rounds 5 ;;
     abspmm) step ab_spmm 300 python tools/ab_spmm_win.py --flags ${SPMM_FLAGS:-0} --rounds 6 ;;
     some) step pytest_some 600 python -u -m pytest ${TESTS} -x -v --timeout 300 --timeout-method thread ;;
+    abfast) step ab_fast 300 python tools/ab_fast.py --keys ${FAST_KEYS:-head_fwd,head_bwd} --flags ${FAST_FLAGS:-0} ;;
     strong) step strong 400 python bench.py --steps 50 --warmup 10 --no-cpu-baseline --batch-sweep "" --extra "" ;;
   esac
 done
