@@ -463,11 +463,18 @@ int snd_plan_param_block(const snd_plan_t* plan, int idx, const char** name,
 size_t snd_plan_workspace_bytes(const snd_plan_t* plan);
 /* Fused TF1 Adam (1 GPU: no all-reduce between gradient and update).  With m and
  * v set (flat buffers in the parameter layout), snd_train_step applies the Adam
- * update of optimizer.py:125,197 to the blocks snd_plan_block_fused() reports (the
- * graph-latent head and d_sg_lin1 weights, whose gradients are produced complete
- * by one kernel) in place, through the params pointer, and does not write their
- * gradient; the caller's snd_adam_tf1 then covers the other blocks.  m = v = NULL
- * turns it off (default).  lr/betas/eps as snd_adam_tf1; grad_scale is 1. */
+ * update of optimizer.py:125,197 in place, through the params pointer, to the blocks
+ * snd_plan_block_fused() reports nonzero; the caller's snd_adam_tf1 then covers the
+ * other blocks (none on the node-latent plans).  m = v = NULL turns it off (default).
+ * lr/betas/eps as snd_adam_tf1; grad_scale is 1.
+ * snd_plan_block_fused (ABI 16): 0 = updated by the caller; 1 = updated inside the
+ * weight-gradient stream that produces the gradient complete (graph-latent head weight,
+ * d_sg_lin1 weight and bias) -- its gradient is NOT written; 2 = updated by the step's final
+ * slab reduction, which writes the gradient and applies Adam to it in the same launch
+ * (every block that launch writes complete), the gradient is written as usual.
+ * The reduction reads the step index t = *step_counter + 1 that the step's
+ * reparameterisation kernel publishes in the workspace, since the same launch's
+ * finalize workgroup advances *step_counter. */
 int snd_plan_fuse_adam(snd_plan_t* plan, float* m, float* v, float lr, float beta1,
                        float beta2, float eps);
 int snd_plan_block_fused(const snd_plan_t* plan, int idx);

@@ -31,6 +31,7 @@ constexpr int kReparamGrid = 2048;
 // division; rows stride over the grid.  L <= 256.
 __global__ void __launch_bounds__(256) reparam_fwd_kernel(ReparamFwdArgs a) {
   const unsigned off = a.step ? (unsigned)(*a.step) : 0u;
+  if (a.stepn && blockIdx.x == 0 && threadIdx.x == 0) *a.stepn = (int)off + 1;
   const int rpb = 256 / a.L;                       // rows per block pass
   const int c = threadIdx.x % a.L, rl = threadIdx.x / a.L;
   double kl = 0.0;
@@ -87,6 +88,7 @@ __global__ void __launch_bounds__(256) small_head_fwd_kernel(SmallHeadFwdArgs a)
   for (int i = t; i < a.rows * a.gh; i += 256) hs[i / a.gh][i % a.gh] = a.hh[i];
   __syncthreads();
   const unsigned off = a.step ? (unsigned)(*a.step) : 0u;
+  if (a.stepn && blockIdx.x == 0 && t == 0) *a.stepn = (int)off + 1;
   const int b = t / kSHC, j = t - b * kSHC, c = c0 + j;
   double kl = 0.0;
   if (b < a.rows && c < a.L) {
@@ -371,9 +373,10 @@ struct ReducePack {
 
 template <int NTF> __device__ void finalize_block(const FinalizeArgs& a);
 
-// fin: block 0 computes the loss terms (finalize) instead of a reduction block
-template <bool FIN>
-__global__ void __launch_bounds__(256) reduce_kernel(ReducePack pk, FinalizeArgs fin) {
+// fin: block 0 computes the loss terms (finalize) instead of a reduction block;
+// ADAM: descriptors of ra.mask (this launch's bits) also take their TF1 Adam update
+template <bool FIN, bool ADAM>
+__global__ void __launch_bounds__(256) reduce_kernel(ReducePack pk, FinalizeArgs fin, ReduceAdam ra) {
   if constexpr (FIN) {
     if (blockIdx.x == 0) { finalize_block<256>(fin); return; }
   }
@@ -382,6 +385,13 @@ __global__ void __launch_bounds__(256) reduce_kernel(ReducePack pk, FinalizeArgs
   while (di + 1 < kMaxReduce && bid >= pk.bstart[di + 1]) ++di;   // uniform
   const ReduceDesc& d = pk.d[di];
   const int bx = bid - pk.bstart[di];
+  // bias-corrected step size (snd_adam_tf1's arithmetic), while the slab loads are in flight
+  const bool dad = ADAM && ((ra.mask >> di) & 1ull);   // uniform per block
+  float lrt = 0.f;
+  if (dad) {
+    const int st = *ra.stepn;
+    lrt = (float)((double)ra.lr * sqrt(1.0 - pow((double)ra.b2, st)) / (1.0 - pow((double)ra.b1, st)));
+  }
   __shared__ double red[256];
   const int rows = d.rows > 0 ? d.rows : 1;
   const long long items = (long long)rows * d.len;
@@ -417,6 +427,16 @@ __global__ void __launch_bounds__(256) reduce_kernel(ReducePack pk, FinalizeArgs
     float v = (float)(t * (double)d.scale);
     if (d.accumulate) v += *dst;
     *dst = v;
+    if constexpr (ADAM) {
+      if (dad) {
+        const long long k = dst - ra.gbase;
+        float pi = ra.p[k], mi = ra.m[k], vi = ra.v[k];
+        adam_elem(pi, mi, vi, __fmul_rn(v, 1.f), ra.b1, ra.b2, ra.eps, lrt);
+        ra.m[k] = mi;
+        ra.v[k] = vi;
+        ra.p[k] = pi;
+      }
+    }
   }
 }
 
@@ -575,9 +595,19 @@ int launch_enc_bwd(const EncBwdArgs& a, int rows, hipStream_t s) {
   return 0;
 }
 
-int launch_reduce(const ReduceDesc* d, int n, hipStream_t s, const FinalizeArgs* fin) {
+int launch_reduce(const ReduceDesc* d, int n, hipStream_t s, const FinalizeArgs* fin,
+                  const ReduceAdam* adam) {
+  SND_CHECK_ARG(!adam || (n <= 64 && adam->gbase && adam->p && adam->m && adam->v && adam->stepn),
+                "reduce: fused Adam needs <= 64 descriptors and its operands");
   for (int base = 0; base < n || (base == 0 && fin); base += kMaxReduce) {
     const bool last = base + kMaxReduce >= n;
+    ReduceAdam ra{};
+    if (adam) {
+      ra = *adam;
+      ra.mask = adam->mask >> base;
+      if (n - base < 64) ra.mask &= (1ull << (n - base)) - 1;
+    }
+    const bool ad = ra.mask != 0;
     ReducePack pk{};
     const int cnt = n - base < kMaxReduce ? n - base : kMaxReduce;
     long long nb = 0;
@@ -592,10 +622,12 @@ int launch_reduce(const ReduceDesc* d, int n, hipStream_t s, const FinalizeArgs*
     }
     pk.bstart[kMaxReduce] = (int)nb;
     if (fin && last) {   // the loss terms ride in the last reduction launch
-      hipLaunchKernelGGL(reduce_kernel<true>, dim3((unsigned)nb + 1), dim3(256), 0, s, pk, *fin);
+      if (ad) hipLaunchKernelGGL((reduce_kernel<true, true>), dim3((unsigned)nb + 1), dim3(256), 0, s, pk, *fin, ra);
+      else hipLaunchKernelGGL((reduce_kernel<true, false>), dim3((unsigned)nb + 1), dim3(256), 0, s, pk, *fin, ra);
     } else {
       if (nb == 0) continue;
-      hipLaunchKernelGGL(reduce_kernel<false>, dim3((unsigned)nb), dim3(256), 0, s, pk, FinalizeArgs{});
+      if (ad) hipLaunchKernelGGL((reduce_kernel<false, true>), dim3((unsigned)nb), dim3(256), 0, s, pk, FinalizeArgs{}, ra);
+      else hipLaunchKernelGGL((reduce_kernel<false, false>), dim3((unsigned)nb), dim3(256), 0, s, pk, FinalizeArgs{}, ra);
     }
     SND_LAUNCH_CHECK("reduce_kernel");
   }

@@ -11,6 +11,7 @@ struct ReparamFwdArgs {
   double* kl_part;            // [blocks]
   __bf16* zb; int ldzb;       // optional bf16 copy of z (fast-path MFMA operand)
   unsigned long long eps_base = 0;   // Philox element index of row 0 (data parallel: rank * rows * L)
+  int* stepn = nullptr;        // optional: *step + 1 published for the fused-Adam reduction (ReduceAdam)
 };
 int reparam_blocks(int rows, int L);
 int launch_reparam_fwd(const ReparamFwdArgs& a, hipStream_t s);
@@ -29,6 +30,7 @@ struct SmallHeadFwdArgs {
   const float* eps_in; unsigned long long seed; const int* step; unsigned long long eps_base;
   float* eps_out; float* z;                   // [rows][L]
   double* kl_part;                            // [small_head_fwd_blocks(L)]
+  int* stepn = nullptr;        // optional: *step + 1 published for the fused-Adam reduction (ReduceAdam)
 };
 struct SmallHeadBwdArgs {
   const float* hh; int rows; int gh;

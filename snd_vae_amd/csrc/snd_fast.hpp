@@ -195,6 +195,7 @@ struct ReparamPrepArgs {
   double* kl_part;            // [ngraphs * npad / 64]
   int stage_only;             // 1: ms is J itself (T-ref projection output); no eps / KL
   unsigned long long eps_base = 0;   // Philox element index of row 0 (data parallel: rank * rows * L)
+  int* stepn = nullptr;        // optional: *step + 1 published for the fused-Adam reduction (ReduceAdam)
 };
 int reparam_prep_blocks(int ngraphs, int npad);
 

@@ -598,6 +598,7 @@ __global__ void __launch_bounds__(NT) reparam_prep_kernel(ReparamPrepArgs a) {
   const int g = blockIdx.y, rb = blockIdx.x;
   const int L = a.L;                      // multiple of 4 (16 / 32 / 64 / 128)
   const unsigned off = a.step ? (unsigned)(*a.step) : 0u;
+  if (a.stepn && g == 0 && rb == 0 && threadIdx.x == 0) *a.stepn = (int)off + 1;
   const float sc = 1.2011224087864498f;  // sqrt(log2 e)
   constexpr int Q = DP / 4;               // 4-column quads per row: one Philox block each
   double kl = 0.0;

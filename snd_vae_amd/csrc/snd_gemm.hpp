@@ -42,9 +42,23 @@ struct ReduceDesc {
 };
 constexpr int kMaxReduce = 48;
 struct FinalizeArgs;
+// TF1 Adam applied by the reduction itself (single device, snd_plan_fuse_adam): every
+// element of a descriptor whose bit is set in mask is a complete gradient g of the
+// parameter at (dst - gbase) of p / m / v; the reduction stores g and updates that
+// parameter (same arithmetic as snd_adam_tf1).  stepn: the step the update uses,
+// *step + 1, published by the step's reparameterisation kernel -- the finalize block of
+// the same launch advances *step, so the reduction blocks cannot read *step itself.
+struct ReduceAdam {
+  const float* gbase;
+  float* p; float* m; float* v;
+  float lr, b1, b2, eps;
+  const int* stepn;
+  unsigned long long mask;      // bit i: descriptor i of the launch's descriptor list
+};
 // Deterministic slab reductions; with fin, the same launch also computes the loss
 // terms (snd_elem.hpp FinalizeArgs) in an extra workgroup.
-int launch_reduce(const ReduceDesc* d, int n, hipStream_t s, const FinalizeArgs* fin = nullptr);
+int launch_reduce(const ReduceDesc* d, int n, hipStream_t s, const FinalizeArgs* fin = nullptr,
+                  const ReduceAdam* adam = nullptr);
 
 // Column partial sums written by elementwise kernels are laid out as
 // slab[block][ncols]; helpers compute the block count used.

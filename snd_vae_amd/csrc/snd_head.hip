@@ -240,6 +240,7 @@ __global__ void __launch_bounds__(HR * 8) head_fwd_kernel(HeadFwdArgs a) {
   // every wave takes rows x Philox quads of the tile
   {
     const unsigned off = a.step ? (unsigned)(*a.step) : 0u;
+    if (a.stepn && blockIdx.x == 0 && tid == 0) *a.stepn = (int)off + 1;
     const int nq = L >> 2;
     double kl[HR / 64];
 #pragma unroll

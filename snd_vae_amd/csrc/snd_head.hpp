@@ -30,6 +30,7 @@ struct HeadFwdArgs {
   __bf16* jrow; __bf16* jt; float* colpart;   // zz^T staging (zzt_stage), DP == L
   double* kl_part;                            // [ngraphs * npad / 64]
   int dbg;
+  int* stepn = nullptr;                       // optional: *step + 1 for the fused-Adam reduction
 };
 bool head_fwd_supported(int h1, int f, int gh, int L, int kp1, int np1, int kp2, int np2);
 int launch_head_fwd(const HeadFwdArgs& a, hipStream_t s);

@@ -123,8 +123,18 @@ struct snd_plan {
   // rank draws the normals a single device would draw for its rows of the global batch
   unsigned long long rng_row0 = 0;
   unsigned long long eps_base() const { return rng_row0 * (unsigned long long)c.latent; }
-  bool block_fused(const std::string& n) const {
-    return fuse_m && tref && (n == "dec.Wp" || (n == "enc.Wh" && !sg));
+  // blocks updated inside a weight-gradient stream (graph latent: gradient not written)
+  bool stream_fused(const std::string& n) const {
+    return fuse_m && tref && (n == "dec.Wp" || n == "dec.bp" || (n == "enc.Wh" && !sg));
+  }
+  // blocks whose every element the step's final reduction writes exactly once
+  // (reduce_adam_cover, at snd_plan_fuse_adam): with fuse_m their Adam update rides in
+  // that launch (ReduceAdam), gradient still written
+  std::vector<char> radam;
+  bool reduce_fused(size_t i) const { return fuse_m && i < radam.size() && radam[i]; }
+  // 0 separate Adam, 1 fused into a stream, 2 fused into the final reduction
+  int fused_kind(size_t i) const {
+    return stream_fused(blocks[i].name) ? 1 : (reduce_fused(i) ? 2 : 0);
   }
   // parameters of the last snd_train_step (snd_plan_launch re-runs kernels on them)
   mutable const float* last_params = nullptr;
@@ -174,7 +184,7 @@ struct snd_plan {
 };
 
 extern "C" const char* snd_last_error(void) { return g_err; }
-extern "C" int snd_abi_version(void) { return 15; }
+extern "C" int snd_abi_version(void) { return 16; }
 
 // zz^T column splits with the concurrent decoder on: zz^T keeps the CUs the decoder's
 // tiles do not take (one 1024-thread workgroup per CU for either kernel)
@@ -298,6 +308,7 @@ extern "C" int snd_plan_create(const snd_config_t* cfg, int n_graphs, snd_plan_t
   const int nz = zzt_dense_blocks(p->B, p->N, c.dtype), ne = edge_blocks(p->R, dj);
   const int nk = reparam_blocks(p->RH, L), nh = head_blocks(p->R), nc = col_blocks(p->R);
   p->add_buf("PZZT", 2LL * nz, 8); p->add_buf("PEDGE", 2LL * std::max(ne, edge_bf16_blocks(p->R)), 8); p->add_buf("PKL", std::max({nk, reparam_prep_blocks(p->B, zzt_npad(p->N)), small_head_fwd_blocks(c.latent)}), 8);
+  p->add_buf("STEPN", 1);   // *step + 1, for the fused-Adam reduction (ReduceAdam)
   p->add_buf("PSSES", nh, 8); p->add_buf("PSSEN", nh, 8);
   p->add_buf("PHS", (long long)nh * (c.s3 * c.spatial_dim + c.spatial_dim));
   p->add_buf("PHN", (long long)nh * (c.n2 * c.num_feature + c.num_feature));
@@ -540,11 +551,14 @@ extern "C" int snd_plan_set_option(snd_plan_t* p, const char* name, int value) {
   return SND_ERR_ARG;
 }
 
+void reduce_adam_cover(snd_plan& p);
+
 extern "C" int snd_plan_fuse_adam(snd_plan_t* p, float* m, float* v, float lr, float beta1,
                                   float beta2, float eps) {
   SND_CHECK_ARG(p && ((m && v) || (!m && !v)), "snd_plan_fuse_adam: bad args");
   p->fuse_m = m; p->fuse_v = v;
   p->fuse_lr = lr; p->fuse_b1 = beta1; p->fuse_b2 = beta2; p->fuse_eps = eps;
+  if (m && p->radam.empty()) reduce_adam_cover(*p);
   return 0;
 }
 
@@ -563,7 +577,7 @@ extern "C" int snd_plan_grad_event(snd_plan_t* p, int idx, void* event) {
 }
 extern "C" int snd_plan_block_fused(const snd_plan_t* p, int idx) {
   SND_CHECK_ARG(p && idx >= 0 && idx < (int)p->blocks.size(), "snd_plan_block_fused: bad index");
-  return p->block_fused(p->blocks[idx].name) ? 1 : 0;
+  return p->fused_kind((size_t)idx);
 }
 extern "C" int snd_plan_buffer(const snd_plan_t* p, const char* name, long long* off,
                                long long* numel) {
@@ -593,6 +607,7 @@ struct Ctx {
   double* d(const char* n) const { return (double*)(ws + p->buf(n)); }
   const float* w(const char* n) const { return P + p->blk(n); }
   float* g(const char* n) const { return Gr + p->blk(n); }
+  int* stepn() const { return reinterpret_cast<int*>(ws + p->buf("STEPN")); }
 };
 
 // Adam state of a block updated inside the step (snd_plan_fuse_adam); params are
@@ -1000,6 +1015,7 @@ int head_fwd_fused(const Ctx& x, const snd_batch_t* batch, const float* eps, uns
   a.z = x.f("Z"); a.eps_out = x.f("EPS"); a.zb = reinterpret_cast<__bf16*>(x.f("ZB"));
   a.jrow = reinterpret_cast<__bf16*>(stg.jrow); a.jt = reinterpret_cast<__bf16*>(stg.jt);
   a.colpart = stg.colpart; a.kl_part = x.d("PKL");
+  a.stepn = x.stepn();
   a.dbg = debug_flags();
   return launch_head_fwd(a, x.s);
 }
@@ -1505,6 +1521,117 @@ extern "C" int snd_plan_launch(const snd_plan_t* plan, const snd_batch_t* batch,
   return SND_ERR_ARG;
 }
 
+// the step's final reduction: every slab / column partial -> its gradient block, in one
+// launch with the loss terms (snd_train_step); also walked, on placeholder bases, by
+// reduce_adam_cover to find the blocks the reduction writes complete
+void final_reduce_descs(const Ctx& x, std::vector<ReduceDesc>& rd) {
+  const snd_plan& p = *x.p;
+  const snd_config_t& c = p.c;
+  const int R = p.R, N = p.N, f = c.f_in, h0 = c.h0, h1 = c.h1, gh = c.g_hidden, L = c.latent;
+  const int W = p.W, C1 = p.C1, s1 = c.s1, s2 = c.s2, s3 = c.s3, n1 = c.n1, n2 = c.n2;
+  const int sd = c.spatial_dim, nf = c.num_feature;
+  const int dj = p.dj, RH = p.RH;
+  const long long KH = (long long)N * W;
+  const int nc = col_blocks(R), nh = head_blocks(R);
+  auto slab = [&](const char* buf, const Split& sp, int Mtot, int N_, const char* wname,
+                  int wlen, const char* bname) {
+    const float* s0 = x.f(buf);
+    rd.push_back({s0, x.g(wname), sp.splits, wlen, (long long)Mtot * N_, 1.f, 0});
+    if (bname) rd.push_back({s0 + wlen, x.g(bname), sp.splits, N_, (long long)Mtot * N_, 1.f, 0});
+  };
+  if (p.sg) {
+    slab("SWH", p.sWh, (int)KH + 1, gh, "enc.Wh", (int)KH * gh, "enc.bh");
+  } else if (p.fast_enc) {
+    encoder_fast_reduce(x, rd);
+  } else {
+    slab("SW0", p.sW0, f, h0, "enc.W0", f * h0, nullptr);
+    slab("SW1", p.sW1, h0 + f, h1, "enc.W1", (h0 + f) * h1, nullptr);
+    if (!p.tref) slab("SWH", p.sWh, W + 1, gh, "enc.Wh", W * gh, "enc.bh");
+  }
+  if (p.tref && !p.sg)   // dbh = sum over graphs of dh
+    rd.push_back({x.f("DH"), x.g("enc.bh"), RH, gh, (long long)gh, 1.f, 0});
+  if (!p.fast_enc || p.tref) slab("SWMS", p.sWms, gh + 1, 2 * L, "enc.Wms", gh * 2 * L, "enc.bms");
+  if (!p.fast) {
+    slab("SK1", p.sK1, 5 * dj, C1, "dec.K1", 5 * dj * C1, nullptr);
+    slab("SK2S", p.sK2s, 5 * s1, s2, "dec.K2s", 5 * s1 * s2, nullptr);
+    slab("SK2N", p.sK2n, 5 * n1, n2, "dec.K2n", 5 * n1 * n2, nullptr);
+    slab("SK3S", p.sK3s, 5 * s2, s3, "dec.K3s", 5 * s2 * s3, nullptr);
+  }
+  auto cols = [&](const char* buf, int stride, int off, int len, const char* dst) {
+    rd.push_back({x.f(buf) + off, x.g(dst), nc, len, (long long)stride, 1.f, 0});
+  };
+  if (!p.fast_enc && !p.sg) {
+    cols("PENC1", 2 * W + 2 * h1, 0, W, "enc.bne.gamma");
+    cols("PENC1", 2 * W + 2 * h1, W, W, "enc.bne.beta");
+    cols("PENC1", 2 * W + 2 * h1, 2 * W, h1, "enc.bn1.gamma");
+    cols("PENC1", 2 * W + 2 * h1, 2 * W + h1, h1, "enc.bn1.beta");
+    cols("PENC0", 2 * h0, 0, h0, "enc.bn0.gamma");
+    cols("PENC0", 2 * h0, h0, h0, "enc.bn0.beta");
+  }
+  auto dec = [&](const char* buf, int w, const char* g, const char* b, const char* bias) {
+    cols(buf, 3 * w, 0, w, g);
+    cols(buf, 3 * w, w, w, b);
+    cols(buf, 3 * w, 2 * w, w, bias);
+  };
+  if (p.fast) {
+    decoder_fast_reduce(x, rd);
+  } else {
+    dec("PDEC3", s3, "dec.bn3s.gamma", "dec.bn3s.beta", "dec.b3s");
+    dec("PDEC2S", s2, "dec.bn2s.gamma", "dec.bn2s.beta", "dec.b2s");
+    dec("PDEC2N", n2, "dec.bn2n.gamma", "dec.bn2n.beta", "dec.b2n");
+    dec("PDEC1", C1, "dec.bn1.gamma", "dec.bn1.beta", "dec.b1");
+    const int hs = s3 * sd + sd, hn = n2 * nf + nf;
+    rd.push_back({x.f("PHS"), x.g("dec.Ws"), nh, s3 * sd, (long long)hs, 1.f, 0});
+    rd.push_back({x.f("PHS") + s3 * sd, x.g("dec.bs"), nh, sd, (long long)hs, 1.f, 0});
+    rd.push_back({x.f("PHN"), x.g("dec.Wn"), nh, n2 * nf, (long long)hn, 1.f, 0});
+    rd.push_back({x.f("PHN") + n2 * nf, x.g("dec.bn"), nh, nf, (long long)hn, 1.f, 0});
+  }
+}
+
+// Which blocks the final reduction writes complete: its descriptors built on placeholder
+// bases (offsets, not addresses), every element of a block written exactly once, by a
+// descriptor that stores (no accumulate).  Structural, so computed once per plan.
+void reduce_adam_cover(snd_plan& p) {
+  const uintptr_t wsb = (uintptr_t)1 << 44, gb = (uintptr_t)1 << 45;
+  Ctx x{&p, (char*)wsb, (const float*)((uintptr_t)1 << 46), (float*)gb, nullptr};
+  std::vector<ReduceDesc> rd;
+  final_reduce_descs(x, rd);
+  std::vector<unsigned char> hits((size_t)p.pcount, 0);
+  std::vector<char> bad(p.blocks.size(), 0);
+  for (const ReduceDesc& d : rd) {
+    const long long o = d.dst - (float*)gb;
+    const int rows = d.rows > 0 ? d.rows : 1;
+    for (int r = 0; r < rows; ++r)
+      for (int i = 0; i < d.len; ++i) {
+        const long long k = o + (long long)r * d.dst_rs + i;
+        if (k < 0 || k >= p.pcount) continue;
+        if (hits[(size_t)k] < 2) ++hits[(size_t)k];
+        if (d.accumulate) hits[(size_t)k] = 2;
+      }
+  }
+  p.radam.assign(p.blocks.size(), 0);
+  for (size_t b = 0; b < p.blocks.size(); ++b) {
+    const Block& bl = p.blocks[b];
+    if (p.stream_fused(bl.name) || bl.numel == 0) continue;
+    bool ok = true;
+    for (long long k = bl.off; k < bl.off + bl.numel && ok; ++k) ok = hits[(size_t)k] == 1;
+    p.radam[b] = ok;
+  }
+}
+
+// the final reduction's fused-Adam descriptors: those whose destination lies in a
+// reduce-fused block (a descriptor never straddles blocks)
+unsigned long long reduce_adam_mask(const snd_plan& p, const std::vector<ReduceDesc>& rd, const float* G) {
+  unsigned long long mask = 0;
+  for (size_t i = 0; i < rd.size() && i < 64; ++i) {
+    const long long o = rd[i].dst - G;
+    for (size_t b = 0; b < p.blocks.size(); ++b)
+      if (o >= p.blocks[b].off && o < p.blocks[b].off + p.blocks[b].numel && p.reduce_fused(b))
+        mask |= 1ull << i;
+  }
+  return mask;
+}
+
 extern "C" int snd_train_step(const snd_plan_t* plan, const snd_batch_t* batch,
                               const float* params, float* grads, void* workspace,
                               const float* eps, unsigned long long seed, int* step_counter,
@@ -1580,11 +1707,13 @@ extern "C" int snd_train_step(const snd_plan_t* plan, const snd_batch_t* batch,
     if (p.small_head) {   // [mu || s] = h Wms + bms, z and the KL terms in one launch
       SmallHeadFwdArgs a{x.f("Hh"), RH, gh, x.w("enc.Wms"), x.w("enc.bms"), L, x.f("MS"), eps, seed,
                          step_counter, p.eps_base(), x.f("EPS"), x.f("ZL"), x.d("PKL")};
+      a.stepn = x.stepn();
       SND_TRY(launch_small_head_fwd(a, x.s));
     } else {   // z [B, L] (model_joint.py:89); SND_SGJOINT: [B*S, L] (model.py:157)
       ReparamFwdArgs a{x.f("MS"), 2 * L, RH, L, eps, seed, step_counter, x.f("EPS"), x.f("ZL"),
                        x.d("PKL"), nullptr, L};
       a.eps_base = p.eps_base();
+      a.stepn = x.stepn();
       SND_TRY(launch_reparam_fwd(a, x.s));
     }
     // SND_SGJOINT: mean over the copies before the (affine) projection (model.py:177,180)
@@ -1606,11 +1735,13 @@ extern "C" int snd_train_step(const snd_plan_t* plan, const snd_batch_t* batch,
                       x.f("EPS"), (__bf16*)x.f("ZB"), (__bf16*)stg.jrow, (__bf16*)stg.jt, stg.colpart,
                       x.d("PKL")};
     a.eps_base = p.eps_base();
+    a.stepn = x.stepn();
     SND_TRY(launch_reparam_prep(a, zzt_dp(L), x.s));
   } else {
     ReparamFwdArgs a{x.f("MS"), 2 * L, R, L, eps, seed, step_counter, x.f("EPS"), x.f("Z"),
                      x.d("PKL"), nullptr, L};
     a.eps_base = p.eps_base();
+    a.stepn = x.stepn();
     SND_TRY(launch_reparam_fwd(a, x.s));
   }
   // inner-product decoder + CE (fused) and per-edge terms
@@ -1710,7 +1841,8 @@ extern "C" int snd_train_step(const snd_plan_t* plan, const snd_batch_t* batch,
       {   // d_sg_lin1 backward: dWp, dbp written; dz partials per block
         TrefProjBwdArgs a{x.f(p.sg ? "ZBAR" : "ZL"), p.B, L, x.w("dec.Wp"), CP, x.f("DZDEC"), x.f("DJD"),
                           x.f("EJ"), adj_scale, x.g("dec.Wp"), x.g("dec.bp"), x.f("PDZ")};
-        if (p.block_fused("dec.Wp")) a.adam = fused_adam(x, "dec.Wp", step_counter);
+        if (p.stream_fused("dec.Wp")) a.adam = fused_adam(x, "dec.Wp", step_counter);
+        if (p.stream_fused("dec.bp")) a.adam_b = fused_adam(x, "dec.bp", step_counter);
         SND_TRY(launch_tref_proj_bwd(a, x.s));
         if (p.ev_proj && hipEventRecord(p.ev_proj, x.s) != hipSuccess) {
           set_error("train step: grad event (dec.Wp) record failed");
@@ -1750,7 +1882,7 @@ extern "C" int snd_train_step(const snd_plan_t* plan, const snd_batch_t* batch,
         a.gb = reinterpret_cast<const __bf16*>(x.f("FG")); a.ldg = p.ldg; a.W = W; a.npg = N;
         a.dgb = reinterpret_cast<__bf16*>(x.f("FDG"));
       }
-      if (p.block_fused("enc.Wh")) a.adam = fused_adam(x, "enc.Wh", step_counter);
+      if (p.stream_fused("enc.Wh")) a.adam = fused_adam(x, "enc.Wh", step_counter);
       SND_TRY(launch_tref_head_bwd(a, x.s));
       if (p.ev_head && hipEventRecord(p.ev_head, x.s) != hipSuccess) {
         set_error("train step: grad event (enc.Wh) record failed");
@@ -1799,61 +1931,9 @@ extern "C" int snd_train_step(const snd_plan_t* plan, const snd_batch_t* batch,
   }
 
   // ======================= deterministic gradient reduction =================
-  const int nc = col_blocks(R), nh = head_blocks(R);
   std::vector<ReduceDesc> rd;
-  auto slab = [&](const char* buf, const Split& sp, int Mtot, int N_, const char* wname,
-                  int wlen, const char* bname) {
-    const float* s0 = x.f(buf);
-    rd.push_back({s0, x.g(wname), sp.splits, wlen, (long long)Mtot * N_, 1.f, 0});
-    if (bname) rd.push_back({s0 + wlen, x.g(bname), sp.splits, N_, (long long)Mtot * N_, 1.f, 0});
-  };
-  if (p.sg) {
-    slab("SWH", p.sWh, (int)KH + 1, gh, "enc.Wh", (int)KH * gh, "enc.bh");
-  } else if (p.fast_enc) {
-    encoder_fast_reduce(x, rd);
-  } else {
-    slab("SW0", p.sW0, f, h0, "enc.W0", f * h0, nullptr);
-    slab("SW1", p.sW1, h0 + f, h1, "enc.W1", (h0 + f) * h1, nullptr);
-    if (!p.tref) slab("SWH", p.sWh, W + 1, gh, "enc.Wh", W * gh, "enc.bh");
-  }
-  if (p.tref && !p.sg)   // dbh = sum over graphs of dh
-    rd.push_back({x.f("DH"), x.g("enc.bh"), RH, gh, (long long)gh, 1.f, 0});
-  if (!p.fast_enc || p.tref) slab("SWMS", p.sWms, gh + 1, 2 * L, "enc.Wms", gh * 2 * L, "enc.bms");
-  if (!p.fast) {
-    slab("SK1", p.sK1, 5 * dj, C1, "dec.K1", 5 * dj * C1, nullptr);
-    slab("SK2S", p.sK2s, 5 * s1, s2, "dec.K2s", 5 * s1 * s2, nullptr);
-    slab("SK2N", p.sK2n, 5 * n1, n2, "dec.K2n", 5 * n1 * n2, nullptr);
-    slab("SK3S", p.sK3s, 5 * s2, s3, "dec.K3s", 5 * s2 * s3, nullptr);
-  }
-  auto cols = [&](const char* buf, int stride, int off, int len, const char* dst) {
-    rd.push_back({x.f(buf) + off, x.g(dst), nc, len, (long long)stride, 1.f, 0});
-  };
-  if (!p.fast_enc && !p.sg) {
-    cols("PENC1", 2 * W + 2 * h1, 0, W, "enc.bne.gamma");
-    cols("PENC1", 2 * W + 2 * h1, W, W, "enc.bne.beta");
-    cols("PENC1", 2 * W + 2 * h1, 2 * W, h1, "enc.bn1.gamma");
-    cols("PENC1", 2 * W + 2 * h1, 2 * W + h1, h1, "enc.bn1.beta");
-    cols("PENC0", 2 * h0, 0, h0, "enc.bn0.gamma");
-    cols("PENC0", 2 * h0, h0, h0, "enc.bn0.beta");
-  }
-  auto dec = [&](const char* buf, int w, const char* g, const char* b, const char* bias) {
-    cols(buf, 3 * w, 0, w, g);
-    cols(buf, 3 * w, w, w, b);
-    cols(buf, 3 * w, 2 * w, w, bias);
-  };
-  if (p.fast) {
-    decoder_fast_reduce(x, rd);
-  } else {
-    dec("PDEC3", s3, "dec.bn3s.gamma", "dec.bn3s.beta", "dec.b3s");
-    dec("PDEC2S", s2, "dec.bn2s.gamma", "dec.bn2s.beta", "dec.b2s");
-    dec("PDEC2N", n2, "dec.bn2n.gamma", "dec.bn2n.beta", "dec.b2n");
-    dec("PDEC1", C1, "dec.bn1.gamma", "dec.bn1.beta", "dec.b1");
-    const int hs = s3 * sd + sd, hn = n2 * nf + nf;
-    rd.push_back({x.f("PHS"), x.g("dec.Ws"), nh, s3 * sd, (long long)hs, 1.f, 0});
-    rd.push_back({x.f("PHS") + s3 * sd, x.g("dec.bs"), nh, sd, (long long)hs, 1.f, 0});
-    rd.push_back({x.f("PHN"), x.g("dec.Wn"), nh, n2 * nf, (long long)hn, 1.f, 0});
-    rd.push_back({x.f("PHN") + n2 * nf, x.g("dec.bn"), nh, nf, (long long)hn, 1.f, 0});
-  }
+  final_reduce_descs(x, rd);
+  const int nh = head_blocks(R);
   const int n_kl = (p.fast && !p.tref) ? reparam_prep_blocks(p.B, zzt_npad(N))
                    : (p.small_head ? small_head_fwd_blocks(L) : reparam_blocks(RH, L));
   FinalizeArgs fa{x.d("PZZT"), p.B * (zzt_npad(N) / 128) * (c.dtype == SND_BF16 ? p.zzt_ts : 1), x.d("PEDGE"),
@@ -1862,5 +1942,12 @@ extern "C" int snd_train_step(const snd_plan_t* plan, const snd_batch_t* batch,
                   x.d(p.dec_fused ? "PDSSEN" : "PSSEN"), p.dec_fused ? p.dtiles : nh,
                   rp, p.B, N, L, sd, nf, c.beta, c.norm, losses, grads + p.pcount, step_counter,
                   (double)RH * L};
+  const unsigned long long amask = p.fuse_m ? reduce_adam_mask(p, rd, grads) : 0ull;
+  if (amask) {   // + TF1 Adam of the blocks it completes (snd_plan_fuse_adam)
+    SND_CHECK_ARG(step_counter && rd.size() <= 64, "train step: fused Adam needs the step counter");
+    const ReduceAdam ra{grads, const_cast<float*>(params), p.fuse_m, p.fuse_v, p.fuse_lr, p.fuse_b1,
+                        p.fuse_b2, p.fuse_eps, reinterpret_cast<const int*>(x.f("STEPN")), amask};
+    return launch_reduce(rd.data(), (int)rd.size(), x.s, &fa, &ra);
+  }
   return launch_reduce(rd.data(), (int)rd.size(), x.s, &fa);   // + loss terms in one launch
 }

@@ -340,7 +340,11 @@ __global__ void __launch_bounds__(PB_T) tref_proj_bwd_kernel(TrefProjBwdArgs a) 
     float4 s = d[0];
 #pragma unroll
     for (int b = 1; b < B8; ++b) { s.x += d[b].x; s.y += d[b].y; s.z += d[b].z; s.w += d[b].w; }
-    *reinterpret_cast<float4*>(a.dbp + c4) = s;
+    if (a.adam_b.p)
+      adam4(a.adam_b, adam_lrt(a.adam_b), c4, s, ld_nt(a.adam_b.p + c4), ld_nt(a.adam_b.m + c4),
+            ld_nt(a.adam_b.v + c4));
+    else
+      *reinterpret_cast<float4*>(a.dbp + c4) = s;
   }
   __syncthreads();
   const bool fused = a.adam.p != nullptr;
@@ -517,10 +521,12 @@ int tref_proj_bwd_blocks(long long Cp) { return cdiv(Cp, 256); }
 int launch_tref_proj_bwd(const TrefProjBwdArgs& a, hipStream_t s) {
   SND_CHECK_ARG(a.B >= 1 && a.B <= B8 && a.L >= 1 && a.L <= 128 && a.Cp % 4 == 0 && a.Cp > 0,
                 "tref_proj_bwd: B in 1..8, L <= 128, Cp %% 4");
-  SND_CHECK_ARG(a.z && a.wp && a.dz_dec && a.dJd && a.ej && (a.dwp || a.adam.p) && a.dbp && a.slab,
-                "tref_proj_bwd: null operand");
+  SND_CHECK_ARG(a.z && a.wp && a.dz_dec && a.dJd && a.ej && (a.dwp || a.adam.p) && (a.dbp || a.adam_b.p) &&
+                    a.slab, "tref_proj_bwd: null operand");
   SND_CHECK_ARG(!a.adam.p || (a.adam.m && a.adam.v && a.adam.step && a.adam.p == a.wp),
                 "tref_proj_bwd: fused Adam needs m, v, step and p == wp");
+  SND_CHECK_ARG(!a.adam_b.p || (a.adam_b.m && a.adam_b.v && a.adam_b.step),
+                "tref_proj_bwd: fused bias Adam needs m, v, step");
   hipLaunchKernelGGL(tref_proj_bwd_kernel, dim3(tref_proj_bwd_blocks(a.Cp)), dim3(PB_T), 0, s, a);
   SND_LAUNCH_CHECK("tref_proj_bwd_kernel");
   return 0;

@@ -62,6 +62,7 @@ struct TrefProjBwdArgs {
   float* dwp; float* dbp;
   float* slab;
   AdamFuse adam;              // adam.p != null: update Wp in place instead of writing dwp
+  AdamFuse adam_b{};          // adam_b.p != null: update bp in place instead of writing dbp
 };
 int tref_proj_bwd_blocks(long long Cp);
 int launch_tref_proj_bwd(const TrefProjBwdArgs& a, hipStream_t s);

@@ -36,9 +36,12 @@ class OptimizerVAE:
                  epsilon: Optional[float] = None, process_group=None, seed: int = 1234,
                  fuse_adam: Optional[bool] = None, bucketed: Optional[bool] = None,
                  shard_min: Optional[int] = None):
-        """fuse_adam (default: on without a process group): blocks whose gradient one
-        kernel produces complete (graph-latent heads / d_sg_lin1) take their Adam
-        update inside the step (snd_plan_fuse_adam); their gradient is then not written.
+        """fuse_adam (default: on without a process group): Adam runs inside the step
+        (snd_plan_fuse_adam) -- in the weight-gradient streams of the blocks one kernel
+        produces complete (graph-latent heads / d_sg_lin1; their gradient is then not
+        written), and in the final slab reduction for every block it writes complete
+        (gradient written); snd_adam_tf1 updates whatever is left (nothing on the
+        node-latent plans, so the step is one launch shorter).
 
         process_group: data parallel.  Its presence (not its size) selects the
         distributed step: the all-reduce always runs and Adam is never fused, so a
@@ -317,7 +320,8 @@ class OptimizerVAE:
         return int(self.step_counter.item())
 
     def grad_blocks(self):
-        """Flat gradient by block (fused-Adam blocks are updated in the step, not stored).
+        """Flat gradient by block (blocks updated in a weight-gradient stream --
+        snd_plan_block_fused == 1 -- are not stored; the reduction-fused ones are).
 
         With sharded buckets (bucketed exchange) only this rank's chunk of each sharded
         bucket holds the reduced gradient; the rest of such a bucket is this rank's local,

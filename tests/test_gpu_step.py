@@ -135,25 +135,36 @@ def test_train_step_c4_size_vs_oracle(dtype, ltol, gtol):
     assert model.z_mean_sg.shape == (2, cfg.latent)
 
 
+@pytest.mark.parametrize("kind", ["tref", "tscale"])
 @pytest.mark.parametrize("dtype", ["f32", "bf16"])
-def test_fused_adam_matches_separate_update(dtype):
-    """Graph-latent heads / d_sg_lin1 updated inside the step (snd_plan_fuse_adam)
-    give the parameters and Adam moments of the separate snd_adam_tf1 pass."""
+def test_fused_adam_matches_separate_update(dtype, kind):
+    """Adam inside the step (snd_plan_fuse_adam) -- in the graph-latent head / d_sg_lin1
+    weight streams (kind 1) and in the final slab reduction (kind 2, every block of the
+    node-latent plans) -- gives the parameters and Adam moments of the separate
+    snd_adam_tf1 pass, bit for bit over three steps, eager and graph-replayed."""
+    from snd_vae_amd import _lib
     from snd_vae_amd.params import init_blocks
-    cfg = tref(1024, 64)
+    cfg = tref(1024, 64) if kind == "tref" else tscale(2048, 64)
     batch = synthetic_batch(cfg, 2, seed=4)
     p0 = init_blocks(cfg, 0)
     runs = []
     for fuse in (False, True):
         m, o, b = make(cfg, batch, p0, dtype, fuse_adam=fuse)
-        for _ in range(3):
-            o.step(b)
+        o.step(b)
+        o.capture(b)
+        o.replay()
+        o.replay()
         torch.cuda.synchronize()
         runs.append((m, o))
     (m0, o0), (m1, o1) = runs
     assert o1.fused and not o0.fused and o1.global_step == 3
-    for k in ("enc.Wh", "dec.Wp"):
-        assert k in m1.layout.shapes
+    names = list(m1.layout.shapes)
+    kinds = {k: _lib.lib().snd_plan_block_fused(m1.plan, i) for i, k in enumerate(names)}
+    if kind == "tref":
+        assert kinds["enc.Wh"] == 1 and kinds["dec.Wp"] == 1 and kinds["dec.bp"] == 1
+    else:   # every block in the reduction
+        assert set(kinds.values()) == {2}
+    assert o1._adam_ranges == []   # no separate Adam launch at all
     p_a, p_b = m0.blocks(), m1.blocks()
     # same gradients and one shared element update with explicit roundings (snd_common.hpp
     # adam_elem): the fused and the separate update agree bit for bit, over three steps
@@ -161,7 +172,11 @@ def test_fused_adam_matches_separate_update(dtype):
         assert np.array_equal(p_a[k], p_b[k]), (k, np.abs(p_a[k] - p_b[k]).max())
     for a, b in ((o0.m, o1.m), (o0.v, o1.v)):
         assert torch.equal(a, b)
-    assert o0.loss_dict()["cost"] == pytest.approx(o1.loss_dict()["cost"], rel=1e-5)
+    g_a, g_b = o0.grad_blocks(), o1.grad_blocks()
+    for k in names:   # the reduction-fused blocks still store their gradient
+        if kinds[k] != 1:
+            assert np.array_equal(g_a[k], g_b[k]), k
+    assert o0.loss_dict()["cost"] == o1.loss_dict()["cost"]
 
 
 def test_device_rng_same_draw_on_both_engines():

@@ -331,3 +331,31 @@ def test_grad_event_points_and_buckets(lib_built):
         else:
             assert [(b.lo, b.hi, b.point, b.sharded) for b in bk] == [(0, lay.total + 8, 0, False)]
         L.snd_plan_destroy(h)
+
+
+def test_fused_adam_block_kinds(lib_built):
+    """snd_plan_block_fused (ABI 16) after snd_plan_fuse_adam: the node-latent plans
+    update every block inside the final slab reduction (2); the graph-latent plans
+    update d_sg_lin1 (weight and bias) / the head weight in their weight streams (1),
+    and the rest in the reduction: no separate Adam launch on any preset.  Without m / v nothing is fused."""
+    from snd_vae_amd import _lib
+    from snd_vae_amd.model import c_config
+    L = _lib.lib()
+    state = (ctypes.c_float * 4)()
+    for preset in ("C2", "C3", "C4", "C5"):
+        cfg = PRESETS[preset]
+        h = ctypes.c_void_p()
+        cc = c_config(cfg, "bf16")
+        rc = L.snd_plan_create(ctypes.byref(cc), 1 if preset == "C3" else 8, ctypes.byref(h))
+        if rc != 0 and "hipFuncSetAttribute" in _lib.last_error():
+            pytest.skip("HIP runtime unavailable on this host")
+        _lib.check(rc)
+        names = list(flat_layout(cfg).shapes)
+        assert [L.snd_plan_block_fused(h, i) for i in range(len(names))] == [0] * len(names)
+        _lib.check(L.snd_plan_fuse_adam(h, state, state, 1e-3, 0.9, 0.999, 1e-8))
+        kinds = {k: L.snd_plan_block_fused(h, i) for i, k in enumerate(names)}
+        want = {"enc.Wh": 1, "dec.Wp": 1, "dec.bp": 1} if preset == "C4" else {}
+        assert kinds == {k: want.get(k, 2) for k in names}, preset
+        _lib.check(L.snd_plan_fuse_adam(h, None, None, 1e-3, 0.9, 0.999, 1e-8))
+        assert [L.snd_plan_block_fused(h, i) for i in range(len(names))] == [0] * len(names)
+        L.snd_plan_destroy(h)

@@ -6,6 +6,10 @@ export TMPDIR=/tmp
 mkdir -p gpurun_out
 fatal() { case "$1" in 124|134|137|139) return 0;; *) return 1;; esac; }
 run() { local secs=$1; shift; timeout -k 10 "$secs" "$@"; local rc=$?; if fatal $rc; then echo "FATAL $rc: $*"; exit $rc; fi; return $rc; }
+run 400 python -u -m pytest tests/test_gpu_step.py -k "fused_adam or replay" -x -q --timeout 300 > gpurun_out/fadam_tests.log 2>&1
+echo "fused-adam tests rc=$?"; tail -3 gpurun_out/fadam_tests.log
+run 300 python -u bench.py --steps 50 --warmup 5 > gpurun_out/bench_fadam.json 2> gpurun_out/bench_fadam.err
+echo "bench rc=$?"; python -c "import json;j=json.loads(open('gpurun_out/bench_fadam.json').read().splitlines()[-1]);print(j['value'],j['ms_per_step'])"
 SND_LIB_PATH=$PWD/ab/hb64.so run 400 python -u -m pytest tests/test_gpu_step.py -k "backward_head or c2_size or replay" -x -q --timeout 300 > gpurun_out/hb64_tests.log 2>&1
 echo "hb64 tests rc=$?"; tail -2 gpurun_out/hb64_tests.log
 rm -f gpurun_out/ab.jsonl
