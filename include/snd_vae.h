@@ -542,9 +542,13 @@ int snd_debug_set(int flags);
  * 0 = serial, -1 = auto (the default: on for graphs of N >= 2048 with at most 64
  * decoder tiles -- one or two N = 4096 graphs, C3's per-rank batch -- where neither
  * kernel fills the chip).  The
- * side stream is created by the first non-capturing step.  Returns 1 when the option
- * is in effect for this plan, 0 when the plan cannot use it, SND_ERR_ARG for an
- * unknown option. */
+ * side stream is created by the first non-capturing step.
+ * "reduce_adam" (ABI 16): 1 (default) = with snd_plan_fuse_adam set, the blocks the
+ * final reduction completes take their Adam update in that launch (snd_plan_block_fused
+ * 2); 0 = they are left to the caller's snd_adam_tf1 (kind 0).  Set it before
+ * snd_plan_fuse_adam / the optimizer reads the kinds.
+ * Returns 1 when the option is in effect for this plan, 0 when the plan cannot use it,
+ * SND_ERR_ARG for an unknown option. */
 int snd_plan_set_option(snd_plan_t* plan, const char* name, int value);
 
 #ifdef __cplusplus

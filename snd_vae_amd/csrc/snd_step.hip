@@ -131,7 +131,8 @@ struct snd_plan {
   // (reduce_adam_cover, at snd_plan_fuse_adam): with fuse_m their Adam update rides in
   // that launch (ReduceAdam), gradient still written
   std::vector<char> radam;
-  bool reduce_fused(size_t i) const { return fuse_m && i < radam.size() && radam[i]; }
+  bool reduce_adam = true;   // plan option "reduce_adam"
+  bool reduce_fused(size_t i) const { return fuse_m && reduce_adam && i < radam.size() && radam[i]; }
   // 0 separate Adam, 1 fused into a stream, 2 fused into the final reduction
   int fused_kind(size_t i) const {
     return stream_fused(blocks[i].name) ? 1 : (reduce_fused(i) ? 2 : 0);
@@ -546,6 +547,10 @@ extern "C" int snd_plan_set_option(snd_plan_t* p, const char* name, int value) {
     p->conc_dec = value;
     p->zzt_ts = conc_zzt_ts(*p);
     return p->conc_dec_on() ? 1 : 0;
+  }
+  if (!strcmp(name, "reduce_adam")) {
+    p->reduce_adam = value != 0;
+    return p->reduce_adam ? 1 : 0;
   }
   set_error("snd_plan_set_option: unknown option '%s'", name);
   return SND_ERR_ARG;

@@ -359,3 +359,26 @@ def test_fused_adam_block_kinds(lib_built):
         _lib.check(L.snd_plan_fuse_adam(h, None, None, 1e-3, 0.9, 0.999, 1e-8))
         assert [L.snd_plan_block_fused(h, i) for i in range(len(names))] == [0] * len(names)
         L.snd_plan_destroy(h)
+
+
+def test_reduce_adam_option(lib_built):
+    """Plan option "reduce_adam" = 0 leaves the reduction-completed blocks to the caller's
+    snd_adam_tf1 (kind 0); the weight-stream kinds are unaffected."""
+    from snd_vae_amd import _lib
+    from snd_vae_amd.model import c_config
+    L = _lib.lib()
+    state = (ctypes.c_float * 4)()
+    cfg = PRESETS["C4"]
+    h = ctypes.c_void_p()
+    rc = L.snd_plan_create(ctypes.byref(c_config(cfg, "bf16")), 2, ctypes.byref(h))
+    if rc != 0 and "hipFuncSetAttribute" in _lib.last_error():
+        pytest.skip("HIP runtime unavailable on this host")
+    _lib.check(rc)
+    names = list(flat_layout(cfg).shapes)
+    assert L.snd_plan_set_option(h, b"reduce_adam", 0) == 0
+    _lib.check(L.snd_plan_fuse_adam(h, state, state, 1e-3, 0.9, 0.999, 1e-8))
+    kinds = {k: L.snd_plan_block_fused(h, i) for i, k in enumerate(names)}
+    assert kinds == {k: 1 if k in ("enc.Wh", "dec.Wp", "dec.bp") else 0 for k in names}
+    assert L.snd_plan_set_option(h, b"reduce_adam", 1) == 1
+    assert L.snd_plan_block_fused(h, names.index("enc.W0")) == 2
+    L.snd_plan_destroy(h)
