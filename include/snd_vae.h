@@ -490,6 +490,10 @@ int snd_plan_block_fused(const snd_plan_t* plan, int idx);
  * it), 0 when the block's gradient is completed by the step's final reduction
  * (nothing kept), <0 on a bad index. */
 int snd_plan_grad_event(snd_plan_t* plan, int idx, void* event);
+/* ABI 17: the event currently registered for block idx (NULL when none) in *event;
+ * returns the block's completion point as snd_plan_grad_event does.  Lets a host
+ * binding check that a freed optimizer did not unregister a newer one's events. */
+int snd_plan_grad_event_get(const snd_plan_t* plan, int idx, void** event);
 /* Data parallel (ABI 6): the device Philox normals of this plan's head rows start at
  * global head row `head_row_offset` (rank * n_graphs for SND_TREF, rank * n_graphs *
  * n_nodes for SND_TSCALE), so every rank of a sharded global batch draws exactly the

@@ -17,7 +17,7 @@ c_int, c_ll, c_float, c_size, c_ull = C.c_int, C.c_longlong, C.c_float, C.c_size
 vp = C.c_void_p
 
 
-ABI_VERSION = 16
+ABI_VERSION = 17
 GEN_MODES = {"sample": 0, "mean": 1, "prior": 2, "given": 3}
 TOPOLOGY = {"tscale": 0, "tref": 1, "sgjoint": 2}
 
@@ -137,6 +137,7 @@ _SIGS = {
     "snd_plan_fuse_adam": (c_int, [vp, vp, vp, c_float, c_float, c_float, c_float]),
     "snd_plan_block_fused": (c_int, [vp, c_int]),
     "snd_plan_grad_event": (c_int, [vp, c_int, vp]),
+    "snd_plan_grad_event_get": (c_int, [vp, c_int, C.POINTER(vp)]),
     "snd_plan_set_rng_offset": (c_int, [vp, c_ll]),
     "snd_plan_buffer": (c_int, [vp, C.c_char_p, C.POINTER(c_ll), C.POINTER(c_ll)]),
     "snd_train_step": (c_int, [vp, C.POINTER(Batch), vp, vp, vp, vp, c_ull, vp, vp, vp]),

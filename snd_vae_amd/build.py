@@ -52,22 +52,61 @@ def source_digest() -> str:
     return _digest(srcs + _headers(), FLAGS + [ARCH])
 
 
+# the compiler's per-kernel resource remarks (no effect on code generation): every
+# kernel's VGPRs, spills and scratch are recorded beside its object and in BUILD_INFO,
+# so a register spill in a shipped kernel is visible without a GPU (tests/test_host.py;
+# round 5: a 72-VGPR spill in dec_bwd_kernel cost 26 us per C2 step unnoticed)
+REMARKS = ["-Rpass-analysis=kernel-resource-usage"]
+_RES_KEYS = {"VGPRs": "vgprs", "AGPRs": "agprs", "VGPRs Spill": "vgpr_spill",
+             "SGPRs Spill": "sgpr_spill", "ScratchSize [bytes/lane]": "scratch",
+             "Occupancy [waves/SIMD]": "occupancy", "LDS Size [bytes/block]": "lds"}
+
+
+def parse_resources(text: str) -> dict:
+    """{mangled kernel name: {vgprs, vgpr_spill, scratch, ...}} from hipcc's
+    kernel-resource-usage remarks."""
+    import re
+    out, name = {}, None
+    for line in text.splitlines():
+        m = re.search(r"remark: Function Name: (\S+)", line)
+        if m:
+            name = m.group(1)
+            out[name] = {}
+            continue
+        m = re.search(r"remark:\s+([A-Za-z ]+(?:\[[^\]]*\])?): (\d+)", line)
+        if m and name and m.group(1).strip() in _RES_KEYS:
+            out[name][_RES_KEYS[m.group(1).strip()]] = int(m.group(2))
+    return out
+
+
 def _compile(src):
     """Staleness by content: an object is rebuilt when the hash of its source, the
     headers and the flags differs from the one recorded beside it (mtimes do not
     survive a snapshot copy to the GPU box)."""
     obj = os.path.join(BUILD, os.path.basename(src) + ".o")
     want = _digest([src] + _headers(), FLAGS + [ARCH])
-    stamp = obj + ".sha256"
-    if os.path.exists(obj) and os.path.exists(stamp) and open(stamp).read() == want:
+    stamp, res = obj + ".sha256", obj + ".res.json"
+    if (os.path.exists(obj) and os.path.exists(stamp) and os.path.exists(res)
+            and open(stamp).read() == want):
         return obj, False
-    cmd = [HIPCC] + FLAGS + ["-c", src, "-o", obj]
+    cmd = [HIPCC] + FLAGS + REMARKS + ["-c", src, "-o", obj]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"hipcc failed for {src}:\n{r.stdout}\n{r.stderr}")
+    with open(res, "w") as f:
+        json.dump(parse_resources(r.stderr), f)
     with open(stamp, "w") as f:
         f.write(want)
     return obj, True
+
+
+def kernel_resources() -> dict:
+    """Every kernel's resource record of the current objects (see REMARKS)."""
+    out = {}
+    for p in sorted(glob.glob(os.path.join(BUILD, "*.res.json"))):
+        with open(p) as f:
+            out.update(json.load(f))
+    return out
 
 
 def build(force: bool = False, verbose: bool = False) -> str:
@@ -91,10 +130,13 @@ def build(force: bool = False, verbose: bool = False) -> str:
             raise RuntimeError(f"link failed:\n{r.stdout}\n{r.stderr}")
         with open(LIB, "rb") as f:
             lib_sha = hashlib.sha256(f.read()).hexdigest()
+        spills = {k: {"vgpr_spill": v.get("vgpr_spill", 0), "scratch": v.get("scratch", 0)}
+                  for k, v in kernel_resources().items()
+                  if v.get("vgpr_spill", 0) or v.get("scratch", 0)}
         with open(BUILD_INFO, "w") as f:
             json.dump({"source_sha256": digest, "lib_sha256": lib_sha,
                        "objects_recompiled": recompiled, "host": platform.node(),
-                       "time": time.strftime("%Y-%m-%dT%H:%M:%S")}, f)
+                       "time": time.strftime("%Y-%m-%dT%H:%M:%S"), "spills": spills}, f)
     if verbose:
         print(LIB)
     return LIB

@@ -162,6 +162,10 @@ __device__ __forceinline__ void conv_phase_t(const __bf16* xs, int kpx, const __
   const int cg = w % ncg, k0 = w / ncg;
   if (k0 >= wpc) return;
   const int nb0 = cg * NBH;
+  // callers pass the RUNTIME bits (a.dbg, not kdbg(a.dbg)): the scalar branch around the
+  // MFMA block bounds the scheduling region.  With the bit folded to a constant the
+  // compiler hoisted the epilogue operands over the MFMAs and dec_bwd_kernel spilled
+  // 72 VGPRs (22.6 -> 49.1 us, the round-4 C2 regression; tools/gpu_bisect.sh)
   const bool mm = !(dbg & 4);
   const int kcs = KCS ? KCS : kpw >> 5;
   const int wsw = dswz(li, kpw);
@@ -419,7 +423,7 @@ __global__ void __launch_bounds__(DT) dec_fwd_kernel(DecChainFwdArgs a) {
           *reinterpret_cast<bf16x4*>(a.u1 + (long long)gr * a.ldy1 + n0) = ub;
         }
       }
-    }, kdbg(a.dbg));
+    }, a.dbg);
   }
   __syncthreads();
   if (stamp) ts[2] = __builtin_amdgcn_s_memrealtime();
@@ -458,7 +462,7 @@ __global__ void __launch_bounds__(DT) dec_fwd_kernel(DecChainFwdArgs a) {
             *reinterpret_cast<f32x4*>(&y2n[(gr - tl.r0) * L.ldY2n + (n0 - a.m2.offb)]) = yv;
         }
       }
-    }, kdbg(a.dbg));
+    }, a.dbg);
   }
   __syncthreads();
   if (stamp) ts[4] = __builtin_amdgcn_s_memrealtime();
@@ -481,7 +485,7 @@ __global__ void __launch_bounds__(DT) dec_fwd_kernel(DecChainFwdArgs a) {
       }
       *reinterpret_cast<float4*>(u3 + orow * 16 + n0) = make_float4(o[0], o[1], o[2], o[3]);
       *reinterpret_cast<float4*>(y3 + orow * 16 + n0) = make_float4(yv[0], yv[1], yv[2], yv[3]);
-    }, kdbg(a.dbg));
+    }, a.dbg);
   }
   __syncthreads();
   if (stamp) ts[6] = __builtin_amdgcn_s_memrealtime();
@@ -652,7 +656,7 @@ __global__ void __launch_bounds__(DT) dec_bwd_kernel(DecChainBwdArgs a) {
 #pragma unroll
           for (int e = 0; e < 4; ++e) if (n0 + e < N) dp[e] = ob[e];
       }
-    }, kdbg(a.dbg));
+    }, a.dbg);
     if (w / ncg < wpc) colpart_flush<1>(q, slots, a.k3t.np, nb0, nbc, w / ncg);
     __syncthreads();
     for (int i = tid; i < 3 * N; i += DT) {
@@ -708,7 +712,7 @@ __global__ void __launch_bounds__(DT) dec_bwd_kernel(DecChainBwdArgs a) {
         *reinterpret_cast<bf16x4*>(img_at(d1, orow, kpo, n0)) = ob;
         if (mine && !(kdbg(a.dbg) & 8)) *reinterpret_cast<bf16x4*>(a.dy1 + (long long)gr * a.lddy1 + n0) = ob;
       }
-    }, kdbg(a.dbg));
+    }, a.dbg);
     __syncthreads();   // slots: the conv3^T partials were consumed above
     if (w / ncg < wpc) colpart_flush<2>(q, slots, a.k2t.np, nb0, nbc, w / ncg);
     __syncthreads();
@@ -738,7 +742,7 @@ __global__ void __launch_bounds__(DT) dec_bwd_kernel(DecChainBwdArgs a) {
         *reinterpret_cast<float4*>(a.dz + gr * a.lddz + n0) =
             make_float4(acc[i][0], acc[i][1], acc[i][2], acc[i][3]);
       }
-    }, kdbg(a.dbg));
+    }, a.dbg);
   }
   if (stamp) {
     ts[6] = __builtin_amdgcn_s_memrealtime();
@@ -776,9 +780,7 @@ bool dec_fused_supported(int dj, const ColMap& m1, const ColMap& m2, int s3, int
   return 16 % ((k2t.np / 16 + 1) / 2) == 0 && 16 % (k3t.np / 16) == 0;
 }
 
-int dec_init_attributes() {
-  static int done = 0;
-  if (done) return 0;
+static int dec_init_attributes_once() {
   if (hipFuncSetAttribute(reinterpret_cast<const void*>(dec_fwd_kernel),
                           hipFuncAttributeMaxDynamicSharedMemorySize, kDynLds) != hipSuccess ||
       hipFuncSetAttribute(reinterpret_cast<const void*>(dec_bwd_kernel),
@@ -786,8 +788,13 @@ int dec_init_attributes() {
     set_error("dec: hipFuncSetAttribute failed");
     return SND_ERR_HIP;
   }
-  done = 1;
   return 0;
+}
+
+// once per process, thread-safe (a function-local static's initialiser runs exactly once)
+int dec_init_attributes() {
+  static const int rc = dec_init_attributes_once();
+  return rc;
 }
 
 int launch_dec_chain_fwd(const DecChainFwdArgs& a, hipStream_t s) {

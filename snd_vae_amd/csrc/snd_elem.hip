@@ -46,7 +46,7 @@ __global__ void __launch_bounds__(256) reparam_fwd_kernel(ReparamFwdArgs a) {
       a.z[i] = zv;
       if (a.zb) a.zb[(long long)r * a.ldzb + c] = (__bf16)zv;
       if (a.eps_out) a.eps_out[i] = eps;
-      kl += (double)(1.f + 2.f * ls - mu * mu - es * es);   // optimizer.py:193
+      kl += (double)kl_elem(ls, mu);   // optimizer.py:193
     }
   }
   const double t = block_sum(kl);
@@ -106,7 +106,7 @@ __global__ void __launch_bounds__(256) small_head_fwd_kernel(SmallHeadFwdArgs a)
     const float es = __expf(ls);
     a.z[i] = mu + eps * es;                // model.py:159
     if (a.eps_out) a.eps_out[i] = eps;
-    kl = (double)(1.f + 2.f * ls - mu * mu - es * es);   // optimizer.py:193
+    kl = (double)kl_elem(ls, mu);   // optimizer.py:193
   }
   const double s = block_sum(kl);
   if (t == 0) a.kl_part[blockIdx.x] = s;

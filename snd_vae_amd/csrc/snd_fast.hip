@@ -959,12 +959,10 @@ int launch_wgrad(const WgArgs& a, hipStream_t s) {
   }
 }
 
-static int g_dbg = 0;
+static thread_local int g_dbg = 0;   // per calling thread (snd_debug_set): no process-wide mutable state
 int debug_flags() { return g_dbg; }
 
-int fast_init_attributes() {
-  static int done = 0;
-  if (done) return 0;
+static int fast_init_attributes_once() {
 #define SND_ATTR(K)                                                                       \
   if (hipFuncSetAttribute(reinterpret_cast<const void*>(K),                               \
                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMaxDynLds) != \
@@ -985,8 +983,13 @@ int fast_init_attributes() {
     set_error("hipFuncSetAttribute(wgrad_multi_kernel) failed");
     return SND_ERR_HIP;
   }
-  done = 1;
   return 0;
+}
+
+// once per process, thread-safe (a function-local static's initialiser runs exactly once)
+int fast_init_attributes() {
+  static const int rc = fast_init_attributes_once();
+  return rc;
 }
 
 }  // namespace snd

@@ -622,7 +622,7 @@ __global__ void __launch_bounds__(NT) reparam_prep_kernel(ReparamPrepArgs a) {
         for (int t = 0; t < 4; ++t) {
           const float es = __expf(s[t]);
           z[t] = mu[t] + e[t] * es;                                      // model.py:159
-          kl += (double)(1.f + 2.f * s[t] - mu[t] * mu[t] - es * es);    // optimizer.py:193
+          kl += (double)kl_elem(s[t], mu[t]);    // optimizer.py:193
         }
         *reinterpret_cast<float4*>(a.z + i) = make_float4(z[0], z[1], z[2], z[3]);
         *reinterpret_cast<float4*>(a.eps_out + i) = ep;

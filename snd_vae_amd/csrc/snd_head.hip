@@ -262,7 +262,7 @@ __global__ void __launch_bounds__(HR * 8) head_fwd_kernel(HeadFwdArgs a) {
         for (int t = 0; t < 4; ++t) {
           const float es = __expf(s[t]);
           z4[t] = mu[t] + e[t] * es;                                          // model.py:159
-          kq += (double)(1.f + 2.f * s[t] - mu[t] * mu[t] - es * es);        // optimizer.py:193
+          kq += (double)kl_elem(s[t], mu[t]);        // optimizer.py:193
         }
 #pragma unroll
         for (int h = 0; h < HR / 64; ++h) kl[h] += (zr >> 6) == h ? kq : 0.0;
@@ -882,9 +882,7 @@ int launch_head_fwd(const HeadFwdArgs& a, hipStream_t s) {
   return (a.dbg & 131072) ? head_fwd_dispatch<128>(a, s) : head_fwd_dispatch<kHeadRows>(a, s);
 }
 
-int head_init_attributes() {
-  static int done = 0;
-  if (done) return 0;
+static int head_init_attributes_once() {
   const void* ks[] = {reinterpret_cast<const void*>(head_fwd_kernel<64, 1, 2>),
                       reinterpret_cast<const void*>(head_fwd_kernel<64, 1, 4>),
                       reinterpret_cast<const void*>(head_fwd_kernel<64, 2, 2>),
@@ -925,8 +923,13 @@ int head_init_attributes() {
       return SND_ERR_HIP;
     }
   }
-  done = 1;
   return 0;
+}
+
+// once per process, thread-safe (a function-local static's initialiser runs exactly once)
+int head_init_attributes() {
+  static const int rc = head_init_attributes_once();
+  return rc;
 }
 
 }  // namespace snd

@@ -151,7 +151,9 @@ struct snd_plan {
   // or two N = 4096 graphs; C3's one-graph step 0.1704 -> 0.1626 ms,
   // profiles/r04_bench_strong_conc.json.  Small graphs stay serial: launch-bound)
   int conc_dec = -1;
-  int zzt_ts = 1;
+  int zzt_ts = 1;        // zz^T column splits of a serial step
+  int zzt_ts_conc = 1;   // ... of a step whose decoder runs beside zz^T (cdec)
+  mutable int last_zts = 1;   // the split count the last snd_train_step used (snd_plan_launch)
   bool conc_dec_on() const {
     return (conc_dec > 0 || (conc_dec < 0 && dtiles <= 64 && N >= 2048)) && fast && dec_fused && !tref;
   }
@@ -185,15 +187,19 @@ struct snd_plan {
 };
 
 extern "C" const char* snd_last_error(void) { return g_err; }
-extern "C" int snd_abi_version(void) { return 16; }
+extern "C" int snd_abi_version(void) { return 17; }
 
 // zz^T column splits with the concurrent decoder on: zz^T keeps the CUs the decoder's
-// tiles do not take (one 1024-thread workgroup per CU for either kernel)
-static int conc_zzt_ts(const snd_plan& p) {
-  const int full = zzt_tsplit(p.B, p.N, p.c.dtype);
-  if (!p.conc_dec_on()) return full;
-  const int wgs = p.B * (zzt_npad(p.N) / 128);
-  return std::max(1, std::min(full, (256 - p.dtiles) / wgs));
+// tiles do not take (one 1024-thread workgroup per CU for either kernel).  A step uses
+// this count only when its decoder actually runs on the side stream (cdec); a serial
+// step -- a capture before any eager step, or no side stream -- keeps the full count.
+static void set_zzt_splits(snd_plan& p) {
+  p.zzt_ts = zzt_tsplit(p.B, p.N, p.c.dtype);
+  p.zzt_ts_conc = p.zzt_ts;
+  if (p.conc_dec_on()) {
+    const int wgs = p.B * (zzt_npad(p.N) / 128);
+    p.zzt_ts_conc = std::max(1, std::min(p.zzt_ts, (device_cu_count() - p.dtiles) / wgs));
+  }
 }
 
 extern "C" int snd_plan_create(const snd_config_t* cfg, int n_graphs, snd_plan_t** out) {
@@ -523,7 +529,7 @@ extern "C" int snd_plan_create(const snd_config_t* cfg, int n_graphs, snd_plan_t
   // GraphConvolution 0, XW1 and the packed weight images in one launch (debug bit 1048576:
   // pack + gcn0 + a row-engine launch)
   p->front_fused = p->fast_enc && !(dbg & 1048576) && front_supported(c.f_in, c.h0, c.h1, p->pw1f.kp, p->pw1f.np);
-  p->zzt_ts = conc_zzt_ts(*p);
+  set_zzt_splits(*p);
   *out = p;
   return 0;
 }
@@ -545,10 +551,15 @@ extern "C" int snd_plan_set_option(snd_plan_t* p, const char* name, int value) {
   SND_CHECK_ARG(p && name, "snd_plan_set_option: bad args");
   if (!strcmp(name, "conc_decoder")) {
     p->conc_dec = value;
-    p->zzt_ts = conc_zzt_ts(*p);
+    set_zzt_splits(*p);
     return p->conc_dec_on() ? 1 : 0;
   }
   if (!strcmp(name, "reduce_adam")) {
+    // the block kinds are fixed while an update is fused: a caller that cached them
+    // (OptimizerVAE._adam_ranges) would skip or double a block's update
+    SND_CHECK_ARG(!p->fuse_m || (value != 0) == p->reduce_adam,
+                  "snd_plan_set_option: reduce_adam cannot change while Adam is fused "
+                  "(snd_plan_fuse_adam(plan, NULL, NULL, ...) first)");
     p->reduce_adam = value != 0;
     return p->reduce_adam ? 1 : 0;
   }
@@ -580,6 +591,12 @@ extern "C" int snd_plan_grad_event(snd_plan_t* p, int idx, void* event) {
   if (pt == 2) p->ev_head = (hipEvent_t)event;
   return pt;
 }
+extern "C" int snd_plan_grad_event_get(const snd_plan_t* p, int idx, void** event) {
+  SND_CHECK_ARG(p && event && idx >= 0 && idx < (int)p->blocks.size(), "snd_plan_grad_event_get: bad args");
+  const int pt = p->grad_point(p->blocks[idx].name);
+  *event = pt == 1 ? (void*)p->ev_proj : pt == 2 ? (void*)p->ev_head : nullptr;
+  return pt;
+}
 extern "C" int snd_plan_block_fused(const snd_plan_t* p, int idx) {
   SND_CHECK_ARG(p && idx >= 0 && idx < (int)p->blocks.size(), "snd_plan_block_fused: bad index");
   return p->fused_kind((size_t)idx);
@@ -608,6 +625,7 @@ struct Ctx {
   hipStream_t side = nullptr;   // null: single-stream
   int* nev = nullptr;           // next free event of p->ev
   std::vector<WgArgs>* wq = nullptr;   // deferred weight gradients (one launch at the end)
+  int zts = 1;                  // zz^T column splits of this step (launch, split sums, finalize)
   float* f(const char* n) const { return (float*)(ws + p->buf(n)); }
   double* d(const char* n) const { return (double*)(ws + p->buf(n)); }
   const float* w(const char* n) const { return P + p->blk(n); }
@@ -1038,7 +1056,7 @@ int head_bwd_fused(const Ctx& x, const snd_batch_t* batch, float adj_scale, floa
     a.rowptr = batch->rowptr; a.colidx = batch->colidx; a.R = R;
     a.zb = bf("ZB"); a.L = L; a.pos_weight = c.pos_weight; a.edge_part = x.d("PEDGE");
     a.ms = x.f("MS"); a.eps = x.f("EPS"); a.dz_dec = x.f("DZDEC"); a.dJd = x.f("DJD");
-    a.dJd_extra = x.f("DJDX"); a.nextra = p.zzt_ts - 1;   // deferred split sum
+    a.dJd_extra = x.f("DJDX"); a.nextra = x.zts - 1;   // deferred split sum
     a.adj_scale = adj_scale; a.kl_scale = kl_scale;
     a.dms = bf("FDMS"); a.bms_part = x.f("PHBMS");
     a.wmsb_img = reinterpret_cast<const __bf16*>(x.ws + p.pwmsb.off); a.kp1 = p.pwmsb.kp; a.np1 = p.pwmsb.np;
@@ -1068,7 +1086,7 @@ int encoder_fast_bwd(const Ctx& x, const snd_batch_t* batch, float adj_scale, fl
   {
     ReparamBwdFastArgs a{x.f("MS"), 2 * L, R, L, x.f("EPS"), x.f("DZDEC"), x.f("DJD"), x.f("EJ"),
                          adj_scale, kl_scale, bf("FDMS"), 2 * L, x.f("PFBMS")};
-    a.dJd_extra = x.f("DJDX"); a.nextra = p.zzt_ts - 1;   // deferred split sum
+    a.dJd_extra = x.f("DJDX"); a.nextra = x.zts - 1;   // deferred split sum
     SND_TRY(launch_reparam_bwd_fast(a, x.s));
   }
   SND_TRY(fork(x));
@@ -1501,6 +1519,7 @@ extern "C" int snd_plan_launch(const snd_plan_t* plan, const snd_batch_t* batch,
   if (!strcmp(kernel, "head_bwd")) {   // fused backward head (the step's scales)
     SND_CHECK_ARG(p.head_bwd && p.last_params, "snd_plan_launch: head_bwd needs a fused-head step first");
     Ctx x{&p, ws, p.last_params, p.last_grads, s};
+    x.zts = p.last_zts;
     const double pairs = (double)p.B * p.N * (double)p.N;
     return head_bwd_fused(x, batch, (float)(2.0 * (double)p.c.norm / pairs),
                           (float)((double)p.c.beta / ((double)p.RH * p.c.latent)));
@@ -1666,6 +1685,8 @@ extern "C" int snd_train_step(const snd_plan_t* plan, const snd_batch_t* batch,
     cdec = p.conc == 1;
     if (cdec) x.nev = &nev;
   }
+  x.zts = cdec ? p.zzt_ts_conc : p.zzt_ts;
+  p.last_zts = x.zts;
   // single stream: every fast-path weight gradient waits for one launch before the
   // reduction (debug bit 4096: one launch per weight, as before)
   std::vector<WgArgs> wq;
@@ -1770,7 +1791,7 @@ extern "C" int snd_train_step(const snd_plan_t* plan, const snd_batch_t* batch,
     if (!p.fast) SND_TRY(launch_zzt_prep(x.f("Z"), p.B, N, dj, c.dtype, stg, x.s));
     ZztArgs za{stg.jrow, stg.jt, N, zzt_npad(N), p.B, dj, x.f("DJD"), x.d("PZZT"), stg.colpart, 0,
                x.f("DJDX")};
-    za.tsplit = p.zzt_ts;
+    za.tsplit = x.zts;
     // concurrent decoder: the fused decoder on the side stream beside zz^T (forked after
     // the staging that both read, joined before the backward head that reads both)
     if (cdec) {
@@ -1941,7 +1962,7 @@ extern "C" int snd_train_step(const snd_plan_t* plan, const snd_batch_t* batch,
   const int nh = head_blocks(R);
   const int n_kl = (p.fast && !p.tref) ? reparam_prep_blocks(p.B, zzt_npad(N))
                    : (p.small_head ? small_head_fwd_blocks(L) : reparam_blocks(RH, L));
-  FinalizeArgs fa{x.d("PZZT"), p.B * (zzt_npad(N) / 128) * (c.dtype == SND_BF16 ? p.zzt_ts : 1), x.d("PEDGE"),
+  FinalizeArgs fa{x.d("PZZT"), p.B * (zzt_npad(N) / 128) * (c.dtype == SND_BF16 ? x.zts : 1), x.d("PEDGE"),
                   p.head_bwd ? head_tiles(R) : (p.fast ? edge_bf16_blocks(R) : edge_blocks(R, dj)),
                   x.d("PKL"), n_kl, x.d(p.dec_fused ? "PDSSES" : "PSSES"),
                   x.d(p.dec_fused ? "PDSSEN" : "PSSEN"), p.dec_fused ? p.dtiles : nh,

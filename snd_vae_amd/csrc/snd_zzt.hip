@@ -1195,11 +1195,11 @@ int zzt_tsplit(int ngraphs, int n, int dtype) {
   return zzt_tsplit_blocks(ngraphs * (zzt_npad(n) / ROWS), n, dtype);
 }
 int zzt_tsplit_blocks(int wgs, int n, int dtype) {
-  const int ntiles = zzt_npad(n) / TJ2;
-  if (dtype != SND_BF16 || wgs >= 256) return 1;
+  const int ntiles = zzt_npad(n) / TJ2, ncu = device_cu_count();
+  if (dtype != SND_BF16 || wgs >= ncu) return 1;
   // up to 8 column splits: one C2 graph (32 row blocks) then fills 256 CUs (B = 1 step
   // 0.1546 -> 0.1512 ms against 4 splits; B = 2 unchanged at 4)
-  return std::max(1, std::min({cdiv(256, wgs), 8, ntiles}));
+  return std::max(1, std::min({cdiv(ncu, wgs), 8, ntiles}));
 }
 int zzt_dense_blocks(int ngraphs, int n, int dtype) {
   return ngraphs * (zzt_npad(n) / ROWS) * zzt_tsplit(ngraphs, n, dtype);

@@ -112,7 +112,12 @@ class OptimizerVAE:
         self.buckets = []
         self._events = {}
         # the plan records raw hipEvent_t pointers for the early buckets: drop whatever a
-        # previous optimizer of this plan registered (its torch events may be freed)
+        # previous optimizer of this plan registered (its torch events may be freed), and
+        # take ownership, so that the previous optimizer's close() / __del__ (which may
+        # run after this constructor: `opt = OptimizerVAE(model, ...)` rebinding) leaves
+        # this optimizer's events alone
+        self._owner = object()
+        model._grad_event_owner = self._owner
         self._unregister_events()
         if self.bucketed:
             self._init_buckets(shard_min)
@@ -127,9 +132,12 @@ class OptimizerVAE:
 
     def close(self):
         """Unregister this optimizer's completion events from the plan (idempotent);
-        called by __del__, so a freed optimizer never leaves dangling events behind."""
+        called by __del__, so a freed optimizer never leaves dangling events behind.
+        Only while this optimizer still owns the plan's events: a newer optimizer of the
+        same model has replaced them with its own."""
         if getattr(self, "_events", None):
-            self._unregister_events()
+            if getattr(self.model, "_grad_event_owner", None) is self._owner:
+                self._unregister_events()
             self._events = {}
 
     def __del__(self):
@@ -172,6 +180,13 @@ class OptimizerVAE:
     # ------------------------------------------------------------------ step
     def forward_backward(self, batch: DeviceBatch, eps: Optional[torch.Tensor] = None,
                          stream=None):
+        """snd_train_step: forward, backward, gradients into `self.grads`.
+
+        With the update fused (`self.fused`, the single-device default) this call ALSO
+        applies TF1 Adam in place to every block the plan reports fused
+        (snd_plan_block_fused != 0: on C2/C3/C5 all of them, inside the final reduction)
+        and advances the step counter; `apply()` then updates only the rest.  A caller
+        that wants gradients without an update builds the optimizer with fuse_adam=False."""
         m = self.model
         self._batch_c = batch.c_struct()
         _lib.check(_lib.lib().snd_train_step(

@@ -1,0 +1,136 @@
+"""C2, the headline, at the benchmarked shape with the SHIPPED update path, step by step.
+
+bench.py's C2 step: tscale(4096, 64), B = 8 graphs of synthetic_batch seed 1000, the
+weights of init seed 0, and TF1 Adam fused into the step's final slab reduction
+(snd_plan_fuse_adam + plan option "reduce_adam" on: every block of the node-latent plan
+is updated inside `reduce_kernel`, ABI 16) -- exactly what the bench times.  Reference:
+`model.py:104-161`, `model_joint.py:112-145`, `optimizer.py:125,135-197`,
+`main.py:315-331`.
+
+Every step t starts the float64 oracle (forward_backward with row_chunk + adam_tf1) from
+the parameters and Adam moments the GPU held before step t, with the same injected eps,
+and compares after step t:
+* the loss terms (f32 1e-5 relative: the north_star's ELBO bar; bf16 2e-2);
+* the gradient blocks the step wrote, against the oracle's (f32 2e-4 / bf16 1e-1 of
+  max-abs; the bf16 gap to the float64 oracle is the bf16 operands' rounding and is
+  parity-unpinned against TF, which has no bf16 path);
+* the fused update against the GPU's OWN gradient, in float64: m, v and the parameters
+  after the step must equal TF1 Adam applied to the GPU gradient up to fp32 rounding
+  (m, v 1e-6 relative per element + an absolute floor of 1e-6 of the block's max, the
+  parameters within 1e-3 lr + 4 fp32 ulps).  This pins the reduction-fused Adam tightly
+  in BOTH precisions: a wrong bias correction, step index, moment order or a skipped /
+  doubled block fails here whatever the gradient's precision;
+* fp32 only: the parameters against the oracle's update in units of lr (Adam moves every
+  element by ~lr, so a sign-ambiguous near-zero gradient moves it up to 2 lr the other
+  way): all but 1e-4 of a block's elements within 0.05 lr + 4 ulps.
+Measured errors go to gpurun_out/parity_errors.jsonl.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import ref_numpy as R
+from snd_vae_amd.config import tscale
+from snd_vae_amd.data import synthetic_batch
+from snd_vae_amd.params import init_blocks
+
+pytestmark = pytest.mark.gpu
+TERMS = ("cost", "spatial_cost", "adj_cost", "node_cost", "kl")
+STEPS = 3
+LOSS_TOL = {"f32": 1e-5, "bf16": 2e-2}
+GRAD_TOL = {"f32": 2e-4, "bf16": 1e-1}
+EPS32 = float(np.finfo(np.float32).eps)
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu(lib_built):
+    if not torch.cuda.is_available():
+        pytest.fail("GPU tests need a ROCm device")
+
+
+def block_err(g, ref):
+    return float(np.abs(g - ref).max() / max(np.abs(ref).max(), 1e-30))
+
+
+def adam_from(p, g, m, v, t, lr, b1, b2, eps):
+    """TF1 Adam (optimizer.py:125 -> tf.train.AdamOptimizer) in float64 on one block."""
+    m2 = b1 * m + (1 - b1) * g
+    v2 = b2 * v + (1 - b2) * g * g
+    lr_t = lr * np.sqrt(1 - b2 ** t) / (1 - b1 ** t)
+    return p - lr_t * m2 / (np.sqrt(v2) + eps), m2, v2
+
+
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+def test_c2_bench_batch_steps_vs_oracle(dtype):
+    from snd_vae_amd.model import DeviceBatch, SGCNModelVAE
+    from snd_vae_amd.optimizer import OptimizerVAE
+    cfg = tscale(4096, 64)
+    B = 8
+    batch = synthetic_batch(cfg, B, seed=1000)          # bench.py run_workload, rank 0
+    adj = [batch.sparse_adj(b) for b in range(B)]
+    p0 = {k: v.astype(np.float32).astype(np.float64) for k, v in init_blocks(cfg, 0).items()}
+    rng = np.random.default_rng(9)
+    eps = [rng.standard_normal((B * cfg.n_nodes, cfg.latent)).astype(np.float32) for _ in range(STEPS)]
+
+    model = SGCNModelVAE(cfg, B, dtype=dtype, blocks=p0)
+    opt = OptimizerVAE(model)                            # bench.py: fused by default
+    assert opt.fused and not opt._adam_ranges, "every C2 block must be reduce-fused"
+    db = DeviceBatch(batch)
+    lr, b1, b2, ae = cfg.learning_rate, cfg.adam_beta1, cfg.adam_beta2, cfg.adam_eps
+    fails = []
+    for t in range(1, STEPS + 1):
+        p = {k: np.asarray(v, np.float64) for k, v in model.blocks().items()}
+        m, v = opt.state_blocks()
+        m = {k: np.asarray(x, np.float64) for k, x in m.items()}
+        v = {k: np.asarray(x, np.float64) for k, x in v.items()}
+        opt.step(db, torch.from_numpy(eps[t - 1]).cuda())
+        torch.cuda.synchronize()
+        rl, rg, _ = R.forward_backward(p, adj, batch.features, batch.feature_truth,
+                                       batch.spatial_truth, eps[t - 1].astype(np.float64),
+                                       cfg, row_chunk=1024)
+        pr = {k: x.copy() for k, x in p.items()}
+        mr = {k: x.copy() for k, x in m.items()}
+        vr = {k: x.copy() for k, x in v.items()}
+        R.adam_tf1(pr, rg, mr, vr, t, lr, b1, b2, ae)
+        got = opt.loss_dict()
+        gg = {k: np.asarray(x, np.float64) for k, x in opt.grad_blocks().items()}
+        gp = {k: np.asarray(x, np.float64) for k, x in model.blocks().items()}
+        gm, gv = opt.state_blocks()
+        gm = {k: np.asarray(x, np.float64) for k, x in gm.items()}
+        gv = {k: np.asarray(x, np.float64) for k, x in gv.items()}
+        rec = {"test": "c2_bench_batch_steps", "dtype": dtype, "step": t, "loss_rel": {},
+               "grad_err": {}, "self_adam_err": {}, "param_off_frac": {}}
+        for k in TERMS:
+            e = abs(got[k] - rl[k]) / max(abs(rl[k]), 1e-30)
+            rec["loss_rel"][k] = e
+            if e > LOSS_TOL[dtype]:
+                fails.append((t, "loss", k, got[k], rl[k]))
+        for k in p:
+            e = block_err(gg[k], rg[k])
+            rec["grad_err"][k] = e
+            if e > GRAD_TOL[dtype]:
+                fails.append((t, "grad", k, e))
+            # the fused update vs TF1 Adam on the GPU's own gradient (tight, any dtype)
+            sp, sm, sv = adam_from(p[k], gg[k], m[k], v[k], t, lr, b1, b2, ae)
+            em = float(np.max(np.abs(gm[k] - sm) / (1e-6 * np.abs(sm) + 1e-6 * np.abs(sm).max() + 1e-30)))
+            ev = float(np.max(np.abs(gv[k] - sv) / (1e-6 * np.abs(sv) + 1e-6 * np.abs(sv).max() + 1e-30)))
+            dp = np.abs(gp[k] - sp)
+            ep = float(np.max(dp / (1e-3 * lr + 4 * EPS32 * np.abs(p[k]))))
+            rec["self_adam_err"][k] = [em, ev, ep]
+            if em > 1 or ev > 1 or ep > 1:
+                fails.append((t, "self_adam", k, em, ev, ep))
+            if dtype == "f32":
+                d = np.abs(gp[k] - pr[k])
+                off = float(np.mean(d > 0.05 * lr + 4 * EPS32 * np.abs(p[k])))
+                rec["param_off_frac"][k] = off
+                if off > 1e-4 or d.max() > 2.05 * lr:
+                    fails.append((t, "param", k, off, float(d.max() / lr)))
+        os.makedirs("gpurun_out", exist_ok=True)
+        with open(os.path.join("gpurun_out", "parity_errors.jsonl"), "a") as f:
+            f.write(json.dumps(rec) + "\n")
+    assert opt.global_step == STEPS
+    assert not fails, fails[:12]

@@ -92,3 +92,38 @@ def test_c2_distributed_is_one_allreduce(pg):
     o = OptimizerVAE(m, process_group=pg, bucketed=True)
     assert [(b.lo, b.hi, b.point, b.sharded) for b in o.buckets] == [(0, m.param_count + 8, 0, False)]
     assert o._comm is None
+
+
+def test_rebinding_bucketed_optimizer_keeps_events(pg):
+    """`opt = OptimizerVAE(model, pg, bucketed=True)` twice on one model -- the
+    old optimizer's __del__ runs after the new one registered its completion events and
+    must not unregister them (snd_plan_grad_event_get reads what the plan holds)."""
+    import ctypes as C
+    import gc
+
+    from snd_vae_amd import _lib
+    from snd_vae_amd.model import SGCNModelVAE
+    from snd_vae_amd.optimizer import OptimizerVAE
+    cfg = tref(256, 16)
+    m = SGCNModelVAE(cfg, 4, dtype="f32")
+    L = _lib.lib()
+
+    def held():
+        out = {}
+        for i in range(len(m.layout.shapes)):
+            ev = C.c_void_p()
+            pt = L.snd_plan_grad_event_get(m.plan, i, C.byref(ev))
+            assert pt >= 0, _lib.last_error()
+            if pt:
+                out[i] = (pt, ev.value)
+        return out
+
+    opt = OptimizerVAE(m, process_group=pg, bucketed=True, shard_min=1024)
+    first = held()
+    assert first and all(v for _, v in first.values())
+    opt = OptimizerVAE(m, process_group=pg, bucketed=True, shard_min=1024)   # rebinding frees the first
+    gc.collect()
+    now = held()
+    assert {i: v for i, (_, v) in now.items()} == {i: opt._events[pt].cuda_event for i, (pt, _) in now.items()}
+    opt.close()
+    assert all(v is None for _, v in held().values())

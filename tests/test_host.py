@@ -379,6 +379,42 @@ def test_reduce_adam_option(lib_built):
     _lib.check(L.snd_plan_fuse_adam(h, state, state, 1e-3, 0.9, 0.999, 1e-8))
     kinds = {k: L.snd_plan_block_fused(h, i) for i, k in enumerate(names)}
     assert kinds == {k: 1 if k in ("enc.Wh", "dec.Wp", "dec.bp") else 0 for k in names}
+    # the kinds cannot change under a fused update (a cached range list would skip or
+    # double a block's update): unfuse first
+    assert L.snd_plan_set_option(h, b"reduce_adam", 1) == -1   # SND_ERR_ARG
+    assert L.snd_plan_set_option(h, b"reduce_adam", 0) == 0
+    _lib.check(L.snd_plan_fuse_adam(h, None, None, 1e-3, 0.9, 0.999, 1e-8))
     assert L.snd_plan_set_option(h, b"reduce_adam", 1) == 1
+    _lib.check(L.snd_plan_fuse_adam(h, state, state, 1e-3, 0.9, 0.999, 1e-8))
     assert L.snd_plan_block_fused(h, names.index("enc.W0")) == 2
     L.snd_plan_destroy(h)
+
+
+# kernels that may spill, with the most they may spill (VGPRs per lane); every other
+# kernel of the library must not.  Not on the C2 step: the register-gather fallbacks,
+# the v1 zz^T at d = 128 and the fp32 parity zz^T.
+KNOWN_SPILLS = {
+    "spmm_bf16_tiled_kernelILi1ELi1ELi1E": 4, "spmm_bf16_tiled_kernelILi1ELi1ELi2E": 30,
+    "zzt_dense_bf16ILi128E": 0, "zzt_dense_f32ILi128E": 42,
+    "zzt_dense_bf16_v7": 2,            # C5's zz^T
+    "rowconv_kernelILi3ELi4E": 6,      # RC_ENC1 at 4 column blocks (C5 widths)
+}
+
+
+def test_no_register_spills_in_shipped_kernels(lib_built):
+    """hipcc's kernel-resource remarks, recorded by build.py per object: a kernel that
+    starts spilling (round 4: dec_bwd_kernel, 72 VGPRs, 26 us per C2 step) fails here on
+    the CPU, before any GPU run."""
+    from snd_vae_amd.build import kernel_resources
+    res = kernel_resources()
+    assert len(res) > 50
+    bad = {}
+    for k, v in res.items():
+        allow = next((n for sub, n in KNOWN_SPILLS.items() if sub in k), 0)
+        if v.get("vgpr_spill", 0) > allow or (v.get("scratch", 0) and not any(s in k for s in KNOWN_SPILLS)):
+            bad[k] = v
+    assert not bad, bad
+    for hot in ("dec_bwd_kernel", "dec_fwd_kernel", "head_bwd_kernel", "head_fwd_kernel",
+                "enc_front_kernel", "zzt_dense_bf16_v4", "wgrad_multi_kernel", "spmm_win_kernel"):
+        ks = [k for k in res if hot in k]
+        assert ks and all(res[k].get("vgpr_spill", 0) == 0 and res[k].get("scratch", 0) == 0 for k in ks), hot
