@@ -56,9 +56,14 @@ def block_err(g, ref):
 
 
 def adam_from(p, g, m, v, t, lr, b1, b2, eps):
-    """TF1 Adam (optimizer.py:125 -> tf.train.AdamOptimizer) in float64 on one block."""
-    m2 = b1 * m + (1 - b1) * g
-    v2 = b2 * v + (1 - b2) * g * g
+    """TF1 Adam (optimizer.py:125 -> tf.train.AdamOptimizer) in float64 on one block, with
+    TF's float32 coefficients: its ApplyAdam kernel forms 1 - beta1 and 1 - beta2 in the
+    variable's dtype, and float32(1 - 0.999f) is 1.3e-5 relative off 0.001 -- the
+    fused update does the same (adam_elem), a float64 (1 - b2) would not."""
+    f32 = np.float32
+    c1, c2 = float(f32(1) - f32(b1)), float(f32(1) - f32(b2))
+    m2 = float(f32(b1)) * m + c1 * g
+    v2 = float(f32(b2)) * v + c2 * g * g
     lr_t = lr * np.sqrt(1 - b2 ** t) / (1 - b1 ** t)
     return p - lr_t * m2 / (np.sqrt(v2) + eps), m2, v2
 

@@ -37,6 +37,15 @@ for s in ${STAGES:-tests smoke ab bench timeline}; do
       done ;;
     prof) step rocprof 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run \
              --output-format csv -- python bench.py --steps 20 --warmup 5 --no-cpu-baseline --extra "" ;;
+    benchq) step benchq 300 python -u bench.py --steps 50 --warmup 10 --no-cpu-baseline --batch-sweep "" --extra "" ;;
+    traffic)   # per-kernel HBM bytes of eager C2 steps: one counter per rocprofv3 run
+      step pmc_fetch 200 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o run --output-format csv \
+        -- python tools/prof_step.py --steps 3
+      step pmc_write 200 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write -o run --output-format csv \
+        -- python tools/prof_step.py --steps 3
+      python tools/pmc_kernels.py gpurun_out/pmc_fetch gpurun_out/pmc_write gpurun_out/traffic_c2.json \
+        --alg zzt_dense_bf16_v4=17039360 ;;
+    sq) step pmc_sq 900 bash tools/pmc_step.sh ;;
     custom) step custom ${CUSTOM_SECS:-300} bash -c "$CUSTOM" ;;
   esac
 done

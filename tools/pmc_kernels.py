@@ -22,7 +22,7 @@ def load(d, counter):
         rows += [r for r in csv.DictReader(open(p)) if r["Counter_Name"] == counter]
     acc = collections.defaultdict(list)
     for r in rows:
-        acc[r["Kernel_Name"].split("(")[0]].append(float(r["Counter_Value"]))
+        acc[r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0]].append(float(r["Counter_Value"]))
     return acc
 
 

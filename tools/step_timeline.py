@@ -9,8 +9,10 @@ import sys
 def main(path):
     rows = list(csv.DictReader(open(path)))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-    # a step ends with its last Adam launch (graph-latent plans run several Adam passes)
-    ad = ["adam" in r["Kernel_Name"] for r in rows]
+    # a step ends with its last Adam launch (graph-latent plans run several Adam passes),
+    # or with the final reduction when Adam rides in it (ABI 16)
+    key = "adam" if any("adam" in r["Kernel_Name"] for r in rows) else "reduce_kernel"
+    ad = [key in r["Kernel_Name"] for r in rows]
     ends = [i for i in range(len(rows)) if ad[i] and (i + 1 == len(rows) or not ad[i + 1])]
     a, b = ends[-2] + 1, ends[-1] + 1
     t0 = int(rows[a]["Start_Timestamp"])
