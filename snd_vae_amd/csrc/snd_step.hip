@@ -312,7 +312,7 @@ extern "C" int snd_plan_create(const snd_config_t* cfg, int n_graphs, snd_plan_t
   p->add_buf("DMS", RH * 2 * L); p->add_buf("DH", RH * gh); p->add_buf("DG", R * W);
   p->add_buf("DP1", R * h1);  p->add_buf("DXW1", R * h1); p->add_buf("DH1", R * h0);
   p->add_buf("DP0", R * h0);  p->add_buf("DXW0", R * h0);
-  const int nz = zzt_dense_blocks(p->B, p->N, c.dtype), ne = edge_blocks(p->R, dj);
+  const int nz = zzt_dense_blocks(p->B, p->N, dj, c.dtype), ne = edge_blocks(p->R, dj);
   const int nk = reparam_blocks(p->RH, L), nh = head_blocks(p->R), nc = col_blocks(p->R);
   p->add_buf("PZZT", 2LL * nz, 8); p->add_buf("PEDGE", 2LL * std::max(ne, edge_bf16_blocks(p->R)), 8); p->add_buf("PKL", std::max({nk, reparam_prep_blocks(p->B, zzt_npad(p->N)), small_head_fwd_blocks(c.latent)}), 8);
   p->add_buf("STEPN", 1);   // *step + 1, for the fused-Adam reduction (ReduceAdam)
@@ -1962,7 +1962,7 @@ extern "C" int snd_train_step(const snd_plan_t* plan, const snd_batch_t* batch,
   const int nh = head_blocks(R);
   const int n_kl = (p.fast && !p.tref) ? reparam_prep_blocks(p.B, zzt_npad(N))
                    : (p.small_head ? small_head_fwd_blocks(L) : reparam_blocks(RH, L));
-  FinalizeArgs fa{x.d("PZZT"), p.B * (zzt_npad(N) / 128) * (c.dtype == SND_BF16 ? x.zts : 1), x.d("PEDGE"),
+  FinalizeArgs fa{x.d("PZZT"), p.B * (zzt_npad(N) / 128) * (c.dtype == SND_BF16 ? x.zts : 1) * zzt_wpb(dj, c.dtype), x.d("PEDGE"),
                   p.head_bwd ? head_tiles(R) : (p.fast ? edge_bf16_blocks(R) : edge_blocks(R, dj)),
                   x.d("PKL"), n_kl, x.d(p.dec_fused ? "PDSSES" : "PSSES"),
                   x.d(p.dec_fused ? "PDSSEN" : "PSSEN"), p.dec_fused ? p.dtiles : nh,

@@ -36,6 +36,9 @@
 
 #include <algorithm>
 
+#ifndef SND_ZZT_V9
+#define SND_ZZT_V9 0     // 1: the default d <= 64 kernel is v9 (two 512-thread workgroups per CU),
+#endif                   // 2: v9 with the odd column blocks one tile late (A/B builds)
 #ifndef SND_ZZT_PIPE
 #define SND_ZZT_PIPE 0   // v4 software-pipelined tile (A/B build: -DSND_ZZT_PIPE=1)
 #endif
@@ -1133,6 +1136,290 @@ __global__ void __launch_bounds__(NTH2) zzt_dense_bf16_v7(ZztArgs a) {
   }
 }
 
+
+// ---------------------------------------------------------------- bf16 MFMA, v9 (d <= 64, A/B)
+// v4's per-wave work (one 32 x 32 logit block per 128-column tile, the same signed
+// epilogue) in HALF-size workgroups -- 512 threads = 2 row groups (64 rows i) x 4
+// column blocks -- with v7's single dual-use LDS image per tile (16 KB at d = 64:
+// ds_read_b128 rows for the forward, ds_read_b64_tr_b16 for the backward), so that
+// TWO workgroups fit on a CU (~59 KB of LDS each, 4 waves per SIMD in all).  Each
+// workgroup has its own barrier: the two drift apart, and one workgroup's epilogue
+// VALU can issue under the other's MFMAs -- in v4 the 16 waves of the CU's one
+// workgroup leave every tile barrier together, so the matrix and vector phases add up
+// (DESIGN §5).  Tiles arrive by LDS-DMA into a 3-deep ring; the image holds
+// z * sqrt(log2 e) (v7), so the backward result is divided by sqrt(log2 e) once.
+// STAG: the odd column-block waves run one tile late (v7's stagger).
+constexpr int NTH9 = 512;
+constexpr int ROWS9 = 64;
+__device__ __forceinline__ int zoa64(int row, int ch) {   // [128][64] bf16 image, 16-byte chunk ch
+  return 1024 * (row >> 3) + 512 * (ch >> 2) + 64 * (row & 7) + 16 * ((ch & 3) ^ ((row >> 2) & 3));
+}
+
+template <bool STAG>
+__global__ void __launch_bounds__(NTH9) __attribute__((amdgpu_waves_per_eu(4, 4)))
+zzt_dense_bf16_v9(ZztArgs a) {
+  constexpr int DP = 64, NT = NTH9, NW = NT / 64;
+  constexpr int KS = DP / 16;          // forward k-steps
+  constexpr int CB = DP / 32;          // backward 32-column output blocks
+  constexpr int IMG = TJ2 * DP * 2;    // one [128][64] bf16 image, 16 KB
+  __shared__ __attribute__((aligned(16))) char lds[3 * IMG + ROWS9 * DP * 2];   // ring, -z_i rows
+  __shared__ float colsum[DP];
+  __shared__ float csred[NT / DP][DP];
+  __shared__ float dsg[2][32];
+  __shared__ double sl[NW];
+  __shared__ unsigned sc[NW];
+  char* brows = lds + 3 * IMG;
+  const unsigned lds0 = (unsigned)(uintptr_t)(zlptr_t)lds;
+
+  const int wgs = a.ngraphs * zrb(a) * 2;
+  const int sp = blockIdx.x / wgs, bx = blockIdx.x - sp * wgs;
+  const int nsplit = gridDim.x / wgs;
+  const int g = bx % a.ngraphs, hb = bx / a.ngraphs;            // hb: 64-row block of the range
+  const int rb = a.rb0 + (hb >> 1), half = hb & 1;              // its 128-row block and half
+  const int r0 = rb * ROWS + ROWS9 * half;                      // first row
+  const __bf16* Jg = reinterpret_cast<const __bf16*>(a.jrow) + (long long)g * a.npad * DP;
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, r = lane & 31, h = lane >> 5;
+  const int rg = w & 1, cb = w >> 1;
+  const int i0 = __builtin_amdgcn_readfirstlane(r0 + 32 * rg);
+  const int i_me = i0 + r;
+  const int ntot = a.npad / TJ2;
+  const int t0 = sp * ntot / nsplit, t1 = (sp + 1) * ntot / nsplit;
+
+  // tile t -> ring slot b: 16 pieces of 1 KB (8 rows each), wave w issues pieces w and w + 8
+  int dsrc[2];
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int P = w + 8 * k;
+    const int row = 8 * P + ((lane >> 2) & 7);
+    const int ch = 4 * (lane >> 5) + ((lane & 3) ^ ((row >> 2) & 3));
+    dsrc[k] = row * DP + 8 * ch;
+  }
+  auto dma = [&](int t, int b) {
+#pragma unroll
+    for (int k = 0; k < 2; ++k)
+      zdma16(Jg + (long long)t * TJ2 * DP + dsrc[k],
+             __builtin_amdgcn_readfirstlane(lds0 + b * IMG + 1024 * (w + 8 * k)));
+  };
+
+  // ---- prologue: tile t0 in flight; -z_i rows; column sums
+  dma(t0, 0);
+  for (int idx = tid; idx < ROWS9 * (DP / 8); idx += NT) {
+    const int row = idx >> 3, ch = idx & 7;
+    const uint4 u = *reinterpret_cast<const uint4*>(Jg + (long long)(r0 + row) * DP + ch * 8);
+    *reinterpret_cast<uint4*>(brows + zoa64(row, ch)) =
+        make_uint4(u.x ^ 0x80008000u, u.y ^ 0x80008000u, u.z ^ 0x80008000u, u.w ^ 0x80008000u);
+  }
+  {
+    const int nrb = a.npad / 64;
+    const int k = tid % DP, grp = tid / DP;
+    float s = 0.f;
+    for (int p = grp; p < nrb; p += NT / DP) s += a.colpart[((long long)g * nrb + p) * DP + k];
+    csred[grp][k] = s;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid < DP) {
+    float s = 0.f;
+    for (int p = 0; p < NT / DP; ++p) s += csred[p][tid];
+    colsum[tid] = s;
+  }
+
+  f32x16 acc[CB];
+#pragma unroll
+  for (int q = 0; q < CB; ++q)
+#pragma unroll
+    for (int v = 0; v < 16; ++v) acc[q][v] = 0.f;
+  // forward operand bases (k-step s: base[s & 1] + 512 (s >> 1))
+  const int ja = 32 * cb + r, ia = 32 * rg + r;
+  const int fa0 = zoa64(ja, h), fa1 = zoa64(ja, 2 + h);
+  const int fb0 = zoa64(ia, h), fb1 = zoa64(ia, 2 + h);
+  // backward transposed-read bases (v7's, 8-row groups of 1 KB): lane 4 qq + pp of group
+  // gq supplies row 32 cb + 16 s + 8 t + 4 (gq >> 1) + qq, columns 32 q + 16 (gq & 1) + 4 pp
+  const int gq = lane >> 4, qq = (lane >> 2) & 3, pp = lane & 3;
+  const int c0 = 2 * (gq & 1) + (pp >> 1);
+  const int tb0 = 1024 * (4 * cb) + 64 * (4 * (gq >> 1) + qq) + 16 * (c0 ^ (gq >> 1)) + 8 * (pp & 1);
+  const int tb1 = 1024 * (4 * cb + 1) + 64 * (4 * (gq >> 1) + qq) + 16 * (c0 ^ ((gq >> 1) + 2)) + 8 * (pp & 1);
+  auto fwd = [&](int b) {
+    f32x16 X;
+#pragma unroll
+    for (int v = 0; v < 16; ++v) X[v] = 0.f;
+    const char* T = lds + b * IMG;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      const bf16x8 av = *reinterpret_cast<const bf16x8*>(T + ((s & 1) ? fa1 : fa0) + 512 * (s >> 1));
+      const bf16x8 bv = *reinterpret_cast<const bf16x8*>(brows + ((s & 1) ? fb1 : fb0) + 512 * (s >> 1));
+      X = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, bv, X, 0, 0, 0);
+    }
+    return X;
+  };
+  float lacc = 0.f;
+  double ltot = 0.0;
+  unsigned lcnt = 0;
+  bool ovf = false;   // sticky per wave, as v4
+  auto epi = [&](const f32x16& Y, bf16x8 (&sA)[2]) {   // v4's epilogue, y = -x
+    float q[16], lt = 0.f;
+#pragma unroll
+    for (int v = 0; v < 16; ++v) {
+      const float e = __builtin_amdgcn_exp2f(Y[v]);
+      q[v] = e + 1.f;
+      sA[v >> 3][v & 7] = (__bf16)__builtin_amdgcn_rcpf(q[v]);
+    }
+#pragma unroll
+    for (int g4 = 0; g4 < 4; ++g4) {
+      const unsigned t01 = __builtin_amdgcn_perm(__float_as_uint(Y[4 * g4 + 1]),
+                                                 __float_as_uint(Y[4 * g4]), 0x0C0C0703u);
+      const unsigned t23 = __builtin_amdgcn_perm(__float_as_uint(Y[4 * g4 + 3]),
+                                                 __float_as_uint(Y[4 * g4 + 2]), 0x07030C0Cu);
+      lcnt += (unsigned)__builtin_popcount((t01 | t23) & 0x80808080u);
+    }
+    if (!ovf) {
+#pragma unroll
+      for (int p = 0; p < 4; ++p)
+        lt += __builtin_amdgcn_logf((q[4 * p] * q[4 * p + 1]) * (q[4 * p + 2] * q[4 * p + 3]));
+      ovf = __builtin_amdgcn_ballot_w64(!__builtin_isfinite(lt)) != 0;
+    }
+    if (__builtin_expect(ovf, 0)) {
+      lt = 0.f;
+#pragma unroll
+      for (int v = 0; v < 16; ++v) lt += Y[v] > 24.f ? Y[v] : __builtin_amdgcn_logf(q[v]);
+    }
+    lacc += lt;
+  };
+  auto bwd = [&](int b, const bf16x8 (&sA)[2]) {
+    const char* T = lds + b * IMG;
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int q = 0; q < CB; ++q) {
+        const bf16x8 bv = ztr_pair(T + tb0 + 2048 * s + 512 * q, T + tb1 + 2048 * s + 512 * q);
+        acc[q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(sA[s], bv, acc[q], 0, 0, 0);
+      }
+  };
+  auto run = [&](auto late_c) {
+    constexpr bool LATE = decltype(late_c)::value;
+    f32x16 Yp;
+#pragma unroll
+    for (int v = 0; v < 16; ++v) Yp[v] = 0.f;
+    auto tile = [&](int t, auto cc) {
+      constexpr int CUR = decltype(cc)::value, NN = (CUR + 2) % 3;
+      if (t + 1 < t1) dma(t + 1, (CUR + 1) % 3);
+      if constexpr (LATE) {
+        if (t > t0) {
+          bf16x8 sA[2];
+          epi(Yp, sA);
+          bwd(NN, sA);   // tile t-1's slot
+        }
+        Yp = fwd(CUR);
+      } else {
+        const f32x16 Y = fwd(CUR);
+        bf16x8 sA[2];
+        epi(Y, sA);
+        bwd(CUR, sA);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // tile t+1 landed
+      __syncthreads();
+    };
+    for (int t = t0; t < t1; t += 3) {
+      tile(t, std::integral_constant<int, 0>{});
+      if (t + 1 < t1) tile(t + 1, std::integral_constant<int, 1>{});
+      if (t + 2 < t1) tile(t + 2, std::integral_constant<int, 2>{});
+      ltot += (double)lacc;
+      lacc = 0.f;
+    }
+    if (LATE && t1 > t0) {
+      bf16x8 sA[2];
+      epi(Yp, sA);
+      bwd((t1 - 1 - t0) % 3, sA);
+      ltot += (double)lacc;
+      lacc = 0.f;
+    }
+  };
+  if (STAG && (cb & 1)) {
+    __builtin_amdgcn_s_setprio(1);
+    run(std::true_type{});
+    __builtin_amdgcn_s_setprio(0);
+  } else {
+    run(std::false_type{});
+  }
+
+  // ---- per-row corrections (row i_me; lanes r and r + 32 hold its two k halves)
+  float xd = 0.f, xs = 0.f;
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+    const bf16x8 bv = *reinterpret_cast<const bf16x8*>(brows + ((s & 1) ? fb1 : fb0) + 512 * (s >> 1));
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float bb = (float)bv[e];
+      xd += bb * bb;
+      xs += bb * colsum[16 * s + 8 * h + e];
+    }
+  }
+  xd += __shfl_xor(xd, 32, 64);
+  xs += __shfl_xor(xs, 32, 64);
+  xs = -xs;
+  const bool row_valid = i_me < a.n;
+  const bool corr = sp == 0;
+  const bool own = cb == 0 && h == 0 && row_valid && corr;
+  const float exd = __builtin_amdgcn_exp2f(-fabsf(xd));
+  if (own) {
+    ltot += (double)xs;
+    ltot -= (double)(fmaxf(xd, 0.f) + __builtin_amdgcn_logf(1.f + exd));
+  }
+  const unsigned dpos = (unsigned)__popcll(__ballot(own && xd > 0.f));
+  if (cb == 0 && h == 0) {   // s'_ii as the backward MFMA consumed it (bf16), 0 outside split 0
+    const float sg = __builtin_amdgcn_rcpf(__builtin_amdgcn_exp2f(-xd) + 1.f);
+    dsg[rg][r] = corr ? (float)(__bf16)sg : 0.f;
+  }
+
+  // ---- combine the four column blocks' partial dJ (fixed order) through the ring's
+  // 48 KB; the diagonal term subtracted with the scaled z_i the backward products used,
+  // then the sqrt(log2 e) scale removed
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  float* red = reinterpret_cast<float*>(lds);        // [cb-1][rg][CB * 16][64]
+  float* dst = (sp == 0 ? a.dJd : a.dJd_extra + (long long)(sp - 1) * a.ngraphs * a.n * a.d) +
+               (long long)g * a.n * a.d;
+  const __bf16* zi = Jg + (long long)(r0 + 32 * rg) * DP;
+  if (cb > 0) {
+#pragma unroll
+    for (int q = 0; q < CB; ++q)
+#pragma unroll
+      for (int v = 0; v < 16; ++v)
+        red[(((cb - 1) * 2 + rg) * (CB * 16) + q * 16 + v) * 64 + lane] = acc[q][v];
+  }
+  __syncthreads();
+  if (cb == 0) {
+#pragma unroll
+    for (int q = 0; q < CB; ++q) {
+      const int c = 32 * q + r;
+#pragma unroll
+      for (int v = 0; v < 16; ++v) {
+        float o = acc[q][v];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) o += red[((k * 2 + rg) * (CB * 16) + q * 16 + v) * 64 + lane];
+        const int il = (v & 3) + 8 * (v >> 2) + 4 * h;   // D row within the row group
+        const int i = i0 + il;
+        if (i < a.n && c < a.d)
+          dst[(long long)i * a.d + c] = (o - dsg[rg][il] * (float)zi[il * DP + c]) * kInvSqrtLog2e;
+      }
+    }
+  }
+  const double l = wave_sum_d(ltot);
+  const unsigned wcnt = wave_sum_u(lcnt);
+  if (lane == 0) { sl[w] = l; sc[w] = wcnt - dpos; }
+  __syncthreads();
+  if (tid == 0) {
+    double tl = 0.0, tc = 0.0;
+    for (int k = 0; k < NW; ++k) { tl += sl[k]; tc += (double)sc[k]; }
+    if (corr) {   // padded pairs of this 64-row block: x = 0 exactly, softplus2(0) = 1 each
+      const int valid = max(0, min(ROWS9, a.n - r0));
+      tl -= (double)ROWS9 * a.npad - (double)valid * a.n;
+    }
+    a.part[2 * blockIdx.x] = tl * (double)kLn2;
+    a.part[2 * blockIdx.x + 1] = tc;
+  }
+}
+
 // dJd += sum of the column-split partials (fixed order)
 __global__ void zzt_split_sum_kernel(float* dJd, const float* extra, long long n, long long stride,
                                      int nextra) {
@@ -1201,8 +1488,9 @@ int zzt_tsplit_blocks(int wgs, int n, int dtype) {
   // 0.1546 -> 0.1512 ms against 4 splits; B = 2 unchanged at 4)
   return std::max(1, std::min({cdiv(ncu, wgs), 8, ntiles}));
 }
-int zzt_dense_blocks(int ngraphs, int n, int dtype) {
-  return ngraphs * (zzt_npad(n) / ROWS) * zzt_tsplit(ngraphs, n, dtype);
+int zzt_wpb(int d, int dtype) { return (SND_ZZT_V9 && dtype == SND_BF16 && zzt_dp(d) == 64) ? 2 : 1; }
+int zzt_dense_blocks(int ngraphs, int n, int d, int dtype) {
+  return ngraphs * (zzt_npad(n) / ROWS) * zzt_tsplit(ngraphs, n, dtype) * zzt_wpb(d, dtype);
 }
 
 size_t zzt_staging_bytes(int ngraphs, int n, int d, int dtype) {
@@ -1256,6 +1544,10 @@ int launch_zzt_dense(const ZztArgs& a, int dtype, hipStream_t s, bool defer_spli
     if (dp == 32) hipLaunchKernelGGL((zzt_dense_bf16<32>), grid, dim3(NTH), 0, s, a);
     else if (dp == 64) hipLaunchKernelGGL((zzt_dense_bf16<64>), grid, dim3(NTH), 0, s, a);
     else hipLaunchKernelGGL((zzt_dense_bf16<128>), grid, dim3(NTH), 0, s, a);
+  } else if (dtype == SND_BF16 && dp == 64 && SND_ZZT_V9 && a.variant == 0) {   // v9 (A/B build)
+    const dim3 g9(grid.x * 2);
+    if (SND_ZZT_V9 == 2) hipLaunchKernelGGL((zzt_dense_bf16_v9<true>), g9, dim3(NTH9), 0, s, a);
+    else hipLaunchKernelGGL((zzt_dense_bf16_v9<false>), g9, dim3(NTH9), 0, s, a);
   } else if (dtype == SND_BF16 && dp <= 64) {         // v4 (default, d <= 64)
     // variant >= 256: the measurement build (phase skips / stamps, variant >> 8)
     if (a.variant >= 256) {
@@ -1287,10 +1579,8 @@ int launch_zzt_dense(const ZztArgs& a, int dtype, hipStream_t s, bool defer_spli
   return 0;
 }
 
-int zzt_init_attributes() {
-  // the f32 variants use up to 128 KiB of dynamic LDS; set once per process
-  static bool done = false;
-  if (done) return 0;
+static int zzt_init_attributes_once() {
+  // the f32 variants use up to 128 KiB of dynamic LDS
   hipError_t e = hipFuncSetAttribute((const void*)zzt_dense_f32<128>,
                                      hipFuncAttributeMaxDynamicSharedMemorySize, 131072);
   if (e != hipSuccess) {
@@ -1303,8 +1593,12 @@ int zzt_init_attributes() {
     set_error("zzt: hipFuncSetAttribute: %s", hipGetErrorString(e));
     return SND_ERR_HIP;
   }
-  done = true;
   return 0;
+}
+// once per process, thread-safe (a function-local static's initialiser runs exactly once)
+int zzt_init_attributes() {
+  static const int rc = zzt_init_attributes_once();
+  return rc;
 }
 
 }  // namespace snd
@@ -1316,7 +1610,7 @@ extern "C" size_t snd_zzt_ce_workspace(int n_graphs, int n, int d, int dtype) {
   const long long rows = (long long)n_graphs * n;
   size_t b = round_up(zzt_staging_bytes(n_graphs, n, d, dtype), 256);
   b += round_up(rows * d * sizeof(float), 256);                               // ej
-  b += round_up(2 * sizeof(double) * (size_t)zzt_dense_blocks(n_graphs, n, dtype), 256);
+  b += round_up(2 * sizeof(double) * (size_t)zzt_dense_blocks(n_graphs, n, d, dtype), 256);
   b += round_up(2 * sizeof(double) * (size_t)edge_blocks((int)rows, d), 256);
   b += round_up((size_t)(zzt_tsplit(n_graphs, n, dtype) - 1) * rows * d * sizeof(float), 256);
   return b;
@@ -1342,7 +1636,7 @@ extern "C" int snd_zzt_ce(const float* z, int n_graphs, int n, int d, const int*
   float* ej = (float*)p;
   p += round_up(rows * d * sizeof(float), 256);
   double* pd = (double*)p;
-  p += round_up(2 * sizeof(double) * (size_t)zzt_dense_blocks(n_graphs, n, dtype), 256);
+  p += round_up(2 * sizeof(double) * (size_t)zzt_dense_blocks(n_graphs, n, d, dtype), 256);
   double* pe = (double*)p;
   p += round_up(2 * sizeof(double) * (size_t)edge_blocks((int)rows, d), 256);
   float* extra = (float*)p;
@@ -1356,7 +1650,7 @@ extern "C" int snd_zzt_ce(const float* z, int n_graphs, int n, int d, const int*
   hipLaunchKernelGGL(zzt_combine_kernel, dim3(1024), dim3(256), 0, s, dz, ej, rows * d, 2.f * norm);
   SND_LAUNCH_CHECK("zzt_combine_kernel");
   hipLaunchKernelGGL(zzt_stats_kernel, dim3(1), dim3(64), 0, s, pd,
-                     zzt_dense_blocks(n_graphs, n, dtype), pe, edge_blocks((int)rows, d), rowptr,
+                     zzt_dense_blocks(n_graphs, n, d, dtype), pe, edge_blocks((int)rows, d), rowptr,
                      n_graphs, n, norm, stats);
   SND_LAUNCH_CHECK("zzt_stats_kernel");
   return 0;
@@ -1374,7 +1668,7 @@ static void zrows_layout(int n, int d, int row0, int row1, int dtype, size_t* of
   off[0] = b; b += round_up(zzt_staging_bytes(1, n, d, dtype), 256);              // images
   off[1] = b; b += round_up((size_t)n * d * sizeof(float), 256);                  // dJd (full rows)
   off[2] = b; b += round_up((size_t)rows * d * sizeof(float), 256);               // ej
-  off[3] = b; b += round_up(2 * sizeof(double) * (size_t)nrb * ts, 256);          // dense partials
+  off[3] = b; b += round_up(2 * sizeof(double) * (size_t)nrb * ts * zzt_wpb(d, dtype), 256);   // dense partials
   off[4] = b; b += round_up(2 * sizeof(double) * (size_t)edge_blocks(rows, d), 256);
   off[5] = b; b += round_up((size_t)std::max(0, ts - 1) * n * d * sizeof(float), 256);   // splits
   *total = b;
@@ -1424,7 +1718,7 @@ extern "C" int snd_zzt_ce_rows(const float* z, int n, int d, int row0, int row1,
   SND_LAUNCH_CHECK("zzt_combine2_kernel");
   const int ts = zzt_tsplit_blocks(nrb, n, dtype == SND_BF16 ? SND_BF16 : dtype);
   hipLaunchKernelGGL(zzt_stats_rows_kernel, dim3(1), dim3(64), 0, s, pd,
-                     nrb * ((dtype == SND_BF16) ? ts : 1), pe, edge_blocks(rows, d), rowptr, rows, n,
+                     nrb * ((dtype == SND_BF16) ? ts : 1) * zzt_wpb(d, dtype), pe, edge_blocks(rows, d), rowptr, rows, n,
                      norm, stats);
   SND_LAUNCH_CHECK("zzt_stats_rows_kernel");
   return 0;

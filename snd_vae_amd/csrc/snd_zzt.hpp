@@ -33,7 +33,8 @@ int zzt_npad(int n);
 // in fixed order by launch_zzt_dense.  Loss partials: zzt_dense_blocks() entries.
 int zzt_tsplit(int ngraphs, int n, int dtype);
 int zzt_tsplit_blocks(int row_blocks, int n, int dtype);   // the same for a row-block count
-int zzt_dense_blocks(int ngraphs, int n, int dtype);
+int zzt_dense_blocks(int ngraphs, int n, int d, int dtype);
+int zzt_wpb(int d, int dtype);   // loss partials per 128-row block and split (v9: 2)
 size_t zzt_staging_bytes(int ngraphs, int n, int d, int dtype);
 ZztStage zzt_stage(void* base, int ngraphs, int n, int d, int dtype);
 int zzt_init_attributes();
