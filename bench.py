@@ -583,7 +583,10 @@ def main():
                    "n_nodes": N, "latent": d, "graphs_per_gpu": B, "global_batch": B * info.world,
                    "nnz_per_graph": round(host.nnz / B, 1), "parallelism": f"dp{info.world}",
                    "hip_graph": not args.no_graph},
-        "roofline": {"kernel": "zzt_dense (fused z z^T + CE fwd+bwd)", "bound": "mfma",
+        "roofline": {"kernel": "zzt_dense (fused z z^T + CE fwd+bwd; " +
+                               ("zzt_dense_bf16_v9: two 512-thread workgroups per CU" if fast and d <= 64 and d > 32
+                                else "zzt_dense_bf16_v7" if fast and d > 64 else "v4 / fp32") + ")",
+                     "bound": "mfma",
                      "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
                      "frac": round(achieved / peak, 4),
                      "traffic": load_traffic(N, d, B, args.dtype),

@@ -335,8 +335,7 @@ int head_fwd_dispatch(const HeadFwdArgs& a, hipStream_t s) {
 // ---------------------------------------------------------------- backward head
 // LDS of head_bwd_kernel (bytes): Wms^T image | Wh^T image | d[mu | s] image | dh image |
 // per-wave bias sums of d[mu | s]
-// Rows per backward-head tile (kHeadBwdRows, snd_head.hpp): 128 rows x 1024 threads, or 64
-// rows x 512 threads (two workgroups per CU, A/B build -DSND_HB_ROWS=64)
+// Rows per backward-head tile (kHeadBwdRows, snd_head.hpp): 128 rows x 1024 threads
 struct BwdLay {
   int w1, w2, m, h, red, total;
   __host__ __device__ BwdLay(int kp1, int np1, int kp2, int np2, int L, int hr = kHeadBwdRows) {

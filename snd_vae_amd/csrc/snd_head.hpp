@@ -59,10 +59,10 @@ struct HeadBwdArgs {
   int dbg;
 };
 bool head_bwd_supported(int L, int gh, int W, int h1, int kp1, int np1, int kp2, int np2);
-#ifndef SND_HB_ROWS
-#define SND_HB_ROWS 128   // rows per backward-head tile (A/B build: -DSND_HB_ROWS=64)
-#endif
-constexpr int kHeadBwdRows = SND_HB_ROWS;
+// rows per backward-head tile (round 5: 64-row tiles, two workgroups per CU, measured
+// head_bwd 25.4 vs 25.7 us with no step change, and their column partials no longer
+// match the unfused chain bit for bit: retired)
+constexpr int kHeadBwdRows = 128;
 int head_tiles(int R);   // backward-head tiles (kHeadBwdRows rows each)
 int launch_head_bwd(const HeadBwdArgs& a, hipStream_t s);
 

@@ -59,9 +59,9 @@ namespace snd {
 int debug_flags();
 namespace {
 
-#ifndef SND_WIN_GK
-#define SND_WIN_GK 4           // neighbour reads issued before a chunk's adds (A/B builds: -DSND_WIN_GK=8)
-#endif
+// neighbour reads issued before a chunk's adds (round 5, 256-graph batch, one box,
+// alternating processes: GK 2 / 4 / 8 = 88.7-90.4 / 85.1-87.6 / 87.4-91.7 us)
+constexpr int kWinGK = 4;
 constexpr int WT = 1024;       // threads: 16 waves x 8 rows
 constexpr int RR = 1096;       // ring rows
 constexpr int STEP = 128;      // rows per step
@@ -325,8 +325,8 @@ int launch_spmm_window(const SpmmWinArgs& w, hipStream_t st) {
   WinArgs a{w.meta, w.slots, w.rows, w.order, reinterpret_cast<const __bf16*>(w.h), w.ldh,
             reinterpret_cast<__bf16*>(w.out), w.ldo, w.n_per_graph, cdiv(w.n_per_graph, seg), seg, beta8,
             debug_flags() >> 24};
-  if (a.dbg & 7) hipLaunchKernelGGL((spmm_win_kernel<SND_WIN_GK, true>), dim3(w.n_graphs * a.spg), dim3(WT), 0, st, a);
-  else hipLaunchKernelGGL((spmm_win_kernel<SND_WIN_GK, false>), dim3(w.n_graphs * a.spg), dim3(WT), 0, st, a);
+  if (a.dbg & 7) hipLaunchKernelGGL((spmm_win_kernel<kWinGK, true>), dim3(w.n_graphs * a.spg), dim3(WT), 0, st, a);
+  else hipLaunchKernelGGL((spmm_win_kernel<kWinGK, false>), dim3(w.n_graphs * a.spg), dim3(WT), 0, st, a);
   SND_LAUNCH_CHECK("spmm_win_kernel");
   return 0;
 }

@@ -37,11 +37,8 @@
 #include <algorithm>
 
 #ifndef SND_ZZT_V9
-#define SND_ZZT_V9 0     // 1: the default d <= 64 kernel is v9 (two 512-thread workgroups per CU),
-#endif                   // 2: v9 with the odd column blocks one tile late (A/B builds)
-#ifndef SND_ZZT_PIPE
-#define SND_ZZT_PIPE 0   // v4 software-pipelined tile (A/B build: -DSND_ZZT_PIPE=1)
-#endif
+#define SND_ZZT_V9 1     // the d = 64 kernel: 1 v9 (two 512-thread workgroups per CU, round 5:
+#endif                   // 55.2 vs v4's 56.7 us), 0 v4, 2 v9 with v7's stagger (55.7 us); A/B builds
 
 namespace snd {
 namespace {
@@ -640,64 +637,6 @@ __global__ void __launch_bounds__(NTH2) zzt_dense_bf16_v4(ZztArgs a) {
       }
   };
 
-#if SND_ZZT_PIPE
-  // Software-pipelined tile (production builds): tile t's epilogue runs on logits
-  // computed during tile t - 1, and the forward MFMAs of tile t + 1 (already staged:
-  // buffer (CUR + 1) % 3) are issued between its four 4-logit chunks, so the matrix
-  // core works under the epilogue VALU instead of before it (all waves of a SIMD reach
-  // the forward at the same barrier; in the unpipelined order they all wait for it).
-  // The last tile's look-ahead reads a stale buffer and is discarded.
-  f32x16 Xn = (skip & 2) ? cinit : fwd(lds);
-  auto tile = [&](int t, auto cc) {
-    constexpr int CUR = decltype(cc)::value, NXT = (CUR + 1) % 3, NN = (CUR + 2) % 3;
-    if (!(skip & 8)) gload(min(t + 2, t1 - 1));
-    const f32x16 Yc = Xn;
-    f32x16 X = cinit;
-    const __bf16* Ln = lds + NXT * BUF;
-    const int j = 32 * cb + r;
-    bf16x8 sA[2];
-    float p4[4];
-#pragma unroll
-    for (int g4 = 0; g4 < 4; ++g4) {
-      if (g4 < KS && !(skip & 2)) {
-        const bf16x8 av = *reinterpret_cast<const bf16x8*>(&Ln[j * JST + (2 * g4 + h) * 8]);
-        const bf16x8 bv = *reinterpret_cast<const bf16x8*>(&brows[(32 * rg + r) * JST + (2 * g4 + h) * 8]);
-        X = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, bv, X, 0, 0, 0);
-      }
-      float qq[4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int v = 4 * g4 + u;
-        qq[u] = __builtin_amdgcn_exp2f(Yc[v]) + 1.f;
-        sA[v >> 3][v & 7] = (__bf16)__builtin_amdgcn_rcpf(qq[u]);
-      }
-      const unsigned t01 = __builtin_amdgcn_perm(__float_as_uint(Yc[4 * g4 + 1]),
-                                                 __float_as_uint(Yc[4 * g4]), 0x0C0C0703u);
-      const unsigned t23 = __builtin_amdgcn_perm(__float_as_uint(Yc[4 * g4 + 3]),
-                                                 __float_as_uint(Yc[4 * g4 + 2]), 0x07030C0Cu);
-      lcnt += (unsigned)__builtin_popcount((t01 | t23) & 0x80808080u);
-      p4[g4] = (qq[0] * qq[1]) * (qq[2] * qq[3]);
-    }
-    if (!(skip & 2)) Xn = X;
-    float lt = 0.f;
-    if (!ovf) {
-#pragma unroll
-      for (int g4 = 0; g4 < 4; ++g4) lt += __builtin_amdgcn_logf(p4[g4]);
-      ovf = __builtin_amdgcn_ballot_w64(!__builtin_isfinite(lt)) != 0;
-    }
-    if (__builtin_expect(ovf, 0)) {   // per logit, as epi() below
-      lt = 0.f;
-#pragma unroll
-      for (int v = 0; v < 16; ++v)
-        lt += Yc[v] > 24.f ? Yc[v] : __builtin_amdgcn_logf(__builtin_amdgcn_exp2f(Yc[v]) + 1.f);
-    }
-    lacc += lt;
-    if (!(skip & 4)) bwd(lds + CUR * BUF, sA);
-    else lacc += (float)sA[0][0];
-    if (!(skip & 8)) sstore(lds + NN * BUF);
-    if (!(skip & 64)) __syncthreads();
-  };
-#else
   f32x16 Y;
   // one tile; buffer indices are compile-time, the last tiles re-stage the final
   // tile (branch-free body)
@@ -717,7 +656,6 @@ __global__ void __launch_bounds__(NTH2) zzt_dense_bf16_v4(ZztArgs a) {
     if (!(skip & 8)) sstore(lds + NN * BUF);
     if (!(skip & 64)) __syncthreads();
   };
-#endif
   const int tl1 = (skip & 16) ? t0 : t1;
   for (int t = t0; t < tl1; t += 3) {
     tile(t, std::integral_constant<int, 0>{});

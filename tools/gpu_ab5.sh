@@ -22,10 +22,14 @@ PY
 }
 SND_LIB_PATH=$PWD/ab/zpipe.so run 300 python -u -m pytest tests/test_gpu_ops.py -k "zzt" -x -q --timeout 200 > gpurun_out/zpipe_tests.log 2>&1
 echo "zpipe tests rc=$?"; tail -2 gpurun_out/zpipe_tests.log
+for v in v9 v9s; do
+  SND_LIB_PATH=$PWD/ab/$v.so run 300 python -u -m pytest tests/test_gpu_ops.py tests/test_gpu_configs.py -k "zzt or c2_bench" -x -q --timeout 250 > gpurun_out/${v}_tests.log 2>&1
+  echo "$v tests rc=$?"; tail -2 gpurun_out/${v}_tests.log
+done
 SND_LIB_PATH=$PWD/ab/hb64.so run 400 python -u -m pytest tests/test_gpu_step.py -k "backward_head or c2_size or replay" -x -q --timeout 300 > gpurun_out/hb64_tests.log 2>&1
 echo "hb64 tests rc=$?"; tail -2 gpurun_out/hb64_tests.log
 rm -f gpurun_out/ab.jsonl
-run 600 bash tools/ab_multi.sh "--kernels zzt_dense,head_bwd,head_fwd --steps 200" 3 default ab/zpipe.so ab/hb64.so
+run 700 bash tools/ab_multi.sh "--kernels zzt_dense,head_bwd,head_fwd --steps 200" 3 default ab/zpipe.so ab/hb64.so ab/v9.so ab/v9s.so
 summ gpurun_out/ab.jsonl
 for r in 1 2; do
   for lib in ab/gk2.so default ab/gk8.so; do
