@@ -44,7 +44,7 @@ for s in ${STAGES:-tests smoke ab bench timeline}; do
       step pmc_write 200 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write -o run --output-format csv \
         -- python tools/prof_step.py --steps 3
       python tools/pmc_kernels.py gpurun_out/pmc_fetch gpurun_out/pmc_write gpurun_out/traffic_c2.json \
-        --alg zzt_dense_bf16_v4=17039360 ;;
+        --alg zzt_dense=17039360 --zzt-json gpurun_out/pmc_zzt_c2.json ;;
     sq) step pmc_sq 900 bash tools/pmc_step.sh ;;
     custom) step custom ${CUSTOM_SECS:-300} bash -c "$CUSTOM" ;;
   esac

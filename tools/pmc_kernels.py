@@ -32,6 +32,8 @@ def main():
     ap.add_argument("write_dir")
     ap.add_argument("out")
     ap.add_argument("--alg", nargs="*", default=[], help="kernel-substring=bytes per launch")
+    ap.add_argument("--zzt-json", default="", help="also write the zz^T kernel's bytes per launch in "
+                    "bench.load_traffic's format (C2: N 4096, d 64, 8 graphs, bf16)")
     args = ap.parse_args()
     f, w = load(args.fetch_dir, "FETCH_SIZE"), load(args.write_dir, "WRITE_SIZE")
     alg = {k: float(v) for k, v in (a.split("=") for a in args.alg)}
@@ -48,6 +50,14 @@ def main():
                 e["traffic_over_algorithmic"] = round((fb + wb) / b, 3)
         out["kernels"][k] = e
     json.dump(out, open(args.out, "w"), indent=1)
+    if args.zzt_json:
+        k, e = next((k, e) for k, e in out["kernels"].items() if "zzt_dense" in k)
+        json.dump({"kernel": k, "n_nodes": 4096, "latent": 64, "graphs": 8, "dtype": "bf16",
+                   "launches": e["launches"], "fetch_bytes": e["fetch_bytes"], "write_bytes": e["write_bytes"],
+                   "hbm_bytes_per_launch": e["hbm_bytes_per_launch"],
+                   "source": "tools/pmc_kernels.py over rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of "
+                             "tools/prof_step.py --steps 3 (eager C2 steps); FETCH doubled (gfx950)"},
+                  open(args.zzt_json, "w"), indent=1)
     top = sorted(out["kernels"].items(), key=lambda kv: -kv[1]["hbm_bytes_per_launch"])[:12]
     for k, e in top:
         print(f"{e['hbm_bytes_per_launch'] / 1e6:9.2f} MB  {k[-60:]}  {e.get('traffic_over_algorithmic', '')}")
