@@ -36,10 +36,6 @@
 
 #include <algorithm>
 
-#ifndef SND_ZZT_NRCP
-#define SND_ZZT_NRCP 0   // v9: sigma by Newton steps on the VALU instead of v_rcp_f32 (A/B build)
-#endif
-typedef float f32x2 __attribute__((ext_vector_type(2)));
 #ifndef SND_ZZT_V9
 #define SND_ZZT_V9 1     // the d = 64 kernel: 1 v9 (two 512-thread workgroups per CU, round 5:
 #endif                   // 55.2 vs v4's 56.7 us), 0 v4, 2 v9 with v7's stagger (55.7 us); A/B builds
@@ -1200,34 +1196,12 @@ zzt_dense_bf16_v9(ZztArgs a) {
   bool ovf = false;   // sticky per wave, as v4
   auto epi = [&](const f32x16& Y, bf16x8 (&sA)[2]) {   // v4's epilogue, y = -x
     float q[16], lt = 0.f;
-#if SND_ZZT_NRCP
-    // sigma = 1/q by two Newton steps from an integer seed, packed over logit pairs
-    // (A/B: plain VALU, which issues beside the MFMAs, instead of v_rcp_f32; q clamped to
-    // 2^64 for the seed -- sigma below 2^-64 is 0 to the bf16 operand either way)
-#pragma unroll
-    for (int v = 0; v < 16; v += 2) {
-      q[v] = __builtin_amdgcn_exp2f(Y[v]) + 1.f;
-      q[v + 1] = __builtin_amdgcn_exp2f(Y[v + 1]) + 1.f;
-      f32x2 qc = {fminf(q[v], 1.8446744e19f), fminf(q[v + 1], 1.8446744e19f)};
-      f32x2 r = {__uint_as_float(0x7EF311C7u - __float_as_uint(qc[0])),
-                 __uint_as_float(0x7EF311C7u - __float_as_uint(qc[1]))};
-      const f32x2 one = {1.f, 1.f};
-#pragma unroll
-      for (int it = 0; it < 2; ++it) {
-        const f32x2 er = __builtin_elementwise_fma(-qc, r, one);
-        r = __builtin_elementwise_fma(r, er, r);
-      }
-      sA[v >> 3][v & 7] = (__bf16)r[0];
-      sA[v >> 3][(v & 7) + 1] = (__bf16)r[1];
-    }
-#else
 #pragma unroll
     for (int v = 0; v < 16; ++v) {
       const float e = __builtin_amdgcn_exp2f(Y[v]);
       q[v] = e + 1.f;
       sA[v >> 3][v & 7] = (__bf16)__builtin_amdgcn_rcpf(q[v]);
     }
-#endif
 #pragma unroll
     for (int g4 = 0; g4 < 4; ++g4) {
       const unsigned t01 = __builtin_amdgcn_perm(__float_as_uint(Y[4 * g4 + 1]),
