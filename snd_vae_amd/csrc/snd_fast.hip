@@ -18,6 +18,7 @@
 // 512-row chunk and a group of (tap, 16-column) pairs, and writes one
 // deterministic partial slab; snd_reduce sums the slabs in a fixed order.
 #include "snd_fast.hpp"
+#include "snd_gather.hpp"
 #include "snd_pack.hpp"
 
 #include <algorithm>
@@ -173,7 +174,25 @@ __global__ void __launch_bounds__(RCT) rowconv_kernel(RcArgs a) {
     }
     if (!first) __syncthreads();
     // ---- x rows [r0 - H, r0 - H + XR), zero outside [glo, ghi)
-    if (!(kdbg(a.dbg) & 2)) {
+    bool gathered = false;
+    if constexpr (EPI == RC_ENC0 && NBH <= 2) {   // (np <= 64: the wide instances keep their registers)
+      if (a.g_rowptr) {   // x = A @ x rows (T = 1, kp = 64: 8 lanes x 16 B per row)
+        gathered = true;
+        const int rs = tid >> 3, sub = tid & 7;
+        const int gr = r0 + rs;
+        float acc8[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        if (gr < rend) {
+          const __amdgpu_buffer_rsrc_t rsx = rows_rsrc(a.x, (long long)a.R * a.ldx * 2);
+          gather_rows16<1>(a.g_colidx, a.g_rowptr[gr], a.g_rowptr[gr + 1], rsx, 2u * a.ldx, sub,
+                           [&](int, const u32x4 (&v)[1], bool) { acc8v(acc8, v[0]); });
+        }
+        const uint4 o = to_bf16x8(acc8);
+        *reinterpret_cast<uint4*>(xs + rs * kp + ((sub ^ swz(rs, kp)) << 3)) = o;
+        if (gr < rend && 8 * sub < a.K)
+          *reinterpret_cast<uint4*>(reinterpret_cast<__bf16*>(a.gout) + (long long)gr * a.ldgo + 8 * sub) = o;
+      }
+    }
+    if (!gathered && !(kdbg(a.dbg) & 2)) {
       const int kc = 1 << lkc;
       for (int j = w; j < (xch >> 6); j += RCT / 64) {
         const int q = (j << 6) + lane;
@@ -861,12 +880,16 @@ int launch_rowconv(const RcArgs& a0, int epi, hipStream_t s) {
   // windows split further, down to 32 columns (debug bit 1 << 19: off)
   for (;;) {
     const int nb = (int)round_up(cdiv(a.npb, 2), 16);
-    if ((a.dbg & (1 << 19)) || rc_blocks(a.R) * cdiv(a.np, a.npb) >= SND_RC_FILL || nb < 32 || nb >= a.npb) break;
+    if ((a.dbg & (1 << 19)) || a.g_rowptr || rc_blocks(a.R) * cdiv(a.np, a.npb) >= SND_RC_FILL || nb < 32 ||
+        nb >= a.npb) break;
     a.npb = nb;
   }
   SND_CHECK_ARG(a.x && a.wpk && a.out && a.zero && a.x_bf16, "rowconv: null operand / fp32 x");
   SND_CHECK_ARG(!a.colpart || (a.ncp >= 1 && a.ncp <= 4), "rowconv: ncp");
   SND_CHECK_ARG(a.npg > 0, "rowconv: npg");
+  SND_CHECK_ARG(!a.g_rowptr || (epi == RC_ENC0 && a.T == 1 && a.kp == 64 && a.K <= 64 && a.np <= 64 && a.g_colidx &&
+                                a.gout && a.ldgo % 8 == 0 && a.ldx % 8 == 0 && a.npb == a.np),
+                "rowconv: the gathered x rows need RC_ENC0, T 1, kp 64, one column window");
   switch (epi) {
     case RC_LIN: return rc_launch_epi<RC_LIN>(a, s);
     case RC_FWD:

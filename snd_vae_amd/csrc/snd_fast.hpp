@@ -81,6 +81,11 @@ struct RcArgs {
   int npb;                      // image columns per workgroup (set by launch_rowconv: np, or a
                                 // 16-multiple window when the whole image exceeds the LDS budget;
                                 // blockIdx.y selects the window)
+  // RC_ENC0 with T = 1 and a CSR (round 5): the x rows are A @ x, gathered into the LDS
+  // image by the workgroup itself (the register-gather SpMM's fp32 sums in colidx order,
+  // bitwise its output) and also stored to gout [R][ldgo] (bf16) for the weight gradient:
+  // the separate A @ dP1 SpMM launch and its output's re-read disappear
+  const int* g_rowptr; const int* g_colidx; void* gout; int ldgo;
 };
 constexpr int kRcRows = 128;    // rows per workgroup tile
 constexpr size_t kRcLdsLimit = 136 * 1024;   // dynamic LDS (static partials use the rest)

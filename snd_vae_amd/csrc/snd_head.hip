@@ -684,21 +684,23 @@ __global__ void __launch_bounds__(1024) enc_front_kernel(FrontArgs a) {
     sp[4][i] = a.g0[i] * kBnC;
     sp[5][i] = a.b0[i];
   }
-  {   // W1 image [np1][kp1]: element (n, k) = W1[k][n] (pack mode 0)
-    const int kc = a.kp1 >> 3;
-    for (int i = tid; i < a.np1 * kc; i += 1024) {
-      const int c = i % kc, n = i / kc;
-      const int lc = c ^ img_swz(n, a.kp1);
-      bf16x8 v;
+  __syncthreads();   // sp[] (read by the H1 math below)
+  // W1 image [np1][kp1]: element (n, k) = W1[k][n] (pack mode 0).  Its loads are issued
+  // before the A X gather and written to LDS after it, so their latency overlaps the
+  // gather's dependent rowptr -> colidx -> x chain instead of preceding it (np1 * kp1 / 8
+  // <= 1024 chunks: one per thread at the C2 widths, loops otherwise)
+  const int kc = a.kp1 >> 3;
+  const bool w1one = a.np1 * kc <= 1024;
+  float w1v[8];
+  if (w1one && tid < a.np1 * kc) {
+    const int c = tid % kc, n = tid / kc;
+    const int lc = c ^ img_swz(n, a.kp1);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int k = 8 * lc + j;
-        v[j] = (__bf16)((k < K1 && n < a.n1) ? a.w1[k * a.n1 + n] : 0.f);
-      }
-      *reinterpret_cast<bf16x8*>(wimg + n * a.kp1 + 8 * c) = v;
+    for (int j = 0; j < 8; ++j) {
+      const int k = 8 * lc + j;
+      w1v[j] = (k < K1 && n < a.n1) ? a.w1[k * a.n1 + n] : 0.f;
     }
   }
-  __syncthreads();
   // ---- AX for row rs (gcn0_kernel: two neighbours in flight per lane)
   const int rs = tid >> 3, sub = tid & 7;
   const int r = r0 + rs;
@@ -755,6 +757,27 @@ __global__ void __launch_bounds__(1024) enc_front_kernel(FrontArgs a) {
     const uint4 v1 = make_uint4(x1 ? hx.x : 0u, x1 ? hx.y : 0u, x1 ? hx.z : 0u, x1 ? hx.w : 0u);
     if (sub < kc1) *reinterpret_cast<uint4*>(himg + rs * a.kp1 + ((sub ^ hswz(rs, a.kp1)) << 3)) = v0;
     if (sub + 8 < kc1) *reinterpret_cast<uint4*>(himg + rs * a.kp1 + (((sub + 8) ^ hswz(rs, a.kp1)) << 3)) = v1;
+  }
+  if (w1one) {
+    if (tid < a.np1 * kc) {
+      const int c = tid % kc, n = tid / kc;
+      bf16x8 v;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = (__bf16)w1v[j];
+      *reinterpret_cast<bf16x8*>(wimg + n * a.kp1 + 8 * c) = v;
+    }
+  } else {
+    for (int i = tid; i < a.np1 * kc; i += 1024) {
+      const int c = i % kc, n = i / kc;
+      const int lc = c ^ img_swz(n, a.kp1);
+      bf16x8 v;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int k = 8 * lc + j;
+        v[j] = (__bf16)((k < K1 && n < a.n1) ? a.w1[k * a.n1 + n] : 0.f);
+      }
+      *reinterpret_cast<bf16x8*>(wimg + n * a.kp1 + 8 * c) = v;
+    }
   }
   if (rv && !(kdbg(a.dbg) & 8)) {
     if (sub < nch) *reinterpret_cast<uint4*>(a.h1 + (long long)r * a.ldh1 + 8 * sub) = hd;

@@ -95,6 +95,7 @@ struct snd_plan {
   bool head_fused = false;     // fused encoder forward tail (snd_head.hip): 1 launch instead of 4
   bool head_bwd = false;       // fused edge terms + encoder backward head (snd_head.hip): 1 instead of 4
   bool front_fused = false;    // gcn0 + H1 W1 + the weight images in one launch (snd_head.hip)
+  bool enc0_gather = false;    // A @ dP1 gathered inside the RC_ENC0 launch (no SpMM launch)
   bool small_head = false;     // graph latent: [mu || s] head + reparameterisation (snd_elem.hip small_head_*)
   int ldh1 = 0, ldg = 0;
   Img pw1f{}, pwhf{}, pwmsf{}, pwmsb{}, pwhb{}, pw1b{};
@@ -529,6 +530,9 @@ extern "C" int snd_plan_create(const snd_config_t* cfg, int n_graphs, snd_plan_t
   // GraphConvolution 0, XW1 and the packed weight images in one launch (debug bit 1048576:
   // pack + gcn0 + a row-engine launch)
   p->front_fused = p->fast_enc && !(dbg & 1048576) && front_supported(c.f_in, c.h0, c.h1, p->pw1f.kp, p->pw1f.np);
+  // the GCN1 backward SpMM A @ dP1 inside the RC_ENC0 launch that consumes it (round 5;
+  // debug bit 128: the separate SpMM launch)
+  p->enc0_gather = p->fast_enc && !(dbg & 128) && c.h1 == 64 && p->pw1b.kp == 64 && c.f_in <= 4;
   set_zzt_splits(*p);
   *out = p;
   return 0;
@@ -1123,17 +1127,31 @@ int encoder_fast_bwd_tail(const Ctx& x, const snd_batch_t* batch, bool enc1_done
     a.out = bf("FDP1"); a.ldo = h1; a.out_bf16 = 1; a.colpart = x.f("PFENC1"); a.ncp = 4;
     SND_TRY(launch_rowconv(a, RC_ENC1, x.s));
   }
-  SND_TRY(spmm_bf16_plain(batch, R, p.N, p.B, bf("FDP1"), h1, h1, bf("FDXW1"), h1, x.s));
-  SND_TRY(fork(x));
-  SND_TRY(wgrad(x, wg_args(p, x.ws, p.gW1, bf("FH1"), p.ldh1, p.kw1, bf("FDXW1"), h1, h1, x.f("FSW1"), 1), side(x)));
-  if (p.kw1 < h0 + f)
-    SND_TRY(wgrad(x, wg_args(p, x.ws, p.gW1t, bf("FH1") + p.kw1, p.ldh1, h0 + f - p.kw1, bf("FDXW1"), h1, h1,
-                             x.f("FSW1T"), 1), side(x)));
+  auto w1grad = [&]() -> int {
+    SND_TRY(wgrad(x, wg_args(p, x.ws, p.gW1, bf("FH1"), p.ldh1, p.kw1, bf("FDXW1"), h1, h1, x.f("FSW1"), 1), side(x)));
+    if (p.kw1 < h0 + f)
+      SND_TRY(wgrad(x, wg_args(p, x.ws, p.gW1t, bf("FH1") + p.kw1, p.ldh1, h0 + f - p.kw1, bf("FDXW1"), h1, h1,
+                               x.f("FSW1T"), 1), side(x)));
+    return 0;
+  };
+  if (!p.enc0_gather) {
+    SND_TRY(spmm_bf16_plain(batch, R, p.N, p.B, bf("FDP1"), h1, h1, bf("FDXW1"), h1, x.s));
+    SND_TRY(fork(x));
+    SND_TRY(w1grad());
+  }
   {
-    RcArgs a = rc_args(p, x.ws, p.pw1b, bf("FDXW1"), h1, h1, h0, colmap_plain(h0));
+    RcArgs a = rc_args(p, x.ws, p.pw1b, p.enc0_gather ? (const void*)bf("FDP1") : (const void*)bf("FDXW1"), h1, h1,
+                       h0, colmap_plain(h0));
     a.gamma = x.w("enc.bn0.gamma"); a.p = x.f("AX"); a.ldp = 4; a.w0 = x.w("enc.W0"); a.f = f;
     a.out = bf("FDP0"); a.ldo = h0; a.out_bf16 = 1; a.colpart = x.f("PFENC0"); a.ncp = 2;
+    if (p.enc0_gather) {   // dXW1 = A @ dP1 gathered by the launch (and stored for dW1)
+      a.g_rowptr = batch->rowptr; a.g_colidx = batch->colidx; a.gout = bf("FDXW1"); a.ldgo = h1;
+    }
     SND_TRY(launch_rowconv(a, RC_ENC0, x.s));
+  }
+  if (p.enc0_gather) {
+    SND_TRY(fork(x));
+    SND_TRY(w1grad());
   }
   SND_TRY(fork(x));
   return wgrad(x, wg_args(p, x.ws, p.gW0, bf("AXB"), 8, f, bf("FDP0"), h0, h0, x.f("FSW0"), 1), side(x));

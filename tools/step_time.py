@@ -22,6 +22,7 @@ def main():
     ap.add_argument("--eager", type=int, default=0, help="run N eager steps (for rocprof) and exit")
     ap.add_argument("--option", action="append", default=[], help="plan option name=value")
     ap.add_argument("--tag", default="")
+    ap.add_argument("--debug", type=int, default=0, help="snd_debug_set bits before the plan is built (A/B)")
     args = ap.parse_args()
     root = os.path.abspath(args.root)
     sys.path.insert(0, root)
@@ -32,6 +33,9 @@ def main():
     from snd_vae_amd.optimizer import OptimizerVAE
     import snd_vae_amd
     assert os.path.dirname(os.path.abspath(snd_vae_amd.__file__)).startswith(root), snd_vae_amd.__file__
+    if args.debug:
+        from snd_vae_amd import _lib
+        _lib.lib().snd_debug_set(args.debug)
     cfg = PRESETS[args.config] if args.config else tscale(args.nodes, args.latent)
     host = synthetic_batch(cfg, args.graphs, seed=1000)
     db = DeviceBatch(host, tile_rows=default_tile_rows(cfg.g_conv_hidden[1]))
