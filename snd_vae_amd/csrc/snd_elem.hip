@@ -406,6 +406,15 @@ __global__ void __launch_bounds__(256) reduce_kernel(ReducePack pk, FinalizeArgs
     i = (int)(j - (long long)r * d.len);
     const float* src = d.src + (long long)r * d.src_rs + i;
     int p = pl;
+    // 8 loads in flight per round (the 64-part weight slabs at 8 part lanes: one round
+    // trip instead of two); the adds stay in part order
+    for (; p + 7 * PL < d.nparts; p += 8 * PL) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = src[(long long)(p + u * PL) * d.stride];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) acc += (double)v[u];
+    }
     for (; p + 3 * PL < d.nparts; p += 4 * PL) {
       const float v0 = src[(long long)p * d.stride];
       const float v1 = src[(long long)(p + PL) * d.stride];
