@@ -105,7 +105,14 @@ __global__ void __launch_bounds__(RCT) rowconv_kernel(RcArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int li = lane & 15, lg = lane >> 4;
   const int rb = w & 7, nb0 = NBH * (w >> 3);
-  const int r0 = blockIdx.x * kRcRows;
+  // tile of this workgroup: natural order, or XCD-aware when the launch gathers its x rows
+  // (graph g's tiles on block group g % 8, so the gathered rows stay in one L2)
+  int tb = blockIdx.x;
+  if (EPI == RC_ENC0 && a.g_rowptr && a.npg % kRcRows == 0 && (a.R / a.npg) % 8 == 0) {
+    const int tpg = a.npg / kRcRows, x = tb & 7, sq = tb >> 3, g8 = sq / tpg;
+    tb = (x + 8 * g8) * tpg + (sq - g8 * tpg);
+  }
+  const int r0 = tb * kRcRows;
   const int rend = min(r0 + kRcRows, a.R);
   // column window of this workgroup: image columns [nbase, nbase + nloc); LDS, colp and
   // cps are indexed by the local column, global memory by nbase + local
@@ -404,7 +411,7 @@ __global__ void __launch_bounds__(RCT) rowconv_kernel(RcArgs a) {
         float t = 0.f;
 #pragma unroll
         for (int b = 0; b < 8; ++b) t += cps[b][q][nl];
-        a.colpart[((long long)blockIdx.x * NCP + q) * a.N + n] = t;
+        a.colpart[((long long)tb * NCP + q) * a.N + n] = t;
       }
     }
   }

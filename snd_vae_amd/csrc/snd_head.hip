@@ -118,7 +118,16 @@ __global__ void __launch_bounds__(HR * 8) head_fwd_kernel(HeadFwdArgs a) {
   const int L = a.L, sxs = L + 4, zts = L + 1;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int tpg = a.npad / HR;
-  const int gi = blockIdx.x / tpg, lt = blockIdx.x - gi * tpg;
+  // XCD-aware tile order (as head_bwd and the gather kernels): blocks b and b + 8 share an
+  // XCD, so graph g's tiles go to block group g % 8 and its gathered XW1 rows stay in one L2
+  // (natural order spread every graph over all 8 L2s: 32 MB fetched per launch)
+  int tb = blockIdx.x;
+  if (a.ngraphs % 8 == 0 && a.ngraphs > 0) {
+    const int x = tb & 7, sq = tb >> 3;
+    const int g8 = sq / tpg;
+    tb = (x + 8 * g8) * tpg + (sq - g8 * tpg);
+  }
+  const int gi = tb / tpg, lt = tb - gi * tpg;
   const int lr0 = lt * HR;                          // first row of the tile in its graph
   const long long gr0 = (long long)gi * a.npg;      // the graph's first global row
 
