@@ -79,7 +79,7 @@ inline int device_cu_count() {
 // cancellation of 1 + 2s - e^{2s}, which is O(s^2) near the initial s ~ 0 (round 4:
 // the fp32 kl term 6.8e-6 off the float64 oracle at C2):  -(expm1(2s) - 2s) - mu^2, the
 // bracket as the Taylor series x^2/2! + ... + x^10/10! for |x| = |2s| < 1/2 (truncation
-// < 3e-10 relative) and expm1f(x) - x above (no cancellation there beyond ~2 bits).
+// < 3e-10 relative) and (e^x - 1) - x above (no cancellation there beyond ~2 bits).
 __device__ __forceinline__ float kl_elem(float s, float mu) {
   const float x = 2.f * s;
   float r;
@@ -94,8 +94,9 @@ __device__ __forceinline__ float kl_elem(float s, float mu) {
     t = __fmaf_rn(t, x, 1.f / 6.f);
     t = __fmaf_rn(t, x, 0.5f);
     r = __fmul_rn(__fmul_rn(x, x), t);
-  } else {
-    r = __fsub_rn(expm1f(x), x);
+  } else {   // no cancellation in e^x - 1 here; __expf (v_exp_f32) like the old form, so
+             // every kernel evaluates the element bit for bit alike
+    r = __fsub_rn(__fsub_rn(__expf(x), 1.f), x);
   }
   return __fsub_rn(-r, __fmul_rn(mu, mu));
 }

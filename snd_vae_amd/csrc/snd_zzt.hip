@@ -1139,12 +1139,6 @@ zzt_dense_bf16_v9(ZztArgs a) {
              __builtin_amdgcn_readfirstlane(lds0 + b * IMG + 1024 * (w + 8 * k)));
   };
 
-#ifdef SND_ZZT_V9_SLEEP
-  // A/B: the second half of the grid (the second workgroup of each CU, by dispatch
-  // order) starts SND_ZZT_V9_SLEEP x 64 cycles late, so the two workgroups of a CU
-  // run their tiles out of phase (one's epilogue VALU beside the other's MFMAs)
-  if ((int)blockIdx.x >= (int)(gridDim.x >> 1)) __builtin_amdgcn_s_sleep(SND_ZZT_V9_SLEEP);
-#endif
   // ---- prologue: tile t0 in flight; -z_i rows; column sums
   dma(t0, 0);
   for (int idx = tid; idx < ROWS9 * (DP / 8); idx += NT) {
