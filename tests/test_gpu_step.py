@@ -438,7 +438,10 @@ def test_fused_encoder_head_matches_chain(n, d, B):
     h = G Wh + bh, [mu | s] = h Wms + bms, reparameterisation and the zz^T staging images in
     one launch) against the four-launch chain (debug bit 65536): P1, G, h, [mu | s], z,
     eps and the staging images are bitwise equal, so is everything downstream (dJ, dP1);
-    the KL partials group rows differently (fp64 sums: the losses agree to 1e-12).
+    the KL partials group rows differently (fp64 sums: the losses agree to 1e-12; the KL term
+    alone to 1e-9 since round 5, whose per-element KL is the cancellation-free
+    -(expm1(2s) - 2s) - mu^2 with full fp32 mantissas instead of values quantized to the
+    O(1) terms' ulp, so the grouping of the fp64 sums shows: 2.5e-11 measured).
     N = 300 covers partial 128-row tiles, d = 32 the narrower heads."""
     from snd_vae_amd import _lib
     from snd_vae_amd.params import init_blocks
@@ -460,7 +463,7 @@ def test_fused_encoder_head_matches_chain(n, d, B):
         assert torch.equal(m0.buffer(name, dt), m1.buffer(name, dt)), name
     l0, l1 = o0.loss_dict(), o1.loss_dict()
     for k in ("cost", "adj_cost", "kl", "acc"):
-        assert l1[k] == pytest.approx(l0[k], rel=1e-12, abs=1e-15), k
+        assert l1[k] == pytest.approx(l0[k], rel=1e-9 if k == "kl" else 1e-12, abs=1e-15), k
     g0, g1 = o0.grad_blocks(), o1.grad_blocks()
     for k in g0:
         np.testing.assert_allclose(g1[k], g0[k], rtol=1e-5, atol=1e-6 * max(1.0, np.abs(g0[k]).max()), err_msg=k)
@@ -494,7 +497,7 @@ def test_fused_backward_head_matches_chain(n, d, B):
         assert torch.equal(m0.buffer(name, dt), m1.buffer(name, dt)), name
     l0, l1 = o0.loss_dict(), o1.loss_dict()
     for k in ("cost", "adj_cost", "kl", "acc"):
-        assert l1[k] == pytest.approx(l0[k], rel=1e-12, abs=1e-15), k
+        assert l1[k] == pytest.approx(l0[k], rel=1e-9 if k == "kl" else 1e-12, abs=1e-15), k
     g0, g1 = o0.grad_blocks(), o1.grad_blocks()
     for k in g0:
         if k == "enc.bms":
