@@ -486,7 +486,8 @@ __device__ __forceinline__ void wgrad_body(const WgArgs& a, const int bx, const 
   const int kpy = a.N <= 32 ? 32 : (a.N <= 64 ? 64 : 128);
   const int xch = ((XR << log2kc(kpx)) + 63) & ~63;
   const int bufe = (xch << 3) + kRcRows * kpy;          // elements per staging buffer
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  // the wave index as a scalar: the pair bookkeeping below stays in SGPRs
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int li = lane & 15, lg = lane >> 4, tq = li >> 2, tp = li & 3;
   const int cbn = (a.K + 15) >> 4;
   const int P = T * cbn;
@@ -545,9 +546,9 @@ __device__ __forceinline__ void wgrad_body(const WgArgs& a, const int bx, const 
     xoff2[i] = tr_off(rk0 + ts[i] + 4, 16 * cbs[i] + 4 * tp, kpx);   // + t may carry into bit 3
   }
   const int doff = rk0 * kpy;
-  int dobo[NBO];
-#pragma unroll
-  for (int ob = 0; ob < NBO; ++ob) dobo[ob] = tr_off(rk0, 16 * ob + 4 * tp, kpy) - doff;
+  // dy piece of column block ob: ((2 ob + tp / 2) ^ swd) << 3 | (4 tp & 4), formed at
+  // each use (NBO offsets held across the loop cost the registers 8 waves/SIMD lack)
+  const int swd = trsw(rk0, kpy), tpl = (4 * tp) & 4, tph = tp >> 1;
   if (c0 < c1) {
     WgUnit u = wg_unit(a, c0, c0, c1);
     stage(u, 0);
@@ -574,7 +575,8 @@ __device__ __forceinline__ void wgrad_body(const WgArgs& a, const int bx, const 
           for (int i = 0; i < NPW; ++i) bxv[i] = tr_pair(xb + xoff[i], xb + xoff2[i]);
 #pragma unroll
           for (int ob = 0; ob < NBO; ++ob) {
-            const bf16x8 af = tr_pair(db + dobo[ob], db + dobo[ob] + 4 * kpy);
+            const int dob = (((2 * ob + tph) ^ swd) << 3) | tpl;
+            const bf16x8 af = tr_pair(db + dob, db + dob + 4 * kpy);
 #pragma unroll
             for (int i = 0; i < NPW; ++i)
               if (i == 0 || pvs[i]) acc[i][ob] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bxv[i], acc[i][ob], 0, 0, 0);
@@ -587,13 +589,14 @@ __device__ __forceinline__ void wgrad_body(const WgArgs& a, const int bx, const 
   }
   // D[m = n (dy col)][n = k (x col)]: lane holds k = 16cb + li, n = 16ob + 4lg + e
   if (kdbg(a.dbg) & 8) return;
-  // slab rows padded to a multiple of 4 floats: every store is a float4
-  const int n4 = (a.N + 3) & ~3;
+  // slab rows padded to a multiple of 4 floats: every store is a float4; a window
+  // (sK, sn4, wk0, wn0) writes its block of the whole weight's slab
+  const int sK = a.sK, sn4 = a.sn4;
 #pragma unroll
   for (int i = 0; i < NPW; ++i) {
     const int k = 16 * cbs[i] + li;
     if (!pvs[i] || k >= a.K) continue;
-    float* row = a.slab + (long long)bx * T * a.K * n4 + ((long long)ts[i] * a.K + k) * n4;
+    float* row = a.slab + (long long)bx * T * sK * sn4 + ((long long)ts[i] * sK + a.wk0 + k) * sn4 + a.wn0;
 #pragma unroll
     for (int ob = 0; ob < NBO; ++ob) {
       const int n0 = 16 * ob + 4 * lg;
@@ -621,7 +624,11 @@ struct WgMultiPack {
   int nseg;
 };
 
-__global__ void __launch_bounds__(WGT) wgrad_multi_kernel(WgMultiPack m) {
+// Every segment is at most 64 columns of dy wide (launch_wgrad_multi splits wider ones)
+// and its staging at most 68 KB: the kernel is built for 8 waves per SIMD (<= 64 VGPRs),
+// two workgroups per CU.
+__global__ void __launch_bounds__(WGT) __attribute__((amdgpu_waves_per_eu(8, 8)))
+wgrad_multi_kernel(WgMultiPack m) {
   extern __shared__ __attribute__((aligned(16))) __bf16 lds[];
   int s = 0;
   while (s + 1 < m.nseg && (int)blockIdx.x >= m.start[s + 1]) ++s;
@@ -635,11 +642,7 @@ __global__ void __launch_bounds__(WGT) wgrad_multi_kernel(WgMultiPack m) {
     case 1: if (two) wgrad_body<1, 2>(a, bx, by, lds); else wgrad_body<1>(a, bx, by, lds); break;
     case 2: if (two) wgrad_body<2, 2>(a, bx, by, lds); else wgrad_body<2>(a, bx, by, lds); break;
     case 3: if (two) wgrad_body<3, 2>(a, bx, by, lds); else wgrad_body<3>(a, bx, by, lds); break;
-    case 4: if (two) wgrad_body<4, 2>(a, bx, by, lds); else wgrad_body<4>(a, bx, by, lds); break;
-    case 5: if (two) wgrad_body<5, 2>(a, bx, by, lds); else wgrad_body<5>(a, bx, by, lds); break;
-    case 6: if (two) wgrad_body<6, 2>(a, bx, by, lds); else wgrad_body<6>(a, bx, by, lds); break;
-    case 7: if (two) wgrad_body<7, 2>(a, bx, by, lds); else wgrad_body<7>(a, bx, by, lds); break;
-    default: if (two) wgrad_body<8, 2>(a, bx, by, lds); else wgrad_body<8>(a, bx, by, lds); break;
+    default: if (two) wgrad_body<4, 2>(a, bx, by, lds); else wgrad_body<4>(a, bx, by, lds); break;
   }
 }
 
@@ -915,29 +918,68 @@ int launch_rowconv(const RcArgs& a0, int epi, hipStream_t s) {
   }
 }
 
+// a descriptor's own slab geometry (sK, sn4 = 0: the whole weight at origin 0)
+static WgArgs wg_norm(const WgArgs& a) {
+  WgArgs x = a;
+  if (x.sK == 0) { x.sK = x.K; x.sn4 = wgrad_n4(x.N); x.wk0 = 0; x.wn0 = 0; }
+  return x;
+}
+
+// Column windows of 64: over dy always, over x when the double-buffered staging would
+// need more than kWgSplitLds.  With every segment at <= 68 KB of LDS and <= 64 VGPRs two
+// 1024-thread workgroups share a CU, and one's LDS-DMA round trip hides under the
+// other's MFMAs.  Each window stages its own x / dy columns and writes its block of the
+// same slab, so the reduction is unchanged.
+constexpr size_t kWgSplitLds = 80 * 1024;
+static int wg_split(const WgArgs& a, WgArgs* out, int cap) {
+  // n: always (the multi kernel is built for <= 4 column blocks); k: over the LDS budget
+  const bool sk = a.K > 64 && wg_lds_bytes(a.T, a.K, std::min(a.N, 64)) > kWgSplitLds, sn = a.N > 64;
+  int n = 0;
+  for (int k0 = 0; k0 < a.K; k0 += sk ? 64 : a.K)
+    for (int n0 = 0; n0 < a.N; n0 += sn ? 64 : a.N) {
+      if (n >= cap) return -1;
+      WgArgs w = a;
+      w.K = sk ? std::min(64, a.K - k0) : a.K;
+      w.N = sn ? std::min(64, a.N - n0) : a.N;
+      w.x = static_cast<const __bf16*>(a.x) + k0;
+      w.dy = static_cast<const __bf16*>(a.dy) + n0;
+      w.wk0 = a.wk0 + k0; w.wn0 = a.wn0 + n0;
+      w.pairs_per_wg = std::min(a.pairs_per_wg, a.T * cdiv(w.K, 16));
+      out[n++] = w;
+    }
+  return n;
+}
+
 int launch_wgrad_multi(const WgArgs* a, int n, hipStream_t s) {
   if (n <= 0) return 0;
-  SND_CHECK_ARG(n <= kMaxWgMulti, "wgrad_multi: at most %d segments", kMaxWgMulti);
   WgMultiPack pk{};
   size_t lds = 0;
   int total = 0;
   pk.nseg = 0;
   for (int i = 0; i < n; ++i) {
-    const WgArgs& x = a[i];
-    if (x.R <= 0) continue;
-    SND_CHECK_ARG(x.T == 1 || x.T == 5, "wgrad_multi: T must be 1 or 5");
-    SND_CHECK_ARG(x.K > 0 && x.K <= 128 && x.N > 0 && x.N <= 128, "wgrad_multi: K %d N %d", x.K, x.N);
-    SND_CHECK_ARG(x.ldx % 8 == 0 && x.lddy % 8 == 0 && x.x_bf16 && x.dy_bf16,
+    const WgArgs x0 = wg_norm(a[i]);
+    if (x0.R <= 0) continue;
+    SND_CHECK_ARG(x0.T == 1 || x0.T == 5, "wgrad_multi: T must be 1 or 5");
+    SND_CHECK_ARG(x0.K > 0 && x0.K <= 128 && x0.N > 0 && x0.N <= 128, "wgrad_multi: K %d N %d", x0.K, x0.N);
+    SND_CHECK_ARG(x0.ldx % 8 == 0 && x0.lddy % 8 == 0 && x0.x_bf16 && x0.dy_bf16,
                   "wgrad_multi: bf16 operands with leading dims %% 8");
-    SND_CHECK_ARG(x.rows_per_wg % kRcRows == 0 && x.pairs_per_wg >= 1 && x.pairs_per_wg <= 2 * WGT / 64,
+    SND_CHECK_ARG(x0.rows_per_wg % kRcRows == 0 && x0.pairs_per_wg >= 1 && x0.pairs_per_wg <= 2 * WGT / 64,
                   "wgrad_multi: geometry");
-    SND_CHECK_ARG(x.x && x.dy && x.slab && x.zero && x.npg > 0, "wgrad_multi: null operand");
-    const int P = x.T * cdiv(x.K, 16);
-    pk.a[pk.nseg] = x;
-    pk.start[pk.nseg] = total;
-    total += cdiv(x.R, x.rows_per_wg) * cdiv(P, x.pairs_per_wg);
-    lds = std::max(lds, wg_lds_bytes(x.T, x.K, x.N));
-    ++pk.nseg;
+    SND_CHECK_ARG(x0.x && x0.dy && x0.slab && x0.zero && x0.npg > 0, "wgrad_multi: null operand");
+    SND_CHECK_ARG(x0.sn4 % 4 == 0 && x0.wn0 % 4 == 0 && x0.wk0 + x0.K <= x0.sK &&
+                  x0.wn0 + wgrad_n4(x0.N) <= x0.sn4, "wgrad_multi: slab window");
+    WgArgs win[4];
+    const int nw = wg_split(x0, win, 4);
+    SND_CHECK_ARG(nw > 0 && pk.nseg + nw <= kMaxWgMulti, "wgrad_multi: at most %d segments", kMaxWgMulti);
+    for (int j = 0; j < nw; ++j) {
+      const WgArgs& x = win[j];
+      const int P = x.T * cdiv(x.K, 16);
+      pk.a[pk.nseg] = x;
+      pk.start[pk.nseg] = total;
+      total += cdiv(x.R, x.rows_per_wg) * cdiv(P, x.pairs_per_wg);
+      lds = std::max(lds, wg_lds_bytes(x.T, x.K, x.N));
+      ++pk.nseg;
+    }
   }
   if (pk.nseg == 0) return 0;
   pk.start[pk.nseg] = total;
@@ -966,7 +1008,8 @@ WgGeom wgrad_geom(int R, int T, int K, int N, int chunks) {
   return g;
 }
 
-int launch_wgrad(const WgArgs& a, hipStream_t s) {
+int launch_wgrad(const WgArgs& a0, hipStream_t s) {
+  const WgArgs a = wg_norm(a0);
   if (a.R <= 0) return 0;
   SND_CHECK_ARG(a.T == 1 || a.T == 5, "wgrad: T must be 1 or 5");
   SND_CHECK_ARG(a.K > 0 && a.K <= 128 && a.N > 0 && a.N <= 128, "wgrad: K %d N %d", a.K, a.N);

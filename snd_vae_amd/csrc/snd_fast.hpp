@@ -109,6 +109,10 @@ struct WgArgs {
   float* slab;
   const void* zero;             // >= 16 zero bytes in device memory
   int dbg;
+  // slab geometry of the whole weight when this descriptor is a (k, n) window of it
+  // (launch_wgrad_multi's LDS split): rows sK, padded width sn4, window origin
+  // (wk0, wn0); 0 = the descriptor's own K / n4(N) at origin 0
+  int sK, sn4, wk0, wn0;
 };
 struct WgGeom { int rows_per_wg, pairs_per_wg, gx, gy; };
 // chunks > 0: that many row chunks per weight (the step's multi-segment launch);
@@ -117,7 +121,7 @@ WgGeom wgrad_geom(int R, int T, int K, int N, int chunks = 0);
 inline int wgrad_n4(int N) { return (N + 3) & ~3; }
 int launch_wgrad(const WgArgs& a, hipStream_t s);
 // n independent weight gradients (each its own geometry and slab) in one launch
-constexpr int kMaxWgMulti = 12;
+constexpr int kMaxWgMulti = 24;   // segments after the column-window split
 int launch_wgrad_multi(const WgArgs* a, int n, hipStream_t s);
 
 // ---- fused sigmoid head + MSE + backward + BN/lrelu backward of the head's

@@ -24,6 +24,7 @@ def main():
     ap.add_argument("--config", default="", help="preset (C4, C5, ...) instead of --nodes/--latent")
     ap.add_argument("--adam-per-range", action="store_true",
                     help="A/B: one snd_adam_tf1 launch per unfused range instead of snd_adam_tf1_ranges")
+    ap.add_argument("--debug", default="", help="comma list of snd_debug_set bits: each kernel is timed under each")
     args = ap.parse_args()
     import torch
 
@@ -57,8 +58,12 @@ def main():
     out = {"tag": args.tag, "step_ms": round(e0.elapsed_time(e1) / args.steps, 5),
            "losses": {k: round(v, 6) for k, v in opt.loss_dict().items()}}
     km = bench.kernel_timer(model, db.c_struct(), args.reps)
-    for k in [k for k in args.kernels.split(",") if k]:
-        out[k + "_us"] = round(1000 * min(km(k) for _ in range(3)), 2)
+    for d in [int(v) for v in args.debug.split(",") if v] or [None]:
+        if d is not None:   # measurement library (-DSND_MEAS=1): phase-skip bits at launch time
+            _lib.lib().snd_debug_set(d)
+        sfx = "" if d is None else f"_dbg{d}"
+        for k in [k for k in args.kernels.split(",") if k]:
+            out[k + sfx + "_us"] = round(1000 * min(km(k) for _ in range(3)), 2)
     print(json.dumps(out), flush=True)
 
 
