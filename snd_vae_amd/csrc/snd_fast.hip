@@ -545,6 +545,7 @@ __device__ __forceinline__ void wgrad_body(const WgArgs& a, const int bx, const 
     xoff[i] = tr_off(rk0 + ts[i], 16 * cbs[i] + 4 * tp, kpx);
     xoff2[i] = tr_off(rk0 + ts[i] + 4, 16 * cbs[i] + 4 * tp, kpx);   // + t may carry into bit 3
   }
+  if (kdbg(a.dbg) & 32) return;   // measurement only: the prologue alone
   const int doff = rk0 * kpy;
   // dy piece of column block ob: ((2 ob + tp / 2) ^ swd) << 3 | (4 tp & 4), formed at
   // each use (NBO offsets held across the loop cost the registers 8 waves/SIMD lack)
@@ -639,6 +640,7 @@ wgrad_multi_kernel(WgMultiPack m) {
   const int gx = cdiv_d(a.R, a.rows_per_wg);
   const int bx = local % gx, by = local / gx;
   const bool two = a.pairs_per_wg > WGT / 64;
+  if (kdbg(a.dbg) & 16) return;   // measurement only: launch + segment lookup
   switch ((a.N + 15) >> 4) {
     case 1: if (two) wgrad_body<1, 2>(a, bx, by, lds); else wgrad_body<1>(a, bx, by, lds); break;
     case 2: if (two) wgrad_body<2, 2>(a, bx, by, lds); else wgrad_body<2>(a, bx, by, lds); break;
