@@ -381,8 +381,12 @@ __global__ void __launch_bounds__(256) reduce_kernel(ReducePack pk, FinalizeArgs
     if (blockIdx.x == 0) { finalize_block<256>(fin); return; }
   }
   const int bid = (int)blockIdx.x - (FIN ? 1 : 0);
+  // descriptor of this block: the count of later starts <= bid (bstart is non-decreasing,
+  // unused entries hold the total): independent scalar loads, no dependent search chain
   int di = 0;
-  while (di + 1 < kMaxReduce && bid >= pk.bstart[di + 1]) ++di;   // uniform
+#pragma unroll
+  for (int i = 1; i < kMaxReduce; ++i) di += bid >= pk.bstart[i] ? 1 : 0;
+  di = __builtin_amdgcn_readfirstlane(di);
   const ReduceDesc& d = pk.d[di];
   const int bx = bid - pk.bstart[di];
   // bias-corrected step size (snd_adam_tf1's arithmetic), while the slab loads are in flight

@@ -632,8 +632,11 @@ __global__ void __launch_bounds__(WGT) __attribute__((amdgpu_waves_per_eu(8, 8))
 wgrad_multi_kernel(WgMultiPack m) {
   extern __shared__ __attribute__((aligned(16))) __bf16 lds[];
   if (kdbg(m.a[0].dbg) & 1) return;   // measurement only: the launch alone
+  // segment of this block: independent scalar loads of the starts (entries past nseg hold
+  // the grid size), no dependent search chain
   int s = 0;
-  while (s + 1 < m.nseg && (int)blockIdx.x >= m.start[s + 1]) ++s;
+#pragma unroll
+  for (int i = 1; i < kMaxWgMulti; ++i) s += (int)blockIdx.x >= m.start[i] ? 1 : 0;
   s = __builtin_amdgcn_readfirstlane(s);
   const WgArgs a = m.a[s];   // by value: field reads stay scalar loads from the kernarg segment
   const int local = blockIdx.x - m.start[s];
@@ -985,7 +988,7 @@ int launch_wgrad_multi(const WgArgs* a, int n, hipStream_t s) {
     }
   }
   if (pk.nseg == 0) return 0;
-  pk.start[pk.nseg] = total;
+  for (int i = pk.nseg; i <= kMaxWgMulti; ++i) pk.start[i] = total;
   hipLaunchKernelGGL(wgrad_multi_kernel, dim3(total), dim3(WGT), lds, s, pk);
   SND_LAUNCH_CHECK("wgrad_multi_kernel");
   return 0;
