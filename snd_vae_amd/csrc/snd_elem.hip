@@ -363,8 +363,11 @@ __global__ void __launch_bounds__(256) enc_bwd_kernel(EncBwdArgs a, int rows) {
 // part lanes of a descriptor (uniform per block): a thread sums nparts / PL parts in a
 // dependent chain, so the many-part partials (C4's split-K head / projection slabs, ~1000
 // parts) take wider lane groups and more blocks
+#ifndef SND_RED_PLS
+#define SND_RED_PLS 4  // part lanes of a < 64-part partial
+#endif
 __host__ __device__ __forceinline__ int red_pl(int nparts) {
-  return nparts >= 1024 ? 64 : (nparts >= 256 ? 32 : (nparts >= 64 ? SND_RED_PL : 4));
+  return nparts >= 1024 ? 64 : (nparts >= 256 ? 32 : (nparts >= 64 ? SND_RED_PL : SND_RED_PLS));
 }
 struct ReducePack {
   ReduceDesc d[kMaxReduce];
