@@ -358,7 +358,8 @@ __global__ void __launch_bounds__(256) enc_bwd_kernel(EncBwdArgs a, int rows) {
 
 // ---------------------------------------------------------------- reduce
 #ifndef SND_RED_PL
-#define SND_RED_PL 8   // part lanes of a >= 64-part slab (C2 step 0.2368 vs 0.2389 ms at 16, 0.2380 at 4)
+#define SND_RED_PL 2   // part lanes of a >= 64-part slab (round 5, C2 step on one box: 0.2220 ms at 2,
+                       // 0.2228 at 4, 0.2226 at 1; another box: 0.2210 at 4 vs 0.2236 at 8, 0.2300 at 16)
 #endif
 // part lanes of a descriptor (uniform per block): a thread sums nparts / PL parts in a
 // dependent chain, so the many-part partials (C4's split-K head / projection slabs, ~1000

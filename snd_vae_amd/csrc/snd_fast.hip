@@ -624,6 +624,7 @@ struct WgMultiPack {
   int start[kMaxWgMulti + 1];
   int nseg;
 };
+static_assert(sizeof(WgMultiPack) <= 4096, "wgrad_multi: kernel arguments over 4 KB");
 
 // Every segment is at most 64 columns of dy wide (launch_wgrad_multi splits wider ones)
 // and its staging at most 68 KB: the kernel is built for 8 waves per SIMD (<= 64 VGPRs),
@@ -956,6 +957,15 @@ static int wg_split(const WgArgs& a, WgArgs* out, int cap) {
   return n;
 }
 
+static int wg_multi_flush(WgMultiPack& pk, int total, size_t lds, hipStream_t s) {
+  if (pk.nseg == 0) return 0;
+  for (int i = pk.nseg; i <= kMaxWgMulti; ++i) pk.start[i] = total;
+  hipLaunchKernelGGL(wgrad_multi_kernel, dim3(total), dim3(WGT), lds, s, pk);
+  SND_LAUNCH_CHECK("wgrad_multi_kernel");
+  return 0;
+}
+
+// one launch per kMaxWgMulti segments (C2: 13 segments after the window split, one launch)
 int launch_wgrad_multi(const WgArgs* a, int n, hipStream_t s) {
   if (n <= 0) return 0;
   WgMultiPack pk{};
@@ -976,8 +986,14 @@ int launch_wgrad_multi(const WgArgs* a, int n, hipStream_t s) {
                   x0.wn0 + wgrad_n4(x0.N) <= x0.sn4, "wgrad_multi: slab window");
     WgArgs win[4];
     const int nw = wg_split(x0, win, 4);
-    SND_CHECK_ARG(nw > 0 && pk.nseg + nw <= kMaxWgMulti, "wgrad_multi: at most %d segments", kMaxWgMulti);
+    SND_CHECK_ARG(nw > 0, "wgrad_multi: window split");
     for (int j = 0; j < nw; ++j) {
+      if (pk.nseg == kMaxWgMulti) {   // pack full: launch it, start the next
+        SND_TRY(wg_multi_flush(pk, total, lds, s));
+        pk = WgMultiPack{};
+        lds = 0;
+        total = 0;
+      }
       const WgArgs& x = win[j];
       const int P = x.T * cdiv(x.K, 16);
       pk.a[pk.nseg] = x;
@@ -987,11 +1003,7 @@ int launch_wgrad_multi(const WgArgs* a, int n, hipStream_t s) {
       ++pk.nseg;
     }
   }
-  if (pk.nseg == 0) return 0;
-  for (int i = pk.nseg; i <= kMaxWgMulti; ++i) pk.start[i] = total;
-  hipLaunchKernelGGL(wgrad_multi_kernel, dim3(total), dim3(WGT), lds, s, pk);
-  SND_LAUNCH_CHECK("wgrad_multi_kernel");
-  return 0;
+  return wg_multi_flush(pk, total, lds, s);
 }
 
 WgGeom wgrad_geom(int R, int T, int K, int N, int chunks) {

@@ -121,7 +121,7 @@ WgGeom wgrad_geom(int R, int T, int K, int N, int chunks = 0);
 inline int wgrad_n4(int N) { return (N + 3) & ~3; }
 int launch_wgrad(const WgArgs& a, hipStream_t s);
 // n independent weight gradients (each its own geometry and slab) in one launch
-constexpr int kMaxWgMulti = 24;   // segments after the column-window split
+constexpr int kMaxWgMulti = 32;   // segments after the column-window split (C5: 29)
 int launch_wgrad_multi(const WgArgs* a, int n, hipStream_t s);
 
 // ---- fused sigmoid head + MSE + backward + BN/lrelu backward of the head's
