@@ -937,7 +937,10 @@ static WgArgs wg_norm(const WgArgs& a) {
 // 1024-thread workgroups share a CU, and one's LDS-DMA round trip hides under the
 // other's MFMAs.  Each window stages its own x / dy columns and writes its block of the
 // same slab, so the reduction is unchanged.
-constexpr size_t kWgSplitLds = 80 * 1024;
+#ifndef SND_WG_SPLIT_LDS
+#define SND_WG_SPLIT_LDS (80 * 1024)
+#endif
+constexpr size_t kWgSplitLds = SND_WG_SPLIT_LDS;
 static int wg_split(const WgArgs& a, WgArgs* out, int cap) {
   // n: always (the multi kernel is built for <= 4 column blocks); k: over the LDS budget
   const bool sk = a.K > 64 && wg_lds_bytes(a.T, a.K, std::min(a.N, 64)) > kWgSplitLds, sn = a.N > 64;
