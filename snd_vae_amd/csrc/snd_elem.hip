@@ -358,17 +358,21 @@ __global__ void __launch_bounds__(256) enc_bwd_kernel(EncBwdArgs a, int rows) {
 
 // ---------------------------------------------------------------- reduce
 #ifndef SND_RED_PL
-#define SND_RED_PL 2   // part lanes of a >= 64-part slab (round 5, C2 step on one box: 0.2220 ms at 2,
-                       // 0.2228 at 4, 0.2226 at 1; another box: 0.2210 at 4 vs 0.2236 at 8, 0.2300 at 16)
+#define SND_RED_PL 2   // part lanes of a >= 64-part slab of >= kRedWide items (round 5, C2 step on one
+                       // box: 0.2220 ms at 2, 0.2228 at 4, 0.2226 at 1; another: 0.2210 at 4 vs 0.2236
+                       // at 8, 0.2300 at 16)
 #endif
-// part lanes of a descriptor (uniform per block): a thread sums nparts / PL parts in a
-// dependent chain, so the many-part partials (C4's split-K head / projection slabs, ~1000
-// parts) take wider lane groups and more blocks
 #ifndef SND_RED_PLS
 #define SND_RED_PLS 4  // part lanes of a < 64-part partial
 #endif
-__host__ __device__ __forceinline__ int red_pl(int nparts) {
-  return nparts >= 1024 ? 64 : (nparts >= 256 ? 32 : (nparts >= 64 ? SND_RED_PL : SND_RED_PLS));
+constexpr long long kRedWide = 2048;
+// part lanes of a descriptor (uniform per block): a thread sums nparts / PL parts in a
+// dependent chain, so the many-part partials (C4's split-K head / projection slabs, ~1000
+// parts) take wider lane groups and more blocks; a 64..255-part partial of few items
+// (the per-tile column sums of the BN parameters) keeps 8 lanes, a wide weight slab 2
+__host__ __device__ __forceinline__ int red_pl(int nparts, long long items) {
+  return nparts >= 1024 ? 64
+                        : (nparts >= 256 ? 32 : (nparts >= 64 ? (items >= kRedWide ? SND_RED_PL : 8) : SND_RED_PLS));
 }
 struct ReducePack {
   ReduceDesc d[kMaxReduce];
@@ -403,7 +407,7 @@ __global__ void __launch_bounds__(256) reduce_kernel(ReducePack pk, FinalizeArgs
   __shared__ double red[256];
   const int rows = d.rows > 0 ? d.rows : 1;
   const long long items = (long long)rows * d.len;
-  const int PL = red_pl(d.nparts);               // part lanes
+  const int PL = red_pl(d.nparts, items);        // part lanes
   const int IPB = 256 / PL;                      // items per block
   const int it = threadIdx.x % IPB, pl = threadIdx.x / IPB;
   const long long j = (long long)bx * IPB + it;
@@ -633,7 +637,7 @@ int launch_reduce(const ReduceDesc* d, int n, hipStream_t s, const FinalizeArgs*
       if (i < cnt) {
         pk.d[i] = d[base + i];
         const long long items = (long long)(pk.d[i].rows > 0 ? pk.d[i].rows : 1) * pk.d[i].len;
-        const int ipb = 256 / red_pl(pk.d[i].nparts);
+        const int ipb = 256 / red_pl(pk.d[i].nparts, items);
         nb += (items + ipb - 1) / ipb;
       }
     }
