@@ -318,9 +318,11 @@ def kernel_timer(model, bc, reps):
     from snd_vae_amd import _lib
     L = _lib.lib()
 
-    def kernel_ms(name):
-        return time_launches(lambda sp: _lib.check(L.snd_plan_launch(
-            model.plan, bc, model.workspace.data_ptr(), name.encode(), sp)), reps)
+    def kernel_ms(name):   # "a+b": the plan kernels a and b back to back, per launch pair
+        def launch(sp):
+            for part in name.split("+"):
+                _lib.check(L.snd_plan_launch(model.plan, bc, model.workspace.data_ptr(), part.encode(), sp))
+        return time_launches(launch, reps)
 
     return kernel_ms
 

@@ -478,8 +478,17 @@ __device__ __forceinline__ WgUnit wg_unit(const WgArgs& a, int sub, int s0, int 
 
 // NPW (tap, 16-column) pairs per wave: 1, or 2 (pairs w and w + 16 share every dy
 // operand read: one staging pass serves up to 32 pairs)
+// measurement only (debug bit 1 << 21, SND_MEAS builds): s_memrealtime at the phase
+// boundaries of every workgroup, [start, args, prologue, unit 0..5, end, HW_ID, XCC_ID]
+constexpr int kWgStampWords = 12;
+__device__ __forceinline__ void wg_stamp(unsigned* ts, int i, bool on) {
+  if (on && threadIdx.x == 0 && i < kWgStampWords) ts[i] = (unsigned)__builtin_amdgcn_s_memrealtime();
+}
+
 template <int NBO, int NPW = 1>
-__device__ __forceinline__ void wgrad_body(const WgArgs& a, const int bx, const int by, __bf16* lds) {
+__device__ __forceinline__ void wgrad_body(const WgArgs& a, const int bx, const int by, __bf16* lds,
+                                           unsigned* tsp = nullptr) {
+  const bool stamp = tsp != nullptr;
   const int T = a.T, H = (T - 1) >> 1;
   const int XR = kRcRows + T - 1;
   const int kpx = a.K <= 32 ? 32 : (a.K <= 64 ? 64 : 128);
@@ -550,12 +559,14 @@ __device__ __forceinline__ void wgrad_body(const WgArgs& a, const int bx, const 
   // dy piece of column block ob: ((2 ob + tp / 2) ^ swd) << 3 | (4 tp & 4), formed at
   // each use (NBO offsets held across the loop cost the registers 8 waves/SIMD lack)
   const int swd = trsw(rk0, kpy), tpl = (4 * tp) & 4, tph = tp >> 1;
+  wg_stamp(tsp, 2, stamp);
   if (c0 < c1) {
     WgUnit u = wg_unit(a, c0, c0, c1);
     stage(u, 0);
     for (int k = 0;; ++k) {
       __builtin_amdgcn_s_waitcnt(0x0F70);
       __syncthreads();
+      wg_stamp(tsp, 3 + k, stamp && k < 6);
       // next unit: next graph segment of this 128-row block, else the next block
       int nsub = u.sub, ns0 = u.s1;
       if (ns0 >= min(c1, u.sub + kRcRows)) { nsub = u.sub + kRcRows; ns0 = nsub; }
@@ -632,6 +643,9 @@ static_assert(sizeof(WgMultiPack) <= 4096, "wgrad_multi: kernel arguments over 4
 __global__ void __launch_bounds__(WGT) __attribute__((amdgpu_waves_per_eu(8, 8)))
 wgrad_multi_kernel(WgMultiPack m) {
   extern __shared__ __attribute__((aligned(16))) __bf16 lds[];
+  __shared__ unsigned tsl[kWgStampWords];
+  const bool stamp = (kdbg(m.a[0].dbg) & (1 << 21)) && m.a[0].stamps;
+  wg_stamp(tsl, 0, stamp);
   if (kdbg(m.a[0].dbg) & 1) return;   // measurement only: the launch alone
   // segment of this block: independent scalar loads of the starts (entries past nseg hold
   // the grid size), no dependent search chain
@@ -645,11 +659,23 @@ wgrad_multi_kernel(WgMultiPack m) {
   const int bx = local % gx, by = local / gx;
   const bool two = a.pairs_per_wg > WGT / 64;
   if (kdbg(a.dbg) & 16) return;   // measurement only: launch + segment lookup
+  unsigned* ts = stamp ? tsl : nullptr;
+  wg_stamp(ts, 1, stamp);
   switch ((a.N + 15) >> 4) {
-    case 1: if (two) wgrad_body<1, 2>(a, bx, by, lds); else wgrad_body<1>(a, bx, by, lds); break;
-    case 2: if (two) wgrad_body<2, 2>(a, bx, by, lds); else wgrad_body<2>(a, bx, by, lds); break;
-    case 3: if (two) wgrad_body<3, 2>(a, bx, by, lds); else wgrad_body<3>(a, bx, by, lds); break;
-    default: if (two) wgrad_body<4, 2>(a, bx, by, lds); else wgrad_body<4>(a, bx, by, lds); break;
+    case 1: if (two) wgrad_body<1, 2>(a, bx, by, lds, ts); else wgrad_body<1>(a, bx, by, lds, ts); break;
+    case 2: if (two) wgrad_body<2, 2>(a, bx, by, lds, ts); else wgrad_body<2>(a, bx, by, lds, ts); break;
+    case 3: if (two) wgrad_body<3, 2>(a, bx, by, lds, ts); else wgrad_body<3>(a, bx, by, lds, ts); break;
+    default: if (two) wgrad_body<4, 2>(a, bx, by, lds, ts); else wgrad_body<4>(a, bx, by, lds, ts); break;
+  }
+  if (stamp) {
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      unsigned* o = m.a[0].stamps + (long long)blockIdx.x * kWgStampWords;
+      for (int i = 0; i < 9; ++i) o[i] = tsl[i];
+      o[9] = (unsigned)__builtin_amdgcn_s_memrealtime();
+      o[10] = __builtin_amdgcn_s_getreg((31 << 11) | 4);    // HW_REG_HW_ID
+      o[11] = __builtin_amdgcn_s_getreg((31 << 11) | 20);   // HW_REG_XCC_ID
+    }
   }
 }
 

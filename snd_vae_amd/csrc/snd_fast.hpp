@@ -113,6 +113,7 @@ struct WgArgs {
   // (launch_wgrad_multi's LDS split): rows sK, padded width sn4, window origin
   // (wk0, wn0); 0 = the descriptor's own K / n4(N) at origin 0
   int sK, sn4, wk0, wn0;
+  unsigned* stamps;             // measurement only (debug bit 1 << 21): 12 words per workgroup
 };
 struct WgGeom { int rows_per_wg, pairs_per_wg, gx, gy; };
 // chunks > 0: that many row chunks per weight (the step's multi-segment launch);

@@ -1531,7 +1531,12 @@ extern "C" int snd_plan_launch(const snd_plan_t* plan, const snd_batch_t* batch,
   if (!strcmp(kernel, "wgrad_multi")) {   // the last step's weight gradients (current debug bits)
     SND_CHECK_ARG(!p.last_wq.empty(), "snd_plan_launch: no multi-segment weight-gradient launch yet");
     std::vector<WgArgs> q = p.last_wq;
-    for (auto& w : q) w.dbg = debug_flags();
+    for (auto& w : q) {
+      w.dbg = debug_flags();
+      // measurement only: per-workgroup stamps into the fused decoder's head partials
+      // (unused by this launch; 12 words x the launch's workgroups must fit)
+      w.stamps = (w.dbg & (1 << 21)) && p.dec_fused ? reinterpret_cast<unsigned*>(ws + p.buf("PDHS")) : nullptr;
+    }
     return launch_wgrad_multi(q.data(), (int)q.size(), s);
   }
   if (!strcmp(kernel, "head_bwd")) {   // fused backward head (the step's scales)
