@@ -838,7 +838,7 @@ int wg_launch(const WgArgs& a, dim3 grid, hipStream_t s) {
 }
 
 constexpr size_t kMaxDynLds = kRcLdsLimit;
-constexpr size_t kWgMultiLds = 160 * 1024;
+constexpr size_t kWgMultiLds = 128 * 1024;   // segments stage <= 68 KB (window split); room for static LDS
 
 }  // namespace
 
