@@ -413,9 +413,22 @@ __global__ void __launch_bounds__(256) reduce_kernel(ReducePack pk, FinalizeArgs
   const long long j = (long long)bx * IPB + it;
   int r = 0, i = 0;
   double acc = 0.0;
+  // the Adam operands (and an accumulated destination) do not depend on the sums: the
+  // item's owner lane loads them before the slab loads, one round trip for both
+  float pi = 0.f, mi = 0.f, vi = 0.f, prev = 0.f;
   if (j < items) {
     r = (int)(j / d.len);
     i = (int)(j - (long long)r * d.len);
+    if (pl == 0) {
+      const float* dst = d.dst + (long long)r * d.dst_rs + i;
+      if (d.accumulate) prev = *dst;
+      if constexpr (ADAM) {
+        if (dad) {
+          const long long k = dst - ra.gbase;
+          pi = ra.p[k]; mi = ra.m[k]; vi = ra.v[k];
+        }
+      }
+    }
     const float* src = d.src + (long long)r * d.src_rs + i;
     int p = pl;
     // 8 loads in flight per round (the 64-part weight slabs at 8 part lanes: one round
@@ -446,12 +459,11 @@ __global__ void __launch_bounds__(256) reduce_kernel(ReducePack pk, FinalizeArgs
     for (int q = 0; q < PL; ++q) t += red[q * IPB + it];
     float* dst = d.dst + (long long)r * d.dst_rs + i;
     float v = (float)(t * (double)d.scale);
-    if (d.accumulate) v += *dst;
+    if (d.accumulate) v += prev;
     *dst = v;
     if constexpr (ADAM) {
       if (dad) {
         const long long k = dst - ra.gbase;
-        float pi = ra.p[k], mi = ra.m[k], vi = ra.v[k];
         adam_elem(pi, mi, vi, __fmul_rn(v, 1.f), ra.b1, ra.b2, ra.eps, lrt);
         ra.m[k] = mi;
         ra.v[k] = vi;
