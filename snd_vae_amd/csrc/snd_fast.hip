@@ -498,25 +498,6 @@ __device__ __forceinline__ void wgrad_body(const WgArgs& a, const int bx, const 
   // the wave index as a scalar: the pair bookkeeping below stays in SGPRs
   const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int li = lane & 15, lg = lane >> 4, tq = li >> 2, tp = li & 3;
-  const int cbn = (a.K + 15) >> 4;
-  const int P = T * cbn;
-  bool pvs[NPW];
-  int ts[NPW], cbs[NPW];
-#pragma unroll
-  for (int i = 0; i < NPW; ++i) {
-    const int wl = w + 16 * i, p = by * a.pairs_per_wg + wl;
-    pvs[i] = wl < a.pairs_per_wg && p < P;
-    ts[i] = pvs[i] ? p / cbn : 0;
-    cbs[i] = pvs[i] ? p - ts[i] * cbn : 0;
-  }
-  const bool pv = pvs[0];
-
-  f32x4 acc[NPW][NBO];
-#pragma unroll
-  for (int i = 0; i < NPW; ++i)
-#pragma unroll
-    for (int j = 0; j < NBO; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
   const __bf16* xg = reinterpret_cast<const __bf16*>(a.x);
   const __bf16* dg = reinterpret_cast<const __bf16*>(a.dy);
   const int c0 = bx * a.rows_per_wg, c1 = min(a.R, c0 + a.rows_per_wg);
@@ -546,6 +527,29 @@ __device__ __forceinline__ void wgrad_body(const WgArgs& a, const int bx, const 
     }
   };
 
+  // the first unit's DMA goes out before the pair bookkeeping below (round 5 stamps: the
+  // first unit's round trip was 3.7 us of a 12.8 us workgroup)
+  const WgUnit u0 = wg_unit(a, c0, c0, c1);
+  if (c0 < c1) stage(u0, 0);
+  const int cbn = (a.K + 15) >> 4;
+  const int P = T * cbn;
+  bool pvs[NPW];
+  int ts[NPW], cbs[NPW];
+#pragma unroll
+  for (int i = 0; i < NPW; ++i) {
+    const int wl = w + 16 * i, p = by * a.pairs_per_wg + wl;
+    pvs[i] = wl < a.pairs_per_wg && p < P;
+    ts[i] = pvs[i] ? p / cbn : 0;
+    cbs[i] = pvs[i] ? p - ts[i] * cbn : 0;
+  }
+  const bool pv = pvs[0];
+
+  f32x4 acc[NPW][NBO];
+#pragma unroll
+  for (int i = 0; i < NPW; ++i)
+#pragma unroll
+    for (int j = 0; j < NBO; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
   // per-lane tr-read offsets (elements) at k-step 0
   const int rk0 = 8 * lg + tq;
   int xoff[NPW], xoff2[NPW];
@@ -561,8 +565,7 @@ __device__ __forceinline__ void wgrad_body(const WgArgs& a, const int bx, const 
   const int swd = trsw(rk0, kpy), tpl = (4 * tp) & 4, tph = tp >> 1;
   wg_stamp(tsp, 2, stamp);
   if (c0 < c1) {
-    WgUnit u = wg_unit(a, c0, c0, c1);
-    stage(u, 0);
+    WgUnit u = u0;
     for (int k = 0;; ++k) {
       __builtin_amdgcn_s_waitcnt(0x0F70);
       __syncthreads();
@@ -649,12 +652,19 @@ wgrad_multi_kernel(WgMultiPack m) {
   if (kdbg(m.a[0].dbg) & 1) return;   // measurement only: the launch alone
   // segment of this block: independent scalar loads of the starts (entries past nseg hold
   // the grid size), no dependent search chain
+  // (a 2-D grid when every segment has the same item count: the segment is blockIdx.y,
+  // and its arguments are the workgroup's first kernel-argument loads)
+  const int bid = blockIdx.y * gridDim.x + blockIdx.x;
   int s = 0;
+  if (gridDim.y > 1) {
+    s = blockIdx.y;
+  } else {
 #pragma unroll
-  for (int i = 1; i < kMaxWgMulti; ++i) s += (int)blockIdx.x >= m.start[i] ? 1 : 0;
+    for (int i = 1; i < kMaxWgMulti; ++i) s += (int)blockIdx.x >= m.start[i] ? 1 : 0;
+  }
   s = __builtin_amdgcn_readfirstlane(s);
   const WgArgs a = m.a[s];   // by value: field reads stay scalar loads from the kernarg segment
-  const int local = blockIdx.x - m.start[s];
+  const int local = gridDim.y > 1 ? (int)blockIdx.x : (int)blockIdx.x - m.start[s];
   const int gx = cdiv_d(a.R, a.rows_per_wg);
   const int bx = local % gx, by = local / gx;
   const bool two = a.pairs_per_wg > WGT / 64;
@@ -670,7 +680,7 @@ wgrad_multi_kernel(WgMultiPack m) {
   if (stamp) {
     __syncthreads();
     if (threadIdx.x == 0) {
-      unsigned* o = m.a[0].stamps + (long long)blockIdx.x * kWgStampWords;
+      unsigned* o = m.a[0].stamps + (long long)bid * kWgStampWords;
       for (int i = 0; i < 9; ++i) o[i] = tsl[i];
       o[9] = (unsigned)__builtin_amdgcn_s_memrealtime();
       o[10] = __builtin_amdgcn_s_getreg((31 << 11) | 4);    // HW_REG_HW_ID
@@ -989,7 +999,10 @@ static int wg_split(const WgArgs& a, WgArgs* out, int cap) {
 static int wg_multi_flush(WgMultiPack& pk, int total, size_t lds, hipStream_t s) {
   if (pk.nseg == 0) return 0;
   for (int i = pk.nseg; i <= kMaxWgMulti; ++i) pk.start[i] = total;
-  hipLaunchKernelGGL(wgrad_multi_kernel, dim3(total), dim3(WGT), lds, s, pk);
+  bool uniform = pk.nseg > 1;
+  for (int i = 1; i < pk.nseg; ++i) uniform = uniform && pk.start[i + 1] - pk.start[i] == pk.start[1];
+  const dim3 grid = uniform ? dim3(pk.start[1], pk.nseg) : dim3(total);
+  hipLaunchKernelGGL(wgrad_multi_kernel, grid, dim3(WGT), lds, s, pk);
   SND_LAUNCH_CHECK("wgrad_multi_kernel");
   return 0;
 }
