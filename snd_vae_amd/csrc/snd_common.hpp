@@ -75,6 +75,27 @@ inline int device_cu_count() {
   return n;
 }
 
+// The per-edge terms of the weighted CE of an A = 1 pair with logit x (optimizer.py:142-144,
+// tf.nn.weighted_cross_entropy_with_logits, target 1):  loss pw softplus(-x) = pw
+// (softplus(x) - x) and d/dx = pw (sigmoid(x) - 1), written as the caller accumulates them
+// (coef = -pw + (pw - 1) sigmoid(x), loss += (pw - 1) softplus(x) - pw x with the -pw x
+// part added by the caller).  One exponential serves both: e = e^-|x|, sigmoid = 1/(1+e)
+// for x >= 0 and e/(1+e) below, softplus = max(x, 0) + log(1 + e); a hardware reciprocal
+// and logarithm (round 5: the IEEE division and log1pf were ~20 of the ~30 instructions
+// per edge and lane, repeated by the row's 8 lanes).  Shared by the bf16 edge kernels so
+// the fused backward head and edge_bf16_kernel stay bit for bit alike.
+__device__ __forceinline__ void edge_ce_terms(float x, float pw, float& coef, float& loss) {
+  coef = -pw;
+  if (pw != 1.f) {
+    const float e = __expf(-fabsf(x));
+    const float q = 1.f + e;
+    const float r = __builtin_amdgcn_rcpf(q);
+    const float sg = x >= 0.f ? r : e * r;
+    coef += (pw - 1.f) * sg;
+    loss += (pw - 1.f) * (fmaxf(x, 0.f) + __logf(q));
+  }
+}
+
 // One KL element 1 + 2s - (e^s)^2 - mu^2 (optimizer.py:193) without the fp32
 // cancellation of 1 + 2s - e^{2s}, which is O(s^2) near the initial s ~ 0 (round 4:
 // the fp32 kl term 6.8e-6 off the float64 oracle at C2):  -(expm1(2s) - 2s) - mu^2, the

@@ -496,12 +496,8 @@ __global__ void __launch_bounds__(NT) edge_bf16_kernel(EdgeBfArgs a) {
       for (int j = 0; j < 8; ++j) dot += zi[q][j] * zj[q][j];
     const float L = row8_sum(dot);
     if (!valid) return;
-    float coef = -pw;
-    if (pw != 1.f) {
-      const float sg = 1.f / (1.f + __expf(-L));
-      coef += (pw - 1.f) * sg;
-      lossr += (pw - 1.f) * (fmaxf(L, 0.f) + log1pf(__expf(-fabsf(L))));
-    }
+    float coef;
+    edge_ce_terms(L, pw, coef, lossr);
     lossr -= pw * L;
     tp += L > 0.f ? 1u : 0u;
 #pragma unroll

@@ -451,12 +451,8 @@ __global__ void __launch_bounds__(HR * 8) head_bwd_kernel(HeadBwdArgs a) {
           }
         const float Lij = row8_sum(dot);
         if (!valid) return;
-        float coef = -pw;
-        if (pw != 1.f) {
-          const float sg = 1.f / (1.f + __expf(-Lij));
-          coef += (pw - 1.f) * sg;
-          lossr += (pw - 1.f) * (fmaxf(Lij, 0.f) + log1pf(__expf(-fabsf(Lij))));
-        }
+        float coef;
+        edge_ce_terms(Lij, pw, coef, lossr);
         lossr -= pw * Lij;
         tp += Lij > 0.f ? 1u : 0u;
 #pragma unroll

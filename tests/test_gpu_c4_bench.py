@@ -35,7 +35,13 @@ rows with cancellation: measured 3.4e-4 at step 1, 1.4e-3 for dec.K1 at step 3 o
 lr = 1e-6 schedule); bf16 1e-1, and 1.0 for blocks of at most 32 elements (scalar-like
 bias sums whose terms cancel: dec.bn, ONE element, measured 0.15 at step 1 and 0.74
 at step 2 -- bf16 operands leave only its order of magnitude); v (~g^2) twice the m
-tolerance, capped at 1.0.
+tolerance, capped at 1.0.  The bf16 bounds against the float64 oracle are loose by
+necessity (the oracle gap of bf16 operands, parity unpinned below them); what pins the
+fused update itself is the self-consistency check, in every dtype: the GPU's new m and
+the old m give the gradient the update used (g = (m' - b1 m) / (1 - b1), TF's float32
+coefficients), and v' and the parameters must follow from it and from m', v' by TF1 Adam
+to float32 rounding (`self_adam_err`: v within 1e-4 of |v'| + 1e-4 of the block's max,
+parameters within 1e-3 lr + 4 ulps).
 """
 import dataclasses
 import json
@@ -74,6 +80,20 @@ def block_err(g, ref):
     return float(np.abs(g - ref).max() / max(np.abs(ref).max(), 1e-30))
 
 
+def self_adam(p, m, v, gp, gm, gv, t, lr, b1, b2, eps):
+    """(v error, parameter error) of the GPU's step against TF1 Adam applied to the
+    gradient its own moments imply; 1.0 = the tolerance."""
+    f32 = np.float32
+    c1, c2 = float(f32(1) - f32(b1)), float(f32(1) - f32(b2))
+    g = (gm - float(f32(b1)) * m) / c1
+    sv = float(f32(b2)) * v + c2 * g * g
+    ev = float(np.max(np.abs(gv - sv) / (1e-4 * np.abs(sv) + 1e-4 * np.abs(sv).max() + 1e-30)))
+    lr_t = lr * np.sqrt(1 - b2 ** t) / (1 - b1 ** t)
+    sp = p - lr_t * gm / (np.sqrt(gv) + eps)
+    ep = float(np.max(np.abs(gp - sp) / (1e-3 * lr + 4 * EPS32 * np.abs(p))))
+    return ev, ep
+
+
 @pytest.mark.timeout(900)
 @pytest.mark.parametrize("lr,steps", [(None, 1), (1e-6, STEPS)])
 @pytest.mark.parametrize("dtype", ["f32", "bf16"])
@@ -110,7 +130,7 @@ def test_c4_bench_batch_vs_oracle(dtype, lr, steps):
         R.adam_tf1(p, rg, m, v, t, lr, cfg.adam_beta1, cfg.adam_beta2, cfg.adam_eps)
         got = opt.loss_dict()
         rec = {"test": "c4_bench_batch", "dtype": dtype, "lr": lr, "step": t, "loss_rel": {},
-               "param_far_frac": {}, "param_max_lr": {}, "m_err": {}, "v_err": {}}
+               "param_far_frac": {}, "param_max_lr": {}, "m_err": {}, "v_err": {}, "self_adam_err": {}}
         for k in TERMS:
             e = abs(got[k] - rl[k]) / max(abs(rl[k]), 1e-30)
             rec["loss_rel"][k] = e
@@ -130,6 +150,11 @@ def test_c4_bench_batch_vs_oracle(dtype, lr, steps):
                     fails.append((t, "param", k, off, float(d.max() / lr)))
             elif far > 0.03 or d.max() > 2.05 * lr:
                 fails.append((t, "param", k, far, float(d.max() / lr)))
+            ev, ep = self_adam(p[k], m[k], v[k], np.asarray(gp[k], np.float64), np.asarray(gm[k], np.float64),
+                               np.asarray(gv[k], np.float64), t, lr, cfg.adam_beta1, cfg.adam_beta2, cfg.adam_eps)
+            rec["self_adam_err"][k] = [ev, ep]
+            if ev > 1 or ep > 1:
+                fails.append((t, "self_adam", k, ev, ep))
             mt = M_TOL[dtype][0 if p[k].size > 32 else 1]
             for name, a, r, tol in (("m", gm[k], m[k], mt), ("v", gv[k], v[k], min(2 * mt, 1.0))):
                 e = block_err(np.asarray(a, np.float64), r)
