@@ -37,6 +37,9 @@ for s in ${STAGES:-tests smoke ab bench timeline}; do
       done ;;
     prof) step rocprof 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run \
              --output-format csv -- python bench.py --steps 20 --warmup 5 --no-cpu-baseline --extra "" ;;
+    profh) step rocprof_headline 400 rocprofv3 --kernel-trace --stats -d gpurun_out/profh -o run \
+             --output-format csv -- python bench.py --steps 20 --warmup 5 --no-cpu-baseline --extra "" \
+             --batch-sweep "" --no-modes ;;
     benchq) step benchq 300 python -u bench.py --steps 50 --warmup 10 --no-cpu-baseline --batch-sweep "" --extra "" ;;
     traffic)   # per-kernel HBM bytes of eager C2 steps: one counter per rocprofv3 run
       step pmc_fetch 200 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o run --output-format csv \
