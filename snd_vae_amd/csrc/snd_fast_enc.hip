@@ -464,18 +464,20 @@ __global__ void __launch_bounds__(NT) edge_bf16_kernel(EdgeBfArgs a) {
   for (int q = 0; q < NQ; ++q) qv[q] = sub + 8 * q < nch;
   float lossr = 0.f;
   unsigned tp = 0;
-  float zi[NQ][8], acc[NQ][8];
+  u32x4 zip[NQ];   // z_i packed (bf16 pairs): the dot2 operand
+  float acc[NQ][8];
 #pragma unroll
-  for (int q = 0; q < NQ; ++q)
+  for (int q = 0; q < NQ; ++q) {
+    zip[q] = u32x4{0u, 0u, 0u, 0u};
 #pragma unroll
-    for (int j = 0; j < 8; ++j) { zi[q][j] = 0.f; acc[q][j] = 0.f; }
+    for (int j = 0; j < 8; ++j) acc[q][j] = 0.f;
+  }
   if (rv)
 #pragma unroll
     for (int q = 0; q < NQ; ++q)
       if (qv[q]) {
         const bf16x8 v = *reinterpret_cast<const bf16x8*>(a.z + (long long)r * a.d + 64 * q + 8 * sub);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) zi[q][j] = (float)v[j];
+        zip[q] = __builtin_bit_cast(u32x4, v);
       }
   const float pw = a.pos_weight;
   const __amdgpu_buffer_rsrc_t rs = rows_rsrc(a.z, (long long)a.R * a.d * 2);
@@ -492,8 +494,7 @@ __global__ void __launch_bounds__(NT) edge_bf16_kernel(EdgeBfArgs a) {
       }
 #pragma unroll
     for (int q = 0; q < NQ; ++q)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) dot += zi[q][j] * zj[q][j];
+      if (qv[q]) dot = dot8_bf16(zip[q], v[q], dot);   // as head_bwd_kernel
     const float L = row8_sum(dot);
     if (!valid) return;
     float coef;

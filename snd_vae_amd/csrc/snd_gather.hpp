@@ -9,6 +9,17 @@ namespace snd {
 constexpr int kLpr = 8;   // lanes per row (aligned DPP half-rows)
 
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 gbf16x2 __attribute__((ext_vector_type(2)));
+
+// a . b over one 8-column chunk of packed bf16 pairs (the per-edge logit z_i . z_j of the
+// bf16 edge kernels): four v_dot2_f32_bf16 on the packed words, no widening
+__device__ __forceinline__ float dot8_bf16(const u32x4& a, const u32x4& b, float acc) {
+#pragma unroll
+  for (int p = 0; p < 4; ++p)
+    acc = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(gbf16x2, a[p]), __builtin_bit_cast(gbf16x2, b[p]),
+                                          acc, false);
+  return acc;
+}
 
 // Lane u of each aligned 8-lane group to all 8 lanes (ds_swizzle bit mode:
 // and-mask 0x18 keeps the group, or-mask u selects the lane; no LDS access).

@@ -444,11 +444,7 @@ __global__ void __launch_bounds__(HR * 8) head_bwd_kernel(HeadBwdArgs a) {
           }
 #pragma unroll
         for (int q = 0; q < NQ; ++q)
-#pragma unroll
-          for (int p = 0; p < 4; ++p) {
-            dot += __uint_as_float(zi[q][p] << 16) * zj[q][2 * p];
-            dot += __uint_as_float(zi[q][p] & 0xFFFF0000u) * zj[q][2 * p + 1];
-          }
+          if (qv[q]) dot = dot8_bf16(zi[q], v[q], dot);   // as edge_bf16_kernel
         const float Lij = row8_sum(dot);
         if (!valid) return;
         float coef;
