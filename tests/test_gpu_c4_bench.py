@@ -122,6 +122,7 @@ def test_c4_bench_batch_vs_oracle(dtype, lr, steps):
         m, v = opt.state_blocks()
         m = {k: np.asarray(x, np.float64) for k, x in m.items()}
         v = {k: np.asarray(x, np.float64) for k, x in v.items()}
+        p0s, m0s, v0s = ({k: x.copy() for k, x in d.items()} for d in (p, m, v))   # adam_tf1 updates in place
         opt.step(db, torch.from_numpy(eps[t - 1]).cuda())
         torch.cuda.synchronize()
         rl, rg, _ = R.forward_backward(p, adj, batch.features, batch.feature_truth,
@@ -150,7 +151,7 @@ def test_c4_bench_batch_vs_oracle(dtype, lr, steps):
                     fails.append((t, "param", k, off, float(d.max() / lr)))
             elif far > 0.03 or d.max() > 2.05 * lr:
                 fails.append((t, "param", k, far, float(d.max() / lr)))
-            ev, ep = self_adam(p[k], m[k], v[k], np.asarray(gp[k], np.float64), np.asarray(gm[k], np.float64),
+            ev, ep = self_adam(p0s[k], m0s[k], v0s[k], np.asarray(gp[k], np.float64), np.asarray(gm[k], np.float64),
                                np.asarray(gv[k], np.float64), t, lr, cfg.adam_beta1, cfg.adam_beta2, cfg.adam_eps)
             rec["self_adam_err"][k] = [ev, ep]
             if ev > 1 or ep > 1:
