@@ -41,7 +41,7 @@ fused update itself is the self-consistency check, in every dtype: the GPU's new
 the old m give the gradient the update used (g = (m' - b1 m) / (1 - b1), TF's float32
 coefficients), and v' and the parameters must follow from it and from m', v' by TF1 Adam
 to float32 rounding (`self_adam_err`: v within 1e-5 of |v'| + 1e-5 of the block's max,
-parameters within 5e-4 lr + 4 ulps; measured, round 5: v 9e-9, parameters 1.25e-4 lr).
+parameters within 5e-4 lr + 4 ulps; measured, round 5: v 9e-8, parameters 1.25e-4 lr).
 """
 import dataclasses
 import json
