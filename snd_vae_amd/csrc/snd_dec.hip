@@ -131,6 +131,24 @@ __device__ __forceinline__ void stage_weights(const DecImg& im, char* dst, int d
   const char* g = reinterpret_cast<const char*>(im.w) + lane * 16;
   for (int j = w; j < npc; j += NW) dglds16(g + (j << 10), dst + (j << 10));
 }
+// The weight DMA of a LATER phase, issued from inline asm: the compiler does not track it,
+// so the current phase's ds_reads do not wait for it (with the builtin it drains vmcnt(0)
+// before the next LDS read).  The caller owns the wait: wait_dma() before the image is read.
+__device__ __forceinline__ void dglds16_async(const void* g, void* lds_base) {
+  const unsigned dst = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(lptr_t)lds_base);
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+               "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(g), "s"(dst) : "memory");
+}
+__device__ __forceinline__ void stage_weights_async(const DecImg& im, char* dst, int dbg) {
+  if (dbg & 1) return;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int npc = (5 * im.np * im.kp * 2) >> 10;
+  const char* g = reinterpret_cast<const char*>(im.w) + lane * 16;
+  for (int j = w; j < npc; j += NW) dglds16_async(g + (j << 10), dst + (j << 10));
+}
+__host__ __device__ __forceinline__ int wimg_bytes(const DecImg& im) { return 5 * im.np * im.kp * 2; }
 __device__ __forceinline__ void wait_dma() {
   __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0)
   __syncthreads();
@@ -429,6 +447,12 @@ __global__ void __launch_bounds__(DT) dec_fwd_kernel(DecChainFwdArgs a) {
   if (stamp) ts[2] = __builtin_amdgcn_s_memrealtime();
   stage_weights(a.k2, reinterpret_cast<char*>(wimg), kdbg(a.dbg));
   wait_dma();
+  // conv3's image at the tail of the weight region when it fits beside conv2's: its DMA
+  // runs under conv2 (round 5)
+  const int k3o = (L.a - L.w) - wimg_bytes(a.k3);
+  const bool pre3 = wimg_bytes(a.k2) <= k3o && (k3o & 1023) == 0;
+  __bf16* wimg3 = pre3 ? wimg + k3o / 2 : wimg;
+  if (pre3) stage_weights_async(a.k3, reinterpret_cast<char*>(wimg3), kdbg(a.dbg));
   if (stamp) ts[3] = __builtin_amdgcn_s_memrealtime();
   // ---- conv2: window [r0 - 2, r0 + own + 2) -> U2 image; Y2 / U2 own rows; Y2n own rows in LDS
   {
@@ -466,13 +490,13 @@ __global__ void __launch_bounds__(DT) dec_fwd_kernel(DecChainFwdArgs a) {
   }
   __syncthreads();
   if (stamp) ts[4] = __builtin_amdgcn_s_memrealtime();
-  stage_weights(a.k3, reinterpret_cast<char*>(wimg), kdbg(a.dbg));
+  if (!pre3) stage_weights(a.k3, reinterpret_cast<char*>(wimg3), kdbg(a.dbg));
   wait_dma();
   if (stamp) ts[5] = __builtin_amdgcn_s_memrealtime();
   // ---- conv3 (s branch): own rows -> U3, Y3 (fp32, LDS; the spatial head's input)
   {
     const int n_out = own;
-    conv_phase<1, 2>(u2img, kpu2, wimg, a.k3.kp, a.k3.np, n_out, nopre,
+    conv_phase<1, 2>(u2img, kpu2, wimg3, a.k3.kp, a.k3.np, n_out, nopre,
                   [&](int orow, int nb0, f32x4 (&acc)[1], f32x4 (&)[1]) {
       if (orow >= n_out) return;
       const int n0 = 16 * nb0 + 4 * lg;
@@ -588,7 +612,12 @@ __global__ void __launch_bounds__(DT) dec_bwd_kernel(DecChainBwdArgs a) {
   // dY3 window [r0 - 6, r0 + own + 6), conv3^T weights
   if (!(kdbg(a.dbg) & 16)) stage_window(a.dy3, a.lddy3, a.s3, tl.r0 - 6, in_rows(TR + 8), own + 12, tl.glo, tl.ghi, a.k3t.kp,
                reinterpret_cast<char*>(d3), a.zero);
-  stage_weights(a.k3t, reinterpret_cast<char*>(wimg), kdbg(a.dbg));
+  // conv3^T's image at the tail of the weight region when conv2^T's fits beside it: conv2^T's
+  // DMA then runs under conv3^T (round 5; "W2t staged" was 0.9 us of a 20.5 us chain)
+  const int wb3 = L.d3 - L.w, k3o = wb3 - wimg_bytes(a.k3t);
+  const bool pre2 = wimg_bytes(a.k2t) <= k3o && (k3o & 1023) == 0;
+  __bf16* wimg3 = pre2 ? wimg + k3o / 2 : wimg;
+  stage_weights(a.k3t, reinterpret_cast<char*>(wimg3), kdbg(a.dbg));
   if (tid < 128) {
     const int n = tid;
     const ColMap ms{a.m2.a, 0, a.m2.a};
@@ -611,6 +640,7 @@ __global__ void __launch_bounds__(DT) dec_bwd_kernel(DecChainBwdArgs a) {
     }
   }
   wait_dma();
+  if (pre2) stage_weights_async(a.k2t, reinterpret_cast<char*>(wimg), kdbg(a.dbg));
   if (stamp) ts[1] = __builtin_amdgcn_s_memrealtime();
   // ---- conv3^T: window [r0 - 4, r0 + own + 4): dU2s -> BN/lrelu backward -> dY2s
   {
@@ -618,7 +648,7 @@ __global__ void __launch_bounds__(DT) dec_bwd_kernel(DecChainBwdArgs a) {
     const int nbc = a.k3t.np >> 4, ncg = nbc, wpc = NW / ncg;
     const int nb0 = w % ncg;
     float q[3][1][4] = {};
-    conv_phase<1, 1>(d3, a.k3t.kp, wimg, a.k3t.kp, a.k3t.np, n_out,
+    conv_phase<1, 1>(d3, a.k3t.kp, wimg3, a.k3t.kp, a.k3t.np, n_out,
                   [&](int orow, int nb, f32x4 (&yp)[1]) {
                     yp[0] = f32x4{0.f, 0.f, 0.f, 0.f};
                     const int gr = wr0 + orow;
@@ -668,7 +698,7 @@ __global__ void __launch_bounds__(DT) dec_bwd_kernel(DecChainBwdArgs a) {
   }
   __syncthreads();
   if (stamp) ts[2] = __builtin_amdgcn_s_memrealtime();
-  stage_weights(a.k2t, reinterpret_cast<char*>(wimg), kdbg(a.dbg));
+  if (!pre2) stage_weights(a.k2t, reinterpret_cast<char*>(wimg), kdbg(a.dbg));
   wait_dma();
   if (stamp) ts[3] = __builtin_amdgcn_s_memrealtime();
   // ---- conv2^T: window [r0 - 2, r0 + own + 2): dU1 -> BN/lrelu backward -> dY1
