@@ -184,8 +184,10 @@ __device__ __forceinline__ float4 philox_normal4(unsigned long long seed, unsign
   const uint4 r = philox4x32_10(make_uint4((unsigned)q, (unsigned)(q >> 32), offset, 0u),
                                 make_uint2((unsigned)seed, (unsigned)(seed >> 32)));
   const float k = 2.3283064365386963e-10f;
-  const float m1 = sqrtf(-2.0f * __logf(((float)r.x + 1.0f) * k));   // u in (0, 1]
-  const float m2 = sqrtf(-2.0f * __logf(((float)r.z + 1.0f) * k));
+  // hardware square root (1 ulp; the correctly rounded sqrtf adds ~10 scaling / fix-up
+  // instructions): the oracle restatement is float64, the tolerance 5e-3 (fast log / sincos)
+  const float m1 = __builtin_amdgcn_sqrtf(-2.0f * __logf(((float)r.x + 1.0f) * k));   // u in (0, 1]
+  const float m2 = __builtin_amdgcn_sqrtf(-2.0f * __logf(((float)r.z + 1.0f) * k));
   float s1, c1, s2, c2;
   __sincosf(6.283185307179586f * ((float)r.y * k), &s1, &c1);
   __sincosf(6.283185307179586f * ((float)r.w * k), &s2, &c2);

@@ -66,12 +66,23 @@ __device__ __forceinline__ void gather_rows16(const int* colidx, int s, int e, _
 }
 
 // acc[0..7] += the 8 bf16 of a packed 16-byte chunk (exact widening + fp32 add)
+// fp32 sums without widening: v_dot2_f32_bf16 with (1, 0) / (0, 1) adds the low / high
+// bf16 of a word to an fp32 accumulator (x * 1 and y * 0 are exact: one rounding, the
+// plain add's result), one instruction per element instead of a shift / mask and an add
+// (the window SpMM's acc8_dot; round 5: every gather sum)
 __device__ __forceinline__ void acc8v(float (&a)[8], const u32x4& v) {
+  // (1, 0) and (0, 1) through SGPRs: hipcc encodes the bf16 pair (1, 0) as the inline
+  // constant 1.0, which the hardware reads as the fp32 word 0x3F800000 = (0, 1)
+  unsigned lo1u, hi1u;
+  asm volatile("s_mov_b32 %0, 0x3f80" : "=s"(lo1u));
+  asm volatile("s_mov_b32 %0, 0x3f800000" : "=s"(hi1u));
+  const gbf16x2 lo1 = __builtin_bit_cast(gbf16x2, lo1u);
+  const gbf16x2 hi1 = __builtin_bit_cast(gbf16x2, hi1u);
 #pragma unroll
   for (int p = 0; p < 4; ++p) {
-    const unsigned w = v[p];
-    a[2 * p] += __uint_as_float(w << 16);
-    a[2 * p + 1] += __uint_as_float(w & 0xFFFF0000u);
+    const gbf16x2 x = __builtin_bit_cast(gbf16x2, v[p]);
+    a[2 * p] = __builtin_amdgcn_fdot2_f32_bf16(x, lo1, a[2 * p], false);
+    a[2 * p + 1] = __builtin_amdgcn_fdot2_f32_bf16(x, hi1, a[2 * p + 1], false);
   }
 }
 
