@@ -29,7 +29,8 @@ namespace {
 
 // HR rows of one graph per workgroup, 8 lanes per row in the gather: HR * 8 threads.
 // 64-row tiles (8 waves, ~73 KB LDS at C2) put two workgroups on a CU, so one's
-// gather latency overlaps the other's GEMMs and stores; 128 (debug bit 131072) is one.
+// gather latency overlaps the other's GEMMs and stores (the 128-row variant, one per CU,
+// measured slower and was removed in round 5).
 constexpr int kHeadRows = 64;
 constexpr int HWMAX = 16;
 constexpr float kSqrtLog2e = 1.2011224087864498f;
@@ -902,18 +903,14 @@ int launch_head_fwd(const HeadFwdArgs& a, hipStream_t s) {
                     a.zb && a.jrow && a.jt && a.colpart && a.kl_part,
                 "head_fwd: null operand");
   SND_TRY(head_init_attributes());
-  return (a.dbg & 131072) ? head_fwd_dispatch<128>(a, s) : head_fwd_dispatch<kHeadRows>(a, s);
+  return head_fwd_dispatch<kHeadRows>(a, s);
 }
 
 static int head_init_attributes_once() {
   const void* ks[] = {reinterpret_cast<const void*>(head_fwd_kernel<64, 1, 2>),
                       reinterpret_cast<const void*>(head_fwd_kernel<64, 1, 4>),
                       reinterpret_cast<const void*>(head_fwd_kernel<64, 2, 2>),
-                      reinterpret_cast<const void*>(head_fwd_kernel<64, 2, 4>),
-                      reinterpret_cast<const void*>(head_fwd_kernel<128, 1, 2>),
-                      reinterpret_cast<const void*>(head_fwd_kernel<128, 1, 4>),
-                      reinterpret_cast<const void*>(head_fwd_kernel<128, 2, 2>),
-                      reinterpret_cast<const void*>(head_fwd_kernel<128, 2, 4>)};
+                      reinterpret_cast<const void*>(head_fwd_kernel<64, 2, 4>)};
   const void* kb[] = {reinterpret_cast<const void*>(head_bwd_kernel<kHeadBwdRows, 1, 1, 1>),
                       reinterpret_cast<const void*>(head_bwd_kernel<kHeadBwdRows, 1, 1, 2>),
                       reinterpret_cast<const void*>(head_bwd_kernel<kHeadBwdRows, 1, 1, 3>),
