@@ -13,10 +13,13 @@ typedef __bf16 gbf16x2 __attribute__((ext_vector_type(2)));
 
 // a . b over one 8-column chunk of packed bf16 pairs (the per-edge logit z_i . z_j of the
 // bf16 edge kernels): four v_dot2_f32_bf16 on the packed words, no widening
+// (the words go through plain arrays first: bit-casting the ext_vector elements in place
+// made hipcc feed the first word to all four dot2 instructions)
 __device__ __forceinline__ float dot8_bf16(const u32x4& a, const u32x4& b, float acc) {
+  const unsigned wa[4] = {a.x, a.y, a.z, a.w}, wb[4] = {b.x, b.y, b.z, b.w};
 #pragma unroll
   for (int p = 0; p < 4; ++p)
-    acc = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(gbf16x2, a[p]), __builtin_bit_cast(gbf16x2, b[p]),
+    acc = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(gbf16x2, wa[p]), __builtin_bit_cast(gbf16x2, wb[p]),
                                           acc, false);
   return acc;
 }
@@ -78,9 +81,10 @@ __device__ __forceinline__ void acc8v(float (&a)[8], const u32x4& v) {
   asm volatile("s_mov_b32 %0, 0x3f800000" : "=s"(hi1u));
   const gbf16x2 lo1 = __builtin_bit_cast(gbf16x2, lo1u);
   const gbf16x2 hi1 = __builtin_bit_cast(gbf16x2, hi1u);
+  const unsigned w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
   for (int p = 0; p < 4; ++p) {
-    const gbf16x2 x = __builtin_bit_cast(gbf16x2, v[p]);
+    const gbf16x2 x = __builtin_bit_cast(gbf16x2, w[p]);
     a[2 * p] = __builtin_amdgcn_fdot2_f32_bf16(x, lo1, a[2 * p], false);
     a[2 * p + 1] = __builtin_amdgcn_fdot2_f32_bf16(x, hi1, a[2 * p + 1], false);
   }
