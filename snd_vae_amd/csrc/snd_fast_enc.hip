@@ -483,7 +483,15 @@ __global__ void __launch_bounds__(NT) edge_bf16_kernel(EdgeBfArgs a) {
   const __amdgpu_buffer_rsrc_t rs = rows_rsrc(a.z, (long long)a.R * a.d * 2);
   gather_rows16<NQ>(a.colidx, rv ? a.rowptr[r] : 0, rv ? a.rowptr[r + 1] : 0, rs, 2u * a.d, sub,
                     [&](int, const u32x4 (&v)[NQ], bool valid) {
-    float dot = 0.f;
+    float zj[NQ][8], dot = 0.f;
+#pragma unroll
+    for (int q = 0; q < NQ; ++q)
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        const unsigned w = v[q][p];
+        zj[q][2 * p] = qv[q] ? __uint_as_float(w << 16) : 0.f;
+        zj[q][2 * p + 1] = qv[q] ? __uint_as_float(w & 0xFFFF0000u) : 0.f;
+      }
 #pragma unroll
     for (int q = 0; q < NQ; ++q)
       if (qv[q]) dot = dot8_bf16(zip[q], v[q], dot);   // as head_bwd_kernel
@@ -495,7 +503,8 @@ __global__ void __launch_bounds__(NT) edge_bf16_kernel(EdgeBfArgs a) {
     tp += L > 0.f ? 1u : 0u;
 #pragma unroll
     for (int q = 0; q < NQ; ++q)
-      if (qv[q]) acc8_axpy(acc[q], v[q], coef, pw == 1.f);   // as head_bwd_kernel
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[q][j] += coef * zj[q][j];
   });
   if (rv) {
 #pragma unroll

@@ -90,33 +90,6 @@ __device__ __forceinline__ void acc8v(float (&a)[8], const u32x4& v) {
   }
 }
 
-// a[0..7] += coef * the 8 bf16 of a packed chunk (the per-edge gradient sum_j coef_ij z_j).
-// neg1 (pos_weight == 1, the reference's effective value: every coefficient is -1): dot2
-// with (-1, 0) / (0, -1), one rounding of a - z like the FMA, no widening; otherwise the
-// widened values through explicit FMAs.  Shared by the bf16 edge kernels (bitwise alike).
-__device__ __forceinline__ void acc8_axpy(float (&a)[8], const u32x4& v, float coef, bool neg1) {
-  const unsigned w[4] = {v.x, v.y, v.z, v.w};
-  if (neg1) {
-    unsigned lo1u, hi1u;   // the bf16 pairs (-1, 0) and (0, -1), through SGPRs as in acc8v
-    asm volatile("s_mov_b32 %0, 0xbf80" : "=s"(lo1u));
-    asm volatile("s_mov_b32 %0, 0xbf800000" : "=s"(hi1u));
-    const gbf16x2 lo1 = __builtin_bit_cast(gbf16x2, lo1u);
-    const gbf16x2 hi1 = __builtin_bit_cast(gbf16x2, hi1u);
-#pragma unroll
-    for (int p = 0; p < 4; ++p) {
-      const gbf16x2 x = __builtin_bit_cast(gbf16x2, w[p]);
-      a[2 * p] = __builtin_amdgcn_fdot2_f32_bf16(x, lo1, a[2 * p], false);
-      a[2 * p + 1] = __builtin_amdgcn_fdot2_f32_bf16(x, hi1, a[2 * p + 1], false);
-    }
-  } else {
-#pragma unroll
-    for (int p = 0; p < 4; ++p) {
-      a[2 * p] = __fmaf_rn(coef, __uint_as_float(w[p] << 16), a[2 * p]);
-      a[2 * p + 1] = __fmaf_rn(coef, __uint_as_float(w[p] & 0xFFFF0000u), a[2 * p + 1]);
-    }
-  }
-}
-
 // the 8 bf16 of a packed chunk, widened
 __device__ __forceinline__ void widen8(float (&a)[8], const u32x4& v) {
 #pragma unroll

@@ -434,7 +434,15 @@ __global__ void __launch_bounds__(HR * 8) head_bwd_kernel(HeadBwdArgs a) {
       const __amdgpu_buffer_rsrc_t rsd = rows_rsrc(a.zb, (long long)a.R * L * 2);
       gather_rows16<NQ>(a.colidx, a.rowptr[r], a.rowptr[r + 1], rsd, 2u * L, sub,
                         [&](int, const u32x4 (&v)[NQ], bool valid) {
-        float dot = 0.f;
+        float zj[NQ][8], dot = 0.f;
+#pragma unroll
+        for (int q = 0; q < NQ; ++q)
+#pragma unroll
+          for (int p = 0; p < 4; ++p) {
+            const unsigned wv = v[q][p];
+            zj[q][2 * p] = qv[q] ? __uint_as_float(wv << 16) : 0.f;
+            zj[q][2 * p + 1] = qv[q] ? __uint_as_float(wv & 0xFFFF0000u) : 0.f;
+          }
 #pragma unroll
         for (int q = 0; q < NQ; ++q)
           if (qv[q]) dot = dot8_bf16(zi[q], v[q], dot);   // as edge_bf16_kernel
@@ -446,7 +454,8 @@ __global__ void __launch_bounds__(HR * 8) head_bwd_kernel(HeadBwdArgs a) {
         tp += Lij > 0.f ? 1u : 0u;
 #pragma unroll
         for (int q = 0; q < NQ; ++q)
-          if (qv[q]) acc8_axpy(ej[q], v[q], coef, pw == 1.f);   // as edge_bf16_kernel
+#pragma unroll
+          for (int j = 0; j < 8; ++j) ej[q][j] += coef * zj[q][j];
       });
     }
     if (sub != 0 || !rv) { lossr = 0.f; tp = 0; }   // the row's 8 lanes hold the same sums
