@@ -17,6 +17,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--graphs", type=int, default=8)
     ap.add_argument("--flags", default="0", help="extra measurement-only debug bits, comma list")
+    ap.add_argument("--per-seg", type=int, default=64, help="items per segment (C2: 64 row chunks)")
     args = ap.parse_args()
     import numpy as np
     import torch
@@ -64,6 +65,15 @@ def main():
             d = d[~np.isnan(d)]
             if len(d):
                 print(f"  {names[a_]:>9s} -> {names[b_]:9s} median {np.median(d):6.2f}  p90 {np.percentile(d, 90):6.2f}  n {len(d)}")
+        # per segment (items are numbered segment-major; --per-seg items per segment)
+        idx = np.nonzero(raw[:n * 12].reshape(n, 12)[:, 9] != 0)[0]
+        seg = idx // args.per_seg
+        for sg in np.unique(seg):
+            m = seg == sg
+            lf = rel[m, 9] - rel[m, 0]
+            u = rel[m, 6] - rel[m, 3]
+            print(f"  segment {int(sg):2d}: {int(m.sum())} wg, start median {np.median(rel[m, 0]):6.2f}, "
+                  f"lifetime median {np.median(lf):6.2f} max {lf.max():6.2f}, units u0->u3 median {np.nanmedian(u):5.2f} us")
         life = rel[:, 9] - rel[:, 0]
         print(f"  lifetime median {np.median(life):.2f}  p10 {np.percentile(life, 10):.2f}  p90 {np.percentile(life, 90):.2f} us")
         # per CU: workgroups and the idle gaps between one workgroup's end and the next start
