@@ -1972,9 +1972,10 @@ extern "C" int snd_train_step(const snd_plan_t* plan, const snd_batch_t* batch,
   SND_TRY(join(x));   // weight-gradient slabs from the side stream
   if (x.wq && !x.wq->empty()) {
     // largest weight first: its workgroups start in the first wave of the launch
-    // (A/B, host debug bit 1 << 25: the k = 5 weights with narrow outputs first -- the
-    // round-5 stamps measured their workgroups longest, 20 us against 10-15)
-    const bool k5n = debug_flags() & (1 << 25);
+    // except the k = 5 weights with narrow outputs (the decoder's conv2): the round-5 stamps
+    // (tools/wg_stamps.py) measured their workgroups longest, 20 us against 10-15, so they
+    // start first (C2 step 0.2178 -> 0.2168 ms; host debug bit 1 << 25: the plain order)
+    const bool k5n = !(debug_flags() & (1 << 25));
     auto key = [k5n](const WgArgs& u) {
       const long long c = (long long)u.T * u.K * u.N;
       return k5n && u.T == 5 && u.N <= 32 && u.K >= 32 ? 8 * c : c;
