@@ -991,10 +991,6 @@ static int wg_split(const WgArgs& a, WgArgs* out, int cap) {
       w.dy = static_cast<const __bf16*>(a.dy) + n0;
       w.wk0 = a.wk0 + k0; w.wn0 = a.wn0 + n0;
       w.pairs_per_wg = std::min(a.pairs_per_wg, a.T * cdiv(w.K, 16));
-      if ((debug_flags() & (1 << 26)) && w.pairs_per_wg > WGT / 64) {   // A/B: one pair per wave
-        const int P = a.T * cdiv(w.K, 16);
-        w.pairs_per_wg = cdiv(P, cdiv(P, WGT / 64));
-      }
       out[n++] = w;
     }
   return n;
