@@ -390,7 +390,12 @@ extern "C" int snd_plan_create(const snd_config_t* cfg, int n_graphs, snd_plan_t
     if (ok) {
       p->fast = true;
       p->m1 = m1; p->m2 = m2;
-      p->ld1 = (int)round_up(w1, 8); p->ld2 = (int)round_up(w2, 8); p->ld3 = (int)round_up(c.s3, 8);
+      // row pitch of the decoder activations (A/B build knob SND_LD_ALIGN: elements)
+#ifndef SND_LD_ALIGN
+#define SND_LD_ALIGN 8
+#endif
+      p->ld1 = (int)round_up(w1, SND_LD_ALIGN); p->ld2 = (int)round_up(w2, SND_LD_ALIGN);
+      p->ld3 = (int)round_up(c.s3, 8);
       const char* nm[6] = {"PK1F", "PK2F", "PK3F", "PK3B", "PK2B", "PK1B"};
       for (int i = 0; i < 6; ++i) {
         p->add_buf(nm[i], (long long)pack_bytes(ims[i].T, ims[i].kp, ims[i].np), 1);
