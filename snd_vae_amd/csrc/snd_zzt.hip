@@ -40,10 +40,6 @@
 #define SND_ZZT_V9 1     // the d = 64 kernel: 1 v9 (two 512-thread workgroups per CU, round 5:
 #endif                   // 55.2 vs v4's 56.7 us), 0 v4, 2 v9 with v7's stagger (55.7 us); A/B builds
 
-#ifndef SND_ZZT_BALLOT
-#define SND_ZZT_BALLOT 0
-#endif
-
 namespace snd {
 namespace {
 
@@ -1196,7 +1192,6 @@ zzt_dense_bf16_v9(ZztArgs a) {
   };
   float lacc = 0.f;
   double ltot = 0.0;
-  unsigned scnt = 0;   // SND_ZZT_BALLOT: the wave's count (uniform)
   unsigned lcnt = 0;
   bool ovf = false;   // sticky per wave, as v4
   auto epi = [&](const f32x16& Y, bf16x8 (&sA)[2]) {   // v4's epilogue, y = -x
@@ -1207,12 +1202,6 @@ zzt_dense_bf16_v9(ZztArgs a) {
       q[v] = e + 1.f;
       sA[v >> 3][v & 7] = (__bf16)__builtin_amdgcn_rcpf(q[v]);
     }
-#if SND_ZZT_BALLOT
-    // sign bits counted on the scalar unit: one compare per logit, the lane masks popcounted
-    // by SALU (A/B against the per-lane perm / popcount of v4)
-#pragma unroll
-    for (int v = 0; v < 16; ++v) scnt += (unsigned)__popcll(__ballot(__float_as_int(Y[v]) < 0));
-#else
 #pragma unroll
     for (int g4 = 0; g4 < 4; ++g4) {
       const unsigned t01 = __builtin_amdgcn_perm(__float_as_uint(Y[4 * g4 + 1]),
@@ -1221,7 +1210,6 @@ zzt_dense_bf16_v9(ZztArgs a) {
                                                  __float_as_uint(Y[4 * g4 + 2]), 0x07030C0Cu);
       lcnt += (unsigned)__builtin_popcount((t01 | t23) & 0x80808080u);
     }
-#endif
     if (!ovf) {
 #pragma unroll
       for (int p = 0; p < 4; ++p)
@@ -1355,7 +1343,7 @@ zzt_dense_bf16_v9(ZztArgs a) {
     }
   }
   const double l = wave_sum_d(ltot);
-  const unsigned wcnt = SND_ZZT_BALLOT ? __builtin_amdgcn_readfirstlane(scnt) : wave_sum_u(lcnt);
+  const unsigned wcnt = wave_sum_u(lcnt);
   if (lane == 0) { sl[w] = l; sc[w] = wcnt - dpos; }
   __syncthreads();
   if (tid == 0) {
