@@ -1029,11 +1029,8 @@ int launch_wgrad_multi(const WgArgs* a0, int n, hipStream_t s) {
     SND_CHECK_ARG(nw >= 0, "wgrad_multi: window split");
     for (int j = 0; j < nw; ++j) all.push_back(win[j]);
   }
-  if (debug_flags() & (3 << 26)) {   // 1 << 26: classes 0, 1, 2; 1 << 27: classes 1, 0, 2
-    const bool lf = debug_flags() & (1 << 27);
-    auto rank = [lf](const WgArgs& w) { const int c = wg_class(w); return lf && c < 2 ? 1 - c : c; };
-    std::stable_sort(all.begin(), all.end(), [&](const WgArgs& u, const WgArgs& v) { return rank(u) < rank(v); });
-  }
+  if (debug_flags() & (1 << 26))
+    std::stable_sort(all.begin(), all.end(), [](const WgArgs& u, const WgArgs& v) { return wg_class(u) < wg_class(v); });
   const WgArgs* a = all.data();
   n = (int)all.size();
   WgMultiPack pk{};
