@@ -22,7 +22,6 @@
 #include "snd_pack.hpp"
 
 #include <algorithm>
-#include <vector>
 
 namespace snd {
 
@@ -1008,31 +1007,9 @@ static int wg_multi_flush(WgMultiPack& pk, int total, size_t lds, hipStream_t s)
   return 0;
 }
 
-// dispatch class of a window (A/B, host debug bit 1 << 26): the k = 5 weights with >= 32 input
-// columns first (they fill the CUs' first slots), then the light windows (<= 16 input
-// columns, or k = 5 with < 32: they take the second slots, where the younger waves lose the
-// issue arbitration to the first, round-5 stamps), then the rest
-static int wg_class(const WgArgs& w) {
-  if (w.T == 5 && w.K >= 32) return 0;
-  if (w.K <= 16 || w.T == 5) return 1;
-  return 2;
-}
-
-// one launch per kMaxWgMulti segments (C2: 12 segments after the window split, one launch)
-int launch_wgrad_multi(const WgArgs* a0, int n, hipStream_t s) {
+// one launch per kMaxWgMulti segments (C2: 13 segments after the window split, one launch)
+int launch_wgrad_multi(const WgArgs* a, int n, hipStream_t s) {
   if (n <= 0) return 0;
-  std::vector<WgArgs> all;
-  for (int i = 0; i < n; ++i) {
-    WgArgs win[4];
-    const WgArgs x0 = wg_norm(a0[i]);
-    const int nw = x0.R > 0 ? wg_split(x0, win, 4) : 0;
-    SND_CHECK_ARG(nw >= 0, "wgrad_multi: window split");
-    for (int j = 0; j < nw; ++j) all.push_back(win[j]);
-  }
-  if (debug_flags() & (1 << 26))
-    std::stable_sort(all.begin(), all.end(), [](const WgArgs& u, const WgArgs& v) { return wg_class(u) < wg_class(v); });
-  const WgArgs* a = all.data();
-  n = (int)all.size();
   WgMultiPack pk{};
   size_t lds = 0;
   int total = 0;
