@@ -640,9 +640,11 @@ struct WgMultiPack {
 };
 static_assert(sizeof(WgMultiPack) <= 4096, "wgrad_multi: kernel arguments over 4 KB");
 
-// One workgroup's item of the multi-segment launch; WIDE: output blocks up to 8 (whole weights)
-template <bool WIDE>
-__device__ __forceinline__ void wgrad_multi_items(const WgMultiPack& m) {
+// Every segment is at most 64 columns of dy wide (launch_wgrad_multi splits wider ones)
+// and its staging at most 68 KB: the kernel is built for 8 waves per SIMD (<= 64 VGPRs),
+// two workgroups per CU.
+__global__ void __launch_bounds__(WGT) __attribute__((amdgpu_waves_per_eu(8, 8)))
+wgrad_multi_kernel(WgMultiPack m) {
   extern __shared__ __attribute__((aligned(16))) __bf16 lds[];
   __shared__ unsigned tsl[kWgStampWords];
   const bool stamp = (kdbg(m.a[0].dbg) & (1 << 21)) && m.a[0].stamps;
@@ -669,15 +671,11 @@ __device__ __forceinline__ void wgrad_multi_items(const WgMultiPack& m) {
   if (kdbg(a.dbg) & 16) return;   // measurement only: launch + segment lookup
   unsigned* ts = stamp ? tsl : nullptr;
   wg_stamp(ts, 1, stamp);
-  switch (WIDE ? (a.N + 15) >> 4 : min((a.N + 15) >> 4, 4)) {
+  switch ((a.N + 15) >> 4) {
     case 1: if (two) wgrad_body<1, 2>(a, bx, by, lds, ts); else wgrad_body<1>(a, bx, by, lds, ts); break;
     case 2: if (two) wgrad_body<2, 2>(a, bx, by, lds, ts); else wgrad_body<2>(a, bx, by, lds, ts); break;
     case 3: if (two) wgrad_body<3, 2>(a, bx, by, lds, ts); else wgrad_body<3>(a, bx, by, lds, ts); break;
-    case 4: if (two) wgrad_body<4, 2>(a, bx, by, lds, ts); else wgrad_body<4>(a, bx, by, lds, ts); break;
-    case 5: if constexpr (WIDE) { if (two) wgrad_body<5, 2>(a, bx, by, lds, ts); else wgrad_body<5>(a, bx, by, lds, ts); } break;
-    case 6: if constexpr (WIDE) { if (two) wgrad_body<6, 2>(a, bx, by, lds, ts); else wgrad_body<6>(a, bx, by, lds, ts); } break;
-    case 7: if constexpr (WIDE) { if (two) wgrad_body<7, 2>(a, bx, by, lds, ts); else wgrad_body<7>(a, bx, by, lds, ts); } break;
-    default: if constexpr (WIDE) { if (two) wgrad_body<8, 2>(a, bx, by, lds, ts); else wgrad_body<8>(a, bx, by, lds, ts); } break;
+    default: if (two) wgrad_body<4, 2>(a, bx, by, lds, ts); else wgrad_body<4>(a, bx, by, lds, ts); break;
   }
   if (stamp) {
     __syncthreads();
@@ -690,17 +688,6 @@ __device__ __forceinline__ void wgrad_multi_items(const WgMultiPack& m) {
     }
   }
 }
-
-// Every segment at most 64 columns of dy wide and <= 68 KB of staging (the window split):
-// built for 8 waves per SIMD (<= 64 VGPRs), two workgroups per CU.
-__global__ void __launch_bounds__(WGT) __attribute__((amdgpu_waves_per_eu(8, 8)))
-wgrad_multi_kernel(WgMultiPack m) { wgrad_multi_items<false>(m); }
-
-// Whole weights up to 128 columns (no window split), one workgroup per CU: the plans of
-// under 32768 rows (C5's one N = 16384 graph, a data-parallel rank's one graph), where
-// the split's duplicated staging cost more than the second workgroup gained (round 5: C5
-// 0.3993 vs 0.4049 ms)
-__global__ void __launch_bounds__(WGT) wgrad_multi_wide_kernel(WgMultiPack m) { wgrad_multi_items<true>(m); }
 
 // ---------------------------------------------------------------- heads
 struct HeadFastPack { HeadFastArgs h[2]; };
@@ -861,7 +848,6 @@ int wg_launch(const WgArgs& a, dim3 grid, hipStream_t s) {
 }
 
 constexpr size_t kMaxDynLds = kRcLdsLimit;
-constexpr size_t kWgWideLds = 159 * 1024;     // whole weights: up to 133 KB (k = 5, 128 x 128)
 constexpr size_t kWgMultiLds = 128 * 1024;   // segments stage <= 68 KB (window split); room for static LDS
 
 }  // namespace
@@ -1010,14 +996,13 @@ static int wg_split(const WgArgs& a, WgArgs* out, int cap) {
   return n;
 }
 
-static int wg_multi_flush(WgMultiPack& pk, int total, size_t lds, hipStream_t s, bool wide) {
+static int wg_multi_flush(WgMultiPack& pk, int total, size_t lds, hipStream_t s) {
   if (pk.nseg == 0) return 0;
   for (int i = pk.nseg; i <= kMaxWgMulti; ++i) pk.start[i] = total;
   bool uniform = pk.nseg > 1;
   for (int i = 1; i < pk.nseg; ++i) uniform = uniform && pk.start[i + 1] - pk.start[i] == pk.start[1];
   const dim3 grid = uniform ? dim3(pk.start[1], pk.nseg) : dim3(total);
-  if (wide) hipLaunchKernelGGL(wgrad_multi_wide_kernel, grid, dim3(WGT), lds, s, pk);
-  else hipLaunchKernelGGL(wgrad_multi_kernel, grid, dim3(WGT), lds, s, pk);
+  hipLaunchKernelGGL(wgrad_multi_kernel, grid, dim3(WGT), lds, s, pk);
   SND_LAUNCH_CHECK("wgrad_multi_kernel");
   return 0;
 }
@@ -1025,8 +1010,6 @@ static int wg_multi_flush(WgMultiPack& pk, int total, size_t lds, hipStream_t s,
 // one launch per kMaxWgMulti segments (C2: 13 segments after the window split, one launch)
 int launch_wgrad_multi(const WgArgs* a, int n, hipStream_t s) {
   if (n <= 0) return 0;
-  // under 32768 rows: whole weights on the wide kernel (host debug bit 1 << 26: the windows)
-  const bool wide = a[0].R < 32768 && !(debug_flags() & (1 << 26));
   WgMultiPack pk{};
   size_t lds = 0;
   int total = 0;
@@ -1044,12 +1027,11 @@ int launch_wgrad_multi(const WgArgs* a, int n, hipStream_t s) {
     SND_CHECK_ARG(x0.sn4 % 4 == 0 && x0.wn0 % 4 == 0 && x0.wk0 + x0.K <= x0.sK &&
                   x0.wn0 + wgrad_n4(x0.N) <= x0.sn4, "wgrad_multi: slab window");
     WgArgs win[4];
-    win[0] = x0;
-    const int nw = wide ? 1 : wg_split(x0, win, 4);
+    const int nw = wg_split(x0, win, 4);
     SND_CHECK_ARG(nw > 0, "wgrad_multi: window split");
     for (int j = 0; j < nw; ++j) {
       if (pk.nseg == kMaxWgMulti) {   // pack full: launch it, start the next
-        SND_TRY(wg_multi_flush(pk, total, lds, s, wide));
+        SND_TRY(wg_multi_flush(pk, total, lds, s));
         pk = WgMultiPack{};
         lds = 0;
         total = 0;
@@ -1063,7 +1045,7 @@ int launch_wgrad_multi(const WgArgs* a, int n, hipStream_t s) {
       ++pk.nseg;
     }
   }
-  return wg_multi_flush(pk, total, lds, s, wide);
+  return wg_multi_flush(pk, total, lds, s);
 }
 
 WgGeom wgrad_geom(int R, int T, int K, int N, int chunks) {
@@ -1129,11 +1111,6 @@ static int fast_init_attributes_once() {
   SND_ATTR((wgrad_kernel<4>)) SND_ATTR((wgrad_kernel<5>)) SND_ATTR((wgrad_kernel<6>))
   SND_ATTR((wgrad_kernel<7>)) SND_ATTR((wgrad_kernel<8>))
 #undef SND_ATTR
-  if (hipFuncSetAttribute(reinterpret_cast<const void*>(wgrad_multi_wide_kernel),
-                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)kWgWideLds) != hipSuccess) {
-    set_error("hipFuncSetAttribute(wgrad_multi_wide_kernel) failed");
-    return SND_ERR_HIP;
-  }
   if (hipFuncSetAttribute(reinterpret_cast<const void*>(wgrad_multi_kernel),
                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)kWgMultiLds) != hipSuccess) {
     set_error("hipFuncSetAttribute(wgrad_multi_kernel) failed");
