@@ -31,7 +31,6 @@ namespace {
 
 constexpr int DT = 1024;                  // 16 waves
 constexpr int NW = DT / 64;
-constexpr int TR = kDecRows;
 // dynamic LDS of both kernels (their static LDS -- column parameters, head partials -- stays
 // below 160 KB - kDynLds)
 constexpr int kDynLds = 148 * 1024;
@@ -63,10 +62,11 @@ __host__ __device__ constexpr int head_scr_bytes() {
 __host__ __device__ __forceinline__ int in_rows(int n_out) { return rup(n_out, 16) + 4; }
 
 // ---- LDS layouts (bytes), shared by host (launch size) and device
+// (TR: the tile's own rows, kDecRows or kDecRowsSmall)
 struct FwdLay {
   int w, a, b, c, total;        // offsets: weights | A: J -> U2 | B: U1 -> U3,Y3 | C: Y2n
   int ldY2n;
-  __host__ __device__ FwdLay(const DecChainFwdArgs& p) {
+  __host__ __device__ FwdLay(const DecChainFwdArgs& p, int TR) {
     const int wb = max(max(max(p.k1.np * p.k1.kp, p.k2.np * p.k2.kp), p.k3.np * p.k3.kp) * 5 * 2,
                        (head_scr_bytes() + 1023) & ~1023);
     const int kp_u2 = p.m2.phys() <= 32 ? 32 : (p.m2.phys() <= 64 ? 64 : 128);
@@ -81,7 +81,7 @@ struct FwdLay {
 };
 struct BwdLay {
   int w, d3, d2, d1, cps, total;
-  __host__ __device__ BwdLay(const DecChainBwdArgs& p) {
+  __host__ __device__ BwdLay(const DecChainBwdArgs& p, int TR) {
     const int wb = max(max(p.k3t.np * p.k3t.kp, p.k2t.np * p.k2t.kp), p.k1t.np * p.k1t.kp) * 5 * 2;
     w = 0;
     d3 = wb;
@@ -97,6 +97,7 @@ struct BwdLay {
 
 // tile -> own rows [r0, rend) of graph [glo, ghi)
 struct Tile { int r0, rend, glo, ghi; };
+template <int TR>
 __device__ __forceinline__ Tile tile_of(int t, int npg) {
   const int tpg = (npg + TR - 1) / TR;
   const int g = t / tpg, lt = t - g * tpg;
@@ -319,12 +320,13 @@ __device__ __forceinline__ void head_tile(int hi, int orow, bool rv, long long g
 }
 
 // ------------------------------------------------------------------ forward
+template <int TR>
 __global__ void __launch_bounds__(DT) dec_fwd_kernel(DecChainFwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   __shared__ __attribute__((aligned(16))) float cp1[3][128], cp2[3][128], cp3[3][16];
   __shared__ float hp[2][64];   // head parameters (head_tile layout)
-  const FwdLay L(a);
-  const Tile tl = tile_of(blockIdx.x, a.npg);
+  const FwdLay L(a, TR);
+  const Tile tl = tile_of<TR>(blockIdx.x, a.npg);
   const int tid = threadIdx.x, lane = tid & 63, lg = lane >> 4;
   __bf16* wimg = reinterpret_cast<__bf16*>(smem + L.w);
   __bf16* jimg = reinterpret_cast<__bf16*>(smem + L.a);
@@ -381,11 +383,11 @@ __global__ void __launch_bounds__(DT) dec_fwd_kernel(DecChainFwdArgs a) {
     hp[hh][j] = v;
   }
   float tg[2] = {0.f, 0.f};
-  if (tid < 256) {
-    const int orow = tid & 127;
+  if (tid < 2 * TR) {
+    const int orow = tid % TR;
     const long long gr = tl.r0 + orow;
     if (orow < own) {
-      if (tid < 128) { tg[0] = a.s_truth[gr * 2]; tg[1] = a.s_truth[gr * 2 + 1]; }
+      if (tid < TR) { tg[0] = a.s_truth[gr * 2]; tg[1] = a.s_truth[gr * 2 + 1]; }
       else tg[0] = a.x_truth[gr];
     }
   }
@@ -513,15 +515,15 @@ __global__ void __launch_bounds__(DT) dec_fwd_kernel(DecChainFwdArgs a) {
   }
   __syncthreads();
   if (stamp) ts[6] = __builtin_amdgcn_s_memrealtime();
-  // ---- heads: spatial (s3 -> sd) on threads 0..127, node (n2 -> nf) on 128..255; the
+  // ---- heads: spatial (s3 -> sd) on threads [0, TR), node (n2 -> nf) on [TR, 2 TR); the
   // per-row partial quantities go to scratch over the (now idle) weight image
   const int t = blockIdx.x;
   constexpr int NQS = head_nq(10, 2), NQN = head_nq(20, 1);
   float* scr = reinterpret_cast<float*>(smem + L.w);
   double* sscr = reinterpret_cast<double*>(smem + L.w + (NQS + NQN) * kScr * 4);
   if (!(kdbg(a.dbg) & 2)) {
-    if (tid < 256) {
-      const int hi = tid >> 7, orow = tid & 127;
+    if (tid < 2 * TR) {
+      const int hi = tid / TR, orow = tid % TR;
       const bool rv = orow < own;
       const long long gr = tl.r0 + orow;
       if (hi == 0) {
@@ -540,24 +542,24 @@ __global__ void __launch_bounds__(DT) dec_fwd_kernel(DecChainFwdArgs a) {
         }
         const float t1[1] = {tg[0]};
         head_tile<20, 1>(1, orow, rv, gr, u, yv, hp[1], t1, a.cnt_n, a.xhat, a.dy2 + gr * a.lddy2 + a.m2.offb,
-                         scr + NQS * kScr, sscr + 128);
+                         scr + NQS * kScr, sscr + TR);
       }
     }
     __syncthreads();
     if (stamp) ts[7] = __builtin_amdgcn_s_memrealtime();
-    // tile partials: each quantity summed over the 128 rows in order
+    // tile partials: each quantity summed over the TR rows in order
     if (tid < NQS + NQN) {
       const float* src = scr + tid * kScr;
       float v = 0.f;
 #pragma unroll 32
-      for (int r = 0; r < 128; ++r) v += src[r];
+      for (int r = 0; r < TR; ++r) v += src[r];
       if (tid < NQS) a.phs[(long long)t * NQS + tid] = v;
       else a.phn[(long long)t * NQN + tid - NQS] = v;
     } else if (tid >= 256 && tid < 258) {
-      const double* src = sscr + 128 * (tid - 256);
+      const double* src = sscr + TR * (tid - 256);
       double v = 0.0;
 #pragma unroll 32
-      for (int r = 0; r < 128; ++r) v += src[r];
+      for (int r = 0; r < TR; ++r) v += src[r];
       (tid == 256 ? a.sse_s : a.sse_n)[t] = v;
     }
   }
@@ -588,11 +590,12 @@ __device__ __forceinline__ void colpart_flush(float (&q)[3][NBH][4], float* slot
       }
 }
 
+template <int TR>
 __global__ void __launch_bounds__(DT) dec_bwd_kernel(DecChainBwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   __shared__ __attribute__((aligned(16))) float cpa[2][128], cpb[2][128];   // conv2-s BN (gamma c, beta), conv1 BN
-  const BwdLay L(a);
-  const Tile tl = tile_of(blockIdx.x, a.npg);
+  const BwdLay L(a, TR);
+  const Tile tl = tile_of<TR>(blockIdx.x, a.npg);
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, lg = lane >> 4;
   __bf16* wimg = reinterpret_cast<__bf16*>(smem + L.w);
   __bf16* d3 = reinterpret_cast<__bf16*>(smem + L.d3);
@@ -787,7 +790,13 @@ __global__ void __launch_bounds__(DT) dec_bwd_kernel(DecChainBwdArgs a) {
 
 }  // namespace
 
-int dec_tiles(int ngraphs, int npg) { return ngraphs * ((npg + kDecRows - 1) / kDecRows); }
+int dec_rows(int ngraphs, int npg) {
+  return ngraphs * ((npg + kDecRows - 1) / kDecRows) < kDecSmall ? kDecRowsSmall : kDecRows;
+}
+int dec_tiles(int ngraphs, int npg) {
+  const int tr = dec_rows(ngraphs, npg);
+  return ngraphs * ((npg + tr - 1) / tr);
+}
 int dec_head_parts(int cin, int cout) { return head_nq(cin, cout); }
 
 bool dec_fused_supported(int dj, const ColMap& m1, const ColMap& m2, int s3, int sd, int nf,
@@ -800,7 +809,7 @@ bool dec_fused_supported(int dj, const ColMap& m1, const ColMap& m2, int s3, int
   DecChainBwdArgs b{};
   b.k3t = k3t; b.k2t = k2t; b.k1t = k1t; b.m1 = m1; b.m2 = m2; b.s3 = s3; b.dj = dj;
   const int lim = kDynLds;
-  if (FwdLay(f).total > lim || BwdLay(b).total > lim) return false;
+  if (FwdLay(f, kDecRows).total > lim || BwdLay(b, kDecRows).total > lim) return false;
   if (k2.kp - k1.np > 16) return false;   // dec_fwd zeroes at most 4 pad groups of U1 per row
   // image kp: conv inputs must match the packed images
   if (k3.kp > 64 || k3t.np != 32 || k2t.np > 128 || k1t.np != ((dj + 15) / 16) * 16) return false;
@@ -811,13 +820,15 @@ bool dec_fused_supported(int dj, const ColMap& m1, const ColMap& m2, int s3, int
 }
 
 static int dec_init_attributes_once() {
-  if (hipFuncSetAttribute(reinterpret_cast<const void*>(dec_fwd_kernel),
-                          hipFuncAttributeMaxDynamicSharedMemorySize, kDynLds) != hipSuccess ||
-      hipFuncSetAttribute(reinterpret_cast<const void*>(dec_bwd_kernel),
-                          hipFuncAttributeMaxDynamicSharedMemorySize, kDynLds) != hipSuccess) {
-    set_error("dec: hipFuncSetAttribute failed");
-    return SND_ERR_HIP;
-  }
+  const void* ks[] = {reinterpret_cast<const void*>(dec_fwd_kernel<kDecRows>),
+                      reinterpret_cast<const void*>(dec_bwd_kernel<kDecRows>),
+                      reinterpret_cast<const void*>(dec_fwd_kernel<kDecRowsSmall>),
+                      reinterpret_cast<const void*>(dec_bwd_kernel<kDecRowsSmall>)};
+  for (const void* k : ks)
+    if (hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, kDynLds) != hipSuccess) {
+      set_error("dec: hipFuncSetAttribute failed");
+      return SND_ERR_HIP;
+    }
   return 0;
 }
 
@@ -835,8 +846,12 @@ int launch_dec_chain_fwd(const DecChainFwdArgs& a, hipStream_t s) {
   SND_CHECK_ARG(a.ldz % 8 == 0 && a.ldy1 % 4 == 0 && a.ldy2 % 4 == 0 && a.lddy3 % 4 == 0 && a.lddy2 % 4 == 0,
                 "dec_fwd: leading dims");
   SND_TRY(dec_init_attributes());
-  const size_t lds = FwdLay(a).total;
-  hipLaunchKernelGGL(dec_fwd_kernel, dim3(dec_tiles(a.ngraphs, a.npg)), dim3(DT), lds, s, a);
+  const int tr = dec_rows(a.ngraphs, a.npg);
+  const size_t lds = FwdLay(a, tr).total;
+  if (tr == kDecRowsSmall)
+    hipLaunchKernelGGL(dec_fwd_kernel<kDecRowsSmall>, dim3(dec_tiles(a.ngraphs, a.npg)), dim3(DT), lds, s, a);
+  else
+    hipLaunchKernelGGL(dec_fwd_kernel<kDecRows>, dim3(dec_tiles(a.ngraphs, a.npg)), dim3(DT), lds, s, a);
   SND_LAUNCH_CHECK("dec_fwd_kernel");
   return 0;
 }
@@ -848,8 +863,12 @@ int launch_dec_chain_bwd(const DecChainBwdArgs& a, hipStream_t s) {
   SND_CHECK_ARG(a.lddy3 % 8 == 0 && a.lddy2 % 4 == 0 && a.lddy1 % 4 == 0 && a.lddz % 4 == 0,
                 "dec_bwd: leading dims");
   SND_TRY(dec_init_attributes());
-  const size_t lds = BwdLay(a).total;
-  hipLaunchKernelGGL(dec_bwd_kernel, dim3(dec_tiles(a.ngraphs, a.npg)), dim3(DT), lds, s, a);
+  const int tr = dec_rows(a.ngraphs, a.npg);
+  const size_t lds = BwdLay(a, tr).total;
+  if (tr == kDecRowsSmall)
+    hipLaunchKernelGGL(dec_bwd_kernel<kDecRowsSmall>, dim3(dec_tiles(a.ngraphs, a.npg)), dim3(DT), lds, s, a);
+  else
+    hipLaunchKernelGGL(dec_bwd_kernel<kDecRows>, dim3(dec_tiles(a.ngraphs, a.npg)), dim3(DT), lds, s, a);
   SND_LAUNCH_CHECK("dec_bwd_kernel");
   return 0;
 }

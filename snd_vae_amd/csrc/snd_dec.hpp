@@ -6,6 +6,13 @@
 namespace snd {
 
 constexpr int kDecRows = 128;   // own rows per tile (one workgroup per tile, tiles never span graphs)
+// 64-row tiles when 128-row tiles would leave more than half the CUs idle (fewer than
+// kDecSmall tiles: one or two graphs of 4096 rows, the C3 per-rank step)
+constexpr int kDecRowsSmall = 64;
+#ifndef SND_DEC_SMALL
+#define SND_DEC_SMALL 128
+#endif
+constexpr int kDecSmall = SND_DEC_SMALL;
 
 // Packed weight image in the workspace (pack_kernel layout [tap][n][k], T = 5)
 struct DecImg { const __bf16* w; int kp, np; };
@@ -49,6 +56,7 @@ struct DecChainBwdArgs {
   int dbg;
 };
 
+int dec_rows(int ngraphs, int npg);    // kDecRows or kDecRowsSmall
 int dec_tiles(int ngraphs, int npg);
 int dec_head_parts(int cin, int cout);        // == heads_fast_parts
 bool dec_fused_supported(int dj, const ColMap& m1, const ColMap& m2, int s3, int sd, int nf,

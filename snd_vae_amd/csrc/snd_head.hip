@@ -647,9 +647,13 @@ __global__ void __launch_bounds__(HR * 8) head_bwd_kernel(HeadBwdArgs a) {
 
 template <int NQ, int NB1, int NB2>
 int head_bwd_launch(const HeadBwdArgs& a, hipStream_t s) {
-  const size_t lds = (size_t)BwdLay(a.kp1, a.np1, a.kp2, a.np2, a.L).total;
-  hipLaunchKernelGGL((head_bwd_kernel<kHeadBwdRows, NQ, NB1, NB2>), dim3(head_tiles(a.R)),
-                     dim3(kHeadBwdRows * 8), lds, s, a);
+  const int hr = head_bwd_rows(a.R);
+  const size_t lds = (size_t)BwdLay(a.kp1, a.np1, a.kp2, a.np2, a.L, hr).total;
+  if (hr == 64)
+    hipLaunchKernelGGL((head_bwd_kernel<64, NQ, NB1, NB2>), dim3(head_tiles(a.R)), dim3(64 * 8), lds, s, a);
+  else
+    hipLaunchKernelGGL((head_bwd_kernel<kHeadBwdRows, NQ, NB1, NB2>), dim3(head_tiles(a.R)),
+                       dim3(kHeadBwdRows * 8), lds, s, a);
   SND_LAUNCH_CHECK("head_bwd_kernel");
   return 0;
 }
@@ -850,7 +854,8 @@ int launch_front(FrontArgs& a, const PackDesc* pack, int npack, hipStream_t s) {
   return 0;
 }
 
-int head_tiles(int R) { return cdiv(R, kHeadBwdRows); }
+int head_bwd_rows(int R) { return cdiv(R, kHeadBwdRows) < kHeadBwdSmall ? 64 : kHeadBwdRows; }
+int head_tiles(int R) { return cdiv(R, head_bwd_rows(R)); }
 
 bool head_bwd_supported(int L, int gh, int W, int h1, int kp1, int np1, int kp2, int np2) {
   if ((L != 16 && L != 32 && L != 64) || kp1 != 2 * L) return false;
@@ -918,7 +923,15 @@ static int head_init_attributes_once() {
                       reinterpret_cast<const void*>(head_bwd_kernel<kHeadBwdRows, 1, 2, 1>),
                       reinterpret_cast<const void*>(head_bwd_kernel<kHeadBwdRows, 1, 2, 2>),
                       reinterpret_cast<const void*>(head_bwd_kernel<kHeadBwdRows, 1, 2, 3>),
-                      reinterpret_cast<const void*>(head_bwd_kernel<kHeadBwdRows, 1, 2, 4>)};
+                      reinterpret_cast<const void*>(head_bwd_kernel<kHeadBwdRows, 1, 2, 4>),
+                      reinterpret_cast<const void*>(head_bwd_kernel<64, 1, 1, 1>),
+                      reinterpret_cast<const void*>(head_bwd_kernel<64, 1, 1, 2>),
+                      reinterpret_cast<const void*>(head_bwd_kernel<64, 1, 1, 3>),
+                      reinterpret_cast<const void*>(head_bwd_kernel<64, 1, 1, 4>),
+                      reinterpret_cast<const void*>(head_bwd_kernel<64, 1, 2, 1>),
+                      reinterpret_cast<const void*>(head_bwd_kernel<64, 1, 2, 2>),
+                      reinterpret_cast<const void*>(head_bwd_kernel<64, 1, 2, 3>),
+                      reinterpret_cast<const void*>(head_bwd_kernel<64, 1, 2, 4>)};
   const void* kf[] = {reinterpret_cast<const void*>(enc_front_kernel<1>),
                       reinterpret_cast<const void*>(enc_front_kernel<2>),
                       reinterpret_cast<const void*>(enc_front_kernel<3>),

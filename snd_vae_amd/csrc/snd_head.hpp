@@ -59,11 +59,17 @@ struct HeadBwdArgs {
   int dbg;
 };
 bool head_bwd_supported(int L, int gh, int W, int h1, int kp1, int np1, int kp2, int np2);
-// rows per backward-head tile (round 5: 64-row tiles, two workgroups per CU, measured
-// head_bwd 25.4 vs 25.7 us with no step change, and their column partials no longer
-// match the unfused chain bit for bit: retired)
+// rows per backward-head tile: 128, or 64 when 128-row tiles would leave more than half
+// the CUs idle (fewer than kHeadBwdSmall tiles: one or two graphs of 4096 rows, the C3
+// per-rank step).  At the full batch 64-row tiles measured head_bwd 25.4 vs 25.7 us with
+// no step change (round 5), so the batch keeps 128.
 constexpr int kHeadBwdRows = 128;
-int head_tiles(int R);   // backward-head tiles (kHeadBwdRows rows each)
+#ifndef SND_HB_SMALL
+#define SND_HB_SMALL 128
+#endif
+constexpr int kHeadBwdSmall = SND_HB_SMALL;
+int head_bwd_rows(int R);
+int head_tiles(int R);   // backward-head tiles (head_bwd_rows(R) rows each)
 int launch_head_bwd(const HeadBwdArgs& a, hipStream_t s);
 
 // GraphConvolution 0 as (A X) W0 (gcn0 semantics: AX, H1 = [BN0(lrelu(AX W0)) | X]) and

@@ -148,7 +148,7 @@ struct snd_plan {
   // kernel's column splits and the decoder's 32-64 tiles do not both fill the chip, so the
   // fused decoder runs on the side stream beside zz^T, which leaves it dec_tiles CUs
   // (zzt_ts: the column splits every zz^T consumer uses -- launch, split sum, finalize)
-  // (default -1 = auto: on for graphs of N >= 2048 with at most 64 decoder tiles, i.e. one
+  // (default -1 = auto: on for graphs of N >= 2048 with at most 64 128-row tiles, i.e. one
   // or two N = 4096 graphs; C3's one-graph step 0.1704 -> 0.1626 ms,
   // profiles/r04_bench_strong_conc.json.  Small graphs stay serial: launch-bound)
   int conc_dec = -1;
@@ -156,7 +156,7 @@ struct snd_plan {
   int zzt_ts_conc = 1;   // ... of a step whose decoder runs beside zz^T (cdec)
   mutable int last_zts = 1;   // the split count the last snd_train_step used (snd_plan_launch)
   bool conc_dec_on() const {
-    return (conc_dec > 0 || (conc_dec < 0 && dtiles <= 64 && N >= 2048)) && fast && dec_fused && !tref;
+    return (conc_dec > 0 || (conc_dec < 0 && B * ((N + 127) / 128) <= 64 && N >= 2048)) && fast && dec_fused && !tref;
   }
   static constexpr int kEvents = 16;
   mutable hipStream_t side = nullptr;
@@ -315,7 +315,7 @@ extern "C" int snd_plan_create(const snd_config_t* cfg, int n_graphs, snd_plan_t
   p->add_buf("DP0", R * h0);  p->add_buf("DXW0", R * h0);
   const int nz = zzt_dense_blocks(p->B, p->N, dj, c.dtype), ne = edge_blocks(p->R, dj);
   const int nk = reparam_blocks(p->RH, L), nh = head_blocks(p->R), nc = col_blocks(p->R);
-  p->add_buf("PZZT", 2LL * nz, 8); p->add_buf("PEDGE", 2LL * std::max(ne, edge_bf16_blocks(p->R)), 8); p->add_buf("PKL", std::max({nk, reparam_prep_blocks(p->B, zzt_npad(p->N)), small_head_fwd_blocks(c.latent)}), 8);
+  p->add_buf("PZZT", 2LL * nz, 8); p->add_buf("PEDGE", 2LL * std::max({ne, edge_bf16_blocks(p->R), head_tiles(p->R)}), 8); p->add_buf("PKL", std::max({nk, reparam_prep_blocks(p->B, zzt_npad(p->N)), small_head_fwd_blocks(c.latent)}), 8);
   p->add_buf("STEPN", 1);   // *step + 1, for the fused-Adam reduction (ReduceAdam)
   p->add_buf("PSSES", nh, 8); p->add_buf("PSSEN", nh, 8);
   p->add_buf("PHS", (long long)nh * (c.s3 * c.spatial_dim + c.spatial_dim));

@@ -53,6 +53,8 @@ def test_edge_terms_vs_float64(pos_weight, debug):
     R, L = B * n, cfg.latent
     z = model.buffer("ZB", torch.bfloat16)[:R * L].view(R, L).double().cpu().numpy()
     tiles = (R + 127) // 128
+    if tiles < 128:   # head_bwd_rows (snd_head.hip): 64-row tiles below 128 tiles of 128 rows
+        tiles = (R + 63) // 64
     pe = model.buffer("PEDGE", torch.float64).cpu().numpy()
     got_loss = float(pe[0:2 * tiles:2].sum()) if debug == 0 else float(pe[0::2].sum())
     got_tp = float(pe[1:2 * tiles:2].sum()) if debug == 0 else float(pe[1::2].sum())

@@ -476,7 +476,8 @@ def test_fused_backward_head_matches_chain(n, d, B):
     launch) against edge_bf16 + reparam_bwd_fast + two row-engine launches (debug bit
     262144): d[mu | s], dh and dP1 are bitwise equal and so is every weight gradient
     computed from them; the bias gradient of the [mu | s] head and the edge loss partials
-    group rows differently (agree to fp32 / fp64 reassociation)."""
+    group rows differently (agree to fp32 / fp64 reassociation), and so do the bias / BN
+    gradients from column partials when the kernel runs 64-row tiles (small batches)."""
     from snd_vae_amd import _lib
     from snd_vae_amd.params import init_blocks
     cfg = tscale(n, d)
@@ -499,8 +500,13 @@ def test_fused_backward_head_matches_chain(n, d, B):
     for k in ("cost", "adj_cost", "kl", "acc"):
         assert l1[k] == pytest.approx(l0[k], rel=1e-9 if k == "kl" else 1e-12, abs=1e-15), k
     g0, g1 = o0.grad_blocks(), o1.grad_blocks()
+    # below 128 tiles of 128 rows the fused kernel runs 64-row tiles (head_bwd_rows): the
+    # column partials behind the bias / BN gradients then group rows differently too
+    tiled = {"enc.bms"}
+    if B * ((n + 127) // 128) < 128:
+        tiled |= {"enc.bh", "enc.bn1.gamma", "enc.bn1.beta", "enc.bne.gamma", "enc.bne.beta"}
     for k in g0:
-        if k == "enc.bms":
+        if k in tiled:
             np.testing.assert_allclose(g1[k], g0[k], rtol=1e-4, atol=1e-6 * max(1.0, np.abs(g0[k]).max()), err_msg=k)
         else:
             assert np.array_equal(g0[k], g1[k]), k
