@@ -791,7 +791,8 @@ __global__ void __launch_bounds__(DT) dec_bwd_kernel(DecChainBwdArgs a) {
 }  // namespace
 
 int dec_rows(int ngraphs, int npg) {
-  return ngraphs * ((npg + kDecRows - 1) / kDecRows) < kDecSmall ? kDecRowsSmall : kDecRows;
+  if (ngraphs * ((npg + kDecRows - 1) / kDecRows) >= kDecSmall) return kDecRows;
+  return ngraphs * ((npg + kDecRowsSmall - 1) / kDecRowsSmall) < kDecTiny ? kDecRowsTiny : kDecRowsSmall;
 }
 int dec_tiles(int ngraphs, int npg) {
   const int tr = dec_rows(ngraphs, npg);
@@ -823,7 +824,9 @@ static int dec_init_attributes_once() {
   const void* ks[] = {reinterpret_cast<const void*>(dec_fwd_kernel<kDecRows>),
                       reinterpret_cast<const void*>(dec_bwd_kernel<kDecRows>),
                       reinterpret_cast<const void*>(dec_fwd_kernel<kDecRowsSmall>),
-                      reinterpret_cast<const void*>(dec_bwd_kernel<kDecRowsSmall>)};
+                      reinterpret_cast<const void*>(dec_bwd_kernel<kDecRowsSmall>),
+                      reinterpret_cast<const void*>(dec_fwd_kernel<kDecRowsTiny>),
+                      reinterpret_cast<const void*>(dec_bwd_kernel<kDecRowsTiny>)};
   for (const void* k : ks)
     if (hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, kDynLds) != hipSuccess) {
       set_error("dec: hipFuncSetAttribute failed");
@@ -848,7 +851,9 @@ int launch_dec_chain_fwd(const DecChainFwdArgs& a, hipStream_t s) {
   SND_TRY(dec_init_attributes());
   const int tr = dec_rows(a.ngraphs, a.npg);
   const size_t lds = FwdLay(a, tr).total;
-  if (tr == kDecRowsSmall)
+  if (tr == kDecRowsTiny)
+    hipLaunchKernelGGL(dec_fwd_kernel<kDecRowsTiny>, dim3(dec_tiles(a.ngraphs, a.npg)), dim3(DT), lds, s, a);
+  else if (tr == kDecRowsSmall)
     hipLaunchKernelGGL(dec_fwd_kernel<kDecRowsSmall>, dim3(dec_tiles(a.ngraphs, a.npg)), dim3(DT), lds, s, a);
   else
     hipLaunchKernelGGL(dec_fwd_kernel<kDecRows>, dim3(dec_tiles(a.ngraphs, a.npg)), dim3(DT), lds, s, a);
@@ -865,7 +870,9 @@ int launch_dec_chain_bwd(const DecChainBwdArgs& a, hipStream_t s) {
   SND_TRY(dec_init_attributes());
   const int tr = dec_rows(a.ngraphs, a.npg);
   const size_t lds = BwdLay(a, tr).total;
-  if (tr == kDecRowsSmall)
+  if (tr == kDecRowsTiny)
+    hipLaunchKernelGGL(dec_bwd_kernel<kDecRowsTiny>, dim3(dec_tiles(a.ngraphs, a.npg)), dim3(DT), lds, s, a);
+  else if (tr == kDecRowsSmall)
     hipLaunchKernelGGL(dec_bwd_kernel<kDecRowsSmall>, dim3(dec_tiles(a.ngraphs, a.npg)), dim3(DT), lds, s, a);
   else
     hipLaunchKernelGGL(dec_bwd_kernel<kDecRows>, dim3(dec_tiles(a.ngraphs, a.npg)), dim3(DT), lds, s, a);

@@ -13,6 +13,12 @@ constexpr int kDecRowsSmall = 64;
 #define SND_DEC_SMALL 128
 #endif
 constexpr int kDecSmall = SND_DEC_SMALL;
+// 32-row tiles when even 64-row tiles stay under kDecTiny (0: never)
+constexpr int kDecRowsTiny = 32;
+#ifndef SND_DEC_TINY
+#define SND_DEC_TINY 0
+#endif
+constexpr int kDecTiny = SND_DEC_TINY;
 
 // Packed weight image in the workspace (pack_kernel layout [tap][n][k], T = 5)
 struct DecImg { const __bf16* w; int kp, np; };
