@@ -68,6 +68,11 @@ constexpr int kHeadBwdRows = 128;
 #define SND_HB_SMALL 128
 #endif
 constexpr int kHeadBwdSmall = SND_HB_SMALL;
+// 32-row tiles when even 64-row tiles stay under kHeadBwdTiny (0: never)
+#ifndef SND_HB_TINY
+#define SND_HB_TINY 0
+#endif
+constexpr int kHeadBwdTiny = SND_HB_TINY;
 int head_bwd_rows(int R);
 int head_tiles(int R);   // backward-head tiles (head_bwd_rows(R) rows each)
 int launch_head_bwd(const HeadBwdArgs& a, hipStream_t s);
