@@ -649,8 +649,9 @@ template <int NQ, int NB1, int NB2>
 int head_bwd_launch(const HeadBwdArgs& a, hipStream_t s) {
   const int hr = head_bwd_rows(a.R);
   const size_t lds = (size_t)BwdLay(a.kp1, a.np1, a.kp2, a.np2, a.L, hr).total;
-  if (hr == 32)
-    hipLaunchKernelGGL((head_bwd_kernel<32, NQ, NB1, NB2>), dim3(head_tiles(a.R)), dim3(32 * 8), lds, s, a);
+  if (hr == kHeadBwdTinyRows)
+    hipLaunchKernelGGL((head_bwd_kernel<kHeadBwdTinyRows, NQ, NB1, NB2>), dim3(head_tiles(a.R)),
+                       dim3(kHeadBwdTinyRows * 8), lds, s, a);
   else if (hr == 64)
     hipLaunchKernelGGL((head_bwd_kernel<64, NQ, NB1, NB2>), dim3(head_tiles(a.R)), dim3(64 * 8), lds, s, a);
   else
@@ -858,7 +859,7 @@ int launch_front(FrontArgs& a, const PackDesc* pack, int npack, hipStream_t s) {
 
 int head_bwd_rows(int R) {
   if (cdiv(R, kHeadBwdRows) >= kHeadBwdSmall) return kHeadBwdRows;
-  return cdiv(R, 64) < kHeadBwdTiny ? 32 : 64;
+  return cdiv(R, 64) < kHeadBwdTiny ? kHeadBwdTinyRows : 64;
 }
 int head_tiles(int R) { return cdiv(R, head_bwd_rows(R)); }
 
@@ -937,14 +938,14 @@ static int head_init_attributes_once() {
                       reinterpret_cast<const void*>(head_bwd_kernel<64, 1, 2, 2>),
                       reinterpret_cast<const void*>(head_bwd_kernel<64, 1, 2, 3>),
                       reinterpret_cast<const void*>(head_bwd_kernel<64, 1, 2, 4>),
-                      reinterpret_cast<const void*>(head_bwd_kernel<32, 1, 1, 1>),
-                      reinterpret_cast<const void*>(head_bwd_kernel<32, 1, 1, 2>),
-                      reinterpret_cast<const void*>(head_bwd_kernel<32, 1, 1, 3>),
-                      reinterpret_cast<const void*>(head_bwd_kernel<32, 1, 1, 4>),
-                      reinterpret_cast<const void*>(head_bwd_kernel<32, 1, 2, 1>),
-                      reinterpret_cast<const void*>(head_bwd_kernel<32, 1, 2, 2>),
-                      reinterpret_cast<const void*>(head_bwd_kernel<32, 1, 2, 3>),
-                      reinterpret_cast<const void*>(head_bwd_kernel<32, 1, 2, 4>)};
+                      reinterpret_cast<const void*>(head_bwd_kernel<kHeadBwdTinyRows, 1, 1, 1>),
+                      reinterpret_cast<const void*>(head_bwd_kernel<kHeadBwdTinyRows, 1, 1, 2>),
+                      reinterpret_cast<const void*>(head_bwd_kernel<kHeadBwdTinyRows, 1, 1, 3>),
+                      reinterpret_cast<const void*>(head_bwd_kernel<kHeadBwdTinyRows, 1, 1, 4>),
+                      reinterpret_cast<const void*>(head_bwd_kernel<kHeadBwdTinyRows, 1, 2, 1>),
+                      reinterpret_cast<const void*>(head_bwd_kernel<kHeadBwdTinyRows, 1, 2, 2>),
+                      reinterpret_cast<const void*>(head_bwd_kernel<kHeadBwdTinyRows, 1, 2, 3>),
+                      reinterpret_cast<const void*>(head_bwd_kernel<kHeadBwdTinyRows, 1, 2, 4>)};
   const void* kf[] = {reinterpret_cast<const void*>(enc_front_kernel<1>),
                       reinterpret_cast<const void*>(enc_front_kernel<2>),
                       reinterpret_cast<const void*>(enc_front_kernel<3>),

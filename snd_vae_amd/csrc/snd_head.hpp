@@ -68,10 +68,14 @@ constexpr int kHeadBwdRows = 128;
 #define SND_HB_SMALL 128
 #endif
 constexpr int kHeadBwdSmall = SND_HB_SMALL;
-// 32-row tiles when even 64-row tiles stay under kHeadBwdTiny (0: never)
+// 32-row tiles when even 64-row tiles stay under kHeadBwdTiny (one N = 4096 graph)
 #ifndef SND_HB_TINY
-#define SND_HB_TINY 0
+#define SND_HB_TINY 128
 #endif
+#ifndef SND_HB_TINY_ROWS
+#define SND_HB_TINY_ROWS 32
+#endif
+constexpr int kHeadBwdTinyRows = SND_HB_TINY_ROWS;
 constexpr int kHeadBwdTiny = SND_HB_TINY;
 int head_bwd_rows(int R);
 int head_tiles(int R);   // backward-head tiles (head_bwd_rows(R) rows each)
