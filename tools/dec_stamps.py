@@ -39,7 +39,10 @@ def main():
     torch.cuda.synchronize()
     bc = db.c_struct()
     L = _lib.lib()
-    nb = args.graphs * 4096 // 128
+    # tile rows as snd_dec.hip dec_rows (default knobs): 128, 64 under 128 tiles, 32 under 128 of 64
+    t128 = args.graphs * 4096 // 128
+    rows = 128 if t128 >= 128 else (32 if 2 * t128 < 128 else 64)
+    nb = args.graphs * 4096 // rows
     for key, fl in [(k, int(f, 0)) for k in args.keys.split(",") for f in args.flags.split(",")]:
         buf, stride, names = KERNELS[key]
         _lib.check(L.snd_debug_set((1 << 21) | fl))

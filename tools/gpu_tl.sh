@@ -11,6 +11,7 @@ if [ -n "$TESTS" ]; then
 fi
 for c in "c2b8:--graphs 8" "c2b4:--graphs 4" "c2b1:--graphs 1" "c5:--config C5 --graphs 1"; do
   n=${c%%:*}; a=${c#*:}
+  [ -n "$ONLY" ] && [ "$ONLY" != "$n" ] && continue
   run 200 rocprofv3 --kernel-trace --stats -d gpurun_out/st/$n -o run --output-format csv -- python tools/prof_step.py --steps 4 $a > gpurun_out/st/$n.log 2>&1 || exit $?
   python tools/step_timeline.py gpurun_out/st/$n/run_kernel_trace.csv > gpurun_out/st/$n.timeline.txt
   echo "== $n"; cat gpurun_out/st/$n.timeline.txt
