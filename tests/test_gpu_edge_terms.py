@@ -52,9 +52,10 @@ def test_edge_terms_vs_float64(pos_weight, debug):
     torch.cuda.synchronize()
     R, L = B * n, cfg.latent
     z = model.buffer("ZB", torch.bfloat16)[:R * L].view(R, L).double().cpu().numpy()
-    tiles = (R + 127) // 128
-    if tiles < 128:   # head_bwd_rows (snd_head.hip): 64-row tiles below 128 tiles of 128 rows
-        tiles = (R + 63) // 64
+    # backward-head tile rows as head_bwd_rows (snd_head.hip): 128; 64 below 128 tiles of
+    # 128 rows; 32 below 128 tiles of 64 rows
+    rows = 128 if (R + 127) // 128 >= 128 else (32 if (R + 63) // 64 < 128 else 64)
+    tiles = (R + rows - 1) // rows
     pe = model.buffer("PEDGE", torch.float64).cpu().numpy()
     got_loss = float(pe[0:2 * tiles:2].sum()) if debug == 0 else float(pe[0::2].sum())
     got_tp = float(pe[1:2 * tiles:2].sum()) if debug == 0 else float(pe[1::2].sum())
