@@ -193,9 +193,15 @@ __device__ __forceinline__ void conv_phase_t(const __bf16* xs, int kpx, const __
   int wb[NBH];
 #pragma unroll
   for (int i = 0; i < NBH; ++i) wb[i] = 16 * min(nb0 + i, nbc - 1) * kpw;
+  // the epilogue operands of a wave's NEXT row block are loaded before this block's MFMAs
+  // (round 5: one HBM round trip per row-block pass was exposed in the backward phases)
+  f32x4 ypn[NBH];
+  if (k0 < nrb) pre(16 * k0 + li, nb0, ypn);
   for (int rb = k0; rb < nrb; rb += wpc) {
     f32x4 yp[NBH];
-    pre(16 * rb + li, nb0, yp);
+#pragma unroll
+    for (int i = 0; i < NBH; ++i) yp[i] = ypn[i];
+    if (rb + wpc < nrb) pre(16 * (rb + wpc) + li, nb0, ypn);
     f32x4 acc[NBH];
 #pragma unroll
     for (int i = 0; i < NBH; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
