@@ -194,12 +194,15 @@ extern "C" int snd_abi_version(void) { return 17; }
 // tiles do not take (one 1024-thread workgroup per CU for either kernel).  A step uses
 // this count only when its decoder actually runs on the side stream (cdec); a serial
 // step -- a capture before any eager step, or no side stream -- keeps the full count.
+#ifndef SND_CONC_TS_EXTRA
+#define SND_CONC_TS_EXTRA 0   // A/B builds: zz^T splits beyond the CUs the decoder leaves free
+#endif
 static void set_zzt_splits(snd_plan& p) {
   p.zzt_ts = zzt_tsplit(p.B, p.N, p.c.dtype);
   p.zzt_ts_conc = p.zzt_ts;
   if (p.conc_dec_on()) {
     const int wgs = p.B * (zzt_npad(p.N) / 128);
-    p.zzt_ts_conc = std::max(1, std::min(p.zzt_ts, (device_cu_count() - p.dtiles) / wgs));
+    p.zzt_ts_conc = std::max(1, std::min(p.zzt_ts, (device_cu_count() - p.dtiles) / wgs + SND_CONC_TS_EXTRA));
   }
 }
 
