@@ -37,6 +37,8 @@ enum {
 enum { SND_F32 = 0, SND_BF16 = 1 }; /* MFMA operand dtype; accumulation always fp32 */
 
 const char* snd_last_error(void);
+/* the ABI this header describes; snd_abi_version() returns it */
+#define SND_ABI_VERSION 17
 int snd_abi_version(void);
 
 /* ---- a1: adjacency ingest ------------------------------------------------

@@ -637,6 +637,7 @@ struct WgMultiPack {
   WgArgs a[kMaxWgMulti];
   int start[kMaxWgMulti + 1];
   int nseg;
+  int stamp_base;   // measurement only: workgroups of the earlier launches of the same call
 };
 static_assert(sizeof(WgMultiPack) <= 4096, "wgrad_multi: kernel arguments over 4 KB");
 
@@ -680,7 +681,7 @@ wgrad_multi_kernel(WgMultiPack m) {
   if (stamp) {
     __syncthreads();
     if (threadIdx.x == 0) {
-      unsigned* o = m.a[0].stamps + (long long)bid * kWgStampWords;
+      unsigned* o = m.a[0].stamps + ((long long)m.stamp_base + bid) * kWgStampWords;
       for (int i = 0; i < 9; ++i) o[i] = tsl[i];
       o[9] = (unsigned)__builtin_amdgcn_s_memrealtime();
       o[10] = __builtin_amdgcn_s_getreg((31 << 11) | 4);    // HW_REG_HW_ID
@@ -1012,8 +1013,9 @@ int launch_wgrad_multi(const WgArgs* a, int n, hipStream_t s) {
   if (n <= 0) return 0;
   WgMultiPack pk{};
   size_t lds = 0;
-  int total = 0;
+  int total = 0, base = 0;
   pk.nseg = 0;
+  const bool stamps = a[0].stamps != nullptr;
   for (int i = 0; i < n; ++i) {
     const WgArgs x0 = wg_norm(a[i]);
     if (x0.R <= 0) continue;
@@ -1032,7 +1034,9 @@ int launch_wgrad_multi(const WgArgs* a, int n, hipStream_t s) {
     for (int j = 0; j < nw; ++j) {
       if (pk.nseg == kMaxWgMulti) {   // pack full: launch it, start the next
         SND_TRY(wg_multi_flush(pk, total, lds, s));
+        base += total;
         pk = WgMultiPack{};
+        pk.stamp_base = base;
         lds = 0;
         total = 0;
       }
@@ -1043,6 +1047,9 @@ int launch_wgrad_multi(const WgArgs* a, int n, hipStream_t s) {
       total += cdiv(x.R, x.rows_per_wg) * cdiv(P, x.pairs_per_wg);
       lds = std::max(lds, wg_lds_bytes(x.T, x.K, x.N));
       ++pk.nseg;
+      SND_CHECK_ARG(!stamps || ((long long)base + total) * kWgStampWords <= a[0].stamp_words,
+                    "wgrad_multi: %d workgroups' stamps exceed the %lld-word buffer", base + total,
+                    a[0].stamp_words);
     }
   }
   return wg_multi_flush(pk, total, lds, s);

@@ -114,6 +114,7 @@ struct WgArgs {
   // (wk0, wn0); 0 = the descriptor's own K / n4(N) at origin 0
   int sK, sn4, wk0, wn0;
   unsigned* stamps;             // measurement only (debug bit 1 << 21): 12 words per workgroup
+  long long stamp_words;        // capacity of stamps in words (checked by launch_wgrad_multi)
 };
 struct WgGeom { int rows_per_wg, pairs_per_wg, gx, gy; };
 // chunks > 0: that many row chunks per weight (the step's multi-segment launch);

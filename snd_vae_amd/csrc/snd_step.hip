@@ -177,6 +177,10 @@ struct snd_plan {
     for (auto& b : bufs) if (b.name == n) return b.off;
     return -1;
   }
+  long long buf_numel(const char* n) const {
+    for (auto& b : bufs) if (b.name == n) return b.numel;
+    return 0;
+  }
   void add_block(const char* n, long long numel) {
     blocks.push_back({n, pcount, numel});
     pcount += round_up(numel, 64);
@@ -188,7 +192,7 @@ struct snd_plan {
 };
 
 extern "C" const char* snd_last_error(void) { return g_err; }
-extern "C" int snd_abi_version(void) { return 17; }
+extern "C" int snd_abi_version(void) { return SND_ABI_VERSION; }
 
 // zz^T column splits with the concurrent decoder on: zz^T keeps the CUs the decoder's
 // tiles do not take (one 1024-thread workgroup per CU for either kernel).  A step uses
@@ -1542,8 +1546,11 @@ extern "C" int snd_plan_launch(const snd_plan_t* plan, const snd_batch_t* batch,
     for (auto& w : q) {
       w.dbg = debug_flags();
       // measurement only: per-workgroup stamps into the fused decoder's head partials
-      // (unused by this launch; 12 words x the launch's workgroups must fit)
-      w.stamps = (w.dbg & (1 << 21)) && p.dec_fused ? reinterpret_cast<unsigned*>(ws + p.buf("PDHS")) : nullptr;
+      // (unused by this launch; launch_wgrad_multi checks that 12 words x the workgroups
+      // of all its launches fit the buffer)
+      const bool st = (w.dbg & (1 << 21)) && p.dec_fused;
+      w.stamps = st ? reinterpret_cast<unsigned*>(ws + p.buf("PDHS")) : nullptr;
+      w.stamp_words = st ? p.buf_numel("PDHS") : 0;
     }
     return launch_wgrad_multi(q.data(), (int)q.size(), s);
   }

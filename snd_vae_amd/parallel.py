@@ -191,6 +191,23 @@ def allgather_rows(x_local: torch.Tensor, ranges, group) -> torch.Tensor:
     return torch.cat([parts[r][:r1 - r0] for r, (r0, r1) in enumerate(ranges)])
 
 
+def reducescatter_rows(x_full: torch.Tensor, ranges, group) -> torch.Tensor:
+    """Sum over ranks of x_full [n, ...], returned as THIS rank's rows of its contiguous
+    range: one reduce-scatter over the ranges padded to the largest (allgather_rows'
+    layout), so each rank receives only its own rows instead of all n."""
+    import torch.distributed as dist
+    world = len(ranges)
+    rmax = max(r1 - r0 for r0, r1 in ranges)
+    tail = tuple(x_full.shape[1:])
+    inp = torch.zeros((world * rmax,) + tail, dtype=x_full.dtype, device=x_full.device)
+    for r, (r0, r1) in enumerate(ranges):
+        inp[r * rmax:r * rmax + (r1 - r0)] = x_full[r0:r1]
+    out = torch.empty((rmax,) + tail, dtype=x_full.dtype, device=x_full.device)
+    dist.reduce_scatter_tensor(out, inp, group=group)
+    r0, r1 = ranges[dist.get_rank(group)]
+    return out[:r1 - r0].contiguous()
+
+
 def halo_rows(x_local: torch.Tensor, ranges, rank: int, halo: int, group) -> torch.Tensor:
     """Rows [row0 - halo, row1 + halo) clipped to [0, n) of a contiguously row-sharded
     matrix, on this rank: its own rows plus `halo` boundary rows from each side

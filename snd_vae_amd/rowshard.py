@@ -64,6 +64,9 @@ class RowShardPlan:
         self.n, self.rank, self.world = n, rank, world
         self.ranges = row_ranges(n, world, block)
         self.r0, self.r1 = self.ranges[rank]
+        if any(b <= a for a, b in self.ranges):
+            raise ValueError(f"row sharding: {world} ranks over {n} rows in {block}-row blocks leaves "
+                             f"a rank without rows ({self.ranges}); use at most {-(-n // block)} ranks")
         rowptr = np.asarray(rowptr, np.int64)
         colidx = np.asarray(colidx, np.int64)
         A = sp.csr_matrix((np.ones(len(colidx)), colidx, rowptr), shape=(n, n))
@@ -199,8 +202,16 @@ class TorchComm:
         import torch.distributed as dist
         self.dist, self.group, self.staged = dist, group, staged
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
-        # where host-side scalars go for the collective (RCCL takes device tensors only)
-        self.scalar_device = device if (device is not None and not staged) else torch.device("cpu")
+        # where host-side scalars go for the collective: RCCL takes device tensors only,
+        # so a non-staged RCCL group without an explicit device uses the current GPU
+        if staged:
+            self.scalar_device = torch.device("cpu")
+        elif device is not None:
+            self.scalar_device = torch.device(device)
+        elif dist.is_initialized() and dist.get_backend(group) in ("nccl", "rccl"):
+            self.scalar_device = torch.device("cuda", torch.cuda.current_device())
+        else:
+            self.scalar_device = torch.device("cpu")
 
     def _io(self, t):
         return t.cpu() if self.staged else t
@@ -215,13 +226,11 @@ class TorchComm:
         return self._back(allgather_rows(self._io(x_own).contiguous(), ranges, self.group), x_own)
 
     def reduce_scatter_rows(self, x_full, ranges):
-        """Sum over ranks of x_full [N, ...], this rank's rows."""
+        """Sum over ranks of x_full [N, ...], this rank's rows (one reduce-scatter)."""
         if self.world == 1:
             return x_full
-        t = self._io(x_full).contiguous()
-        self.dist.all_reduce(t, group=self.group)
-        r0, r1 = ranges[self.dist.get_rank(self.group)]
-        return self._back(t[r0:r1].contiguous(), x_full)
+        from .parallel import reducescatter_rows
+        return self._back(reducescatter_rows(self._io(x_full).contiguous(), ranges, self.group), x_full)
 
     def all_reduce_host(self, t):
         if self.world > 1:

@@ -108,6 +108,23 @@ def test_library_exports_every_header_symbol(lib_built):
     assert set(_lib.EXPORTS) == set(names)
 
 
+def test_abi_version_agrees_everywhere(lib_built):
+    """One ABI number: the header's SND_ABI_VERSION, the library's snd_abi_version(), the
+    Python binding's ABI_VERSION and the ctypes stub a maintainer copies from
+    INTEGRATION.md (round 5 shipped a stub asserting 14 against a library at 17)."""
+    from snd_vae_amd import _lib
+    hdr = open(os.path.join(ROOT, "include", "snd_vae.h")).read()
+    m = re.search(r"#define\s+SND_ABI_VERSION\s+(\d+)", hdr)
+    assert m, "include/snd_vae.h must define SND_ABI_VERSION"
+    so = ctypes.CDLL(lib_built)
+    so.snd_abi_version.restype = ctypes.c_int
+    doc = open(os.path.join(ROOT, "INTEGRATION.md")).read()
+    stub = [int(v) for v in re.findall(r"^SND_ABI_VERSION\s*=\s*(\d+)", doc, flags=re.M)]
+    assert "assert lib.snd_abi_version() == SND_ABI_VERSION" in doc
+    assert stub == [int(m.group(1))], stub
+    assert so.snd_abi_version() == int(m.group(1)) == _lib.ABI_VERSION
+
+
 def test_plan_layout_matches_python(lib_built):
     """snd_plan_create needs no GPU: check its flat layout against params.py."""
     from snd_vae_amd import _lib

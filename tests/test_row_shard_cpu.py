@@ -60,7 +60,8 @@ def _oracle_rows(z_full, r0, r1, rowptr, colidx, A=None):
 def _worker(rank, world, port, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
-    from snd_vae_amd.parallel import halo_rows, init_from_env, row_ranges, row_sharded_adj_ce
+    from snd_vae_amd.parallel import (halo_rows, init_from_env, reducescatter_rows, row_ranges,
+                                      row_sharded_adj_ce)
     info = init_from_env("gloo")
     A, beta, z, h = _case()
     ranges = row_ranges(N, world)
@@ -71,7 +72,9 @@ def _worker(rank, world, port, q):
                                    compute=_oracle_rows, A=A)
     xh, lo = halo_rows(torch.from_numpy(h[r0:r1]), ranges, rank, beta, info.group)
     spmm_loc = A_loc[:, lo:lo + xh.shape[0]] @ xh.numpy()        # this rank's rows of A @ H
-    q.put((rank, stats.numpy(), dz.numpy(), lo, xh.numpy(), spmm_loc))
+    # reduce-scatter of per-rank [N, w] contributions (rank r adds (r + 1) * h): own rows
+    rs = reducescatter_rows(torch.from_numpy(h * (rank + 1.0)), ranges, info.group)
+    q.put((rank, stats.numpy(), dz.numpy(), lo, xh.numpy(), spmm_loc, rs.numpy()))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -96,7 +99,7 @@ def test_row_sharded_ce_and_halo_equal_whole_graph(world):
     A, beta, z, h = _case()
     ce, dJ, correct = R.adj_ce(z, [A], N, row_chunk=128)
     for r in range(world):
-        stats, dz, lo, xh, spmm_loc = got[r]
+        stats, dz, lo, xh, spmm_loc, rs = got[r]
         r0, r1 = ranges[r]
         # all-reduced loss terms = the whole graph's; dz rows = its rows of the full dz
         assert stats[0] == pytest.approx(ce, rel=1e-12)
@@ -106,3 +109,30 @@ def test_row_sharded_ce_and_halo_equal_whole_graph(world):
         assert lo == max(0, r0 - beta)
         assert np.array_equal(xh, h[lo:min(N, r1 + beta)])
         assert np.allclose(spmm_loc, (A @ h)[r0:r1], rtol=1e-12, atol=1e-12)
+        assert rs.shape == (r1 - r0, h.shape[1])
+        assert np.allclose(rs, h[r0:r1] * (world * (world + 1) / 2), rtol=1e-12, atol=0)
+
+
+def test_row_shard_plan_rejects_empty_ranks():
+    """More ranks than 128-row blocks would leave a rank without rows: a clear error at
+    plan time, not an argument error deep inside snd_zzt_ce_rows."""
+    from snd_vae_amd.rowshard import RowShardPlan
+    A, _, _, _ = _case()
+    with pytest.raises(ValueError, match="without rows"):
+        RowShardPlan(A.indptr, A.indices, N, 0, -(-N // 128) + 1, "cpu")
+
+
+def test_torchcomm_rccl_scalars_go_to_the_device(monkeypatch):
+    """A non-staged RCCL group without an explicit device sends the loss-stats all-reduce
+    from the current GPU (RCCL rejects CPU tensors); gloo keeps host tensors."""
+    import torch.distributed as tdist
+    from snd_vae_amd.rowshard import TorchComm
+    monkeypatch.setattr(tdist, "is_initialized", lambda: True)
+    monkeypatch.setattr(tdist, "get_world_size", lambda group=None: 2)
+    monkeypatch.setattr(torch.cuda, "current_device", lambda: 3)
+    monkeypatch.setattr(tdist, "get_backend", lambda group=None: "nccl")
+    assert TorchComm().scalar_device == torch.device("cuda", 3)
+    assert TorchComm(staged=True).scalar_device == torch.device("cpu")
+    assert TorchComm(device="cuda:1").scalar_device == torch.device("cuda", 1)
+    monkeypatch.setattr(tdist, "get_backend", lambda group=None: "gloo")
+    assert TorchComm().scalar_device == torch.device("cpu")
