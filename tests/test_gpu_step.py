@@ -41,6 +41,30 @@ def block_err(g, ref):
     return np.abs(g - ref).max() / max(np.abs(ref).max(), 1e-30)
 
 
+def check_terms_grads(case, dtype, got, ref, g, rg, ltol, gtol):
+    """Loss terms and gradient blocks: fp32 at the fixed bars, bf16 at the measured ones
+    (tests/parity_bars.json; ltol / gtol are the fallbacks)."""
+    import parity_bars as PB
+    bars = PB.Bars(case, dtype=dtype)
+    for k in ("cost", "spatial_cost", "adj_cost", "node_cost", "kl"):
+        e = abs(got[k] - ref[k]) / max(abs(ref[k]), 1e-30)
+        if dtype == "f32":
+            bars.rec.setdefault("loss", {})[k] = e
+            assert e <= ltol, (k, got[k], ref[k])
+        else:
+            bars.check("loss", k, e, ltol)
+    for k in rg:
+        e = float(block_err(g[k], rg[k]))
+        if dtype == "f32":
+            bars.rec.setdefault("grad", {})[k] = e
+            if e > gtol:
+                bars.fails.append(("grad", k, e))
+        else:
+            bars.check("grad", k, e, gtol)
+    bars.flush()
+    assert not bars.fails, bars.fails
+
+
 @pytest.mark.parametrize("name", golden_io.NAMES)
 def test_train_steps_f32_vs_golden(name):
     z, cfg, batch, p0 = load_fixture(name)
@@ -65,24 +89,31 @@ def test_train_steps_f32_vs_golden(name):
 
 @pytest.mark.parametrize("name", ["tscale_n200_d16", "tref_c1_n200_d16"])
 def test_train_step_bf16_vs_golden(name):
+    import parity_bars as PB
     z, cfg, batch, p0 = load_fixture(name)
     model, opt, db = make(cfg, batch, p0, "bf16")
     opt.step(db, torch.from_numpy(z["eps"][0]).cuda())
     got = opt.loss_dict()
-    for k in ("cost", "adj_cost", "kl"):
-        assert got[k] == pytest.approx(float(z[f"s0/loss/{k}"]), rel=2e-2), k
+    bars = PB.Bars(f"golden_{name}/bf16", dtype="bf16")
+    for k in ("cost", "spatial_cost", "adj_cost", "node_cost", "kl"):
+        ref = float(z[f"s0/loss/{k}"])
+        bars.check("loss", k, abs(got[k] - ref) / max(abs(ref), 1e-30), 2e-2)
     grads = opt.grad_blocks()
-    # bf16 operands (8-bit mantissa) in sums with cancellation: compare norm-wise.
-    # The decoder-conv gradients sit at 3-5 % on both the fast and the generic
-    # bf16 engines (tools/bf16_errors.py); encoder blocks at ~0.3 %.
+    # bf16 operands (8-bit mantissa) in sums with cancellation: compare norm-wise, each
+    # block against 2x its measured error (parity_bars.json); fallbacks: the decoder-conv
+    # gradients sit at 3-5 % on both the fast and the generic bf16 engines
+    # (tools/bf16_errors.py), encoder blocks at ~0.3 %
     for k, g in grads.items():
         if f"s0/grad/{k}" not in z.files:     # sampled big block: sampled max-abs check
             err, nerr = golden_io.block_error(z, "s0/grad", k, g)
-            assert err < 5e-2 and nerr < 2e-2, (k, err, nerr)
+            bars.check("grad", k, float(err), 5e-2)
+            bars.check("gradn", k, float(nerr), 2e-2)
             continue
         ref = z[f"s0/grad/{k}"]
         err = np.linalg.norm(g - ref) / max(np.linalg.norm(ref), 1e-30)
-        assert err < (1e-1 if k.startswith("dec.") else 2e-2), (k, err)
+        bars.check("gradn", k, float(err), 1e-1 if k.startswith("dec.") else 2e-2)
+    bars.flush()
+    assert not bars.fails, bars.fails
 
 
 @pytest.mark.parametrize("dtype,ltol,gtol", [("f32", 1e-5, 2e-4), ("bf16", 2e-2, 1e-1)])
@@ -99,12 +130,8 @@ def test_train_step_c2_size_vs_oracle(dtype, ltol, gtol):
     adj = [batch.dense_adj(b) for b in range(2)]
     ref, rg, _ = R.forward_backward(p0, adj, batch.features, batch.feature_truth,
                                     batch.spatial_truth, eps.astype(np.float64), cfg)
-    for k in ("cost", "spatial_cost", "adj_cost", "node_cost", "kl"):
-        assert got[k] == pytest.approx(ref[k], rel=ltol), (k, got[k], ref[k])
     assert abs(got["acc"] - ref["acc"]) < (1e-6 if dtype == "f32" else 1e-3)
-    g = opt.grad_blocks()
-    bad = {k: block_err(g[k], rg[k]) for k in rg if block_err(g[k], rg[k]) > gtol}
-    assert not bad, bad
+    check_terms_grads(f"c2_size_b2/{dtype}", dtype, got, ref, opt.grad_blocks(), rg, ltol, gtol)
 
 
 @pytest.mark.parametrize("dtype,ltol,gtol", [("f32", 1e-5, 2e-4), ("bf16", 2e-2, 1e-1)])
@@ -124,12 +151,8 @@ def test_train_step_c4_size_vs_oracle(dtype, ltol, gtol):
     adj = [batch.dense_adj(b) for b in range(2)]
     ref, rg, _ = R.forward_backward(p0, adj, batch.features, batch.feature_truth,
                                     batch.spatial_truth, eps.astype(np.float64), cfg)
-    for k in ("cost", "spatial_cost", "adj_cost", "node_cost", "kl"):
-        assert got[k] == pytest.approx(ref[k], rel=ltol), (k, got[k], ref[k])
     assert abs(got["acc"] - ref["acc"]) < (1e-6 if dtype == "f32" else 1e-3)
-    g = opt.grad_blocks()
-    bad = {k: block_err(g[k], rg[k]) for k in rg if block_err(g[k], rg[k]) > gtol}
-    assert not bad, bad
+    check_terms_grads(f"c4_size_b2/{dtype}", dtype, got, ref, opt.grad_blocks(), rg, ltol, gtol)
     # decoder input J and the graph latent read back under the reference names
     assert model.joint_h.shape == (2 * 4096, 64) and model.z_sg.shape == (2, cfg.latent)
     assert model.z_mean_sg.shape == (2, cfg.latent)
