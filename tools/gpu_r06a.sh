@@ -1,0 +1,17 @@
+#!/bin/bash
+# Round 6, session A: GPU tests with the measured bars (recording every bf16 error),
+# the broken-edge library against the C2 bench-batch test (must fail), the default bench.
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+rm -f gpurun_out/parity_errors.jsonl
+STAGES="tests" bash tools/gpu_session.sh || exit $?
+cp gpurun_out/parity_errors.jsonl gpurun_out/parity_errors_main.jsonl
+echo "== broken-edge library (expected: FAIL)"
+SND_LIB_PATH=$PWD/ab/edge_broken.so timeout -k 10 400 python -u -m pytest tests/test_gpu_c2_bench.py \
+  -k bf16 -x -v --timeout 900 --timeout-method thread > gpurun_out/edge_broken_c2.log 2>&1
+rc=$?
+echo "== broken exit $rc"; tail -n 25 gpurun_out/edge_broken_c2.log | cut -c1-800
+case $rc in 124|134|137|139) exit $rc;; esac
+cp gpurun_out/parity_errors.jsonl gpurun_out/parity_errors_all.jsonl
+STAGES="smoke bench" bash tools/gpu_session.sh
