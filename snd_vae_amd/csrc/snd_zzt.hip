@@ -961,7 +961,7 @@ __global__ void __launch_bounds__(NTH2) zzt_dense_bf16_v7(ZztArgs a) {
           bwd(NN, sA);   // tile t-1's slot
         }
         Yp = fwd(CUR);
-      } else {
+      } else if (!(MEAS && (skip & 16) && (t & 1))) {
         const f32x16 Y = fwd(CUR);
         bf16x8 sA[2];
         epi(Y, sA);
@@ -1093,10 +1093,16 @@ __device__ __forceinline__ int zoa64(int row, int ch) {   // [128][64] bf16 imag
   return 1024 * (row >> 3) + 512 * (ch >> 2) + 64 * (row & 7) + 16 * ((ch & 3) ^ ((row >> 2) & 3));
 }
 
-template <bool STAG>
+// MEAS (variant >= 256, measurement build; results wrong): phase skips, variant >> 8 --
+//   1 no epilogue, 4 no backward MFMAs, 16 the symmetric-tile proxy: odd tiles only DMA
+//   and barrier, even tiles run their epilogue once and the backward MFMAs twice (what a
+//   J >= I tile kernel computes per logit block: forward 4 + epilogue + 2 x 4 backward
+//   MFMAs over half the blocks; DESIGN §5 "symmetric tiles, measured")
+template <bool STAG, bool MEAS>
 __global__ void __launch_bounds__(NTH9) __attribute__((amdgpu_waves_per_eu(4, 4)))
 zzt_dense_bf16_v9(ZztArgs a) {
   constexpr int DP = 64, NT = NTH9, NW = NT / 64;
+  const int skip = MEAS ? __builtin_amdgcn_readfirstlane(a.variant >> 8) : 0;
   constexpr int KS = DP / 16;          // forward k-steps
   constexpr int CB = DP / 32;          // backward 32-column output blocks
   constexpr int IMG = TJ2 * DP * 2;    // one [128][64] bf16 image, 16 KB
@@ -1195,6 +1201,11 @@ zzt_dense_bf16_v9(ZztArgs a) {
   unsigned lcnt = 0;
   bool ovf = false;   // sticky per wave, as v4
   auto epi = [&](const f32x16& Y, bf16x8 (&sA)[2]) {   // v4's epilogue, y = -x
+    if (MEAS && (skip & 1)) {
+#pragma unroll
+      for (int v = 0; v < 16; ++v) sA[v >> 3][v & 7] = (__bf16)Y[v];
+      return;
+    }
     float q[16], lt = 0.f;
 #pragma unroll
     for (int v = 0; v < 16; ++v) {
@@ -1224,12 +1235,15 @@ zzt_dense_bf16_v9(ZztArgs a) {
     lacc += lt;
   };
   auto bwd = [&](int b, const bf16x8 (&sA)[2]) {
+    if (MEAS && (skip & 4)) { lacc += (float)sA[0][0]; return; }
     const char* T = lds + b * IMG;
+#pragma unroll
+    for (int rep = 0; rep < ((MEAS && (skip & 16)) ? 2 : 1); ++rep)
 #pragma unroll
     for (int s = 0; s < 2; ++s)
 #pragma unroll
       for (int q = 0; q < CB; ++q) {
-        const bf16x8 bv = ztr_pair(T + tb0 + 2048 * s + 512 * q, T + tb1 + 2048 * s + 512 * q);
+        const bf16x8 bv = ztr_pair(T + tb0 + 2048 * s + 512 * q + 8 * rep, T + tb1 + 2048 * s + 512 * q + 8 * rep);
         acc[q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(sA[s], bv, acc[q], 0, 0, 0);
       }
   };
@@ -1272,7 +1286,7 @@ zzt_dense_bf16_v9(ZztArgs a) {
       lacc = 0.f;
     }
   };
-  if (STAG && (cb & 1)) {
+  if (STAG && !MEAS && (cb & 1)) {
     __builtin_amdgcn_s_setprio(1);
     run(std::true_type{});
     __builtin_amdgcn_s_setprio(0);
@@ -1482,10 +1496,11 @@ int launch_zzt_dense(const ZztArgs& a, int dtype, hipStream_t s, bool defer_spli
     if (dp == 32) hipLaunchKernelGGL((zzt_dense_bf16<32>), grid, dim3(NTH), 0, s, a);
     else if (dp == 64) hipLaunchKernelGGL((zzt_dense_bf16<64>), grid, dim3(NTH), 0, s, a);
     else hipLaunchKernelGGL((zzt_dense_bf16<128>), grid, dim3(NTH), 0, s, a);
-  } else if (dtype == SND_BF16 && dp == 64 && SND_ZZT_V9 && a.variant == 0) {   // v9 (A/B build)
+  } else if (dtype == SND_BF16 && dp == 64 && SND_ZZT_V9 && (a.variant == 0 || a.variant >= 256)) {   // v9
     const dim3 g9(grid.x * 2);
-    if (SND_ZZT_V9 == 2) hipLaunchKernelGGL((zzt_dense_bf16_v9<true>), g9, dim3(NTH9), 0, s, a);
-    else hipLaunchKernelGGL((zzt_dense_bf16_v9<false>), g9, dim3(NTH9), 0, s, a);
+    if (a.variant >= 256) hipLaunchKernelGGL((zzt_dense_bf16_v9<false, true>), g9, dim3(NTH9), 0, s, a);
+    else if (SND_ZZT_V9 == 2) hipLaunchKernelGGL((zzt_dense_bf16_v9<true, false>), g9, dim3(NTH9), 0, s, a);
+    else hipLaunchKernelGGL((zzt_dense_bf16_v9<false, false>), g9, dim3(NTH9), 0, s, a);
   } else if (dtype == SND_BF16 && dp <= 64) {         // v4 (default, d <= 64)
     // variant >= 256: the measurement build (phase skips / stamps, variant >> 8)
     if (a.variant >= 256) {

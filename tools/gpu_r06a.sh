@@ -15,3 +15,12 @@ echo "== broken exit $rc"; tail -n 25 gpurun_out/edge_broken_c2.log | cut -c1-80
 case $rc in 124|134|137|139) exit $rc;; esac
 cp gpurun_out/parity_errors.jsonl gpurun_out/parity_errors_all.jsonl
 STAGES="smoke bench" bash tools/gpu_session.sh
+# A/B: the library built without SLP vectorisation (no v_pk_*_f32 in the epilogues)
+# against HEAD, alternating processes, step + chain kernels
+rm -f gpurun_out/ab.jsonl
+bash tools/ab.sh "--kernels zzt_dense,head_fwd,head_bwd,dec:fwd,dec:bwd,wgrad_multi" ab/base.so ab/noslp.so 3
+# zz^T symmetric-tile evidence: the v9 phase-skip proxy and the slab microbenchmark
+timeout -k 10 300 python -u tools/ab_zzt.py --rounds 3 --reps 20 \
+  --variants zzt_dense,zzt_dense_v256,zzt_dense_v1024,zzt_dense_v4096 > gpurun_out/zzt_sym_proxy.txt 2>&1
+echo "== zzt proxy exit $?"; tail -12 gpurun_out/zzt_sym_proxy.txt
+timeout -k 10 120 tools/micro/slab_cost > gpurun_out/slab_cost.json 2>&1; echo "== slab exit $?"; cat gpurun_out/slab_cost.json
