@@ -176,6 +176,35 @@ def test_spmm_bf16_window_bitwise(n, B, kbar, seed):
         assert np.abs(out.float().cpu().numpy() - r64).max() <= 2 ** -7 * max(np.abs(r64).max(), 1.0)
 
 
+def test_gather_sums_nonfinite_column_pairing():
+    """Pins how a non-finite bf16 value spreads in the dot2 gather sums: every
+    gather kernel adds the low / high bf16 of a 32-bit word through v_dot2_f32_bf16 with
+    (1, 0) / (0, 1), so the other half of the word is multiplied by 0 -- an inf in column
+    2c turns column 2c + 1 of every neighbouring output row into NaN (inf * 0), and the
+    other columns stay finite.  Finite inputs are unaffected (bitwise the widening adds)."""
+    from snd_vae_amd import layers
+    from snd_vae_amd.data import GraphBatch, locality_order, window_plan
+    n, B = 512, 1
+    rp, ci, _ = rand_batch(n, B, 8, 5)
+    gb = GraphBatch(B, n, rp, ci, np.zeros((n, 1), np.float32), np.zeros((n, 1), np.float32),
+                    np.zeros((n, 2), np.float32))
+    order = locality_order(gb)
+    h = np.random.default_rng(1).standard_normal((n, 64)).astype(np.float32)
+    bad = int(np.argmax(np.diff(rp)))              # a row with neighbours
+    h[bad, 6] = np.inf                             # word 3 = (column 6, column 7)
+    hb = torch.from_numpy(h).to(torch.bfloat16)
+    d_rp, d_ci = cu(rp, torch.int32), cu(ci, torch.int32)
+    outs = [layers.spmm_bf16(d_rp, d_ci, hb.cuda(), n, B, cu(order, torch.int32)),
+            layers.spmm_bf16_window(layers.DeviceWindowPlan(window_plan(gb, order)), hb.cuda(), n, B)]
+    torch.cuda.synchronize()
+    touched = np.array([bad in ci[rp[r]:rp[r + 1]] for r in range(n)])
+    for o in outs:
+        o = o.float().cpu().numpy()
+        assert np.isinf(o[touched, 6]).all() and np.isnan(o[touched, 7]).all()
+        assert np.isfinite(np.delete(o[touched], [6, 7], axis=1)).all()
+        assert np.isfinite(o[~touched]).all()
+
+
 def test_spmm_bf16_window_rejects_wide_window():
     """Natural (generator) order puts neighbours ~N apart: the window plan's beta
     exceeds the ring and the launch refuses (the caller keeps the tiled kernel)."""
