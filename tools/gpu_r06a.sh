@@ -24,3 +24,10 @@ timeout -k 10 300 python -u tools/ab_zzt.py --rounds 3 --reps 20 \
   --variants zzt_dense,zzt_dense_v256,zzt_dense_v1024,zzt_dense_v4096 > gpurun_out/zzt_sym_proxy.txt 2>&1
 echo "== zzt proxy exit $?"; tail -12 gpurun_out/zzt_sym_proxy.txt
 timeout -k 10 120 tools/micro/slab_cost > gpurun_out/slab_cost.json 2>&1; echo "== slab exit $?"; cat gpurun_out/slab_cost.json
+# graph-replay kernel traces (the bench's own path, side streams as captured): B = 1 and 8
+for B in 1 8; do
+  timeout -k 10 200 rocprofv3 --kernel-trace -d gpurun_out/st/g$B -o run --output-format csv \
+    -- python tools/prof_step.py --graphs $B --steps 6 --graph > gpurun_out/st_g$B.log 2>&1
+  rc=$?; echo "== trace B=$B exit $rc"; case $rc in 124|134|137|139) exit $rc;; esac
+  python tools/step_timeline.py gpurun_out/st/g$B/run_kernel_trace.csv > gpurun_out/st/g$B.timeline.txt && cat gpurun_out/st/g$B.timeline.txt
+done

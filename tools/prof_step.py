@@ -1,4 +1,5 @@
-"""Run a few eager (non-graph) train steps for per-dispatch PMC profiling.
+"""Run a few eager (non-graph) train steps for per-dispatch PMC profiling, or (--graph)
+replays of the captured step for a kernel trace of the bench's own path.
 
     rocprofv3 --pmc SQ_WAVES ... -d gpurun_out/pmcX -o run --output-format csv -- \
         python tools/prof_step.py --steps 3
@@ -18,6 +19,9 @@ def main():
     ap.add_argument("--latent", type=int, default=64)
     ap.add_argument("--dtype", default="bf16")
     ap.add_argument("--config", default="", help="preset (C4, C5, ...) instead of --nodes/--latent")
+    ap.add_argument("--graph", action="store_true",
+                    help="capture the step in a HIP graph and time REPLAYS (the bench's path; side-stream "
+                         "concurrency as the bench runs it) instead of eager steps")
     args = ap.parse_args()
     import torch
     from snd_vae_amd.config import PRESETS, tscale
@@ -28,8 +32,13 @@ def main():
     db = DeviceBatch(synthetic_batch(cfg, args.graphs, seed=1000), tile_rows=default_tile_rows(cfg.g_conv_hidden[1]))
     model = SGCNModelVAE(cfg, args.graphs, dtype=args.dtype)
     opt = OptimizerVAE(model)
-    for _ in range(args.steps):
-        opt.step(db)
+    if args.graph:
+        opt.capture(db)
+        for _ in range(args.steps):
+            opt.replay()
+    else:
+        for _ in range(args.steps):
+            opt.step(db)
     torch.cuda.synchronize()
     print("ok", args.steps)
 
