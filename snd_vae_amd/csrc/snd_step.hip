@@ -728,7 +728,16 @@ void init_concurrency(const snd_plan& p, hipStream_t main) {
   hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
   if (hipStreamIsCapturing(main, &st) != hipSuccess || st != hipStreamCaptureStatusNone) return;
   p.conc = -1;
-  if (hipStreamCreateWithFlags(&p.side, hipStreamNonBlocking) != hipSuccess) return;
+  // A/B (SND_SIDE_PRIO=1): the side stream at the device's highest priority, so the
+  // concurrent decoder's workgroups are dispatched ahead of zz^T's when CUs free up
+  const char* sp = getenv("SND_SIDE_PRIO");
+  if (sp && atoi(sp) > 0) {
+    int lo = 0, hi = 0;
+    if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess ||
+        hipStreamCreateWithPriority(&p.side, hipStreamNonBlocking, hi) != hipSuccess) return;
+  } else if (hipStreamCreateWithFlags(&p.side, hipStreamNonBlocking) != hipSuccess) {
+    return;
+  }
   for (auto& e : p.ev)
     if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return;
   p.conc = 1;

@@ -31,3 +31,14 @@ for B in 1 8; do
   rc=$?; echo "== trace B=$B exit $rc"; case $rc in 124|134|137|139) exit $rc;; esac
   python tools/step_timeline.py gpurun_out/st/g$B/run_kernel_trace.csv > gpurun_out/st/g$B.timeline.txt && cat gpurun_out/st/g$B.timeline.txt
 done
+# one-graph step (C3 per rank): side stream at the highest priority or not, alternating
+for r in 1 2 3; do
+  for pr in 0 1; do
+    SND_SIDE_PRIO=$pr timeout -k 10 180 python tools/ab_run.py --graphs 1 --kernels zzt_dense --tag prio$pr \
+      >> gpurun_out/ab_prio.jsonl 2>> gpurun_out/ab_prio.err || { echo "prio run failed"; tail -5 gpurun_out/ab_prio.err; break 2; }
+    tail -1 gpurun_out/ab_prio.jsonl | cut -c1-160
+  done
+done
+SND_SIDE_PRIO=1 timeout -k 10 200 rocprofv3 --kernel-trace -d gpurun_out/st/g1p -o run --output-format csv \
+  -- python tools/prof_step.py --graphs 1 --steps 6 --graph > gpurun_out/st_g1p.log 2>&1 && \
+  python tools/step_timeline.py gpurun_out/st/g1p/run_kernel_trace.csv > gpurun_out/st/g1p.timeline.txt && cat gpurun_out/st/g1p.timeline.txt
