@@ -19,6 +19,9 @@ STAGES="smoke bench" bash tools/gpu_session.sh
 # against HEAD, alternating processes, step + chain kernels
 rm -f gpurun_out/ab.jsonl
 bash tools/ab.sh "--kernels zzt_dense,head_fwd,head_bwd,dec:fwd,dec:bwd,wgrad_multi" ab/base.so ab/noslp.so 3
+# A/B: the dec_fwd head phase on 4 threads per row
+bash tools/ab.sh "--kernels dec:fwd" ab/base.so ab/decheads.so 3
+bash tools/ab.sh "--kernels dec:fwd --graphs 1" ab/base.so ab/decheads.so 2
 # zz^T symmetric-tile evidence: the v9 phase-skip proxy and the slab microbenchmark
 timeout -k 10 300 python -u tools/ab_zzt.py --rounds 3 --reps 20 \
   --variants zzt_dense,zzt_dense_v256,zzt_dense_v1024,zzt_dense_v4096 > gpurun_out/zzt_sym_proxy.txt 2>&1
