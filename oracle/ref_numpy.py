@@ -178,7 +178,7 @@ def adj_ce_rows(J, A, n, r0, r1, pos_weight=1.0, norm=1.0, row_chunk=1024):
 
 # ----------------------------------------------------------------- model
 def forward_backward(p: Dict[str, np.ndarray], adj, X, Xf, S, eps, cfg,
-                     want_grads=True, row_chunk=None, amb_tol=None):
+                     want_grads=True, row_chunk=None, amb_tol=None, kink_tol=None):
     """One training step's forward + hand-derived backward.
 
     adj: list of B [N,N] 0/1 adjacencies (dense arrays, or scipy sparse for
@@ -186,6 +186,14 @@ def forward_backward(p: Dict[str, np.ndarray], adj, X, Xf, S, eps, cfg,
     S [B*N, 2]; eps [B*N, L] (tscale) or [B, L] (tref, model_joint.py:89).
     Returns (losses dict, grads dict, cache); with ``amb_tol`` the losses hold
     ``ambiguous`` = #{off-diagonal |L| < amb_tol}.
+
+    ``kink_tol``: cache["kink"][block] = the element-wise envelope of how far that
+    gradient block moves if every lrelu pre-activation within kink_tol x (its layer's
+    max |pre-activation|) of the kink took the other derivative (1 <-> 0.2): a finite-
+    precision evaluation may legitimately land on either side there.  Only the blocks a
+    flipped dT reaches directly (the layer's BN gamma / beta, conv bias and weights; the
+    encoder's W0 / W1 through A) are bounded; the data gradients further upstream move by
+    one row's worth, far below their blocks' max-abs.
     """
     n = cfg.n_nodes
     R = X.shape[0]
@@ -272,6 +280,11 @@ def forward_backward(p: Dict[str, np.ndarray], adj, X, Xf, S, eps, cfg,
     g["dec.bn"] = dZn.sum(0)
     dU2n = dZn @ p["dec.Wn"].T
 
+    kink = {}
+
+    def near_kink(T):
+        return np.abs(T) < kink_tol * max(np.abs(T).max(), 1e-30)
+
     def dec_layer(dU, T, Y, Xin, pre, wname, bname):
         dT = dU * lrelu_grad(T)
         g[pre + ".gamma"] = (dT * Y).sum(0) * c
@@ -280,6 +293,13 @@ def forward_backward(p: Dict[str, np.ndarray], adj, X, Xf, S, eps, cfg,
         dX, dW, db = per_graph_conv_bwd(Xin, p[wname], dY, n)
         g[wname] = dW
         g[bname] = db
+        if kink_tol is not None:   # flip envelope: |delta dT| = 0.8 |dU| at near-kink elements
+            E = 0.8 * np.abs(dU) * near_kink(T)
+            Ey = E * np.abs(p[pre + ".gamma"] * c)
+            kink[pre + ".beta"] = E.sum(0)
+            kink[pre + ".gamma"] = (E * np.abs(Y)).sum(0) * c
+            kink[bname] = Ey.sum(0)
+            kink[wname] = per_graph_conv_bwd(np.abs(Xin), p[wname], Ey, n)[1]
         return dX
 
     dU2s = dec_layer(dU3s, T3s, Y3s, U2s, "dec.bn3s", "dec.K3s", "dec.b3s")
@@ -316,6 +336,9 @@ def forward_backward(p: Dict[str, np.ndarray], adj, X, Xf, S, eps, cfg,
     dP1 = dB1 * (p["enc.bn1.gamma"] * c) * lrelu_grad(P1)
     dXW1 = spmm(adj, dP1, n)                     # A symmetric
     g["enc.W1"] = H1.T @ dXW1
+    if kink_tol is not None:
+        E1 = 0.8 * np.abs(dB1 * (p["enc.bn1.gamma"] * c)) * near_kink(P1)
+        kink["enc.W1"] = np.abs(H1).T @ spmm(adj, E1, n)
     dH1 = dXW1 @ p["enc.W1"].T
     dB0 = dH1[:, :h0]
     g["enc.bn0.gamma"] = (dB0 * A0).sum(0) * c
@@ -323,6 +346,10 @@ def forward_backward(p: Dict[str, np.ndarray], adj, X, Xf, S, eps, cfg,
     dP0 = dB0 * (p["enc.bn0.gamma"] * c) * lrelu_grad(P0)
     dXW0 = spmm(adj, dP0, n)
     g["enc.W0"] = X.T @ dXW0
+    if kink_tol is not None:
+        E0 = 0.8 * np.abs(dB0 * (p["enc.bn0.gamma"] * c)) * near_kink(P0)
+        kink["enc.W0"] = np.abs(X).T @ spmm(adj, E0, n)
+        cache["kink"] = kink
     cache["dJ"] = dJ
     return losses, g, cache
 

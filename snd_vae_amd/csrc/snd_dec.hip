@@ -259,11 +259,11 @@ __device__ __forceinline__ float colpar(const ColMap& m, int n, const float* A, 
 // thread per row left 12 of the 16 waves idle for the whole phase (round 3 stamps:
 // 3.9 us of a 13 us 32-row workgroup); the values are bitwise those of one thread per
 // row.  Partial sums {dW, db, sum dt*y, sum dt, sum dy} reduced over the tile later.
-#ifndef SND_DEC_HEAD_PARTS
-#define SND_DEC_HEAD_PARTS 4
-#endif
-constexpr int HP = SND_DEC_HEAD_PARTS;
-template <int CIN, int COUT>
+// Only below 128-row tiles: at 128 rows (B = 8) the 1024 head threads already fill the
+// workgroup and the parts' repeated head sums cost more than the parallelism gains
+// (dec_fwd 21.2-21.6 -> 23.1-23.2 us; 32-row tiles 14.7 -> 13.6-13.7 us; round 6).
+template <int TR> constexpr int head_parts() { return TR < 128 ? 4 : 1; }
+template <int CIN, int COUT, int HP>
 __device__ __forceinline__ void head_tile(int part, int orow, bool rv, long long gr, const float (&u)[CIN],
                                           const float (&yv)[CIN], const float* hp, const float (&tg)[COUT],
                                           float count, float* yhat, __bf16* dyp, float* scr,
@@ -399,6 +399,7 @@ __global__ void __launch_bounds__(DT) dec_fwd_kernel(DecChainFwdArgs a) {
     else if (j >= 24 + cin && j < 24 + 2 * cin) v = be[j - 24 - cin];
     hp[hh][j] = v;
   }
+  constexpr int HP = head_parts<TR>();
   float tg[2] = {0.f, 0.f};
   if (tid < 2 * TR * HP) {   // thread (row-head rh, part tid % HP): the head phase's mapping
     const int rh = tid / HP, orow = rh % TR;
@@ -538,7 +539,7 @@ __global__ void __launch_bounds__(DT) dec_fwd_kernel(DecChainFwdArgs a) {
   constexpr int NQS = head_nq(10, 2), NQN = head_nq(20, 1);
   float* scr = reinterpret_cast<float*>(smem + L.w);
   double* sscr = reinterpret_cast<double*>(smem + L.w + (NQS + NQN) * kScr * 4);
-  static_assert(2 * kDecRows * HP <= DT, "dec_fwd: head threads");
+  static_assert(2 * TR * HP <= DT, "dec_fwd: head threads");
   if (!(kdbg(a.dbg) & 2)) {
     if (tid < 2 * TR * HP) {
       const int part = tid % HP, rh = tid / HP;
@@ -550,7 +551,7 @@ __global__ void __launch_bounds__(DT) dec_fwd_kernel(DecChainFwdArgs a) {
 #pragma unroll
         for (int k = 0; k < 10; ++k) { u[k] = rv ? u3[orow * 16 + k] : 0.f; yv[k] = rv ? y3[orow * 16 + k] : 0.f; }
         const float t2[2] = {tg[0], tg[1]};
-        head_tile<10, 2>(part, orow, rv, gr, u, yv, hp[0], t2, a.cnt_s, a.shat, a.dy3 + gr * a.lddy3, scr, sscr);
+        head_tile<10, 2, HP>(part, orow, rv, gr, u, yv, hp[0], t2, a.cnt_s, a.shat, a.dy3 + gr * a.lddy3, scr, sscr);
       } else {
         float u[20], yv[20];
 #pragma unroll
@@ -560,7 +561,7 @@ __global__ void __launch_bounds__(DT) dec_fwd_kernel(DecChainFwdArgs a) {
           yv[k] = rv ? y2n[orow * L.ldY2n + k] : 0.f;
         }
         const float t1[1] = {tg[0]};
-        head_tile<20, 1>(part, orow, rv, gr, u, yv, hp[1], t1, a.cnt_n, a.xhat, a.dy2 + gr * a.lddy2 + a.m2.offb,
+        head_tile<20, 1, HP>(part, orow, rv, gr, u, yv, hp[1], t1, a.cnt_n, a.xhat, a.dy2 + gr * a.lddy2 + a.m2.offb,
                          scr + NQS * kScr, sscr + TR);
       }
     }

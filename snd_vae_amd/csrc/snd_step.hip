@@ -728,16 +728,9 @@ void init_concurrency(const snd_plan& p, hipStream_t main) {
   hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
   if (hipStreamIsCapturing(main, &st) != hipSuccess || st != hipStreamCaptureStatusNone) return;
   p.conc = -1;
-  // A/B (SND_SIDE_PRIO=1): the side stream at the device's highest priority, so the
-  // concurrent decoder's workgroups are dispatched ahead of zz^T's when CUs free up
-  const char* sp = getenv("SND_SIDE_PRIO");
-  if (sp && atoi(sp) > 0) {
-    int lo = 0, hi = 0;
-    if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess ||
-        hipStreamCreateWithPriority(&p.side, hipStreamNonBlocking, hi) != hipSuccess) return;
-  } else if (hipStreamCreateWithFlags(&p.side, hipStreamNonBlocking) != hipSuccess) {
-    return;
-  }
+  // (a side stream at the device's highest priority made the captured one-graph step
+  // 3.5x slower, 0.118 -> 0.42 ms: round 6, profiles/r06_ab_b1_concurrency.txt)
+  if (hipStreamCreateWithFlags(&p.side, hipStreamNonBlocking) != hipSuccess) return;
   for (auto& e : p.ev)
     if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return;
   p.conc = 1;
@@ -1841,7 +1834,8 @@ extern "C" int snd_train_step(const snd_plan_t* plan, const snd_batch_t* batch,
     za.tsplit = x.zts;
     // concurrent decoder: the fused decoder on the side stream beside zz^T (forked after
     // the staging that both read, joined before the backward head that reads both)
-    if (cdec) {
+    const bool zzt_side = cdec && (debug_flags() & (1 << 17));   // A/B: the roles swapped
+    if (cdec && !zzt_side) {
       SND_TRY(fork_to(x, p.side));
       Ctx xd = x;
       xd.s = p.side;
@@ -1849,8 +1843,18 @@ extern "C" int snd_train_step(const snd_plan_t* plan, const snd_batch_t* batch,
       SND_TRY(decoder_fast(xd, batch));
     }
     // the column-split sum is folded into head_bwd / reparam_bwd_fast (node latent, fast encoder)
-    SND_TRY(launch_zzt_dense(za, c.dtype, x.s, p.fast_enc && !p.tref));
-    if (cdec) SND_TRY(join_from(x, p.side));
+    if (zzt_side) {
+      // zz^T (the shorter branch) on the side stream, the decoder chain on main: the main
+      // stream runs head_fwd -> dec_fwd -> dec_bwd -> head_bwd with no cross-queue wait on
+      // its own critical path; the join waits for zz^T, which has finished by then
+      SND_TRY(fork_to(x, p.side));
+      SND_TRY(launch_zzt_dense(za, c.dtype, p.side, p.fast_enc && !p.tref));
+      SND_TRY(decoder_fast(x, batch));
+      SND_TRY(join_from(x, p.side));
+    } else {
+      SND_TRY(launch_zzt_dense(za, c.dtype, x.s, p.fast_enc && !p.tref));
+    }
+    if (cdec && !zzt_side) SND_TRY(join_from(x, p.side));
   }
   if (p.fast) {
     if (!cdec) SND_TRY(decoder_fast(x, batch));

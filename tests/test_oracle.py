@@ -155,3 +155,44 @@ def test_adj_ce_chunked_sparse_equals_dense():
     assert abs(ce1 - ce0) <= 1e-12 * abs(ce0)
     np.testing.assert_allclose(dj1, dj0, rtol=1e-12, atol=1e-12)
     assert c1 == c0 and amb >= 0
+
+
+def test_kink_envelope_bounds_a_flipped_derivative():
+    """forward_backward(kink_tol=...) returns, per gradient block a flipped lrelu' reaches
+    directly, the envelope of that flip (fp32 evaluations may land on either
+    side of the kink for pre-activations within rounding of 0).  Flip every near-kink
+    derivative (1 <-> 0.2) and check the decoder's first-in-backward layers (3s, 2n: their
+    upstream gradient comes straight from the heads, so only their own flips move them)
+    stay inside their envelopes, and that the envelope is zero when nothing is near 0."""
+    import oracle.ref_numpy as RN
+    from snd_vae_amd.config import tscale
+    from snd_vae_amd.data import synthetic_batch
+    from snd_vae_amd.params import init_blocks
+    cfg = tscale(60, 16, mean_degree=5.0)
+    b = synthetic_batch(cfg, 2, seed=4)
+    p = {k: v.astype(np.float64) for k, v in init_blocks(cfg, 1).items()}
+    eps = np.random.default_rng(3).standard_normal((2 * 60, 16))
+    adj = [b.dense_adj(i) for i in range(2)]
+    tol = 0.05
+    _, g, cache = RN.forward_backward(p, adj, b.features, b.feature_truth, b.spatial_truth, eps, cfg, kink_tol=tol)
+    env = cache["kink"]
+    orig = RN.lrelu_grad
+
+    def flipped(x):
+        d = orig(x)
+        near = np.abs(x) < tol * max(np.abs(x).max(), 1e-30)
+        return np.where(near, 1.2 - d, d)        # 1 <-> 0.2
+    RN.lrelu_grad = flipped
+    try:
+        _, g2, _ = RN.forward_backward(p, adj, b.features, b.feature_truth, b.spatial_truth, eps, cfg)
+    finally:
+        RN.lrelu_grad = orig
+    moved = 0.0
+    for k in ("dec.bn3s.beta", "dec.bn3s.gamma", "dec.b3s", "dec.K3s", "dec.bn2n.beta", "dec.bn2n.gamma",
+              "dec.b2n", "dec.K2n"):
+        d = np.abs(g2[k] - g[k])
+        assert (d <= env[k] * (1 + 1e-9) + 1e-15).all(), k
+        moved = max(moved, d.max())
+    assert moved > 0                               # the flips did move these blocks
+    _, _, c0 = RN.forward_backward(p, adj, b.features, b.feature_truth, b.spatial_truth, eps, cfg, kink_tol=0.0)
+    assert all(np.all(v == 0) for v in c0["kink"].values())

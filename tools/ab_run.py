@@ -25,6 +25,8 @@ def main():
     ap.add_argument("--adam-per-range", action="store_true",
                     help="A/B: one snd_adam_tf1 launch per unfused range instead of snd_adam_tf1_ranges")
     ap.add_argument("--debug", default="", help="comma list of snd_debug_set bits: each kernel is timed under each")
+    ap.add_argument("--step-debug", type=int, default=0,
+                    help="snd_debug_set bits for the captured step itself (host-side A/B switches)")
     args = ap.parse_args()
     import torch
 
@@ -35,6 +37,9 @@ def main():
     from snd_vae_amd.model import DeviceBatch, SGCNModelVAE
     from snd_vae_amd.optimizer import OptimizerVAE
     from snd_vae_amd.config import PRESETS
+    if args.step_debug:
+        _lib.lib().snd_debug_set(args.step_debug)
+        args.tag += f" dbg{args.step_debug}"
     cfg = PRESETS[args.config] if args.config else tscale(args.nodes, args.latent)
     db = DeviceBatch(synthetic_batch(cfg, args.graphs, seed=1000))
     model = SGCNModelVAE(cfg, args.graphs, dtype="bf16")

@@ -22,12 +22,16 @@ def main():
     ap.add_argument("--graph", action="store_true",
                     help="capture the step in a HIP graph and time REPLAYS (the bench's path; side-stream "
                          "concurrency as the bench runs it) instead of eager steps")
+    ap.add_argument("--debug", type=int, default=0, help="snd_debug_set bits for the steps (A/B switches)")
     args = ap.parse_args()
     import torch
     from snd_vae_amd.config import PRESETS, tscale
     from snd_vae_amd.data import default_tile_rows, synthetic_batch
     from snd_vae_amd.model import DeviceBatch, SGCNModelVAE
     from snd_vae_amd.optimizer import OptimizerVAE
+    if args.debug:
+        from snd_vae_amd import _lib
+        _lib.lib().snd_debug_set(args.debug)
     cfg = PRESETS[args.config] if args.config else tscale(args.nodes, args.latent)
     db = DeviceBatch(synthetic_batch(cfg, args.graphs, seed=1000), tile_rows=default_tile_rows(cfg.g_conv_hidden[1]))
     model = SGCNModelVAE(cfg, args.graphs, dtype=args.dtype)
