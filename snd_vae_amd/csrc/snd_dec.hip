@@ -567,33 +567,22 @@ __global__ void __launch_bounds__(DT) dec_fwd_kernel(DecChainFwdArgs a) {
     }
     __syncthreads();
     if (stamp) ts[7] = __builtin_amdgcn_s_memrealtime();
-    // tile partials: each quantity over the TR rows by 4 consecutive lanes, lane j summing
-    // rows j, j + 4, ... in order, then (l0 + l1) + (l2 + l3); the squared errors the same
-    // way on the lanes after them
-    constexpr int NQ = NQS + NQN;
-    static_assert(4 * (NQ + 2) <= DT, "dec_fwd: partial lanes");
-    if (tid < 4 * (NQ + 2)) {
-      const int qi = tid >> 2, j = tid & 3;
-      if (qi < NQ) {
-        const float* src = scr + qi * kScr;
-        float v = 0.f;
-#pragma unroll 8
-        for (int r = j; r < TR; r += 4) v += src[r];
-        v += __shfl_xor(v, 1, 4);
-        v += __shfl_xor(v, 2, 4);
-        if (j == 0) {
-          if (qi < NQS) a.phs[(long long)t * NQS + qi] = v;
-          else a.phn[(long long)t * NQN + qi - NQS] = v;
-        }
-      } else {
-        const double* src = sscr + TR * (qi - NQ);
-        double v = 0.0;
-#pragma unroll 8
-        for (int r = j; r < TR; r += 4) v += src[r];
-        v += __shfl_xor(v, 1, 4);
-        v += __shfl_xor(v, 2, 4);
-        if (j == 0) (qi == NQ ? a.sse_s : a.sse_n)[t] = v;
-      }
+    // tile partials: each quantity summed over the TR rows in order (4 lanes per quantity,
+    // (l0 + l1) + (l2 + l3), measured 0.9 us slower at 128-row tiles: their scratch reads
+    // collide in the LDS banks; round 6)
+    if (tid < NQS + NQN) {
+      const float* src = scr + tid * kScr;
+      float v = 0.f;
+#pragma unroll 32
+      for (int r = 0; r < TR; ++r) v += src[r];
+      if (tid < NQS) a.phs[(long long)t * NQS + tid] = v;
+      else a.phn[(long long)t * NQN + tid - NQS] = v;
+    } else if (tid >= 256 && tid < 258) {
+      const double* src = sscr + TR * (tid - 256);
+      double v = 0.0;
+#pragma unroll 32
+      for (int r = 0; r < TR; ++r) v += src[r];
+      (tid == 256 ? a.sse_s : a.sse_n)[t] = v;
     }
   }
   if (stamp) {

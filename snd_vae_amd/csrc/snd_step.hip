@@ -1834,8 +1834,10 @@ extern "C" int snd_train_step(const snd_plan_t* plan, const snd_batch_t* batch,
     za.tsplit = x.zts;
     // concurrent decoder: the fused decoder on the side stream beside zz^T (forked after
     // the staging that both read, joined before the backward head that reads both)
-    const bool zzt_side = cdec && (debug_flags() & (1 << 17));   // A/B: the roles swapped
-    if (cdec && !zzt_side) {
+    // (the roles swapped -- zz^T on the side stream, the decoder chain on main, so that the
+    // main stream has no cross-queue wait before the decoder -- measured 0.1163-0.1183 ->
+    // 0.1353-0.1356 ms: zz^T, dispatched first, takes the CUs the decoder needs; round 6)
+    if (cdec) {
       SND_TRY(fork_to(x, p.side));
       Ctx xd = x;
       xd.s = p.side;
@@ -1843,18 +1845,8 @@ extern "C" int snd_train_step(const snd_plan_t* plan, const snd_batch_t* batch,
       SND_TRY(decoder_fast(xd, batch));
     }
     // the column-split sum is folded into head_bwd / reparam_bwd_fast (node latent, fast encoder)
-    if (zzt_side) {
-      // zz^T (the shorter branch) on the side stream, the decoder chain on main: the main
-      // stream runs head_fwd -> dec_fwd -> dec_bwd -> head_bwd with no cross-queue wait on
-      // its own critical path; the join waits for zz^T, which has finished by then
-      SND_TRY(fork_to(x, p.side));
-      SND_TRY(launch_zzt_dense(za, c.dtype, p.side, p.fast_enc && !p.tref));
-      SND_TRY(decoder_fast(x, batch));
-      SND_TRY(join_from(x, p.side));
-    } else {
-      SND_TRY(launch_zzt_dense(za, c.dtype, x.s, p.fast_enc && !p.tref));
-    }
-    if (cdec && !zzt_side) SND_TRY(join_from(x, p.side));
+    SND_TRY(launch_zzt_dense(za, c.dtype, x.s, p.fast_enc && !p.tref));
+    if (cdec) SND_TRY(join_from(x, p.side));
   }
   if (p.fast) {
     if (!cdec) SND_TRY(decoder_fast(x, batch));

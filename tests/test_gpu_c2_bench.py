@@ -18,8 +18,12 @@ and compares after step t:
   away from |L| < 1e-4 -- a wrong logit anywhere in zz^T or the per-edge terms fails here;
 * the gradient blocks the step wrote, against the oracle's, as max-abs error over the
   block's max-abs: f32 max(2e-4, 10 e32), e32 being the reference formulation's own
-  float32 error on that block (oracle/ref_torch.py, autograd) -- the decoder's conv1 sums
-  over 32768 rows cancel in any fp32 evaluation; bf16 2x the measured error per block
+  float32 error on that block (oracle/ref_torch.py, autograd); where the fp32 step's
+  lrelu' differs from the oracle's at a pre-activation that is zero to within 1e-6 of
+  its layer's scale (a rounding tie at the kink, layers.py:112-113), the oracle takes the
+  GPU's side (gpu_kink_choices) -- measured: one element at step 3, T = 5e-8, which alone
+  moved dec.K1 / dec.b1 / dec.bn1.beta by 1.3-2.0e-3 of their max-abs; a disagreement
+  farther from 0 fails; bf16 2x the measured error per block
   (parity_bars.json; the bf16 gap to the float64 oracle is the bf16 operands' rounding
   and is parity-unpinned against TF, which has no bf16 path);
 * the fused update against the GPU's OWN gradient, in float64: m, v and the parameters
@@ -61,6 +65,40 @@ def block_err(g, ref):
     return float(np.abs(g - ref).max() / max(np.abs(ref).max(), 1e-30))
 
 
+# a derivative disagreement with the oracle is a rounding tie only where the oracle's own
+# pre-activation is this close to 0 (relative to its layer's max |value|); measured, round
+# 6: ONE element over the three fp32 steps, at 1.7e-8 (tools/diag_kink.py)
+KINK_REL = 1e-6
+KINK_LAYERS = {"P0": ("P0", None), "P1": ("P1", None), "T1": ("Y1", "dec.bn1"),
+               "T2s": ("Y2S", "dec.bn2s"), "T2n": ("Y2N", "dec.bn2n"), "T3s": ("Y3S", "dec.bn3s")}
+
+
+def gpu_kink_choices(model, p, cache, cfg, B):
+    """The lrelu derivative the fp32 step actually used wherever it differs from the
+    oracle's.  lrelu' is discontinuous at 0 (layers.py:112-113), so a pre-activation that
+    is zero to within rounding may land on either side in any finite-precision evaluation:
+    at such an element the oracle takes the GPU's side (ref_numpy lrelu_override), and the
+    gradients are then held to the unchanged bars.  Any disagreement at a pre-activation
+    NOT within KINK_REL of zero is reported as a failure ("beyond_rounding")."""
+    R_ = B * cfg.n_nodes
+    over, info = {}, {}
+    for name, (buf, bn) in KINK_LAYERS.items():
+        ref = cache[name]
+        w = ref.shape[1]
+        y = model.buffer(buf)[:R_ * w].view(R_, w).double().cpu().numpy()
+        gpu = y if bn is None else y * (p[bn + ".gamma"] * R.BN_C) + p[bn + ".beta"]
+        scale = max(np.abs(ref).max(), 1e-30)
+        assert np.abs(gpu - ref).max() <= 1e-4 * scale, (name, "GPU pre-activation buffer layout")
+        diff = (gpu >= 0) != (ref >= 0)
+        if diff.any():
+            o = np.full(ref.shape, np.nan)
+            o[diff] = np.where(gpu[diff] >= 0, 1.0, 0.2)
+            over[name] = o
+            info[name] = {"n": int(diff.sum()), "max_rel": float(np.abs(ref[diff]).max() / scale),
+                          "beyond_rounding": bool(np.abs(ref[diff]).max() > KINK_REL * scale)}
+    return over, info
+
+
 def adam_from(p, g, m, v, t, lr, b1, b2, eps):
     """TF1 Adam (optimizer.py:125 -> tf.train.AdamOptimizer) in float64 on one block, with
     TF's float32 coefficients: its ApplyAdam kernel forms 1 - beta1 and 1 - beta2 in the
@@ -100,9 +138,16 @@ def test_c2_bench_batch_steps_vs_oracle(dtype):
         v = {k: np.asarray(x, np.float64) for k, x in v.items()}
         opt.step(db, torch.from_numpy(eps[t - 1]).cuda())
         torch.cuda.synchronize()
-        rl, rg, _ = R.forward_backward(p, adj, batch.features, batch.feature_truth,
-                                       batch.spatial_truth, eps[t - 1].astype(np.float64),
-                                       cfg, row_chunk=1024)
+        rl, rg, rc = R.forward_backward(p, adj, batch.features, batch.feature_truth,
+                                        batch.spatial_truth, eps[t - 1].astype(np.float64),
+                                        cfg, row_chunk=1024)
+        kinks = {}
+        if dtype == "f32":   # lrelu' at pre-activations that are zero within fp32 rounding
+            over, kinks = gpu_kink_choices(model, p, rc, cfg, B)
+            if over:
+                rg = R.forward_backward(p, adj, batch.features, batch.feature_truth, batch.spatial_truth,
+                                        eps[t - 1].astype(np.float64), cfg, row_chunk=1024,
+                                        lrelu_override=over)[1]
         pr = {k: x.copy() for k, x in p.items()}
         mr = {k: x.copy() for k, x in m.items()}
         vr = {k: x.copy() for k, x in v.items()}
@@ -114,6 +159,9 @@ def test_c2_bench_batch_steps_vs_oracle(dtype):
         gm = {k: np.asarray(x, np.float64) for k, x in gm.items()}
         gv = {k: np.asarray(x, np.float64) for k, x in gv.items()}
         bars = PB.Bars(f"c2_bench_steps/{dtype}", dtype=dtype, step=t)
+        if kinks:
+            bars.note("kink_choices", kinks)
+            fails += [(t, "kink", k, v) for k, v in kinks.items() if v["beyond_rounding"]]
         for k in TERMS:
             e = abs(got[k] - rl[k]) / max(abs(rl[k]), 1e-30)
             if dtype == "f32":

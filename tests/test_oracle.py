@@ -157,13 +157,12 @@ def test_adj_ce_chunked_sparse_equals_dense():
     assert c1 == c0 and amb >= 0
 
 
-def test_kink_envelope_bounds_a_flipped_derivative():
-    """forward_backward(kink_tol=...) returns, per gradient block a flipped lrelu' reaches
-    directly, the envelope of that flip (fp32 evaluations may land on either
-    side of the kink for pre-activations within rounding of 0).  Flip every near-kink
-    derivative (1 <-> 0.2) and check the decoder's first-in-backward layers (3s, 2n: their
-    upstream gradient comes straight from the heads, so only their own flips move them)
-    stay inside their envelopes, and that the envelope is zero when nothing is near 0."""
+
+def test_lrelu_override_changes_exactly_the_overridden_derivatives():
+    """forward_backward(lrelu_override=...) evaluates the backward pass with the given
+    lrelu' at the given elements (NaN elsewhere = the oracle's own choice): overriding every
+    element with the oracle's own derivative changes nothing, and flipping ONE element of
+    the decoder's layer-1 pre-activation moves dec.b1 by exactly 0.8 dU1 gamma c there."""
     import oracle.ref_numpy as RN
     from snd_vae_amd.config import tscale
     from snd_vae_amd.data import synthetic_batch
@@ -173,26 +172,20 @@ def test_kink_envelope_bounds_a_flipped_derivative():
     p = {k: v.astype(np.float64) for k, v in init_blocks(cfg, 1).items()}
     eps = np.random.default_rng(3).standard_normal((2 * 60, 16))
     adj = [b.dense_adj(i) for i in range(2)]
-    tol = 0.05
-    _, g, cache = RN.forward_backward(p, adj, b.features, b.feature_truth, b.spatial_truth, eps, cfg, kink_tol=tol)
-    env = cache["kink"]
-    orig = RN.lrelu_grad
-
-    def flipped(x):
-        d = orig(x)
-        near = np.abs(x) < tol * max(np.abs(x).max(), 1e-30)
-        return np.where(near, 1.2 - d, d)        # 1 <-> 0.2
-    RN.lrelu_grad = flipped
-    try:
-        _, g2, _ = RN.forward_backward(p, adj, b.features, b.feature_truth, b.spatial_truth, eps, cfg)
-    finally:
-        RN.lrelu_grad = orig
-    moved = 0.0
-    for k in ("dec.bn3s.beta", "dec.bn3s.gamma", "dec.b3s", "dec.K3s", "dec.bn2n.beta", "dec.bn2n.gamma",
-              "dec.b2n", "dec.K2n"):
-        d = np.abs(g2[k] - g[k])
-        assert (d <= env[k] * (1 + 1e-9) + 1e-15).all(), k
-        moved = max(moved, d.max())
-    assert moved > 0                               # the flips did move these blocks
-    _, _, c0 = RN.forward_backward(p, adj, b.features, b.feature_truth, b.spatial_truth, eps, cfg, kink_tol=0.0)
-    assert all(np.all(v == 0) for v in c0["kink"].values())
+    args = (p, adj, b.features, b.feature_truth, b.spatial_truth, eps, cfg)
+    _, g, cache = RN.forward_backward(*args)
+    same = {k: RN.lrelu_grad(cache[k]) for k in ("P0", "P1", "T1", "T2s", "T3s", "T2n")}
+    _, g_same, _ = RN.forward_backward(*args, lrelu_override=same)
+    assert all(np.array_equal(g[k], g_same[k]) for k in g)
+    T1 = cache["T1"]
+    r, col = np.unravel_index(np.argmin(np.abs(T1)), T1.shape)
+    o = np.full(T1.shape, np.nan)
+    o[r, col] = 1.2 - RN.lrelu_grad(T1[r, col])      # the other side: 1 <-> 0.2
+    _, g_flip, c2 = RN.forward_backward(*args, lrelu_override={"T1": o})
+    # dU1 at (r, col) from the flipped run's own backward: recompute it from dT1 = dU1 * d
+    gam = p["dec.bn1.gamma"][col] * RN.BN_C
+    delta = g_flip["dec.b1"] - g["dec.b1"]
+    assert np.count_nonzero(delta) == 1 and delta[col] != 0
+    d_old, d_new = RN.lrelu_grad(T1[r, col]), o[r, col]
+    dU = (g_flip["dec.bn1.beta"][col] - g["dec.bn1.beta"][col]) / (d_new - d_old)
+    assert delta[col] == pytest.approx(dU * (d_new - d_old) * gam, rel=1e-9)
