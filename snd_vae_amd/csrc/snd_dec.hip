@@ -251,29 +251,23 @@ __device__ __forceinline__ float colpar(const ColMap& m, int n, const float* A, 
 }
 
 // ------------------------------------------------------------------ heads
-// HP threads per own row (model_joint.py:121,144; optimizer.py:149,153): as
-// heads_fast_kernel's head_rows, with the inputs read from LDS.  Every part computes the
-// row's head outputs (the same sums in the same order); part p then takes the input
-// channel groups of 4 with index % HP == p -- their backward (dt, dy) and their per-row
-// partial quantities -- and part 0 the head bias terms and the squared error.  One
-// thread per row left 12 of the 16 waves idle for the whole phase (round 3 stamps:
-// 3.9 us of a 13 us 32-row workgroup); the values are bitwise those of one thread per
-// row.  Partial sums {dW, db, sum dt*y, sum dt, sum dy} reduced over the tile later.
-// Only below 128-row tiles: at 128 rows (B = 8) the 1024 head threads already fill the
-// workgroup and the parts' repeated head sums cost more than the parallelism gains
-// (dec_fwd 21.2-21.6 -> 23.1-23.2 us; 32-row tiles 14.7 -> 13.6-13.7 us; round 6).
-template <int TR> constexpr int head_parts() { return TR < 128 ? 4 : 1; }
-template <int CIN, int COUT, int HP>
-__device__ __forceinline__ void head_tile(int part, int orow, bool rv, long long gr, const float (&u)[CIN],
+// One thread per own row (model_joint.py:121,144; optimizer.py:149,153): as
+// heads_fast_kernel's head_rows, with the inputs read from LDS.  Partial sums
+// {dW, db, sum dt*y, sum dt, sum dy} reduced over the tile in fixed order.
+template <int CIN, int COUT>
+__device__ __forceinline__ void head_tile(int hi, int orow, bool rv, long long gr, const float (&u)[CIN],
                                           const float (&yv)[CIN], const float* hp, const float (&tg)[COUT],
                                           float count, float* yhat, __bf16* dyp, float* scr,
                                           double* sscr) {
   // hp (LDS, loaded at kernel start): W [CIN][COUT] | b [COUT] at 20 | gamma at 24 | beta at 24 + CIN
-  float wv[CIN][COUT], bv[COUT];
+  float wv[CIN][COUT], bv[COUT], gk[CIN], bk[CIN];
 #pragma unroll
-  for (int k = 0; k < CIN; ++k)
+  for (int k = 0; k < CIN; ++k) {
 #pragma unroll
     for (int o = 0; o < COUT; ++o) wv[k][o] = hp[k * COUT + o];
+    gk[k] = hp[24 + k] * kBnC;
+    bk[k] = hp[24 + CIN + k];
+  }
 #pragma unroll
   for (int o = 0; o < COUT; ++o) bv[o] = hp[20 + o];
   float dp[COUT];
@@ -285,55 +279,50 @@ __device__ __forceinline__ void head_tile(int part, int orow, bool rv, long long
     for (int k = 0; k < CIN; ++k) zo += u[k] * wv[k][o];
     const float yh = 1.f / (1.f + __expf(-zo));
     const float diff = yh - tg[o];
-    if (rv && part == 0) {
+    if (rv) {
       if (yhat) yhat[gr * COUT + o] = yh;
       sse += (double)diff * diff;
     }
     dp[o] = rv ? 2.f * diff / count * yh * (1.f - yh) : 0.f;
   }
-  // per-row quantities into q-major scratch (row stride kScr: conflict-free both ways);
-  // the caller sums rows
+  float dt[CIN], dyv[CIN];
+#pragma unroll
+  for (int k = 0; k < CIN; ++k) {
+    float du = 0.f;
+#pragma unroll
+    for (int o = 0; o < COUT; ++o) du += dp[o] * wv[k][o];
+    dt[k] = du * lrelu_grad(yv[k] * gk[k] + bk[k]);
+    dyv[k] = dt[k] * gk[k];
+  }
+  if (rv) {
+#pragma unroll
+    for (int c = 0; c < CIN / 4; ++c) {
+      bf16x4 v;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[j] = (__bf16)dyv[4 * c + j];
+      *reinterpret_cast<bf16x4*>(dyp + 4 * c) = v;
+    }
+#pragma unroll
+    for (int k = (CIN / 4) * 4; k < CIN; ++k) dyp[k] = (__bf16)dyv[k];
+  }
+  // per-row quantities {dW, db, sum dt*y, sum dt, sum dy} and the squared error into
+  // q-major scratch (row stride kScr: conflict-free both ways); the caller sums rows
   float* sc = scr + orow;
+#pragma unroll
+  for (int k = 0; k < CIN; ++k)
+#pragma unroll
+    for (int o = 0; o < COUT; ++o) sc[(k * COUT + o) * kScr] = u[k] * dp[o];
+#pragma unroll
+  for (int o = 0; o < COUT; ++o) sc[(CIN * COUT + o) * kScr] = dp[o];
   constexpr int QB = CIN * COUT + COUT;
-  constexpr int NG = (CIN + 3) / 4;
 #pragma unroll
-  for (int g = 0; g < NG; ++g) {
-    if (g % HP != part) continue;
-    float dyv[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int k = 4 * g + j;
-      if (k >= CIN) break;
-      float du = 0.f;
-#pragma unroll
-      for (int o = 0; o < COUT; ++o) du += dp[o] * wv[k][o];
-      const float gk = hp[24 + k] * kBnC, bk = hp[24 + CIN + k];
-      const float dt = du * lrelu_grad(yv[k] * gk + bk);
-      dyv[j] = dt * gk;
-#pragma unroll
-      for (int o = 0; o < COUT; ++o) sc[(k * COUT + o) * kScr] = u[k] * dp[o];
-      sc[(QB + k) * kScr] = dt * yv[k];
-      sc[(QB + CIN + k) * kScr] = dt;
-      sc[(QB + 2 * CIN + k) * kScr] = dyv[j];
-    }
-    if (rv) {
-      if (4 * g + 4 <= CIN) {
-        bf16x4 v;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) v[j] = (__bf16)dyv[j];
-        *reinterpret_cast<bf16x4*>(dyp + 4 * g) = v;
-      } else {
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          if (4 * g + j < CIN) dyp[4 * g + j] = (__bf16)dyv[j];
-      }
-    }
+  for (int k = 0; k < CIN; ++k) {
+    sc[(QB + k) * kScr] = dt[k] * yv[k];
+    sc[(QB + CIN + k) * kScr] = dt[k];
+    sc[(QB + 2 * CIN + k) * kScr] = dyv[k];
   }
-  if (part == 0) {
-#pragma unroll
-    for (int o = 0; o < COUT; ++o) sc[(CIN * COUT + o) * kScr] = dp[o];
-    sscr[orow] = sse;
-  }
+  sscr[orow] = sse;
+  (void)hi; (void)gr;
 }
 
 // ------------------------------------------------------------------ forward
@@ -399,13 +388,12 @@ __global__ void __launch_bounds__(DT) dec_fwd_kernel(DecChainFwdArgs a) {
     else if (j >= 24 + cin && j < 24 + 2 * cin) v = be[j - 24 - cin];
     hp[hh][j] = v;
   }
-  constexpr int HP = head_parts<TR>();
   float tg[2] = {0.f, 0.f};
-  if (tid < 2 * TR * HP) {   // thread (row-head rh, part tid % HP): the head phase's mapping
-    const int rh = tid / HP, orow = rh % TR;
+  if (tid < 2 * TR) {
+    const int orow = tid % TR;
     const long long gr = tl.r0 + orow;
     if (orow < own) {
-      if (rh < TR) { tg[0] = a.s_truth[gr * 2]; tg[1] = a.s_truth[gr * 2 + 1]; }
+      if (tid < TR) { tg[0] = a.s_truth[gr * 2]; tg[1] = a.s_truth[gr * 2 + 1]; }
       else tg[0] = a.x_truth[gr];
     }
   }
@@ -539,11 +527,9 @@ __global__ void __launch_bounds__(DT) dec_fwd_kernel(DecChainFwdArgs a) {
   constexpr int NQS = head_nq(10, 2), NQN = head_nq(20, 1);
   float* scr = reinterpret_cast<float*>(smem + L.w);
   double* sscr = reinterpret_cast<double*>(smem + L.w + (NQS + NQN) * kScr * 4);
-  static_assert(2 * TR * HP <= DT, "dec_fwd: head threads");
   if (!(kdbg(a.dbg) & 2)) {
-    if (tid < 2 * TR * HP) {
-      const int part = tid % HP, rh = tid / HP;
-      const int hi = rh / TR, orow = rh % TR;
+    if (tid < 2 * TR) {
+      const int hi = tid / TR, orow = tid % TR;
       const bool rv = orow < own;
       const long long gr = tl.r0 + orow;
       if (hi == 0) {
@@ -551,7 +537,7 @@ __global__ void __launch_bounds__(DT) dec_fwd_kernel(DecChainFwdArgs a) {
 #pragma unroll
         for (int k = 0; k < 10; ++k) { u[k] = rv ? u3[orow * 16 + k] : 0.f; yv[k] = rv ? y3[orow * 16 + k] : 0.f; }
         const float t2[2] = {tg[0], tg[1]};
-        head_tile<10, 2, HP>(part, orow, rv, gr, u, yv, hp[0], t2, a.cnt_s, a.shat, a.dy3 + gr * a.lddy3, scr, sscr);
+        head_tile<10, 2>(0, orow, rv, gr, u, yv, hp[0], t2, a.cnt_s, a.shat, a.dy3 + gr * a.lddy3, scr, sscr);
       } else {
         float u[20], yv[20];
 #pragma unroll
@@ -561,15 +547,13 @@ __global__ void __launch_bounds__(DT) dec_fwd_kernel(DecChainFwdArgs a) {
           yv[k] = rv ? y2n[orow * L.ldY2n + k] : 0.f;
         }
         const float t1[1] = {tg[0]};
-        head_tile<20, 1, HP>(part, orow, rv, gr, u, yv, hp[1], t1, a.cnt_n, a.xhat, a.dy2 + gr * a.lddy2 + a.m2.offb,
+        head_tile<20, 1>(1, orow, rv, gr, u, yv, hp[1], t1, a.cnt_n, a.xhat, a.dy2 + gr * a.lddy2 + a.m2.offb,
                          scr + NQS * kScr, sscr + TR);
       }
     }
     __syncthreads();
     if (stamp) ts[7] = __builtin_amdgcn_s_memrealtime();
-    // tile partials: each quantity summed over the TR rows in order (4 lanes per quantity,
-    // (l0 + l1) + (l2 + l3), measured 0.9 us slower at 128-row tiles: their scratch reads
-    // collide in the LDS banks; round 6)
+    // tile partials: each quantity summed over the TR rows in order
     if (tid < NQS + NQN) {
       const float* src = scr + tid * kScr;
       float v = 0.f;
