@@ -1846,6 +1846,9 @@ extern "C" int snd_train_step(const snd_plan_t* plan, const snd_batch_t* batch,
     }
     // the column-split sum is folded into head_bwd / reparam_bwd_fast (node latent, fast encoder)
     SND_TRY(launch_zzt_dense(za, c.dtype, x.s, p.fast_enc && !p.tref));
+    // measurement only (debug bit 1 << 17): the same zz^T launch again (it recomputes the
+    // same partials), so a kernel trace shows a warm in-step launch beside the first one
+    if (debug_flags() & (1 << 17)) SND_TRY(launch_zzt_dense(za, c.dtype, x.s, p.fast_enc && !p.tref));
     if (cdec) SND_TRY(join_from(x, p.side));
   }
   if (p.fast) {
