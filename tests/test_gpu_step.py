@@ -574,6 +574,30 @@ def test_fused_encoder_front_matches_chain(topology, n, d, B):
         assert np.array_equal(g0[k], g1[k]), k
 
 
+@pytest.mark.parametrize("n,B", [(4096, 8), (1000, 3)])
+def test_step_window_rings_bitwise(n, B):
+    """The step with the deep-ring window plan (the default when beta fits, 1024 rows)
+    and with the 1096-row ring: the same sums in the same order -- every gradient and
+    loss term bitwise equal."""
+    from snd_vae_amd.model import DeviceBatch
+    from snd_vae_amd.params import init_blocks
+    cfg = tscale(n, 64)
+    batch = synthetic_batch(cfg, B, seed=22)
+    p0 = init_blocks(cfg, 1)
+    runs = []
+    for ring in (None, 1096):
+        m, o, _ = make(cfg, batch, p0, "bf16")
+        b = DeviceBatch(batch, window_ring=ring)
+        assert b.window is not None and b.window[5] == (ring or 1024)
+        o.forward_backward(b)
+        torch.cuda.synchronize()
+        runs.append((o.losses.cpu().numpy().copy(), o.grad_blocks()))
+    (l0, g0), (l1, g1) = runs
+    np.testing.assert_array_equal(l1, l0)
+    for k in g0:
+        np.testing.assert_array_equal(g1[k], g0[k], err_msg=k)
+
+
 @pytest.mark.parametrize("n,B", [(4096, 8), (4096, 1), (1000, 3)])
 def test_step_window_spmm_matches_row_tiles(n, B):
     """The step's GraphConvolution backward SpMM A @ dP1 on the window kernel (the batch
