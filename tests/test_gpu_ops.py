@@ -153,9 +153,11 @@ def test_spmm_bf16_window_bitwise(n, B, kbar, seed):
     hb = torch.from_numpy(np.random.default_rng(seed).standard_normal((n * B, 64)).astype(np.float32)).to(torch.bfloat16)
     d_rp, d_ci = cu(rp, torch.int32), cu(ci if len(ci) else np.zeros(1, np.int32), torch.int32)
     ref = layers.spmm_bf16(d_rp, d_ci, hb.cuda(), n, B, cu(order, torch.int32))
-    for ring in (1096, 1024):
+    for ring, bound in ((1096, 352), (1024, 312)):
         wp = window_plan(gb, order, ring)
-        assert (wp.beta + 7) // 8 * 8 <= 312            # every case fits both rings
+        assert (wp.beta + 7) // 8 * 8 <= 352
+        if (wp.beta + 7) // 8 * 8 > bound:              # 64 graphs: beta 331, the 1096 ring only
+            continue
         if kbar >= 40:
             assert wp.max_degree > 32
         out = layers.spmm_bf16_window(layers.DeviceWindowPlan(wp), hb.cuda(), n, B)

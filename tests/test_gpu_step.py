@@ -392,7 +392,7 @@ DEC_BUFS = (("FY1", torch.float32), ("FU1", torch.bfloat16), ("FY2", torch.float
 
 
 @pytest.mark.parametrize("topology,n,d,B", [("tscale", 512, 64, 2), ("tscale", 200, 16, 3),
-                                            ("tref", 300, 32, 2)])
+                                            ("tref", 300, 32, 2), ("tscale", 4096, 64, 4)])
 def test_fused_decoder_matches_row_engine(topology, n, d, B):
     """The fused decoder (snd_dec.hip: conv chain + heads in one launch, the
     backward data chain in another, halos recomputed in LDS) against the row
@@ -400,7 +400,9 @@ def test_fused_decoder_matches_row_engine(topology, n, d, B):
     and head output is bitwise equal; the parameter gradients built from
     column partials (biases, BN, heads) agree to fp32 reassociation, and the
     conv weight gradients (same operands) are bitwise equal.  Covers partial
-    tiles (N = 200, 300: 128-row tiles never span graphs) and the graph latent."""
+    tiles (N = 200, 300: 128-row tiles never span graphs) and the graph latent.  N = 4096,
+    B = 4 (128 tiles of 128 rows: the chip is full) runs the dual kernels: 64-row tiles on
+    8 waves with the conv weights streamed through LDS tap by tap, two per CU."""
     from snd_vae_amd import _lib
     from snd_vae_amd.params import init_blocks
     cfg = tscale(n, d) if topology == "tscale" else tref(n, d, g_hidden=16, latent=8)
