@@ -272,7 +272,8 @@ __device__ __forceinline__ void conv_phase(const __bf16* xs, int kpx, const __bf
 // into the buffer tap t - 1 used, and runs tap t over ALL the wave's row blocks (their
 // accumulators live across the taps).  Per output the MFMA order is conv_phase_t's (taps
 // outer, k chunks inner): bitwise the same sums.  Every wave reaches every barrier.
-// MAXRB: the most row blocks a wave owns (checked on the host, dec_dual_supported).
+// MAXRB: the most row blocks a wave owns (checked on the host, dec_dual_fits_*); KCS: the
+// k chunks per tap the call site expects (unrolled when kp == 32 KCS, a runtime loop else).
 template <int NBH, int KCS, int NWV, int MAXRB, class Pre, class Epi>
 __device__ __forceinline__ void conv_phase_str(const __bf16* xs, int kpx, const DecImg& im, char* wb0, char* wb1,
                                                int g0, const DecImg* next, int n_out, Pre&& pre, Epi&& epi,
@@ -324,11 +325,11 @@ __device__ __forceinline__ void conv_phase_str(const __bf16* xs, int kpx, const 
             acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aw, bx, acc[j][i], 0, 0, 0);
           }
         };
-        if constexpr (KCS == 0) {
-          for (int ks = 0; ks < (kpw >> 5); ++ks) chunk(ks);
-        } else {
+        if (KCS > 0 && kpw == 32 * KCS) {   // the call site's expected width: unrolled
 #pragma unroll
           for (int ks = 0; ks < KCS; ++ks) chunk(ks);
+        } else {
+          for (int ks = 0; ks < (kpw >> 5); ++ks) chunk(ks);
         }
       }
     }
