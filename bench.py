@@ -394,16 +394,16 @@ def spmm_batched(host, width, copies, reps):
            "frac": frac(ms_reg)}
     # headline: the sliding-window kernel (h rows DMA'd once into an LDS ring) when the
     # schedule's bandwidth fits its ring, else the row-tile kernel
-    from snd_vae_amd.data import window_plan_auto
+    from snd_vae_amd.data import window_plan
     from snd_vae_amd.layers import DeviceWindowPlan
-    wp = window_plan_auto(big, order.astype(np.int32))      # the ring the step's DeviceBatch picks
-    if wp is not None and width == 64:
+    wp = window_plan(big, order.astype(np.int32))
+    if (wp.beta + 7) // 8 * 8 <= 352 and width == 64:
         dw = DeviceWindowPlan(wp)
-        ms = time_launches(lambda sp: _lib.check(L.snd_csr_spmm_bf16_window_ring(
+        ms = time_launches(lambda sp: _lib.check(L.snd_csr_spmm_bf16_window(
             dw.meta.data_ptr(), dw.slots.data_ptr(), dw.rows.data_ptr(), dw.order.data_ptr(), R, host.n_nodes, ng, wp.beta,
-            h.data_ptr(), width, width, out.data_ptr(), width, wp.ring, sp)), reps)
+            h.data_ptr(), width, width, out.data_ptr(), width, sp)), reps)
         kern = (f"csr_spmm_bf16_window (A @ H, width {width}, {ng} graphs block-diagonal, {len(ci)} nnz, "
-                f"RCM schedule, beta {wp.beta}, {wp.ring}-row LDS ring; the kernel snd_train_step launches "
+                f"RCM schedule, beta {wp.beta}, 1096-row LDS ring; the kernel snd_train_step launches "
                 f"for the GraphConvolution backward A @ dP1)")
         prev = dict(tiled, previous_variant=reg)
     else:

@@ -38,7 +38,7 @@ enum { SND_F32 = 0, SND_BF16 = 1 }; /* MFMA operand dtype; accumulation always f
 
 const char* snd_last_error(void);
 /* the ABI this header describes; snd_abi_version() returns it */
-#define SND_ABI_VERSION 18
+#define SND_ABI_VERSION 17
 int snd_abi_version(void);
 
 /* ---- a1: adjacency ingest ------------------------------------------------
@@ -150,16 +150,6 @@ int snd_csr_spmm_bf16_window(const int* meta, const uint16_t* slots, const int* 
                              int n_rows, int n_per_graph, int n_graphs, int beta,
                              const void* h, int ldh, int width, void* out, int ldo,
                              snd_stream_t stream);
-/* snd_csr_spmm_bf16_window with the ring size the plan was built for (ABI 18):
- * ring 1096 is snd_csr_spmm_bf16_window; ring 1024 ("deep") DMAs slot lists two
- * steps ahead instead of one and needs ceil8(beta) <= 312 (SND_ERR_ARG above).
- * Plan slots are neighbour position % ring, padded with slot ring.  Same sums,
- * same order: bitwise equal results. */
-int snd_csr_spmm_bf16_window_ring(const int* meta, const uint16_t* slots, const int* rows,
-                                  const int* order,
-                                  int n_rows, int n_per_graph, int n_graphs, int beta,
-                                  const void* h, int ldh, int width, void* out, int ldo,
-                                  int ring, snd_stream_t stream);
 /* ---- a5: linear / dense GEMM on MFMA ---------------------------------------
  * Replaces linear() (layers.py:566-576) and the X@w of GraphConvolution
  * (layers.py:120-121; the tile() copy is not needed):
@@ -443,7 +433,6 @@ typedef struct snd_window_plan {
   const int* rows;              /* [n_rows] */
   const int* order;             /* [n_rows] */
   int beta;
-  int ring;                     /* ring rows the slots address: 1096 (0 = 1096) or 1024 (ABI 18) */
 } snd_window_plan_t;
 
 typedef struct snd_batch {

@@ -17,7 +17,7 @@ c_int, c_ll, c_float, c_size, c_ull = C.c_int, C.c_longlong, C.c_float, C.c_size
 vp = C.c_void_p
 
 
-ABI_VERSION = 18
+ABI_VERSION = 17
 GEN_MODES = {"sample": 0, "mean": 1, "prior": 2, "given": 3}
 TOPOLOGY = {"tscale": 0, "tref": 1, "sgjoint": 2}
 
@@ -51,8 +51,7 @@ class RowTiles(C.Structure):
 
 class WindowPlan(C.Structure):
     """snd_window_plan_t"""
-    _fields_ = [("meta", vp), ("slots", vp), ("rows", vp), ("order", vp), ("beta", c_int),
-                ("ring", c_int)]
+    _fields_ = [("meta", vp), ("slots", vp), ("rows", vp), ("order", vp), ("beta", c_int)]
 
 
 class Batch(C.Structure):
@@ -83,8 +82,6 @@ _SIGS = {
                                         c_int, c_int, c_int, vp, vp]),
     "snd_csr_spmm_bf16_window": (c_int, [vp, vp, vp, vp, c_int, c_int, c_int, c_int, vp, c_int, c_int,
                                          vp, c_int, vp]),
-    "snd_csr_spmm_bf16_window_ring": (c_int, [vp, vp, vp, vp, c_int, c_int, c_int, c_int, vp, c_int,
-                                              c_int, vp, c_int, c_int, vp]),
     "snd_gemm": (c_int, [c_int, c_int, c_int, c_int, c_int, vp, c_int, vp, c_int, vp, c_int,
                          vp, c_int, vp]),
     "snd_conv1d_same_fwd": (c_int, [vp, c_int, c_int, c_int, c_int, vp, c_int, vp, vp, vp,

@@ -24,12 +24,6 @@ constexpr int kDecRowsTiny = SND_DEC_TINY_ROWS;
 #endif
 constexpr int kDecTiny = SND_DEC_TINY;
 
-// 64-row "dual" tiles (8 waves, conv weights streamed by tap, two workgroups per CU) where
-// 128-row tiles would fill the chip (snd_dec.hip; -DSND_DEC_DUAL=0: the 128-row tiles, A/B)
-#ifndef SND_DEC_DUAL
-#define SND_DEC_DUAL 1
-#endif
-
 // Packed weight image in the workspace (pack_kernel layout [tap][n][k], T = 5)
 struct DecImg { const __bf16* w; int kp, np; };
 

@@ -34,10 +34,7 @@ struct SpmmWinArgs {
   int n_rows, n_per_graph, n_graphs;
   const void* h; int ldh; int width;
   void* out; int ldo;
-  int ring;              // LDS ring rows the plan's slots address: 1096 (0 = 1096) or 1024
 };
 int launch_spmm_window(const SpmmWinArgs& w, hipStream_t s);
 int spmm_win_max_beta();
-int spmm_win_deep_ring();
-int spmm_win_deep_max_beta();
 }  // namespace snd

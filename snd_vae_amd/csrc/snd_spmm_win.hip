@@ -63,30 +63,13 @@ namespace {
 // alternating processes: GK 2 / 4 / 8 = 88.7-90.4 / 85.1-87.6 / 87.4-91.7 us)
 constexpr int kWinGK = 4;
 constexpr int WT = 1024;       // threads: 16 waves x 8 rows
+constexpr int RR = 1096;       // ring rows
 constexpr int STEP = 128;      // rows per step
 constexpr int WIDTH = 64;      // bf16 columns (128-byte rows)
-
-// LDS geometry of the two rings (plan.ring; the plan's slots are positions mod RR, its
-// list padding the zero row's slot RR):
-//   1096 rows: index DMA'd 3 steps ahead (4 blocks), slot lists 1 step ahead (2 buffers);
-//              any beta8 <= 352 (two barriers per step above 288)
-//   1024 rows ("deep", round 6): index 4 steps ahead (5 blocks), slot lists 2 steps ahead
-//              (3 buffers): a step waits only for what was issued two steps earlier, so
-//              one HBM round trip of slot lists is no longer exposed per step; one barrier
-//              per step, beta8 <= 312 (2 beta8 + 398 <= 1024: the piece e(s) lands at
-//              positions <= p + 390 + beta8 while step s still reads p - beta8)
-template <bool DEEP> struct WinGeo {
-  static constexpr int RR = DEEP ? 1024 : 1096;       // ring rows
-  static constexpr int NIDX = DEEP ? 5 : 4;           // 16 waves x 96 B index blocks
-  static constexpr int NSL = DEEP ? 3 : 2;            // 16 waves x 512 B slot-list buffers
-  static constexpr int IA = DEEP ? 4 : 3;             // index DMA'd IA steps ahead
-  static constexpr int SA = DEEP ? 2 : 1;             // slot lists SA steps ahead
-  static constexpr int OFF_IDX = (RR + 2) * WIDTH * 2;
-  static constexpr int OFF_SL = OFF_IDX + NIDX * 16 * 96;
-  static constexpr int LDS_BYTES = OFF_SL + NSL * 16 * 512;
-};
-static_assert(WinGeo<false>::LDS_BYTES <= 163840 && WinGeo<true>::LDS_BYTES <= 163840, "spmm_win: LDS");
-constexpr int kDeepRing = 1024, kDeepMaxBeta8 = 312;
+constexpr int ZROW = RR;       // the zero rows' slots: RR (even) and RR + 1 (odd, pair plans)
+constexpr int OFF_IDX = (RR + 2) * WIDTH * 2;       // 4 x 1536 B index blocks
+constexpr int OFF_SL = OFF_IDX + 4 * 16 * 96;       // 2 x 8192 B slot-list buffers
+constexpr int LDS_BYTES = OFF_SL + 2 * 16 * 512;
 
 typedef __attribute__((address_space(3))) void* lptr_t;
 
@@ -160,13 +143,11 @@ __device__ __forceinline__ void raw_barrier() {
   asm volatile("" ::: "memory");
 }
 
-template <int GK, bool MEAS, bool DEEP>
+template <int GK, bool MEAS>
 __global__ void __launch_bounds__(WT) spmm_win_kernel(WinArgs a) {
-  using G = WinGeo<DEEP>;
-  constexpr int RR = G::RR, OFF_IDX = G::OFF_IDX, OFF_SL = G::OFF_SL;
   // the phase-skip bits exist in the measurement instantiation only
   const int skip = MEAS ? (a.dbg & 7) : 0;
-  __shared__ __attribute__((aligned(16))) char lds[G::LDS_BYTES];
+  __shared__ __attribute__((aligned(16))) char lds[LDS_BYTES];
   const unsigned lds0 = (unsigned)(uintptr_t)(lptr_t)lds;   // LDS byte address of lds[0]
   const int g = blockIdx.x / a.spg, sg = blockIdx.x - g * a.spg;
   const int gb = g * a.n;                         // graph's first global position / row
@@ -188,8 +169,8 @@ __global__ void __launch_bounds__(WT) spmm_win_kernel(WinArgs a) {
   // first position of the 8-row piece this wave DMAs at step s (8-aligned; past the
   // window end it lands in dead ring rows)
   auto dpiece = [&](int s) { return ((hi(s + 1) + 8) & ~7) + 8 * w; };
-  auto idx_blk = [&](int s) { return OFF_IDX + (s % G::NIDX) * (16 * 96) + 96 * w; };
-  auto sl_buf = [&](int s) { return OFF_SL + (s % G::NSL) * (16 * 512) + 512 * w; };
+  auto idx_blk = [&](int s) { return OFF_IDX + (s & 3) * (16 * 96) + 96 * w; };
+  auto sl_buf = [&](int s) { return OFF_SL + (s & 1) * (16 * 512) + 512 * w; };
 
   // c: index(s) -> lanes 0-7 meta, 8-15 row id, 16-23 row id of the window piece of step s
   auto dma_index = [&](int s) {
@@ -219,11 +200,12 @@ __global__ void __launch_bounds__(WT) spmm_win_kernel(WinArgs a) {
   };
   auto lds_i32 = [&](int off) { return *reinterpret_cast<const int*>(lds + off); };
 
-  // ---- prologue: zero row, index(0 .. IA-1), slots(0 .. SA-1), window [Q0, hi(1)]
+  // ---- prologue: zero row, index(0..2), slots(0), window [Q0, hi(1)]
   if (tid < 2 * WIDTH * 2 / 16)
     reinterpret_cast<uint4*>(lds + RR * WIDTH * 2)[tid] = make_uint4(0u, 0u, 0u, 0u);
-#pragma unroll
-  for (int k = 0; k < G::IA; ++k) dma_index(k);
+  dma_index(0);
+  dma_index(1);
+  dma_index(2);
   {
     const int np = (hi(1) - Q0) / 8 + 1;          // window pieces
     for (int j = w; j < np; j += WT / 64) {
@@ -233,32 +215,29 @@ __global__ void __launch_bounds__(WT) spmm_win_kernel(WinArgs a) {
   }
   __builtin_amdgcn_s_waitcnt(0);
   __syncthreads();
-#pragma unroll
-  for (int k = 0; k < G::SA; ++k) dma_slots(k, lds_i32(idx_blk(k) + 4 * (lane >> 2)) >> 6);
+  dma_slots(0, lds_i32(idx_blk(0) + 4 * (lane >> 2)) >> 6);
   __builtin_amdgcn_s_waitcnt(0);
   __syncthreads();
 
   const unsigned base = (unsigned)(l8 * 16);
   // b-e: the step's reads of index(s) / index(s+1) and its DMAs
   auto issue = [&](int s) {
-    const int st1 = lds_i32(idx_blk(s + G::SA) + 4 * (lane >> 2)) >> 6;
+    const int st1 = lds_i32(idx_blk(s + 1) + 4 * (lane >> 2)) >> 6;
     const int prow = lds_i32(idx_blk(s) + 64 + 4 * r8);
-    dma_index(s + G::IA);
-    if (!(skip & 4)) dma_slots(s + G::SA, st1);
+    dma_index(s + 3);
+    if (!(skip & 4)) dma_slots(s + 1, st1);
     if (!(skip & 2)) dma_piece(dpiece(s), prow);
   };
   // One barrier per step when the window leaves room: the DMAs of step s are issued
   // after its barrier (every wave has finished step s-1, the last reader of the
   // index block, slot buffer and ring rows they overwrite; the ring rows e(s)
   // overwrites lie below every position step s reads while 2 beta8 < 592).
-  const bool one = DEEP || (a.beta8 <= 288 && !(a.dbg & 32));
+  const bool one = a.beta8 <= 288 && !(a.dbg & 32);
   for (int s = 0; s < nsteps; ++s) {
     if (one) {
-      // 1096 ring: slots(s) (d of step s-1, followed by e(s-1) and the store of s-1) and
-      // every older DMA are in.  Deep ring: e(s-2) -- the window piece step s reads, issued
-      // after slots(s) and index(s+2) -- is in; the store of s-2 and c/d/e/store of s-1
-      // may still fly
-      __builtin_amdgcn_s_waitcnt(vmcnt_imm(DEEP ? 5 : 2));
+      // slots(s) (d of step s-1, followed by e(s-1) and the store of s-1) and every
+      // older DMA are in
+      __builtin_amdgcn_s_waitcnt(vmcnt_imm(2));
       raw_barrier();
       issue(s);
     } else {
@@ -323,8 +302,6 @@ __global__ void __launch_bounds__(WT) spmm_win_kernel(WinArgs a) {
 }  // namespace
 
 int spmm_win_max_beta() { return 352; }   // 8-aligned, 2 beta < RR - 3 STEP (712)
-int spmm_win_deep_ring() { return kDeepRing; }
-int spmm_win_deep_max_beta() { return kDeepMaxBeta8; }
 
 }  // namespace snd
 
@@ -339,12 +316,8 @@ int launch_spmm_window(const SpmmWinArgs& w, hipStream_t st) {
   SND_CHECK_ARG(w.ldh % 8 == 0 && w.ldo % 8 == 0 && w.ldh >= w.width && w.ldo >= w.width,
                 "snd_csr_spmm_bf16_window: ldh / ldo must be multiples of 8 >= width");
   const int beta8 = (w.beta + 7) & ~7;
-  const int ring = w.ring ? w.ring : 1096;
-  SND_CHECK_ARG(ring == 1096 || ring == kDeepRing, "snd_csr_spmm_bf16_window: ring %d (1096 or %d)", ring, kDeepRing);
-  const bool deep = ring == kDeepRing;
-  const int maxb = deep ? kDeepMaxBeta8 : spmm_win_max_beta();
-  SND_CHECK_ARG(w.beta >= 0 && beta8 <= maxb && (long long)w.n_rows < (1LL << 31),
-                "snd_csr_spmm_bf16_window: beta %d exceeds the %d-row ring (<= %d)", w.beta, ring, maxb);
+  SND_CHECK_ARG(w.beta >= 0 && beta8 <= spmm_win_max_beta() && (long long)w.n_rows < (1LL << 31),
+                "snd_csr_spmm_bf16_window: beta %d exceeds the ring (<= %d)", w.beta, spmm_win_max_beta());
   // segments: about 256 workgroups in all, at least one step each
   const int steps = cdiv(w.n_per_graph, STEP);
   const int spg = std::max(1, std::min(steps, cdiv(256, w.n_graphs)));
@@ -352,14 +325,8 @@ int launch_spmm_window(const SpmmWinArgs& w, hipStream_t st) {
   WinArgs a{w.meta, w.slots, w.rows, w.order, reinterpret_cast<const __bf16*>(w.h), w.ldh,
             reinterpret_cast<__bf16*>(w.out), w.ldo, w.n_per_graph, cdiv(w.n_per_graph, seg), seg, beta8,
             debug_flags() >> 24};
-  const dim3 grid(w.n_graphs * a.spg);
-  if (deep) {
-    if (a.dbg & 7) hipLaunchKernelGGL((spmm_win_kernel<kWinGK, true, true>), grid, dim3(WT), 0, st, a);
-    else hipLaunchKernelGGL((spmm_win_kernel<kWinGK, false, true>), grid, dim3(WT), 0, st, a);
-  } else {
-    if (a.dbg & 7) hipLaunchKernelGGL((spmm_win_kernel<kWinGK, true, false>), grid, dim3(WT), 0, st, a);
-    else hipLaunchKernelGGL((spmm_win_kernel<kWinGK, false, false>), grid, dim3(WT), 0, st, a);
-  }
+  if (a.dbg & 7) hipLaunchKernelGGL((spmm_win_kernel<kWinGK, true>), dim3(w.n_graphs * a.spg), dim3(WT), 0, st, a);
+  else hipLaunchKernelGGL((spmm_win_kernel<kWinGK, false>), dim3(w.n_graphs * a.spg), dim3(WT), 0, st, a);
   SND_LAUNCH_CHECK("spmm_win_kernel");
   return 0;
 }
@@ -370,15 +337,6 @@ extern "C" int snd_csr_spmm_bf16_window(const int* meta, const uint16_t* slots, 
                                         int n_rows, int n_per_graph, int n_graphs, int beta,
                                         const void* h, int ldh, int width, void* out, int ldo,
                                         snd_stream_t stream) {
-  SpmmWinArgs w{meta, slots, rows, order, beta, n_rows, n_per_graph, n_graphs, h, ldh, width, out, ldo, 1096};
-  return launch_spmm_window(w, (hipStream_t)stream);
-}
-
-extern "C" int snd_csr_spmm_bf16_window_ring(const int* meta, const uint16_t* slots, const int* rows,
-                                             const int* order,
-                                             int n_rows, int n_per_graph, int n_graphs, int beta,
-                                             const void* h, int ldh, int width, void* out, int ldo,
-                                             int ring, snd_stream_t stream) {
-  SpmmWinArgs w{meta, slots, rows, order, beta, n_rows, n_per_graph, n_graphs, h, ldh, width, out, ldo, ring};
+  SpmmWinArgs w{meta, slots, rows, order, beta, n_rows, n_per_graph, n_graphs, h, ldh, width, out, ldo};
   return launch_spmm_window(w, (hipStream_t)stream);
 }

@@ -970,10 +970,9 @@ static void use_tiles(SpmmBfArgs& a, const snd_batch_t* batch, int npg, int ngra
 static int spmm_bf16_plain(const snd_batch_t* batch, int R, int npg, int ngraphs, const __bf16* h,
                            int ldh, int width, __bf16* out, int ldo, hipStream_t s) {
   const snd_window_plan_t& w = batch->window;
-  const int wmax = w.ring == spmm_win_deep_ring() ? spmm_win_deep_max_beta() : spmm_win_max_beta();
-  if (w.meta && width == 64 && w.beta >= 0 && ((w.beta + 7) & ~7) <= wmax &&
+  if (w.meta && width == 64 && w.beta >= 0 && ((w.beta + 7) & ~7) <= spmm_win_max_beta() &&
       !(debug_flags() & (1 << 22))) {   // debug bit 1 << 22: the row tiles (A/B)
-    SpmmWinArgs a{w.meta, w.slots, w.rows, w.order, w.beta, R, npg, ngraphs, h, ldh, width, out, ldo, w.ring};
+    SpmmWinArgs a{w.meta, w.slots, w.rows, w.order, w.beta, R, npg, ngraphs, h, ldh, width, out, ldo};
     return launch_spmm_window(a, s);
   }
   SpmmBfArgs a{batch->rowptr, batch->colidx, R, h, ldh, width, SND_SPMM_PLAIN, out, ldo};

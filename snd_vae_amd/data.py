@@ -316,29 +316,6 @@ class WindowPlan(NamedTuple):
     order: np.ndarray    # int32 [R]: the row at each position (the schedule)
     beta: int            # largest |position(neighbour) - position(row)|
     max_degree: int
-    ring: int = 1096     # LDS ring rows the slots address (1096, or 1024: the deep-prefetch kernel)
-
-
-# the window kernel's two rings (snd_spmm_win.hip WinGeo): ring rows -> largest ceil8(beta)
-WINDOW_RINGS = {1096: 352, 1024: 312}
-
-
-def window_plan_auto(batch: GraphBatch, order: np.ndarray, ring: Optional[int] = None) -> Optional[WindowPlan]:
-    """window_plan for the kernel variant the schedule's bandwidth allows: the deep
-    (1024-row) ring when ceil8(beta) <= 312, else the 1096-row ring; None when beta
-    exceeds both or a degree exceeds the metadata field.  ``ring`` forces one ring
-    (None if beta does not fit it)."""
-    rings = [ring] if ring else [1024, 1096]
-    for rr in rings:
-        if rr not in WINDOW_RINGS:
-            raise ValueError(f"window_plan_auto: ring {rr} (one of {sorted(WINDOW_RINGS)})")
-        try:
-            wp = window_plan(batch, order, rr)
-        except ValueError:            # a degree past the plan's 6-bit field
-            return None
-        if (wp.beta + 7) // 8 * 8 <= WINDOW_RINGS[rr]:
-            return wp
-    return None
 
 
 def window_plan(batch: GraphBatch, order: np.ndarray, ring: int = 1096) -> WindowPlan:
@@ -397,7 +374,7 @@ def window_plan(batch: GraphBatch, order: np.ndarray, ring: int = 1096) -> Windo
         slots[np.repeat(start[:-1], deg) + run] = (npos % ring).astype(np.uint16)
     meta = ((start[:-1] // 8) << 6 | deg).astype(np.int32)
     return WindowPlan(meta[srt], slots, order[srt].astype(np.int32), order.astype(np.int32), beta,
-                      int(deg.max()) if deg.size else 0, ring)
+                      int(deg.max()) if deg.size else 0)
 
 
 def shard(batch: GraphBatch, rank: int, world: int) -> GraphBatch:

@@ -107,21 +107,20 @@ class DeviceWindowPlan:
         self.rows = torch.from_numpy(plan.rows).to(device)
         self.order = torch.from_numpy(plan.order).to(device)
         self.beta = plan.beta
-        self.ring = plan.ring
 
 
 def spmm_bf16_window(wplan, h, n_per_graph, n_graphs):
-    """spmm_bf16 streamed through an LDS window (snd_csr_spmm_bf16_window_ring; plan:
-    data.window_plan / window_plan_auto, either ring): bit-identical to spmm_bf16 on every tested batch.
+    """spmm_bf16 streamed through an LDS window (snd_csr_spmm_bf16_window; plan:
+    data.window_plan): bit-identical to spmm_bf16 on every tested batch.
     wplan: DeviceWindowPlan."""
     if not (h.is_cuda and h.is_contiguous() and h.dtype == torch.bfloat16):
         raise ValueError("spmm_bf16_window: expected a contiguous bfloat16 device tensor")
     rows, width = h.shape
     out = torch.empty_like(h)
     L = _lib.lib()
-    fn, name = L.snd_csr_spmm_bf16_window_ring, "snd_csr_spmm_bf16_window_ring"
+    fn, name = L.snd_csr_spmm_bf16_window, "snd_csr_spmm_bf16_window"
     _lib.check(fn(_P(wplan.meta), _P(wplan.slots), _P(wplan.rows), _P(wplan.order), rows, n_per_graph, n_graphs,
-                  wplan.beta, _P(h), width, width, _P(out), width, wplan.ring, _lib.stream_ptr()), name)
+                  wplan.beta, _P(h), width, width, _P(out), width, _lib.stream_ptr()), name)
     return out
 
 

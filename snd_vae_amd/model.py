@@ -24,11 +24,12 @@ import torch
 
 from . import _lib
 from .config import SNDConfig
-from .data import GraphBatch, SGBatch, locality_order, row_tiles, window_plan_auto
+from .data import GraphBatch, SGBatch, locality_order, row_tiles, window_plan
 from .params import flat_layout, init_blocks
 
 DTYPES = {"f32": 0, "fp32": 0, "bf16": 1}
 TAIL = 64  # floats after the parameters in the gradient buffer (loss terms for the all-reduce)
+WINDOW_MAX_BETA = 352  # the window SpMM's ring bound (spmm_win_max_beta)
 
 
 def c_config(cfg: SNDConfig, dtype: str) -> _lib.Config:
@@ -64,15 +65,13 @@ class DeviceBatch:
     """A GraphBatch resident in HBM (the feed dict of `main.py:327-329`)."""
 
     def __init__(self, batch: GraphBatch, device="cuda", locality: bool = True, tile_rows: int = 64,
-                 window: bool = True, window_ring: Optional[int] = None):
+                 window: bool = True):
         """locality: upload the per-graph RCM row schedule of the gather kernels
         (data.locality_order); results do not depend on it.  tile_rows > 0 (with
         locality) also uploads the SpMM row tiles over that schedule
         (data.row_tiles, data.default_tile_rows); bit-identical results.  window
         (with locality): the window SpMM's plan over the schedule (data.window_plan),
-        used by the step's width-64 backward SpMM when its beta fits the ring
-        (data.window_plan_auto: the deep 1024-row ring when beta allows; window_ring
-        forces one)."""
+        used by the step's width-64 backward SpMM when its beta fits the ring."""
         t = lambda a, dt: torch.from_numpy(np.ascontiguousarray(a)).to(device=device, dtype=dt)
         self.sg = isinstance(batch, SGBatch)
         if self.sg:   # spatial-graph encoder: its trees and rel; the gather schedules do not apply
@@ -100,19 +99,20 @@ class DeviceBatch:
             self.tiles = DeviceTiles(row_tiles(batch, order, tile_rows), device)
         self.window = None
         if order is not None and window:
-            wp = window_plan_auto(batch, order, window_ring)
-            if wp is not None:
+            try:
+                wp = window_plan(batch, order)
+            except ValueError:        # a degree past the plan's 6-bit field: no window plan
+                wp = None
+            if wp is not None and (wp.beta + 7) // 8 * 8 <= WINDOW_MAX_BETA:
                 t8 = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(device)
-                self.window = (t8(wp.meta), t8(wp.slots.view(np.int16)), t8(wp.rows), t8(wp.order), wp.beta,
-                               wp.ring)
+                self.window = (t8(wp.meta), t8(wp.slots.view(np.int16)), t8(wp.rows), t8(wp.order), wp.beta)
         self.host = batch
 
     def c_struct(self) -> _lib.Batch:
         p = _lib.ptr
         tl = self.tiles.c_struct() if self.tiles else _lib.RowTiles()
         w = self.window
-        wp = (_lib.WindowPlan(p(w[0]), p(w[1]), p(w[2]), p(w[3]), w[4], w[5]) if w
-              else _lib.WindowPlan(None, None, None, None, -1, 0))
+        wp = _lib.WindowPlan(p(w[0]), p(w[1]), p(w[2]), p(w[3]), w[4]) if w else _lib.WindowPlan(None, None, None, None, -1)
         sg = (p(self.tree_rowptr), p(self.tree_colidx), p(self.rel)) if self.sg else (None, None, None)
         return _lib.Batch(p(self.rowptr), p(self.colidx), p(self.features),
                           p(self.feature_truth), p(self.spatial_truth), p(self.row_order), tl, wp, *sg)

@@ -137,44 +137,40 @@ def test_spmm_bf16_tiled_bitwise(n, B, kbar, width, tile_rows, locality):
                                              (1000, 3, 16.0, 4), (300, 3, 10.0, 5), (96, 2, 0.0, 6),
                                              (256, 4, 40.0, 7), (200, 1, 50.0, 8), (130, 5, 3.0, 2)])
 def test_spmm_bf16_window_bitwise(n, B, kbar, seed):
-    """The sliding-window SpMM (h rows DMA'd once into an LDS ring, two 128-row steps
-    ahead) sums every row's neighbours in colidx order: bitwise equal to spmm_bf16, on
-    both rings (1096 rows, slot lists one step ahead; 1024 rows, two steps ahead).
-    64 graphs: one workgroup per graph, 32 steps; 8 graphs: 32 one-step segments per
-    graph; n = 1000 / 130: partial last steps; kbar 40 / 50: rows past 32 neighbours;
-    kbar 0: empty rows.  N = 4096 (beta ~ 260): one barrier per step, and (forced) the
-    1096 ring's two-barrier step of wider windows."""
-    from snd_vae_amd import _lib, layers
+    """The sliding-window SpMM (h rows DMA'd once into a 1096-row LDS ring, two
+    128-row steps ahead) sums every row's neighbours in colidx order: bitwise equal
+    to spmm_bf16.  64 graphs: one workgroup per graph, 32 steps; 8 graphs: 32
+    one-step segments per graph; n = 1000 / 130: partial last steps; kbar 40 / 50:
+    rows past 32 neighbours; kbar 0: empty rows.  N = 4096 (beta ~ 260): one
+    barrier per step, and (forced) the two-barrier step of wider windows."""
+    from snd_vae_amd import layers
     from snd_vae_amd.data import GraphBatch, locality_order, window_plan
     rp, ci, dense = rand_batch(n, B, kbar, seed) if B <= 8 else rand_batch_csr(n, B, kbar, seed)
     gb = GraphBatch(B, n, rp, ci, np.zeros((n * B, 1), np.float32), np.zeros((n * B, 1), np.float32),
                     np.zeros((n * B, 2), np.float32))
     order = locality_order(gb)
+    wp = window_plan(gb, order)
+    assert (wp.beta + 7) // 8 * 8 <= 352
+    if kbar >= 40:
+        assert wp.max_degree > 32
     hb = torch.from_numpy(np.random.default_rng(seed).standard_normal((n * B, 64)).astype(np.float32)).to(torch.bfloat16)
     d_rp, d_ci = cu(rp, torch.int32), cu(ci if len(ci) else np.zeros(1, np.int32), torch.int32)
     ref = layers.spmm_bf16(d_rp, d_ci, hb.cuda(), n, B, cu(order, torch.int32))
-    for ring, bound in ((1096, 352), (1024, 312)):
-        wp = window_plan(gb, order, ring)
-        assert (wp.beta + 7) // 8 * 8 <= 352
-        if (wp.beta + 7) // 8 * 8 > bound:              # 64 graphs: beta 331, the 1096 ring only
-            continue
-        if kbar >= 40:
-            assert wp.max_degree > 32
-        out = layers.spmm_bf16_window(layers.DeviceWindowPlan(wp), hb.cuda(), n, B)
-        torch.cuda.synchronize()
-        assert torch.equal(out.view(torch.int16), ref.view(torch.int16)), ring
-        if n == 4096 and B in (1, 8):
-            # the two-barrier step (the 1096 ring's schedule for beta > 288), forced by debug
-            # bit 32 << 24 (the deep ring ignores it), and the unbalanced group order (wave w
-            # sums group w, bit 64 << 24): same sums
-            for flag in (32 << 24, 64 << 24):
-                _lib.check(_lib.lib().snd_debug_set(flag))
-                try:
-                    out2 = layers.spmm_bf16_window(layers.DeviceWindowPlan(wp), hb.cuda(), n, B)
-                    torch.cuda.synchronize()
-                finally:
-                    _lib.check(_lib.lib().snd_debug_set(0))
-                assert torch.equal(out2.view(torch.int16), ref.view(torch.int16)), (ring, flag)
+    out = layers.spmm_bf16_window(layers.DeviceWindowPlan(wp), hb.cuda(), n, B)
+    torch.cuda.synchronize()
+    assert torch.equal(out.view(torch.int16), ref.view(torch.int16))
+    if n == 4096 and B in (1, 8):
+        # the two-barrier step (the schedule for beta > 288), forced by debug bit 32 << 24,
+        # and the unbalanced group order (wave w sums group w, bit 64 << 24): same sums
+        from snd_vae_amd import _lib
+        for flag in (32 << 24, 64 << 24):
+            _lib.check(_lib.lib().snd_debug_set(flag))
+            try:
+                out2 = layers.spmm_bf16_window(layers.DeviceWindowPlan(wp), hb.cuda(), n, B)
+                torch.cuda.synchronize()
+            finally:
+                _lib.check(_lib.lib().snd_debug_set(0))
+            assert torch.equal(out2.view(torch.int16), ref.view(torch.int16)), flag
     if dense is not None:
         r64 = R.spmm(dense, hb.float().numpy().astype(np.float64), n)
         assert np.abs(out.float().cpu().numpy() - r64).max() <= 2 ** -7 * max(np.abs(r64).max(), 1.0)
@@ -222,34 +218,6 @@ def test_spmm_bf16_window_rejects_wide_window():
     assert wp.beta > 352
     with pytest.raises(_lib.SNDError):
         layers.spmm_bf16_window(layers.DeviceWindowPlan(wp), torch.zeros(n, 64, dtype=torch.bfloat16, device="cuda"), n, B)
-
-
-def test_spmm_bf16_window_ring_bounds():
-    """A schedule of bandwidth 330 (edges i <-> i + 330 in natural order): ceil8 = 336
-    fits the 1096-row ring (bitwise spmm_bf16) but not the deep 1024-row one (<= 312),
-    whose launch refuses; window_plan_auto picks the 1096 ring for it and the deep ring
-    for an RCM schedule."""
-    from snd_vae_amd import _lib, layers
-    from snd_vae_amd.data import GraphBatch, locality_order, window_plan, window_plan_auto
-    n, B, d = 1024, 1, 330
-    pairs = [(i, i + d) for i in range(n - d)]
-    rp, ci = csr_from_pairs(n, pairs)
-    gb = GraphBatch(B, n, rp, ci, np.zeros((n, 1), np.float32), np.zeros((n, 1), np.float32),
-                    np.zeros((n, 2), np.float32))
-    order = np.arange(n, dtype=np.int32)
-    hb = torch.from_numpy(np.random.default_rng(0).standard_normal((n, 64)).astype(np.float32)).to(torch.bfloat16)
-    ref = layers.spmm_bf16(cu(rp, torch.int32), cu(ci, torch.int32), hb.cuda(), n, B, cu(order, torch.int32))
-    wa = window_plan_auto(gb, order)
-    assert wa.beta == d and wa.ring == 1096
-    out = layers.spmm_bf16_window(layers.DeviceWindowPlan(wa), hb.cuda(), n, B)
-    torch.cuda.synchronize()
-    assert torch.equal(out.view(torch.int16), ref.view(torch.int16))
-    with pytest.raises(_lib.SNDError):
-        layers.spmm_bf16_window(layers.DeviceWindowPlan(window_plan(gb, order, 1024)), hb.cuda(), n, B)
-    rp2, ci2 = rand_batch_csr(4096, 1, 16.0, 1)[:2]
-    gb2 = GraphBatch(1, 4096, rp2, ci2, np.zeros((4096, 1), np.float32), np.zeros((4096, 1), np.float32),
-                     np.zeros((4096, 2), np.float32))
-    assert window_plan_auto(gb2, locality_order(gb2)).ring == 1024
 
 
 def test_graph_convolution_epilogue():

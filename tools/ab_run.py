@@ -25,8 +25,6 @@ def main():
     ap.add_argument("--adam-per-range", action="store_true",
                     help="A/B: one snd_adam_tf1 launch per unfused range instead of snd_adam_tf1_ranges")
     ap.add_argument("--debug", default="", help="comma list of snd_debug_set bits: each kernel is timed under each")
-    ap.add_argument("--window-ring", type=int, default=0,
-                    help="force the window SpMM plan's LDS ring (1096 / 1024; 0: data.window_plan_auto)")
     ap.add_argument("--step-debug", type=int, default=0,
                     help="snd_debug_set bits for the captured step itself (host-side A/B switches)")
     args = ap.parse_args()
@@ -43,9 +41,7 @@ def main():
         _lib.lib().snd_debug_set(args.step_debug)
         args.tag += f" dbg{args.step_debug}"
     cfg = PRESETS[args.config] if args.config else tscale(args.nodes, args.latent)
-    db = DeviceBatch(synthetic_batch(cfg, args.graphs, seed=1000), window_ring=args.window_ring or None)
-    if db.window is not None:
-        args.tag += f" ring{db.window[5]}"
+    db = DeviceBatch(synthetic_batch(cfg, args.graphs, seed=1000))
     model = SGCNModelVAE(cfg, args.graphs, dtype="bf16")
     opt = OptimizerVAE(model)
     if args.adam_per_range:

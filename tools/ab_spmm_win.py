@@ -1,7 +1,7 @@
-"""A/B the window SpMM (snd_csr_spmm_bf16_window_ring) on bench.py's 256-graph batch under
-snd_debug_set flags and LDS rings, alternating the variants within one process (HIP events).
+"""A/B the window SpMM (snd_csr_spmm_bf16_window) on bench.py's 256-graph batch under
+snd_debug_set flags, alternating the flags within one process (HIP events).
 
-    python tools/ab_spmm_win.py --flags 0,524288 --rings 1096,1024 --rounds 4
+    python tools/ab_spmm_win.py --flags 0,524288 --rounds 4
 """
 import argparse
 import os
@@ -15,7 +15,6 @@ def main():
     ap.add_argument("--flags", default="0")
     ap.add_argument("--rounds", type=int, default=4)
     ap.add_argument("--copies", type=int, default=32)
-    ap.add_argument("--rings", default="1096")
     args = ap.parse_args()
     import ctypes
 
@@ -38,41 +37,35 @@ def main():
     R = R0 * c
     z = np.zeros((1, 1), np.float32)
     big = GraphBatch(host.n_graphs * c, host.n_nodes, rp.astype(np.int32), ci.astype(np.int32), z, z, z)
-    rings = [int(r) for r in args.rings.split(",")]
-    plans = {r: window_plan(big, order, r) for r in rings}
-    dws = {r: DeviceWindowPlan(p) for r, p in plans.items()}
+    wp = window_plan(big, order)
+    dw = DeviceWindowPlan(wp)
     h = torch.randn(R, 64, device="cuda").to(torch.bfloat16)
     out = torch.empty_like(h)
     L = _lib.lib()
     ng = host.n_graphs * c
     byts = 4 * (R + 1) + 4 * len(ci) + 2 * 2 * R * 64
-
-    def runner(r):
-        dw, wp = dws[r], plans[r]
-        return lambda sp: _lib.check(L.snd_csr_spmm_bf16_window_ring(
-            dw.meta.data_ptr(), dw.slots.data_ptr(), dw.rows.data_ptr(), dw.order.data_ptr(), R, host.n_nodes, ng,
-            wp.beta, h.data_ptr(), 64, 64, out.data_ptr(), 64, r, sp))
-    print(f"beta {plans[rings[0]].beta}", flush=True)
+    run = lambda sp: _lib.check(L.snd_csr_spmm_bf16_window(
+        dw.meta.data_ptr(), dw.slots.data_ptr(), dw.rows.data_ptr(), dw.order.data_ptr(), R, host.n_nodes, ng,
+        wp.beta, h.data_ptr(), 64, 64, out.data_ptr(), 64, sp))
     flags = [int(f, 0) for f in args.flags.split(",")]
-    variants = [(r, f) for r in rings for f in flags]
     ref = None
-    res = {v: [] for v in variants}
+    res = {f: [] for f in flags}
     for rnd in range(args.rounds):
-        for r, f in variants:
+        for f in flags:
             _lib.check(L.snd_debug_set(f))
-            ms = bench.time_launches(runner(r), 10)
-            res[(r, f)].append(ms)
+            ms = bench.time_launches(run, 10)
+            res[f].append(ms)
             if rnd == 0:
                 torch.cuda.synchronize()
                 o = out.float()
                 if ref is None:
                     ref = o.clone()
-                print(f"ring {r} flags {f}: max |out - out(first variant)| = {float((o - ref).abs().max()):.3e}",
+                print(f"flags {f}: max |out - out(flags {flags[0]})| = {float((o - ref).abs().max()):.3e}",
                       flush=True)
     _lib.check(L.snd_debug_set(0))
-    for r, f in variants:
-        t = sorted(res[(r, f)])
-        print(f"ring {r} flags {f:>9d}: median {t[len(t) // 2] * 1e3:7.2f} us  min {t[0] * 1e3:7.2f} us  "
+    for f in flags:
+        t = sorted(res[f])
+        print(f"flags {f:>9d}: median {t[len(t) // 2] * 1e3:7.2f} us  min {t[0] * 1e3:7.2f} us  "
               f"{byts / (t[len(t) // 2] * 1e-3) / 8e12:.4f} of 8 TB/s")
 
 
