@@ -25,6 +25,8 @@ def main():
     ap.add_argument("--adam-per-range", action="store_true",
                     help="A/B: one snd_adam_tf1 launch per unfused range instead of snd_adam_tf1_ranges")
     ap.add_argument("--debug", default="", help="comma list of snd_debug_set bits: each kernel is timed under each")
+    ap.add_argument("--option", action="append", default=[],
+                    help="plan option name=value (snd_plan_set_option), e.g. conc_decoder=1")
     ap.add_argument("--step-debug", type=int, default=0,
                     help="snd_debug_set bits for the captured step itself (host-side A/B switches)")
     args = ap.parse_args()
@@ -43,6 +45,9 @@ def main():
     cfg = PRESETS[args.config] if args.config else tscale(args.nodes, args.latent)
     db = DeviceBatch(synthetic_batch(cfg, args.graphs, seed=1000))
     model = SGCNModelVAE(cfg, args.graphs, dtype="bf16")
+    for o in args.option:
+        k, v = o.split("=")
+        args.tag += f" {k}={v}:{int(model.set_option(k, int(v)))}"
     opt = OptimizerVAE(model)
     if args.adam_per_range:
         def per_range(stream=None):
