@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round 6, session F: the fused decoder beside zz^T at C2 (B = 8, plan option conc_decoder=1)
 # with the 128-row decoder (one 148 KB workgroup per CU: it cannot share a CU with zz^T) and
-# with the reverted dual decoder (ab/dual.so, commit 56f1efd: 76 KB, 8 waves -- one zz^T and
+# with the reverted dual decoder (ab/dual.so, snd_dec.* of commit 56f1efd on the current tree: 76 KB, 8 waves -- one zz^T and
 # one decoder workgroup fit a CU together); alternating processes.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
