@@ -47,6 +47,7 @@ def main():
     run = lambda sp: _lib.check(L.snd_csr_spmm_bf16_window(
         dw.meta.data_ptr(), dw.slots.data_ptr(), dw.rows.data_ptr(), dw.order.data_ptr(), R, host.n_nodes, ng,
         wp.beta, h.data_ptr(), 64, 64, out.data_ptr(), 64, sp))
+    print(f"beta {wp.beta} nnz {len(ci)}", flush=True)
     flags = [int(f, 0) for f in args.flags.split(",")]
     ref = None
     res = {f: [] for f in flags}

@@ -2,7 +2,7 @@
 rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE) of tools/ab_spmm_win.py, in the format
 bench.load_spmm_traffic reads (profiles/*pmc_spmm_win.json).
 
-    python tools/pmc_spmm_win.py FETCH_DIR WRITE_DIR OUT_JSON --ring 1024 --nnz 16266176 --beta 258
+    python tools/pmc_spmm_win.py FETCH_DIR WRITE_DIR OUT_JSON --nnz 16266176 --beta 258
 """
 import argparse
 import json
@@ -19,7 +19,6 @@ def main():
     ap.add_argument("fetch_dir")
     ap.add_argument("write_dir")
     ap.add_argument("out")
-    ap.add_argument("--ring", type=int, required=True)
     ap.add_argument("--nnz", type=int, required=True)
     ap.add_argument("--beta", type=int, required=True)
     ap.add_argument("--rows", type=int, default=256 * 4096)
@@ -31,11 +30,11 @@ def main():
     rd, wr = int(2 * 1024 * fk), int(1024 * wk)
     alg = 4 * (args.rows + 1) + 4 * args.nnz + 2 * 2 * args.rows * 64
     out = {
-        "kernel": f"{k} (snd_csr_spmm_bf16_window_ring, ring {args.ring})",
+        "kernel": f"{k} (snd_csr_spmm_bf16_window)",
         "workload": (f"bench secondary roofline: A @ H, width 64, 256 graphs block-diagonal (8 RGGs N=4096 x 32 "
-                     f"copies), {args.nnz} nnz, RCM schedule, beta {args.beta}, {args.ring}-row LDS ring"),
+                     f"copies), {args.nnz} nnz, RCM schedule, beta {args.beta}, 1096-row LDS ring"),
         "command": "rocprofv3 --pmc FETCH_SIZE | WRITE_SIZE (one pass each) -- python tools/ab_spmm_win.py "
-                   f"--rings {args.ring} --flags 0 --rounds 1",
+                   "--flags 0 --rounds 1",
         "launches": len(f[k]),
         "fetch_size_kib_per_launch": round(fk, 1),
         "write_size_kib_per_launch": round(wk, 1),
