@@ -1,0 +1,14 @@
+#!/bin/bash
+# Round 6, session I: wgrad_multi with raised wave priority until the first unit lands
+# (ab/prio.so, -DSND_WG_PRIO=1) against the shipped library; C2 step + the plan's
+# wgrad_multi back to back, alternating processes.
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+fatal() { case "$1" in 124|134|137|139) return 0;; *) return 1;; esac; }
+run() { local secs=$1; shift; timeout -k 10 "$secs" "$@"; local rc=$?; if fatal $rc; then echo "FATAL $rc: $*"; exit $rc; fi; return $rc; }
+for i in 1 2 3; do
+  run 200 python tools/ab_run.py --kernels wgrad_multi --tag base >> gpurun_out/i_prio.jsonl 2>>gpurun_out/i_err.log || exit 1
+  SND_LIB_PATH=ab/prio.so run 200 python tools/ab_run.py --kernels wgrad_multi --tag prio >> gpurun_out/i_prio.jsonl 2>>gpurun_out/i_err.log || exit 1
+done
+cat gpurun_out/i_prio.jsonl
