@@ -12,12 +12,13 @@ __host__ __device__ __forceinline__ int img_swz(int row, int kp) {
 }
 
 // physical chunk i of image d: dst[t][n][8 c .. 8 c + 7] = W values of logical chunk c ^ swz
-__device__ __forceinline__ void pack_chunk(const PackDesc& d, int i) {
+// chunk i's 8 values (fp32) and its store, split so that a caller can issue the loads
+// early and store late (enc_front's spread packing); pack_chunk = both, back to back
+__device__ __forceinline__ void pack_chunk_vals(const PackDesc& d, int i, float (&vals)[8]) {
   const int kc = d.kp >> 3;
   const int c = i % kc, tn = i / kc;
   const int n = tn % d.np, t = tn / d.np;
   const int lc = c ^ img_swz(n, d.kp);          // logical chunk stored at physical chunk c
-  bf16x8 v;
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     const int k = 8 * lc + j;
@@ -34,9 +35,22 @@ __device__ __forceinline__ void pack_chunk(const PackDesc& d, int i) {
       if (aa >= s.a0 && aa < s.a1 && bb >= s.b0 && bb < s.b1)
         val = s.w[((long long)tt * s.A + aa) * s.B + bb];
     }
-    v[j] = (__bf16)val;
+    vals[j] = val;
   }
+}
+__device__ __forceinline__ void pack_chunk_store(const PackDesc& d, int i, const float (&vals)[8]) {
+  const int kc = d.kp >> 3;
+  const int c = i % kc, tn = i / kc;
+  const int n = tn % d.np, t = tn / d.np;
+  bf16x8 v;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] = (__bf16)vals[j];
   *reinterpret_cast<bf16x8*>(d.dst + ((long long)(t * d.np + n) * d.kp + 8 * c)) = v;
+}
+__device__ __forceinline__ void pack_chunk(const PackDesc& d, int i) {
+  float vals[8];
+  pack_chunk_vals(d, i, vals);
+  pack_chunk_store(d, i, vals);
 }
 
 __host__ __device__ __forceinline__ int pack_chunks(const PackDesc& d) { return d.T * d.np * (d.kp >> 3); }
