@@ -459,9 +459,6 @@ __device__ __forceinline__ int tr_off(int row, int col, int kp) {
 }
 
 constexpr int WGT = 1024;   // 16 waves; wave w owns the (tap, 16-col k block) pair pg0 + w
-#ifndef SND_WG_PRIO
-#define SND_WG_PRIO 0
-#endif
 
 __device__ __forceinline__ int cdiv_d(int a, int b) { return (a + b - 1) / b; }
 
@@ -572,7 +569,6 @@ __device__ __forceinline__ void wgrad_body(const WgArgs& a, const int bx, const 
     for (int k = 0;; ++k) {
       __builtin_amdgcn_s_waitcnt(0x0F70);
       __syncthreads();
-      if (SND_WG_PRIO && k == 0) __builtin_amdgcn_s_setprio(0);   // A/B: end of the raised prologue
       wg_stamp(tsp, 3 + k, stamp && k < 6);
       // next unit: next graph segment of this 128-row block, else the next block
       int nsub = u.sub, ns0 = u.s1;
@@ -650,10 +646,6 @@ static_assert(sizeof(WgMultiPack) <= 4096, "wgrad_multi: kernel arguments over 4
 // two workgroups per CU.
 __global__ void __launch_bounds__(WGT) __attribute__((amdgpu_waves_per_eu(8, 8)))
 wgrad_multi_kernel(WgMultiPack m) {
-  // A/B build (-DSND_WG_PRIO=1): the waves issue at raised priority until their first
-  // unit's staging has landed (the second workgroup of a CU otherwise waits for issue
-  // slots behind the first one's MFMAs before its first DMA goes out)
-  if (SND_WG_PRIO) __builtin_amdgcn_s_setprio(2);
   extern __shared__ __attribute__((aligned(16))) __bf16 lds[];
   __shared__ unsigned tsl[kWgStampWords];
   const bool stamp = (kdbg(m.a[0].dbg) & (1 << 21)) && m.a[0].stamps;

@@ -330,28 +330,11 @@ int head_bwd_launch(const HeadBwdArgs& a, hipStream_t s) {
 // gradient and the backward read it) and into LDS, then XW1 = H1 W1 on MFMA with the
 // W1 image built in LDS from the fp32 weights (pack_kernel's image, bit for bit).
 // Workgroups past the tiles build the step's packed weight images (pack_chunk).
-#ifndef SND_FRONT_SPREAD
-#define SND_FRONT_SPREAD 0   // A/B: the weight images packed by the tiles themselves (no extra workgroups)
-#endif
 template <int NB>
 __global__ void __launch_bounds__(1024) enc_front_kernel(FrontArgs a) {
   const int tid = threadIdx.x;
   const int ntiles = cdiv_dev(a.R, 128);
-  // spread packing: this tile's pack_per chunks of the concatenated images, values loaded
-  // here (their latency under the gather) and stored at the end
-  int pks = -1, pki = 0;
-  float pkv[8];
-  if (SND_FRONT_SPREAD && tid < a.pack_per) {
-    const int gi = blockIdx.x * a.pack_per + tid;
-    if (gi < a.pack_wg[a.npack]) {
-      int s = 0;
-      while (s + 1 < a.npack && gi >= a.pack_wg[s + 1]) ++s;
-      pks = s;
-      pki = gi - a.pack_wg[s];
-      pack_chunk_vals(a.pack[s], pki, pkv);
-    }
-  }
-  if (!SND_FRONT_SPREAD && (int)blockIdx.x >= ntiles) {
+  if ((int)blockIdx.x >= ntiles) {
     const int pb = blockIdx.x - ntiles;
     int s = 0;
     while (s + 1 < a.npack && pb >= a.pack_wg[s + 1]) ++s;
@@ -477,7 +460,6 @@ __global__ void __launch_bounds__(1024) enc_front_kernel(FrontArgs a) {
       *reinterpret_cast<uint4*>(a.axb + (long long)r * 8) = to_bf16x8(axp);
     }
   }
-  if (SND_FRONT_SPREAD && pks >= 0) pack_chunk_store(a.pack[pks], pki, pkv);
   __syncthreads();
   // ---- XW1 = H1 W1 (row engine RC_LIN, no bias)
   const int lane = tid & 63, w = tid >> 6;
@@ -522,14 +504,12 @@ int launch_front(FrontArgs& a, const PackDesc* pack, int npack, hipStream_t s) {
                   "front: bad pack descriptor %d", i);
     a.pack[i] = x;
     a.pack_wg[i] = wg;
-    wg += SND_FRONT_SPREAD ? pack_chunks(x) : cdiv(pack_chunks(x), 1024);   // spread: chunks
+    wg += cdiv(pack_chunks(x), 1024);
   }
   a.pack_wg[npack] = wg;
-  a.pack_per = SND_FRONT_SPREAD ? cdiv(wg, cdiv(a.R, 128)) : 0;
-  SND_CHECK_ARG(a.pack_per <= 1024, "front: %d pack chunks per tile", a.pack_per);
   SND_TRY(head_init_attributes());
   const size_t lds = (size_t)(a.np1 + 128) * a.kp1 * 2;
-  const dim3 grid(cdiv(a.R, 128) + (SND_FRONT_SPREAD ? 0 : wg));
+  const dim3 grid(cdiv(a.R, 128) + wg);
   switch ((a.np1 / 16 + 1) / 2) {
     case 1: hipLaunchKernelGGL((enc_front_kernel<1>), grid, dim3(1024), lds, s, a); break;
     case 2: hipLaunchKernelGGL((enc_front_kernel<2>), grid, dim3(1024), lds, s, a); break;

@@ -92,8 +92,7 @@ struct FrontArgs {
   const float* w1; int n1; int kp1, np1;     // W1 [h0 + f][n1] fp32; its image geometry
   __bf16* xw1;                               // [R][n1]
   PackDesc pack[kMaxPack]; int npack;        // weight images built by the extra workgroups
-  int pack_wg[kMaxPack + 1];                 // workgroup prefix per image (spread: chunk prefix)
-  int pack_per;                              // spread packing (SND_FRONT_SPREAD): chunks per tile
+  int pack_wg[kMaxPack + 1];                 // workgroup prefix per image
   int dbg;
 };
 bool front_supported(int f, int h0, int n1, int kp1, int np1);

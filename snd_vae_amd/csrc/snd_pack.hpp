@@ -12,8 +12,7 @@ __host__ __device__ __forceinline__ int img_swz(int row, int kp) {
 }
 
 // physical chunk i of image d: dst[t][n][8 c .. 8 c + 7] = W values of logical chunk c ^ swz
-// chunk i's 8 values (fp32) and its store, split so that a caller can issue the loads
-// early and store late (enc_front's spread packing); pack_chunk = both, back to back
+// chunk i's 8 values (fp32) and its store; pack_chunk = both, back to back
 __device__ __forceinline__ void pack_chunk_vals(const PackDesc& d, int i, float (&vals)[8]) {
   const int kc = d.kp >> 3;
   const int c = i % kc, tn = i / kc;
