@@ -23,7 +23,6 @@
 // same epilogues): every activation and data gradient equals the unfused
 // path's bit for bit; only the column partial sums are added in another order.
 #include "snd_dec.hpp"
-#include "snd_head_bwd.hpp"
 
 #include <algorithm>
 
@@ -597,13 +596,12 @@ __device__ __forceinline__ void colpart_flush(float (&q)[3][NBH][4], float* slot
       }
 }
 
-// the backward chain of tile t on the calling workgroup (dec_bwd_kernel, and the head of
-// dec_bwd_head_kernel below); smem: the dynamic LDS (BwdLay)
 template <int TR>
-__device__ __forceinline__ void dec_bwd_tile(const DecChainBwdArgs& a, const int t, char* smem) {
+__global__ void __launch_bounds__(DT) dec_bwd_kernel(DecChainBwdArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
   __shared__ __attribute__((aligned(16))) float cpa[2][128], cpb[2][128];   // conv2-s BN (gamma c, beta), conv1 BN
   const BwdLay L(a, TR);
-  const Tile tl = tile_of<TR>(t, a.npg);
+  const Tile tl = tile_of<TR>(blockIdx.x, a.npg);
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, lg = lane >> 4;
   __bf16* wimg = reinterpret_cast<__bf16*>(smem + L.w);
   __bf16* d3 = reinterpret_cast<__bf16*>(smem + L.d3);
@@ -611,6 +609,7 @@ __device__ __forceinline__ void dec_bwd_tile(const DecChainBwdArgs& a, const int
   __bf16* d1 = reinterpret_cast<__bf16*>(smem + L.d1);
   float* slots = reinterpret_cast<float*>(smem + L.cps);
   const int own = tl.rend - tl.r0;
+  const int t = blockIdx.x;
   const bool stamp = kdbg(a.dbg) & (1 << 21);   // measurement only, as dec_fwd_kernel (over pc1)
   unsigned long long ts[8] = {};
   if (stamp) ts[0] = __builtin_amdgcn_s_memrealtime();
@@ -795,37 +794,6 @@ __device__ __forceinline__ void dec_bwd_tile(const DecChainBwdArgs& a, const int
   }
 }
 
-template <int TR>
-__global__ void __launch_bounds__(DT) dec_bwd_kernel(DecChainBwdArgs a) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  dec_bwd_tile<TR>(a, blockIdx.x, smem);
-}
-
-// The decoder's backward chain and the backward head on the same 128-row tile, one launch
-// (C2's serial step, where both run 128-row tiles of 1024 threads): the head's inputs are
-// row-local -- dz of the decoders (this tile's conv1^T output), dJ of zz^T, [mu | s], eps,
-// P1, X of the tile's rows, and z rows of the tile's neighbours (written by head_fwd) --
-// so the tile continues into the head without a grid-wide boundary.  The head's LDS
-// starts at 0 once the decoder is done; its per-tile partial scratch (static in
-// head_bwd_kernel) sits at hoff, past the head's layout, inside the decoder's dynamic
-// LDS.  The tile order is the head's XCD-aware one (a graph's tiles on one XCD); the
-// decoder's partials are indexed by tile, so both halves compute exactly what their
-// separate kernels do.
-template <int NQ, int NB1, int NB2>
-__global__ void __launch_bounds__(DT) dec_bwd_head_kernel(DecChainBwdArgs a, HeadBwdArgs h, int hoff) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  __shared__ double sl[DT / 64];
-  __shared__ unsigned stp[DT / 64];
-  const int t = hbk::head_tile_xcd(h, kDecRows, blockIdx.x);
-  dec_bwd_tile<kDecRows>(a, t, smem);
-  __syncthreads();   // the decoder's LDS is dead; its dz rows (global) are visible to the workgroup
-  constexpr int NRB = kDecRows / 16;
-  auto cps = reinterpret_cast<float (*)[4][128]>(smem + hoff);
-  auto cpb = reinterpret_cast<float (*)[128]>(smem + hoff + NRB * 4 * 128 * 4);
-  auto colp = reinterpret_cast<float (*)[128]>(smem + hoff + NRB * 5 * 128 * 4);
-  hbk::head_bwd_tile<kDecRows, NQ, NB1, NB2>(h, t, smem, cps, cpb, colp, sl, stp);
-}
-
 }  // namespace
 
 int dec_rows(int ngraphs, int npg) {
@@ -858,23 +826,6 @@ bool dec_fused_supported(int dj, const ColMap& m1, const ColMap& m2, int s3, int
   return 16 % ((k2t.np / 16 + 1) / 2) == 0 && 16 % (k3t.np / 16) == 0;
 }
 
-// the fused decoder-backward + backward-head launch: its dynamic LDS and the head's partial
-// scratch offset, or 0 when the shapes do not allow it (then the two kernels run apart)
-constexpr int kHeadScratch = (kDecRows / 16) * 5 * 128 * 4;
-static size_t dec_head_lds(const DecChainBwdArgs& a, const HeadBwdArgs& h, int* hoff) {
-  if (dec_rows(a.ngraphs, a.npg) != kDecRows || head_bwd_rows(h.R) != kDecRows || a.npg % kDecRows ||
-      h.R != a.R || h.npg != a.npg || h.ngraphs != a.ngraphs || h.L > 64 ||
-      !head_bwd_supported(h.L, h.gh, h.W, h.h1, h.kp1, h.np1, h.kp2, h.np2))
-    return 0;
-  const int ho = (int)rup(hbk::BwdLay(h.kp1, h.np1, h.kp2, h.np2, h.L, kDecRows).total, 16);
-  const size_t lds = std::max((size_t)BwdLay(a, kDecRows).total, (size_t)ho + kHeadScratch);
-  if (lds > (size_t)kDynLds) return 0;
-  *hoff = ho;
-  return lds;
-}
-#define SND_DEC_HEAD_KERNELS(X)                                                            \
-  X(1, 1) X(1, 2) X(1, 3) X(1, 4) X(2, 1) X(2, 2) X(2, 3) X(2, 4)
-
 static int dec_init_attributes_once() {
   const void* ks[] = {reinterpret_cast<const void*>(dec_fwd_kernel<kDecRows>),
                       reinterpret_cast<const void*>(dec_bwd_kernel<kDecRows>),
@@ -887,14 +838,6 @@ static int dec_init_attributes_once() {
       set_error("dec: hipFuncSetAttribute failed");
       return SND_ERR_HIP;
     }
-#define SND_ATTR_DH(B1, B2)                                                                             \
-  if (hipFuncSetAttribute(reinterpret_cast<const void*>(dec_bwd_head_kernel<1, B1, B2>),                \
-                          hipFuncAttributeMaxDynamicSharedMemorySize, kDynLds) != hipSuccess) {         \
-    set_error("dec: hipFuncSetAttribute (dec_bwd_head) failed");                                       \
-    return SND_ERR_HIP;                                                                                \
-  }
-  SND_DEC_HEAD_KERNELS(SND_ATTR_DH)
-#undef SND_ATTR_DH
   return 0;
 }
 
@@ -941,40 +884,6 @@ int launch_dec_chain_bwd(const DecChainBwdArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(dec_bwd_kernel<kDecRows>, dim3(dec_tiles(a.ngraphs, a.npg)), dim3(DT), lds, s, a);
   SND_LAUNCH_CHECK("dec_bwd_kernel");
   return 0;
-}
-
-bool dec_head_fusable(const DecChainBwdArgs& a, const HeadBwdArgs& h) {
-  int ho = 0;
-  return dec_head_lds(a, h, &ho) > 0;
-}
-
-int launch_dec_bwd_head(const DecChainBwdArgs& a, const HeadBwdArgs& h, hipStream_t s) {
-  int hoff = 0;
-  const size_t lds = dec_head_lds(a, h, &hoff);
-  SND_CHECK_ARG(lds > 0, "dec_bwd_head: shapes outside the fused launch (use the two kernels)");
-  SND_CHECK_ARG(a.R == a.npg * a.ngraphs && a.R > 0, "dec_bwd_head: R != npg * ngraphs");
-  SND_CHECK_ARG(a.y1 && a.y2 && a.dy3 && a.dy2 && a.dy1 && a.dz && a.pc2s && a.pc1 && a.zero &&
-                    a.k3t.w && a.k2t.w && a.k1t.w, "dec_bwd_head: null decoder operand");
-  SND_CHECK_ARG(a.lddy3 % 8 == 0 && a.lddy2 % 4 == 0 && a.lddy1 % 4 == 0 && a.lddz % 4 == 0,
-                "dec_bwd_head: leading dims");
-  SND_CHECK_ARG(h.dz_dec == a.dz && h.rowptr && h.colidx && h.zb && h.edge_part && h.ms && h.eps && h.dJd &&
-                    h.dms && h.bms_part && h.wmsb_img && h.dh && h.bh_part && h.whb_img && h.ge && h.g1 && h.b1 &&
-                    h.p1 && h.x && h.dp1 && h.enc1_part,
-                "dec_bwd_head: null head operand (or the head's dz_dec is not the decoder's dz)");
-  SND_CHECK_ARG((long long)h.R * h.L * 2 < (1ll << 31), "dec_bwd_head: rows x L beyond the 2 GB buffer range");
-  SND_TRY(dec_init_attributes());
-  const int nb1 = (h.np1 / 16 + 1) / 2, nb2 = (h.np2 / 16 + 1) / 2;
-  const dim3 grid(dec_tiles(a.ngraphs, a.npg));
-#define SND_LAUNCH_DH(B1, B2)                                                                   \
-  if (nb1 == B1 && nb2 == B2) {                                                                 \
-    hipLaunchKernelGGL((dec_bwd_head_kernel<1, B1, B2>), grid, dim3(DT), lds, s, a, h, hoff);   \
-    SND_LAUNCH_CHECK("dec_bwd_head_kernel");                                                    \
-    return 0;                                                                                   \
-  }
-  SND_DEC_HEAD_KERNELS(SND_LAUNCH_DH)
-#undef SND_LAUNCH_DH
-  set_error("dec_bwd_head: column blocks (%d, %d) not built", nb1, nb2);
-  return SND_ERR_ARG;
 }
 
 }  // namespace snd

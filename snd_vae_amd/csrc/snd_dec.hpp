@@ -74,11 +74,6 @@ bool dec_fused_supported(int dj, const ColMap& m1, const ColMap& m2, int s3, int
                          const DecImg& k2t, const DecImg& k1t);
 int launch_dec_chain_fwd(const DecChainFwdArgs& a, hipStream_t s);
 int launch_dec_chain_bwd(const DecChainBwdArgs& a, hipStream_t s);
-// dec_bwd + the fused backward head (snd_head.hpp HeadBwdArgs, h.dz_dec == a.dz) on the same
-// 128-row tiles in one launch; dec_head_fusable: whether the shapes allow it
-struct HeadBwdArgs;
-bool dec_head_fusable(const DecChainBwdArgs& a, const HeadBwdArgs& h);
-int launch_dec_bwd_head(const DecChainBwdArgs& a, const HeadBwdArgs& h, hipStream_t s);
 int dec_init_attributes();
 
 }  // namespace snd

@@ -642,7 +642,6 @@ struct Ctx {
   int* nev = nullptr;           // next free event of p->ev
   std::vector<WgArgs>* wq = nullptr;   // deferred weight gradients (one launch at the end)
   int zts = 1;                  // zz^T column splits of this step (launch, split sums, finalize)
-  bool* head_done = nullptr;    // set when the backward head ran fused with the decoder's backward
   float* f(const char* n) const { return (float*)(ws + p->buf(n)); }
   double* d(const char* n) const { return (double*)(ws + p->buf(n)); }
   const float* w(const char* n) const { return P + p->blk(n); }
@@ -1064,17 +1063,8 @@ int head_fwd_fused(const Ctx& x, const snd_batch_t* batch, const float* eps, uns
 
 int encoder_fast_bwd_tail(const Ctx& x, const snd_batch_t* batch, bool enc1_done = false);
 
-// the reparameterisation backward's scales (snd_train_step, the fused backward head)
-static void step_scales(const snd_plan& p, float& adj_scale, float& kl_scale) {
-  const double pairs = (double)p.B * p.N * (double)p.N;
-  // dL/dJ_i = sum_j (G_ij + G_ji) J_j = 2 sum_j G_ij J_j (G symmetric)
-  adj_scale = (float)(2.0 * (double)p.c.norm / pairs);
-  kl_scale = (float)((double)p.c.beta / ((double)p.RH * p.c.latent));
-}
-
-// the fused backward head's arguments (alone: head_bwd_fused; with the decoder's
-// backward: decoder_fast)
-static HeadBwdArgs head_bwd_args(const Ctx& x, const snd_batch_t* batch, float adj_scale, float kl_scale) {
+// the fused backward head alone (encoder_fast_bwd; snd_plan_launch "head_bwd")
+int head_bwd_fused(const Ctx& x, const snd_batch_t* batch, float adj_scale, float kl_scale) {
   const snd_plan& p = *x.p;
   const snd_config_t& c = p.c;
   const int R = p.R, L = c.latent, f = c.f_in, h1 = c.h1, gh = c.g_hidden, W = p.W;
@@ -1095,13 +1085,8 @@ static HeadBwdArgs head_bwd_args(const Ctx& x, const snd_batch_t* batch, float a
     a.p1 = x.f("FP1"); a.x = batch->features; a.ldx = f;
     a.dp1 = bf("FDP1"); a.enc1_part = x.f("PFENC1");
     a.npg = p.N; a.ngraphs = p.B; a.dbg = debug_flags();
-    return a;
+    return launch_head_bwd(a, x.s);
   }
-}
-
-// the fused backward head alone (encoder_fast_bwd; snd_plan_launch "head_bwd")
-int head_bwd_fused(const Ctx& x, const snd_batch_t* batch, float adj_scale, float kl_scale) {
-  return launch_head_bwd(head_bwd_args(x, batch, adj_scale, kl_scale), x.s);
 }
 
 // encoder backward: reparam -> heads -> GCN1 -> GCN0 (all weight gradients as slabs)
@@ -1111,7 +1096,7 @@ int encoder_fast_bwd(const Ctx& x, const snd_batch_t* batch, float adj_scale, fl
   const int R = p.R, L = c.latent, f = c.f_in, h0 = c.h0, h1 = c.h1, gh = c.g_hidden, W = p.W;
   auto bf = [&](const char* n) { return reinterpret_cast<__bf16*>(x.f(n)); };
   if (p.head_bwd) {
-    if (!(x.head_done && *x.head_done)) SND_TRY(head_bwd_fused(x, batch, adj_scale, kl_scale));
+    SND_TRY(head_bwd_fused(x, batch, adj_scale, kl_scale));
     SND_TRY(wgrad(x, wg_args(p, x.ws, p.gWms, bf("FHH"), gh, gh, bf("FDMS"), 2 * L, 2 * L, x.f("FSWMS"), 1), x.s));
     SND_TRY(wgrad(x, wg_args(p, x.ws, p.gWh, bf("FG"), p.ldg, W, bf("FDH"), gh, gh, x.f("FSWH"), 1), x.s));
     return encoder_fast_bwd_tail(x, batch, true);
@@ -1229,7 +1214,7 @@ void encoder_fast_reduce(const Ctx& x, std::vector<ReduceDesc>& rd) {
 }
 
 // decoder forward + heads + backward (model_joint.py:112-145, optimizer.py:149,153)
-int decoder_fast(const Ctx& x, const snd_batch_t* batch, int only = -1, bool fuse_head = false) {
+int decoder_fast(const Ctx& x, const snd_batch_t* batch, int only = -1) {
   const snd_plan& p = *x.p;
   const snd_config_t& c = p.c;
   const int R = p.R, L = p.dj, s2 = c.s2, s3 = c.s3, n2 = c.n2;   // L: width of J here
@@ -1259,7 +1244,7 @@ int decoder_fast(const Ctx& x, const snd_batch_t* batch, int only = -1, bool fus
     f.phs = x.f("PDHS"); f.phn = x.f("PDHN"); f.sse_s = x.d("PDSSES"); f.sse_n = x.d("PDSSEN");
     f.zero = x.ws + p.buf("ZERO");
     f.dbg = debug_flags();
-    if (only != 101 && only != 102) SND_TRY(launch_dec_chain_fwd(f, x.s));
+    if (only != 101) SND_TRY(launch_dec_chain_fwd(f, x.s));
     if (only == 100) return 0;
     DecChainBwdArgs b{};
     b.R = R; b.npg = p.N; b.ngraphs = p.B; b.dj = L;
@@ -1273,20 +1258,8 @@ int decoder_fast(const Ctx& x, const snd_batch_t* batch, int only = -1, bool fus
     b.pc2s = x.f("PDC2S"); b.pc1 = x.f("PDC1");
     b.zero = x.ws + p.buf("ZERO");
     b.dbg = debug_flags();
-    // the backward head on the decoder's tiles in the same launch (serial step, 128-row
-    // tiles; host debug bit 1 << 20: the two kernels apart, A/B)
-    bool fused_head = false;
-    if (fuse_head && (only < 0 || only == 102) && x.head_done && p.head_bwd && p.fast_enc && !p.tref && !(debug_flags() & (1 << 20))) {
-      float adj_scale, kl_scale;
-      step_scales(p, adj_scale, kl_scale);
-      const HeadBwdArgs h = head_bwd_args(x, batch, adj_scale, kl_scale);
-      if (dec_head_fusable(b, h)) {
-        SND_TRY(launch_dec_bwd_head(b, h, x.s));
-        *x.head_done = fused_head = true;
-      }
-    }
-    if (!fused_head && only != 102) SND_TRY(launch_dec_chain_bwd(b, x.s));
-    if (only == 101 || only == 102) return 0;
+    SND_TRY(launch_dec_chain_bwd(b, x.s));
+    if (only == 101) return 0;
     SND_TRY(wgrad(x, wg_args(p, x.ws, p.gK3s, bf("FU2"), p.ld2, s2, bf("FDY3"), p.ld3, s3, x.f("FSK3S")), x.s));
     SND_TRY(wgrad(x, wg_args(p, x.ws, p.gK2s, bf("FU1"), p.ld1, c.s1, bf("FDY2"), p.ld2, s2, x.f("FSK2S")), x.s));
     SND_TRY(wgrad(x, wg_args(p, x.ws, p.gK2n, bf("FU1") + o1, p.ld1, c.n1, bf("FDY2") + o2, p.ld2, n2,
@@ -1606,15 +1579,6 @@ extern "C" int snd_plan_launch(const snd_plan_t* plan, const snd_batch_t* batch,
       SND_CHECK_ARG(p.dec_fused, "snd_plan_launch: %s needs the fused decoder", kernel);
       return decoder_fast(x, batch, kernel[4] == 'f' ? 100 : 101);
     }
-    if (!strcmp(kernel, "dec:bwdhead")) {   // the decoder's backward with the backward head fused
-      SND_CHECK_ARG(p.dec_fused && p.head_bwd, "snd_plan_launch: %s needs the fused decoder and head", kernel);
-      bool done = false;
-      x.head_done = &done;
-      x.zts = p.last_zts;
-      SND_TRY(decoder_fast(x, batch, 102, true));
-      SND_CHECK_ARG(done, "snd_plan_launch: dec:bwdhead: shapes outside the fused launch");
-      return 0;
-    }
     return decoder_fast(x, batch, atoi(kernel + 4));
   }
   set_error("snd_plan_launch: unknown kernel '%s'", kernel);
@@ -1887,10 +1851,8 @@ extern "C" int snd_train_step(const snd_plan_t* plan, const snd_batch_t* batch,
     if (debug_flags() & (1 << 17)) SND_TRY(launch_zzt_dense(za, c.dtype, x.s, p.fast_enc && !p.tref));
     if (cdec) SND_TRY(join_from(x, p.side));
   }
-  bool head_done = false;
-  x.head_done = &head_done;
   if (p.fast) {
-    if (!cdec) SND_TRY(decoder_fast(x, batch, -1, true));
+    if (!cdec) SND_TRY(decoder_fast(x, batch));
   } else {
     // decoders (model_joint.py:112-145): conv1d k5 SAME -> BN -> lrelu
     SND_TRY(conv_fwd(x, x.f("Z"), dj, dj, "dec.K1", C1, "dec.b1", "dec.bn1.gamma", "dec.bn1.beta",
@@ -1939,8 +1901,10 @@ extern "C" int snd_train_step(const snd_plan_t* plan, const snd_batch_t* batch,
     SND_TRY(conv_wgrad(x, x.f("Z"), dj, dj, x.f("DY1"), C1, x.f("SK1"), p.sK1));
   }
   // reparameterisation + KL backward; dJ = conv-decoder grad + zz^T CE grad
-  float adj_scale, kl_scale;
-  step_scales(p, adj_scale, kl_scale);
+  const double pairs = (double)p.B * N * (double)N;
+  // dL/dJ_i = sum_j (G_ij + G_ji) J_j = 2 sum_j G_ij J_j (G symmetric)
+  const float adj_scale = (float)(2.0 * (double)c.norm / pairs);
+  const float kl_scale = (float)((double)c.beta / ((double)RH * L));
   SND_TRY(wait_mark(x, edge_mark));   // EJ
   if (p.fast_enc && !p.tref) {
     SND_TRY(encoder_fast_bwd(x, batch, adj_scale, kl_scale));

@@ -451,39 +451,6 @@ def test_fused_decoder_matches_row_engine(topology, n, d, B):
         assert torch.equal(m1.buffer(name, dt), snap[name]), f"{name} with NaN-poisoned LDS"
 
 
-def test_decoder_backward_and_head_one_launch_bitwise():
-    """C2 shapes (8 graphs of 4096 rows: 128-row tiles for both): the decoder's backward
-    chain and the backward head in one launch (dec_bwd_head_kernel, the step's default
-    there) against the two kernels (host debug bit 1 << 20): every activation, data
-    gradient, per-tile partial, parameter gradient and loss term bitwise equal -- the
-    launch moves the head onto the decoder's tiles without changing any operation."""
-    from snd_vae_amd import _lib
-    from snd_vae_amd.params import init_blocks
-    cfg = tscale(4096, 64)
-    batch = synthetic_batch(cfg, 8, seed=31)
-    p0 = init_blocks(cfg, 3)
-    runs = []
-    for flags in (1 << 20, 0):
-        m, o, b = make(cfg, batch, p0, "bf16")
-        _lib.check(_lib.lib().snd_debug_set(flags))
-        try:
-            o.forward_backward(b)
-            torch.cuda.synchronize()
-        finally:
-            _lib.check(_lib.lib().snd_debug_set(0))
-        runs.append((m, o))
-    (m0, o0), (m1, o1) = runs
-    bufs = DEC_BUFS + (("FDMS", torch.bfloat16), ("FDH", torch.bfloat16), ("FDP1", torch.bfloat16),
-                       ("PEDGE", torch.float64), ("PHBMS", torch.float32), ("PFBH", torch.float32),
-                       ("PFENC1", torch.float32), ("PDC2S", torch.float32), ("PDC1", torch.float32))
-    for name, dt in bufs:
-        assert torch.equal(m0.buffer(name, dt).view(torch.uint8), m1.buffer(name, dt).view(torch.uint8)), name
-    g0, g1 = o0.grad_blocks(), o1.grad_blocks()
-    for k in g0:
-        np.testing.assert_array_equal(g1[k], g0[k], err_msg=k)
-    assert torch.equal(o0.losses, o1.losses)
-
-
 HEAD_BUFS = (("FP1", torch.float32), ("FG", torch.bfloat16), ("FHH", torch.bfloat16), ("MS", torch.float32),
              ("Z", torch.float32), ("ZB", torch.bfloat16), ("EPS", torch.float32), ("ZSTAGE", torch.uint8),
              ("DJD", torch.float32), ("FDP1", torch.bfloat16))
