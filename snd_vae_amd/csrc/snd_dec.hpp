@@ -66,8 +66,8 @@ struct DecChainBwdArgs {
   int dbg;
 };
 
-int dec_rows(int ngraphs, int npg);    // kDecRows or kDecRowsSmall
-int dec_tiles(int ngraphs, int npg);
+int dec_rows(int ngraphs, int npg, int dj);    // kDecRows, kDecRowsSmall or kDecRowsTiny (dj > 64: small)
+int dec_tiles(int ngraphs, int npg, int dj);
 int dec_head_parts(int cin, int cout);        // == heads_fast_parts
 bool dec_fused_supported(int dj, const ColMap& m1, const ColMap& m2, int s3, int sd, int nf,
                          const DecImg& k1, const DecImg& k2, const DecImg& k3, const DecImg& k3t,

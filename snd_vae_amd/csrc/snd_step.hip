@@ -435,7 +435,7 @@ extern "C" int snd_plan_create(const snd_config_t* cfg, int n_graphs, snd_plan_t
           dec_fused_supported(dj, m1, m2, c.s3, c.spatial_dim, c.num_feature, dimg(p->pk1f), dimg(p->pk2f),
                               dimg(p->pk3f), dimg(p->pk3b), dimg(p->pk2b), dimg(p->pk1b))) {
         p->dec_fused = true;
-        p->dtiles = dec_tiles(p->B, p->N);
+        p->dtiles = dec_tiles(p->B, p->N, dj);
         const long long t = p->dtiles;
         p->add_buf("PDHS", t * dec_head_parts(c.s3, c.spatial_dim));
         p->add_buf("PDHN", t * dec_head_parts(c.n2, c.num_feature));

@@ -392,7 +392,8 @@ DEC_BUFS = (("FY1", torch.float32), ("FU1", torch.bfloat16), ("FY2", torch.float
 
 
 @pytest.mark.parametrize("topology,n,d,B", [("tscale", 512, 64, 2), ("tscale", 200, 16, 3),
-                                            ("tref", 300, 32, 2), ("tscale", 4096, 64, 4)])
+                                            ("tref", 300, 32, 2), ("tscale", 4096, 64, 4),
+                                            ("tscale", 1000, 128, 2)])
 def test_fused_decoder_matches_row_engine(topology, n, d, B):
     """The fused decoder (snd_dec.hip: conv chain + heads in one launch, the
     backward data chain in another, halos recomputed in LDS) against the row
@@ -401,7 +402,9 @@ def test_fused_decoder_matches_row_engine(topology, n, d, B):
     column partials (biases, BN, heads) agree to fp32 reassociation, and the
     conv weight gradients (same operands) are bitwise equal.  Covers partial
     tiles (N = 200, 300: 128-row tiles never span graphs) and the graph latent; N = 4096,
-    B = 4 the 128-row tiles of a full chip (128 tiles), the bench's tiling."""
+    B = 4 the 128-row tiles of a full chip (128 tiles), the bench's tiling; d = 128 (C5's
+    width) the streamed kernels: 64-row tiles, every conv's weights through two one-tap
+    LDS buffers (N = 1000: a partial last tile)."""
     from snd_vae_amd import _lib
     from snd_vae_amd.params import init_blocks
     cfg = tscale(n, d) if topology == "tscale" else tref(n, d, g_hidden=16, latent=8)
