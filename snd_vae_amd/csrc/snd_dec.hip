@@ -94,7 +94,7 @@ struct BwdLay {
   __host__ __device__ BwdLay(const DecChainBwdArgs& p, int TR, bool str = false) {
     tapb = max(max(tap_bytes(p.k3t), tap_bytes(p.k2t)), tap_bytes(p.k1t));
     const int wb = str ? 2 * tapb : max(max(p.k3t.np * p.k3t.kp, p.k2t.np * p.k2t.kp), p.k1t.np * p.k1t.kp) * 5 * 2;
-    const int nw = str ? 8 : 16;
+    const int nw = NW;   // the kernels' waves (slots per column group)
     w = 0;
     d3 = wb;
     d2 = d3 + img_bytes(in_rows(TR + 8), p.k3t.kp);
