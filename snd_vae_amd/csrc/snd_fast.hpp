@@ -196,6 +196,9 @@ struct ReparamBwdFastArgs {
   const float* dJd_extra = nullptr; int nextra = 0;
 };
 int reparam_bwd_fast_blocks(int R, int L);
+// edge_bf16 + reparam_bwd_fast in one launch (e.ej unused): partials {loss, tp} into e.part
+// and [mu | s] bias sums into a.colpart, edge_reparam_blocks(R) blocks each
+int edge_reparam_blocks(int R);
 
 // reparameterisation + KL fused with the zz^T staging images (snd_zzt.hpp ZztStage)
 struct ReparamPrepArgs {
@@ -224,6 +227,7 @@ int edge_bf16_blocks(int R);
 int launch_edge_bf16(const EdgeBfArgs& a, hipStream_t s);
 int launch_reparam_prep(const ReparamPrepArgs& a, int dp, hipStream_t s);
 int launch_reparam_bwd_fast(const ReparamBwdFastArgs& a, hipStream_t s);
+int launch_edge_reparam_bwd(const EdgeBfArgs& e, const ReparamBwdFastArgs& a, hipStream_t s);
 
 int fast_init_attributes();
 int debug_flags();

@@ -582,6 +582,135 @@ __global__ void __launch_bounds__(NT) reparam_bwd_fast_kernel(ReparamBwdFastArgs
 }
 
 
+// ---------------------------------------------------------------- per-edge terms + reparam backward
+// edge_bf16_kernel and reparam_bwd_fast_kernel in one launch, for the node-latent fast
+// encoder without the fused backward head (L = 128, C5): row r's 8 lanes gather its
+// neighbours' z and keep e_r = sum_j coef_ij z_j in registers (edge_bf16_kernel's
+// arithmetic, bit for bit), then apply the reparameterisation backward to their 8 (x NQ)
+// columns of the row (reparam_bwd_fast_kernel's, bit for bit) -- no EJ round trip, one
+// launch fewer, and the per-edge gather runs after zz^T instead of before it.  Partials:
+// {loss, tp} per block (as edge_bf16_kernel) and the [mu | s] bias column sums per block
+// (the block's 32 rows: shuffles over each wave's 8 rows, then the 4 waves in order).
+template <int NQ>
+__global__ void __launch_bounds__(NT) edge_reparam_bwd_kernel(EdgeBfArgs e, ReparamBwdFastArgs a) {
+  __shared__ double sl[NT / 64];
+  __shared__ unsigned st[NT / 64];
+  __shared__ float bred[NT / 64][2 * 64 * NQ];
+  const int sub = threadIdx.x & (LPR - 1), w = threadIdx.x >> 6;
+  const int r = row_of(e.row_order, xcd_rowblock(blockIdx.x, e.xcd_nbg), e.R);
+  const bool rv = r < e.R;
+  const int L = a.L, nch = L >> 3;
+  bool qv[NQ];
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) qv[q] = sub + 8 * q < nch;
+  float lossr = 0.f;
+  unsigned tp = 0;
+  u32x4 zip[NQ];
+  float acc[NQ][8];
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) {
+    zip[q] = u32x4{0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[q][j] = 0.f;
+  }
+  if (rv)
+#pragma unroll
+    for (int q = 0; q < NQ; ++q)
+      if (qv[q]) {
+        const bf16x8 v = *reinterpret_cast<const bf16x8*>(e.z + (long long)r * e.d + 64 * q + 8 * sub);
+        zip[q] = __builtin_bit_cast(u32x4, v);
+      }
+  const float pw = e.pos_weight;
+  const __amdgpu_buffer_rsrc_t rs = rows_rsrc(e.z, (long long)e.R * e.d * 2);
+  gather_rows16<NQ>(e.colidx, rv ? e.rowptr[r] : 0, rv ? e.rowptr[r + 1] : 0, rs, 2u * e.d, sub,
+                    [&](int, const u32x4 (&v)[NQ], bool valid) {
+    float zj[NQ][8], dot = 0.f;
+#pragma unroll
+    for (int q = 0; q < NQ; ++q)
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        const unsigned wv = v[q][p];
+        zj[q][2 * p] = qv[q] ? __uint_as_float(wv << 16) : 0.f;
+        zj[q][2 * p + 1] = qv[q] ? __uint_as_float(wv & 0xFFFF0000u) : 0.f;
+      }
+#pragma unroll
+    for (int q = 0; q < NQ; ++q)
+      if (qv[q]) dot = dot8_bf16(zip[q], v[q], dot);
+    const float Lij = row8_sum(dot);
+    if (!valid) return;
+    float coef;
+    edge_ce_terms(Lij, pw, coef, lossr);
+    lossr -= pw * Lij;
+    tp += Lij > 0.f ? 1u : 0u;
+#pragma unroll
+    for (int q = 0; q < NQ; ++q)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[q][j] += coef * zj[q][j];
+  });
+  // reparameterisation backward of the lane's columns (reparam_bwd_fast_kernel per element)
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) {
+    float dm[8], dl[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { dm[j] = 0.f; dl[j] = 0.f; }
+    const int c0 = 64 * q + 8 * sub;
+    if (rv && qv[q]) {
+      const float* msr = a.ms + (long long)r * a.ldms;
+      const long long ie = (long long)r * L + c0;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const float4 mu = *reinterpret_cast<const float4*>(msr + c0 + 4 * h);
+        const float4 ls = *reinterpret_cast<const float4*>(msr + L + c0 + 4 * h);
+        const float4 ep = *reinterpret_cast<const float4*>(a.eps + ie + 4 * h);
+        float4 dj = *reinterpret_cast<const float4*>(a.dJd + ie + 4 * h);
+        for (int sx = 0; sx < a.nextra; ++sx) {   // zzt_split_sum_kernel's order
+          const float4 x = *reinterpret_cast<const float4*>(a.dJd_extra + (long long)sx * e.R * L + ie + 4 * h);
+          dj.x += x.x; dj.y += x.y; dj.z += x.z; dj.w += x.w;
+        }
+        const float4 dd = *reinterpret_cast<const float4*>(a.dz_dec + ie + 4 * h);
+        const float m4[4] = {mu.x, mu.y, mu.z, mu.w}, l4[4] = {ls.x, ls.y, ls.z, ls.w};
+        const float e4[4] = {ep.x, ep.y, ep.z, ep.w}, j4[4] = {dj.x, dj.y, dj.z, dj.w};
+        const float d4[4] = {dd.x, dd.y, dd.z, dd.w};
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          reparam_bwd_elem(m4[u], l4[u], e4[u], j4[u], acc[q][4 * h + u], d4[u], a.adj_scale, a.kl_scale,
+                           dm[4 * h + u], dl[4 * h + u]);
+      }
+      bf16x8 om, os;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { om[j] = (__bf16)dm[j]; os[j] = (__bf16)dl[j]; }
+      *reinterpret_cast<bf16x8*>(a.dms + (long long)r * a.lddms + c0) = om;
+      *reinterpret_cast<bf16x8*>(a.dms + (long long)r * a.lddms + L + c0) = os;
+    }
+    if (qv[q]) {   // bias sums over the wave's 8 rows (lanes sub, sub + 8, ..., sub + 56)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float sm = dm[j], ss = dl[j];
+        sm += __shfl_xor(sm, 8, 64); sm += __shfl_xor(sm, 16, 64); sm += __shfl_xor(sm, 32, 64);
+        ss += __shfl_xor(ss, 8, 64); ss += __shfl_xor(ss, 16, 64); ss += __shfl_xor(ss, 32, 64);
+        if ((threadIdx.x & 63) < 8) { bred[w][c0 + j] = sm; bred[w][L + c0 + j] = ss; }
+      }
+    }
+  }
+  if (sub != 0 || !rv) { lossr = 0.f; tp = 0; }   // the row's 8 lanes hold the same sums
+  const double l = wave_sum_d((double)lossr);
+  const unsigned t = wave_sum_u(tp);
+  if ((threadIdx.x & 63) == 0) { sl[w] = l; st[w] = t; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double tl = 0.0, tt = 0.0;
+    for (int k = 0; k < NT / 64; ++k) { tl += sl[k]; tt += (double)st[k]; }
+    e.part[2 * blockIdx.x] = tl;
+    e.part[2 * blockIdx.x + 1] = tt;
+  }
+  for (int c = threadIdx.x; c < 2 * L; c += NT) {
+    float v = 0.f;
+#pragma unroll
+    for (int k = 0; k < NT / 64; ++k) v += bred[k][c];
+    a.colpart[(long long)blockIdx.x * 2 * L + c] = v;
+  }
+}
+
 // ---------------------------------------------------------------- reparam + zz^T staging
 // z = mu + eps e^s (model.py:159) with the KL partial (optimizer.py:193), fused
 // with the zz^T staging images: one block = 64 rows of one graph, writes z (fp32,
@@ -777,6 +906,22 @@ int launch_reparam_prep(const ReparamPrepArgs& a, int dp, hipStream_t s) {
     default: set_error("reparam_prep: dp %d", dp); return SND_ERR_ARG;
   }
   SND_LAUNCH_CHECK("reparam_prep_kernel");
+  return 0;
+}
+
+int edge_reparam_blocks(int R) { return cdiv(R, RPB); }
+
+int launch_edge_reparam_bwd(const EdgeBfArgs& e, const ReparamBwdFastArgs& a, hipStream_t s) {
+  if (e.R <= 0) return 0;
+  SND_CHECK_ARG(e.d == a.L && e.R == a.R && e.d % 8 == 0 && e.d <= 128 && e.z && e.part && e.rowptr,
+                "edge_reparam_bwd: edge operands");
+  SND_CHECK_ARG((a.L == 16 || a.L == 32 || a.L == 64 || a.L == 128) && a.ldms % 4 == 0 && a.lddms % 8 == 0,
+                "edge_reparam_bwd: L / leading dims");
+  SND_CHECK_ARG(a.dz_dec && a.dJd && a.eps && a.dms && a.colpart && a.ms, "edge_reparam_bwd: null operand");
+  SND_CHECK_ARG((long long)e.R * e.d * 2 < (1ll << 31), "edge_reparam_bwd: rows x d beyond the 2 GB buffer range");
+  if (a.L > 64) hipLaunchKernelGGL(edge_reparam_bwd_kernel<2>, dim3(edge_reparam_blocks(e.R)), dim3(NT), 0, s, e, a);
+  else hipLaunchKernelGGL(edge_reparam_bwd_kernel<1>, dim3(edge_reparam_blocks(e.R)), dim3(NT), 0, s, e, a);
+  SND_LAUNCH_CHECK("edge_reparam_bwd_kernel");
   return 0;
 }
 

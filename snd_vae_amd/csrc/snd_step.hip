@@ -94,6 +94,7 @@ struct snd_plan {
   bool fast_enc = false;
   bool head_fused = false;     // fused encoder forward tail (snd_head.hip): 1 launch instead of 4
   bool head_bwd = false;       // fused edge terms + encoder backward head (snd_head.hip): 1 instead of 4
+  bool edge_reparam = false;   // without it: per-edge terms + reparam backward in one launch (snd_fast_enc.hip)
   bool front_fused = false;    // gcn0 + H1 W1 + the weight images in one launch (snd_head.hip)
   bool enc0_gather = false;    // A @ dP1 gathered inside the RC_ENC0 launch (no SpMM launch)
   bool small_head = false;     // graph latent: [mu || s] head + reparameterisation (snd_elem.hip small_head_*)
@@ -507,7 +508,7 @@ extern "C" int snd_plan_create(const snd_config_t* cfg, int n_graphs, snd_plan_t
       p->add_buf("FDXW1", R * h1, 2);     p->add_buf("FDP0", R * h0, 2);
       // column partials: the row engine's 128-row blocks, or the backward head's tiles
       const int rcb = std::max(rc_blocks(p->R), head_tiles(p->R));
-      p->add_buf("PFBMS", (long long)reparam_bwd_fast_blocks(p->R, L) * 2 * L);
+      p->add_buf("PFBMS", (long long)std::max(reparam_bwd_fast_blocks(p->R, L), edge_reparam_blocks(p->R)) * 2 * L);
       p->add_buf("PFBH", (long long)rcb * gh);
       p->add_buf("PFENC1", (long long)rcb * 4 * W);
       p->add_buf("PFENC0", (long long)rcb * 2 * h0);
@@ -537,6 +538,9 @@ extern "C" int snd_plan_create(const snd_config_t* cfg, int n_graphs, snd_plan_t
       p->head_bwd = !(dbg & 262144) &&
                     head_bwd_supported(L, gh, W, h1, p->pwmsb.kp, p->pwmsb.np, p->pwhb.kp, p->pwhb.np);
       if (p->head_bwd) p->add_buf("PHBMS", (long long)head_tiles(p->R) * 2 * L);
+      // no fused backward head (L = 128, C5): the per-edge terms ride in the reparameterisation
+      // backward's launch (debug bit 1 << 27: edge_bf16 before zz^T + reparam_bwd_fast)
+      p->edge_reparam = !p->head_bwd && !tref && !(dbg & (1 << 27));
     }
   }
   // GraphConvolution 0, XW1 and the packed weight images in one launch (debug bit 1048576:
@@ -1105,7 +1109,14 @@ int encoder_fast_bwd(const Ctx& x, const snd_batch_t* batch, float adj_scale, fl
     ReparamBwdFastArgs a{x.f("MS"), 2 * L, R, L, x.f("EPS"), x.f("DZDEC"), x.f("DJD"), x.f("EJ"),
                          adj_scale, kl_scale, bf("FDMS"), 2 * L, x.f("PFBMS")};
     a.dJd_extra = x.f("DJDX"); a.nextra = x.zts - 1;   // deferred split sum
-    SND_TRY(launch_reparam_bwd_fast(a, x.s));
+    if (p.edge_reparam) {   // the per-edge terms here, not before zz^T
+      EdgeBfArgs ea{batch->rowptr, batch->colidx, R, reinterpret_cast<const __bf16*>(x.f("ZB")), L, c.pos_weight,
+                    nullptr, x.d("PEDGE"), xcd_nbg(p.N, p.B)};
+      ea.row_order = batch->row_order;
+      SND_TRY(launch_edge_reparam_bwd(ea, a, x.s));
+    } else {
+      SND_TRY(launch_reparam_bwd_fast(a, x.s));
+    }
   }
   SND_TRY(fork(x));
   for (int h = 0; h < 2 * L; h += p.nms)   // [mu | logstd] in nms-column halves
@@ -1195,7 +1206,8 @@ void encoder_fast_reduce(const Ctx& x, std::vector<ReduceDesc>& rd) {
       slab_at(x.f("FSWMS") + (long long)(h / p.nms) * p.gWms.gx * gh * wgrad_n4(p.nms), p.gWms.gx, gh, p.nms,
               x.g("enc.Wms") + h, 2 * L);
     if (p.head_bwd) flat("PHBMS", head_tiles(p.R), 2 * L, 2 * L, "enc.bms", 1.f);
-    else flat("PFBMS", reparam_bwd_fast_blocks(p.R, L), 2 * L, 2 * L, "enc.bms", 1.f);
+    else flat("PFBMS", p.edge_reparam ? edge_reparam_blocks(p.R) : reparam_bwd_fast_blocks(p.R, L), 2 * L, 2 * L,
+              "enc.bms", 1.f);
     slab2d("FSWH", p.gWh.gx, p.kwh, gh, "enc.Wh");
     if (p.kwh < W) slab_at(x.f("FSWHT"), p.gWht.gx, W - p.kwh, gh, x.g("enc.Wh") + (long long)p.kwh * gh, gh);
     flat("PFBH", hcb, gh, gh, "enc.bh", 1.f);
@@ -1815,8 +1827,8 @@ extern "C" int snd_train_step(const snd_plan_t* plan, const snd_batch_t* batch,
   {
     // per-edge terms on the side stream, overlapping the dense kernel / decoder
     SND_TRY(fork(x));
-    if (p.head_bwd) {
-      // per-edge terms run inside head_bwd_kernel (the backward head)
+    if (p.head_bwd || p.edge_reparam) {
+      // per-edge terms run inside head_bwd_kernel (the backward head) / edge_reparam_bwd_kernel
     } else if (p.fast) {
       EdgeBfArgs ea{rp, ci, R, (const __bf16*)x.f("ZB"), dj, c.pos_weight, x.f("EJ"), x.d("PEDGE"),
                     xcd_nbg(N, p.B)};

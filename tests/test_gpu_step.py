@@ -454,6 +454,39 @@ def test_fused_decoder_matches_row_engine(topology, n, d, B):
         assert torch.equal(m1.buffer(name, dt), snap[name]), f"{name} with NaN-poisoned LDS"
 
 
+def test_edge_terms_in_reparam_backward_launch():
+    """d = 128 (no fused backward head, C5's width): the per-edge terms computed inside the
+    reparameterisation backward (edge_reparam_bwd_kernel) against edge_bf16 before zz^T +
+    reparam_bwd_fast (debug bit 1 << 27 at plan creation): d[mu | s], every gradient but
+    the [mu | s] bias (its column sums group rows by the fused kernel's 32-row blocks) and
+    every loss term bitwise equal."""
+    from snd_vae_amd import _lib
+    from snd_vae_amd.params import init_blocks
+    cfg = tscale(2048, 128)
+    batch = synthetic_batch(cfg, 2, seed=41)
+    p0 = init_blocks(cfg, 4)
+    runs = []
+    for flags in (1 << 27, 0):
+        _lib.check(_lib.lib().snd_debug_set(flags))
+        try:
+            m, o, b = make(cfg, batch, p0, "bf16")
+        finally:
+            _lib.check(_lib.lib().snd_debug_set(0))
+        o.forward_backward(b)
+        torch.cuda.synchronize()
+        runs.append((m, o))
+    (m0, o0), (m1, o1) = runs
+    for name, dt in (("FDMS", torch.bfloat16), ("FDH", torch.bfloat16), ("FDP1", torch.bfloat16)):
+        assert torch.equal(m0.buffer(name, dt), m1.buffer(name, dt)), name
+    g0, g1 = o0.grad_blocks(), o1.grad_blocks()
+    for k in g0:
+        if k == "enc.bms":
+            np.testing.assert_allclose(g1[k], g0[k], rtol=1e-5, atol=1e-7 * max(1.0, np.abs(g0[k]).max()), err_msg=k)
+        else:
+            np.testing.assert_array_equal(g1[k], g0[k], err_msg=k)
+    assert torch.equal(o0.losses, o1.losses)
+
+
 HEAD_BUFS = (("FP1", torch.float32), ("FG", torch.bfloat16), ("FHH", torch.bfloat16), ("MS", torch.float32),
              ("Z", torch.float32), ("ZB", torch.bfloat16), ("EPS", torch.float32), ("ZSTAGE", torch.uint8),
              ("DJD", torch.float32), ("FDP1", torch.bfloat16))
