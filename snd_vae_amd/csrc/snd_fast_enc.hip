@@ -716,8 +716,12 @@ __global__ void __launch_bounds__(NT) edge_reparam_bwd_kernel(EdgeBfArgs e, Repa
 // with the zz^T staging images: one block = 64 rows of one graph, writes z (fp32,
 // edge terms), eps, z (bf16, decoder operand), z sqrt(log2 e) (bf16, K role),
 // z^T (bf16, V role, through an LDS transpose) and the per-64-row column sums.
+// (1024 threads: at DP = 128 a 256-thread block ran 8 dependent load -> store rounds per
+// thread over its 64 rows, one workgroup per CU -- latency-bound; now 2)
+constexpr int NTP = 1024;
 template <int DP>
-__global__ void __launch_bounds__(NT) reparam_prep_kernel(ReparamPrepArgs a) {
+__global__ void __launch_bounds__(NTP) reparam_prep_kernel(ReparamPrepArgs a) {
+  constexpr int NT = NTP;
   __shared__ float tile[64][DP + 1];
   __shared__ float stile[64][DP + 1];
   __shared__ double red[NT / 64];
@@ -900,9 +904,9 @@ int launch_reparam_prep(const ReparamPrepArgs& a, int dp, hipStream_t s) {
                 "reparam_prep: null operand");
   dim3 grid(a.npad / 64, a.ngraphs);
   switch (dp) {
-    case 32: hipLaunchKernelGGL((reparam_prep_kernel<32>), grid, dim3(NT), 0, s, a); break;
-    case 64: hipLaunchKernelGGL((reparam_prep_kernel<64>), grid, dim3(NT), 0, s, a); break;
-    case 128: hipLaunchKernelGGL((reparam_prep_kernel<128>), grid, dim3(NT), 0, s, a); break;
+    case 32: hipLaunchKernelGGL((reparam_prep_kernel<32>), grid, dim3(NTP), 0, s, a); break;
+    case 64: hipLaunchKernelGGL((reparam_prep_kernel<64>), grid, dim3(NTP), 0, s, a); break;
+    case 128: hipLaunchKernelGGL((reparam_prep_kernel<128>), grid, dim3(NTP), 0, s, a); break;
     default: set_error("reparam_prep: dp %d", dp); return SND_ERR_ARG;
   }
   SND_LAUNCH_CHECK("reparam_prep_kernel");
