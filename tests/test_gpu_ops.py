@@ -376,8 +376,9 @@ def test_zzt_v10_matches_v7(n, B):
     wave computes the same 32 x 32 logit blocks with the same MFMAs and epilogue and
     combines its partial dJ over the four column blocks in v7's order; the default launch
     splits the columns over workgroups (variant 7 runs one split), so dJ agrees to fp32
-    reassociation of its column sums, the loss to 1e-12 (fp64 partials) and the accuracy
-    count exactly.  N = 1000: partial tiles and padded pairs."""
+    reassociation of its column sums, the loss to 1e-7 (each wave's fp32 tile sums go to
+    fp64 every 2 tiles in v10, every 3 in v7: 6.5e-10 measured) and the accuracy count
+    exactly.  N = 1000: partial tiles and padded pairs."""
     from snd_vae_amd import _lib
     from snd_vae_amd.model import DeviceBatch, SGCNModelVAE
     from snd_vae_amd.optimizer import OptimizerVAE
@@ -400,7 +401,7 @@ def test_zzt_v10_matches_v7(n, B):
         torch.cuda.synchronize()
         out[name] = (pz.view(-1, 2).sum(0).cpu().numpy(), djd.clone().cpu().numpy())
     (s7, d7), (s10, d10) = out["zzt_dense_v7"], out["zzt_dense"]
-    assert s10[0] == pytest.approx(s7[0], rel=1e-12)
+    assert s10[0] == pytest.approx(s7[0], rel=1e-7)
     assert s10[1] == s7[1]
     assert np.abs(d10 - d7).max() <= 1e-5 * np.abs(d7).max()
 
