@@ -39,9 +39,6 @@
 #ifndef SND_ZZT_V9
 #define SND_ZZT_V9 1     // the d = 64 kernel: 1 v9 (two 512-thread workgroups per CU, round 5:
 #endif                   // 55.2 vs v4's 56.7 us), 0 v4, 2 v9 with v7's stagger (55.7 us); A/B builds
-#ifndef SND_ZZT_V10
-#define SND_ZZT_V10 1    // the d = 128 kernel: 1 v10 (two 512-thread workgroups per CU, round 6), 0 v7
-#endif
 
 namespace snd {
 namespace {
@@ -1375,277 +1372,6 @@ zzt_dense_bf16_v9(ZztArgs a) {
   }
 }
 
-// ---------------------------------------------------------------- bf16 MFMA, v10 (d = 128)
-// v9's shape at d = 128: half-size workgroups (512 threads = 2 row groups (64 rows i) x 4
-// column blocks) so that TWO share a CU and one's epilogue VALU issues under the other's
-// MFMAs -- v7 (one 1024-thread workgroup per CU, 128 KB of LDS) runs its matrix and vector
-// phases one after the other (C5: 170 us ~ 110 of epilogue + 55 of MFMA).  Two per CU
-// means <= 80 KB each: a 2-deep ring of v7's [128][128] bf16 tile images (64 KB; tile t + 1
-// DMA'd under tile t) and the -z_i rows (16 KB), and no static LDS at all: the per-row
-// corrections (which read only the z_i rows and the column sums) run in the prologue, with
-// the column sums in ring slot 1 before its first DMA, and the end's scratch (the partial
-// dJ exchange, s'_ii, the wave sums) reuses the ring.  Per wave and tile: v7's 8 forward +
-// 8 backward 32x32x16 MFMAs and epilogue; dJ combined over the four column blocks in two
-// passes of two 32-column output blocks, in v7's order.
-constexpr int NTH10 = 512;
-constexpr int ROWS10 = 64;
-template <bool MEAS>
-__global__ void __launch_bounds__(NTH10) __attribute__((amdgpu_waves_per_eu(4, 4)))
-zzt_dense_bf16_v10(ZztArgs a) {
-  constexpr int DP = 128, NT = NTH10, NW = NT / 64;
-  const int skip = MEAS ? __builtin_amdgcn_readfirstlane(a.variant >> 8) : 0;
-  constexpr int KS = DP / 16;          // forward k-steps
-  constexpr int CB = DP / 32;          // backward 32-column output blocks
-  constexpr int IMG = TJ2 * DP * 2;    // one [128][128] bf16 image, 32 KB
-  constexpr int BROWS = ROWS10 * DP * 2;                        // the -z_i rows, 16 KB
-  __shared__ __attribute__((aligned(16))) char lds[2 * IMG + BROWS];
-  char* brows = lds + 2 * IMG;
-  const unsigned lds0 = (unsigned)(uintptr_t)(zlptr_t)lds;
-
-  const int wgs = a.ngraphs * zrb(a) * 2;
-  const int sp = blockIdx.x / wgs, bx = blockIdx.x - sp * wgs;
-  const int nsplit = gridDim.x / wgs;
-  const int g = bx % a.ngraphs, hb = bx / a.ngraphs;            // hb: 64-row block of the range
-  const int rb = a.rb0 + (hb >> 1), half = hb & 1;              // its 128-row block and half
-  const int r0 = rb * ROWS + ROWS10 * half;                     // first row
-  const __bf16* Jg = reinterpret_cast<const __bf16*>(a.jrow) + (long long)g * a.npad * DP;
-  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, r = lane & 31, h = lane >> 5;
-  const int rg = w & 1, cb = w >> 1;
-  const int i0 = __builtin_amdgcn_readfirstlane(r0 + 32 * rg);
-  const int i_me = i0 + r;
-  const int ntot = a.npad / TJ2;
-  const int t0 = sp * ntot / nsplit, t1 = (sp + 1) * ntot / nsplit;
-
-  // tile t -> ring slot b: 32 pieces of 1 KB, wave w issues pieces w + 8 k (v7's layout:
-  // piece P, lane l lands at row 8 (P >> 1) + ((l >> 2) & 7), chunk
-  // 4 (2 (P & 1) + (l >> 5)) + ((l & 3) ^ ((row >> 2) & 3)))
-  int dsrc[4];
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const int P = w + 8 * k;
-    const int row = 8 * (P >> 1) + ((lane >> 2) & 7);
-    const int ch = 4 * (2 * (P & 1) + (lane >> 5)) + ((lane & 3) ^ ((row >> 2) & 3));
-    dsrc[k] = row * DP + 8 * ch;
-  }
-  auto dma = [&](int t, int b) {
-#pragma unroll
-    for (int k = 0; k < 4; ++k)
-      zdma16(Jg + (long long)t * TJ2 * DP + dsrc[k],
-             __builtin_amdgcn_readfirstlane(lds0 + b * IMG + 1024 * (w + 8 * k)));
-  };
-
-  // ---- prologue: tile t0 in flight into slot 0; the -z_i rows; the column sums in slot 1
-  dma(t0, 0);
-  for (int idx = tid; idx < ROWS10 * (DP / 8); idx += NT) {
-    const int row = idx >> 4, ch = idx & 15;
-    const uint4 u = *reinterpret_cast<const uint4*>(Jg + (long long)(r0 + row) * DP + ch * 8);
-    *reinterpret_cast<uint4*>(brows + zoa(row, ch)) =
-        make_uint4(u.x ^ 0x80008000u, u.y ^ 0x80008000u, u.z ^ 0x80008000u, u.w ^ 0x80008000u);
-  }
-  float* csred = reinterpret_cast<float*>(lds + IMG);           // [NT / DP][DP], slot 1
-  float* colsum = csred + (NT / DP) * DP;                       // [DP], slot 1
-  {
-    const int nrb = a.npad / 64;
-    const int k = tid % DP, grp = tid / DP;
-    float s2 = 0.f;
-    for (int p = grp; p < nrb; p += NT / DP) s2 += a.colpart[((long long)g * nrb + p) * DP + k];
-    csred[grp * DP + k] = s2;
-  }
-  __syncthreads();
-  if (tid < DP) {
-    float s2 = 0.f;
-    for (int p = 0; p < NT / DP; ++p) s2 += csred[p * DP + tid];
-    colsum[tid] = s2;
-  }
-  __syncthreads();   // brows and colsum written
-
-  // forward operand bases (k-step s: base[s & 1] + 512 (s >> 1))
-  const int ja = 32 * cb + r, ia = 32 * rg + r;
-  const int fa0 = zoa(ja, h), fa1 = zoa(ja, 2 + h);
-  const int fb0 = zoa(ia, h), fb1 = zoa(ia, 2 + h);
-
-  // ---- per-row corrections (row i_me; lanes r and r + 32 hold its two k halves): the
-  // diagonal pair and the column-sum term, from the z_i rows alone (v7 computes them after
-  // the tiles)
-  double ltot = 0.0;
-  float dsg_me = 0.f;
-  unsigned dpos;
-  {
-    float xd = 0.f, xs = 0.f;
-#pragma unroll
-    for (int s2 = 0; s2 < KS; ++s2) {
-      const bf16x8 bv = *reinterpret_cast<const bf16x8*>(brows + ((s2 & 1) ? fb1 : fb0) + 512 * (s2 >> 1));
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const float bb = (float)bv[e];
-        xd += bb * bb;
-        xs += bb * colsum[16 * s2 + 8 * h + e];
-      }
-    }
-    xd += __shfl_xor(xd, 32, 64);
-    xs += __shfl_xor(xs, 32, 64);
-    xs = -xs;
-    const bool row_valid = i_me < a.n;
-    const bool corr = sp == 0;
-    const bool own = cb == 0 && h == 0 && row_valid && corr;
-    const float exd = __builtin_amdgcn_exp2f(-fabsf(xd));
-    if (own) {
-      ltot += (double)xs;
-      ltot -= (double)(fmaxf(xd, 0.f) + __builtin_amdgcn_logf(1.f + exd));
-    }
-    dpos = (unsigned)__popcll(__ballot(own && xd > 0.f));
-    // s'_ii as the backward MFMA consumed it (bf16), 0 outside split 0 (lanes cb 0, h 0)
-    const float sg = __builtin_amdgcn_rcpf(__builtin_amdgcn_exp2f(-xd) + 1.f);
-    dsg_me = corr ? (float)(__bf16)sg : 0.f;
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // tile t0 landed
-  __syncthreads();   // and slot 1 (the column sums) is free
-
-  f32x16 acc[CB];
-#pragma unroll
-  for (int q = 0; q < CB; ++q)
-#pragma unroll
-    for (int v = 0; v < 16; ++v) acc[q][v] = 0.f;
-  const int gq = lane >> 4, qq = (lane >> 2) & 3, pp = lane & 3;
-  const int c0 = 2 * (gq & 1) + (pp >> 1);
-  const int tb0 = 2048 * (4 * cb) + 64 * (4 * (gq >> 1) + qq) + 16 * (c0 ^ (gq >> 1)) + 8 * (pp & 1);
-  const int tb1 = 2048 * (4 * cb + 1) + 64 * (4 * (gq >> 1) + qq) + 16 * (c0 ^ ((gq >> 1) + 2)) + 8 * (pp & 1);
-  auto fwd = [&](int b) {
-    f32x16 X;
-#pragma unroll
-    for (int v = 0; v < 16; ++v) X[v] = 0.f;
-    const char* T = lds + b * IMG;
-#pragma unroll
-    for (int s2 = 0; s2 < KS; ++s2) {
-      const bf16x8 av = *reinterpret_cast<const bf16x8*>(T + ((s2 & 1) ? fa1 : fa0) + 512 * (s2 >> 1));
-      const bf16x8 bv = *reinterpret_cast<const bf16x8*>(brows + ((s2 & 1) ? fb1 : fb0) + 512 * (s2 >> 1));
-      X = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, bv, X, 0, 0, 0);
-    }
-    return X;
-  };
-  float lacc = 0.f;
-  unsigned lcnt = 0;
-  bool ovf = false;   // sticky per wave, as v9
-  auto epi = [&](const f32x16& Y, bf16x8 (&sA)[2]) {   // v7's epilogue, y = -x
-    if (MEAS && (skip & 1)) {
-#pragma unroll
-      for (int v = 0; v < 16; ++v) sA[v >> 3][v & 7] = (__bf16)Y[v];
-      return;
-    }
-    float q[16], lt = 0.f;
-#pragma unroll
-    for (int v = 0; v < 16; ++v) {
-      const float e = __builtin_amdgcn_exp2f(Y[v]);
-      q[v] = e + 1.f;
-      sA[v >> 3][v & 7] = (__bf16)__builtin_amdgcn_rcpf(q[v]);
-    }
-#pragma unroll
-    for (int g4 = 0; g4 < 4; ++g4) {
-      const unsigned t01 = __builtin_amdgcn_perm(__float_as_uint(Y[4 * g4 + 1]),
-                                                 __float_as_uint(Y[4 * g4]), 0x0C0C0703u);
-      const unsigned t23 = __builtin_amdgcn_perm(__float_as_uint(Y[4 * g4 + 3]),
-                                                 __float_as_uint(Y[4 * g4 + 2]), 0x07030C0Cu);
-      lcnt += (unsigned)__builtin_popcount((t01 | t23) & 0x80808080u);
-    }
-    if (!ovf) {
-#pragma unroll
-      for (int p = 0; p < 4; ++p)
-        lt += __builtin_amdgcn_logf((q[4 * p] * q[4 * p + 1]) * (q[4 * p + 2] * q[4 * p + 3]));
-      ovf = __builtin_amdgcn_ballot_w64(!__builtin_isfinite(lt)) != 0;
-    }
-    if (__builtin_expect(ovf, 0)) {
-      lt = 0.f;
-#pragma unroll
-      for (int v = 0; v < 16; ++v) lt += Y[v] > 24.f ? Y[v] : __builtin_amdgcn_logf(q[v]);
-    }
-    lacc += lt;
-  };
-  auto bwd = [&](int b, const bf16x8 (&sA)[2]) {
-    if (MEAS && (skip & 4)) { lacc += (float)sA[0][0]; return; }
-    const char* T = lds + b * IMG;
-#pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-      for (int q = 0; q < CB; ++q) {
-        const bf16x8 bv = ztr_pair(T + tb0 + 4096 * s2 + 512 * q, T + tb1 + 4096 * s2 + 512 * q);
-        acc[q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(sA[s2], bv, acc[q], 0, 0, 0);
-      }
-  };
-  // tile t in slot CUR: DMA of tile t + 1 into the other slot (tile t - 1's: every wave
-  // passed the barrier that closed it), forward, epilogue, backward; wait, barrier
-  auto tile = [&](int t, auto cc) {
-    constexpr int CUR = decltype(cc)::value;
-    if (t + 1 < t1) dma(t + 1, CUR ^ 1);
-    const f32x16 Y = fwd(CUR);
-    bf16x8 sA[2];
-    epi(Y, sA);
-    bwd(CUR, sA);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // tile t + 1 landed
-    __syncthreads();
-  };
-  for (int t = t0; t < t1; t += 2) {
-    tile(t, std::integral_constant<int, 0>{});
-    if (t + 1 < t1) tile(t + 1, std::integral_constant<int, 1>{});
-    ltot += (double)lacc;
-    lacc = 0.f;
-  }
-
-  // ---- combine the four column blocks' partial dJ (fixed order) through the ring, two
-  // 32-column output blocks per pass (48 KB); the diagonal term subtracted with the scaled
-  // z_i the backward products used, then the sqrt(log2 e) scale removed.  (The last tile's
-  // barrier closed every read of the ring; no DMA is in flight.)
-  float* red = reinterpret_cast<float*>(lds);        // [cb-1][rg][2 * 16][64]
-  float* dsg = reinterpret_cast<float*>(lds + 3 * 2 * 32 * 64 * 4);   // [2][32], past red
-  if (cb == 0 && h == 0) dsg[rg * 32 + r] = dsg_me;
-  float* dst = (sp == 0 ? a.dJd : a.dJd_extra + (long long)(sp - 1) * a.ngraphs * a.n * a.d) +
-               (long long)g * a.n * a.d;
-  const __bf16* zi = Jg + (long long)(r0 + 32 * rg) * DP;
-#pragma unroll
-  for (int pass = 0; pass < 2; ++pass) {
-    if (cb > 0) {
-#pragma unroll
-      for (int qh = 0; qh < 2; ++qh)
-#pragma unroll
-        for (int v = 0; v < 16; ++v)
-          red[(((cb - 1) * 2 + rg) * 32 + qh * 16 + v) * 64 + lane] = acc[2 * pass + qh][v];
-    }
-    __syncthreads();
-    if (cb == 0) {
-#pragma unroll
-      for (int qh = 0; qh < 2; ++qh) {
-        const int c = 32 * (2 * pass + qh) + r;
-#pragma unroll
-        for (int v = 0; v < 16; ++v) {
-          float o = acc[2 * pass + qh][v];
-#pragma unroll
-          for (int k = 0; k < 3; ++k) o += red[((k * 2 + rg) * 32 + qh * 16 + v) * 64 + lane];
-          const int il = (v & 3) + 8 * (v >> 2) + 4 * h;   // D row within the row group
-          const int i = i0 + il;
-          if (i < a.n && c < a.d)
-            dst[(long long)i * a.d + c] = (o - dsg[rg * 32 + il] * (float)zi[il * DP + c]) * kInvSqrtLog2e;
-        }
-      }
-    }
-    __syncthreads();
-  }
-  double* sl = reinterpret_cast<double*>(lds);       // [NW], the ring again
-  unsigned* sc = reinterpret_cast<unsigned*>(lds + NW * sizeof(double));
-  const double l = wave_sum_d(ltot);
-  const unsigned wcnt = wave_sum_u(lcnt);
-  if (lane == 0) { sl[w] = l; sc[w] = wcnt - dpos; }
-  __syncthreads();
-  if (tid == 0) {
-    double tl = 0.0, tc = 0.0;
-    for (int k = 0; k < NW; ++k) { tl += sl[k]; tc += (double)sc[k]; }
-    if (sp == 0) {   // padded pairs of this 64-row block: x = 0 exactly, softplus2(0) = 1 each
-      const int valid = max(0, min(ROWS10, a.n - r0));
-      tl -= (double)ROWS10 * a.npad - (double)valid * a.n;
-    }
-    a.part[2 * blockIdx.x] = tl * (double)kLn2;
-    a.part[2 * blockIdx.x + 1] = tc;
-  }
-}
-
 // dJd += sum of the column-split partials (fixed order)
 __global__ void zzt_split_sum_kernel(float* dJd, const float* extra, long long n, long long stride,
                                      int nextra) {
@@ -1714,9 +1440,7 @@ int zzt_tsplit_blocks(int wgs, int n, int dtype) {
   // 0.1546 -> 0.1512 ms against 4 splits; B = 2 unchanged at 4)
   return std::max(1, std::min({cdiv(ncu, wgs), 8, ntiles}));
 }
-int zzt_wpb(int d, int dtype) {
-  return dtype == SND_BF16 && ((SND_ZZT_V9 && zzt_dp(d) == 64) || (SND_ZZT_V10 && zzt_dp(d) == 128)) ? 2 : 1;
-}
+int zzt_wpb(int d, int dtype) { return (SND_ZZT_V9 && dtype == SND_BF16 && zzt_dp(d) == 64) ? 2 : 1; }
 int zzt_dense_blocks(int ngraphs, int n, int d, int dtype) {
   return ngraphs * (zzt_npad(n) / ROWS) * zzt_tsplit(ngraphs, n, dtype) * zzt_wpb(d, dtype);
 }
@@ -1786,9 +1510,7 @@ int launch_zzt_dense(const ZztArgs& a, int dtype, hipStream_t s, bool defer_spli
       if (dp == 32) hipLaunchKernelGGL((zzt_dense_bf16_v4<32, false>), grid, dim3(NTH2), 0, s, a);
       else hipLaunchKernelGGL((zzt_dense_bf16_v4<64, false>), grid, dim3(NTH2), 0, s, a);
     }
-  } else if (dtype == SND_BF16 && dp == 128 && SND_ZZT_V10 && a.variant == 0) {   // v10 (d = 128)
-    hipLaunchKernelGGL((zzt_dense_bf16_v10<false>), dim3(grid.x * 2), dim3(NTH10), 0, s, a);
-  } else if (dtype == SND_BF16) {                     // v7 (d = 128; variant 7 / measurement, or SND_ZZT_V10 0)
+  } else if (dtype == SND_BF16) {                     // v7 (d = 128)
     if (a.variant >= 256) hipLaunchKernelGGL((zzt_dense_bf16_v7<true>), grid, dim3(NTH2), 0, s, a);
     else hipLaunchKernelGGL((zzt_dense_bf16_v7<false>), grid, dim3(NTH2), 0, s, a);
   } else {

@@ -414,8 +414,7 @@ def test_reduce_adam_option(lib_built):
 KNOWN_SPILLS = {
     "spmm_bf16_tiled_kernelILi1ELi1ELi1E": 4, "spmm_bf16_tiled_kernelILi1ELi1ELi2E": 30,
     "zzt_dense_bf16ILi128E": 0, "zzt_dense_f32ILi128E": 42,
-    "zzt_dense_bf16_v7": 2,            # C5's zz^T until round 6 (variant 7 since)
-    "zzt_dense_bf16_v10": 1,           # C5's zz^T (round 6; prologue / combine, not the tile loop)
+    "zzt_dense_bf16_v7": 2,            # C5's zz^T
     "rowconv_kernelILi3ELi4E": 6,      # RC_ENC1 at 4 column blocks (C5 widths)
 }
 
