@@ -17,7 +17,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--graphs", type=int, default=8)
     ap.add_argument("--flags", default="0", help="extra measurement-only debug bits, comma list")
-    ap.add_argument("--per-seg", type=int, default=64, help="items per segment (C2: 64 row chunks)")
+    ap.add_argument("--per-seg", default="64",
+                    help="items per segment (C2: 64 row chunks), or a comma list, one count per segment")
     args = ap.parse_args()
     import numpy as np
     import torch
@@ -67,7 +68,8 @@ def main():
                 print(f"  {names[a_]:>9s} -> {names[b_]:9s} median {np.median(d):6.2f}  p90 {np.percentile(d, 90):6.2f}  n {len(d)}")
         # per segment (items are numbered segment-major; --per-seg items per segment)
         idx = np.nonzero(raw[:n * 12].reshape(n, 12)[:, 9] != 0)[0]
-        seg = idx // args.per_seg
+        ps = [int(v) for v in args.per_seg.split(",")]
+        seg = idx // ps[0] if len(ps) == 1 else np.searchsorted(np.cumsum(ps), idx, side="right")
         for sg in np.unique(seg):
             m = seg == sg
             lf = rel[m, 9] - rel[m, 0]
