@@ -380,17 +380,11 @@ extern "C" int snd_plan_create(const snd_config_t* cfg, int n_graphs, snd_plan_t
 #ifndef SND_WGC_SMALL
 #define SND_WGC_SMALL 32   // A/B builds: -DSND_WGC_SMALL=16
 #endif
-#ifndef SND_WGC_T1
-#define SND_WGC_T1 64   // A/B builds: chunks of the k = 1 weights at >= 32768 rows
-#endif
-#ifndef SND_WGC_T5
-#define SND_WGC_T5 64   // A/B builds: chunks of the k = 5 conv weights at >= 32768 rows
-#endif
+  // Per-width counts at C2 (32 or 48 chunks for the k = 1 weights, 96 for the k = 5
+  // convolutions) measured slower: wgrad_multi 26.9-30.4 vs 23.7 us
+  // (profiles/r06_ab_wgrad_chunks.txt).
   const int wgc = (dbg & (4096 | 8192)) ? 0 : ((dbg & 16384) ? 32 : (R < 32768 ? SND_WGC_SMALL : 64));
-  auto wgc_of = [&](int T, int, int) {
-    if (wgc != 64) return wgc;
-    return T == 1 ? SND_WGC_T1 : SND_WGC_T5;
-  };
+  auto wgc_of = [&](int, int, int) { return wgc; };
   // ---- bf16 fast decoder: split [s | n] column layouts, packed weight images
   if (c.dtype == SND_BF16 && !sg && !(debug_flags() & 256)) {
     const ColMap m1 = colmap_split(c.s1, c.n1), m2 = colmap_split(c.s2, c.n2);
