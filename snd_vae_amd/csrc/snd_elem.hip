@@ -433,24 +433,14 @@ __global__ void __launch_bounds__(256) reduce_kernel(ReducePack pk, FinalizeArgs
     int p = pl;
     // 8 loads in flight per round (the 64-part weight slabs at 8 part lanes: one round
     // trip instead of two); the adds stay in part order
-#ifndef SND_RED_RL
-#define SND_RED_RL 8
-#endif
-    for (; p + (SND_RED_RL - 1) * PL < d.nparts; p += SND_RED_RL * PL) {
-      float v[SND_RED_RL];
+    // (16 or 32 loads per round, i.e. 1-2 rounds per thread, measured no faster:
+    // profiles/r06_ab_reduce_rounds.txt)
+    for (; p + 7 * PL < d.nparts; p += 8 * PL) {
+      float v[8];
 #pragma unroll
-      for (int u = 0; u < SND_RED_RL; ++u) v[u] = src[(long long)(p + u * PL) * d.stride];
+      for (int u = 0; u < 8; ++u) v[u] = src[(long long)(p + u * PL) * d.stride];
 #pragma unroll
-      for (int u = 0; u < SND_RED_RL; ++u) acc += (double)v[u];
-    }
-    if constexpr (SND_RED_RL > 8) {
-      for (; p + 7 * PL < d.nparts; p += 8 * PL) {
-        float v[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) v[u] = src[(long long)(p + u * PL) * d.stride];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) acc += (double)v[u];
-      }
+      for (int u = 0; u < 8; ++u) acc += (double)v[u];
     }
     for (; p + 3 * PL < d.nparts; p += 4 * PL) {
       const float v0 = src[(long long)p * d.stride];
