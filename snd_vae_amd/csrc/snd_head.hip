@@ -681,10 +681,6 @@ __global__ void __launch_bounds__(1024) enc_front_kernel(FrontArgs a) {
     if (i < pack_chunks(d)) pack_chunk(d, i);
     return;
   }
-#ifdef SND_FRONT_PRIO
-  // A/B: the tiles' waves ahead of the pack workgroups' on the 27 CUs they share (C2)
-  __builtin_amdgcn_s_setprio(SND_FRONT_PRIO);
-#endif
   extern __shared__ __attribute__((aligned(16))) char smem[];
   __shared__ float sp[6][128];     // W0 rows (f <= 4), gamma0 * c, beta0
   __bf16* wimg = reinterpret_cast<__bf16*>(smem);
