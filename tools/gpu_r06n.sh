@@ -1,7 +1,8 @@
 #!/bin/bash
 # Round 6, session N: zz^T v10 (d = 128: two 512-thread workgroups per CU) -- the zz^T,
 # C5 and row-sharded tests, then the C5 step and the zz^T launch against v7
-# (ab/v7.so, -DSND_ZZT_V10=0), alternating processes.
+# (ab/v7.so, -DSND_ZZT_V10=0), alternating processes.  v10 lost and was reverted
+# (profiles/r06_ab_zzt_v10_c5.txt); the script needs commit 7e251ff's tree.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out
