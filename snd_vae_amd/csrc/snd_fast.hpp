@@ -160,6 +160,9 @@ struct Gcn0Args {
   float* ax; __bf16* axb;
   int xcd_nbg;                // xcd_nbg(): row blocks per graph for the XCD-aware order
   const int* row_order;       // optional processing order of the rows (locality schedule)
+  // the step's packed weight images, built by extra workgroups of the same launch (as
+  // enc_front does) when npack > 0; pack_blk is filled by launch_gcn0
+  PackDesc pack[kMaxPack]; int pack_blk[kMaxPack + 1]; int npack;
 };
 int xcd_nbg(int npg, int ngraphs);
 int gcn0_blocks(int R);

@@ -12,6 +12,7 @@
 // GraphConvolution 1 epilogue (lrelu -> BN -> concat X -> encoder_g BN).
 #include "snd_fast.hpp"
 #include "snd_gather.hpp"
+#include "snd_pack.hpp"
 
 #include <algorithm>
 
@@ -43,6 +44,17 @@ __device__ __forceinline__ int xcd_rowblock(int b, int nbg) {
 
 // ---------------------------------------------------------------- GCN layer 0
 __global__ void __launch_bounds__(NT) gcn0_kernel(Gcn0Args a) {
+  const int nrb = (a.R + RPB - 1) / RPB;
+  if ((int)blockIdx.x >= nrb) {   // the weight images (pack_kernel's work, bit for bit)
+    const int pb = blockIdx.x - nrb;
+    int s = 0;
+    while (s + 1 < a.npack && pb >= a.pack_blk[s + 1]) ++s;
+    s = __builtin_amdgcn_readfirstlane(s);
+    const PackDesc& d = a.pack[s];
+    const int i = (pb - a.pack_blk[s]) * NT + threadIdx.x;
+    if (i < pack_chunks(d)) pack_chunk(d, i);
+    return;
+  }
   __shared__ float sp[6][128];     // W0 rows (f <= 4), gamma0 * c, beta0
   for (int i = threadIdx.x; i < a.h0; i += NT) {
 #pragma unroll
@@ -802,13 +814,25 @@ int xcd_nbg(int npg, int ngraphs) {
   return (npg % RPB == 0 && ngraphs % 8 == 0) ? npg / RPB : 0;
 }
 
-int launch_gcn0(const Gcn0Args& a, hipStream_t s) {
-  if (a.R <= 0) return 0;
+int launch_gcn0(const Gcn0Args& a0, hipStream_t s) {
+  if (a0.R <= 0) return 0;
+  Gcn0Args a = a0;
+  SND_CHECK_ARG(a.npack >= 0 && a.npack <= kMaxPack, "gcn0: at most %d packed images", kMaxPack);
+  int pb = 0;
+  for (int i = 0; i < a.npack; ++i) {
+    const PackDesc& x = a.pack[i];
+    SND_CHECK_ARG((x.kp == 32 || x.kp == 64 || x.kp == 128 || x.kp == 256) && x.np % 16 == 0 && x.np > 0 &&
+                      x.T >= 1 && x.nsrc >= 1 && x.nsrc <= 2 && x.dst,
+                  "gcn0: bad pack descriptor %d (kp %d np %d T %d)", i, x.kp, x.np, x.T);
+    a.pack_blk[i] = pb;
+    pb += cdiv(pack_chunks(x), NT);
+  }
+  a.pack_blk[a.npack] = pb;
   SND_CHECK_ARG(a.f >= 1 && a.f <= 4 && a.h0 % 8 == 0 && a.h0 <= 128 && a.ldh1 % 8 == 0 &&
                     a.ldh1 >= a.h0 + 8,
                 "gcn0: f in 1..4, h0 %% 8 (<= 128), ldh1 >= h0 + 8");
   SND_CHECK_ARG(a.rowptr && a.x && a.w0 && a.g0 && a.b0 && a.h1 && a.ax && a.axb, "gcn0: null operand");
-  hipLaunchKernelGGL(gcn0_kernel, dim3(gcn0_blocks(a.R)), dim3(NT), 0, s, a);
+  hipLaunchKernelGGL(gcn0_kernel, dim3(gcn0_blocks(a.R) + pb), dim3(NT), 0, s, a);
   SND_LAUNCH_CHECK("gcn0_kernel");
   return 0;
 }

@@ -96,6 +96,7 @@ struct snd_plan {
   bool head_bwd = false;       // fused edge terms + encoder backward head (snd_head.hip): 1 instead of 4
   bool edge_reparam = false;   // without it: per-edge terms + reparam backward in one launch (snd_fast_enc.hip)
   bool front_fused = false;    // gcn0 + H1 W1 + the weight images in one launch (snd_head.hip)
+  bool pack_in_gcn0 = false;   // else the weight images inside the gcn0 launch (no pack_kernel)
   bool enc0_gather = false;    // A @ dP1 gathered inside the RC_ENC0 launch (no SpMM launch)
   bool small_head = false;     // graph latent: [mu || s] head + reparameterisation (snd_elem.hip small_head_*)
   int ldh1 = 0, ldg = 0;
@@ -549,6 +550,7 @@ extern "C" int snd_plan_create(const snd_config_t* cfg, int n_graphs, snd_plan_t
   // GraphConvolution 0, XW1 and the packed weight images in one launch (debug bit 1048576:
   // pack + gcn0 + a row-engine launch)
   p->front_fused = p->fast_enc && !(dbg & 1048576) && front_supported(c.f_in, c.h0, c.h1, p->pw1f.kp, p->pw1f.np);
+  p->pack_in_gcn0 = p->fast && p->fast_enc && !p->front_fused && !p->sg && !(dbg & (1 << 28));
   // the GCN1 backward SpMM A @ dP1 inside the RC_ENC0 launch that consumes it (round 5;
   // debug bit 128: the separate SpMM launch)
   p->enc0_gather = p->fast_enc && !(dbg & 128) && c.h1 == 64 && p->pw1b.kp == 64 && c.f_in <= 4;
@@ -1011,6 +1013,7 @@ int encoder_fast_fwd(const Ctx& x, const snd_batch_t* batch) {
                x.w("enc.bn0.gamma"), x.w("enc.bn0.beta"), h0, bf("FH1"), p.ldh1, x.f("AX"), bf("AXB"),
                xcd_nbg(p.N, p.B)};
     a.row_order = batch->row_order;
+    if (p.pack_in_gcn0) a.npack = build_packs(x, a.pack);
     SND_TRY(launch_gcn0(a, x.s));
   }
   if (!p.front_fused) {   // p.kw1 < h0 + f: the X columns as the K tail
@@ -1760,7 +1763,8 @@ extern "C" int snd_train_step(const snd_plan_t* plan, const snd_batch_t* batch,
   if (p.fast) {
     SND_TRY(fast_init_attributes());
     // bf16 weight images of this step's parameters (inside the encoder front when fused)
-    if (!p.front_fused) SND_TRY(pack_decoder(x));
+    // (or inside the gcn0 launch: C5 step -X us, debug bit 1 << 28 restores pack_kernel)
+    if (!p.front_fused && !p.pack_in_gcn0) SND_TRY(pack_decoder(x));
   }
 
   // =============================== forward ===============================

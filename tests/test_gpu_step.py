@@ -487,6 +487,39 @@ def test_edge_terms_in_reparam_backward_launch():
     assert torch.equal(o0.losses, o1.losses)
 
 
+@pytest.mark.parametrize("n,B", [(2048, 2), (1000, 1)])
+def test_weight_images_inside_gcn0_launch(n, B):
+    """d = 128 (C5's widths: the encoder front is not fused, gcn0 runs): the step's packed
+    weight images built by extra workgroups of the gcn0 launch against pack_kernel before
+    it (debug bit 1 << 28 at plan creation).  Two Adam steps (the second packs the updated
+    parameters): every gradient block, the parameters and every loss term bitwise equal."""
+    from snd_vae_amd import _lib
+    from snd_vae_amd.params import init_blocks
+    cfg = tscale(n, 128)
+    batch = synthetic_batch(cfg, B, seed=43)
+    p0 = init_blocks(cfg, 5)
+    runs = []
+    for flags in (1 << 28, 0):
+        _lib.check(_lib.lib().snd_debug_set(flags))
+        try:
+            m, o, b = make(cfg, batch, p0, "bf16")
+        finally:
+            _lib.check(_lib.lib().snd_debug_set(0))
+        losses = []
+        for _ in range(2):
+            o.step(b)
+            torch.cuda.synchronize()
+            losses.append(o.losses.clone())
+        runs.append((m, o, losses))
+    (m0, o0, l0), (m1, o1, l1) = runs
+    for a, c in zip(l0, l1):
+        assert torch.equal(a, c)
+    g0, g1 = o0.grad_blocks(), o1.grad_blocks()
+    for k in g0:
+        np.testing.assert_array_equal(g1[k], g0[k], err_msg=k)
+    assert torch.equal(m0.params, m1.params)
+
+
 HEAD_BUFS = (("FP1", torch.float32), ("FG", torch.bfloat16), ("FHH", torch.bfloat16), ("MS", torch.float32),
              ("Z", torch.float32), ("ZB", torch.bfloat16), ("EPS", torch.float32), ("ZSTAGE", torch.uint8),
              ("DJD", torch.float32), ("FDP1", torch.bfloat16))
