@@ -365,6 +365,9 @@ __global__ void __launch_bounds__(256) enc_bwd_kernel(EncBwdArgs a, int rows) {
 #ifndef SND_RED_PLS
 #define SND_RED_PLS 4  // part lanes of a < 64-part partial
 #endif
+#ifndef SND_RED_PLW
+#define SND_RED_PLW SND_RED_PLS   // A/B builds: part lanes of a < 64-part slab of >= kRedWide items
+#endif
 constexpr long long kRedWide = 2048;
 // part lanes of a descriptor (uniform per block): a thread sums nparts / PL parts in a
 // dependent chain, so the many-part partials (C4's split-K head / projection slabs, ~1000
@@ -372,7 +375,7 @@ constexpr long long kRedWide = 2048;
 // (the per-tile column sums of the BN parameters) keeps 8 lanes, a wide weight slab 2
 __host__ __device__ __forceinline__ int red_pl(int nparts, long long items) {
   return nparts >= 1024 ? 64
-                        : (nparts >= 256 ? 32 : (nparts >= 64 ? (items >= kRedWide ? SND_RED_PL : 8) : SND_RED_PLS));
+                        : (nparts >= 256 ? 32 : (nparts >= 64 ? (items >= kRedWide ? SND_RED_PL : 8) : (items >= kRedWide ? SND_RED_PLW : SND_RED_PLS)));
 }
 struct ReducePack {
   ReduceDesc d[kMaxReduce];
