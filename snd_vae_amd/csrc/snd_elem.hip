@@ -366,7 +366,9 @@ __global__ void __launch_bounds__(256) enc_bwd_kernel(EncBwdArgs a, int rows) {
 #define SND_RED_PLS 4  // part lanes of a < 64-part partial
 #endif
 #ifndef SND_RED_PLW
-#define SND_RED_PLW SND_RED_PLS   // A/B builds: part lanes of a < 64-part slab of >= kRedWide items
+#define SND_RED_PLW 2  // part lanes of a < 64-part slab of >= kRedWide items (C5 and one-graph 32-chunk
+                       // weight slabs; round 6: C5 0.3668-0.3694 -> 0.3635-0.3658 ms at 2, 1 alike,
+                       // profiles/r06_ab_c5_pack_gcn0_reduce_lanes.txt)
 #endif
 constexpr long long kRedWide = 2048;
 // part lanes of a descriptor (uniform per block): a thread sums nparts / PL parts in a

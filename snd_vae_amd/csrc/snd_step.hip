@@ -1763,7 +1763,7 @@ extern "C" int snd_train_step(const snd_plan_t* plan, const snd_batch_t* batch,
   if (p.fast) {
     SND_TRY(fast_init_attributes());
     // bf16 weight images of this step's parameters (inside the encoder front when fused)
-    // (or inside the gcn0 launch: C5 step -X us, debug bit 1 << 28 restores pack_kernel)
+    // (or inside the gcn0 launch: C5 step 0.3726-0.3730 -> 0.3658-0.3683 ms, debug bit 1 << 28 restores pack_kernel)
     if (!p.front_fused && !p.pack_in_gcn0) SND_TRY(pack_decoder(x));
   }
 
