@@ -183,26 +183,20 @@ __global__ void __launch_bounds__(RCT) rowconv_kernel(RcArgs a) {
     // ---- x rows [r0 - H, r0 - H + XR), zero outside [glo, ghi)
     bool gathered = false;
     if constexpr (EPI == RC_ENC0 && NBH <= 2) {   // (np <= 64: the wide instances keep their registers)
-      if (a.g_rowptr) {   // x = A @ x rows (T = 1, kp = 64 or 128: 8 lanes x 16 B per 64-column half)
+      if (a.g_rowptr) {   // x = A @ x rows (T = 1, kp = 64: 8 lanes x 16 B per row)
         gathered = true;
         const int rs = tid >> 3, sub = tid & 7;
         const int gr = r0 + rs;
-        // one gather pass per 64-column half of the row (C5's 128-wide dP1: two passes keep
-        // the in-flight loads at 16 per lane; every window of the launch gathers its rows)
-        for (int hh = 0; hh < (kp >> 6); ++hh) {
-          float acc8[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-          if (gr < rend) {
-            const __amdgpu_buffer_rsrc_t rsx =
-                rows_rsrc(reinterpret_cast<const __bf16*>(a.x) + 64 * hh, (long long)a.R * a.ldx * 2 - 128 * hh);
-            gather_rows16<1>(a.g_colidx, a.g_rowptr[gr], a.g_rowptr[gr + 1], rsx, 2u * a.ldx, sub,
-                             [&](int, const u32x4 (&v)[1], bool) { acc8v(acc8, v[0]); });
-          }
-          const uint4 o = to_bf16x8(acc8);
-          const int c = 8 * hh + sub;   // the lane's 16-byte chunk of the row
-          *reinterpret_cast<uint4*>(xs + rs * kp + ((c ^ swz(rs, kp)) << 3)) = o;
-          if (gr < rend && 8 * c < a.K)
-            *reinterpret_cast<uint4*>(reinterpret_cast<__bf16*>(a.gout) + (long long)gr * a.ldgo + 8 * c) = o;
+        float acc8[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        if (gr < rend) {
+          const __amdgpu_buffer_rsrc_t rsx = rows_rsrc(a.x, (long long)a.R * a.ldx * 2);
+          gather_rows16<1>(a.g_colidx, a.g_rowptr[gr], a.g_rowptr[gr + 1], rsx, 2u * a.ldx, sub,
+                           [&](int, const u32x4 (&v)[1], bool) { acc8v(acc8, v[0]); });
         }
+        const uint4 o = to_bf16x8(acc8);
+        *reinterpret_cast<uint4*>(xs + rs * kp + ((sub ^ swz(rs, kp)) << 3)) = o;
+        if (gr < rend && 8 * sub < a.K)
+          *reinterpret_cast<uint4*>(reinterpret_cast<__bf16*>(a.gout) + (long long)gr * a.ldgo + 8 * sub) = o;
       }
     }
     if (!gathered && !(kdbg(a.dbg) & 2)) {
@@ -947,10 +941,9 @@ int launch_rowconv(const RcArgs& a0, int epi, hipStream_t s) {
   SND_CHECK_ARG(a.x && a.wpk && a.out && a.zero && a.x_bf16, "rowconv: null operand / fp32 x");
   SND_CHECK_ARG(!a.colpart || (a.ncp >= 1 && a.ncp <= 4), "rowconv: ncp");
   SND_CHECK_ARG(a.npg > 0, "rowconv: npg");
-  if (a.g_rowptr) a.npb = std::min(a.npb, 64);   // the gathering instances are the <= 64-column ones
-  SND_CHECK_ARG(!a.g_rowptr || (epi == RC_ENC0 && a.T == 1 && (a.kp == 64 || a.kp == 128) && a.K <= a.kp &&
-                                a.g_colidx && a.gout && a.ldgo % 8 == 0 && a.ldx % 8 == 0 && a.npb <= 64),
-                "rowconv: the gathered x rows need RC_ENC0, T 1, kp 64 or 128, <= 64-column windows");
+  SND_CHECK_ARG(!a.g_rowptr || (epi == RC_ENC0 && a.T == 1 && a.kp == 64 && a.K <= 64 && a.np <= 64 && a.g_colidx &&
+                                a.gout && a.ldgo % 8 == 0 && a.ldx % 8 == 0 && a.npb == a.np),
+                "rowconv: the gathered x rows need RC_ENC0, T 1, kp 64, one column window");
   switch (epi) {
     case RC_LIN: return rc_launch_epi<RC_LIN>(a, s);
     case RC_FWD:

@@ -553,8 +553,7 @@ extern "C" int snd_plan_create(const snd_config_t* cfg, int n_graphs, snd_plan_t
   p->pack_in_gcn0 = p->fast && p->fast_enc && !p->front_fused && !p->sg && !(dbg & (1 << 28));
   // the GCN1 backward SpMM A @ dP1 inside the RC_ENC0 launch that consumes it (round 5;
   // debug bit 128: the separate SpMM launch)
-  p->enc0_gather = p->fast_enc && !(dbg & 128) && ((c.h1 == 64 && p->pw1b.kp == 64) ||
-                   (c.h1 == 128 && p->pw1b.kp == 128)) && c.f_in <= 4;
+  p->enc0_gather = p->fast_enc && !(dbg & 128) && c.h1 == 64 && p->pw1b.kp == 64 && c.f_in <= 4;
   set_zzt_splits(*p);
   *out = p;
   return 0;
