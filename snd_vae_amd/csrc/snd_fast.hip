@@ -230,7 +230,8 @@ __global__ void __launch_bounds__(RCT) rowconv_kernel(RcArgs a) {
 #pragma unroll
               for (int e = 0; e < 4; ++e) if (cvm[i] >> e & 1u) ypf[i][e] = yp[e];
           } else {   // ENC1: P1 for the B1 part, X for the feature part
-            if (cvm[i] == 15u && n0 + 3 < a.h && (a.ldp & 3) == 0 && (reinterpret_cast<uintptr_t>(a.p) & 15) == 0) {   // a whole P1 quad: one 16-byte load
+            if (NBH <= 3 && cvm[i] == 15u && n0 + 3 < a.h && (a.ldp & 3) == 0 &&
+                (reinterpret_cast<uintptr_t>(a.p) & 15) == 0) {   // (NBH 4: registers)   // a whole P1 quad: one 16-byte load
               ypf[i] = *reinterpret_cast<const f32x4*>(a.p + (long long)r * a.ldp + n0);
             } else {
 #pragma unroll
